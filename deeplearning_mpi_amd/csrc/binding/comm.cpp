@@ -1,0 +1,328 @@
+// Native communication layer + DDP gradient-bucket reducer.
+//
+// RcclComm: one RCCL communicator per process (one process per GPU, xGMI), bootstrapped from a
+// 128-byte ncclUniqueId that the launcher layer distributes (MPI_Bcast under mpirun, the c10d
+// TCPStore under torchrun).  Every collective is enqueued on a dedicated high-priority comm HIP
+// stream, ordered after the compute stream with an event, so bucket all-reduces overlap the rest
+// of the backward pass; wait() makes the compute stream wait on the comm stream (no host block).
+// Replaces c10d ProcessGroupNCCL of the reference (SURVEY.md §2.4, K1-K8 call sites §2.6).
+//
+// Reducer: the C++ core of our DistributedDataParallel (replaces torch's C++ DDP Reducer used at
+// /root/reference/pytorch/resnet/main.py:44-46, unet/train.py:68-70).  Gradients live in ONE flat
+// fp32 buffer laid out in reverse registration order (≈ grad-ready order), so every bucket is a
+// contiguous slice and is all-reduced in place: no copy-in/copy-out, no per-tensor launches.
+// Buckets launch strictly in index order (identical collective order on every rank); a bucket
+// goes out as soon as it and all earlier buckets are complete.
+#include "comm.h"
+
+#include <c10/hip/HIPCachingAllocator.h>
+#include <c10/hip/HIPStream.h>
+#include <rccl/rccl.h>
+
+#include <cstring>
+#include <stdexcept>
+
+namespace dlmpi_ext {
+
+static void nccl_check(ncclResult_t r, const char* what) {
+  if (r != ncclSuccess) throw std::runtime_error(std::string("RCCL ") + what + " failed: " + ncclGetErrorString(r));
+}
+static void hip_check(hipError_t e, const char* what) {
+  if (e != hipSuccess) throw std::runtime_error(std::string("HIP ") + what + " failed: " + hipGetErrorString(e));
+}
+
+static ncclDataType_t to_nccl(at::ScalarType t) {
+  switch (t) {
+    case at::kFloat: return ncclFloat32;
+    case at::kBFloat16: return ncclBfloat16;
+    case at::kHalf: return ncclFloat16;
+    case at::kDouble: return ncclFloat64;
+    case at::kLong: return ncclInt64;
+    case at::kInt: return ncclInt32;
+    case at::kByte: return ncclUint8;
+    case at::kChar: return ncclInt8;
+    case at::kBool: return ncclUint8;
+    default: throw std::runtime_error("RcclComm: unsupported dtype");
+  }
+}
+static ncclRedOp_t to_op(const std::string& op) {
+  if (op == "sum") return ncclSum;
+  if (op == "avg") return ncclAvg;
+  if (op == "max") return ncclMax;
+  if (op == "min") return ncclMin;
+  if (op == "prod") return ncclProd;
+  throw std::runtime_error("RcclComm: unknown reduce op " + op);
+}
+
+// ---------------------------------------------------------------------------------------------
+struct RcclComm::Impl {
+  ncclComm_t comm = nullptr;
+  c10::hip::HIPStream stream;
+  int rank = 0, size = 1, device = 0;
+  std::vector<hipEvent_t> events;   // ring of pre-created events for stream fences
+  size_t next_event = 0;
+  explicit Impl(c10::hip::HIPStream s) : stream(s) {}
+  hipEvent_t event() {
+    if (events.empty()) {
+      events.resize(256);
+      for (auto& e : events) hip_check(hipEventCreateWithFlags(&e, hipEventDisableTiming), "hipEventCreate");
+    }
+    hipEvent_t e = events[next_event];
+    next_event = (next_event + 1) % events.size();
+    return e;
+  }
+  ~Impl() {
+    for (auto& e : events) hipEventDestroy(e);
+  }
+};
+
+pybind11::bytes RcclComm::unique_id() {
+  ncclUniqueId id;
+  nccl_check(ncclGetUniqueId(&id), "ncclGetUniqueId");
+  return pybind11::bytes(reinterpret_cast<const char*>(&id), sizeof(id));
+}
+
+RcclComm::RcclComm(const std::string& uid, int rank, int size, int device) {
+  if (uid.size() != sizeof(ncclUniqueId)) throw std::runtime_error("RcclComm: bad unique id size");
+  hip_check(hipSetDevice(device), "hipSetDevice");
+  impl_ = std::make_unique<Impl>(c10::hip::getStreamFromPool(/*isHighPriority=*/true, (c10::DeviceIndex)device));
+  impl_->rank = rank;
+  impl_->size = size;
+  impl_->device = device;
+  ncclUniqueId id;
+  std::memcpy(&id, uid.data(), sizeof(id));
+  nccl_check(ncclCommInitRank(&impl_->comm, size, id, rank), "ncclCommInitRank");
+}
+
+RcclComm::~RcclComm() {
+  if (impl_ && impl_->comm) {
+    hipStreamSynchronize(impl_->stream.stream());
+    ncclCommDestroy(impl_->comm);
+    impl_->comm = nullptr;
+  }
+}
+
+void RcclComm::destroy() {
+  if (impl_ && impl_->comm) {
+    hip_check(hipStreamSynchronize(impl_->stream.stream()), "hipStreamSynchronize");
+    nccl_check(ncclCommDestroy(impl_->comm), "ncclCommDestroy");
+    impl_->comm = nullptr;
+  }
+}
+
+int RcclComm::rank() const { return impl_->rank; }
+int RcclComm::size() const { return impl_->size; }
+int64_t RcclComm::stream_handle() const { return (int64_t)(void*)impl_->stream.stream(); }
+
+// comm stream waits for everything enqueued so far on the caller's current stream
+void RcclComm::fence_in() {
+  hipStream_t cur = c10::hip::getCurrentHIPStream().stream();
+  hipEvent_t ev = impl_->event();
+  hip_check(hipEventRecord(ev, cur), "hipEventRecord");
+  hip_check(hipStreamWaitEvent(impl_->stream.stream(), ev, 0), "hipStreamWaitEvent");
+}
+
+// caller's current stream waits for everything enqueued on the comm stream
+void RcclComm::fence_out() {
+  hipStream_t cur = c10::hip::getCurrentHIPStream().stream();
+  hipEvent_t ev = impl_->event();
+  hip_check(hipEventRecord(ev, impl_->stream.stream()), "hipEventRecord");
+  hip_check(hipStreamWaitEvent(cur, ev, 0), "hipStreamWaitEvent");
+}
+
+void RcclComm::record(const at::Tensor& t) {
+  c10::hip::HIPCachingAllocator::recordStream(t.storage().data_ptr(), impl_->stream);
+}
+
+void RcclComm::allreduce_async(at::Tensor t, const std::string& op) {
+  if (!t.is_contiguous()) throw std::runtime_error("allreduce: tensor must be contiguous");
+  record(t);
+  nccl_check(ncclAllReduce(t.data_ptr(), t.data_ptr(), (size_t)t.numel(), to_nccl(t.scalar_type()), to_op(op),
+                           impl_->comm, impl_->stream.stream()),
+             "ncclAllReduce");
+}
+
+void RcclComm::allreduce(at::Tensor t, const std::string& op, bool async_op) {
+  fence_in();
+  allreduce_async(t, op);
+  if (!async_op) fence_out();
+}
+
+void RcclComm::broadcast(at::Tensor t, int root, bool async_op) {
+  fence_in();
+  record(t);
+  nccl_check(ncclBroadcast(t.data_ptr(), t.data_ptr(), (size_t)t.numel(), to_nccl(t.scalar_type()), root,
+                           impl_->comm, impl_->stream.stream()),
+             "ncclBroadcast");
+  if (!async_op) fence_out();
+}
+
+void RcclComm::allgather(at::Tensor out, const at::Tensor& in, bool async_op) {
+  if (out.numel() != in.numel() * impl_->size) throw std::runtime_error("allgather: out must be size * in");
+  fence_in();
+  record(out);
+  record(in);
+  nccl_check(ncclAllGather(in.data_ptr(), out.data_ptr(), (size_t)in.numel(), to_nccl(in.scalar_type()), impl_->comm,
+                           impl_->stream.stream()),
+             "ncclAllGather");
+  if (!async_op) fence_out();
+}
+
+void RcclComm::reduce_scatter(at::Tensor out, const at::Tensor& in, const std::string& op, bool async_op) {
+  if (in.numel() != out.numel() * impl_->size) throw std::runtime_error("reduce_scatter: in must be size * out");
+  fence_in();
+  record(out);
+  record(in);
+  nccl_check(ncclReduceScatter(in.data_ptr(), out.data_ptr(), (size_t)out.numel(), to_nccl(in.scalar_type()),
+                               to_op(op), impl_->comm, impl_->stream.stream()),
+             "ncclReduceScatter");
+  if (!async_op) fence_out();
+}
+
+void RcclComm::alltoall(at::Tensor out, const at::Tensor& in, bool async_op) {
+  if (in.numel() != out.numel() || in.numel() % impl_->size) throw std::runtime_error("alltoall: bad sizes");
+  fence_in();
+  record(out);
+  record(in);
+  const size_t chunk = (size_t)in.numel() / impl_->size;
+  const size_t esz = in.element_size();
+  nccl_check(ncclGroupStart(), "ncclGroupStart");
+  for (int r = 0; r < impl_->size; ++r) {
+    nccl_check(ncclSend((const char*)in.data_ptr() + r * chunk * esz, chunk, to_nccl(in.scalar_type()), r,
+                        impl_->comm, impl_->stream.stream()),
+               "ncclSend");
+    nccl_check(ncclRecv((char*)out.data_ptr() + r * chunk * esz, chunk, to_nccl(in.scalar_type()), r, impl_->comm,
+                        impl_->stream.stream()),
+               "ncclRecv");
+  }
+  nccl_check(ncclGroupEnd(), "ncclGroupEnd");
+  if (!async_op) fence_out();
+}
+
+void RcclComm::send(const at::Tensor& t, int peer) {
+  fence_in();
+  record(t);
+  nccl_check(ncclSend(t.data_ptr(), (size_t)t.numel(), to_nccl(t.scalar_type()), peer, impl_->comm,
+                      impl_->stream.stream()),
+             "ncclSend");
+  fence_out();
+}
+
+void RcclComm::recv(at::Tensor t, int peer) {
+  fence_in();
+  record(t);
+  nccl_check(ncclRecv(t.data_ptr(), (size_t)t.numel(), to_nccl(t.scalar_type()), peer, impl_->comm,
+                      impl_->stream.stream()),
+             "ncclRecv");
+  fence_out();
+}
+
+void RcclComm::wait() { fence_out(); }
+
+void RcclComm::synchronize() { hip_check(hipStreamSynchronize(impl_->stream.stream()), "hipStreamSynchronize"); }
+
+void RcclComm::barrier() {
+  at::Tensor one = at::ones({1}, at::TensorOptions().dtype(at::kFloat).device(at::kCUDA, impl_->device));
+  allreduce(one, "sum", false);
+  synchronize();
+  hip_check(hipStreamSynchronize(c10::hip::getCurrentHIPStream().stream()), "hipStreamSynchronize");
+}
+
+// ---------------------------------------------------------------------------------------------
+Reducer::Reducer(std::vector<at::Tensor> buckets, std::vector<int64_t> param_bucket, std::shared_ptr<CommBase> comm,
+                 bool average)
+    : buckets_(std::move(buckets)), param_bucket_(std::move(param_bucket)), comm_(std::move(comm)),
+      average_(average) {
+  expected_.assign(buckets_.size(), 0);
+  for (int64_t b : param_bucket_) {
+    if (b < 0 || b >= (int64_t)buckets_.size()) throw std::runtime_error("Reducer: bad bucket index");
+    expected_[b]++;
+  }
+  pending_ = expected_;
+  seen_.assign(param_bucket_.size(), 0);
+}
+
+void Reducer::prepare_for_backward() {
+  pending_ = expected_;
+  std::fill(seen_.begin(), seen_.end(), 0);
+  next_ = 0;
+  launched_ = 0;
+}
+
+void Reducer::launch_ready() {
+  bool fenced = false;
+  while (next_ < (int64_t)buckets_.size() && pending_[next_] == 0) {
+    if (!fenced) {   // comm stream waits for the compute stream once per group of ready buckets
+      comm_->begin_bucket();
+      fenced = true;
+    }
+    comm_->allreduce_bucket(buckets_[next_], average_);
+    ++next_;
+    ++launched_;
+  }
+}
+
+void Reducer::mark_ready(int64_t param_idx) {
+  if (param_idx < 0 || param_idx >= (int64_t)param_bucket_.size()) throw std::runtime_error("Reducer: bad param");
+  if (seen_[param_idx]) return;   // a parameter used twice contributes once (grads accumulate in place)
+  seen_[param_idx] = 1;
+  const int64_t b = param_bucket_[param_idx];
+  if (--pending_[b] == 0) launch_ready();
+}
+
+void Reducer::finalize() {
+  // parameters that received no gradient this iteration: their (zero) slices still go out so
+  // that every rank issues the same collectives in the same order
+  for (size_t b = 0; b < pending_.size(); ++b) pending_[b] = 0;
+  launch_ready();
+  comm_->end_backward();
+}
+
+void register_comm(pybind11::module& m) {
+  namespace py = pybind11;
+  py::class_<RcclComm, std::shared_ptr<RcclComm>>(m, "RcclComm")
+      .def(py::init<const std::string&, int, int, int>(), py::arg("uid"), py::arg("rank"), py::arg("size"),
+           py::arg("device"))
+      .def_static("unique_id", &RcclComm::unique_id)
+      .def("rank", &RcclComm::rank)
+      .def("size", &RcclComm::size)
+      .def("stream_handle", &RcclComm::stream_handle)
+      .def("allreduce", &RcclComm::allreduce, py::arg("t"), py::arg("op") = "sum", py::arg("async_op") = false)
+      .def("broadcast", &RcclComm::broadcast, py::arg("t"), py::arg("root") = 0, py::arg("async_op") = false)
+      .def("allgather", &RcclComm::allgather, py::arg("out"), py::arg("inp"), py::arg("async_op") = false)
+      .def("reduce_scatter", &RcclComm::reduce_scatter, py::arg("out"), py::arg("inp"), py::arg("op") = "sum",
+           py::arg("async_op") = false)
+      .def("alltoall", &RcclComm::alltoall, py::arg("out"), py::arg("inp"), py::arg("async_op") = false)
+      .def("send", &RcclComm::send)
+      .def("recv", &RcclComm::recv)
+      .def("wait", &RcclComm::wait)
+      .def("synchronize", &RcclComm::synchronize)
+      .def("barrier", &RcclComm::barrier)
+      .def("destroy", &RcclComm::destroy);
+
+  py::class_<CommBase, PyCommBase, std::shared_ptr<CommBase>>(m, "CommBase")
+      .def(py::init<>())
+      .def("begin_bucket", &CommBase::begin_bucket)
+      .def("allreduce_bucket", &CommBase::allreduce_bucket)
+      .def("end_backward", &CommBase::end_backward);
+
+  py::class_<RcclBucketComm, CommBase, std::shared_ptr<RcclBucketComm>>(m, "RcclBucketComm")
+      .def(py::init<std::shared_ptr<RcclComm>>());
+
+  py::class_<Reducer, std::shared_ptr<Reducer>>(m, "Reducer")
+      .def(py::init<std::vector<at::Tensor>, std::vector<int64_t>, std::shared_ptr<CommBase>, bool>())
+      .def("prepare_for_backward", &Reducer::prepare_for_backward)
+      .def("mark_ready", &Reducer::mark_ready)
+      .def("finalize", &Reducer::finalize)
+      .def("num_buckets", &Reducer::num_buckets)
+      .def("launched", &Reducer::launched);
+}
+
+// RCCL-backed bucket comm: begin_bucket fences the comm stream behind the compute stream once
+// per newly completed group of buckets, allreduce_bucket enqueues on the comm stream,
+// end_backward makes the compute stream wait for all of them.
+void RcclBucketComm::begin_bucket() { comm_->fence_in(); }
+void RcclBucketComm::allreduce_bucket(at::Tensor t, bool average) { comm_->allreduce_async(t, average ? "avg" : "sum"); }
+void RcclBucketComm::end_backward() { comm_->fence_out(); }
+
+}  // namespace dlmpi_ext

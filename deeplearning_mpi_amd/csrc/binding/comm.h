@@ -1,0 +1,95 @@
+#pragma once
+#include <torch/extension.h>
+
+#include <memory>
+#include <string>
+#include <vector>
+
+namespace dlmpi_ext {
+
+// Native RCCL communicator (one per process / GPU) with a dedicated comm stream.
+class RcclComm {
+ public:
+  static pybind11::bytes unique_id();
+  RcclComm(const std::string& uid, int rank, int size, int device);
+  ~RcclComm();
+  int rank() const;
+  int size() const;
+  int64_t stream_handle() const;
+  void fence_in();
+  void fence_out();
+  void allreduce_async(at::Tensor t, const std::string& op);
+  void allreduce(at::Tensor t, const std::string& op, bool async_op);
+  void broadcast(at::Tensor t, int root, bool async_op);
+  void allgather(at::Tensor out, const at::Tensor& in, bool async_op);
+  void reduce_scatter(at::Tensor out, const at::Tensor& in, const std::string& op, bool async_op);
+  void alltoall(at::Tensor out, const at::Tensor& in, bool async_op);
+  void send(const at::Tensor& t, int peer);
+  void recv(at::Tensor t, int peer);
+  void wait();
+  void synchronize();
+  void barrier();
+  void destroy();
+
+ private:
+  void record(const at::Tensor& t);
+  struct Impl;
+  std::unique_ptr<Impl> impl_;
+};
+
+// What the reducer needs from a communication backend.  Implemented natively over RCCL
+// (RcclBucketComm) and, for CPU / gloo testing, by a Python subclass (PyCommBase trampoline).
+class CommBase {
+ public:
+  virtual ~CommBase() = default;
+  virtual void begin_bucket() {}
+  virtual void allreduce_bucket(at::Tensor t, bool average) = 0;
+  virtual void end_backward() {}
+};
+
+class PyCommBase : public CommBase {
+ public:
+  using CommBase::CommBase;
+  void begin_bucket() override { PYBIND11_OVERRIDE(void, CommBase, begin_bucket, ); }
+  void allreduce_bucket(at::Tensor t, bool average) override {
+    PYBIND11_OVERRIDE_PURE(void, CommBase, allreduce_bucket, t, average);
+  }
+  void end_backward() override { PYBIND11_OVERRIDE(void, CommBase, end_backward, ); }
+};
+
+class RcclBucketComm : public CommBase {
+ public:
+  explicit RcclBucketComm(std::shared_ptr<RcclComm> c) : comm_(std::move(c)) {}
+  void begin_bucket() override;
+  void allreduce_bucket(at::Tensor t, bool average) override;
+  void end_backward() override;
+
+ private:
+  std::shared_ptr<RcclComm> comm_;
+};
+
+// Gradient-bucket reducer (see comm.cpp).
+class Reducer {
+ public:
+  Reducer(std::vector<at::Tensor> buckets, std::vector<int64_t> param_bucket, std::shared_ptr<CommBase> comm,
+          bool average);
+  void prepare_for_backward();
+  void mark_ready(int64_t param_idx);
+  void finalize();
+  int64_t num_buckets() const { return (int64_t)buckets_.size(); }
+  int64_t launched() const { return launched_; }
+
+ private:
+  void launch_ready();
+  std::vector<at::Tensor> buckets_;
+  std::vector<int64_t> param_bucket_;
+  std::shared_ptr<CommBase> comm_;
+  bool average_;
+  std::vector<int64_t> expected_, pending_;
+  std::vector<char> seen_;
+  int64_t next_ = 0, launched_ = 0;
+};
+
+void register_comm(pybind11::module& m);
+
+}  // namespace dlmpi_ext

@@ -1,0 +1,450 @@
+// Torch binding of the gfx950 kernel library: tensor plumbing, conv geometry planning (forward,
+// sub-pixel data-gradient phases, transposed conv, split-K weight-gradient) and tile selection.
+// Every function launches on the current HIP stream and never synchronises, so a whole training
+// step can be captured into a hipGraph.
+#include "ops.h"
+
+#include <c10/hip/HIPStream.h>
+
+#include <algorithm>
+#include <stdexcept>
+
+#include "../kernels/dlmpi_kernels.h"
+
+namespace dlmpi_ext {
+
+using dlmpi::ConvArgs;
+using dlmpi::ConvPhase;
+using dlmpi::make_fastdiv;
+using dlmpi::WgradArgs;
+
+static inline hipStream_t cur_stream() { return c10::hip::getCurrentHIPStream().stream(); }
+
+static inline void check(hipError_t e, const char* what) {
+  if (e != hipSuccess) throw std::runtime_error(std::string("dlmpi kernel launch failed: ") + what + ": " +
+                                                hipGetErrorString(e));
+}
+
+template <typename T>
+static inline T* ptr(const at::Tensor& t) {
+  return reinterpret_cast<T*>(t.data_ptr());
+}
+template <typename T>
+static inline T* optr(const c10::optional<at::Tensor>& t) {
+  return (t.has_value() && t->defined()) ? reinterpret_cast<T*>(t->data_ptr()) : nullptr;
+}
+
+static inline void require_gpu(const at::Tensor& t, const char* name) {
+  if (!t.is_cuda()) throw std::runtime_error(std::string(name) + " must be a GPU tensor");
+}
+
+static inline int ceil_div(int64_t a, int64_t b) { return (int)((a + b - 1) / b); }
+
+// K-iteration constants: the 64-wide reduction step walks channels (C % 64 == 0) or taps (64 % C == 0)
+static void set_kstep(ConvArgs& a, int C) {
+  if (C % 8 != 0) throw std::runtime_error("conv: channel count must be a multiple of 8 (pad it)");
+  if (C >= 64) {
+    if (C % 64 != 0) throw std::runtime_error("conv: channels >= 64 must be a multiple of 64");
+    a.cstep = 64;
+    a.tstep = 0;
+  } else {
+    if (64 % C != 0) throw std::runtime_error("conv: channels < 64 must divide 64");
+    a.cstep = 0;
+    a.tstep = 64 / C;
+  }
+}
+
+static void pick_tiles(int64_t M, int Kout, int& bm, int& bn) {
+  bn = Kout <= 64 ? 64 : 128;
+  bm = 128;
+  const int64_t tiles = ((M + 127) / 128) * ((Kout + bn - 1) / bn);
+  if (tiles < 512) bm = 64;
+}
+
+static void finish_phase(ConvPhase& p, int Nimg, int C, int bm) {
+  p.mtiles = ceil_div((int64_t)Nimg * p.P * p.Q, bm);
+  p.ksteps = ceil_div((int64_t)p.Tr * p.Ts * C, 64);
+  if (p.Tr * p.Ts == 0) p.ksteps = 0;
+  p.fdPQ = make_fastdiv((uint32_t)std::max(1, p.P * p.Q));
+  p.fdQ = make_fastdiv((uint32_t)std::max(1, p.Q));
+  p.fdTs = make_fastdiv((uint32_t)std::max(1, p.Ts));
+}
+
+static void fill_epilogue(ConvArgs& a, at::Tensor& y, int ldy, int yoff, const c10::optional<at::Tensor>& bias,
+                          const c10::optional<at::Tensor>& res, int ldres, int resoff,
+                          const c10::optional<at::Tensor>& scale, const c10::optional<at::Tensor>& shift, bool relu,
+                          const c10::optional<at::Tensor>& stats) {
+  a.y = y.data_ptr();
+  a.out_f32 = y.scalar_type() == at::kFloat ? 1 : 0;
+  a.ldy = ldy;
+  a.yoff = yoff;
+  a.kvalid = a.Kout;
+  a.bias = optr<float>(bias);
+  a.res = optr<uint16_t>(res);
+  a.ldres = ldres;
+  a.resoff = resoff;
+  a.scale = optr<float>(scale);
+  a.shift = optr<float>(shift);
+  a.relu = relu ? 1 : 0;
+  a.stats = optr<float>(stats);
+}
+
+// y[n, p, q, yoff + k] = epilogue( sum_{r,s,c} x[n, p*stride - pad + r, q*stride - pad + s, xoff + c] * w[k][r][s][c] )
+int conv2d_fwd(const at::Tensor& x, int N, int H, int W, int C, int ldx, int xoff, const at::Tensor& w, int K, int R,
+               int S, int stride, int pad, at::Tensor y, int ldy, int yoff, const c10::optional<at::Tensor>& bias,
+               const c10::optional<at::Tensor>& res, int ldres, int resoff, const c10::optional<at::Tensor>& scale,
+               const c10::optional<at::Tensor>& shift, bool relu, const c10::optional<at::Tensor>& stats, int bm_req,
+               int kvalid) {
+  require_gpu(x, "x");
+  const int P = (H + 2 * pad - R) / stride + 1, Q = (W + 2 * pad - S) / stride + 1;
+  ConvArgs a{};
+  a.x = ptr<uint16_t>(x);
+  a.H = H; a.W = W; a.C = C; a.ldx = ldx; a.xoff = xoff;
+  a.w = ptr<uint16_t>(w);
+  a.ldw = R * S * C;
+  a.S = S;
+  a.OH = P; a.OW = Q;
+  a.so = 1; a.sa = stride;
+  a.Nimg = N; a.Kout = K;
+  fill_epilogue(a, y, ldy, yoff, bias, res, ldres, resoff, scale, shift, relu, stats);
+  if (kvalid > 0 && kvalid < K) a.kvalid = kvalid;
+  a.vec_store = (a.kvalid == a.Kout && (ldy % 8) == 0 && (yoff % 8) == 0) ? 1 : 0;
+  set_kstep(a, C);
+  int bm, bn;
+  pick_tiles((int64_t)N * P * Q, K, bm, bn);
+  if (bm_req > 0) bm = bm_req;
+  a.ntiles = ceil_div(K, bn);
+  a.nphase = 1;
+  ConvPhase& p = a.ph[0];
+  p.P = P; p.Q = Q; p.Tr = R; p.Ts = S;
+  p.dh0 = -pad; p.dhs = 1; p.dw0 = -pad; p.dws = 1;
+  p.wr0 = 0; p.wrs = 1; p.ws0 = 0; p.wss = 1;
+  p.oh0 = 0; p.ow0 = 0;
+  finish_phase(p, N, C, bm);
+  check(dlmpi_conv_igemm(&a, bm, bn, cur_stream()), "conv2d_fwd");
+  return p.mtiles;   // rows of the stats partial buffer
+}
+
+// Number of BN-stat partial rows conv2d_fwd will produce (so the caller can size `stats`).
+int conv2d_fwd_mtiles(int N, int H, int W, int K, int R, int S, int stride, int pad, int bm_req) {
+  const int P = (H + 2 * pad - R) / stride + 1, Q = (W + 2 * pad - S) / stride + 1;
+  int bm, bn;
+  pick_tiles((int64_t)N * P * Q, K, bm, bn);
+  if (bm_req > 0) bm = bm_req;
+  return ceil_div((int64_t)N * P * Q, bm);
+}
+
+// dx[n, h, w, dxoff + c] = sum_{r,s,k} dy[n, (h+pad-r)/stride, (w+pad-s)/stride, k] * wT[c][r][s][k]  (+ res)
+// as stride^2 dense sub-pixel phases.
+void conv2d_dgrad(const at::Tensor& dy, int N, int P, int Q, int K, int lddy, int dyoff, const at::Tensor& wT, int C,
+                  int R, int S, int stride, int pad, int H, int W, at::Tensor dx, int lddx, int dxoff,
+                  const c10::optional<at::Tensor>& res, int ldres, int resoff) {
+  require_gpu(dy, "dy");
+  if (stride > 2) throw std::runtime_error("conv2d_dgrad: stride <= 2 supported");
+  ConvArgs a{};
+  a.x = ptr<uint16_t>(dy);
+  a.H = P; a.W = Q; a.C = K; a.ldx = lddy; a.xoff = dyoff;
+  a.w = ptr<uint16_t>(wT);
+  a.ldw = R * S * K;
+  a.S = S;
+  a.OH = H; a.OW = W;
+  a.so = stride; a.sa = 1;
+  a.Nimg = N; a.Kout = C;
+  fill_epilogue(a, dx, lddx, dxoff, c10::nullopt, res, ldres, resoff, c10::nullopt, c10::nullopt, false, c10::nullopt);
+  a.vec_store = ((lddx % 8) == 0 && (dxoff % 8) == 0) ? 1 : 0;
+  set_kstep(a, K);
+  int bm, bn;
+  pick_tiles((int64_t)N * H * W / (stride * stride), C, bm, bn);
+  a.ntiles = ceil_div(C, bn);
+  a.nphase = stride * stride;
+  for (int ph = 0; ph < stride; ++ph) {
+    for (int pw = 0; pw < stride; ++pw) {
+      ConvPhase& p = a.ph[ph * stride + pw];
+      const int r0 = (ph + pad) % stride, s0 = (pw + pad) % stride;
+      p.P = (H - ph + stride - 1) / stride;
+      p.Q = (W - pw + stride - 1) / stride;
+      p.Tr = r0 < R ? (R - r0 + stride - 1) / stride : 0;
+      p.Ts = s0 < S ? (S - s0 + stride - 1) / stride : 0;
+      p.dh0 = (ph + pad - r0) / stride; p.dhs = -1;
+      p.dw0 = (pw + pad - s0) / stride; p.dws = -1;
+      p.wr0 = r0; p.wrs = stride; p.ws0 = s0; p.wss = stride;
+      p.oh0 = ph; p.ow0 = pw;
+      finish_phase(p, N, K, bm);
+    }
+  }
+  check(dlmpi_conv_igemm(&a, bm, bn, cur_stream()), "conv2d_dgrad");
+}
+
+// ConvTranspose2d(k=2, s=2): y[n, 2h+i, 2w+j, yoff + co] = bias[co] + sum_ci x[n,h,w,ci] * wf[co][i][j][ci]
+void convT2x2_fwd(const at::Tensor& x, int N, int H, int W, int Cin, int ldx, int xoff, const at::Tensor& wf, int Cout,
+                  at::Tensor y, int ldy, int yoff, const c10::optional<at::Tensor>& bias) {
+  require_gpu(x, "x");
+  ConvArgs a{};
+  a.x = ptr<uint16_t>(x);
+  a.H = H; a.W = W; a.C = Cin; a.ldx = ldx; a.xoff = xoff;
+  a.w = ptr<uint16_t>(wf);
+  a.ldw = 4 * Cin;
+  a.S = 2;
+  a.OH = 2 * H; a.OW = 2 * W;
+  a.so = 2; a.sa = 1;
+  a.Nimg = N; a.Kout = Cout;
+  fill_epilogue(a, y, ldy, yoff, bias, c10::nullopt, 0, 0, c10::nullopt, c10::nullopt, false, c10::nullopt);
+  a.vec_store = ((ldy % 8) == 0 && (yoff % 8) == 0) ? 1 : 0;
+  set_kstep(a, Cin);
+  int bm, bn;
+  pick_tiles((int64_t)N * H * W, Cout, bm, bn);
+  a.ntiles = ceil_div(Cout, bn);
+  a.nphase = 4;
+  for (int i = 0; i < 2; ++i)
+    for (int j = 0; j < 2; ++j) {
+      ConvPhase& p = a.ph[i * 2 + j];
+      p.P = H; p.Q = W; p.Tr = 1; p.Ts = 1;
+      p.dh0 = 0; p.dhs = 0; p.dw0 = 0; p.dws = 0;
+      p.wr0 = i; p.wrs = 0; p.ws0 = j; p.wss = 0;
+      p.oh0 = i; p.ow0 = j;
+      finish_phase(p, N, Cin, bm);
+    }
+  check(dlmpi_conv_igemm(&a, bm, bn, cur_stream()), "convT2x2_fwd");
+}
+
+// grad[ko][t][c] += sum_pix dy[pix][dyoff + ko] * x[gather(pix, t)][xoff + c]   (c < Creal, ko < Ko_real)
+// dy is over the P x Q output grid of a conv (R x S, stride, pad) applied to x (H x W).
+void conv2d_wgrad(const at::Tensor& dy, int lddy, int dyoff, int Ko, const at::Tensor& x, int N, int H, int W, int C,
+                  int ldx, int xoff, int R, int S, int stride, int pad, int P, int Q, at::Tensor grad, int Creal,
+                  int Ko_real) {
+  require_gpu(dy, "dy");
+  if (C % 8 != 0 || Ko % 8 != 0) throw std::runtime_error("conv2d_wgrad: channels must be multiples of 8");
+  WgradArgs a{};
+  a.dy = ptr<uint16_t>(dy);
+  a.ldy = lddy; a.dyoff = dyoff; a.Ko = Ko;
+  a.x = ptr<uint16_t>(x);
+  a.H = H; a.W = W; a.C = C; a.ldx = ldx; a.xoff = xoff;
+  a.Nimg = N; a.P = P; a.Q = Q; a.S = S;
+  a.stride_h = stride; a.stride_w = stride; a.pad_h = pad; a.pad_w = pad;
+  a.TC = R * S * C;
+  a.npix = N * P * Q;
+  const int bm = Ko <= 64 ? 64 : 128;
+  a.mtiles = ceil_div(Ko, bm);
+  a.ntiles = ceil_div(a.TC, 128);
+  const int tiles = a.mtiles * a.ntiles;
+  const int maxsplit = std::max(1, ceil_div(a.npix, 64));
+  int splits = std::max(1, std::min(maxsplit, ceil_div(2048, tiles)));
+  int pps = ceil_div(a.npix, splits);
+  pps = ceil_div(pps, 64) * 64;
+  splits = ceil_div(a.npix, pps);
+  a.splits = splits;
+  a.pix_per_split = pps;
+  a.fdPQ = make_fastdiv((uint32_t)(P * Q));
+  a.fdQ = make_fastdiv((uint32_t)Q);
+  a.fdC = make_fastdiv((uint32_t)C);
+  a.fdS = make_fastdiv((uint32_t)S);
+  at::Tensor ws = at::empty({(int64_t)splits * Ko * a.TC}, dy.options().dtype(at::kFloat));
+  a.ws = ptr<float>(ws);
+  check(dlmpi_conv_wgrad(&a, bm, cur_stream()), "conv2d_wgrad");
+  check(dlmpi_wgrad_reduce(a.ws, splits, Ko, R * S, C, Creal, Ko_real, ptr<float>(grad), cur_stream()),
+        "wgrad_reduce");
+}
+
+// --------------------------------- batch norm ----------------------------------------------
+void bn_finalize(const at::Tensor& partial, int ntiles, int C, double count, const c10::optional<at::Tensor>& gamma,
+                 const c10::optional<at::Tensor>& beta, const c10::optional<at::Tensor>& running_mean,
+                 const c10::optional<at::Tensor>& running_var, double momentum, double eps, at::Tensor scale,
+                 at::Tensor shift, const c10::optional<at::Tensor>& save_mean,
+                 const c10::optional<at::Tensor>& save_invstd) {
+  check(dlmpi_bn_finalize(ptr<float>(partial), ntiles, C, count, optr<float>(gamma), optr<float>(beta),
+                          optr<float>(running_mean), optr<float>(running_var), (float)momentum, (float)eps,
+                          ptr<float>(scale), ptr<float>(shift), optr<float>(save_mean), optr<float>(save_invstd),
+                          cur_stream()),
+        "bn_finalize");
+}
+
+int reduce_blocks(int64_t M, int C) { return dlmpi_reduce_blocks(M, C); }
+
+void bn_stats(const at::Tensor& x, int64_t M, int C, int ldx, int xoff, at::Tensor partial, int nblk) {
+  check(dlmpi_bn_stats(ptr<uint16_t>(x), M, C, ldx, xoff, ptr<float>(partial), nblk, cur_stream()), "bn_stats");
+}
+
+void bn_apply(const at::Tensor& x, int ldx, int xoff, int64_t M, int C, const at::Tensor& scale,
+              const at::Tensor& shift, const c10::optional<at::Tensor>& res, int ldres, int resoff, bool relu,
+              at::Tensor y, int ldy, int yoff) {
+  check(dlmpi_bn_apply(ptr<uint16_t>(x), ldx, xoff, M, C, ptr<float>(scale), ptr<float>(shift), optr<uint16_t>(res),
+                       ldres, resoff, relu ? 1 : 0, ptr<uint16_t>(y), ldy, yoff, cur_stream()),
+        "bn_apply");
+}
+
+void bn_bwd_reduce(const at::Tensor& dy, int lddy, int dyoff, const c10::optional<at::Tensor>& ymask, int ldym,
+                   int ymoff, const c10::optional<at::Tensor>& x, int ldx, int xoff, int64_t M, int C,
+                   const c10::optional<at::Tensor>& mean, const c10::optional<at::Tensor>& invstd, at::Tensor partial,
+                   int nblk) {
+  check(dlmpi_bn_bwd_reduce(ptr<uint16_t>(dy), lddy, dyoff, optr<uint16_t>(ymask), ldym, ymoff, optr<uint16_t>(x), ldx,
+                            xoff, M, C, optr<float>(mean), optr<float>(invstd), ptr<float>(partial), nblk,
+                            cur_stream()),
+        "bn_bwd_reduce");
+}
+
+void bn_bwd_finalize(const at::Tensor& partial, int nblk, int C, double count, const c10::optional<at::Tensor>& gamma,
+                     const c10::optional<at::Tensor>& mean, const c10::optional<at::Tensor>& invstd,
+                     const c10::optional<at::Tensor>& dgamma, const c10::optional<at::Tensor>& dbeta,
+                     const c10::optional<at::Tensor>& coef) {
+  check(dlmpi_bn_bwd_finalize(ptr<float>(partial), nblk, C, count, optr<float>(gamma), optr<float>(mean),
+                              optr<float>(invstd), optr<float>(dgamma), optr<float>(dbeta), optr<float>(coef),
+                              cur_stream()),
+        "bn_bwd_finalize");
+}
+
+void bn_bwd_apply(const at::Tensor& dy, int lddy, int dyoff, const c10::optional<at::Tensor>& ymask, int ldym,
+                  int ymoff, const at::Tensor& x, int ldx, int xoff, int64_t M, int C, const at::Tensor& coef,
+                  at::Tensor dx, const c10::optional<at::Tensor>& dyr_out) {
+  check(dlmpi_bn_bwd_apply(ptr<uint16_t>(dy), lddy, dyoff, optr<uint16_t>(ymask), ldym, ymoff, ptr<uint16_t>(x), ldx,
+                           xoff, M, C, ptr<float>(coef), ptr<uint16_t>(dx), optr<uint16_t>(dyr_out), cur_stream()),
+        "bn_bwd_apply");
+}
+
+void channel_sum(const at::Tensor& x, int64_t M, int C, int ldx, int xoff, at::Tensor out_acc) {
+  const int nblk = dlmpi_reduce_blocks(M, C);
+  at::Tensor partial = at::empty({(int64_t)nblk * 2 * C}, x.options().dtype(at::kFloat));
+  check(dlmpi_channel_sum(ptr<uint16_t>(x), M, C, ldx, xoff, ptr<float>(out_acc), ptr<float>(partial), nblk,
+                          cur_stream()),
+        "channel_sum");
+}
+
+// --------------------------------- pooling / layout ----------------------------------------
+void maxpool_fwd(const at::Tensor& x, int N, int H, int W, int C, int ldx, int xoff, int k, int stride, int pad,
+                 at::Tensor y, at::Tensor idx, int OH, int OW) {
+  check(dlmpi_maxpool_fwd(ptr<uint16_t>(x), N, H, W, C, ldx, xoff, k, stride, pad, ptr<uint16_t>(y),
+                          ptr<uint8_t>(idx), OH, OW, cur_stream()),
+        "maxpool_fwd");
+}
+void maxpool_bwd(const at::Tensor& dy, const at::Tensor& idx, int N, int H, int W, int C, int k, int stride, int pad,
+                 int OH, int OW, const c10::optional<at::Tensor>& add, int ldadd, int addoff, at::Tensor dx, int lddx,
+                 int dxoff) {
+  check(dlmpi_maxpool_bwd(ptr<uint16_t>(dy), ptr<uint8_t>(idx), N, H, W, C, k, stride, pad, OH, OW,
+                          optr<uint16_t>(add), ldadd, addoff, ptr<uint16_t>(dx), lddx, dxoff, cur_stream()),
+        "maxpool_bwd");
+}
+void avgpool_fwd(const at::Tensor& x, int N, int HW, int C, at::Tensor y) {
+  check(dlmpi_avgpool_fwd(ptr<uint16_t>(x), N, HW, C, ptr<uint16_t>(y), cur_stream()), "avgpool_fwd");
+}
+void avgpool_bwd(const at::Tensor& dy, int N, int HW, int C, at::Tensor dx) {
+  check(dlmpi_avgpool_bwd(ptr<uint16_t>(dy), N, HW, C, ptr<uint16_t>(dx), cur_stream()), "avgpool_bwd");
+}
+void nchw_to_nhwc(const at::Tensor& x, int N, int C, int H, int W, int Cpad, at::Tensor y) {
+  check(dlmpi_nchw_to_nhwc(ptr<float>(x), N, C, H, W, Cpad, ptr<uint16_t>(y), cur_stream()), "nchw_to_nhwc");
+}
+void upsample2x_fwd(const at::Tensor& x, int N, int H, int W, int C, int ldx, int xoff, at::Tensor y, int ldy,
+                    int yoff) {
+  check(dlmpi_upsample2x_fwd(ptr<uint16_t>(x), N, H, W, C, ldx, xoff, ptr<uint16_t>(y), ldy, yoff, cur_stream()),
+        "upsample2x_fwd");
+}
+void upsample2x_bwd(const at::Tensor& dy, int N, int H, int W, int C, int lddy, int dyoff, at::Tensor dx) {
+  at::Tensor ws = at::empty({(int64_t)N * H * W * C}, dy.options().dtype(at::kFloat));
+  check(dlmpi_upsample2x_bwd(ptr<uint16_t>(dy), N, H, W, C, lddy, dyoff, ptr<float>(ws), ptr<uint16_t>(dx),
+                             cur_stream()),
+        "upsample2x_bwd");
+}
+
+// entries: int64 tensor [n][16] on the host: src_ptr, dst_ptr, d0..d3, v0..v3, s0..s3, start
+void cast_weights(const at::Tensor& entries_dev, int n, int64_t total) {
+  check(dlmpi_cast_weights(reinterpret_cast<const CastEntry*>(entries_dev.data_ptr()), n, total, cur_stream()),
+        "cast_weights");
+}
+
+// --------------------------------- losses / eval -------------------------------------------
+void softmax_ce_fwd(const at::Tensor& logits, int ldl, const at::Tensor& labels, int N, int K, at::Tensor loss_rows,
+                    at::Tensor lse, at::Tensor loss) {
+  check(dlmpi_softmax_ce_fwd(ptr<float>(logits), ldl, ptr<int64_t>(labels), N, K, ptr<float>(loss_rows),
+                             ptr<float>(lse), cur_stream()),
+        "softmax_ce_fwd");
+  check(dlmpi_sum_f32(ptr<float>(loss_rows), N, ptr<float>(loss), 1.f / (float)N, cur_stream()), "sum");
+}
+void softmax_ce_bwd(const at::Tensor& logits, int ldl, const at::Tensor& labels, const at::Tensor& lse, int N, int K,
+                    int ldd, const c10::optional<at::Tensor>& go, double scale, at::Tensor dlogits) {
+  check(dlmpi_softmax_ce_bwd(ptr<float>(logits), ldl, ptr<int64_t>(labels), ptr<float>(lse), N, K, ldd,
+                             optr<float>(go), (float)scale, ptr<float>(dlogits), cur_stream()),
+        "softmax_ce_bwd");
+}
+void bce_fwd(const at::Tensor& logits, int ldl, const at::Tensor& target, int64_t M, at::Tensor loss) {
+  int nblk = (int)std::min<int64_t>(1024, std::max<int64_t>(1, (M + 4095) / 4096));
+  at::Tensor partial = at::empty({nblk}, logits.options().dtype(at::kFloat));
+  check(dlmpi_bce_fwd(ptr<float>(logits), ldl, ptr<float>(target), M, ptr<float>(partial), nblk, cur_stream()),
+        "bce_fwd");
+  check(dlmpi_sum_f32(ptr<float>(partial), nblk, ptr<float>(loss), 1.f / (float)M, cur_stream()), "sum");
+}
+void bce_bwd(const at::Tensor& logits, int ldl, const at::Tensor& target, int64_t M,
+             const c10::optional<at::Tensor>& go, double scale, at::Tensor dlogits) {
+  check(dlmpi_bce_bwd(ptr<float>(logits), ldl, ptr<float>(target), M, optr<float>(go), (float)scale,
+                      ptr<float>(dlogits), cur_stream()),
+        "bce_bwd");
+}
+void argmax_correct(const at::Tensor& logits, int ldl, const at::Tensor& labels, int N, int K, at::Tensor correct) {
+  check(dlmpi_argmax_correct(ptr<float>(logits), ldl, ptr<int64_t>(labels), N, K, ptr<int>(correct), cur_stream()),
+        "argmax_correct");
+}
+void dice(const at::Tensor& logits, int ldl, const at::Tensor& target, int N, int64_t HW, at::Tensor out) {
+  check(dlmpi_dice(ptr<float>(logits), ldl, ptr<float>(target), N, HW, ptr<float>(out), cur_stream()), "dice");
+}
+
+// --------------------------------- optimizers ----------------------------------------------
+void sgd_step(at::Tensor p, const at::Tensor& g, at::Tensor m, double lr, double momentum, double dampening,
+              double wd, bool nesterov, bool first, const c10::optional<at::Tensor>& skip_flag) {
+  check(dlmpi_sgd(ptr<float>(p), ptr<float>(g), ptr<float>(m), p.numel(), (float)lr, (float)momentum,
+                  (float)dampening, (float)wd, nesterov ? 1 : 0, first ? 1 : 0, optr<float>(skip_flag), cur_stream()),
+        "sgd");
+}
+void adam_step(at::Tensor p, const at::Tensor& g, at::Tensor m, at::Tensor v, double lr, double b1, double b2,
+               double eps, double wd, bool adamw, double bc1, double bc2, const c10::optional<at::Tensor>& clip) {
+  check(dlmpi_adam(ptr<float>(p), ptr<float>(g), ptr<float>(m), ptr<float>(v), p.numel(), (float)lr, (float)b1,
+                   (float)b2, (float)eps, (float)wd, adamw ? 1 : 0, (float)bc1, (float)bc2, optr<float>(clip),
+                   cur_stream()),
+        "adam");
+}
+// total L2 norm of a flat fp32 buffer -> norm_out[0]; coef_out = {min(1, max_norm/(norm+1e-6)), nonfinite}
+void grad_norm(const at::Tensor& g, double max_norm, at::Tensor norm_out, at::Tensor coef_out) {
+  const int nblk = 512;
+  at::Tensor partial = at::empty({nblk}, g.options().dtype(at::kFloat));
+  check(dlmpi_sumsq(ptr<float>(g), g.numel(), ptr<float>(partial), nblk, cur_stream()), "sumsq");
+  check(dlmpi_clip_coef(ptr<float>(partial), nblk, (float)max_norm, ptr<float>(norm_out), ptr<float>(coef_out),
+                        cur_stream()),
+        "clip_coef");
+}
+void scale_(at::Tensor x, const at::Tensor& coef) {
+  check(dlmpi_scale_f32(ptr<float>(x), x.numel(), ptr<float>(coef), cur_stream()), "scale");
+}
+
+void register_ops(pybind11::module& m) {
+  namespace py = pybind11;
+  m.def("conv2d_fwd", &conv2d_fwd);
+  m.def("conv2d_fwd_mtiles", &conv2d_fwd_mtiles);
+  m.def("conv2d_dgrad", &conv2d_dgrad);
+  m.def("convT2x2_fwd", &convT2x2_fwd);
+  m.def("conv2d_wgrad", &conv2d_wgrad);
+  m.def("bn_finalize", &bn_finalize);
+  m.def("reduce_blocks", &reduce_blocks);
+  m.def("bn_stats", &bn_stats);
+  m.def("bn_apply", &bn_apply);
+  m.def("bn_bwd_reduce", &bn_bwd_reduce);
+  m.def("bn_bwd_finalize", &bn_bwd_finalize);
+  m.def("bn_bwd_apply", &bn_bwd_apply);
+  m.def("channel_sum", &channel_sum);
+  m.def("maxpool_fwd", &maxpool_fwd);
+  m.def("maxpool_bwd", &maxpool_bwd);
+  m.def("avgpool_fwd", &avgpool_fwd);
+  m.def("avgpool_bwd", &avgpool_bwd);
+  m.def("nchw_to_nhwc", &nchw_to_nhwc);
+  m.def("upsample2x_fwd", &upsample2x_fwd);
+  m.def("upsample2x_bwd", &upsample2x_bwd);
+  m.def("cast_weights", &cast_weights);
+  m.def("softmax_ce_fwd", &softmax_ce_fwd);
+  m.def("softmax_ce_bwd", &softmax_ce_bwd);
+  m.def("bce_fwd", &bce_fwd);
+  m.def("bce_bwd", &bce_bwd);
+  m.def("argmax_correct", &argmax_correct);
+  m.def("dice", &dice);
+  m.def("sgd_step", &sgd_step);
+  m.def("adam_step", &adam_step);
+  m.def("grad_norm", &grad_norm);
+  m.def("scale_", &scale_);
+  m.attr("CAST_ENTRY_BYTES") = (int)sizeof(CastEntry);
+}
+
+}  // namespace dlmpi_ext

@@ -1,0 +1,340 @@
+// Training-mode BatchNorm2d on NHWC bf16 activations (fp32 statistics), fused with ReLU and the
+// bottleneck residual add.  Replaces the cuDNN BN fwd/bwd + ATen ReLU/add kernels the reference
+// runs implicitly (/root/reference/pytorch/unet/model.py:9-14, torchvision
+// BasicBlock/Bottleneck used by /root/reference/pytorch/resnet/main.py:40).
+//
+// Forward statistics normally come for free from the conv epilogue (per-tile partial sums);
+// bn_finalize reduces them in double precision in a fixed order (deterministic, no atomics),
+// updates the running statistics with torch semantics (unbiased running_var) and emits the
+// per-channel scale/shift consumed by bn_apply (y = relu(x*scale + shift [+ residual])).
+// Backward: bn_bwd_reduce -> bn_bwd_finalize -> bn_bwd_apply, i.e.
+//   dyr = dy * [y > 0];  dbeta = sum dyr;  dgamma = sum dyr * xhat;
+//   dx  = k1*dyr + k2*x + k3   (k* folded per channel by the finalize kernel).
+// All tensors may be channel slices of a wider buffer (ld*, *off) so UNet's skip concat is free.
+#include "common.h"
+
+namespace dlmpi {
+
+// ---------------- generic chunked row reduction layout --------------------------------------
+// A block of 256 threads walks rows; thread -> (chunk of 8 channels cc, row lane rr).
+struct RowMap {
+  int CC, RPB, cc, rr;
+  bool active;
+};
+__device__ __forceinline__ RowMap rowmap(int C) {
+  RowMap m;
+  m.CC = C >> 3;
+  m.RPB = 256 / m.CC;
+  m.cc = threadIdx.x % m.CC;
+  m.rr = threadIdx.x / m.CC;
+  m.active = m.rr < m.RPB;
+  return m;
+}
+
+// Block-level combine of per-thread [8] sums over threads that share a channel chunk; writes
+// partial[blk][k][C] for k < NS.
+// Fixed summation order over the row lanes -> bit-reproducible partials.
+template <int NS>
+__device__ void block_combine(float (*acc)[8], const RowMap& rm, int C, float* partial) {
+  __shared__ float buf[256 * NS * 8];
+#pragma unroll
+  for (int k = 0; k < NS; ++k)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) buf[(threadIdx.x * NS + k) * 8 + e] = acc[k][e];
+  __syncthreads();
+  for (int i = threadIdx.x; i < NS * C; i += 256) {
+    const int k = i / C, c = i - k * C, cc = c >> 3, e = c & 7;
+    float s = 0.f;
+    for (int r = 0; r < rm.RPB; ++r) s += buf[((r * rm.CC + cc) * NS + k) * 8 + e];
+    partial[(int64_t)blockIdx.x * NS * C + i] = s;
+  }
+}
+
+__global__ __launch_bounds__(256) void bn_stats_kernel(const uint16_t* __restrict__ x, int64_t M, int C, int ldx,
+                                                       int xoff, float* __restrict__ partial) {
+  const RowMap rm = rowmap(C);
+  float acc[2][8] = {};
+  if (rm.active) {
+    for (int64_t row = (int64_t)blockIdx.x * rm.RPB + rm.rr; row < M; row += (int64_t)gridDim.x * rm.RPB) {
+      float v[8];
+      unpack8(*reinterpret_cast<const u32x4*>(x + row * ldx + xoff + rm.cc * 8), v);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) { acc[0][e] += v[e]; acc[1][e] += v[e] * v[e]; }
+    }
+  }
+  block_combine<2>(acc, rm, C, partial);
+}
+
+__global__ __launch_bounds__(256) void bn_finalize_kernel(const float* __restrict__ partial, int ntiles, int C,
+                                                          double count, const float* gamma, const float* beta,
+                                                          float* running_mean, float* running_var, float momentum,
+                                                          float eps, float* scale, float* shift, float* save_mean,
+                                                          float* save_invstd) {
+  __shared__ double r1[8][32], r2[8][32];
+  const int lc = threadIdx.x & 31, rg = threadIdx.x >> 5;
+  const int c = blockIdx.x * 32 + lc;
+  double s1 = 0.0, s2 = 0.0;
+  if (c < C) {
+    for (int t = rg; t < ntiles; t += 8) {
+      s1 += (double)partial[(int64_t)t * 2 * C + c];
+      s2 += (double)partial[(int64_t)t * 2 * C + C + c];
+    }
+  }
+  r1[rg][lc] = s1;
+  r2[rg][lc] = s2;
+  __syncthreads();
+  if (rg == 0 && c < C) {
+    for (int g = 1; g < 8; ++g) { s1 += r1[g][lc]; s2 += r2[g][lc]; }
+    const double mean = s1 / count;
+    double var = s2 / count - mean * mean;
+    if (var < 0.0) var = 0.0;
+    const float invstd = (float)(1.0 / sqrt(var + (double)eps));
+    const float g = gamma ? gamma[c] : 1.f;
+    const float b = beta ? beta[c] : 0.f;
+    const float sc = g * invstd;
+    scale[c] = sc;
+    shift[c] = b - (float)mean * sc;
+    if (save_mean) save_mean[c] = (float)mean;
+    if (save_invstd) save_invstd[c] = invstd;
+    if (running_mean) {
+      const double unbiased = count > 1.0 ? var * count / (count - 1.0) : var;
+      running_mean[c] = (1.f - momentum) * running_mean[c] + momentum * (float)mean;
+      running_var[c] = (1.f - momentum) * running_var[c] + momentum * (float)unbiased;
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void bn_apply_kernel(const uint16_t* __restrict__ x, int ldx, int xoff, int64_t M,
+                                                       int C, FastDiv fdCC, const float* __restrict__ scale,
+                                                       const float* __restrict__ shift,
+                                                       const uint16_t* __restrict__ res, int ldres, int resoff,
+                                                       int relu, uint16_t* __restrict__ y, int ldy, int yoff) {
+  const int CC = C >> 3;
+  const int64_t total = M * CC;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    int64_t row;
+    int cc;
+    if (total < (1ll << 31)) {
+      row = fdiv((uint32_t)i, fdCC);
+      cc = (int)(i - row * CC);
+    } else {
+      row = i / CC;
+      cc = (int)(i - row * CC);
+    }
+    const int c0 = cc * 8;
+    float v[8];
+    unpack8(*reinterpret_cast<const u32x4*>(x + row * ldx + xoff + c0), v);
+    const f32x4 s0 = *reinterpret_cast<const f32x4*>(scale + c0), s1 = *reinterpret_cast<const f32x4*>(scale + c0 + 4);
+    const f32x4 h0 = *reinterpret_cast<const f32x4*>(shift + c0), h1 = *reinterpret_cast<const f32x4*>(shift + c0 + 4);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      v[e] = v[e] * s0[e] + h0[e];
+      v[e + 4] = v[e + 4] * s1[e] + h1[e];
+    }
+    if (res) {
+      float r[8];
+      unpack8(*reinterpret_cast<const u32x4*>(res + row * ldres + resoff + c0), r);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] += r[e];
+    }
+    if (relu) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.f);
+    }
+    *reinterpret_cast<u32x4*>(y + row * ldy + yoff + c0) = pack8(v);
+  }
+}
+
+// partial[blk][0][C] = sum dyr, partial[blk][1][C] = sum dyr * xhat  (x == null: only the first)
+__global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const uint16_t* __restrict__ dy, int lddy, int dyoff,
+                                                            const uint16_t* __restrict__ ym, int ldym, int ymoff,
+                                                            const uint16_t* __restrict__ x, int ldx, int xoff,
+                                                            int64_t M, int C, const float* __restrict__ mean,
+                                                            const float* __restrict__ invstd,
+                                                            float* __restrict__ partial) {
+  const RowMap rm = rowmap(C);
+  float acc[2][8] = {};
+  if (rm.active) {
+    const int c0 = rm.cc * 8;
+    float mu[8], is[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      mu[e] = x ? mean[c0 + e] : 0.f;
+      is[e] = x ? invstd[c0 + e] : 0.f;
+    }
+    for (int64_t row = (int64_t)blockIdx.x * rm.RPB + rm.rr; row < M; row += (int64_t)gridDim.x * rm.RPB) {
+      float g[8];
+      unpack8(*reinterpret_cast<const u32x4*>(dy + row * lddy + dyoff + c0), g);
+      if (ym) {
+        const u32x4 mv = *reinterpret_cast<const u32x4*>(ym + row * ldym + ymoff + c0);
+        float m[8];
+        unpack8(mv, m);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) g[e] = m[e] > 0.f ? g[e] : 0.f;
+      }
+#pragma unroll
+      for (int e = 0; e < 8; ++e) acc[0][e] += g[e];
+      if (x) {
+        float xv[8];
+        unpack8(*reinterpret_cast<const u32x4*>(x + row * ldx + xoff + c0), xv);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) acc[1][e] += g[e] * (xv[e] - mu[e]) * is[e];
+      }
+    }
+  }
+  block_combine<2>(acc, rm, C, partial);
+}
+
+// Reduces the bwd partials; accumulates dgamma/dbeta into the gradient buffers; emits
+// coef[0..2][C] = (k1, k2, k3) with dx = k1*dyr + k2*x + k3.
+__global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(const float* __restrict__ partial, int nblk, int C,
+                                                              double count, const float* gamma,
+                                                              const float* __restrict__ mean,
+                                                              const float* __restrict__ invstd, float* dgamma,
+                                                              float* dbeta, float* coef) {
+  __shared__ double r1[8][32], r2[8][32];
+  const int lc = threadIdx.x & 31, rg = threadIdx.x >> 5;
+  const int c = blockIdx.x * 32 + lc;
+  double s1 = 0.0, s2 = 0.0;
+  if (c < C) {
+    for (int t = rg; t < nblk; t += 8) {
+      s1 += (double)partial[(int64_t)t * 2 * C + c];
+      s2 += (double)partial[(int64_t)t * 2 * C + C + c];
+    }
+  }
+  r1[rg][lc] = s1;
+  r2[rg][lc] = s2;
+  __syncthreads();
+  if (rg == 0 && c < C) {
+    for (int g = 1; g < 8; ++g) { s1 += r1[g][lc]; s2 += r2[g][lc]; }
+    if (dbeta) dbeta[c] += (float)s1;
+    if (dgamma) dgamma[c] += (float)s2;
+    if (coef) {
+      const double is = invstd[c];
+      const double k1 = (gamma ? (double)gamma[c] : 1.0) * is;
+      const double k2 = -k1 * is * s2 / count;
+      const double k3 = -k1 * s1 / count - k2 * (double)mean[c];
+      coef[c] = (float)k1;
+      coef[C + c] = (float)k2;
+      coef[2 * C + c] = (float)k3;
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const uint16_t* __restrict__ dy, int lddy, int dyoff,
+                                                           const uint16_t* __restrict__ ym, int ldym, int ymoff,
+                                                           const uint16_t* __restrict__ x, int ldx, int xoff,
+                                                           int64_t M, int C, FastDiv fdCC,
+                                                           const float* __restrict__ coef, uint16_t* __restrict__ dx,
+                                                           uint16_t* __restrict__ dyr_out) {
+  const int CC = C >> 3;
+  const int64_t total = M * CC;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    int64_t row;
+    int cc;
+    if (total < (1ll << 31)) {
+      row = fdiv((uint32_t)i, fdCC);
+      cc = (int)(i - row * CC);
+    } else {
+      row = i / CC;
+      cc = (int)(i - row * CC);
+    }
+    const int c0 = cc * 8;
+    float g[8], xv[8];
+    unpack8(*reinterpret_cast<const u32x4*>(dy + row * lddy + dyoff + c0), g);
+    if (ym) {
+      float m[8];
+      unpack8(*reinterpret_cast<const u32x4*>(ym + row * ldym + ymoff + c0), m);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) g[e] = m[e] > 0.f ? g[e] : 0.f;
+    }
+    if (dyr_out) *reinterpret_cast<u32x4*>(dyr_out + row * C + c0) = pack8(g);
+    unpack8(*reinterpret_cast<const u32x4*>(x + row * ldx + xoff + c0), xv);
+    float o[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] = coef[c0 + e] * g[e] + coef[C + c0 + e] * xv[e] + coef[2 * C + c0 + e];
+    *reinterpret_cast<u32x4*>(dx + row * C + c0) = pack8(o);
+  }
+}
+
+static inline unsigned ew_blocks(int64_t total) {
+  int64_t b = (total + 255) / 256;
+  if (b > 8192) b = 8192;
+  if (b < 1) b = 1;
+  return (unsigned)b;
+}
+
+}  // namespace dlmpi
+
+using namespace dlmpi;
+
+extern "C" int dlmpi_reduce_blocks(int64_t M, int C) {
+  const int CC = C / 8;
+  const int rpb = 256 / CC;
+  int64_t b = (M + (int64_t)rpb * 16 - 1) / ((int64_t)rpb * 16);
+  if (b > 1024) b = 1024;
+  if (b < 1) b = 1;
+  return (int)b;
+}
+
+extern "C" hipError_t dlmpi_bn_stats(const uint16_t* x, int64_t M, int C, int ldx, int xoff, float* partial, int nblk,
+                                     hipStream_t s) {
+  if (C % 8 || C > 2048) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(bn_stats_kernel, dim3(nblk), dim3(256), 0, s, x, M, C, ldx, xoff, partial);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t dlmpi_bn_finalize(const float* partial, int ntiles, int C, double count, const float* gamma,
+                                        const float* beta, float* running_mean, float* running_var, float momentum,
+                                        float eps, float* scale, float* shift, float* save_mean, float* save_invstd,
+                                        hipStream_t s) {
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 31) / 32), dim3(256), 0, s, partial, ntiles, C, count, gamma, beta,
+                     running_mean, running_var, momentum, eps, scale, shift, save_mean, save_invstd);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t dlmpi_bn_apply(const uint16_t* x, int ldx, int xoff, int64_t M, int C, const float* scale,
+                                     const float* shift, const uint16_t* res, int ldres, int resoff, int relu,
+                                     uint16_t* y, int ldy, int yoff, hipStream_t s) {
+  if (C % 8) return hipErrorInvalidValue;
+  const int64_t total = M * (C / 8);
+  hipLaunchKernelGGL(bn_apply_kernel, dim3(ew_blocks(total)), dim3(256), 0, s, x, ldx, xoff, M, C,
+                     make_fastdiv(C / 8), scale, shift, res, ldres, resoff, relu, y, ldy, yoff);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t dlmpi_bn_bwd_reduce(const uint16_t* dy, int lddy, int dyoff, const uint16_t* ymask, int ldym,
+                                          int ymoff, const uint16_t* x, int ldx, int xoff, int64_t M, int C,
+                                          const float* mean, const float* invstd, float* partial, int nblk,
+                                          hipStream_t s) {
+  if (C % 8 || C > 2048) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3(nblk), dim3(256), 0, s, dy, lddy, dyoff, ymask, ldym, ymoff, x, ldx,
+                     xoff, M, C, mean, invstd, partial);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t dlmpi_bn_bwd_finalize(const float* partial, int nblk, int C, double count, const float* gamma,
+                                            const float* mean, const float* invstd, float* dgamma, float* dbeta,
+                                            float* coef, hipStream_t s) {
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 31) / 32), dim3(256), 0, s, partial, nblk, C, count, gamma,
+                     mean, invstd, dgamma, dbeta, coef);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t dlmpi_bn_bwd_apply(const uint16_t* dy, int lddy, int dyoff, const uint16_t* ymask, int ldym,
+                                         int ymoff, const uint16_t* x, int ldx, int xoff, int64_t M, int C,
+                                         const float* coef, uint16_t* dx, uint16_t* dyr_out, hipStream_t s) {
+  if (C % 8) return hipErrorInvalidValue;
+  const int64_t total = M * (C / 8);
+  hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(ew_blocks(total)), dim3(256), 0, s, dy, lddy, dyoff, ymask, ldym, ymoff,
+                     x, ldx, xoff, M, C, make_fastdiv(C / 8), coef, dx, dyr_out);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t dlmpi_channel_sum(const uint16_t* x, int64_t M, int C, int ldx, int xoff, float* out_acc,
+                                        float* partial, int nblk, hipStream_t s) {
+  hipError_t e = dlmpi_bn_bwd_reduce(x, ldx, xoff, nullptr, 0, 0, nullptr, 0, 0, M, C, nullptr, nullptr, partial,
+                                     nblk, s);
+  if (e != hipSuccess) return e;
+  return dlmpi_bn_bwd_finalize(partial, nblk, C, (double)M, nullptr, nullptr, nullptr, nullptr, out_acc, nullptr, s);
+}

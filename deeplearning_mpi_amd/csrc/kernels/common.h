@@ -1,0 +1,84 @@
+// Shared device helpers for the gfx950 (CDNA4 / MI355X) kernels.
+//
+// Conventions used by every kernel in this directory:
+//   * activations are NHWC, bf16 stored as uint16_t, channel count a multiple of 8
+//     so one 16-byte vector = 8 consecutive channels of one pixel;
+//   * master weights / gradients / BN statistics are fp32;
+//   * all launchers are `extern "C"` and take an explicit hipStream_t so they can be
+//     captured into a hipGraph (no allocation, no synchronisation inside a launcher).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include "dlmpi_kernels.h"
+
+namespace dlmpi {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef short i16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ float bf2f(uint16_t v) { return __uint_as_float(((uint32_t)v) << 16); }
+
+// Round-to-nearest-even f32 -> bf16 (hipcc lowers the cast to v_cvt_pk_bf16_f32, NaN-preserving).
+__device__ __forceinline__ uint16_t f2bf(float f) {
+  __bf16 b = (__bf16)f;
+  return __builtin_bit_cast(uint16_t, b);
+}
+
+__device__ __forceinline__ uint32_t pack2bf(float lo, float hi) {
+  return (uint32_t)f2bf(lo) | ((uint32_t)f2bf(hi) << 16);
+}
+
+// 8 bf16 packed in a u32x4 <-> 8 floats.
+__device__ __forceinline__ void unpack8(const u32x4 v, float* f) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    f[2 * i] = __uint_as_float(v[i] << 16);
+    f[2 * i + 1] = __uint_as_float(v[i] & 0xffff0000u);
+  }
+}
+__device__ __forceinline__ u32x4 pack8(const float* f) {
+  u32x4 r;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) r[i] = pack2bf(f[2 * i], f[2 * i + 1]);
+  return r;
+}
+
+__device__ __forceinline__ uint32_t fdiv(uint32_t n, const FastDiv& f) {
+  return (__umulhi(n, f.mul) + n) >> f.shr;
+}
+
+// Bijective XCD-aware block remap (cdna_hip_programming.md T1): blocks b and b+8 share an XCD
+// (observed round-robin dispatch); give each XCD a contiguous range of logical tiles so that
+// tiles sharing an operand panel share that XCD's L2.  Pure speed choice, never correctness.
+__device__ __forceinline__ uint32_t xcd_remap(uint32_t bid, uint32_t nwg) {
+  if (nwg < 16) return bid;
+  const uint32_t xcd = bid & 7, idx = bid >> 3;
+  const uint32_t q = nwg >> 3, r = nwg & 7;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + idx;
+}
+
+__device__ __forceinline__ float warp_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ double warp_sum_d(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float warp_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// 4 KiB of zeros: out-of-bounds im2col / tile pieces load from here instead of branching
+// around the load (keeps the staging loads unconditional).
+static __device__ u32x4 g_zero_page[16] = {};
+
+}  // namespace dlmpi

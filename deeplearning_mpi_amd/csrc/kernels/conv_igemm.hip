@@ -1,0 +1,292 @@
+// Implicit-GEMM convolution on CDNA4 MFMA (v_mfma_f32_16x16x32_bf16), NHWC bf16, fp32 accumulate.
+//
+// One kernel serves every "gather-A" GEMM of the framework:
+//   * Conv2d forward (any R x S, stride, pad; ResNet stem 7x7/s2, 3x3, 1x1, UNet 3x3),
+//   * Conv2d data-gradient (stride^2 sub-pixel phases, each a dense conv with its own tap list,
+//     so a stride-2 3x3 dgrad does no zero MACs),
+//   * ConvTranspose2d(k=2, s=2) forward (4 phases of a 1x1 GEMM written to strided pixels),
+//   * Linear (a 1x1 conv on a 1x1 image).
+// Replaces what the reference gets implicitly from cuDNN conv fwd/dgrad and cuBLAS
+// (call sites /root/reference/pytorch/unet/model.py:9-14, resnet main.py:40-41).
+//
+// Tile: BM (pixels) x BN (channels) x 64 (reduction), 256 threads = 4 waves in 2x2, each wave
+// (BM/2) x (BN/2) as (BM/32) x (BN/32) MFMA 16x16 tiles.  Operands are register-staged
+// (global -> VGPR -> ds_write_b128) into a double-buffered LDS image with an XOR swizzle that
+// makes the ds_read_b128 fragment reads conflict-free; the next tile's global loads are issued
+// before the current tile's MFMAs (one barrier per K-step).  Out-of-bounds im2col pieces read a
+// zero page so the staging loads stay unconditional.  The epilogue stages the fp32 tile through
+// LDS and emits 16-byte stores with fused bias / residual add / folded-BN affine / ReLU and the
+// per-channel BatchNorm partial sums of the stored (bf16-rounded) values.
+#include "common.h"
+
+namespace dlmpi {
+
+template <int BM, int BN>
+__global__ __launch_bounds__(256) void conv_igemm_kernel(const ConvArgs a) {
+  constexpr int BK = 64;
+  constexpr int WM = BM / 2, WN = BN / 2;
+  constexpr int TM = WM / 16, TN = WN / 16;
+  constexpr int AL = BM / 32, BL = BN / 32;   // 16-byte pieces per thread per tile
+  constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2;
+  constexpr int STAGE_BYTES = 2 * (A_BYTES + B_BYTES);
+  constexpr int CS_LD = BN + 4;
+  constexpr int EPI_BYTES = BM * CS_LD * 4;
+  constexpr int SMEM = STAGE_BYTES > EPI_BYTES ? STAGE_BYTES : EPI_BYTES;
+  __shared__ __attribute__((aligned(16))) char smem[SMEM];
+
+  const ConvPhase& ph = a.ph[blockIdx.z];
+  const uint32_t nwg = (uint32_t)ph.mtiles * (uint32_t)a.ntiles;
+  if (blockIdx.x >= nwg) return;
+  const uint32_t bid = xcd_remap(blockIdx.x, nwg);
+  const int mt = bid / a.ntiles, nt = bid - mt * a.ntiles;
+  const int m0 = mt * BM, n0 = nt * BN;
+  const int PQ = ph.P * ph.Q;
+  const int M = a.Nimg * PQ;
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid >> 1, wn = wid & 1;
+  const int j = tid & 7;          // 16-byte chunk of the 64-wide K slice
+  const int rbase = tid >> 3;     // 0..31
+
+  // ---- per-thread row state -------------------------------------------------------------
+  int a_h[AL], a_w[AL], a_img[AL];
+  bool a_ok[AL];
+#pragma unroll
+  for (int i = 0; i < AL; ++i) {
+    const int m = m0 + rbase + 32 * i;
+    a_ok[i] = m < M;
+    const uint32_t mm = a_ok[i] ? (uint32_t)m : 0u;
+    const uint32_t n_img = fdiv(mm, ph.fdPQ);
+    const uint32_t rem = mm - n_img * PQ;
+    const uint32_t p = fdiv(rem, ph.fdQ);
+    const uint32_t q = rem - p * ph.Q;
+    a_h[i] = (int)p * a.sa;
+    a_w[i] = (int)q * a.sa;
+    a_img[i] = (int)n_img * a.H;
+  }
+  const uint16_t* b_row[BL];
+  bool b_ok[BL];
+#pragma unroll
+  for (int i = 0; i < BL; ++i) {
+    const int n = n0 + rbase + 32 * i;
+    b_ok[i] = n < a.Kout;
+    b_row[i] = a.w + (int64_t)(b_ok[i] ? n : 0) * a.ldw;
+  }
+
+  const int C = a.C;
+  const int T = ph.Tr * ph.Ts;
+  int t_cur, c_cur;
+  if (C >= 64) { t_cur = 0; c_cur = 8 * j; }
+  else { t_cur = (8 * j) / C; c_cur = (8 * j) - t_cur * C; }
+
+  u32x4 ra[AL], rb[BL];
+
+  auto load_tile = [&](int t, int c) {
+    const bool tv = t < T;
+    const int tt = tv ? t : 0;
+    const int tr = (int)fdiv((uint32_t)tt, ph.fdTs);
+    const int ts = tt - tr * ph.Ts;
+    const int dh = ph.dh0 + tr * ph.dhs, dw = ph.dw0 + ts * ph.dws;
+    const int wt = (ph.wr0 + tr * ph.wrs) * a.S + (ph.ws0 + ts * ph.wss);
+#pragma unroll
+    for (int i = 0; i < AL; ++i) {
+      const int ih = a_h[i] + dh, iw = a_w[i] + dw;
+      const bool ok = tv && a_ok[i] && (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W;
+      const int64_t off = ((int64_t)(a_img[i] + ih) * a.W + iw) * a.ldx + a.xoff + c;
+      const u32x4* src = ok ? reinterpret_cast<const u32x4*>(a.x + off) : g_zero_page;
+      ra[i] = *src;
+    }
+#pragma unroll
+    for (int i = 0; i < BL; ++i) {
+      const bool ok = tv && b_ok[i];
+      const u32x4* src = ok ? reinterpret_cast<const u32x4*>(b_row[i] + (int64_t)wt * C + c) : g_zero_page;
+      rb[i] = *src;
+    }
+  };
+  auto store_tile = [&](int buf) {
+    char* As = smem + buf * (A_BYTES + B_BYTES);
+    char* Bs = As + A_BYTES;
+#pragma unroll
+    for (int i = 0; i < AL; ++i) {
+      const int r = rbase + 32 * i;
+      *reinterpret_cast<u32x4*>(As + r * 128 + ((j ^ ((r >> 1) & 7)) << 4)) = ra[i];
+    }
+#pragma unroll
+    for (int i = 0; i < BL; ++i) {
+      const int r = rbase + 32 * i;
+      *reinterpret_cast<u32x4*>(Bs + r * 128 + ((j ^ ((r >> 1) & 7)) << 4)) = rb[i];
+    }
+  };
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int mi = 0; mi < TM; ++mi)
+#pragma unroll
+    for (int ni = 0; ni < TN; ++ni) acc[mi][ni] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = ph.ksteps;
+  if (nk > 0) {
+    load_tile(t_cur, c_cur);
+    store_tile(0);
+    __syncthreads();
+  }
+  const int fr = lane & 15, fg = lane >> 4;
+  for (int ks = 0; ks < nk; ++ks) {
+    const int cur = ks & 1;
+    const bool more = ks + 1 < nk;
+    if (more) {
+      c_cur += a.cstep;
+      t_cur += a.tstep;
+      if (c_cur >= C) { c_cur -= C; t_cur += 1; }
+      load_tile(t_cur, c_cur);
+    }
+    const char* As = smem + cur * (A_BYTES + B_BYTES);
+    const char* Bs = As + A_BYTES;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      bf16x8 af[TM], bfr[TN];
+      const int ch = kk * 4 + fg;
+#pragma unroll
+      for (int mi = 0; mi < TM; ++mi) {
+        const int r = wm * WM + mi * 16 + fr;
+        af[mi] = *reinterpret_cast<const bf16x8*>(As + r * 128 + ((ch ^ ((r >> 1) & 7)) << 4));
+      }
+#pragma unroll
+      for (int ni = 0; ni < TN; ++ni) {
+        const int r = wn * WN + ni * 16 + fr;
+        bfr[ni] = *reinterpret_cast<const bf16x8*>(Bs + r * 128 + ((ch ^ ((r >> 1) & 7)) << 4));
+      }
+#pragma unroll
+      for (int mi = 0; mi < TM; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < TN; ++ni)
+          acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[mi], bfr[ni], acc[mi][ni], 0, 0, 0);
+    }
+    if (more) store_tile(cur ^ 1);
+    __syncthreads();
+  }
+
+  // ---- epilogue ------------------------------------------------------------------------------
+  float* Cs = reinterpret_cast<float*>(smem);
+#pragma unroll
+  for (int mi = 0; mi < TM; ++mi)
+#pragma unroll
+    for (int ni = 0; ni < TN; ++ni)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        Cs[(wm * WM + mi * 16 + fg * 4 + r) * CS_LD + wn * WN + ni * 16 + fr] = acc[mi][ni][r];
+  __syncthreads();
+
+  constexpr int CG = BN / 8;       // channel groups of 8
+  constexpr int RG = 256 / CG;     // row groups
+  const int cg = tid % CG, rg = tid / CG;
+  const int c0 = n0 + cg * 8;
+  const bool cvalid = c0 < a.Kout;
+  float bias[8], scl[8], sft[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) { bias[e] = 0.f; scl[e] = 1.f; sft[e] = 0.f; }
+  if (cvalid) {
+    if (a.bias) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) bias[e] = a.bias[c0 + e];
+    }
+    if (a.scale) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) { scl[e] = a.scale[c0 + e]; sft[e] = a.shift[c0 + e]; }
+    }
+  }
+  float s1[8], s2[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) { s1[e] = 0.f; s2[e] = 0.f; }
+
+  for (int r = rg; r < BM; r += RG) {
+    const int m = m0 + r;
+    if (m >= M || !cvalid) continue;
+    float v[8];
+    const f32x4 v0 = *reinterpret_cast<const f32x4*>(Cs + r * CS_LD + cg * 8);
+    const f32x4 v1 = *reinterpret_cast<const f32x4*>(Cs + r * CS_LD + cg * 8 + 4);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) { v[e] = v0[e] + bias[e]; v[e + 4] = v1[e] + bias[e + 4]; }
+    if (a.stats) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float rv = bf2f(f2bf(v[e]));
+        s1[e] += rv;
+        s2[e] += rv * rv;
+      }
+    }
+    if (a.scale) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = v[e] * scl[e] + sft[e];
+    }
+    const uint32_t n_img = fdiv((uint32_t)m, ph.fdPQ);
+    const uint32_t rem = (uint32_t)m - n_img * PQ;
+    const uint32_t p = fdiv(rem, ph.fdQ);
+    const uint32_t q = rem - p * ph.Q;
+    const int64_t pix = ((int64_t)n_img * a.OH + (int)p * a.so + ph.oh0) * a.OW + (int)q * a.so + ph.ow0;
+    if (a.res) {
+      float rr[8];
+      unpack8(*reinterpret_cast<const u32x4*>(a.res + pix * a.ldres + a.resoff + c0), rr);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] += rr[e];
+    }
+    if (a.relu) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.f);
+    }
+    if (a.vec_store) {
+      if (a.out_f32) {
+        float* yp = reinterpret_cast<float*>(a.y) + pix * a.ldy + a.yoff + c0;
+        *reinterpret_cast<f32x4*>(yp) = f32x4{v[0], v[1], v[2], v[3]};
+        *reinterpret_cast<f32x4*>(yp + 4) = f32x4{v[4], v[5], v[6], v[7]};
+      } else {
+        uint16_t* yp = reinterpret_cast<uint16_t*>(a.y) + pix * a.ldy + a.yoff + c0;
+        *reinterpret_cast<u32x4*>(yp) = pack8(v);
+      }
+    } else {   // narrow / unaligned output (e.g. the 1-channel UNet head written as fp32 [N,1,H,W])
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        if (c0 + e >= a.kvalid) break;
+        if (a.out_f32) reinterpret_cast<float*>(a.y)[pix * a.ldy + a.yoff + c0 + e] = v[e];
+        else reinterpret_cast<uint16_t*>(a.y)[pix * a.ldy + a.yoff + c0 + e] = f2bf(v[e]);
+      }
+    }
+  }
+
+  if (a.stats) {
+    __syncthreads();
+    float* red = reinterpret_cast<float*>(smem);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      red[rg * 2 * BN + cg * 8 + e] = s1[e];
+      red[rg * 2 * BN + BN + cg * 8 + e] = s2[e];
+    }
+    __syncthreads();
+    if (tid < BN && n0 + tid < a.Kout) {
+      float t1 = 0.f, t2 = 0.f;
+      for (int g = 0; g < RG; ++g) {
+        t1 += red[g * 2 * BN + tid];
+        t2 += red[g * 2 * BN + BN + tid];
+      }
+      a.stats[(int64_t)mt * 2 * a.Kout + n0 + tid] = t1;
+      a.stats[(int64_t)mt * 2 * a.Kout + a.Kout + n0 + tid] = t2;
+    }
+  }
+}
+
+}  // namespace dlmpi
+
+using namespace dlmpi;
+
+extern "C" hipError_t dlmpi_conv_igemm(const ConvArgs* a, int bm, int bn, hipStream_t s) {
+  int maxt = 0;
+  for (int i = 0; i < a->nphase; ++i) maxt = a->ph[i].mtiles > maxt ? a->ph[i].mtiles : maxt;
+  dim3 grid((unsigned)(maxt * a->ntiles), 1, (unsigned)a->nphase);
+  if (grid.x == 0) return hipSuccess;
+  if (bm == 128 && bn == 128) hipLaunchKernelGGL((conv_igemm_kernel<128, 128>), grid, dim3(256), 0, s, *a);
+  else if (bm == 128 && bn == 64) hipLaunchKernelGGL((conv_igemm_kernel<128, 64>), grid, dim3(256), 0, s, *a);
+  else if (bm == 64 && bn == 128) hipLaunchKernelGGL((conv_igemm_kernel<64, 128>), grid, dim3(256), 0, s, *a);
+  else if (bm == 64 && bn == 64) hipLaunchKernelGGL((conv_igemm_kernel<64, 64>), grid, dim3(256), 0, s, *a);
+  else return hipErrorInvalidValue;
+  return hipGetLastError();
+}

@@ -1,0 +1,216 @@
+// Convolution weight gradient on CDNA4 MFMA:  dW[ko][t][c] = sum_pix dY[pix][ko] * X[gather(pix,t)][c].
+// Replaces cuDNN wgrad / cuBLAS Linear weight-grad of the reference.
+//
+// Both operands arrive pixel-major (NHWC: the reduction index is the SLOW axis), so they are
+// staged row-major [64 pixels][cols] into LDS and fed to v_mfma_f32_16x16x32_bf16 through the
+// gfx950 hardware-transposing read ds_read_b64_tr_b16 (cdna_hip_programming.md T10), with the
+// XOR swizzle that makes those reads conflict-free.  The pixel axis is split across workgroups
+// (split-K); every split writes an fp32 slab, and a second kernel sums the slabs in a fixed order
+// (bit-reproducible, no float atomics) straight into the flat fp32 gradient buffer, undoing the
+// compute-layout channel padding on the way.
+//
+// Also used for ConvTranspose2d(k2,s2) weight-grad (roles of X and dY swapped, stride 2) and for
+// Linear weight-grad (1x1 "conv" on a 1x1 image).
+#include "common.h"
+
+namespace dlmpi {
+
+typedef __attribute__((address_space(3))) i16x4 lds_i16x4;
+
+// Byte offset of 16-B chunk `ch` of LDS row `row` in a tile with 256-B rows (16 chunks) or 128-B
+// rows (8 chunks).  Both XORs make the 8 rows x 32 bytes touched by one half-wave of transposed
+// reads land on 16 distinct 16-byte bank slots.
+template <int ROW_BYTES>
+__device__ __forceinline__ int tr_off(int row, int ch) {
+  if constexpr (ROW_BYTES == 256) {
+    return row * 256 + ((ch ^ (((row & 3) << 2) | ((row >> 2) & 3))) << 4);
+  } else {
+    return row * 128 + ((ch ^ ((((row >> 1) & 1) << 1) | (((row >> 3) & 1) << 2))) << 4);
+  }
+}
+
+// 16x32 MFMA operand (16 columns starting at column 16*cb, 32 reduction rows starting at k0)
+// from a row-major [k][col] LDS tile: lane (g, i) gets column i, rows k0+8g .. k0+8g+7.
+template <int ROW_BYTES>
+__device__ __forceinline__ bf16x8 tr_frag(const char* tile, int k0, int cb, int lane) {
+  const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
+  const int row = k0 + 8 * g + q;
+  const int ch = 2 * cb + (p >> 1);
+  const int byte = (p & 1) * 8;
+  const char* a0 = tile + tr_off<ROW_BYTES>(row, ch) + byte;
+  const char* a1 = tile + tr_off<ROW_BYTES>(row + 4, ch) + byte;
+  i16x4 v0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4*)(a0));
+  i16x4 v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4*)(a1));
+  typedef short i16x8 __attribute__((ext_vector_type(8)));
+  i16x8 r = __builtin_shufflevector(v0, v1, 0, 1, 2, 3, 4, 5, 6, 7);
+  return __builtin_bit_cast(bf16x8, r);
+}
+
+template <int BM>
+__global__ __launch_bounds__(256) void conv_wgrad_kernel(const WgradArgs a) {
+  constexpr int BN = 128, BK = 64;
+  constexpr int WM = BM / 2, WN = BN / 2, TM = WM / 16, TN = WN / 16;
+  constexpr int A_ROW = BM * 2, B_ROW = BN * 2;          // bytes per LDS row
+  constexpr int CA = BM / 8, CB = BN / 8;                 // 16-B chunks per row
+  constexpr int AL = BK * CA / 256, BL = BK * CB / 256;   // pieces per thread
+  constexpr int A_BYTES = BK * A_ROW, B_BYTES = BK * B_ROW;
+  __shared__ __attribute__((aligned(16))) char smem[2 * (A_BYTES + B_BYTES)];
+
+  const uint32_t ntile = (uint32_t)a.mtiles * a.ntiles;
+  const uint32_t nwg = ntile * a.splits;
+  const uint32_t bid = xcd_remap(blockIdx.x, nwg);
+  const int z = bid / ntile;
+  const int tile = bid - z * ntile;
+  const int mt = tile / a.ntiles, nt = tile - mt * a.ntiles;
+  const int m0 = mt * BM, n0 = nt * BN;
+  const int pbeg = z * a.pix_per_split;
+  const int pend = min(a.npix, pbeg + a.pix_per_split);
+  const int nk = pend > pbeg ? (pend - pbeg + BK - 1) / BK : 0;
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid >> 1, wn = wid & 1;
+  const int PQ = a.P * a.Q;
+
+  // A (dY) pieces: chunk ja of row ra + (256/CA)*i
+  const int ja = tid % CA, ra = tid / CA;
+  const bool a_colok = (m0 + 8 * ja) < a.Ko;
+  // B (X gathered) pieces: column chunk jb is a fixed (tap, channel) for the whole block
+  const int jb = tid % CB, rbb = tid / CB;
+  const int col = n0 + 8 * jb;
+  const bool b_colok = col < a.TC;
+  const uint32_t colc = b_colok ? (uint32_t)col : 0u;
+  const int t = (int)fdiv(colc, a.fdC);
+  const int cch = (int)colc - t * a.C;
+  const int tr = (int)fdiv((uint32_t)t, a.fdS);
+  const int ts = t - tr * a.S;
+  const int dh = tr - a.pad_h, dw = ts - a.pad_w;
+
+  u32x4 va[AL], vb[BL];
+  auto load_tile = [&](int pix0) {
+#pragma unroll
+    for (int i = 0; i < AL; ++i) {
+      const int pix = pix0 + ra + (256 / CA) * i;
+      const bool ok = a_colok && pix < pend;
+      const u32x4* src =
+          ok ? reinterpret_cast<const u32x4*>(a.dy + (int64_t)pix * a.ldy + a.dyoff + m0 + 8 * ja) : g_zero_page;
+      va[i] = *src;
+    }
+#pragma unroll
+    for (int i = 0; i < BL; ++i) {
+      const int pix = pix0 + rbb + (256 / CB) * i;
+      bool ok = b_colok && pix < pend;
+      const uint32_t pp = ok ? (uint32_t)pix : 0u;
+      const uint32_t n_img = fdiv(pp, a.fdPQ);
+      const uint32_t rem = pp - n_img * PQ;
+      const uint32_t p = fdiv(rem, a.fdQ);
+      const uint32_t q = rem - p * a.Q;
+      const int ih = (int)p * a.stride_h + dh, iw = (int)q * a.stride_w + dw;
+      ok = ok && (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W;
+      const int64_t off = (((int64_t)n_img * a.H + ih) * a.W + iw) * a.ldx + a.xoff + cch;
+      const u32x4* src = ok ? reinterpret_cast<const u32x4*>(a.x + off) : g_zero_page;
+      vb[i] = *src;
+    }
+  };
+  auto store_tile = [&](int buf) {
+    char* As = smem + buf * (A_BYTES + B_BYTES);
+    char* Bs = As + A_BYTES;
+#pragma unroll
+    for (int i = 0; i < AL; ++i)
+      *reinterpret_cast<u32x4*>(As + tr_off<A_ROW>(ra + (256 / CA) * i, ja)) = va[i];
+#pragma unroll
+    for (int i = 0; i < BL; ++i)
+      *reinterpret_cast<u32x4*>(Bs + tr_off<B_ROW>(rbb + (256 / CB) * i, jb)) = vb[i];
+  };
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int mi = 0; mi < TM; ++mi)
+#pragma unroll
+    for (int ni = 0; ni < TN; ++ni) acc[mi][ni] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  if (nk > 0) {
+    load_tile(pbeg);
+    store_tile(0);
+    __syncthreads();
+  }
+  for (int ks = 0; ks < nk; ++ks) {
+    const int cur = ks & 1;
+    const bool more = ks + 1 < nk;
+    if (more) load_tile(pbeg + (ks + 1) * BK);
+    const char* As = smem + cur * (A_BYTES + B_BYTES);
+    const char* Bs = As + A_BYTES;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      bf16x8 af[TM], bfr[TN];
+#pragma unroll
+      for (int mi = 0; mi < TM; ++mi) af[mi] = tr_frag<A_ROW>(As, kk * 32, (wm * WM) / 16 + mi, lane);
+#pragma unroll
+      for (int ni = 0; ni < TN; ++ni) bfr[ni] = tr_frag<B_ROW>(Bs, kk * 32, (wn * WN) / 16 + ni, lane);
+#pragma unroll
+      for (int mi = 0; mi < TM; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < TN; ++ni)
+          acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[mi], bfr[ni], acc[mi][ni], 0, 0, 0);
+    }
+    if (more) store_tile(cur ^ 1);
+    __syncthreads();
+  }
+
+  // D[row = ko][col = tc]: lane holds col (lane&15), rows 4*(lane>>4) + r.
+  const int fr = lane & 15, fg = lane >> 4;
+  float* wsz = a.ws + (int64_t)z * a.Ko * a.TC;
+#pragma unroll
+  for (int mi = 0; mi < TM; ++mi)
+#pragma unroll
+    for (int ni = 0; ni < TN; ++ni) {
+      const int cc = n0 + wn * WN + ni * 16 + fr;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int ko = m0 + wm * WM + mi * 16 + fg * 4 + r;
+        if (ko < a.Ko && cc < a.TC) wsz[(int64_t)ko * a.TC + cc] = acc[mi][ni][r];
+      }
+    }
+}
+
+// out[ko][t][c] += sum_z ws[z][ko][t][c] for c < Creal, ko < Ko_real (fixed summation order).
+__global__ void wgrad_reduce_kernel(const float* __restrict__ ws, int splits, int Ko, int T, int Cpad, int Creal,
+                                    int Ko_real, float* __restrict__ out) {
+  const int64_t TC = (int64_t)T * Cpad;
+  const int64_t total = (int64_t)Ko_real * TC;
+  const int64_t zstride = (int64_t)Ko * TC;
+  for (int64_t idx = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; idx < total;
+       idx += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t ko = idx / TC;
+    const int64_t rem = idx - ko * TC;
+    const int64_t tt = rem / Cpad;
+    const int c = (int)(rem - tt * Cpad);
+    if (c >= Creal) continue;
+    float s = 0.f;
+    for (int zz = 0; zz < splits; ++zz) s += ws[zz * zstride + idx];
+    out[(ko * T + tt) * Creal + c] += s;
+  }
+}
+
+}  // namespace dlmpi
+
+using namespace dlmpi;
+
+extern "C" hipError_t dlmpi_conv_wgrad(const WgradArgs* a, int bm, hipStream_t s) {
+  const unsigned nwg = (unsigned)(a->mtiles * a->ntiles * a->splits);
+  if (nwg == 0) return hipSuccess;
+  if (bm == 128) hipLaunchKernelGGL((conv_wgrad_kernel<128>), dim3(nwg), dim3(256), 0, s, *a);
+  else if (bm == 64) hipLaunchKernelGGL((conv_wgrad_kernel<64>), dim3(nwg), dim3(256), 0, s, *a);
+  else return hipErrorInvalidValue;
+  return hipGetLastError();
+}
+
+extern "C" hipError_t dlmpi_wgrad_reduce(const float* ws, int splits, int Ko, int T, int Cpad, int Creal, int Ko_real,
+                                         float* out, hipStream_t s) {
+  const int64_t total = (int64_t)Ko_real * T * Cpad;
+  if (total == 0) return hipSuccess;
+  int64_t blocks = (total + 255) / 256;
+  if (blocks > 4096) blocks = 4096;
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)blocks), dim3(256), 0, s, ws, splits, Ko, T, Cpad, Creal,
+                     Ko_real, out);
+  return hipGetLastError();
+}

@@ -1,0 +1,176 @@
+// Host-visible interface of the gfx950 kernel library (pure HIP, no torch dependency).
+// Included by the .hip kernel files and by the torch binding (compiled with g++).
+#pragma once
+#include <hip/hip_runtime_api.h>
+#include <stdint.h>
+
+namespace dlmpi {
+
+// Unsigned fast division by a runtime constant, valid for n < 2^31:
+// q = (mulhi(n, m) + n) >> l with l = ceil(log2 d), m = floor(2^32 (2^l - d) / d) + 1.
+struct FastDiv {
+  uint32_t d, mul, shr;
+};
+inline FastDiv make_fastdiv(uint32_t d) {
+  FastDiv f;
+  f.d = d;
+  uint32_t l = 0;
+  while ((1ull << l) < d) ++l;
+  f.mul = (uint32_t)((((1ull << 32) * ((1ull << l) - d)) / d) + 1);
+  f.shr = l;
+  return f;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Implicit-GEMM convolution on MFMA (forward, data-gradient, transposed-conv forward, linear).
+//
+// GEMM rows   m = (n, p, q) over an output grid P x Q of one "phase";
+// GEMM cols   k = output channel (Kout);
+// reduction   over taps t = (tr, ts) in a Tr x Ts grid and C input channels.
+// For tap t the A row reads input pixel  ih = p*sa + dh0 + tr*dhs,  iw = q*sa + dw0 + ts*dws
+// and the B row reads weight tap index   (wr0 + tr*wrs)*S + (ws0 + ts*wss)  of a [Kout][R][S][C]
+// weight.  The result goes to output pixel (p*so + oh0, q*so + ow0).
+// A forward conv is one phase (sa = stride, dh0 = -pad); a strided data-gradient or a
+// transposed conv is stride^2 phases (sub-pixel decomposition), selected by blockIdx.z.
+// ---------------------------------------------------------------------------------------------
+struct ConvPhase {
+  int P, Q;
+  int Tr, Ts;
+  int dh0, dhs, dw0, dws;
+  int wr0, wrs, ws0, wss;
+  int oh0, ow0;
+  int mtiles;   // ceil(N*P*Q / BM)
+  int ksteps;   // ceil(Tr*Ts*C / 64)
+  FastDiv fdPQ, fdQ, fdTs;
+};
+
+struct ConvArgs {
+  const uint16_t* x;
+  int H, W, C, ldx, xoff;          // input NHWC, pixel stride ldx, channel offset xoff
+  const uint16_t* w;
+  int ldw, S;                      // weight row stride (= R*S*C), S of the weight tap grid
+  void* y;
+  int OH, OW, ldy, yoff;           // output NHWC geometry
+  int so, sa;                      // output / input coordinate multipliers
+  int out_f32;                     // 1: fp32 output, 0: bf16 output
+  int Nimg, Kout;
+  int kvalid;                      // output channels actually stored (<= Kout)
+  int vec_store;                   // 1: 16-byte stores legal (ldy, yoff multiples of 8 and kvalid == Kout)
+  const float* bias;               // [Kout] or null
+  const uint16_t* res;             // residual added in the epilogue (same pixel grid as y) or null
+  int ldres, resoff;
+  const float* scale;              // per-channel affine after bias (folded eval BN) or null
+  const float* shift;
+  int relu;
+  float* stats;                    // BN partial sums [mtiles][2][Kout] of the (bf16-rounded) output, or null
+  int ntiles;
+  int nphase;
+  int cstep, tstep;                // K-iteration: c += cstep, t += tstep per 64-wide step
+  ConvPhase ph[4];
+};
+
+// ---------------------------------------------------------------------------------------------
+// Weight gradient:  dW[ko][t][c] = sum_pix dY[pix][ko] * X[gather(pix, t)][c]   (split over pix)
+// ---------------------------------------------------------------------------------------------
+struct WgradArgs {
+  const uint16_t* dy;
+  int ldy, dyoff, Ko;
+  const uint16_t* x;
+  int H, W, C, ldx, xoff;
+  int Nimg, P, Q, S, stride_h, stride_w, pad_h, pad_w;
+  int TC;                          // R*S*C
+  int npix, pix_per_split;
+  int mtiles, ntiles, splits;
+  FastDiv fdPQ, fdQ, fdC, fdS;
+  float* ws;                       // [splits][Ko][TC] fp32 partials
+};
+
+}  // namespace dlmpi
+
+extern "C" {
+// conv / gemm
+hipError_t dlmpi_conv_igemm(const dlmpi::ConvArgs* a, int bm, int bn, hipStream_t s);
+hipError_t dlmpi_conv_wgrad(const dlmpi::WgradArgs* a, int bm, hipStream_t s);
+// sum of split partials -> grad (accumulated), with channel un-padding and row limit
+hipError_t dlmpi_wgrad_reduce(const float* ws, int splits, int Ko, int T, int Cpad, int Creal,
+                              int Ko_real, float* out, hipStream_t s);
+
+// batch norm
+hipError_t dlmpi_bn_finalize(const float* partial, int ntiles, int C, double count, const float* gamma,
+                             const float* beta, float* running_mean, float* running_var, float momentum,
+                             float eps, float* scale, float* shift, float* save_mean, float* save_invstd,
+                             hipStream_t s);
+hipError_t dlmpi_bn_stats(const uint16_t* x, int64_t M, int C, int ldx, int xoff, float* partial, int nblk,
+                          hipStream_t s);
+hipError_t dlmpi_bn_apply(const uint16_t* x, int ldx, int xoff, int64_t M, int C, const float* scale,
+                          const float* shift, const uint16_t* res, int ldres, int resoff, int relu, uint16_t* y,
+                          int ldy, int yoff, hipStream_t s);
+hipError_t dlmpi_bn_bwd_reduce(const uint16_t* dy, int lddy, int dyoff, const uint16_t* ymask, int ldym, int ymoff,
+                               const uint16_t* x, int ldx, int xoff, int64_t M, int C, const float* mean,
+                               const float* invstd, float* partial, int nblk, hipStream_t s);
+hipError_t dlmpi_bn_bwd_finalize(const float* partial, int nblk, int C, double count, const float* gamma,
+                                 const float* mean, const float* invstd, float* dgamma, float* dbeta,
+                                 float* coef, hipStream_t s);
+hipError_t dlmpi_bn_bwd_apply(const uint16_t* dy, int lddy, int dyoff, const uint16_t* ymask, int ldym, int ymoff,
+                              const uint16_t* x, int ldx, int xoff, int64_t M, int C, const float* coef,
+                              uint16_t* dx, uint16_t* dyr_out, hipStream_t s);
+hipError_t dlmpi_channel_sum(const uint16_t* x, int64_t M, int C, int ldx, int xoff, float* out_acc, float* partial,
+                             int nblk, hipStream_t s);
+int dlmpi_reduce_blocks(int64_t M, int C);
+
+// pooling / layout
+hipError_t dlmpi_maxpool_fwd(const uint16_t* x, int N, int H, int W, int C, int ldx, int xoff, int k, int stride,
+                             int pad, uint16_t* y, uint8_t* idx, int OH, int OW, hipStream_t s);
+hipError_t dlmpi_maxpool_bwd(const uint16_t* dy, const uint8_t* idx, int N, int H, int W, int C, int k, int stride,
+                             int pad, int OH, int OW, const uint16_t* add, int ldadd, int addoff, uint16_t* dx,
+                             int lddx, int dxoff, hipStream_t s);
+hipError_t dlmpi_avgpool_fwd(const uint16_t* x, int N, int HW, int C, uint16_t* y, hipStream_t s);
+hipError_t dlmpi_avgpool_bwd(const uint16_t* dy, int N, int HW, int C, uint16_t* dx, hipStream_t s);
+hipError_t dlmpi_nchw_to_nhwc(const float* x, int N, int C, int H, int W, int Cpad, uint16_t* y, hipStream_t s);
+hipError_t dlmpi_upsample2x_fwd(const uint16_t* x, int N, int H, int W, int C, int ldx, int xoff, uint16_t* y,
+                                int ldy, int yoff, hipStream_t s);
+hipError_t dlmpi_upsample2x_bwd(const uint16_t* dy, int N, int H, int W, int C, int lddy, int dyoff, float* ws,
+                                uint16_t* dx, hipStream_t s);
+
+// weights: multi-tensor strided 4-D gather + cast fp32 -> bf16 (with zero padding)
+struct CastEntry {
+  const float* src;
+  uint16_t* dst;
+  int d[4];        // destination dims (contiguous)
+  int valid[4];    // indices >= valid are zero
+  int64_t st[4];   // source strides (elements)
+  int64_t start;   // first destination element of this entry in the global enumeration
+};
+hipError_t dlmpi_cast_weights(const CastEntry* entries_dev, int n, int64_t total, hipStream_t s);
+
+// losses (forward saves what the backward needs; backward reads the upstream grad from device)
+hipError_t dlmpi_softmax_ce_fwd(const float* logits, int ldl, const int64_t* labels, int N, int K, float* loss_rows,
+                                float* lse, hipStream_t s);
+hipError_t dlmpi_softmax_ce_bwd(const float* logits, int ldl, const int64_t* labels, const float* lse, int N, int K,
+                                int ldd, const float* go, float scale, float* dlogits, hipStream_t s);
+hipError_t dlmpi_bce_fwd(const float* logits, int ldl, const float* target, int64_t M, float* partial, int nblk,
+                         hipStream_t s);
+hipError_t dlmpi_bce_bwd(const float* logits, int ldl, const float* target, int64_t M, const float* go, float scale,
+                         float* dlogits, hipStream_t s);
+hipError_t dlmpi_sum_f32(const float* x, int64_t n, float* out, float scale, hipStream_t s);
+
+// eval
+hipError_t dlmpi_argmax_correct(const float* logits, int ldl, const int64_t* labels, int N, int K, int* correct,
+                                hipStream_t s);
+hipError_t dlmpi_dice(const float* logits, int ldl, const float* target, int N, int64_t HW, float* dice,
+                      hipStream_t s);
+
+// optimizers on flat fp32 buffers
+hipError_t dlmpi_sgd(float* p, const float* g, float* m, int64_t n, float lr, float momentum, float dampening,
+                     float wd, int nesterov, int first, const float* skip_flag, hipStream_t s);
+hipError_t dlmpi_adam(float* p, const float* g, float* m, float* v, int64_t n, float lr, float b1, float b2,
+                      float eps, float wd, int adamw, float bc1, float bc2, const float* clip_coef, hipStream_t s);
+hipError_t dlmpi_sumsq(const float* x, int64_t n, float* partial, int nblk, hipStream_t s);
+hipError_t dlmpi_clip_coef(const float* partial, int nblk, float max_norm, float* norm_out, float* coef_out,
+                           hipStream_t s);
+hipError_t dlmpi_scale_f32(float* x, int64_t n, const float* coef, hipStream_t s);
+
+// comm helpers
+hipError_t dlmpi_pack(const void* const* srcs, const int64_t* offs, int n, int64_t total_bytes, void* dst,
+                      hipStream_t s);
+}

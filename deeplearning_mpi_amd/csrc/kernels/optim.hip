@@ -1,0 +1,149 @@
+// Fused optimizers over the flat fp32 parameter / gradient / state buffers of a ParamArena:
+// one launch updates every parameter of the model (replaces the foreach SGD/Adam kernels and
+// clip_grad_norm_ of the reference: /root/reference/pytorch/resnet/main.py:114,132,
+// /root/reference/pytorch/unet/train.py:160-161,194,196).  Semantics follow torch.optim
+// (SGD momentum/dampening/nesterov/L2 weight decay, Adam/AdamW with bias correction).
+// `skip_flag` (device scalar, non-zero = skip) lets all ranks skip a step collectively when the
+// all-reduced gradient is non-finite, without a host synchronisation.
+#include "common.h"
+
+namespace dlmpi {
+
+__global__ __launch_bounds__(256) void sgd_kernel(float* __restrict__ p, const float* __restrict__ g,
+                                                  float* __restrict__ m, int64_t n, float lr, float momentum,
+                                                  float dampening, float wd, int nesterov, int first,
+                                                  const float* __restrict__ skip_flag) {
+  if (skip_flag && *skip_flag != 0.f) return;
+  const int64_t n4 = n >> 2;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x) {
+    f32x4 pv = reinterpret_cast<f32x4*>(p)[i];
+    f32x4 gv = reinterpret_cast<const f32x4*>(g)[i];
+    if (wd != 0.f) gv += wd * pv;
+    if (momentum != 0.f) {
+      f32x4 mv = first ? gv : momentum * reinterpret_cast<f32x4*>(m)[i] + (1.f - dampening) * gv;
+      reinterpret_cast<f32x4*>(m)[i] = mv;
+      gv = nesterov ? gv + momentum * mv : mv;
+    }
+    reinterpret_cast<f32x4*>(p)[i] = pv - lr * gv;
+  }
+  // tail
+  const int64_t t = (n4 << 2) + blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (blockIdx.x == 0 && t < n) {
+    float pv = p[t], gv = g[t];
+    if (wd != 0.f) gv += wd * pv;
+    if (momentum != 0.f) {
+      const float mv = first ? gv : momentum * m[t] + (1.f - dampening) * gv;
+      m[t] = mv;
+      gv = nesterov ? gv + momentum * mv : mv;
+    }
+    p[t] = pv - lr * gv;
+  }
+}
+
+__device__ __forceinline__ void adam_elem(float& p, float g, float& m, float& v, float lr, float b1, float b2,
+                                          float eps, float wd, int adamw, float bc1, float bc2, float coef) {
+  g *= coef;
+  if (wd != 0.f) {
+    if (adamw) p *= (1.f - lr * wd);
+    else g += wd * p;
+  }
+  m += (g - m) * (1.f - b1);             // torch: exp_avg.lerp_(grad, 1 - beta1)
+  v = v * b2 + (1.f - b2) * g * g;
+  const float denom = sqrtf(v) / sqrtf(bc2) + eps;
+  p -= (lr / bc1) * m / denom;
+}
+
+__global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, const float* __restrict__ g,
+                                                   float* __restrict__ m, float* __restrict__ v, int64_t n, float lr,
+                                                   float b1, float b2, float eps, float wd, int adamw, float bc1,
+                                                   float bc2, const float* __restrict__ clip_coef) {
+  const float coef = clip_coef ? clip_coef[0] : 1.f;
+  if (clip_coef && clip_coef[1] != 0.f) return;   // non-finite gradient norm: collective skip
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    float pv = p[i], mv = m[i], vv = v[i];
+    adam_elem(pv, g[i], mv, vv, lr, b1, b2, eps, wd, adamw, bc1, bc2, coef);
+    p[i] = pv;
+    m[i] = mv;
+    v[i] = vv;
+  }
+}
+
+__global__ __launch_bounds__(256) void sumsq_kernel(const float* __restrict__ x, int64_t n,
+                                                    float* __restrict__ partial) {
+  __shared__ float sh[4];
+  float s = 0.f;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const float v = x[i];
+    s += v * v;
+  }
+  s = warp_sum(s);
+  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) partial[blockIdx.x] = sh[0] + sh[1] + sh[2] + sh[3];
+}
+
+// norm = sqrt(sum partial); coef_out[0] = min(1, max_norm / (norm + 1e-6)); coef_out[1] = !isfinite(norm)
+__global__ __launch_bounds__(256) void clip_coef_kernel(const float* __restrict__ partial, int nblk, float max_norm,
+                                                        float* __restrict__ norm_out, float* __restrict__ coef_out) {
+  __shared__ double sh[4];
+  double s = 0.0;
+  for (int i = threadIdx.x; i < nblk; i += blockDim.x) s += (double)partial[i];
+  s = warp_sum_d(s);
+  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const double tot = sh[0] + sh[1] + sh[2] + sh[3];
+    const float norm = (float)sqrt(tot);
+    if (norm_out) *norm_out = norm;
+    if (coef_out) {
+      const float c = max_norm / (norm + 1e-6f);
+      coef_out[0] = c < 1.f ? c : 1.f;
+      coef_out[1] = isfinite(norm) ? 0.f : 1.f;
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void scale_kernel(float* __restrict__ x, int64_t n, const float* __restrict__ coef) {
+  const float c = coef[0];
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    x[i] *= c;
+}
+
+static inline unsigned blocks_for(int64_t n) {
+  int64_t b = (n + 255) / 256;
+  if (b > 4096) b = 4096;
+  if (b < 1) b = 1;
+  return (unsigned)b;
+}
+
+}  // namespace dlmpi
+
+using namespace dlmpi;
+
+extern "C" hipError_t dlmpi_sgd(float* p, const float* g, float* m, int64_t n, float lr, float momentum,
+                                float dampening, float wd, int nesterov, int first, const float* skip_flag,
+                                hipStream_t s) {
+  hipLaunchKernelGGL(sgd_kernel, dim3(blocks_for(n / 4 + 1)), dim3(256), 0, s, p, g, m, n, lr, momentum, dampening,
+                     wd, nesterov, first, skip_flag);
+  return hipGetLastError();
+}
+extern "C" hipError_t dlmpi_adam(float* p, const float* g, float* m, float* v, int64_t n, float lr, float b1, float b2,
+                                 float eps, float wd, int adamw, float bc1, float bc2, const float* clip_coef,
+                                 hipStream_t s) {
+  hipLaunchKernelGGL(adam_kernel, dim3(blocks_for(n)), dim3(256), 0, s, p, g, m, v, n, lr, b1, b2, eps, wd, adamw,
+                     bc1, bc2, clip_coef);
+  return hipGetLastError();
+}
+extern "C" hipError_t dlmpi_sumsq(const float* x, int64_t n, float* partial, int nblk, hipStream_t s) {
+  hipLaunchKernelGGL(sumsq_kernel, dim3(nblk), dim3(256), 0, s, x, n, partial);
+  return hipGetLastError();
+}
+extern "C" hipError_t dlmpi_clip_coef(const float* partial, int nblk, float max_norm, float* norm_out,
+                                      float* coef_out, hipStream_t s) {
+  hipLaunchKernelGGL(clip_coef_kernel, dim3(1), dim3(256), 0, s, partial, nblk, max_norm, norm_out, coef_out);
+  return hipGetLastError();
+}
+extern "C" hipError_t dlmpi_scale_f32(float* x, int64_t n, const float* coef, hipStream_t s) {
+  hipLaunchKernelGGL(scale_kernel, dim3(blocks_for(n)), dim3(256), 0, s, x, n, coef);
+  return hipGetLastError();
+}

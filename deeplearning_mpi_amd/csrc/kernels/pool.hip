@@ -1,0 +1,286 @@
+// Pooling / layout / resampling kernels (NHWC bf16, 8 channels per thread, 16-byte vectors).
+// Replace ATen MaxPool2d (ResNet stem 3x3/s2/p1, UNet 2x2/s2: /root/reference/pytorch/unet/model.py:25),
+// AdaptiveAvgPool2d(1) (ResNet head), the host-side NCHW fp32 -> NHWC bf16 input conversion, and
+// nn.Upsample(scale_factor=2, mode='bilinear', align_corners=True) (model.py:39-40).
+#include "common.h"
+
+namespace dlmpi {
+
+static inline unsigned ew_blocks(int64_t total) {
+  int64_t b = (total + 255) / 256;
+  if (b > 16384) b = 16384;
+  if (b < 1) b = 1;
+  return (unsigned)b;
+}
+
+// Max pool forward; idx stores the winning window position (kh*k + kw) per channel, first max
+// in scan order wins (torch semantics).  Padding never wins.
+__global__ void maxpool_fwd_kernel(const uint16_t* __restrict__ x, int N, int H, int W, int C, int ldx, int xoff,
+                                   int k, int stride, int pad, uint16_t* __restrict__ y, uint8_t* __restrict__ idx,
+                                   int OH, int OW) {
+  const int CC = C >> 3;
+  const int64_t total = (int64_t)N * OH * OW * CC;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int cc = (int)(i % CC);
+    int64_t pix = i / CC;
+    const int ow = (int)(pix % OW);
+    const int64_t t2 = pix / OW;
+    const int oh = (int)(t2 % OH);
+    const int n = (int)(t2 / OH);
+    float best[8];
+    uint8_t bi[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) { best[e] = -INFINITY; bi[e] = 0; }
+    for (int kh = 0; kh < k; ++kh) {
+      const int ih = oh * stride - pad + kh;
+      if ((unsigned)ih >= (unsigned)H) continue;
+      for (int kw = 0; kw < k; ++kw) {
+        const int iw = ow * stride - pad + kw;
+        if ((unsigned)iw >= (unsigned)W) continue;
+        float v[8];
+        unpack8(*reinterpret_cast<const u32x4*>(x + (((int64_t)n * H + ih) * W + iw) * ldx + xoff + cc * 8), v);
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+          if (v[e] > best[e] || (v[e] != v[e] && best[e] == best[e])) { best[e] = v[e]; bi[e] = (uint8_t)(kh * k + kw); }
+      }
+    }
+    *reinterpret_cast<u32x4*>(y + pix * C + cc * 8) = pack8(best);
+    uint64_t packed = 0;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) packed |= (uint64_t)bi[e] << (8 * e);
+    *reinterpret_cast<uint64_t*>(idx + pix * C + cc * 8) = packed;
+  }
+}
+
+// Max pool backward as a gather (no atomics): each input pixel sums the gradients of the windows
+// that selected it; optionally adds a second gradient source (UNet skip-concat slice).
+__global__ void maxpool_bwd_kernel(const uint16_t* __restrict__ dy, const uint8_t* __restrict__ idx, int N, int H,
+                                   int W, int C, int k, int stride, int pad, int OH, int OW,
+                                   const uint16_t* __restrict__ add, int ldadd, int addoff, uint16_t* __restrict__ dx,
+                                   int lddx, int dxoff) {
+  const int CC = C >> 3;
+  const int64_t total = (int64_t)N * H * W * CC;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int cc = (int)(i % CC);
+    const int64_t pix = i / CC;
+    const int iw = (int)(pix % W);
+    const int64_t t2 = pix / W;
+    const int ih = (int)(t2 % H);
+    const int n = (int)(t2 / H);
+    float g[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (add) unpack8(*reinterpret_cast<const u32x4*>(add + pix * ldadd + addoff + cc * 8), g);
+    // windows oh with oh*stride - pad <= ih <= oh*stride - pad + k - 1
+    int oh_lo = ih + pad - k + 1;
+    oh_lo = oh_lo <= 0 ? 0 : (oh_lo + stride - 1) / stride;
+    const int oh_hi = min((ih + pad) / stride, OH - 1);
+    int ow_lo = iw + pad - k + 1;
+    ow_lo = ow_lo <= 0 ? 0 : (ow_lo + stride - 1) / stride;
+    const int ow_hi = min((iw + pad) / stride, OW - 1);
+    for (int oh = oh_lo; oh <= oh_hi; ++oh) {
+      for (int ow = ow_lo; ow <= ow_hi; ++ow) {
+        const uint8_t want = (uint8_t)((ih - (oh * stride - pad)) * k + (iw - (ow * stride - pad)));
+        const int64_t op = ((int64_t)n * OH + oh) * OW + ow;
+        const uint64_t id = *reinterpret_cast<const uint64_t*>(idx + op * C + cc * 8);
+        float d[8];
+        unpack8(*reinterpret_cast<const u32x4*>(dy + op * C + cc * 8), d);
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+          if (((id >> (8 * e)) & 0xff) == want) g[e] += d[e];
+      }
+    }
+    *reinterpret_cast<u32x4*>(dx + pix * lddx + dxoff + cc * 8) = pack8(g);
+  }
+}
+
+// Global average pool [N][HW][C] -> [N][C]
+__global__ void avgpool_fwd_kernel(const uint16_t* __restrict__ x, int N, int HW, int C, uint16_t* __restrict__ y) {
+  const int CC = C >> 3;
+  const int64_t total = (int64_t)N * CC;
+  const float inv = 1.f / (float)HW;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int cc = (int)(i % CC);
+    const int n = (int)(i / CC);
+    float s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (int p = 0; p < HW; ++p) {
+      float v[8];
+      unpack8(*reinterpret_cast<const u32x4*>(x + ((int64_t)n * HW + p) * C + cc * 8), v);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) s[e] += v[e];
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) s[e] *= inv;
+    *reinterpret_cast<u32x4*>(y + (int64_t)n * C + cc * 8) = pack8(s);
+  }
+}
+
+__global__ void avgpool_bwd_kernel(const uint16_t* __restrict__ dy, int N, int HW, int C, uint16_t* __restrict__ dx) {
+  const int CC = C >> 3;
+  const int64_t total = (int64_t)N * HW * CC;
+  const float inv = 1.f / (float)HW;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int cc = (int)(i % CC);
+    const int64_t pix = i / CC;
+    const int n = (int)(pix / HW);
+    float v[8];
+    unpack8(*reinterpret_cast<const u32x4*>(dy + (int64_t)n * C + cc * 8), v);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] *= inv;
+    *reinterpret_cast<u32x4*>(dx + pix * C + cc * 8) = pack8(v);
+  }
+}
+
+// NCHW fp32 -> NHWC bf16 with channel zero-padding to Cpad (multiple of 8).
+__global__ void nchw_to_nhwc_kernel(const float* __restrict__ x, int N, int C, int H, int W, int Cpad,
+                                    uint16_t* __restrict__ y) {
+  const int CC = Cpad >> 3;
+  const int64_t HW = (int64_t)H * W;
+  const int64_t total = (int64_t)N * HW * CC;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t pix = i / CC;   // cc-major inner loop keeps reads of one channel plane coalesced
+    const int cc = (int)(i - pix * CC);
+    const int64_t n = pix / HW, hw = pix - n * HW;
+    float v[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int c = cc * 8 + e;
+      v[e] = c < C ? x[(n * C + c) * HW + hw] : 0.f;
+    }
+    *reinterpret_cast<u32x4*>(y + pix * Cpad + cc * 8) = pack8(v);
+  }
+}
+
+// Bilinear x2 upsample, align_corners=True: src = o * (in-1)/(out-1).
+__global__ void upsample2x_fwd_kernel(const uint16_t* __restrict__ x, int N, int H, int W, int C, int ldx, int xoff,
+                                      uint16_t* __restrict__ y, int ldy, int yoff) {
+  const int OH = 2 * H, OW = 2 * W, CC = C >> 3;
+  const float sh = OH > 1 ? (float)(H - 1) / (float)(OH - 1) : 0.f;
+  const float sw = OW > 1 ? (float)(W - 1) / (float)(OW - 1) : 0.f;
+  const int64_t total = (int64_t)N * OH * OW * CC;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int cc = (int)(i % CC);
+    const int64_t pix = i / CC;
+    const int ow = (int)(pix % OW);
+    const int64_t t2 = pix / OW;
+    const int oh = (int)(t2 % OH);
+    const int n = (int)(t2 / OH);
+    const float fh = oh * sh, fw = ow * sw;
+    const int h0 = (int)fh, w0 = (int)fw;
+    const int h1 = min(h0 + 1, H - 1), w1 = min(w0 + 1, W - 1);
+    const float lh = fh - h0, lw = fw - w0;
+    float a[8], b[8], c[8], d[8], o[8];
+    const int64_t base = (int64_t)n * H;
+    unpack8(*reinterpret_cast<const u32x4*>(x + ((base + h0) * W + w0) * ldx + xoff + cc * 8), a);
+    unpack8(*reinterpret_cast<const u32x4*>(x + ((base + h0) * W + w1) * ldx + xoff + cc * 8), b);
+    unpack8(*reinterpret_cast<const u32x4*>(x + ((base + h1) * W + w0) * ldx + xoff + cc * 8), c);
+    unpack8(*reinterpret_cast<const u32x4*>(x + ((base + h1) * W + w1) * ldx + xoff + cc * 8), d);
+#pragma unroll
+    for (int e = 0; e < 8; ++e)
+      o[e] = (1.f - lh) * ((1.f - lw) * a[e] + lw * b[e]) + lh * ((1.f - lw) * c[e] + lw * d[e]);
+    *reinterpret_cast<u32x4*>(y + pix * ldy + yoff + cc * 8) = pack8(o);
+  }
+}
+
+__global__ void upsample2x_bwd_scatter_kernel(const uint16_t* __restrict__ dy, int N, int H, int W, int C, int lddy,
+                                              int dyoff, float* __restrict__ ws) {
+  const int OH = 2 * H, OW = 2 * W, CC = C >> 3;
+  const float sh = OH > 1 ? (float)(H - 1) / (float)(OH - 1) : 0.f;
+  const float sw = OW > 1 ? (float)(W - 1) / (float)(OW - 1) : 0.f;
+  const int64_t total = (int64_t)N * OH * OW * CC;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int cc = (int)(i % CC);
+    const int64_t pix = i / CC;
+    const int ow = (int)(pix % OW);
+    const int64_t t2 = pix / OW;
+    const int oh = (int)(t2 % OH);
+    const int n = (int)(t2 / OH);
+    const float fh = oh * sh, fw = ow * sw;
+    const int h0 = (int)fh, w0 = (int)fw;
+    const int h1 = min(h0 + 1, H - 1), w1 = min(w0 + 1, W - 1);
+    const float lh = fh - h0, lw = fw - w0;
+    float g[8];
+    unpack8(*reinterpret_cast<const u32x4*>(dy + pix * lddy + dyoff + cc * 8), g);
+    const int64_t base = (int64_t)n * H;
+    const int64_t p00 = ((base + h0) * W + w0) * C, p01 = ((base + h0) * W + w1) * C;
+    const int64_t p10 = ((base + h1) * W + w0) * C, p11 = ((base + h1) * W + w1) * C;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int c = cc * 8 + e;
+      atomicAdd(ws + p00 + c, (1.f - lh) * (1.f - lw) * g[e]);
+      atomicAdd(ws + p01 + c, (1.f - lh) * lw * g[e]);
+      atomicAdd(ws + p10 + c, lh * (1.f - lw) * g[e]);
+      atomicAdd(ws + p11 + c, lh * lw * g[e]);
+    }
+  }
+}
+
+__global__ void f32_to_bf16_kernel(const float* __restrict__ x, int64_t n8, uint16_t* __restrict__ y) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n8; i += (int64_t)gridDim.x * blockDim.x) {
+    const f32x4 a = *reinterpret_cast<const f32x4*>(x + 8 * i), b = *reinterpret_cast<const f32x4*>(x + 8 * i + 4);
+    const float v[8] = {a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+    *reinterpret_cast<u32x4*>(y + 8 * i) = pack8(v);
+  }
+}
+
+}  // namespace dlmpi
+
+using namespace dlmpi;
+
+extern "C" hipError_t dlmpi_maxpool_fwd(const uint16_t* x, int N, int H, int W, int C, int ldx, int xoff, int k,
+                                        int stride, int pad, uint16_t* y, uint8_t* idx, int OH, int OW,
+                                        hipStream_t s) {
+  if (C % 8) return hipErrorInvalidValue;
+  const int64_t total = (int64_t)N * OH * OW * (C / 8);
+  hipLaunchKernelGGL(maxpool_fwd_kernel, dim3(ew_blocks(total)), dim3(256), 0, s, x, N, H, W, C, ldx, xoff, k, stride,
+                     pad, y, idx, OH, OW);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t dlmpi_maxpool_bwd(const uint16_t* dy, const uint8_t* idx, int N, int H, int W, int C, int k,
+                                        int stride, int pad, int OH, int OW, const uint16_t* add, int ldadd,
+                                        int addoff, uint16_t* dx, int lddx, int dxoff, hipStream_t s) {
+  if (C % 8) return hipErrorInvalidValue;
+  const int64_t total = (int64_t)N * H * W * (C / 8);
+  hipLaunchKernelGGL(maxpool_bwd_kernel, dim3(ew_blocks(total)), dim3(256), 0, s, dy, idx, N, H, W, C, k, stride, pad,
+                     OH, OW, add, ldadd, addoff, dx, lddx, dxoff);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t dlmpi_avgpool_fwd(const uint16_t* x, int N, int HW, int C, uint16_t* y, hipStream_t s) {
+  const int64_t total = (int64_t)N * (C / 8);
+  hipLaunchKernelGGL(avgpool_fwd_kernel, dim3(ew_blocks(total)), dim3(256), 0, s, x, N, HW, C, y);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t dlmpi_avgpool_bwd(const uint16_t* dy, int N, int HW, int C, uint16_t* dx, hipStream_t s) {
+  const int64_t total = (int64_t)N * HW * (C / 8);
+  hipLaunchKernelGGL(avgpool_bwd_kernel, dim3(ew_blocks(total)), dim3(256), 0, s, dy, N, HW, C, dx);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t dlmpi_nchw_to_nhwc(const float* x, int N, int C, int H, int W, int Cpad, uint16_t* y,
+                                         hipStream_t s) {
+  if (Cpad % 8 || Cpad < C) return hipErrorInvalidValue;
+  const int64_t total = (int64_t)N * H * W * (Cpad / 8);
+  hipLaunchKernelGGL(nchw_to_nhwc_kernel, dim3(ew_blocks(total)), dim3(256), 0, s, x, N, C, H, W, Cpad, y);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t dlmpi_upsample2x_fwd(const uint16_t* x, int N, int H, int W, int C, int ldx, int xoff,
+                                           uint16_t* y, int ldy, int yoff, hipStream_t s) {
+  const int64_t total = (int64_t)N * 4 * H * W * (C / 8);
+  hipLaunchKernelGGL(upsample2x_fwd_kernel, dim3(ew_blocks(total)), dim3(256), 0, s, x, N, H, W, C, ldx, xoff, y, ldy,
+                     yoff);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t dlmpi_upsample2x_bwd(const uint16_t* dy, int N, int H, int W, int C, int lddy, int dyoff,
+                                           float* ws, uint16_t* dx, hipStream_t s) {
+  const int64_t nin = (int64_t)N * H * W * C;
+  hipError_t e = hipMemsetAsync(ws, 0, nin * sizeof(float), s);
+  if (e != hipSuccess) return e;
+  const int64_t total = (int64_t)N * 4 * H * W * (C / 8);
+  hipLaunchKernelGGL(upsample2x_bwd_scatter_kernel, dim3(ew_blocks(total)), dim3(256), 0, s, dy, N, H, W, C, lddy,
+                     dyoff, ws);
+  hipLaunchKernelGGL(f32_to_bf16_kernel, dim3(ew_blocks(nin / 8)), dim3(256), 0, s, ws, nin / 8, dx);
+  return hipGetLastError();
+}

@@ -1,0 +1,3 @@
+from .datasets import (CIFAR10, CarvanaDataset, CifarTransform, SegmentationDataset,  # noqa: F401
+                       SyntheticImages, SyntheticMasks, device_batch)
+from .sampler import DistributedSampler  # noqa: F401

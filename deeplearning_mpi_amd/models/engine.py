@@ -1,0 +1,246 @@
+"""Execution engine: explicit forward / backward schedules over fused layer units.
+
+The models keep torch ``nn.Module`` parameter containers with the reference's exact names (so
+``state_dict`` is key-compatible with torchvision / the reference UNet), but they never run
+``nn.Conv2d.forward``.  Instead a model's ``forward`` runs a hand-written schedule of fused units
+(conv + BatchNorm statistics in the GEMM epilogue + BN-apply/ReLU/residual, pooling, ...) on a
+compute backend (gfx950 kernels on GPU, torch reference on CPU), and its backward is the
+matching hand-written reverse schedule:
+
+* parameter gradients are written (accumulated) straight into the arena's flat gradient buffer
+  and announced to the DDP reducer the moment they are final, so bucket all-reduces start while
+  the rest of the backward is still running;
+* the block-input gradient of a residual block is formed in the data-gradient GEMM epilogue
+  (dgrad(conv1) + identity-grad), never as a separate add;
+* nothing is traced or compiled: the schedule is plain code, so a whole training step can be
+  captured into a hipGraph and replayed.
+
+One ``torch.autograd.Function`` bridges the engine to autograd (loss.backward() works as usual).
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn as nn
+
+from ..ops.act import Act, pad8
+from ..ops.backend import make_backend
+from ..utils.arena import ParamArena
+
+
+class ConvUnit:
+    """conv2d / linear (+ training or folded-eval BatchNorm) (+ residual) (+ ReLU)."""
+
+    def __init__(self, arena: ParamArena, conv, bn=None, relu=True, cin_pad=None, need_dgrad=True):
+        self.arena, self.conv, self.bn, self.relu = arena, conv, bn, relu
+        w = conv.weight
+        self.linear = isinstance(conv, nn.Linear)
+        if self.linear:
+            self.K, self.Cin = w.shape
+            self.R = self.S = 1
+            self.stride, self.pad = 1, 0
+        else:
+            self.K, self.Cin, self.R, self.S = w.shape
+            assert conv.stride[0] == conv.stride[1] and conv.padding[0] == conv.padding[1]
+            assert conv.dilation == (1, 1) and conv.groups == 1
+            self.stride, self.pad = conv.stride[0], conv.padding[0]
+        self.Cp = cin_pad or pad8(self.Cin)
+        self.Kp = pad8(self.K)
+        R, S, K, C = self.R, self.S, self.K, self.Cin
+        if self.linear:   # weight [K, C]
+            self.h_fwd = arena.add_compute(w, (self.Kp, 1, 1, self.Cp), (K, 1, 1, C), (0, None, None, 1))
+            self.h_dg = arena.add_compute(w, (self.Cp, 1, 1, self.Kp), (C, 1, 1, K), (1, None, None, 0)) \
+                if need_dgrad else None
+        else:             # weight [K, C, R, S]
+            self.h_fwd = arena.add_compute(w, (self.Kp, R, S, self.Cp), (K, R, S, C), (0, 2, 3, 1))
+            self.h_dg = arena.add_compute(w, (self.Cp, R, S, self.Kp), (C, R, S, K), (1, 2, 3, 0)) \
+                if need_dgrad else None
+        self.bias = conv.bias
+        self._bias_pad = None
+
+    def out_hw(self, H, W):
+        return ((H + 2 * self.pad - self.R) // self.stride + 1, (W + 2 * self.pad - self.S) // self.stride + 1)
+
+    def _bias_vec(self):
+        if self.bias is None:
+            return None
+        if self.Kp == self.K:
+            return self.bias.data
+        if self._bias_pad is None or self._bias_pad.device != self.bias.device:
+            self._bias_pad = torch.zeros(self.Kp, dtype=torch.float32, device=self.bias.device)
+        self._bias_pad[:self.K].copy_(self.bias.data)
+        return self._bias_pad
+
+    def fwd(self, be, x: Act, train: bool, res: Act = None, out: Act = None, save=True):
+        assert x.C == self.Cp, (x, self.Cp)
+        P, Q = self.out_hw(x.H, x.W)
+        N, dev = x.N, x.device
+        wf = self.arena.get_compute(self.h_fwd)
+        y = out if out is not None else Act.empty(N, P, Q, self.Kp, be.act_dtype, dev)
+        bn = self.bn
+        if bn is None:
+            assert not self.relu or res is None or True
+            be.conv_fwd(x, wf, self.Kp, self.R, self.S, self.stride, self.pad, y, bias=self._bias_vec(), res=res,
+                        relu=self.relu, kvalid=y.C if y.C < self.Kp else 0)
+            return y, ((x, y) if save else None)
+        if train:
+            z = Act.empty(N, P, Q, self.Kp, be.act_dtype, dev)
+            mt = be.conv_mtiles(N, x.H, x.W, self.Kp, self.R, self.S, self.stride, self.pad)
+            stats = torch.empty(mt, 2, self.Kp, dtype=torch.float32, device=dev)
+            be.conv_fwd(x, wf, self.Kp, self.R, self.S, self.stride, self.pad, z, bias=self._bias_vec(), stats=stats)
+            vec = torch.empty(4, self.Kp, dtype=torch.float32, device=dev)
+            scale, shift, mean, invstd = vec[0], vec[1], vec[2], vec[3]
+            mom = bn.momentum
+            if mom is None:   # cumulative moving average
+                mom = 1.0 / float(bn.num_batches_tracked.item())
+            be.bn_finalize(stats, mt, self.Kp, N * P * Q, bn.weight.data if bn.affine else None,
+                           bn.bias.data if bn.affine else None,
+                           bn.running_mean if bn.track_running_stats else None,
+                           bn.running_var if bn.track_running_stats else None, mom, bn.eps, scale, shift, mean,
+                           invstd)
+            be.bn_apply(z, scale, shift, res, self.relu, y)
+            return y, ((x, z, y, mean, invstd) if save else None)
+        # eval: fold BN (and conv bias) into the GEMM epilogue
+        invstd = torch.rsqrt(bn.running_var + bn.eps)
+        scale = bn.weight.data * invstd if bn.affine else invstd
+        shift = (bn.bias.data if bn.affine else 0.0) - bn.running_mean * scale
+        if self.bias is not None:
+            shift = shift + self.bias.data * scale
+        be.conv_fwd(x, wf, self.Kp, self.R, self.S, self.stride, self.pad, y, res=res, scale=scale.contiguous(),
+                    shift=shift.contiguous(), relu=self.relu)
+        return y, None
+
+    def bwd(self, be, ctx, dy: Act, need_dx=True, dx_res: Act = None, dyr_out: Act = None, ymask: Act = None,
+            use_own_mask=True):
+        ar = self.arena
+        bn = self.bn
+        if bn is not None:
+            x, z, y, mean, invstd = ctx
+            mask = ymask if ymask is not None else (y if (self.relu and use_own_mask) else None)
+            dz = Act.empty(z.N, z.H, z.W, z.C, be.act_dtype, z.device)
+            be.bn_bwd(dy, mask, z, mean, invstd, bn.weight.data if bn.affine else None,
+                      ar.grad_flat(bn.weight) if bn.affine else None, ar.grad_flat(bn.bias) if bn.affine else None,
+                      dz, dyr_out)
+            if bn.affine:
+                ar.ready(bn.weight, bn.bias)
+            if self.bias is not None:
+                # d(bias) of a conv followed by training-mode BN is exactly zero (BN removes the mean)
+                ar.ready(self.bias)
+        else:
+            x, y = ctx
+            assert not self.relu, "ReLU without BN is not used by the engine models"
+            dz = dy
+            if self.bias is not None:
+                if self.Kp == self.K:
+                    be.channel_sum(dz, ar.grad_flat(self.bias))
+                else:
+                    tmp = torch.zeros(self.Kp, dtype=torch.float32, device=dz.device)
+                    be.channel_sum(dz, tmp)
+                    ar.grad_flat(self.bias).add_(tmp[:self.K])
+                ar.ready(self.bias)
+        be.conv_wgrad(dz, x, self.R, self.S, self.stride, self.pad, ar.grad_flat(self.conv.weight), self.Cin, self.K)
+        ar.ready(self.conv.weight)
+        if not need_dx:
+            return None
+        dx = Act.empty(x.N, x.H, x.W, self.Cp, be.act_dtype, x.device)
+        be.conv_dgrad(dz, ar.get_compute(self.h_dg), self.Cp, self.R, self.S, self.stride, self.pad, dx, res=dx_res)
+        return dx
+
+
+class ConvTUnit:
+    """ConvTranspose2d(k=2, s=2) with bias (UNet up-sampling, reference model.py:36-38)."""
+
+    def __init__(self, arena: ParamArena, convT: nn.ConvTranspose2d):
+        self.arena, self.m = arena, convT
+        Ci, Co, kh, kw = convT.weight.shape
+        assert (kh, kw) == (2, 2) and convT.stride == (2, 2) and convT.padding == (0, 0)
+        self.Cin, self.Cout = Ci, Co
+        self.Cip, self.Cop = pad8(Ci), pad8(Co)
+        w = convT.weight
+        # forward layout [Cout][i][j][Cin]; data-grad layout [Cin][i][j][Cout] (a stride-2 2x2 conv)
+        self.h_fwd = arena.add_compute(w, (self.Cop, 2, 2, self.Cip), (Co, 2, 2, Ci), (1, 2, 3, 0))
+        self.h_dg = arena.add_compute(w, (self.Cip, 2, 2, self.Cop), (Ci, 2, 2, Co), (0, 2, 3, 1))
+
+    def fwd(self, be, x: Act, out: Act):
+        be.convT_fwd(x, self.arena.get_compute(self.h_fwd), self.Cop, out,
+                     self.m.bias.data if self.m.bias is not None else None)
+        return x
+
+    def bwd(self, be, x: Act, dout: Act):
+        ar = self.arena
+        if self.m.bias is not None:
+            be.channel_sum(dout, ar.grad_flat(self.m.bias))
+            ar.ready(self.m.bias)
+        # dW[ci][i][j][co] = sum_pix x[pix][ci] * dout[2p+i, 2q+j][co]: the wgrad of a stride-2 2x2 conv
+        be.conv_wgrad(x, dout, 2, 2, 2, 0, ar.grad_flat(self.m.weight), self.Cout, self.Cin)
+        ar.ready(self.m.weight)
+        dx = Act.empty(x.N, x.H, x.W, self.Cip, be.act_dtype, x.device)
+        be.conv_fwd(dout, ar.get_compute(self.h_dg), self.Cip, 2, 2, 2, 0, dx)
+        return dx
+
+
+class _EngineFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, mod, x, anchor):
+        out, state = mod._engine_forward(x, train=True, save=True)
+        ctx.mod = mod
+        ctx.state = state
+        return out
+
+    @staticmethod
+    def backward(ctx, gout):
+        mod = ctx.mod
+        state = ctx.state
+        ctx.state = None
+        mod._engine_backward(state, gout)
+        mod._arena.end_backward()
+        return None, None, None
+
+
+class EngineModule(nn.Module):
+    """Base class: lazily builds the backend + arena on the device of the parameters."""
+
+    def __init__(self):
+        super().__init__()
+        self._arena = None
+        self._be = None
+        self._anchor = torch.zeros(0, requires_grad=True)
+
+    def engine_setup(self, device=None):
+        if device is None:
+            device = next(self.parameters()).device
+        device = torch.device(device)
+        if self._arena is not None and self._arena.device == device and self._arena.valid():
+            return self._arena
+        self._be = make_backend(device)
+        self._arena = ParamArena(self, device, self._be)
+        self._build_units(self._arena)
+        self._arena.refresh(force=True)
+        return self._arena
+
+    @property
+    def arena(self) -> ParamArena:
+        return self.engine_setup()
+
+    def _build_units(self, arena):
+        raise NotImplementedError
+
+    def forward(self, x):
+        self.engine_setup(x.device)
+        self._arena.refresh()
+        if self.training and torch.is_grad_enabled():
+            self._arena.attach_grads()
+            if self._arena.ibuf_total:
+                self._arena.ibuf.add_(1)   # every BatchNorm's num_batches_tracked, one launch
+            return _EngineFn.apply(self, x, self._anchor)
+        with torch.no_grad():
+            if self.training and self._arena.ibuf_total:
+                self._arena.ibuf.add_(1)
+            out, _ = self._engine_forward(x, train=self.training, save=False)
+        return out
+
+    # implemented by the model
+    def _engine_forward(self, x, train, save):
+        raise NotImplementedError
+
+    def _engine_backward(self, state, gout):
+        raise NotImplementedError

@@ -1,0 +1,236 @@
+"""ResNet-18/34/50/101/152 on the MI355X engine.
+
+Module names, shapes, dtypes and initialisation follow torchvision's ``resnet*`` exactly, so a
+``state_dict`` is key-for-key compatible with the reference checkpoints
+(/root/reference/pytorch/resnet/main.py:40-41 builds ``torchvision.models.resnet18`` with a
+replaced 10-class ``fc``; BASELINE.json targets ResNet-50/152 at 224x224).
+
+Forward/backward run as an explicit engine schedule (models/engine.py): stem conv7x7+BN+ReLU,
+maxpool, bottleneck/basic blocks with the residual add and ReLU fused into the last BN-apply,
+global average pool and the fc GEMM (fp32 logits).  ``forward_torch`` is the plain eager-PyTorch
+path of the same parameters (stock PyTorch baseline and test oracle).
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from ..ops.act import Act, pad8
+from .engine import ConvUnit, EngineModule
+
+
+def conv3x3(i, o, stride=1):
+    return nn.Conv2d(i, o, 3, stride, 1, bias=False)
+
+
+def conv1x1(i, o, stride=1):
+    return nn.Conv2d(i, o, 1, stride, 0, bias=False)
+
+
+class BasicBlock(nn.Module):
+    expansion = 1
+
+    def __init__(self, inplanes, planes, stride=1, downsample=None):
+        super().__init__()
+        self.conv1 = conv3x3(inplanes, planes, stride)
+        self.bn1 = nn.BatchNorm2d(planes)
+        self.relu = nn.ReLU(inplace=True)
+        self.conv2 = conv3x3(planes, planes)
+        self.bn2 = nn.BatchNorm2d(planes)
+        self.downsample = downsample
+        self.stride = stride
+
+    def forward_torch(self, x):
+        idn = x if self.downsample is None else self.downsample(x)
+        out = self.relu(self.bn1(self.conv1(x)))
+        out = self.bn2(self.conv2(out))
+        return self.relu(out + idn)
+
+    def units(self, ar):
+        u = [ConvUnit(ar, self.conv1, self.bn1, relu=True), ConvUnit(ar, self.conv2, self.bn2, relu=True)]
+        ud = ConvUnit(ar, self.downsample[0], self.downsample[1], relu=False) if self.downsample is not None else None
+        return u, ud
+
+
+class Bottleneck(nn.Module):
+    expansion = 4
+
+    def __init__(self, inplanes, planes, stride=1, downsample=None):
+        super().__init__()
+        width = planes
+        self.conv1 = conv1x1(inplanes, width)
+        self.bn1 = nn.BatchNorm2d(width)
+        self.conv2 = conv3x3(width, width, stride)
+        self.bn2 = nn.BatchNorm2d(width)
+        self.conv3 = conv1x1(width, planes * self.expansion)
+        self.bn3 = nn.BatchNorm2d(planes * self.expansion)
+        self.relu = nn.ReLU(inplace=True)
+        self.downsample = downsample
+        self.stride = stride
+
+    def forward_torch(self, x):
+        idn = x if self.downsample is None else self.downsample(x)
+        out = self.relu(self.bn1(self.conv1(x)))
+        out = self.relu(self.bn2(self.conv2(out)))
+        out = self.bn3(self.conv3(out))
+        return self.relu(out + idn)
+
+    def units(self, ar):
+        u = [ConvUnit(ar, self.conv1, self.bn1, relu=True), ConvUnit(ar, self.conv2, self.bn2, relu=True),
+             ConvUnit(ar, self.conv3, self.bn3, relu=True)]
+        ud = ConvUnit(ar, self.downsample[0], self.downsample[1], relu=False) if self.downsample is not None else None
+        return u, ud
+
+
+class _BlockExec:
+    """Forward/backward schedule of one residual block (basic or bottleneck)."""
+
+    def __init__(self, units, ds):
+        self.u, self.ud = units, ds
+
+    def fwd(self, be, x: Act, train, save):
+        ctxs = []
+        h = x
+        for k, u in enumerate(self.u[:-1]):
+            h, c = u.fwd(be, h, train, save=save)
+            ctxs.append(c)
+        if self.ud is not None:
+            idn, cd = self.ud.fwd(be, x, train, save=save)
+        else:
+            idn, cd = x, None
+        y, c = self.u[-1].fwd(be, h, train, res=idn, save=save)
+        ctxs.append(c)
+        return y, (ctxs, cd)
+
+    def bwd(self, be, st, dy: Act):
+        ctxs, cd = st
+        ylast = ctxs[-1][2]
+        if self.ud is None:
+            dyr = Act.empty(dy.N, dy.H, dy.W, dy.C, be.act_dtype, dy.device)   # identity-path grad
+            dh = self.u[-1].bwd(be, ctxs[-1], dy, dyr_out=dyr)
+        else:
+            dyr = None
+            dh = self.u[-1].bwd(be, ctxs[-1], dy)
+        for k in range(len(self.u) - 2, 0, -1):
+            dh = self.u[k].bwd(be, ctxs[k], dh)
+        if self.ud is not None:
+            # downsample BN sees the same relu-masked output grad as the main branch
+            dres = self.ud.bwd(be, cd, dy, ymask=ylast)
+        else:
+            dres = dyr
+        return self.u[0].bwd(be, ctxs[0], dh, dx_res=dres)
+
+
+class ResNet(EngineModule):
+    def __init__(self, block, layers, num_classes=1000, in_channels=3):
+        super().__init__()
+        self.inplanes = 64
+        self.in_channels = in_channels
+        self.conv1 = nn.Conv2d(in_channels, 64, kernel_size=7, stride=2, padding=3, bias=False)
+        self.bn1 = nn.BatchNorm2d(64)
+        self.relu = nn.ReLU(inplace=True)
+        self.maxpool = nn.MaxPool2d(kernel_size=3, stride=2, padding=1)
+        self.layer1 = self._make_layer(block, 64, layers[0])
+        self.layer2 = self._make_layer(block, 128, layers[1], stride=2)
+        self.layer3 = self._make_layer(block, 256, layers[2], stride=2)
+        self.layer4 = self._make_layer(block, 512, layers[3], stride=2)
+        self.avgpool = nn.AdaptiveAvgPool2d((1, 1))
+        self.fc = nn.Linear(512 * block.expansion, num_classes)
+        for m in self.modules():
+            if isinstance(m, nn.Conv2d):
+                nn.init.kaiming_normal_(m.weight, mode="fan_out", nonlinearity="relu")
+            elif isinstance(m, nn.BatchNorm2d):
+                nn.init.constant_(m.weight, 1)
+                nn.init.constant_(m.bias, 0)
+
+    def _make_layer(self, block, planes, blocks, stride=1):
+        downsample = None
+        if stride != 1 or self.inplanes != planes * block.expansion:
+            downsample = nn.Sequential(conv1x1(self.inplanes, planes * block.expansion, stride),
+                                       nn.BatchNorm2d(planes * block.expansion))
+        layers = [block(self.inplanes, planes, stride, downsample)]
+        self.inplanes = planes * block.expansion
+        for _ in range(1, blocks):
+            layers.append(block(self.inplanes, planes))
+        return nn.Sequential(*layers)
+
+    # ------------------------------------------------------------------ eager torch path
+    def forward_torch(self, x):
+        x = self.maxpool(self.relu(self.bn1(self.conv1(x))))
+        for layer in (self.layer1, self.layer2, self.layer3, self.layer4):
+            for b in layer:
+                x = b.forward_torch(x)
+        x = torch.flatten(self.avgpool(x), 1)
+        return self.fc(x)
+
+    # ------------------------------------------------------------------ engine
+    def _build_units(self, ar):
+        self.cin_pad = pad8(self.in_channels)
+        self.u_stem = ConvUnit(ar, self.conv1, self.bn1, relu=True, cin_pad=self.cin_pad, need_dgrad=False)
+        self.blocks = []
+        for layer in (self.layer1, self.layer2, self.layer3, self.layer4):
+            for b in layer:
+                self.blocks.append(_BlockExec(*b.units(ar)))
+        self.u_fc = ConvUnit(ar, self.fc, None, relu=False)
+
+    def _engine_forward(self, x, train, save):
+        be = self._be
+        N = x.shape[0]
+        a0 = be.nchw_to_nhwc(x, self.cin_pad)
+        h, cs = self.u_stem.fwd(be, a0, train, save=save)
+        OH, OW = (h.H + 2 - 3) // 2 + 1, (h.W + 2 - 3) // 2 + 1
+        p = Act.empty(N, OH, OW, h.C, be.act_dtype, x.device)
+        idx = be.maxpool_fwd(h, 3, 2, 1, p)
+        st_blocks = []
+        a = p
+        for blk in self.blocks:
+            a, st = blk.fwd(be, a, train, save)
+            st_blocks.append(st)
+        pooled = Act.empty(N, 1, 1, a.C, be.act_dtype, x.device)
+        be.avgpool_fwd(a, pooled)
+        K = self.fc.out_features
+        logits = torch.empty(N, K, dtype=torch.float32, device=x.device)
+        la = Act(logits, N, 1, 1, K)
+        _, cf = self.u_fc.fwd(be, pooled, train, out=la, save=save)
+        state = (cs, h, p, idx, st_blocks, a, pooled, cf) if save else None
+        return logits, state
+
+    def _engine_backward(self, state, gout):
+        be = self._be
+        cs, h, p, idx, st_blocks, a, pooled, cf = state
+        N, K = gout.shape
+        dl = be.nchw_to_nhwc(gout.reshape(N, K, 1, 1), self.u_fc.Kp)
+        x_fc, _ = cf
+        dpool = self.u_fc.bwd(be, (x_fc, None), dl)
+        da = Act.empty(a.N, a.H, a.W, a.C, be.act_dtype, a.device)
+        be.avgpool_bwd(dpool, da)
+        for blk, st in zip(reversed(self.blocks), reversed(st_blocks)):
+            da = blk.bwd(be, st, da)
+        dh = Act.empty(h.N, h.H, h.W, h.C, be.act_dtype, h.device)
+        be.maxpool_bwd(da, idx, h, 3, 2, 1, dh)
+        self.u_stem.bwd(be, cs, dh, need_dx=False)
+
+
+def resnet18(num_classes=1000, **kw):
+    return ResNet(BasicBlock, [2, 2, 2, 2], num_classes, **kw)
+
+
+def resnet34(num_classes=1000, **kw):
+    return ResNet(BasicBlock, [3, 4, 6, 3], num_classes, **kw)
+
+
+def resnet50(num_classes=1000, **kw):
+    return ResNet(Bottleneck, [3, 4, 6, 3], num_classes, **kw)
+
+
+def resnet101(num_classes=1000, **kw):
+    return ResNet(Bottleneck, [3, 4, 23, 3], num_classes, **kw)
+
+
+def resnet152(num_classes=1000, **kw):
+    return ResNet(Bottleneck, [3, 8, 36, 3], num_classes, **kw)
+
+
+ARCHS = {"resnet18": resnet18, "resnet34": resnet34, "resnet50": resnet50, "resnet101": resnet101,
+         "resnet152": resnet152}

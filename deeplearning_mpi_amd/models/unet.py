@@ -1,0 +1,193 @@
+"""UNet (4-level encoder/decoder) on the MI355X engine.
+
+Same module tree, parameter names and defaults as /root/reference/pytorch/unet/model.py:5-81
+(``DoubleConv`` = (Conv3x3 with bias -> BN -> ReLU) x 2, ``DownBlock``, ``UpBlock`` with
+ConvTranspose2d(k2,s2) or bilinear Upsample, ``conv_last`` 1x1), so checkpoints load both ways.
+Extension (BASELINE.json config 5): ``in_channels`` (the reference hard-codes 3).
+
+Engine schedule (MI355X-first):
+* the skip concatenation is free: each encoder level's second BN-apply writes the skip tensor
+  straight into channel slice [C_up, C_up+C_skip) of the decoder's preallocated concat buffer,
+  and the decoder's ConvTranspose2d writes the up-sampled tensor into slice [0, C_up)
+  (torch.cat at model.py:47 disappears);
+* ConvTranspose2d(k2, s2) is 4 sub-pixel GEMM phases with a strided-store epilogue;
+* backward: the concat-buffer gradient is produced by ONE data-gradient GEMM, the skip slice of it
+  is added inside the 2x2 max-pool backward kernel (no separate add).
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn as nn
+
+from ..ops.act import Act, pad8
+from .engine import ConvTUnit, ConvUnit, EngineModule
+
+
+class DoubleConv(nn.Module):
+    def __init__(self, in_channels, out_channels):
+        super().__init__()
+        self.double_conv = nn.Sequential(
+            nn.Conv2d(in_channels, out_channels, kernel_size=3, padding=1),
+            nn.BatchNorm2d(out_channels),
+            nn.ReLU(inplace=True),
+            nn.Conv2d(out_channels, out_channels, kernel_size=3, padding=1),
+            nn.BatchNorm2d(out_channels),
+            nn.ReLU(inplace=True),
+        )
+
+    def forward(self, x):
+        return self.double_conv(x)
+
+    def units(self, ar, cin_pad=None, need_dgrad=True):
+        s = self.double_conv
+        return (ConvUnit(ar, s[0], s[1], relu=True, cin_pad=cin_pad, need_dgrad=need_dgrad),
+                ConvUnit(ar, s[3], s[4], relu=True))
+
+
+class DownBlock(nn.Module):
+    def __init__(self, in_channels, out_channels):
+        super().__init__()
+        self.double_conv = DoubleConv(in_channels, out_channels)
+        self.down_sample = nn.MaxPool2d(2)
+
+    def forward(self, x):
+        skip_out = self.double_conv(x)
+        return self.down_sample(skip_out), skip_out
+
+
+class UpBlock(nn.Module):
+    def __init__(self, in_channels, out_channels, up_sample_mode):
+        super().__init__()
+        if up_sample_mode == "conv_transpose":
+            self.up_sample = nn.ConvTranspose2d(in_channels - out_channels, in_channels - out_channels, kernel_size=2,
+                                                stride=2)
+        elif up_sample_mode == "bilinear":
+            self.up_sample = nn.Upsample(scale_factor=2, mode="bilinear", align_corners=True)
+        else:
+            raise ValueError("Unsupported `up_sample_mode` (can take one of `conv_transpose` or `bilinear`)")
+        self.double_conv = DoubleConv(in_channels, out_channels)
+
+    def forward(self, down_input, skip_input):
+        x = self.up_sample(down_input)
+        x = torch.cat([x, skip_input], dim=1)
+        return self.double_conv(x)
+
+
+class UNet(EngineModule):
+    def __init__(self, out_classes=2, up_sample_mode="conv_transpose", in_channels=3):
+        super().__init__()
+        self.up_sample_mode = up_sample_mode
+        self.in_channels = in_channels
+        self.out_classes = out_classes
+        self.down_conv1 = DownBlock(in_channels, 64)
+        self.down_conv2 = DownBlock(64, 128)
+        self.down_conv3 = DownBlock(128, 256)
+        self.down_conv4 = DownBlock(256, 512)
+        self.double_conv = DoubleConv(512, 1024)
+        self.up_conv4 = UpBlock(512 + 1024, 512, self.up_sample_mode)
+        self.up_conv3 = UpBlock(256 + 512, 256, self.up_sample_mode)
+        self.up_conv2 = UpBlock(128 + 256, 128, self.up_sample_mode)
+        self.up_conv1 = UpBlock(128 + 64, 64, self.up_sample_mode)
+        self.conv_last = nn.Conv2d(64, out_classes, kernel_size=1)
+
+    # ------------------------------------------------------------------ eager torch path
+    def forward_torch(self, x):
+        x, s1 = self.down_conv1(x)
+        x, s2 = self.down_conv2(x)
+        x, s3 = self.down_conv3(x)
+        x, s4 = self.down_conv4(x)
+        x = self.double_conv(x)
+        x = self.up_conv4(x, s4)
+        x = self.up_conv3(x, s3)
+        x = self.up_conv2(x, s2)
+        x = self.up_conv1(x, s1)
+        return self.conv_last(x)
+
+    # ------------------------------------------------------------------ engine
+    def _build_units(self, ar):
+        self.cin_pad = pad8(self.in_channels)
+        downs = [self.down_conv1, self.down_conv2, self.down_conv3, self.down_conv4]
+        ups = [self.up_conv1, self.up_conv2, self.up_conv3, self.up_conv4]   # level 1..4
+        self.enc = [d.double_conv.units(ar, cin_pad=self.cin_pad if k == 0 else None, need_dgrad=k != 0)
+                    for k, d in enumerate(downs)]
+        self.bott = self.double_conv.units(ar)
+        self.skip_ch = [64, 128, 256, 512]
+        self.up_ch = [128, 256, 512, 1024]   # channels arriving from below at levels 1..4
+        self.dec = [u.double_conv.units(ar, cin_pad=self.up_ch[k] + self.skip_ch[k]) for k, u in enumerate(ups)]
+        self.upT = [ConvTUnit(ar, u.up_sample) if self.up_sample_mode == "conv_transpose" else None for u in ups]
+        self.u_last = ConvUnit(ar, self.conv_last, None, relu=False)
+
+    def _engine_forward(self, x, train, save):
+        be = self._be
+        N, _, H, W = x.shape
+        assert H % 16 == 0 and W % 16 == 0, "UNet input must be a multiple of 16 (reference model.py:71-79)"
+        dt, dev = be.act_dtype, x.device
+        a = be.nchw_to_nhwc(x, self.cin_pad)
+        cats, ctx_enc, idxs, skips = [], [], [], []
+        h, w = H, W
+        for k in range(4):
+            ccat = self.up_ch[k] + self.skip_ch[k]
+            cat = Act.empty(N, h, w, ccat, dt, dev)
+            cats.append(cat)
+            ua, ub = self.enc[k]
+            t, ca = ua.fwd(be, a, train, save=save)
+            skip = cat.slice(self.up_ch[k], self.skip_ch[k])
+            _, cb = ub.fwd(be, t, train, out=skip, save=save)
+            down = Act.empty(N, h // 2, w // 2, self.skip_ch[k], dt, dev)
+            idx = be.maxpool_fwd(skip, 2, 2, 0, down)
+            ctx_enc.append((ca, cb))
+            idxs.append(idx)
+            skips.append(skip)
+            a = down
+            h, w = h // 2, w // 2
+        ua, ub = self.bott
+        t, cba = ua.fwd(be, a, train, save=save)
+        a, cbb = ub.fwd(be, t, train, save=save)
+        ctx_dec = [None] * 4
+        for k in range(3, -1, -1):
+            cat = cats[k]
+            up = cat.slice(0, self.up_ch[k])
+            if self.upT[k] is not None:
+                self.upT[k].fwd(be, a, up)
+            else:
+                be.upsample_fwd(a, up)
+            below = a
+            ua, ub = self.dec[k]
+            t, ca = ua.fwd(be, cat, train, save=save)
+            a, cb = ub.fwd(be, t, train, save=save)
+            ctx_dec[k] = (below, ca, cb)
+        K = self.out_classes
+        out = torch.empty(N, H, W, K, dtype=torch.float32, device=dev)
+        _, cl = self.u_last.fwd(be, a, train, out=Act(out.view(N * H * W, K), N, H, W, K), save=save)
+        logits = out.permute(0, 3, 1, 2)
+        state = (cats, ctx_enc, idxs, skips, (cba, cbb), ctx_dec, cl) if save else None
+        return logits, state
+
+    def _engine_backward(self, state, gout):
+        be = self._be
+        cats, ctx_enc, idxs, skips, (cba, cbb), ctx_dec, cl = state
+        dl = be.nchw_to_nhwc(gout, self.u_last.Kp)
+        da = self.u_last.bwd(be, (cl[0], None), dl)
+        for k in range(4):                    # decoder, level 1 (last executed) first
+            below, ca, cb = ctx_dec[k]
+            ua, ub = self.dec[k]
+            dt_ = ub.bwd(be, cb, da)
+            dcat = ua.bwd(be, ca, dt_)
+            dup = dcat.slice(0, self.up_ch[k])
+            if self.upT[k] is not None:
+                da = self.upT[k].bwd(be, below, dup)
+            else:
+                da = Act.empty(below.N, below.H, below.W, below.C, be.act_dtype, below.device)
+                be.upsample_bwd(dup, da)
+            ctx_dec[k] = dcat                 # keep the skip-slice gradient for the encoder
+        ua, ub = self.bott
+        da = ua.bwd(be, cba, ub.bwd(be, cbb, da))
+        for k in range(3, -1, -1):
+            skip = skips[k]
+            dskip = Act.empty(skip.N, skip.H, skip.W, skip.C, be.act_dtype, skip.device)
+            be.maxpool_bwd(da, idxs[k], skip, 2, 2, 0, dskip,
+                           add=ctx_dec[k].slice(self.up_ch[k], self.skip_ch[k]))
+            ca, cb = ctx_enc[k]
+            ua, ub = self.enc[k]
+            dt_ = ub.bwd(be, cb, dskip)
+            da = ua.bwd(be, ca, dt_, need_dx=k != 0)

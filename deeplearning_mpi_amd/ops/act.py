@@ -1,0 +1,61 @@
+"""NHWC activation descriptor used by the execution engine.
+
+An :class:`Act` is a (possibly channel-sliced) NHWC tensor stored as a 2-D buffer
+``[N*H*W, ld]``.  Channel slices (``off``, ``C`` < ``ld``) are how the UNet skip concatenation
+is made free: the encoder writes its skip output straight into the decoder's concat buffer
+(replaces ``torch.cat`` at /root/reference/pytorch/unet/model.py:47).
+"""
+from __future__ import annotations
+
+import torch
+
+
+class Act:
+    __slots__ = ("buf", "N", "H", "W", "C", "off")
+
+    def __init__(self, buf: torch.Tensor, N: int, H: int, W: int, C: int, off: int = 0):
+        assert buf.dim() == 2 and buf.shape[0] == N * H * W, (tuple(buf.shape), N, H, W)
+        assert off + C <= buf.shape[1]
+        self.buf, self.N, self.H, self.W, self.C, self.off = buf, N, H, W, C, off
+
+    @property
+    def ld(self) -> int:
+        return self.buf.shape[1]
+
+    @property
+    def rows(self) -> int:
+        return self.N * self.H * self.W
+
+    @property
+    def dtype(self):
+        return self.buf.dtype
+
+    @property
+    def device(self):
+        return self.buf.device
+
+    def nhwc(self) -> torch.Tensor:
+        return self.buf.view(self.N, self.H, self.W, self.ld)[..., self.off:self.off + self.C]
+
+    def nchw(self) -> torch.Tensor:
+        return self.nhwc().permute(0, 3, 1, 2)
+
+    def slice(self, off: int, C: int) -> "Act":
+        return Act(self.buf, self.N, self.H, self.W, C, self.off + off)
+
+    @staticmethod
+    def empty(N, H, W, C, dtype, device, ld=None) -> "Act":
+        ld = C if ld is None else ld
+        return Act(torch.empty(N * H * W, ld, dtype=dtype, device=device), N, H, W, C)
+
+    @staticmethod
+    def zeros(N, H, W, C, dtype, device, ld=None) -> "Act":
+        ld = C if ld is None else ld
+        return Act(torch.zeros(N * H * W, ld, dtype=dtype, device=device), N, H, W, C)
+
+    def __repr__(self):
+        return f"Act(N={self.N},H={self.H},W={self.W},C={self.C},ld={self.ld},off={self.off},{self.dtype})"
+
+
+def pad8(c: int) -> int:
+    return (c + 7) // 8 * 8

@@ -1,0 +1,404 @@
+"""Compute backends of the execution engine.
+
+* :class:`NativeBackend` -- the product path: bf16 NHWC activations, every op is one of our
+  gfx950 HIP kernels (``_C``), launched on the current HIP stream (graph-capturable).
+* :class:`RefBackend` -- fp32 torch reference of exactly the same op set and semantics.  It runs
+  on CPU (CPU test-suite, gloo multi-process tests) and is the numerics oracle for the kernels.
+
+Both expose the same methods; the engine (models/*) is written once against this interface.
+"""
+from __future__ import annotations
+
+import struct
+
+import torch
+import torch.nn.functional as F
+
+from .act import Act
+
+
+# --------------------------------------------------------------------------------------------
+class NativeBackend:
+    name = "native"
+    act_dtype = torch.bfloat16
+
+    def __init__(self, device):
+        from .._ext import native
+
+        self.C = native()
+        self.device = torch.device(device)
+        self._cast_cache = {}
+
+    # ---------------- conv family ----------------
+    def conv_mtiles(self, N, H, W, K, R, S, stride, pad):
+        return self.C.conv2d_fwd_mtiles(N, H, W, K, R, S, stride, pad, 0)
+
+    def conv_fwd(self, x: Act, w, K, R, S, stride, pad, y: Act, bias=None, res: Act = None, scale=None,
+                 shift=None, relu=False, stats=None, kvalid=0):
+        self.C.conv2d_fwd(x.buf, x.N, x.H, x.W, x.C, x.ld, x.off, w, K, R, S, stride, pad, y.buf, y.ld, y.off,
+                          bias, res.buf if res is not None else None, res.ld if res is not None else 0,
+                          res.off if res is not None else 0, scale, shift, bool(relu), stats, 0, int(kvalid))
+
+    def conv_dgrad(self, dy: Act, wT, C, R, S, stride, pad, dx: Act, res: Act = None):
+        self.C.conv2d_dgrad(dy.buf, dy.N, dy.H, dy.W, dy.C, dy.ld, dy.off, wT, C, R, S, stride, pad, dx.H, dx.W,
+                            dx.buf, dx.ld, dx.off, res.buf if res is not None else None,
+                            res.ld if res is not None else 0, res.off if res is not None else 0)
+
+    def convT_fwd(self, x: Act, wf, Cout, y: Act, bias=None):
+        self.C.convT2x2_fwd(x.buf, x.N, x.H, x.W, x.C, x.ld, x.off, wf, Cout, y.buf, y.ld, y.off, bias)
+
+    def conv_wgrad(self, dy: Act, x: Act, R, S, stride, pad, grad, Creal, Ko_real):
+        self.C.conv2d_wgrad(dy.buf, dy.ld, dy.off, dy.C, x.buf, x.N, x.H, x.W, x.C, x.ld, x.off, R, S, stride, pad,
+                            dy.H, dy.W, grad, Creal, Ko_real)
+
+    # ---------------- batch norm ----------------
+    def bn_finalize(self, stats, ntiles, C, count, gamma, beta, rm, rv, momentum, eps, scale, shift, save_mean,
+                    save_invstd):
+        self.C.bn_finalize(stats, ntiles, C, float(count), gamma, beta, rm, rv, float(momentum), float(eps), scale,
+                           shift, save_mean, save_invstd)
+
+    def bn_stats(self, x: Act):
+        nblk = self.C.reduce_blocks(x.rows, x.C)
+        part = torch.empty(nblk, 2, x.C, dtype=torch.float32, device=x.device)
+        self.C.bn_stats(x.buf, x.rows, x.C, x.ld, x.off, part, nblk)
+        return part, nblk
+
+    def bn_apply(self, x: Act, scale, shift, res: Act, relu, y: Act):
+        self.C.bn_apply(x.buf, x.ld, x.off, x.rows, x.C, scale, shift, res.buf if res is not None else None,
+                        res.ld if res is not None else 0, res.off if res is not None else 0, bool(relu), y.buf, y.ld,
+                        y.off)
+
+    def bn_bwd(self, dy: Act, ymask: Act, x: Act, mean, invstd, gamma, dgamma, dbeta, dx: Act, dyr_out: Act = None):
+        M, Cc = x.rows, x.C
+        nblk = self.C.reduce_blocks(M, Cc)
+        part = torch.empty(nblk, 2, Cc, dtype=torch.float32, device=x.device)
+        self.C.bn_bwd_reduce(dy.buf, dy.ld, dy.off, ymask.buf if ymask is not None else None,
+                             ymask.ld if ymask is not None else 0, ymask.off if ymask is not None else 0, x.buf, x.ld,
+                             x.off, M, Cc, mean, invstd, part, nblk)
+        coef = torch.empty(3, Cc, dtype=torch.float32, device=x.device)
+        self.C.bn_bwd_finalize(part, nblk, Cc, float(M), gamma, mean, invstd, dgamma, dbeta, coef)
+        assert dx.ld == Cc and dx.off == 0
+        if dyr_out is not None:
+            assert dyr_out.ld == Cc and dyr_out.off == 0
+        self.C.bn_bwd_apply(dy.buf, dy.ld, dy.off, ymask.buf if ymask is not None else None,
+                            ymask.ld if ymask is not None else 0, ymask.off if ymask is not None else 0, x.buf, x.ld,
+                            x.off, M, Cc, coef, dx.buf, dyr_out.buf if dyr_out is not None else None)
+
+    def channel_sum(self, x: Act, out_acc):
+        self.C.channel_sum(x.buf, x.rows, x.C, x.ld, x.off, out_acc)
+
+    # ---------------- pooling / layout ----------------
+    def maxpool_fwd(self, x: Act, k, s, p, y: Act):
+        idx = torch.empty(y.rows * y.C, dtype=torch.uint8, device=x.device)
+        assert y.ld == y.C and y.off == 0
+        self.C.maxpool_fwd(x.buf, x.N, x.H, x.W, x.C, x.ld, x.off, k, s, p, y.buf, idx, y.H, y.W)
+        return idx
+
+    def maxpool_bwd(self, dy: Act, idx, x: Act, k, s, p, dx: Act, add: Act = None):
+        self.C.maxpool_bwd(dy.buf, idx, x.N, x.H, x.W, x.C, k, s, p, dy.H, dy.W, add.buf if add is not None else None,
+                           add.ld if add is not None else 0, add.off if add is not None else 0, dx.buf, dx.ld, dx.off)
+
+    def avgpool_fwd(self, x: Act, y: Act):
+        self.C.avgpool_fwd(x.buf, x.N, x.H * x.W, x.C, y.buf)
+
+    def avgpool_bwd(self, dy: Act, dx: Act):
+        self.C.avgpool_bwd(dy.buf, dx.N, dx.H * dx.W, dx.C, dx.buf)
+
+    def nchw_to_nhwc(self, x: torch.Tensor, Cpad) -> Act:
+        N, Cc, H, W = x.shape
+        x = x.contiguous().float()
+        y = Act.empty(N, H, W, Cpad, torch.bfloat16, x.device)
+        self.C.nchw_to_nhwc(x, N, Cc, H, W, Cpad, y.buf)
+        return y
+
+    def upsample_fwd(self, x: Act, y: Act):
+        self.C.upsample2x_fwd(x.buf, x.N, x.H, x.W, x.C, x.ld, x.off, y.buf, y.ld, y.off)
+
+    def upsample_bwd(self, dy: Act, dx: Act):
+        assert dx.ld == dx.C and dx.off == 0
+        self.C.upsample2x_bwd(dy.buf, dx.N, dx.H, dx.W, dx.C, dy.ld, dy.off, dx.buf)
+
+    # ---------------- weights ----------------
+    def cast_weights(self, entries, total, dst_flat):
+        """entries: list of (src fp32 tensor view, dst offset, dims[4], valid[4], src strides[4])."""
+        key = id(entries)
+        ent = self._cast_cache.get(key)
+        if ent is None or ent[0] is not entries:
+            blob = bytearray()
+            base = dst_flat.data_ptr()
+            start = 0
+            for (src, doff, d, v, st) in entries:
+                blob += struct.pack("<QQ4i4i4qq", src.data_ptr(), base + 2 * doff, *d, *v, *st, doff)
+                start += d[0] * d[1] * d[2] * d[3]
+            dev = torch.frombuffer(bytes(blob), dtype=torch.uint8).to(self.device)
+            self._cast_cache[key] = ent = (entries, dev)
+        self.C.cast_weights(ent[1], len(entries), int(total))
+
+    # ---------------- losses / eval ----------------
+    def ce_fwd(self, logits, labels):
+        N, K = logits.shape
+        loss_rows = torch.empty(N, dtype=torch.float32, device=logits.device)
+        lse = torch.empty(N, dtype=torch.float32, device=logits.device)
+        loss = torch.empty((), dtype=torch.float32, device=logits.device)
+        self.C.softmax_ce_fwd(logits, logits.stride(0), labels, N, K, loss_rows, lse, loss)
+        return loss, lse
+
+    def ce_bwd(self, logits, labels, lse, go):
+        N, K = logits.shape
+        d = torch.empty(N, K, dtype=torch.float32, device=logits.device)
+        self.C.softmax_ce_bwd(logits, logits.stride(0), labels, lse, N, K, K, go, 1.0 / N, d)
+        return d
+
+    def bce_fwd(self, logits, target):
+        loss = torch.empty((), dtype=torch.float32, device=logits.device)
+        self.C.bce_fwd(logits, 1, target, logits.numel(), loss)
+        return loss
+
+    def bce_bwd(self, logits, target, go):
+        d = torch.empty_like(logits, memory_format=torch.contiguous_format)
+        self.C.bce_bwd(logits, 1, target, logits.numel(), go, 1.0 / logits.numel(), d)
+        return d
+
+    def argmax_correct(self, logits, labels):
+        c = torch.zeros(1, dtype=torch.int32, device=logits.device)
+        self.C.argmax_correct(logits, logits.stride(0), labels, logits.shape[0], logits.shape[1], c)
+        return c
+
+    def dice(self, logits, target):
+        N = target.shape[0]
+        out = torch.empty(N, dtype=torch.float32, device=logits.device)
+        self.C.dice(logits, 1, target, N, target[0].numel(), out)
+        return out
+
+    # ---------------- optimizers ----------------
+    def sgd(self, p, g, m, lr, momentum, dampening, wd, nesterov, first, skip_flag=None):
+        self.C.sgd_step(p, g, m, lr, momentum, dampening, wd, nesterov, first, skip_flag)
+
+    def adam(self, p, g, m, v, lr, b1, b2, eps, wd, adamw, bc1, bc2, clip=None):
+        self.C.adam_step(p, g, m, v, lr, b1, b2, eps, wd, adamw, bc1, bc2, clip)
+
+    def grad_norm(self, g, max_norm, norm_out, coef_out):
+        self.C.grad_norm(g, max_norm, norm_out, coef_out)
+
+    def scale_(self, x, coef):
+        self.C.scale_(x, coef)
+
+
+# --------------------------------------------------------------------------------------------
+class RefBackend:
+    """fp32 torch reference with identical semantics (CPU tests / numerics oracle)."""
+
+    name = "ref"
+    act_dtype = torch.float32
+
+    def __init__(self, device="cpu"):
+        self.device = torch.device(device)
+
+    @staticmethod
+    def _store(y: Act, v_nchw):
+        y.nhwc().copy_(v_nchw[:, :y.C].permute(0, 2, 3, 1))
+
+    def conv_mtiles(self, N, H, W, K, R, S, stride, pad):
+        return 1
+
+    def conv_fwd(self, x: Act, w, K, R, S, stride, pad, y: Act, bias=None, res=None, scale=None, shift=None,
+                 relu=False, stats=None, kvalid=0):
+        wk = w.view(K, R, S, x.C).permute(0, 3, 1, 2).float()
+        out = F.conv2d(x.nchw().float(), wk, None, stride, pad)
+        if bias is not None:
+            out = out + bias.view(1, -1, 1, 1)
+        if stats is not None:
+            stats.view(-1, 2, K)[0, 0].copy_(out.sum((0, 2, 3)))
+            stats.view(-1, 2, K)[0, 1].copy_((out * out).sum((0, 2, 3)))
+        if scale is not None:
+            out = out * scale.view(1, -1, 1, 1) + shift.view(1, -1, 1, 1)
+        if res is not None:
+            out = out + res.nchw().float()
+        if relu:
+            out = F.relu(out)
+        self._store(y, out)
+
+    def conv_dgrad(self, dy: Act, wT, C, R, S, stride, pad, dx: Act, res=None):
+        K = dy.C
+        wk = wT.view(C, R, S, K).permute(3, 0, 1, 2).float()
+        g = torch.nn.grad.conv2d_input((dx.N, C, dx.H, dx.W), wk, dy.nchw().float(), stride, pad)
+        if res is not None:
+            g = g + res.nchw().float()
+        self._store(dx, g)
+
+    def convT_fwd(self, x: Act, wf, Cout, y: Act, bias=None):
+        Cin = x.C
+        wk = wf.view(Cout, 2, 2, Cin).permute(3, 0, 1, 2).float()
+        out = F.conv_transpose2d(x.nchw().float(), wk, bias, stride=2)
+        self._store(y, out)
+
+    def conv_wgrad(self, dy: Act, x: Act, R, S, stride, pad, grad, Creal, Ko_real):
+        Ko, Cc = dy.C, x.C
+        gw = torch.nn.grad.conv2d_weight(x.nchw().float(), (Ko, Cc, R, S), dy.nchw().float(), stride, pad)
+        gw = gw.permute(0, 2, 3, 1)[:Ko_real, :, :, :Creal]
+        grad.view(Ko_real, R, S, Creal).add_(gw)
+
+    def bn_finalize(self, stats, ntiles, C, count, gamma, beta, rm, rv, momentum, eps, scale, shift, save_mean,
+                    save_invstd):
+        s = stats.view(-1, 2, C)[:ntiles].double().sum(0)
+        mean = s[0] / count
+        var = (s[1] / count - mean * mean).clamp_min(0)
+        invstd = 1.0 / torch.sqrt(var + eps)
+        g = gamma.double() if gamma is not None else torch.ones_like(mean)
+        b = beta.double() if beta is not None else torch.zeros_like(mean)
+        sc = (g * invstd).float()
+        scale.copy_(sc)
+        shift.copy_((b - mean * g * invstd).float())
+        if save_mean is not None:
+            save_mean.copy_(mean.float())
+        if save_invstd is not None:
+            save_invstd.copy_(invstd.float())
+        if rm is not None:
+            unb = var * count / (count - 1) if count > 1 else var
+            rm.mul_(1 - momentum).add_(momentum * mean.float())
+            rv.mul_(1 - momentum).add_(momentum * unb.float())
+
+    def bn_stats(self, x: Act):
+        v = x.nhwc().float()
+        part = torch.stack([v.sum((0, 1, 2)), (v * v).sum((0, 1, 2))]).unsqueeze(0)
+        return part, 1
+
+    def bn_apply(self, x: Act, scale, shift, res, relu, y: Act):
+        v = x.nhwc().float() * scale + shift
+        if res is not None:
+            v = v + res.nhwc().float()
+        if relu:
+            v = F.relu(v)
+        y.nhwc().copy_(v)
+
+    def bn_bwd(self, dy: Act, ymask, x: Act, mean, invstd, gamma, dgamma, dbeta, dx: Act, dyr_out=None):
+        g = dy.nhwc().float()
+        if ymask is not None:
+            g = g * (ymask.nhwc() > 0)
+        M = x.rows
+        xhat = (x.nhwc().float() - mean) * invstd
+        s1 = g.sum((0, 1, 2))
+        s2 = (g * xhat).sum((0, 1, 2))
+        if dbeta is not None:
+            dbeta.add_(s1)
+        if dgamma is not None:
+            dgamma.add_(s2)
+        k1 = (gamma if gamma is not None else torch.ones_like(mean)) * invstd
+        dx.nhwc().copy_(k1 * (g - s1 / M - xhat * s2 / M))
+        if dyr_out is not None:
+            dyr_out.nhwc().copy_(g)
+
+    def channel_sum(self, x: Act, out_acc):
+        out_acc.add_(x.nhwc().float().sum((0, 1, 2)))
+
+    def maxpool_fwd(self, x: Act, k, s, p, y: Act):
+        out, idx = F.max_pool2d(x.nchw().float(), k, s, p, return_indices=True)
+        self._store(y, out)
+        return idx
+
+    def maxpool_bwd(self, dy: Act, idx, x: Act, k, s, p, dx: Act, add=None):
+        g = torch.ops.aten.max_pool2d_with_indices_backward(dy.nchw().float().contiguous(), x.nchw().float(), [k, k],
+                                                            [s, s], [p, p], [1, 1], False, idx)
+        if add is not None:
+            g = g + add.nchw().float()
+        self._store(dx, g)
+
+    def avgpool_fwd(self, x: Act, y: Act):
+        y.nhwc().copy_(x.nhwc().float().mean((1, 2), keepdim=True))
+
+    def avgpool_bwd(self, dy: Act, dx: Act):
+        dx.nhwc().copy_(dy.nhwc().float().expand(dx.N, dx.H, dx.W, dx.C) / (dx.H * dx.W))
+
+    def nchw_to_nhwc(self, x: torch.Tensor, Cpad) -> Act:
+        N, Cc, H, W = x.shape
+        y = Act.zeros(N, H, W, Cpad, torch.float32, x.device)
+        y.nhwc()[..., :Cc].copy_(x.permute(0, 2, 3, 1))
+        return y
+
+    def upsample_fwd(self, x: Act, y: Act):
+        out = F.interpolate(x.nchw().float(), scale_factor=2, mode="bilinear", align_corners=True)
+        self._store(y, out)
+
+    def upsample_bwd(self, dy: Act, dx: Act):
+        xin = torch.zeros(dx.N, dx.C, dx.H, dx.W, requires_grad=True)
+        with torch.enable_grad():
+            out = F.interpolate(xin, scale_factor=2, mode="bilinear", align_corners=True)
+            (g,) = torch.autograd.grad(out, xin, dy.nchw().float())
+        self._store(dx, g)
+
+    def cast_weights(self, entries, total, dst_flat):
+        for (src, doff, d, v, st) in entries:
+            n = d[0] * d[1] * d[2] * d[3]
+            dst = dst_flat[doff:doff + n].view(*d)
+            dst.zero_()
+            dst[:v[0], :v[1], :v[2], :v[3]].copy_(src.as_strided(tuple(v), tuple(st)))
+
+    def ce_fwd(self, logits, labels):
+        lse = torch.logsumexp(logits.float(), 1)
+        loss = F.cross_entropy(logits.float(), labels)
+        return loss, lse
+
+    def ce_bwd(self, logits, labels, lse, go):
+        p = torch.exp(logits.float() - lse[:, None])
+        p[torch.arange(len(labels)), labels] -= 1.0
+        return p * (go if go is not None else 1.0) / logits.shape[0]
+
+    def bce_fwd(self, logits, target):
+        return F.binary_cross_entropy_with_logits(logits.float(), target.float())
+
+    def bce_bwd(self, logits, target, go):
+        return (torch.sigmoid(logits.float()) - target) * (go if go is not None else 1.0) / logits.numel()
+
+    def argmax_correct(self, logits, labels):
+        return (logits.argmax(1) == labels).sum().to(torch.int32).view(1)
+
+    def dice(self, logits, target):
+        pred = (logits.reshape(target.shape) > 0).float()
+        inter = (pred * target).flatten(1).sum(1)
+        uni = pred.flatten(1).sum(1) + target.flatten(1).sum(1)
+        return torch.where(uni > 0, (2 * inter + 1e-8) / (uni + 1e-8), torch.ones_like(uni))
+
+    def sgd(self, p, g, m, lr, momentum, dampening, wd, nesterov, first, skip_flag=None):
+        if skip_flag is not None and float(skip_flag.reshape(-1)[0]) != 0:
+            return
+        d = g + wd * p if wd != 0 else g.clone()
+        if momentum != 0:
+            if first:
+                m.copy_(d)
+            else:
+                m.mul_(momentum).add_(d, alpha=1 - dampening)
+            d = d + momentum * m if nesterov else m
+        p.add_(d, alpha=-lr)
+
+    def adam(self, p, g, m, v, lr, b1, b2, eps, wd, adamw, bc1, bc2, clip=None):
+        coef = 1.0
+        if clip is not None:
+            if float(clip[1]) != 0:
+                return
+            coef = clip[0]
+        g = g * coef
+        if wd != 0:
+            if adamw:
+                p.mul_(1 - lr * wd)
+            else:
+                g = g + wd * p
+        m.lerp_(g, 1 - b1)
+        v.mul_(b2).addcmul_(g, g, value=1 - b2)
+        denom = v.sqrt() / (bc2 ** 0.5) + eps
+        p.addcdiv_(m, denom, value=-lr / bc1)
+
+    def grad_norm(self, g, max_norm, norm_out, coef_out):
+        n = g.double().pow(2).sum().sqrt().float()
+        norm_out.reshape(-1)[0] = n
+        coef_out[0] = torch.clamp(max_norm / (n + 1e-6), max=1.0)
+        coef_out[1] = 0.0 if torch.isfinite(n) else 1.0
+
+    def scale_(self, x, coef):
+        x.mul_(coef[0])
+
+
+def make_backend(device) -> "NativeBackend | RefBackend":
+    device = torch.device(device)
+    if device.type == "cuda":
+        return NativeBackend(device)
+    return RefBackend(device)

@@ -1,0 +1,353 @@
+"""Communicators: one object per process exposing the collectives the framework needs.
+
+* :class:`RcclCommunicator` -- the GPU data plane: our native RCCL communicator (``_C.RcclComm``)
+  over xGMI with its own comm stream; RCCL unique id distributed by MPI_Bcast (mpirun) or the
+  gloo control plane (torchrun).
+* :class:`TorchCommunicator` -- ``torch.distributed`` gloo group (CPU tensors; tests, plumbing).
+* :class:`MPICommunicator` -- host MPI collectives through ``_mpi`` (the CPU hello-world path).
+* :class:`SingleCommunicator` -- world size 1, all collectives are no-ops.
+
+``init_distributed()`` picks the launcher and backend; ``get_comm()`` returns the current one.
+The reference uses ``dist.init_process_group('nccl'|'gloo')`` directly
+(/root/reference/pytorch/hello_world/hello_world.py:33-39, resnet/main.py:147-153).
+"""
+from __future__ import annotations
+
+import datetime
+import os
+
+import torch
+import torch.distributed as dist
+
+from .bootstrap import LaunchInfo, detect_launcher, mpi_bring_up
+
+_CURRENT = None
+
+
+class Communicator:
+    backend = "base"
+
+    def __init__(self, info: LaunchInfo, device):
+        self.info = info
+        self.rank, self.world_size = info.rank, info.world_size
+        self.local_rank = info.local_rank
+        self.device = torch.device(device)
+
+    # collectives on tensors (in place where applicable)
+    def allreduce(self, t, op="sum"):
+        raise NotImplementedError
+
+    def broadcast(self, t, src=0):
+        raise NotImplementedError
+
+    def allgather(self, out, t):
+        raise NotImplementedError
+
+    def reduce_scatter(self, out, t, op="sum"):
+        raise NotImplementedError
+
+    def alltoall(self, out, t):
+        raise NotImplementedError
+
+    def send(self, t, dst):
+        raise NotImplementedError
+
+    def recv(self, t, src):
+        raise NotImplementedError
+
+    def barrier(self):
+        raise NotImplementedError
+
+    def bucket_comm(self):
+        """A ``_C.CommBase`` for the gradient reducer."""
+        raise NotImplementedError
+
+    def destroy(self):
+        pass
+
+
+class SingleCommunicator(Communicator):
+    backend = "single"
+
+    def allreduce(self, t, op="sum"):
+        return t
+
+    def broadcast(self, t, src=0):
+        return t
+
+    def allgather(self, out, t):
+        out.view(-1).copy_(t.reshape(-1))
+        return out
+
+    def reduce_scatter(self, out, t, op="sum"):
+        out.copy_(t.reshape(out.shape))
+        return out
+
+    def alltoall(self, out, t):
+        out.copy_(t)
+        return out
+
+    def send(self, t, dst):
+        raise RuntimeError("send with world_size 1")
+
+    def recv(self, t, src):
+        raise RuntimeError("recv with world_size 1")
+
+    def barrier(self):
+        pass
+
+
+class RcclCommunicator(Communicator):
+    backend = "rccl"
+
+    def __init__(self, info, device, native_comm, control_group=None):
+        super().__init__(info, device)
+        self.c = native_comm
+        self.control = control_group
+
+    def allreduce(self, t, op="sum"):
+        self.c.allreduce(t, op, False)
+        return t
+
+    def broadcast(self, t, src=0):
+        self.c.broadcast(t, src, False)
+        return t
+
+    def allgather(self, out, t):
+        self.c.allgather(out, t.contiguous(), False)
+        return out
+
+    def reduce_scatter(self, out, t, op="sum"):
+        self.c.reduce_scatter(out, t.contiguous(), op, False)
+        return out
+
+    def alltoall(self, out, t):
+        self.c.alltoall(out, t.contiguous(), False)
+        return out
+
+    def send(self, t, dst):
+        self.c.send(t, dst)
+
+    def recv(self, t, src):
+        self.c.recv(t, src)
+        return t
+
+    def barrier(self):
+        self.c.barrier()
+
+    def bucket_comm(self):
+        from .._ext import native
+
+        return native().RcclBucketComm(self.c)
+
+    def destroy(self):
+        self.c.destroy()
+        if dist.is_initialized():
+            dist.destroy_process_group()
+
+
+def _make_torch_bucket_comm(group, world_size):
+    from .._ext import native
+
+    class _TorchBucketComm(native().CommBase):
+        """Reducer backend over a torch.distributed group (gloo): async all-reduce per bucket,
+        waited for (and averaged) at the end of the backward pass."""
+
+        def __init__(self):
+            super().__init__()
+            self.works = []
+
+        def allreduce_bucket(self, t, average):
+            self.works.append((dist.all_reduce(t, group=group, async_op=True), t, average))
+
+        def end_backward(self):
+            for w, t, avg in self.works:
+                w.wait()
+                if avg:
+                    t.div_(world_size)
+            self.works.clear()
+
+    return _TorchBucketComm()
+
+
+class TorchCommunicator(Communicator):
+    backend = "gloo"
+
+    _OPS = {"sum": dist.ReduceOp.SUM, "max": dist.ReduceOp.MAX, "min": dist.ReduceOp.MIN,
+            "prod": dist.ReduceOp.PRODUCT}
+
+    def __init__(self, info, device, group=None):
+        super().__init__(info, device)
+        self.group = group
+
+    def allreduce(self, t, op="sum"):
+        if op == "avg":
+            dist.all_reduce(t, dist.ReduceOp.SUM, group=self.group)
+            t.div_(self.world_size)
+        else:
+            dist.all_reduce(t, self._OPS[op], group=self.group)
+        return t
+
+    def broadcast(self, t, src=0):
+        dist.broadcast(t, src, group=self.group)
+        return t
+
+    def allgather(self, out, t):
+        chunks = list(out.view(self.world_size, -1).unbind(0))
+        dist.all_gather(chunks, t.reshape(-1).contiguous(), group=self.group)
+        return out
+
+    def reduce_scatter(self, out, t, op="sum"):
+        full = t.reshape(self.world_size, -1).clone()
+        self.allreduce(full, op)
+        out.view(-1).copy_(full[self.rank])
+        return out
+
+    def alltoall(self, out, t):
+        ins = list(t.reshape(self.world_size, -1).unbind(0))
+        outs = list(out.view(self.world_size, -1).unbind(0))
+        for r in range(self.world_size):   # gloo has no all_to_all: pairwise exchange
+            if r == self.rank:
+                outs[r].copy_(ins[r])
+        reqs = []
+        for r in range(self.world_size):
+            if r != self.rank:
+                reqs.append(dist.isend(ins[r].contiguous(), r, group=self.group))
+                reqs.append(dist.irecv(outs[r], r, group=self.group))
+        for q in reqs:
+            q.wait()
+        return out
+
+    def send(self, t, dst):
+        dist.send(t, dst, group=self.group)
+
+    def recv(self, t, src):
+        dist.recv(t, src, group=self.group)
+        return t
+
+    def barrier(self):
+        dist.barrier(group=self.group)
+
+    def bucket_comm(self):
+        return _make_torch_bucket_comm(self.group, self.world_size)
+
+    def destroy(self):
+        if dist.is_initialized():
+            dist.destroy_process_group()
+
+
+class MPICommunicator(Communicator):
+    """Host-side MPI collectives on CPU tensors (float32 / float64)."""
+
+    backend = "mpi"
+
+    def __init__(self, info, device="cpu"):
+        super().__init__(info, device)
+        from .._ext import mpi
+
+        self.m = mpi()
+
+    def allreduce(self, t, op="sum"):
+        a = t.detach().cpu().contiguous()
+        n = a.numpy()
+        if a.dtype == torch.float64:
+            self.m.allreduce_f64(n, "sum" if op == "avg" else op)
+        else:
+            n32 = n.astype("float32", copy=False)
+            self.m.allreduce_f32(n32, "sum" if op == "avg" else op)
+            a = torch.from_numpy(n32)
+        if op == "avg":
+            a /= self.world_size
+        t.copy_(a)
+        return t
+
+    def broadcast(self, t, src=0):
+        import numpy as np
+
+        data = t.detach().cpu().contiguous().numpy().tobytes() if self.rank == src else b""
+        buf = self.m.bcast_bytes(data, src)
+        t.copy_(torch.from_numpy(np.frombuffer(buf, dtype=t.detach().cpu().numpy().dtype).copy()).view(t.shape))
+        return t
+
+    def send(self, t, dst):
+        self.m.send_f32(t.detach().float().contiguous().numpy(), dst, 0)
+
+    def recv(self, t, src):
+        a = torch.empty(t.shape, dtype=torch.float32)
+        self.m.recv_f32(a.numpy(), src, 0)
+        t.copy_(a)
+        return t
+
+    def barrier(self):
+        self.m.barrier()
+
+    def destroy(self):
+        self.m.finalize()
+
+
+def _resolve_backend(backend: str) -> str:
+    b = (backend or "auto").lower()
+    if b == "auto":
+        return "rccl" if torch.cuda.is_available() else "gloo"
+    if b in ("nccl", "rccl"):
+        return "rccl"
+    if b in ("gloo", "mpi"):
+        return b
+    raise ValueError(f"unknown backend {backend!r}")
+
+
+def init_distributed(backend: str = "auto", timeout_s: float = 1800.0) -> Communicator:
+    """Bring up ranks and the communicator. Safe to call once per process."""
+    global _CURRENT
+    if _CURRENT is not None:
+        return _CURRENT
+    info = detect_launcher()
+    if info.launcher == "mpi":
+        info = mpi_bring_up()
+    be = _resolve_backend(backend)
+    if be == "rccl":
+        if info.local_rank < 0:
+            info.local_rank = info.rank % max(1, torch.cuda.device_count())
+        torch.cuda.set_device(info.local_rank)
+        device = torch.device("cuda", info.local_rank)
+    else:
+        device = torch.device("cpu")
+    if info.world_size == 1:
+        _CURRENT = SingleCommunicator(info, device)
+        return _CURRENT
+    if be == "mpi":
+        _CURRENT = MPICommunicator(info, "cpu")
+        return _CURRENT
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    dist.init_process_group("gloo", rank=info.rank, world_size=info.world_size,
+                            timeout=datetime.timedelta(seconds=timeout_s))
+    if be == "gloo":
+        _CURRENT = TorchCommunicator(info, device)
+        return _CURRENT
+    from .._ext import native
+
+    C = native()
+    uid = [C.RcclComm.unique_id() if info.rank == 0 else None]
+    dist.broadcast_object_list(uid, src=0)
+    nc = C.RcclComm(uid[0], info.rank, info.world_size, info.local_rank)
+    _CURRENT = RcclCommunicator(info, device, nc)
+    return _CURRENT
+
+
+def get_comm() -> Communicator:
+    """Current communicator (a single-process one if init_distributed was never called)."""
+    global _CURRENT
+    if _CURRENT is None:
+        info = detect_launcher()
+        if info.world_size != 1:
+            raise RuntimeError("multi-process launch detected: call init_distributed() first")
+        dev = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else torch.device("cpu")
+        _CURRENT = SingleCommunicator(info, dev)
+    return _CURRENT
+
+
+def destroy_distributed():
+    global _CURRENT
+    if _CURRENT is not None:
+        _CURRENT.destroy()
+    _CURRENT = None

@@ -1,0 +1,236 @@
+"""ParamArena: flat, device-resident parameter / gradient / buffer storage.
+
+Every parameter of a model is re-homed into ONE fp32 buffer (and its gradient into ONE fp32
+gradient buffer) laid out in *reverse registration order* -- roughly the order in which the
+backward pass produces gradients.  Consequences (MI355X-first design):
+
+* DDP gradient buckets are contiguous slices of the flat gradient: all-reduced in place over RCCL,
+  no pack/unpack (the reference's torch DDP Reducer copies grads into bucket buffers);
+* optimizers (SGD / Adam / grad-norm clip) are ONE kernel over the flat buffers;
+* BatchNorm running statistics live in one flat buffer -> the per-step buffer broadcast of DDP
+   is a single collective;
+* conv weights are stored channels-last (memory order [K][R][S][C]) so the fp32 master already
+  has the GEMM layout, and the kernels' weight-gradient output lands in it directly;
+* bf16 compute copies (forward layout and transposed data-gradient layout, channel padded) are
+  produced for all layers by ONE multi-tensor cast launch whenever the masters changed.
+
+``nn.Parameter`` objects are kept (their ``.data`` is re-pointed into the arena), so
+``state_dict()`` keys/shapes/dtypes are unchanged and foreign optimizers still work.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn as nn
+
+_ARENAS = {}   # id(param) -> arena
+
+
+def arena_of(param) -> "ParamArena | None":
+    a = _ARENAS.get(id(param))
+    if a is not None and a.owns(param):
+        return a
+    return None
+
+
+def _conv_like(m):
+    return isinstance(m, (nn.Conv2d, nn.ConvTranspose2d))
+
+
+class ParamArena:
+    ALIGN = 16   # elements (64 bytes): every tensor starts on a 64-B boundary
+
+    def __init__(self, module: nn.Module, device, backend=None):
+        self.device = torch.device(device)
+        self.backend = backend
+        named = []
+        seen = set()
+        for n, p in module.named_parameters():
+            if id(p) in seen:
+                continue
+            seen.add(id(p))
+            named.append((n, p))
+        self.names = [n for n, _ in named]
+        self.params = [p for _, p in named]
+        self.index = {id(p): i for i, p in enumerate(self.params)}
+
+        layout = {}
+        for m in module.modules():
+            if isinstance(m, nn.Conv2d) and m.weight.dim() == 4:
+                layout[id(m.weight)] = "krsc"          # [K,C,R,S] stored as [K][R][S][C]
+            elif isinstance(m, nn.ConvTranspose2d):
+                layout[id(m.weight)] = "convT"         # [Cin,Cout,kh,kw] stored as [Cin][kh][kw][Cout]
+
+        # flat layout in reverse registration order
+        order = list(range(len(self.params)))[::-1]
+        self.offsets = [0] * len(self.params)
+        off = 0
+        for i in order:
+            self.offsets[i] = off
+            n = self.params[i].numel()
+            off += (n + self.ALIGN - 1) // self.ALIGN * self.ALIGN
+        self.total = off
+        self.flat = torch.zeros(self.total, dtype=torch.float32, device=self.device)
+        self.grad = torch.zeros(self.total, dtype=torch.float32, device=self.device)
+        self.order = order
+
+        for i, p in enumerate(self.params):
+            kind = layout.get(id(p), "contig")
+            shape = tuple(p.shape)
+            strides = self._strides(shape, kind)
+            view = self.flat.as_strided(shape, strides, self.offsets[i])
+            with torch.no_grad():
+                view.copy_(p.data)
+            p.data = view
+            p.grad = self.grad.as_strided(shape, strides, self.offsets[i])
+            _ARENAS[id(p)] = self
+        self.layouts = [layout.get(id(p), "contig") for p in self.params]
+
+        # buffers: BN running stats (float) + num_batches_tracked (int64)
+        fbufs, ibufs = [], []
+        for m in module.modules():
+            for bn, b in m._buffers.items():
+                if b is None:
+                    continue
+                (fbufs if b.is_floating_point() else ibufs).append((m, bn, b))
+        self.fbuf_total = sum(b.numel() for _, _, b in fbufs)
+        self.fbuf = torch.zeros(max(1, self.fbuf_total), dtype=torch.float32, device=self.device)
+        o = 0
+        for m, bn, b in fbufs:
+            v = self.fbuf[o:o + b.numel()].view(b.shape)
+            v.copy_(b.to(self.device, torch.float32))
+            m._buffers[bn] = v
+            o += b.numel()
+        self.ibuf_total = sum(b.numel() for _, _, b in ibufs)
+        self.ibuf = torch.zeros(max(1, self.ibuf_total), dtype=torch.int64, device=self.device)
+        o = 0
+        for m, bn, b in ibufs:
+            v = self.ibuf[o:o + b.numel()].view(b.shape)
+            v.copy_(b.to(self.device))
+            m._buffers[bn] = v
+            o += b.numel()
+
+        # compute copies
+        self._entries = []
+        self._compute_total = 0
+        self.compute = None
+        self._synced_version = None
+        self.hook = None            # reducer.mark_ready(param_index) during backward
+        self.backward_end = None    # reducer.finalize() at the end of the engine backward
+        self.zero_pending = False
+
+    @staticmethod
+    def _strides(shape, kind):
+        if kind == "krsc":
+            K, C, R, S = shape
+            return (R * S * C, 1, S * C, C)
+        if kind == "convT":
+            Ci, Co, R, S = shape
+            return (R * S * Co, 1, S * Co, Co)
+        st, acc = [], 1
+        for d in reversed(shape):
+            st.append(acc)
+            acc *= d
+        return tuple(reversed(st))
+
+    # ------------------------------------------------------------------ params / grads
+    def owns(self, p) -> bool:
+        i = self.index.get(id(p))
+        if i is None:
+            return False
+        return p.data.data_ptr() == self.flat.data_ptr() + 4 * self.offsets[i]
+
+    def valid(self) -> bool:
+        return all(self.owns(p) for p in self.params)
+
+    def param_flat(self, p) -> torch.Tensor:
+        i = self.index[id(p)]
+        return self.flat[self.offsets[i]:self.offsets[i] + p.numel()]
+
+    def grad_flat(self, p) -> torch.Tensor:
+        i = self.index[id(p)]
+        return self.grad[self.offsets[i]:self.offsets[i] + p.numel()]
+
+    def attach_grads(self):
+        """Re-attach .grad views (a foreign optimizer's zero_grad(set_to_none=True) drops them)."""
+        dropped = False
+        for i, p in enumerate(self.params):
+            g = p.grad
+            if g is None or g.data_ptr() != self.grad.data_ptr() + 4 * self.offsets[i]:
+                p.grad = self.grad.as_strided(tuple(p.shape), self._strides(tuple(p.shape), self.layouts[i]),
+                                              self.offsets[i])
+                dropped = True
+        if dropped:
+            self.grad.zero_()
+
+    def zero_grad(self):
+        self.grad.zero_()
+
+    def ready(self, *ps):
+        if self.hook is not None:
+            for p in ps:
+                if p is not None:
+                    self.hook(self.index[id(p)])
+
+    def end_backward(self):
+        if self.backward_end is not None:
+            self.backward_end()
+
+    # ------------------------------------------------------------------ compute copies
+    def add_compute(self, p, dims, valid, src_dims):
+        """Register a compute copy of parameter ``p``: destination dims (4-D, contiguous), how many
+        indices of each destination dim are valid (rest zero padding) and, for each destination dim,
+        which source dim of ``p`` it walks (None = broadcast a size-1 dim).  Returns a handle."""
+        st_p = p.data.stride()
+        st = tuple(0 if s is None else st_p[s] for s in src_dims)
+        off = self._compute_total
+        n = dims[0] * dims[1] * dims[2] * dims[3]
+        self._entries.append((p.data, off, tuple(dims), tuple(valid), st))
+        self._compute_total += (n + self.ALIGN - 1) // self.ALIGN * self.ALIGN
+        self.compute = None
+        return (off, n, tuple(dims))
+
+    def get_compute(self, handle) -> torch.Tensor:
+        off, n, dims = handle
+        return self.compute[off:off + n]
+
+    def _version(self):
+        return sum(p._version for p in self.params) + self.flat._version
+
+    def refresh(self, force=False):
+        """Recast all compute copies if any master parameter changed (one kernel launch)."""
+        if self.compute is None:
+            dt = self.backend.act_dtype if self.backend is not None else torch.bfloat16
+            self.compute = torch.zeros(max(1, self._compute_total), dtype=dt, device=self.device)
+            force = True
+        v = self._version()
+        if force or v != self._synced_version:
+            self.backend.cast_weights(self._entries, self._compute_total, self.compute)
+            self._synced_version = v
+
+    def mark_updated(self):
+        self._synced_version = None
+
+    # ------------------------------------------------------------------ buckets
+    def buckets(self, first_cap_bytes, cap_bytes):
+        """Contiguous gradient buckets over the flat buffer (in flat = reverse-registration order).
+        Returns (list of (start, end) element ranges, param -> bucket index list)."""
+        bounds = []
+        pb = [0] * len(self.params)
+        start = 0
+        cur = 0
+        cap = first_cap_bytes
+        for i in self.order:
+            end = self.offsets[i] + self.params[i].numel()
+            end = (end + self.ALIGN - 1) // self.ALIGN * self.ALIGN
+            pb[i] = len(bounds)
+            cur = end
+            if (cur - start) * 4 >= cap:
+                bounds.append((start, cur))
+                start = cur
+                cap = cap_bytes
+        if cur > start or not bounds:
+            bounds.append((start, max(cur, start)))
+        # params assigned after the last closed bucket belong to the final one
+        for i in range(len(pb)):
+            pb[i] = min(pb[i], len(bounds) - 1)
+        return bounds, pb

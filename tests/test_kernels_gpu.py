@@ -1,0 +1,264 @@
+"""Numerics of every gfx950 HIP kernel against the fp32 torch reference backend (same op
+semantics, same bf16-rounded inputs).  Shapes follow SURVEY.md §2.5 (ResNet stem / 3x3 / 1x1 /
+strided / downsample, UNet concat widths, linear heads, odd tile remainders)."""
+import pytest
+import torch
+
+from deeplearning_mpi_amd.ops.act import Act, pad8
+from deeplearning_mpi_amd.ops.backend import NativeBackend, RefBackend
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _be():
+    return NativeBackend(DEV), RefBackend(DEV)
+
+
+def _act(N, H, W, C, ld=None, off=0, scale=1.0):
+    ld = ld or C
+    buf = (torch.randn(N * H * W, ld, device=DEV) * scale).to(torch.bfloat16)
+    a = Act(buf, N, H, W, C, off)
+    r = Act(buf.float(), N, H, W, C, off)
+    return a, r
+
+
+def _empty(N, H, W, C, dtype=torch.bfloat16, ld=None):
+    return Act.empty(N, H, W, C, dtype, DEV, ld)
+
+
+def _rel(a, b):
+    a, b = a.float(), b.float()
+    return ((a - b).abs().max() / b.abs().max().clamp_min(1e-6)).item()
+
+
+CONV_SHAPES = [
+    # N, H, W, Cin, Cout, R, stride, pad
+    (2, 32, 32, 3, 64, 7, 2, 3),       # ResNet stem (Cin padded to 8)
+    (2, 14, 14, 64, 64, 3, 1, 1),
+    (2, 14, 14, 128, 128, 3, 2, 1),
+    (3, 7, 7, 256, 64, 1, 1, 0),       # M = 147: tile remainders
+    (2, 8, 8, 64, 256, 1, 1, 0),
+    (2, 14, 14, 256, 512, 1, 2, 0),    # downsample 1x1 stride 2
+    (1, 16, 24, 192, 64, 3, 1, 1),     # UNet decoder level-1 concat width
+    (2, 15, 20, 512, 1024, 3, 1, 1),   # UNet bottleneck at the reference 240x320 scale
+]
+
+
+@pytest.mark.parametrize("shape", CONV_SHAPES)
+def test_conv_fwd(shape):
+    nb, rb = _be()
+    N, H, W, Cin, K, R, s, p = shape
+    Cp, Kp = pad8(Cin), pad8(K)
+    x, xr = _act(N, H, W, Cp)
+    w = (torch.randn(Kp, R, R, Cp, device=DEV) / (R * R * Cin) ** 0.5).to(torch.bfloat16)
+    bias = torch.randn(Kp, device=DEV)
+    P, Q = (H + 2 * p - R) // s + 1, (W + 2 * p - R) // s + 1
+    res, resr = _act(N, P, Q, Kp)
+    y = _empty(N, P, Q, Kp)
+    yr = _empty(N, P, Q, Kp, torch.float32)
+    mt = nb.conv_mtiles(N, H, W, Kp, R, R, s, p)
+    st = torch.zeros(mt, 2, Kp, device=DEV)
+    str_ = torch.zeros(1, 2, Kp, device=DEV)
+    nb.conv_fwd(x, w, Kp, R, R, s, p, y, bias=bias, stats=st)
+    rb.conv_fwd(xr, w.float(), Kp, R, R, s, p, yr, bias=bias, stats=str_)
+    torch.cuda.synchronize()
+    assert _rel(y.buf, yr.buf) < 1e-2
+    assert _rel(st.sum(0)[0], str_[0, 0]) < 2e-2
+    assert _rel(st.sum(0)[1], str_[0, 1]) < 2e-2
+    # fused residual + relu + affine
+    sc, sh = torch.rand(Kp, device=DEV) + 0.5, torch.randn(Kp, device=DEV)
+    nb.conv_fwd(x, w, Kp, R, R, s, p, y, res=res, scale=sc, shift=sh, relu=True)
+    rb.conv_fwd(xr, w.float(), Kp, R, R, s, p, yr, res=resr, scale=sc, shift=sh, relu=True)
+    assert _rel(y.buf, yr.buf) < 1e-2
+
+
+@pytest.mark.parametrize("shape", CONV_SHAPES[1:])
+def test_conv_dgrad(shape):
+    nb, rb = _be()
+    N, H, W, Cin, K, R, s, p = shape
+    Cp, Kp = pad8(Cin), pad8(K)
+    P, Q = (H + 2 * p - R) // s + 1, (W + 2 * p - R) // s + 1
+    dy, dyr = _act(N, P, Q, Kp)
+    wT = (torch.randn(Cp, R, R, Kp, device=DEV) / (R * R * K) ** 0.5).to(torch.bfloat16)
+    res, resr = _act(N, H, W, Cp)
+    dx = _empty(N, H, W, Cp)
+    dxr = _empty(N, H, W, Cp, torch.float32)
+    nb.conv_dgrad(dy, wT, Cp, R, R, s, p, dx, res=res)
+    rb.conv_dgrad(dyr, wT.float(), Cp, R, R, s, p, dxr, res=resr)
+    torch.cuda.synchronize()
+    assert _rel(dx.buf, dxr.buf) < 1e-2
+
+
+@pytest.mark.parametrize("shape", CONV_SHAPES)
+def test_conv_wgrad(shape):
+    nb, rb = _be()
+    N, H, W, Cin, K, R, s, p = shape
+    Cp, Kp = pad8(Cin), pad8(K)
+    P, Q = (H + 2 * p - R) // s + 1, (W + 2 * p - R) // s + 1
+    x, xr = _act(N, H, W, Cp)
+    dy, dyr = _act(N, P, Q, Kp)
+    g = torch.randn(K * R * R * Cin, device=DEV)
+    gr = g.clone()
+    nb.conv_wgrad(dy, x, R, R, s, p, g, Cin, K)
+    rb.conv_wgrad(dyr, xr, R, R, s, p, gr, Cin, K)
+    torch.cuda.synchronize()
+    assert _rel(g, gr) < 5e-3
+
+
+def test_linear_heads():
+    nb, rb = _be()
+    for (N, Cin, K) in [(8, 2048, 1000), (16, 512, 10)]:
+        Kp = pad8(K)
+        x, xr = _act(N, 1, 1, Cin)
+        w = (torch.randn(Kp, 1, 1, Cin, device=DEV) / Cin ** 0.5).to(torch.bfloat16)
+        w[K:] = 0
+        bias = torch.randn(Kp, device=DEV)
+        out = torch.empty(N, K, device=DEV)
+        outr = torch.empty(N, K, device=DEV)
+        nb.conv_fwd(x, w, Kp, 1, 1, 1, 0, Act(out, N, 1, 1, K), bias=bias, kvalid=K if K < Kp else 0)
+        rb.conv_fwd(xr, w.float(), Kp, 1, 1, 1, 0, Act(outr, N, 1, 1, K), bias=bias)
+        torch.cuda.synchronize()
+        assert _rel(out, outr) < 1e-2
+
+
+def test_unet_head_1ch():
+    nb, rb = _be()
+    N, H, W = 2, 16, 16
+    x, xr = _act(N, H, W, 64)
+    w = (torch.randn(8, 1, 1, 64, device=DEV) / 8).to(torch.bfloat16)
+    w[1:] = 0
+    bias = torch.zeros(8, device=DEV)
+    bias[0] = 0.3
+    o = torch.empty(N * H * W, 1, device=DEV)
+    orf = torch.empty(N * H * W, 1, device=DEV)
+    nb.conv_fwd(x, w, 8, 1, 1, 1, 0, Act(o, N, H, W, 1), bias=bias, kvalid=1)
+    rb.conv_fwd(xr, w.float(), 8, 1, 1, 1, 0, Act(orf, N, H, W, 1), bias=bias)
+    assert _rel(o, orf) < 1e-2
+
+
+def test_convT():
+    nb, rb = _be()
+    N, H, W, Ci, Co = 2, 8, 12, 256, 256
+    x, xr = _act(N, H, W, Ci)
+    wf = (torch.randn(Co, 2, 2, Ci, device=DEV) / Ci ** 0.5).to(torch.bfloat16)
+    bias = torch.randn(Co, device=DEV)
+    cat = _empty(N, 2 * H, 2 * W, Co + 128)
+    catr = _empty(N, 2 * H, 2 * W, Co + 128, torch.float32)
+    nb.convT_fwd(x, wf, Co, cat.slice(0, Co), bias)
+    rb.convT_fwd(xr, wf.float(), Co, catr.slice(0, Co), bias)
+    torch.cuda.synchronize()
+    assert _rel(cat.nhwc()[..., :Co], catr.nhwc()[..., :Co]) < 1e-2
+
+
+def test_bn_family():
+    nb, rb = _be()
+    N, H, W, C = 4, 14, 14, 256
+    x, xr = _act(N, H, W, C)
+    res, resr = _act(N, H, W, C)
+    st, _ = nb.bn_stats(x)
+    str_, _ = rb.bn_stats(xr)
+    assert _rel(st.sum(0), str_.sum(0)) < 1e-4
+    gamma, beta = torch.rand(C, device=DEV) + 0.5, torch.randn(C, device=DEV)
+    outs = []
+    for be, s in ((nb, st), (rb, str_)):
+        rm, rv = torch.zeros(C, device=DEV), torch.ones(C, device=DEV)
+        v = torch.empty(4, C, device=DEV)
+        be.bn_finalize(s, s.shape[0], C, N * H * W, gamma, beta, rm, rv, 0.1, 1e-5, v[0], v[1], v[2], v[3])
+        outs.append((v, rm, rv))
+    for a, b in zip(outs[0], outs[1]):
+        assert _rel(a, b) < 1e-4
+    v = outs[0][0]
+    y = _empty(N, H, W, C)
+    yr = _empty(N, H, W, C, torch.float32)
+    nb.bn_apply(x, v[0], v[1], res, True, y)
+    rb.bn_apply(xr, v[0], v[1], resr, True, yr)
+    assert _rel(y.buf, yr.buf) < 1e-2
+    dy, dyr = _act(N, H, W, C)
+    dg, db = torch.zeros(C, device=DEV), torch.zeros(C, device=DEV)
+    dgr, dbr = torch.zeros(C, device=DEV), torch.zeros(C, device=DEV)
+    dx, dxr = _empty(N, H, W, C), _empty(N, H, W, C, torch.float32)
+    dyo, dyor = _empty(N, H, W, C), _empty(N, H, W, C, torch.float32)
+    yb = Act(y.buf, N, H, W, C)
+    nb.bn_bwd(dy, yb, x, v[2], v[3], gamma, dg, db, dx, dyo)
+    rb.bn_bwd(dyr, Act(y.buf.float(), N, H, W, C), xr, v[2], v[3], gamma, dgr, dbr, dxr, dyor)
+    torch.cuda.synchronize()
+    assert _rel(dg, dgr) < 1e-3 and _rel(db, dbr) < 1e-3
+    assert _rel(dx.buf, dxr.buf) < 2e-2
+    assert _rel(dyo.buf, dyor.buf) < 1e-2
+
+
+def test_pools_and_layout():
+    nb, rb = _be()
+    x = torch.randn(2, 3, 20, 18, device=DEV)
+    a = nb.nchw_to_nhwc(x, 8)
+    ar = rb.nchw_to_nhwc(x, 8)
+    assert _rel(a.buf, ar.buf) < 1e-2
+    for (k, s, p, H, W, C) in [(3, 2, 1, 16, 16, 64), (2, 2, 0, 16, 24, 128)]:
+        xa, xr = _act(2, H, W, C)
+        OH, OW = (H + 2 * p - k) // s + 1, (W + 2 * p - k) // s + 1
+        y, yr = _empty(2, OH, OW, C), _empty(2, OH, OW, C, torch.float32)
+        idx = nb.maxpool_fwd(xa, k, s, p, y)
+        idxr = rb.maxpool_fwd(xr, k, s, p, yr)
+        assert _rel(y.buf, yr.buf) < 1e-6
+        dy, dyr = _act(2, OH, OW, C)
+        add, addr = _act(2, H, W, C)
+        dx, dxr = _empty(2, H, W, C), _empty(2, H, W, C, torch.float32)
+        nb.maxpool_bwd(dy, idx, xa, k, s, p, dx, add=add)
+        rb.maxpool_bwd(dyr, idxr, xr, k, s, p, dxr, add=addr)
+        assert _rel(dx.buf, dxr.buf) < 1e-2
+    xa, xr = _act(4, 7, 7, 2048)
+    y, yr = _empty(4, 1, 1, 2048), _empty(4, 1, 1, 2048, torch.float32)
+    nb.avgpool_fwd(xa, y)
+    rb.avgpool_fwd(xr, yr)
+    assert _rel(y.buf, yr.buf) < 1e-2
+    dx, dxr = _empty(4, 7, 7, 2048), _empty(4, 7, 7, 2048, torch.float32)
+    nb.avgpool_bwd(y, dx)
+    rb.avgpool_bwd(Act(y.buf.float(), 4, 1, 1, 2048), dxr)
+    assert _rel(dx.buf, dxr.buf) < 1e-2
+    xa, xr = _act(2, 8, 6, 64)
+    y, yr = _empty(2, 16, 12, 64), _empty(2, 16, 12, 64, torch.float32)
+    nb.upsample_fwd(xa, y)
+    rb.upsample_fwd(xr, yr)
+    assert _rel(y.buf, yr.buf) < 1e-2
+    dx, dxr = _empty(2, 8, 6, 64), _empty(2, 8, 6, 64, torch.float32)
+    nb.upsample_bwd(y, dx)
+    rb.upsample_bwd(Act(y.buf.float(), 2, 16, 12, 64), dxr)
+    assert _rel(dx.buf, dxr.buf) < 1e-2
+
+
+def test_losses_eval_optim():
+    nb, rb = _be()
+    logits = torch.randn(64, 1000, device=DEV)
+    labels = torch.randint(1000, (64,), device=DEV)
+    go = torch.ones(1, device=DEV)
+    l1, s1 = nb.ce_fwd(logits, labels)
+    l2, s2 = rb.ce_fwd(logits, labels)
+    assert abs(l1.item() - l2.item()) < 1e-4
+    assert _rel(nb.ce_bwd(logits, labels, s1, go), rb.ce_bwd(logits, labels, s2, go)) < 1e-4
+    lg = torch.randn(2, 32, 32, device=DEV)
+    t = (torch.rand(2, 32, 32, device=DEV) > 0.5).float()
+    assert abs(nb.bce_fwd(lg, t).item() - rb.bce_fwd(lg, t).item()) < 1e-5
+    assert _rel(nb.bce_bwd(lg, t, go), rb.bce_bwd(lg, t, go)) < 1e-4
+    assert nb.argmax_correct(logits, labels).item() == rb.argmax_correct(logits, labels).item()
+    assert _rel(nb.dice(lg, t), rb.dice(lg, t)) < 1e-5
+    n = 100003
+    for be_args in [(0.1, 0.9, 0.0, 1e-5, False), (0.05, 0.9, 0.0, 0.0, True)]:
+        p, g, m = torch.randn(n, device=DEV), torch.randn(n, device=DEV), torch.randn(n, device=DEV)
+        p2, g2, m2 = p.clone(), g.clone(), m.clone()
+        for first in (True, False):
+            nb.sgd(p, g, m, *be_args, first)
+            rb.sgd(p2, g2, m2, *be_args, first)
+        assert _rel(p, p2) < 1e-6 and _rel(m, m2) < 1e-6
+    p, g = torch.randn(n, device=DEV), torch.randn(n, device=DEV)
+    m, v = torch.zeros(n, device=DEV), torch.zeros(n, device=DEV)
+    p2, m2, v2 = p.clone(), m.clone(), v.clone()
+    for step in (1, 2):
+        nb.adam(p, g, m, v, 1e-3, 0.9, 0.999, 1e-8, 0.0, False, 1 - 0.9 ** step, 1 - 0.999 ** step)
+        rb.adam(p2, g, m2, v2, 1e-3, 0.9, 0.999, 1e-8, 0.0, False, 1 - 0.9 ** step, 1 - 0.999 ** step)
+    assert _rel(p, p2) < 1e-6
+    nrm, coef = torch.empty(1, device=DEV), torch.empty(2, device=DEV)
+    nrm2, coef2 = torch.empty(1, device=DEV), torch.empty(2, device=DEV)
+    nb.grad_norm(g, 1.0, nrm, coef)
+    rb.grad_norm(g, 1.0, nrm2, coef2)
+    assert _rel(nrm, nrm2) < 1e-5 and _rel(coef, coef2) < 1e-5
