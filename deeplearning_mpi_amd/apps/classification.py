@@ -1,0 +1,154 @@
+"""ResNet data-parallel classification training (the reference's pytorch/resnet/{main,resnet}.py).
+
+Flags keep the reference names and defaults: --num_epochs, --batch_size (per
+process), --learning_rate, --random_seed, --model_dir, --model_filename, --resume.  Non-breaking
+additions: --arch, --num_classes, --synthetic, --data_root, --image_size, --backend, --device,
+--bucket_mb, --workers, --eval_every, --steps_per_epoch.
+
+Deliberate fixes of reference quirks: the sampler's epoch is advanced every epoch;
+evaluation runs on the unwrapped module (no stray rank-0-only collective, K8) with a non-augmenting
+test transform; checkpoints are written by GLOBAL rank 0 only; the per-step loss stays on the
+device (one host sync per epoch instead of one per step).
+"""
+from __future__ import annotations
+
+import argparse
+import os
+import random
+import time
+
+import numpy as np
+import torch
+from torch.utils.data import DataLoader
+
+from .. import parallel
+from ..data import CIFAR10, CifarTransform, DistributedSampler, SyntheticImages
+from ..models import ARCHS
+from ..ops import CrossEntropyLoss, top1_correct
+from ..optim import SGD
+from ..utils.checkpoint import load_checkpoint, save_checkpoint
+
+
+def build_argparser(variant: str = "main") -> argparse.ArgumentParser:
+    p = argparse.ArgumentParser(formatter_class=argparse.ArgumentDefaultsHelpFormatter)
+    p.add_argument("--num_epochs", type=int, help="Number of training epochs.", default=100)
+    p.add_argument("--batch_size", type=int, help="Training batch size for one process.",
+                   default=128 if variant == "main" else 32)
+    p.add_argument("--learning_rate", type=float, help="Learning rate.", default=0.1)
+    p.add_argument("--random_seed", type=int, help="Random seed.", default=0)
+    p.add_argument("--model_dir", type=str, help="Directory for saving models.", default="saved_models")
+    p.add_argument("--model_filename", type=str, help="Model filename.", default="resnet_distributed.pth")
+    p.add_argument("--resume", action="store_true", help="Resume training from saved checkpoint.")
+    # additions
+    p.add_argument("--arch", default="resnet18", choices=sorted(ARCHS))
+    p.add_argument("--num_classes", type=int, default=10)
+    p.add_argument("--synthetic", action="store_true", help="random data instead of CIFAR-10")
+    p.add_argument("--synthetic_size", type=int, default=1024, help="images per epoch (synthetic)")
+    p.add_argument("--data_root", default="./data")
+    p.add_argument("--image_size", type=int, default=32)
+    p.add_argument("--backend", default="nccl", help="nccl|rccl (GPU, RCCL) or gloo (CPU)")
+    p.add_argument("--device", default="auto", help="auto | cpu | cuda")
+    p.add_argument("--bucket_mb", type=float, default=None)
+    p.add_argument("--workers", type=int, default=8 if variant != "main" else 15)
+    p.add_argument("--eval_every", type=int, default=10)
+    p.add_argument("--test_batch_size", type=int, default=None if variant == "main" else 128)
+    p.add_argument("--steps_per_epoch", type=int, default=0, help="cap steps per epoch (0 = full epoch)")
+    p.add_argument("--eval_before_train", action="store_true", default=variant != "main",
+                   help="resnet.py variant: evaluate/save before training on eval epochs")
+    return p
+
+
+def set_random_seeds(seed: int):
+    torch.manual_seed(seed)
+    np.random.seed(seed)
+    random.seed(seed)
+
+
+@torch.no_grad()
+def evaluate(model, device, test_loader) -> float:
+    model.eval()
+    correct = torch.zeros(1, dtype=torch.int64, device=device)
+    total = 0
+    for images, labels in test_loader:
+        images, labels = images.to(device, non_blocking=True), labels.to(device, non_blocking=True)
+        correct += top1_correct(model(images), labels).to(torch.int64)
+        total += labels.size(0)
+    model.train()
+    return correct.item() / max(1, total)
+
+
+def run(args) -> dict:
+    comm = parallel.init_distributed(args.backend)
+    rank, world, local_rank = comm.rank, comm.world_size, comm.local_rank
+    device = comm.device if args.device == "auto" else torch.device(args.device)
+    set_random_seeds(args.random_seed)
+    model = ARCHS[args.arch](num_classes=args.num_classes).to(device)
+    ddp = parallel.DistributedDataParallel(model, bucket_cap_mb=args.bucket_mb)
+    model_filepath = os.path.join(args.model_dir, args.model_filename)
+    if args.resume:
+        load_checkpoint(ddp, model_filepath, map_location=device)
+
+    if args.synthetic:
+        shape = (3, args.image_size, args.image_size)
+        train_set = SyntheticImages(args.synthetic_size, shape, args.num_classes, seed=1)
+        test_set = SyntheticImages(max(64, args.synthetic_size // 8), shape, args.num_classes, seed=2)
+    else:
+        # download=False semantics: the data must already be under data_root (see download.py)
+        train_set = CIFAR10(args.data_root, train=True, transform=CifarTransform(True), seed=args.random_seed + rank)
+        test_set = CIFAR10(args.data_root, train=False, transform=CifarTransform(False))
+    sampler = DistributedSampler(train_set, seed=0)
+    pin = device.type == "cuda"
+    train_loader = DataLoader(train_set, batch_size=args.batch_size, sampler=sampler, num_workers=args.workers,
+                              pin_memory=pin, persistent_workers=args.workers > 0)
+    test_loader = DataLoader(test_set, batch_size=args.test_batch_size or args.batch_size, shuffle=False,
+                             num_workers=args.workers, pin_memory=pin)
+    criterion = CrossEntropyLoss()
+    optimizer = SGD(model.parameters(), lr=args.learning_rate, momentum=0.9, weight_decay=1e-5)
+
+    history = {"loss": [], "accuracy": [], "images_per_sec": []}
+
+    def eval_and_save(epoch):
+        accuracy = evaluate(model, device, test_loader)
+        save_checkpoint(ddp, model_filepath, rank=rank)
+        print("-" * 75)
+        print("Epoch: {}, Accuracy: {}".format(epoch, accuracy))
+        print("-" * 75)
+        history["accuracy"].append(accuracy)
+
+    try:
+        for epoch in range(args.num_epochs):
+            sampler.set_epoch(epoch)
+            if args.eval_before_train and epoch % args.eval_every == 0 and rank == 0:
+                eval_and_save(epoch)
+            print("Local Rank: {}, Epoch: {}, Training ...".format(local_rank, epoch))
+            ddp.train()
+            loss_sum = torch.zeros((), device=device)
+            nb = 0
+            t0 = time.perf_counter()
+            for inputs, labels in train_loader:
+                inputs = inputs.to(device, non_blocking=True)
+                labels = labels.to(device, non_blocking=True)
+                optimizer.zero_grad()
+                loss = criterion(ddp(inputs), labels)
+                loss.backward()
+                optimizer.step()
+                loss_sum += loss.detach()
+                nb += 1
+                if args.steps_per_epoch and nb >= args.steps_per_epoch:
+                    break
+            mean_loss = (loss_sum / max(1, nb)).item()
+            dt = time.perf_counter() - t0
+            history["loss"].append(mean_loss)
+            history["images_per_sec"].append(nb * args.batch_size * world / dt)
+            print("Local Rank: {}, Epoch: {}, Loss: {}".format(local_rank, epoch, mean_loss))
+            if not args.eval_before_train and epoch % args.eval_every == 0 and rank == 0:
+                eval_and_save(epoch)
+            print(f"Epoch {epoch} completed")
+    finally:
+        parallel.destroy_distributed()
+    return history
+
+
+def main(variant="main", argv=None):
+    args = build_argparser(variant).parse_args(argv)
+    return run(args)

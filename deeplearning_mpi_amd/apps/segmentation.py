@@ -1,0 +1,192 @@
+"""UNet data-parallel segmentation training (the reference's pytorch/unet/train.py).
+
+Same flags/defaults (--num_epochs 100, --batch_size 16, --learning_rate 1e-4, --random_seed 42,
+--model_dir saved_models, --model_filename model.pth, --resume), same log file
+(logs/training_log_YYYYmmdd_HHMMSS.log: header, "Started training at", per-epoch
+"Epoch e | Loss: x | Duration: s", every 10 epochs "Epoch e | Dice Score: x", final block) and the
+same Adam + BCEWithLogits + clip_grad_norm_(1.0) step (/root/reference/pytorch/unet/train.py:143-244).
+
+Deliberate fixes: the NaN/Inf skip is collective (decided from the
+all-reduced gradient norm on the device, identical on every rank -> no deadlock, no host sync);
+the log and checkpoints are written by global rank 0 only; evaluation uses the unwrapped module.
+Additions: --synthetic, --image_size, --in_channels, --data_dir, --scale, --up_sample_mode,
+--backend, --device, --max_norm, --steps_per_epoch, --workers.
+"""
+from __future__ import annotations
+
+import argparse
+import os
+import random
+import time
+from datetime import datetime
+
+import numpy as np
+import torch
+from torch.utils.data import DataLoader
+
+from .. import parallel
+from ..data import CarvanaDataset, DistributedSampler, SyntheticMasks
+from ..models import UNet
+from ..ops import BCEWithLogitsLoss, dice_per_sample
+from ..optim import Adam, clip_grad_norm_
+from ..utils.checkpoint import load_checkpoint, save_checkpoint
+
+
+def build_argparser() -> argparse.ArgumentParser:
+    p = argparse.ArgumentParser(formatter_class=argparse.ArgumentDefaultsHelpFormatter)
+    p.add_argument("--num_epochs", type=int, default=100, help="Number of training epochs.")
+    p.add_argument("--batch_size", type=int, default=16, help="Batch size per process.")
+    p.add_argument("--learning_rate", type=float, default=0.0001, help="Learning rate.")
+    p.add_argument("--random_seed", type=int, default=42, help="Seed for reproducibility.")
+    p.add_argument("--model_dir", type=str, default="saved_models", help="Directory to save model.")
+    p.add_argument("--model_filename", type=str, default="model.pth", help="Model filename.")
+    p.add_argument("--resume", action="store_true", help="Resume from a checkpoint.")
+    p.add_argument("--synthetic", action="store_true")
+    p.add_argument("--synthetic_size", type=int, default=64)
+    p.add_argument("--image_size", type=int, default=512)
+    p.add_argument("--in_channels", type=int, default=3)
+    p.add_argument("--data_dir", default="data")
+    p.add_argument("--scale", type=float, default=0.2)
+    p.add_argument("--up_sample_mode", default="conv_transpose", choices=["conv_transpose", "bilinear"])
+    p.add_argument("--backend", default="nccl")
+    p.add_argument("--device", default="auto")
+    p.add_argument("--max_norm", type=float, default=1.0)
+    p.add_argument("--steps_per_epoch", type=int, default=0)
+    p.add_argument("--workers", type=int, default=max(1, (os.cpu_count() or 2) // 2))
+    p.add_argument("--log_dir", default="logs")
+    p.add_argument("--eval_every", type=int, default=10)
+    return p
+
+
+def set_random_seeds(seed):
+    torch.manual_seed(seed)
+    np.random.seed(seed)
+    random.seed(seed)
+
+
+def create_log_file(log_dir="logs") -> str:
+    return os.path.join(log_dir, f"training_log_{datetime.now().strftime('%Y%m%d_%H%M%S')}.log")
+
+
+class RankLog:
+    def __init__(self, path, rank):
+        self.path, self.rank = path, rank
+        if rank == 0 and path:
+            os.makedirs(os.path.dirname(path) or ".", exist_ok=True)
+
+    def __call__(self, msg):
+        if self.rank == 0 and self.path:
+            with open(self.path, "a") as f:
+                f.write(msg + "\n")
+
+
+@torch.no_grad()
+def evaluate_model(model, device, test_loader) -> float:
+    model.eval()
+    scores = []
+    for batch in test_loader:
+        images = batch["image"].to(device, dtype=torch.float32)
+        masks = batch["mask"].to(device, dtype=torch.float32)
+        scores.append(dice_per_sample(model(images), masks))
+    model.train()
+    if not scores:
+        return 0.0
+    return torch.cat(scores).mean().item()
+
+
+def build_data_loaders(args, device):
+    if args.synthetic:
+        ds = SyntheticMasks(args.synthetic_size, (args.in_channels, args.image_size, args.image_size),
+                            seed=args.random_seed)
+    else:
+        ds = CarvanaDataset(images_dir=os.path.join(args.data_dir, "images"),
+                            mask_dir=os.path.join(args.data_dir, "masks"), scale=args.scale)
+    train_size = int(0.8 * len(ds))
+    test_size = len(ds) - train_size
+    # same split on every rank (seeded generator rather than the global RNG)
+    train_ds, test_ds = torch.utils.data.random_split(ds, [train_size, test_size],
+                                                      generator=torch.Generator().manual_seed(args.random_seed))
+    kw = dict(batch_size=args.batch_size, num_workers=args.workers, pin_memory=device.type == "cuda")
+    sampler = DistributedSampler(train_ds)
+    return (DataLoader(train_ds, sampler=sampler, **kw), DataLoader(test_ds, shuffle=False, **kw), sampler)
+
+
+def run(args) -> dict:
+    comm = parallel.init_distributed(args.backend)
+    rank, world, local_rank = comm.rank, comm.world_size, comm.local_rank
+    device = comm.device if args.device == "auto" else torch.device(args.device)
+    set_random_seeds(args.random_seed)
+    log = RankLog(create_log_file(args.log_dir), rank)
+    gpu = torch.cuda.get_device_name(device) if device.type == "cuda" else "cpu"
+    log(f"Batch size: {args.batch_size}")
+    log(f"Number of workers: {os.cpu_count()}")
+    log(f"Learning rate: {args.learning_rate}")
+    log(f"Number of epochs: {args.num_epochs}")
+    log(f"World size: {world}, Local rank: {local_rank}, GPU: {gpu}")
+
+    train_loader, test_loader, sampler = build_data_loaders(args, device)
+    model = UNet(out_classes=1, up_sample_mode=args.up_sample_mode, in_channels=args.in_channels).to(device)
+    ddp = parallel.DistributedDataParallel(model)
+    model_filepath = os.path.join(args.model_dir, args.model_filename)
+    if args.resume:
+        load_checkpoint(ddp, model_filepath, map_location=device)
+    optimizer = Adam(model.parameters(), lr=args.learning_rate)
+    criterion = BCEWithLogitsLoss()
+    history = {"loss": [], "dice": []}
+    if rank == 0:
+        print(f"Logging training progress to: {log.path}")
+    log(f"Started training at {datetime.now()}")
+    try:
+        for epoch in range(args.num_epochs):
+            sampler.set_epoch(epoch)
+            t0 = time.time()
+            ddp.train()
+            loss_sum = torch.zeros((), device=device)
+            nb = 0
+            for batch in train_loader:
+                images = batch["image"].to(device, dtype=torch.float32, non_blocking=True)
+                masks = batch["mask"].to(device, dtype=torch.float32, non_blocking=True)
+                pred = ddp(images).squeeze(1)
+                loss = criterion(pred, masks)
+                optimizer.zero_grad()
+                loss.backward()
+                # collective NaN/Inf guard: a non-finite all-reduced grad norm skips the step on all ranks
+                clip_grad_norm_(model.parameters(), max_norm=args.max_norm, optimizer=optimizer)
+                optimizer.step()
+                loss_sum += torch.nan_to_num(loss.detach(), nan=0.0, posinf=0.0, neginf=0.0)
+                nb += 1
+                if args.steps_per_epoch and nb >= args.steps_per_epoch:
+                    break
+            avg_loss = (loss_sum / max(1, nb)).item()
+            history["loss"].append(avg_loss)
+            print(f"Epoch {epoch + 1} finished with loss: {avg_loss:.4f}")
+            log(f"Epoch {epoch + 1} | Loss: {avg_loss:.4f} | Duration: {time.time() - t0:.2f}s")
+            if (epoch + 1) % args.eval_every == 0 and rank == 0:
+                dice = evaluate_model(model, device, test_loader)
+                save_checkpoint(ddp, model_filepath, rank=rank)
+                print("-" * 75)
+                print(f"Epoch {epoch + 1} Dice Score: {dice:.4f}")
+                print("-" * 75)
+                log(f"Epoch {epoch + 1} | Dice Score: {dice:.4f}")
+                history["dice"].append(dice)
+        if rank == 0:
+            print("\n" + "=" * 80 + "\nTRAINING COMPLETED - FINAL EVALUATION\n" + "=" * 80)
+            final = evaluate_model(model, device, test_loader)
+            save_checkpoint(ddp, model_filepath, rank=rank)
+            print(f"FINAL DICE COEFFICIENT: {final:.4f}\n" + "=" * 80 + "\n")
+            log("=" * 80)
+            log("FINAL TRAINING RESULTS")
+            log("=" * 80)
+            log(f"TRAINING COMPLETED | Final Dice Coefficient: {final:.4f} | Training finished at: {datetime.now()}")
+            log(f"Total training epochs: {args.num_epochs}")
+            log(f"Final learning rate: {args.learning_rate}")
+            log(f"Model saved to: {model_filepath}")
+            log("=" * 80)
+            history["final_dice"] = final
+    finally:
+        parallel.destroy_distributed()
+    return history
+
+
+def main(argv=None):
+    return run(build_argparser().parse_args(argv))

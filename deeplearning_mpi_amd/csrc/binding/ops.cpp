@@ -227,8 +227,10 @@ void conv2d_wgrad(const at::Tensor& dy, int lddy, int dyoff, int Ko, const at::T
   a.mtiles = ceil_div(Ko, bm);
   a.ntiles = ceil_div(a.TC, 128);
   const int tiles = a.mtiles * a.ntiles;
-  const int maxsplit = std::max(1, ceil_div(a.npix, 64));
-  int splits = std::max(1, std::min(maxsplit, ceil_div(2048, tiles)));
+  // split the pixel reduction so the grid covers the chip ~4 blocks deep, but keep each split at
+  // least 8 K-steps (512 pixels) so the fp32 slab traffic stays small next to the MFMA work
+  const int maxsplit = std::max(1, ceil_div(a.npix, 512));
+  int splits = std::max(1, std::min(maxsplit, ceil_div(1024, tiles)));
   int pps = ceil_div(a.npix, splits);
   pps = ceil_div(pps, 64) * 64;
   splits = ceil_div(a.npix, pps);
@@ -238,11 +240,18 @@ void conv2d_wgrad(const at::Tensor& dy, int lddy, int dyoff, int Ko, const at::T
   a.fdQ = make_fastdiv((uint32_t)Q);
   a.fdC = make_fastdiv((uint32_t)C);
   a.fdS = make_fastdiv((uint32_t)S);
-  at::Tensor ws = at::empty({(int64_t)splits * Ko * a.TC}, dy.options().dtype(at::kFloat));
+  const int64_t wsz = (int64_t)Ko * a.TC;
+  const int G = splits > 1 ? dlmpi_wgrad_reduce_groups(splits, wsz) : 0;
+  at::Tensor ws = at::empty({(int64_t)(splits + G) * wsz}, dy.options().dtype(at::kFloat));
   a.ws = ptr<float>(ws);
   check(dlmpi_conv_wgrad(&a, bm, cur_stream()), "conv2d_wgrad");
-  check(dlmpi_wgrad_reduce(a.ws, splits, Ko, R * S, C, Creal, Ko_real, ptr<float>(grad), cur_stream()),
+  check(dlmpi_wgrad_reduce(a.ws, splits, Ko, R * S, C, Creal, Ko_real, ptr<float>(grad), a.ws + (int64_t)splits * wsz,
+                           (int)std::min<int64_t>(INT32_MAX, (int64_t)G * wsz), cur_stream()),
         "wgrad_reduce");
+}
+
+static at::Tensor colsum_ws(const at::Tensor& like, int T, int C) {
+  return at::empty({(int64_t)dlmpi_colsum_ws_doubles(T, C)}, like.options().dtype(at::kDouble));
 }
 
 // --------------------------------- batch norm ----------------------------------------------
@@ -251,10 +260,11 @@ void bn_finalize(const at::Tensor& partial, int ntiles, int C, double count, con
                  const c10::optional<at::Tensor>& running_var, double momentum, double eps, at::Tensor scale,
                  at::Tensor shift, const c10::optional<at::Tensor>& save_mean,
                  const c10::optional<at::Tensor>& save_invstd) {
+  at::Tensor ws = colsum_ws(partial, ntiles, C);
   check(dlmpi_bn_finalize(ptr<float>(partial), ntiles, C, count, optr<float>(gamma), optr<float>(beta),
                           optr<float>(running_mean), optr<float>(running_var), (float)momentum, (float)eps,
                           ptr<float>(scale), ptr<float>(shift), optr<float>(save_mean), optr<float>(save_invstd),
-                          cur_stream()),
+                          ptr<double>(ws), cur_stream()),
         "bn_finalize");
 }
 
@@ -286,9 +296,10 @@ void bn_bwd_finalize(const at::Tensor& partial, int nblk, int C, double count, c
                      const c10::optional<at::Tensor>& mean, const c10::optional<at::Tensor>& invstd,
                      const c10::optional<at::Tensor>& dgamma, const c10::optional<at::Tensor>& dbeta,
                      const c10::optional<at::Tensor>& coef) {
+  at::Tensor ws = colsum_ws(partial, nblk, C);
   check(dlmpi_bn_bwd_finalize(ptr<float>(partial), nblk, C, count, optr<float>(gamma), optr<float>(mean),
                               optr<float>(invstd), optr<float>(dgamma), optr<float>(dbeta), optr<float>(coef),
-                              cur_stream()),
+                              ptr<double>(ws), cur_stream()),
         "bn_bwd_finalize");
 }
 
@@ -303,8 +314,9 @@ void bn_bwd_apply(const at::Tensor& dy, int lddy, int dyoff, const c10::optional
 void channel_sum(const at::Tensor& x, int64_t M, int C, int ldx, int xoff, at::Tensor out_acc) {
   const int nblk = dlmpi_reduce_blocks(M, C);
   at::Tensor partial = at::empty({(int64_t)nblk * 2 * C}, x.options().dtype(at::kFloat));
+  at::Tensor ws = colsum_ws(partial, nblk, C);
   check(dlmpi_channel_sum(ptr<uint16_t>(x), M, C, ldx, xoff, ptr<float>(out_acc), ptr<float>(partial), nblk,
-                          cur_stream()),
+                          ptr<double>(ws), cur_stream()),
         "channel_sum");
 }
 

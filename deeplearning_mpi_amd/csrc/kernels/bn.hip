@@ -65,26 +65,58 @@ __global__ __launch_bounds__(256) void bn_stats_kernel(const uint16_t* __restric
   block_combine<2>(acc, rm, C, partial);
 }
 
-__global__ __launch_bounds__(256) void bn_finalize_kernel(const float* __restrict__ partial, int ntiles, int C,
+// Stage 1 of every per-channel column reduction over [T][2][C] fp32 partials:
+// dpart[s][k][c] = sum of partial[t][k][c] over row slice s (double).  Grid (ceil(C/64), S) so the
+// whole chip works on it (the partial tensors are up to 6272 x 2 x 2048); fixed summation order.
+__global__ __launch_bounds__(256) void colsum2_kernel(const float* __restrict__ partial, int T, int C,
+                                                      double* __restrict__ dpart) {
+  __shared__ double r[2][4][64];
+  const int lc = threadIdx.x & 63, rl = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + lc;
+  const int S = gridDim.y, s = blockIdx.y;
+  const int per = (T + S - 1) / S;
+  const int t0 = s * per, t1 = min(T, t0 + per);
+  double a = 0.0, b = 0.0;
+  if (c < C) {
+    for (int t = t0 + rl; t < t1; t += 4) {
+      a += (double)partial[(int64_t)t * 2 * C + c];
+      b += (double)partial[(int64_t)t * 2 * C + C + c];
+    }
+  }
+  r[0][rl][lc] = a;
+  r[1][rl][lc] = b;
+  __syncthreads();
+  if (rl == 0 && c < C) {
+    for (int g = 1; g < 4; ++g) { a += r[0][g][lc]; b += r[1][g][lc]; }
+    dpart[(int64_t)s * 2 * C + c] = a;
+    dpart[(int64_t)s * 2 * C + C + c] = b;
+  }
+}
+
+__device__ __forceinline__ void colsum2_final(const double* __restrict__ dpart, int S, int C, int c, double& s1,
+                                              double& s2) {
+  s1 = 0.0;
+  s2 = 0.0;
+  for (int s = 0; s < S; ++s) {
+    s1 += dpart[(int64_t)s * 2 * C + c];
+    s2 += dpart[(int64_t)s * 2 * C + C + c];
+  }
+}
+
+static inline int colsum_slices(int T) {
+  int S = (T + 31) / 32;
+  return S < 1 ? 1 : (S > 64 ? 64 : S);
+}
+
+__global__ __launch_bounds__(256) void bn_finalize_kernel(const double* __restrict__ dpart, int S, int C,
                                                           double count, const float* gamma, const float* beta,
                                                           float* running_mean, float* running_var, float momentum,
                                                           float eps, float* scale, float* shift, float* save_mean,
                                                           float* save_invstd) {
-  __shared__ double r1[8][32], r2[8][32];
-  const int lc = threadIdx.x & 31, rg = threadIdx.x >> 5;
-  const int c = blockIdx.x * 32 + lc;
-  double s1 = 0.0, s2 = 0.0;
+  const int c = blockIdx.x * 256 + threadIdx.x;
   if (c < C) {
-    for (int t = rg; t < ntiles; t += 8) {
-      s1 += (double)partial[(int64_t)t * 2 * C + c];
-      s2 += (double)partial[(int64_t)t * 2 * C + C + c];
-    }
-  }
-  r1[rg][lc] = s1;
-  r2[rg][lc] = s2;
-  __syncthreads();
-  if (rg == 0 && c < C) {
-    for (int g = 1; g < 8; ++g) { s1 += r1[g][lc]; s2 += r2[g][lc]; }
+    double s1, s2;
+    colsum2_final(dpart, S, C, c, s1, s2);
     const double mean = s1 / count;
     double var = s2 / count - mean * mean;
     if (var < 0.0) var = 0.0;
@@ -187,26 +219,15 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const uint16_t* __re
 
 // Reduces the bwd partials; accumulates dgamma/dbeta into the gradient buffers; emits
 // coef[0..2][C] = (k1, k2, k3) with dx = k1*dyr + k2*x + k3.
-__global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(const float* __restrict__ partial, int nblk, int C,
+__global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(const double* __restrict__ dpart, int S, int C,
                                                               double count, const float* gamma,
                                                               const float* __restrict__ mean,
                                                               const float* __restrict__ invstd, float* dgamma,
                                                               float* dbeta, float* coef) {
-  __shared__ double r1[8][32], r2[8][32];
-  const int lc = threadIdx.x & 31, rg = threadIdx.x >> 5;
-  const int c = blockIdx.x * 32 + lc;
-  double s1 = 0.0, s2 = 0.0;
+  const int c = blockIdx.x * 256 + threadIdx.x;
   if (c < C) {
-    for (int t = rg; t < nblk; t += 8) {
-      s1 += (double)partial[(int64_t)t * 2 * C + c];
-      s2 += (double)partial[(int64_t)t * 2 * C + C + c];
-    }
-  }
-  r1[rg][lc] = s1;
-  r2[rg][lc] = s2;
-  __syncthreads();
-  if (rg == 0 && c < C) {
-    for (int g = 1; g < 8; ++g) { s1 += r1[g][lc]; s2 += r2[g][lc]; }
+    double s1, s2;
+    colsum2_final(dpart, S, C, c, s1, s2);
     if (dbeta) dbeta[c] += (float)s1;
     if (dgamma) dgamma[c] += (float)s2;
     if (coef) {
@@ -284,11 +305,15 @@ extern "C" hipError_t dlmpi_bn_stats(const uint16_t* x, int64_t M, int C, int ld
   return hipGetLastError();
 }
 
+extern "C" int dlmpi_colsum_ws_doubles(int T, int C) { return colsum_slices(T) * 2 * C; }
+
 extern "C" hipError_t dlmpi_bn_finalize(const float* partial, int ntiles, int C, double count, const float* gamma,
                                         const float* beta, float* running_mean, float* running_var, float momentum,
                                         float eps, float* scale, float* shift, float* save_mean, float* save_invstd,
-                                        hipStream_t s) {
-  hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 31) / 32), dim3(256), 0, s, partial, ntiles, C, count, gamma, beta,
+                                        double* ws, hipStream_t s) {
+  const int S = colsum_slices(ntiles);
+  hipLaunchKernelGGL(colsum2_kernel, dim3((C + 63) / 64, S), dim3(256), 0, s, partial, ntiles, C, ws);
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, s, ws, S, C, count, gamma, beta,
                      running_mean, running_var, momentum, eps, scale, shift, save_mean, save_invstd);
   return hipGetLastError();
 }
@@ -315,9 +340,11 @@ extern "C" hipError_t dlmpi_bn_bwd_reduce(const uint16_t* dy, int lddy, int dyof
 
 extern "C" hipError_t dlmpi_bn_bwd_finalize(const float* partial, int nblk, int C, double count, const float* gamma,
                                             const float* mean, const float* invstd, float* dgamma, float* dbeta,
-                                            float* coef, hipStream_t s) {
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 31) / 32), dim3(256), 0, s, partial, nblk, C, count, gamma,
-                     mean, invstd, dgamma, dbeta, coef);
+                                            float* coef, double* ws, hipStream_t s) {
+  const int S = colsum_slices(nblk);
+  hipLaunchKernelGGL(colsum2_kernel, dim3((C + 63) / 64, S), dim3(256), 0, s, partial, nblk, C, ws);
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, s, ws, S, C, count, gamma, mean,
+                     invstd, dgamma, dbeta, coef);
   return hipGetLastError();
 }
 
@@ -332,9 +359,10 @@ extern "C" hipError_t dlmpi_bn_bwd_apply(const uint16_t* dy, int lddy, int dyoff
 }
 
 extern "C" hipError_t dlmpi_channel_sum(const uint16_t* x, int64_t M, int C, int ldx, int xoff, float* out_acc,
-                                        float* partial, int nblk, hipStream_t s) {
+                                        float* partial, int nblk, double* ws, hipStream_t s) {
   hipError_t e = dlmpi_bn_bwd_reduce(x, ldx, xoff, nullptr, 0, 0, nullptr, 0, 0, M, C, nullptr, nullptr, partial,
                                      nblk, s);
   if (e != hipSuccess) return e;
-  return dlmpi_bn_bwd_finalize(partial, nblk, C, (double)M, nullptr, nullptr, nullptr, nullptr, out_acc, nullptr, s);
+  return dlmpi_bn_bwd_finalize(partial, nblk, C, (double)M, nullptr, nullptr, nullptr, nullptr, out_acc, nullptr, ws,
+                               s);
 }

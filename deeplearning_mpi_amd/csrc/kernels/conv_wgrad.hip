@@ -172,12 +172,26 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(const WgradArgs a) {
     }
 }
 
-// out[ko][t][c] += sum_z ws[z][ko][t][c] for c < Creal, ko < Ko_real (fixed summation order).
-__global__ void wgrad_reduce_kernel(const float* __restrict__ ws, int splits, int Ko, int T, int Cpad, int Creal,
-                                    int Ko_real, float* __restrict__ out) {
+// Split reduction, stage 1: grid (ceil(total/1024), G): block (x, g) sums split slabs
+// [g*per, (g+1)*per) for 1024 consecutive outputs (4 per thread, 16-byte loads) -> ws2[g][idx].
+__global__ __launch_bounds__(256) void wgrad_reduce_stage1(const float* __restrict__ ws, int splits, int64_t total,
+                                                           float* __restrict__ ws2) {
+  const int G = gridDim.y, g = blockIdx.y;
+  const int per = (splits + G - 1) / G;
+  const int z0 = g * per, z1 = min(splits, z0 + per);
+  const int64_t i4 = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) * 4;
+  if (i4 >= total) return;
+  f32x4 s = {0.f, 0.f, 0.f, 0.f};
+  for (int z = z0; z < z1; ++z) s += *reinterpret_cast<const f32x4*>(ws + (int64_t)z * total + i4);
+  *reinterpret_cast<f32x4*>(ws2 + (int64_t)g * total + i4) = s;
+}
+
+// Stage 2: out[ko][t][c] += sum_g src[g][ko][t][c] for c < Creal, ko < Ko_real (fixed order).
+__global__ __launch_bounds__(256) void wgrad_reduce_stage2(const float* __restrict__ src, int G, int Ko, int T,
+                                                           int Cpad, int Creal, int Ko_real, float* __restrict__ out) {
   const int64_t TC = (int64_t)T * Cpad;
   const int64_t total = (int64_t)Ko_real * TC;
-  const int64_t zstride = (int64_t)Ko * TC;
+  const int64_t gstride = (int64_t)Ko * TC;
   for (int64_t idx = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; idx < total;
        idx += (int64_t)gridDim.x * blockDim.x) {
     const int64_t ko = idx / TC;
@@ -186,9 +200,17 @@ __global__ void wgrad_reduce_kernel(const float* __restrict__ ws, int splits, in
     const int c = (int)(rem - tt * Cpad);
     if (c >= Creal) continue;
     float s = 0.f;
-    for (int zz = 0; zz < splits; ++zz) s += ws[zz * zstride + idx];
+    for (int g = 0; g < G; ++g) s += src[g * gstride + idx];
     out[(ko * T + tt) * Creal + c] += s;
   }
+}
+
+static inline int reduce_groups(int splits, int64_t total) {
+  const int64_t xb = (total / 4 + 255) / 256;
+  int64_t G = (1024 + xb - 1) / xb;   // aim at >= 1024 blocks in stage 1
+  if (G > splits) G = splits;
+  if (G > 64) G = 64;
+  return (int)(G < 1 ? 1 : G);
 }
 
 }  // namespace dlmpi
@@ -204,13 +226,26 @@ extern "C" hipError_t dlmpi_conv_wgrad(const WgradArgs* a, int bm, hipStream_t s
   return hipGetLastError();
 }
 
+extern "C" int dlmpi_wgrad_reduce_groups(int splits, int64_t total) { return reduce_groups(splits, total); }
+
+// ws2 must hold reduce_groups(splits, Ko*T*Cpad) * Ko*T*Cpad floats (total % 4 == 0 since Cpad % 8 == 0).
 extern "C" hipError_t dlmpi_wgrad_reduce(const float* ws, int splits, int Ko, int T, int Cpad, int Creal, int Ko_real,
-                                         float* out, hipStream_t s) {
-  const int64_t total = (int64_t)Ko_real * T * Cpad;
-  if (total == 0) return hipSuccess;
-  int64_t blocks = (total + 255) / 256;
-  if (blocks > 4096) blocks = 4096;
-  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)blocks), dim3(256), 0, s, ws, splits, Ko, T, Cpad, Creal,
-                     Ko_real, out);
+                                         float* out, float* ws2, int ws2_floats, hipStream_t s) {
+  const int64_t total = (int64_t)Ko * T * Cpad;
+  if (total == 0 || Ko_real == 0) return hipSuccess;
+  const int G = reduce_groups(splits, total);
+  if ((int64_t)G * total > (int64_t)ws2_floats) return hipErrorInvalidValue;
+  const float* src = ws;
+  int Gs = splits;
+  if (splits > 1) {
+    hipLaunchKernelGGL(wgrad_reduce_stage1, dim3((unsigned)((total / 4 + 255) / 256), G), dim3(256), 0, s, ws, splits,
+                       total, ws2);
+    src = ws2;
+    Gs = G;
+  }
+  int64_t blocks = ((int64_t)Ko_real * T * Cpad + 255) / 256;
+  if (blocks > 8192) blocks = 8192;
+  hipLaunchKernelGGL(wgrad_reduce_stage2, dim3((unsigned)blocks), dim3(256), 0, s, src, Gs, Ko, T, Cpad, Creal, Ko_real,
+                     out);
   return hipGetLastError();
 }

@@ -93,13 +93,15 @@ hipError_t dlmpi_conv_igemm(const dlmpi::ConvArgs* a, int bm, int bn, hipStream_
 hipError_t dlmpi_conv_wgrad(const dlmpi::WgradArgs* a, int bm, hipStream_t s);
 // sum of split partials -> grad (accumulated), with channel un-padding and row limit
 hipError_t dlmpi_wgrad_reduce(const float* ws, int splits, int Ko, int T, int Cpad, int Creal,
-                              int Ko_real, float* out, hipStream_t s);
+                              int Ko_real, float* out, float* ws2, int ws2_floats, hipStream_t s);
+int dlmpi_wgrad_reduce_groups(int splits, int64_t total);
 
 // batch norm
 hipError_t dlmpi_bn_finalize(const float* partial, int ntiles, int C, double count, const float* gamma,
                              const float* beta, float* running_mean, float* running_var, float momentum,
                              float eps, float* scale, float* shift, float* save_mean, float* save_invstd,
-                             hipStream_t s);
+                             double* ws, hipStream_t s);
+int dlmpi_colsum_ws_doubles(int T, int C);
 hipError_t dlmpi_bn_stats(const uint16_t* x, int64_t M, int C, int ldx, int xoff, float* partial, int nblk,
                           hipStream_t s);
 hipError_t dlmpi_bn_apply(const uint16_t* x, int ldx, int xoff, int64_t M, int C, const float* scale,
@@ -110,12 +112,12 @@ hipError_t dlmpi_bn_bwd_reduce(const uint16_t* dy, int lddy, int dyoff, const ui
                                const float* invstd, float* partial, int nblk, hipStream_t s);
 hipError_t dlmpi_bn_bwd_finalize(const float* partial, int nblk, int C, double count, const float* gamma,
                                  const float* mean, const float* invstd, float* dgamma, float* dbeta,
-                                 float* coef, hipStream_t s);
+                                 float* coef, double* ws, hipStream_t s);
 hipError_t dlmpi_bn_bwd_apply(const uint16_t* dy, int lddy, int dyoff, const uint16_t* ymask, int ldym, int ymoff,
                               const uint16_t* x, int ldx, int xoff, int64_t M, int C, const float* coef,
                               uint16_t* dx, uint16_t* dyr_out, hipStream_t s);
 hipError_t dlmpi_channel_sum(const uint16_t* x, int64_t M, int C, int ldx, int xoff, float* out_acc, float* partial,
-                             int nblk, hipStream_t s);
+                             int nblk, double* ws, hipStream_t s);
 int dlmpi_reduce_blocks(int64_t M, int C);
 
 // pooling / layout

@@ -22,7 +22,7 @@ from __future__ import annotations
 import torch
 import torch.nn as nn
 
-from ..ops.act import Act, pad8
+from ..ops.act import Act, padc
 from ..ops.backend import make_backend
 from ..utils.arena import ParamArena
 
@@ -43,8 +43,8 @@ class ConvUnit:
             assert conv.stride[0] == conv.stride[1] and conv.padding[0] == conv.padding[1]
             assert conv.dilation == (1, 1) and conv.groups == 1
             self.stride, self.pad = conv.stride[0], conv.padding[0]
-        self.Cp = cin_pad or pad8(self.Cin)
-        self.Kp = pad8(self.K)
+        self.Cp = cin_pad or padc(self.Cin)
+        self.Kp = padc(self.K)
         R, S, K, C = self.R, self.S, self.K, self.Cin
         if self.linear:   # weight [K, C]
             self.h_fwd = arena.add_compute(w, (self.Kp, 1, 1, self.Cp), (K, 1, 1, C), (0, None, None, 1))
@@ -66,7 +66,7 @@ class ConvUnit:
         if self.Kp == self.K:
             return self.bias.data
         if self._bias_pad is None or self._bias_pad.device != self.bias.device:
-            self._bias_pad = torch.zeros(self.Kp, dtype=torch.float32, device=self.bias.device)
+            self._bias_pad = torch.zeros(self.Kp, dtype=self.bias.dtype, device=self.bias.device)
         self._bias_pad[:self.K].copy_(self.bias.data)
         return self._bias_pad
 
@@ -85,9 +85,9 @@ class ConvUnit:
         if train:
             z = Act.empty(N, P, Q, self.Kp, be.act_dtype, dev)
             mt = be.conv_mtiles(N, x.H, x.W, self.Kp, self.R, self.S, self.stride, self.pad)
-            stats = torch.empty(mt, 2, self.Kp, dtype=torch.float32, device=dev)
+            stats = torch.empty(mt, 2, self.Kp, dtype=be.dt, device=dev)
             be.conv_fwd(x, wf, self.Kp, self.R, self.S, self.stride, self.pad, z, bias=self._bias_vec(), stats=stats)
-            vec = torch.empty(4, self.Kp, dtype=torch.float32, device=dev)
+            vec = torch.empty(4, self.Kp, dtype=be.dt, device=dev)
             scale, shift, mean, invstd = vec[0], vec[1], vec[2], vec[3]
             mom = bn.momentum
             if mom is None:   # cumulative moving average
@@ -133,7 +133,7 @@ class ConvUnit:
                 if self.Kp == self.K:
                     be.channel_sum(dz, ar.grad_flat(self.bias))
                 else:
-                    tmp = torch.zeros(self.Kp, dtype=torch.float32, device=dz.device)
+                    tmp = torch.zeros(self.Kp, dtype=be.dt, device=dz.device)
                     be.channel_sum(dz, tmp)
                     ar.grad_flat(self.bias).add_(tmp[:self.K])
                 ar.ready(self.bias)
@@ -154,7 +154,7 @@ class ConvTUnit:
         Ci, Co, kh, kw = convT.weight.shape
         assert (kh, kw) == (2, 2) and convT.stride == (2, 2) and convT.padding == (0, 0)
         self.Cin, self.Cout = Ci, Co
-        self.Cip, self.Cop = pad8(Ci), pad8(Co)
+        self.Cip, self.Cop = padc(Ci), padc(Co)
         w = convT.weight
         # forward layout [Cout][i][j][Cin]; data-grad layout [Cin][i][j][Cout] (a stride-2 2x2 conv)
         self.h_fwd = arena.add_compute(w, (self.Cop, 2, 2, self.Cip), (Co, 2, 2, Ci), (1, 2, 3, 0))
@@ -211,7 +211,7 @@ class EngineModule(nn.Module):
         device = torch.device(device)
         if self._arena is not None and self._arena.device == device and self._arena.valid():
             return self._arena
-        self._be = make_backend(device)
+        self._be = make_backend(device, next(self.parameters()).dtype)
         self._arena = ParamArena(self, device, self._be)
         self._build_units(self._arena)
         self._arena.refresh(force=True)

@@ -16,7 +16,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from ..ops.act import Act, pad8
+from ..ops.act import Act, padc
 from .engine import ConvUnit, EngineModule
 
 
@@ -166,7 +166,7 @@ class ResNet(EngineModule):
 
     # ------------------------------------------------------------------ engine
     def _build_units(self, ar):
-        self.cin_pad = pad8(self.in_channels)
+        self.cin_pad = padc(self.in_channels)
         self.u_stem = ConvUnit(ar, self.conv1, self.bn1, relu=True, cin_pad=self.cin_pad, need_dgrad=False)
         self.blocks = []
         for layer in (self.layer1, self.layer2, self.layer3, self.layer4):
@@ -190,7 +190,7 @@ class ResNet(EngineModule):
         pooled = Act.empty(N, 1, 1, a.C, be.act_dtype, x.device)
         be.avgpool_fwd(a, pooled)
         K = self.fc.out_features
-        logits = torch.empty(N, K, dtype=torch.float32, device=x.device)
+        logits = torch.empty(N, K, dtype=be.dt, device=x.device)
         la = Act(logits, N, 1, 1, K)
         _, cf = self.u_fc.fwd(be, pooled, train, out=la, save=save)
         state = (cs, h, p, idx, st_blocks, a, pooled, cf) if save else None

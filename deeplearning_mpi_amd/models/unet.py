@@ -19,7 +19,7 @@ from __future__ import annotations
 import torch
 import torch.nn as nn
 
-from ..ops.act import Act, pad8
+from ..ops.act import Act, padc
 from .engine import ConvTUnit, ConvUnit, EngineModule
 
 
@@ -105,7 +105,7 @@ class UNet(EngineModule):
 
     # ------------------------------------------------------------------ engine
     def _build_units(self, ar):
-        self.cin_pad = pad8(self.in_channels)
+        self.cin_pad = padc(self.in_channels)
         downs = [self.down_conv1, self.down_conv2, self.down_conv3, self.down_conv4]
         ups = [self.up_conv1, self.up_conv2, self.up_conv3, self.up_conv4]   # level 1..4
         self.enc = [d.double_conv.units(ar, cin_pad=self.cin_pad if k == 0 else None, need_dgrad=k != 0)
@@ -157,7 +157,7 @@ class UNet(EngineModule):
             a, cb = ub.fwd(be, t, train, save=save)
             ctx_dec[k] = (below, ca, cb)
         K = self.out_classes
-        out = torch.empty(N, H, W, K, dtype=torch.float32, device=dev)
+        out = torch.empty(N, H, W, K, dtype=be.dt, device=dev)
         _, cl = self.u_last.fwd(be, a, train, out=Act(out.view(N * H * W, K), N, H, W, K), save=save)
         logits = out.permute(0, 3, 1, 2)
         state = (cats, ctx_enc, idxs, skips, (cba, cbb), ctx_dec, cl) if save else None

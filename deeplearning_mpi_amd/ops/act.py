@@ -59,3 +59,12 @@ class Act:
 
 def pad8(c: int) -> int:
     return (c + 7) // 8 * 8
+
+
+def padc(c: int) -> int:
+    """Compute-layout channel count: the GEMM kernels reduce 64 channels per step, so channel
+    counts are 8, 16, 32 or a multiple of 64 (zero padded)."""
+    for v in (8, 16, 32):
+        if c <= v:
+            return v
+    return (c + 63) // 64 * 64

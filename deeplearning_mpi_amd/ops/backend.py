@@ -21,6 +21,7 @@ from .act import Act
 class NativeBackend:
     name = "native"
     act_dtype = torch.bfloat16
+    dt = torch.float32
 
     def __init__(self, device):
         from .._ext import native
@@ -106,7 +107,7 @@ class NativeBackend:
 
     def nchw_to_nhwc(self, x: torch.Tensor, Cpad) -> Act:
         N, Cc, H, W = x.shape
-        x = x.contiguous().float()
+        x = x.contiguous().to(self.dt)
         y = Act.empty(N, H, W, Cpad, torch.bfloat16, x.device)
         self.C.nchw_to_nhwc(x, N, Cc, H, W, Cpad, y.buf)
         return y
@@ -130,7 +131,7 @@ class NativeBackend:
             for (src, doff, d, v, st) in entries:
                 blob += struct.pack("<QQ4i4i4qq", src.data_ptr(), base + 2 * doff, *d, *v, *st, doff)
                 start += d[0] * d[1] * d[2] * d[3]
-            dev = torch.frombuffer(bytes(blob), dtype=torch.uint8).to(self.device)
+            dev = torch.frombuffer(bytearray(blob), dtype=torch.uint8).to(self.device)
             self._cast_cache[key] = ent = (entries, dev)
         self.C.cast_weights(ent[1], len(entries), int(total))
 
@@ -189,10 +190,11 @@ class RefBackend:
     """fp32 torch reference with identical semantics (CPU tests / numerics oracle)."""
 
     name = "ref"
-    act_dtype = torch.float32
 
-    def __init__(self, device="cpu"):
+    def __init__(self, device="cpu", dtype=torch.float32):
         self.device = torch.device(device)
+        self.dt = dtype            # float64 turns the whole engine into an fp64 oracle run
+        self.act_dtype = dtype
 
     @staticmethod
     def _store(y: Act, v_nchw):
@@ -203,8 +205,8 @@ class RefBackend:
 
     def conv_fwd(self, x: Act, w, K, R, S, stride, pad, y: Act, bias=None, res=None, scale=None, shift=None,
                  relu=False, stats=None, kvalid=0):
-        wk = w.view(K, R, S, x.C).permute(0, 3, 1, 2).float()
-        out = F.conv2d(x.nchw().float(), wk, None, stride, pad)
+        wk = w.view(K, R, S, x.C).permute(0, 3, 1, 2).to(self.dt)
+        out = F.conv2d(x.nchw().to(self.dt), wk, None, stride, pad)
         if bias is not None:
             out = out + bias.view(1, -1, 1, 1)
         if stats is not None:
@@ -213,28 +215,28 @@ class RefBackend:
         if scale is not None:
             out = out * scale.view(1, -1, 1, 1) + shift.view(1, -1, 1, 1)
         if res is not None:
-            out = out + res.nchw().float()
+            out = out + res.nchw().to(self.dt)
         if relu:
             out = F.relu(out)
         self._store(y, out)
 
     def conv_dgrad(self, dy: Act, wT, C, R, S, stride, pad, dx: Act, res=None):
         K = dy.C
-        wk = wT.view(C, R, S, K).permute(3, 0, 1, 2).float()
-        g = torch.nn.grad.conv2d_input((dx.N, C, dx.H, dx.W), wk, dy.nchw().float(), stride, pad)
+        wk = wT.view(C, R, S, K).permute(3, 0, 1, 2).to(self.dt)
+        g = torch.nn.grad.conv2d_input((dx.N, C, dx.H, dx.W), wk, dy.nchw().to(self.dt), stride, pad)
         if res is not None:
-            g = g + res.nchw().float()
+            g = g + res.nchw().to(self.dt)
         self._store(dx, g)
 
     def convT_fwd(self, x: Act, wf, Cout, y: Act, bias=None):
         Cin = x.C
-        wk = wf.view(Cout, 2, 2, Cin).permute(3, 0, 1, 2).float()
-        out = F.conv_transpose2d(x.nchw().float(), wk, bias, stride=2)
+        wk = wf.view(Cout, 2, 2, Cin).permute(3, 0, 1, 2).to(self.dt)
+        out = F.conv_transpose2d(x.nchw().to(self.dt), wk, bias, stride=2)
         self._store(y, out)
 
     def conv_wgrad(self, dy: Act, x: Act, R, S, stride, pad, grad, Creal, Ko_real):
         Ko, Cc = dy.C, x.C
-        gw = torch.nn.grad.conv2d_weight(x.nchw().float(), (Ko, Cc, R, S), dy.nchw().float(), stride, pad)
+        gw = torch.nn.grad.conv2d_weight(x.nchw().to(self.dt), (Ko, Cc, R, S), dy.nchw().to(self.dt), stride, pad)
         gw = gw.permute(0, 2, 3, 1)[:Ko_real, :, :, :Creal]
         grad.view(Ko_real, R, S, Creal).add_(gw)
 
@@ -246,37 +248,37 @@ class RefBackend:
         invstd = 1.0 / torch.sqrt(var + eps)
         g = gamma.double() if gamma is not None else torch.ones_like(mean)
         b = beta.double() if beta is not None else torch.zeros_like(mean)
-        sc = (g * invstd).float()
+        sc = (g * invstd).to(self.dt)
         scale.copy_(sc)
-        shift.copy_((b - mean * g * invstd).float())
+        shift.copy_((b - mean * g * invstd).to(self.dt))
         if save_mean is not None:
-            save_mean.copy_(mean.float())
+            save_mean.copy_(mean.to(self.dt))
         if save_invstd is not None:
-            save_invstd.copy_(invstd.float())
+            save_invstd.copy_(invstd.to(self.dt))
         if rm is not None:
             unb = var * count / (count - 1) if count > 1 else var
-            rm.mul_(1 - momentum).add_(momentum * mean.float())
-            rv.mul_(1 - momentum).add_(momentum * unb.float())
+            rm.mul_(1 - momentum).add_(momentum * mean.to(self.dt))
+            rv.mul_(1 - momentum).add_(momentum * unb.to(self.dt))
 
     def bn_stats(self, x: Act):
-        v = x.nhwc().float()
+        v = x.nhwc().to(self.dt)
         part = torch.stack([v.sum((0, 1, 2)), (v * v).sum((0, 1, 2))]).unsqueeze(0)
         return part, 1
 
     def bn_apply(self, x: Act, scale, shift, res, relu, y: Act):
-        v = x.nhwc().float() * scale + shift
+        v = x.nhwc().to(self.dt) * scale + shift
         if res is not None:
-            v = v + res.nhwc().float()
+            v = v + res.nhwc().to(self.dt)
         if relu:
             v = F.relu(v)
         y.nhwc().copy_(v)
 
     def bn_bwd(self, dy: Act, ymask, x: Act, mean, invstd, gamma, dgamma, dbeta, dx: Act, dyr_out=None):
-        g = dy.nhwc().float()
+        g = dy.nhwc().to(self.dt)
         if ymask is not None:
             g = g * (ymask.nhwc() > 0)
         M = x.rows
-        xhat = (x.nhwc().float() - mean) * invstd
+        xhat = (x.nhwc().to(self.dt) - mean) * invstd
         s1 = g.sum((0, 1, 2))
         s2 = (g * xhat).sum((0, 1, 2))
         if dbeta is not None:
@@ -289,41 +291,41 @@ class RefBackend:
             dyr_out.nhwc().copy_(g)
 
     def channel_sum(self, x: Act, out_acc):
-        out_acc.add_(x.nhwc().float().sum((0, 1, 2)))
+        out_acc.add_(x.nhwc().to(self.dt).sum((0, 1, 2)))
 
     def maxpool_fwd(self, x: Act, k, s, p, y: Act):
-        out, idx = F.max_pool2d(x.nchw().float(), k, s, p, return_indices=True)
+        out, idx = F.max_pool2d(x.nchw().to(self.dt), k, s, p, return_indices=True)
         self._store(y, out)
         return idx
 
     def maxpool_bwd(self, dy: Act, idx, x: Act, k, s, p, dx: Act, add=None):
-        g = torch.ops.aten.max_pool2d_with_indices_backward(dy.nchw().float().contiguous(), x.nchw().float(), [k, k],
+        g = torch.ops.aten.max_pool2d_with_indices_backward(dy.nchw().to(self.dt).contiguous(), x.nchw().to(self.dt), [k, k],
                                                             [s, s], [p, p], [1, 1], False, idx)
         if add is not None:
-            g = g + add.nchw().float()
+            g = g + add.nchw().to(self.dt)
         self._store(dx, g)
 
     def avgpool_fwd(self, x: Act, y: Act):
-        y.nhwc().copy_(x.nhwc().float().mean((1, 2), keepdim=True))
+        y.nhwc().copy_(x.nhwc().to(self.dt).mean((1, 2), keepdim=True))
 
     def avgpool_bwd(self, dy: Act, dx: Act):
-        dx.nhwc().copy_(dy.nhwc().float().expand(dx.N, dx.H, dx.W, dx.C) / (dx.H * dx.W))
+        dx.nhwc().copy_(dy.nhwc().to(self.dt).expand(dx.N, dx.H, dx.W, dx.C) / (dx.H * dx.W))
 
     def nchw_to_nhwc(self, x: torch.Tensor, Cpad) -> Act:
         N, Cc, H, W = x.shape
-        y = Act.zeros(N, H, W, Cpad, torch.float32, x.device)
+        y = Act.zeros(N, H, W, Cpad, self.dt, x.device)
         y.nhwc()[..., :Cc].copy_(x.permute(0, 2, 3, 1))
         return y
 
     def upsample_fwd(self, x: Act, y: Act):
-        out = F.interpolate(x.nchw().float(), scale_factor=2, mode="bilinear", align_corners=True)
+        out = F.interpolate(x.nchw().to(self.dt), scale_factor=2, mode="bilinear", align_corners=True)
         self._store(y, out)
 
     def upsample_bwd(self, dy: Act, dx: Act):
-        xin = torch.zeros(dx.N, dx.C, dx.H, dx.W, requires_grad=True)
+        xin = torch.zeros(dx.N, dx.C, dx.H, dx.W, dtype=self.dt, device=dy.device, requires_grad=True)
         with torch.enable_grad():
             out = F.interpolate(xin, scale_factor=2, mode="bilinear", align_corners=True)
-            (g,) = torch.autograd.grad(out, xin, dy.nchw().float())
+            (g,) = torch.autograd.grad(out, xin, dy.nchw().to(self.dt))
         self._store(dx, g)
 
     def cast_weights(self, entries, total, dst_flat):
@@ -334,26 +336,26 @@ class RefBackend:
             dst[:v[0], :v[1], :v[2], :v[3]].copy_(src.as_strided(tuple(v), tuple(st)))
 
     def ce_fwd(self, logits, labels):
-        lse = torch.logsumexp(logits.float(), 1)
-        loss = F.cross_entropy(logits.float(), labels)
+        lse = torch.logsumexp(logits.to(self.dt), 1)
+        loss = F.cross_entropy(logits.to(self.dt), labels)
         return loss, lse
 
     def ce_bwd(self, logits, labels, lse, go):
-        p = torch.exp(logits.float() - lse[:, None])
+        p = torch.exp(logits.to(self.dt) - lse[:, None])
         p[torch.arange(len(labels)), labels] -= 1.0
         return p * (go if go is not None else 1.0) / logits.shape[0]
 
     def bce_fwd(self, logits, target):
-        return F.binary_cross_entropy_with_logits(logits.float(), target.float())
+        return F.binary_cross_entropy_with_logits(logits.to(self.dt), target.to(self.dt))
 
     def bce_bwd(self, logits, target, go):
-        return (torch.sigmoid(logits.float()) - target) * (go if go is not None else 1.0) / logits.numel()
+        return (torch.sigmoid(logits.to(self.dt)) - target) * (go if go is not None else 1.0) / logits.numel()
 
     def argmax_correct(self, logits, labels):
         return (logits.argmax(1) == labels).sum().to(torch.int32).view(1)
 
     def dice(self, logits, target):
-        pred = (logits.reshape(target.shape) > 0).float()
+        pred = (logits.reshape(target.shape) > 0).to(self.dt)
         inter = (pred * target).flatten(1).sum(1)
         uni = pred.flatten(1).sum(1) + target.flatten(1).sum(1)
         return torch.where(uni > 0, (2 * inter + 1e-8) / (uni + 1e-8), torch.ones_like(uni))
@@ -388,7 +390,7 @@ class RefBackend:
         p.addcdiv_(m, denom, value=-lr / bc1)
 
     def grad_norm(self, g, max_norm, norm_out, coef_out):
-        n = g.double().pow(2).sum().sqrt().float()
+        n = g.double().pow(2).sum().sqrt().to(self.dt)
         norm_out.reshape(-1)[0] = n
         coef_out[0] = torch.clamp(max_norm / (n + 1e-6), max=1.0)
         coef_out[1] = 0.0 if torch.isfinite(n) else 1.0
@@ -397,8 +399,8 @@ class RefBackend:
         x.mul_(coef[0])
 
 
-def make_backend(device) -> "NativeBackend | RefBackend":
+def make_backend(device, dtype=torch.float32) -> "NativeBackend | RefBackend":
     device = torch.device(device)
     if device.type == "cuda":
         return NativeBackend(device)
-    return RefBackend(device)
+    return RefBackend(device, dtype)

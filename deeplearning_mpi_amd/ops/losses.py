@@ -14,11 +14,12 @@ from .backend import make_backend
 _BE = {}
 
 
-def _be(device):
-    key = str(device)
+def _be(device, dtype=None):
+    dt = torch.float64 if dtype == torch.float64 else torch.float32
+    key = (str(device), dt)
     b = _BE.get(key)
     if b is None:
-        b = _BE[key] = make_backend(device)
+        b = _BE[key] = make_backend(device, dt)
     return b
 
 
@@ -26,16 +27,16 @@ class _CE(torch.autograd.Function):
     @staticmethod
     def forward(ctx, logits, labels):
         logits = logits.contiguous()
-        be = _be(logits.device)
-        loss, lse = be.ce_fwd(logits.float(), labels)
+        be = _be(logits.device, logits.dtype)
+        loss, lse = be.ce_fwd(logits.to(be.dt), labels)
         ctx.save_for_backward(logits, labels, lse)
         return loss
 
     @staticmethod
     def backward(ctx, go):
         logits, labels, lse = ctx.saved_tensors
-        be = _be(logits.device)
-        g = be.ce_bwd(logits.float(), labels, lse, go.reshape(1).float().contiguous())
+        be = _be(logits.device, logits.dtype)
+        g = be.ce_bwd(logits.to(be.dt), labels, lse, go.reshape(1).to(be.dt).contiguous())
         return g.to(logits.dtype), None
 
 
@@ -43,17 +44,17 @@ class _BCE(torch.autograd.Function):
     @staticmethod
     def forward(ctx, logits, target):
         logits = logits.contiguous()
-        target = target.contiguous().float()
-        be = _be(logits.device)
-        loss = be.bce_fwd(logits.float(), target)
+        target = target.contiguous().to(_be(logits.device, logits.dtype).dt)
+        be = _be(logits.device, logits.dtype)
+        loss = be.bce_fwd(logits.to(be.dt), target)
         ctx.save_for_backward(logits, target)
         return loss
 
     @staticmethod
     def backward(ctx, go):
         logits, target = ctx.saved_tensors
-        be = _be(logits.device)
-        g = be.bce_bwd(logits.float(), target, go.reshape(1).float().contiguous())
+        be = _be(logits.device, logits.dtype)
+        g = be.bce_bwd(logits.to(be.dt), target, go.reshape(1).to(be.dt).contiguous())
         return g.view(logits.shape).to(logits.dtype), None
 
 
@@ -78,7 +79,7 @@ class BCEWithLogitsLoss(nn.Module):
 @torch.no_grad()
 def top1_correct(logits, labels) -> torch.Tensor:
     """Device int32[1] count of argmax(logits) == labels (reference main.py:65-71)."""
-    return _be(logits.device).argmax_correct(logits.float().contiguous(), labels)
+    return _be(logits.device, logits.dtype).argmax_correct(logits.float().contiguous(), labels)
 
 
 @torch.no_grad()
@@ -86,4 +87,4 @@ def dice_per_sample(logits, target) -> torch.Tensor:
     """Per-sample Dice of (sigmoid(logits) > 0.5) vs target, 1.0 when both are empty
     (reference train.py:121-137).  logits [N,1,H,W] or [N,H,W]; target [N,H,W]."""
     lg = logits.reshape(target.shape).float().contiguous()
-    return _be(logits.device).dice(lg, target.float().contiguous())
+    return _be(logits.device, logits.dtype).dice(lg, target.float().contiguous())

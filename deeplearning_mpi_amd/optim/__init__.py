@@ -34,13 +34,24 @@ class _FusedBase(torch.optim.Optimizer):
         self._step_count = 0
 
     def zero_grad(self, set_to_none: bool = True):
+        self._resolve_arena()
         if self._arena is not None:
             self._arena.zero_grad()   # grads are views of the flat buffer: one memset
         else:
             super().zero_grad(set_to_none=set_to_none)
 
+    def _resolve_arena(self):
+        # the engine builds its arena lazily (first forward / DDP construction), possibly after the
+        # optimizer was created: pick it up as soon as it exists
+        if (self._arena is None or not self._arena.valid()) and len(self.param_groups) == 1:
+            a = _single_arena(self.param_groups[0]["params"])
+            if a is not None:
+                self._arena = a
+                self._be = a.backend
+
     def _groups(self):
         """Yield (group, p, g, state-key-prefix) as flat (arena) or per-tensor views."""
+        self._resolve_arena()
         if self._arena is not None:
             g = self.param_groups[0]
             yield g, self._arena.flat, self._arena.grad, "__flat__"

@@ -69,8 +69,9 @@ class ParamArena:
             n = self.params[i].numel()
             off += (n + self.ALIGN - 1) // self.ALIGN * self.ALIGN
         self.total = off
-        self.flat = torch.zeros(self.total, dtype=torch.float32, device=self.device)
-        self.grad = torch.zeros(self.total, dtype=torch.float32, device=self.device)
+        self.dtype = backend.dt if backend is not None else torch.float32
+        self.flat = torch.zeros(self.total, dtype=self.dtype, device=self.device)
+        self.grad = torch.zeros(self.total, dtype=self.dtype, device=self.device)
         self.order = order
 
         for i, p in enumerate(self.params):
@@ -93,11 +94,11 @@ class ParamArena:
                     continue
                 (fbufs if b.is_floating_point() else ibufs).append((m, bn, b))
         self.fbuf_total = sum(b.numel() for _, _, b in fbufs)
-        self.fbuf = torch.zeros(max(1, self.fbuf_total), dtype=torch.float32, device=self.device)
+        self.fbuf = torch.zeros(max(1, self.fbuf_total), dtype=self.dtype, device=self.device)
         o = 0
         for m, bn, b in fbufs:
             v = self.fbuf[o:o + b.numel()].view(b.shape)
-            v.copy_(b.to(self.device, torch.float32))
+            v.copy_(b.to(self.device, self.dtype))
             m._buffers[bn] = v
             o += b.numel()
         self.ibuf_total = sum(b.numel() for _, _, b in ibufs)
@@ -137,7 +138,7 @@ class ParamArena:
         i = self.index.get(id(p))
         if i is None:
             return False
-        return p.data.data_ptr() == self.flat.data_ptr() + 4 * self.offsets[i]
+        return p.data.data_ptr() == self.flat.data_ptr() + self.flat.element_size() * self.offsets[i]
 
     def valid(self) -> bool:
         return all(self.owns(p) for p in self.params)
@@ -155,7 +156,7 @@ class ParamArena:
         dropped = False
         for i, p in enumerate(self.params):
             g = p.grad
-            if g is None or g.data_ptr() != self.grad.data_ptr() + 4 * self.offsets[i]:
+            if g is None or g.data_ptr() != self.grad.data_ptr() + self.flat.element_size() * self.offsets[i]:
                 p.grad = self.grad.as_strided(tuple(p.shape), self._strides(tuple(p.shape), self.layouts[i]),
                                               self.offsets[i])
                 dropped = True

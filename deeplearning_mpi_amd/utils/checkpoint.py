@@ -1,0 +1,74 @@
+"""Checkpoints, layout-compatible with the reference.
+
+The main file is exactly what the reference writes -- ``torch.save(ddp_model.state_dict(), path)``
+(/root/reference/pytorch/resnet/main.py:139, unet/train.py:216): a flat dict of fp32 tensors whose
+keys carry the ``module.`` prefix -- so reference checkpoints load here and ours load there.
+Optional resume state (optimizer, epoch, RNG, sampler epoch) goes to a sidecar ``<path>.state``
+so the main file layout never changes.  Only GLOBAL rank 0 writes (the reference gates on
+LOCAL_RANK, which collides across nodes on a shared filesystem).
+Loading uses ``torch.load(..., weights_only=True)`` and accepts either key style.
+"""
+from __future__ import annotations
+
+import os
+
+import torch
+
+
+def _target(model):
+    return model
+
+
+def save_checkpoint(model, path, optimizer=None, extra=None, rank=None):
+    if rank is None:
+        from ..parallel.comm import get_comm
+
+        rank = get_comm().rank
+    if rank != 0:
+        return None
+    d = os.path.dirname(path)
+    if d:
+        os.makedirs(d, exist_ok=True)
+    sd = {k: v.detach().cpu() for k, v in model.state_dict().items()}
+    tmp = path + ".tmp"
+    torch.save(sd, tmp)
+    os.replace(tmp, path)
+    if optimizer is not None or extra:
+        state = dict(extra or {})
+        if optimizer is not None:
+            state["optimizer"] = optimizer.state_dict()
+        torch.save(state, path + ".state.tmp")
+        os.replace(path + ".state.tmp", path + ".state")
+    return path
+
+
+def _adapt_keys(sd, want_prefix):
+    has = all(k.startswith("module.") for k in sd)
+    if want_prefix and not has:
+        return {"module." + k: v for k, v in sd.items()}
+    if not want_prefix and has:
+        return {k[len("module."):]: v for k, v in sd.items()}
+    return sd
+
+
+def load_checkpoint(model, path, map_location=None, optimizer=None, strict=True):
+    """Load weights (and, when present, the sidecar resume state). Returns the sidecar dict."""
+    if map_location is None:
+        p = next(model.parameters())
+        map_location = p.device
+    sd = torch.load(path, map_location=map_location, weights_only=True)
+    want_prefix = all(k.startswith("module.") for k in model.state_dict())
+    sd = _adapt_keys(sd, want_prefix)
+    with torch.no_grad():
+        model.load_state_dict(sd, strict=strict)
+    meta = {}
+    if os.path.exists(path + ".state"):
+        meta = torch.load(path + ".state", map_location=map_location, weights_only=True)
+        if optimizer is not None and "optimizer" in meta:
+            optimizer.load_state_dict(meta["optimizer"])
+    from .arena import arena_of
+
+    a = arena_of(next(iter(model.parameters())))
+    if a is not None:
+        a.mark_updated()
+    return meta

@@ -1,0 +1,76 @@
+import copy
+import os
+
+import torch
+
+from deeplearning_mpi_amd.models import UNet, resnet18, resnet50
+from deeplearning_mpi_amd.parallel import DistributedDataParallel
+from deeplearning_mpi_amd.utils import checkpoint as ck
+
+
+def test_state_dict_keys_match_reference():
+    m = resnet18(num_classes=10)
+    ddp = DistributedDataParallel(m)
+    sd = ddp.state_dict()
+    assert len(sd) == 122   # SURVEY.md §5.4 (torchvision resnet18 + 10-class fc, DDP-wrapped)
+    assert "module.conv1.weight" in sd and "module.layer1.0.conv1.weight" in sd and "module.fc.bias" in sd
+    assert sd["module.bn1.num_batches_tracked"].dtype == torch.int64
+    u = DistributedDataParallel(UNet(out_classes=1))
+    sdu = u.state_dict()
+    assert len(sdu) == 136
+    assert "module.down_conv1.double_conv.double_conv.0.weight" in sdu and "module.conv_last.bias" in sdu
+
+
+def test_param_counts():
+    assert sum(p.numel() for p in resnet18(num_classes=10).parameters()) == 11181642
+    assert sum(p.numel() for p in UNet(out_classes=1).parameters()) == 36963201   # SURVEY.md §2.2 C8 (train.py uses 1 class)
+
+
+def test_arena_rehomes_and_buckets():
+    m = resnet50(num_classes=1000)
+    ref = copy.deepcopy(m)
+    ar = m.engine_setup("cpu")
+    for (n, p), (_, q) in zip(m.named_parameters(), ref.named_parameters()):
+        assert torch.equal(p, q), n
+        assert ar.owns(p)
+        assert p.grad is not None and p.grad.shape == p.shape
+    bounds, pb = ar.buckets(2 * 2 ** 20, 32 * 2 ** 20)
+    assert bounds[0][0] == 0 and bounds[-1][1] >= ar.total - ar.ALIGN
+    for (s0, e0), (s1, e1) in zip(bounds, bounds[1:]):
+        assert e0 == s1
+    assert max(pb) == len(bounds) - 1
+    # fc is registered last -> first in the flat buffer -> first bucket
+    assert pb[ar.index[id(m.fc.weight)]] == 0
+
+
+def test_compute_copy_refresh():
+    m = resnet18(num_classes=10)
+    ar = m.engine_setup("cpu")
+    w = ar.get_compute(m.u_stem.h_fwd).view(64, 7, 7, 8).clone()
+    with torch.no_grad():
+        m.conv1.weight.add_(1.0)
+    ar.refresh()
+    w2 = ar.get_compute(m.u_stem.h_fwd).view(64, 7, 7, 8)
+    assert torch.allclose(w2[..., :3].permute(0, 3, 1, 2), m.conv1.weight)
+    assert torch.all(w2[..., 3:] == 0)
+    assert not torch.equal(w, w2)
+
+
+def test_checkpoint_roundtrip(tmp_path):
+    torch.manual_seed(0)
+    m = resnet18(num_classes=10)
+    ddp = DistributedDataParallel(m)
+    p = os.path.join(tmp_path, "resnet_distributed.pth")
+    ck.save_checkpoint(ddp, p, extra={"epoch": 3})
+    m2 = resnet18(num_classes=10)
+    ddp2 = DistributedDataParallel(m2)
+    meta = ck.load_checkpoint(ddp2, p)
+    for (n, a), (_, b) in zip(ddp.state_dict().items(), ddp2.state_dict().items()):
+        assert torch.equal(a, b), n
+    assert meta.get("epoch") == 3
+    # a plain (non-DDP) torchvision-style state_dict without the module. prefix also loads
+    sd = {k[len("module."):]: v for k, v in ddp.state_dict().items()}
+    torch.save(sd, p + ".plain")
+    m3 = resnet18(num_classes=10)
+    ck.load_checkpoint(m3, p + ".plain")
+    assert torch.equal(m3.fc.weight, m.fc.weight)

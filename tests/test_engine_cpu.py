@@ -1,0 +1,109 @@
+"""The engine's hand-written forward/backward schedules vs eager torch autograd (CPU, fp32
+reference backend).  Sizes are chosen so BatchNorm is well conditioned."""
+import copy
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+from deeplearning_mpi_amd.models import UNet, resnet18, resnet50
+from deeplearning_mpi_amd.ops import bce_with_logits, cross_entropy
+from deeplearning_mpi_amd.ops.act import Act
+
+
+def _err(a, ref):
+    return ((a.double() - ref).abs().max() / ref.abs().max().clamp_min(1e-30)).item()
+
+
+def _run_pair(make, x, y, loss_e, loss_t, skip=lambda n: False):
+    """The engine (reference backend in float64) against eager torch autograd in float64: with the
+    rounding noise removed the hand-written schedules must reproduce autograd essentially exactly
+    (fp32 comparisons are dominated by BatchNorm conditioning)."""
+    torch.manual_seed(0)
+    m1 = make().double()
+    m3 = copy.deepcopy(m1)
+    x = x.double()
+    y = y.double() if y.is_floating_point() else y
+    m1.train()
+    m3.train()
+    o1 = m1(x)
+    l1 = loss_e(o1, y)
+    l1.backward()
+    o3 = m3.forward_torch(x)
+    l3 = loss_t(o3, y)
+    l3.backward()
+    assert _err(o1.detach(), o3.detach()) < 1e-9
+    assert abs(l1.item() - l3.item()) < 1e-9
+    for (n, p1), (_, p3) in zip(m1.named_parameters(), m3.named_parameters()):
+        if skip(n) or p3.grad.abs().max() == 0:
+            continue
+        assert _err(p1.grad, p3.grad) < 1e-6, (n, _err(p1.grad, p3.grad))
+    for (n, b1), (_, b3) in zip(m1.named_buffers(), m3.named_buffers()):
+        if b1.is_floating_point():
+            assert _err(b1, b3) < 1e-9, n
+        else:
+            assert torch.equal(b1, b3), n
+    m1.eval()
+    m3.eval()
+    with torch.no_grad():
+        assert _err(m1(x), m3.forward_torch(x)) < 1e-9
+    return m1
+
+
+def test_resnet18_train_step_matches_torch():
+    g = torch.Generator().manual_seed(1)
+    x = torch.randn(16, 3, 64, 64, generator=g)
+    y = torch.randint(10, (16,), generator=g)
+    _run_pair(lambda: resnet18(num_classes=10), x, y, cross_entropy, F.cross_entropy)
+
+
+def test_bottleneck_blocks_exact():
+    torch.manual_seed(0)
+    m = resnet50(num_classes=10)
+    m2 = copy.deepcopy(m)
+    m.train()
+    m2.train()
+    ar = m.engine_setup("cpu")
+    be = m._be
+    for bi, (blk, ref) in enumerate([(m.blocks[0], m2.layer1[0]), (m.blocks[1], m2.layer1[1]),
+                                     (m.blocks[3], m2.layer2[0])]):
+        N, H, W = 4, 8, 8
+        Cin = ref.conv1.in_channels
+        x = torch.randn(N, Cin, H, W)
+        xa = Act.empty(N, H, W, Cin, torch.float32, "cpu")
+        xa.nhwc().copy_(x.permute(0, 2, 3, 1))
+        ar.zero_grad()
+        y, st = blk.fwd(be, xa, True, True)
+        gy = torch.randn(N, y.C, y.H, y.W)
+        dya = Act.empty(N, y.H, y.W, y.C, torch.float32, "cpu")
+        dya.nhwc().copy_(gy.permute(0, 2, 3, 1))
+        dx = blk.bwd(be, st, dya)
+        xt = x.clone().requires_grad_(True)
+        for p in ref.parameters():
+            p.grad = None
+        yt = ref.forward_torch(xt)
+        yt.backward(gy)
+        assert torch.allclose(y.nchw(), yt, atol=1e-4)
+        assert torch.allclose(dx.nchw(), xt.grad, atol=1e-4, rtol=1e-3)
+        mod = [m.layer1[0], m.layer1[1], m.layer2[0]][bi]
+        for (n, p1), (_, p2) in zip(mod.named_parameters(), ref.named_parameters()):
+            assert ((p1.grad - p2.grad).abs().max() / p2.grad.abs().max()).item() < 1e-5, n
+
+
+@pytest.mark.parametrize("mode", ["conv_transpose", "bilinear"])
+def test_unet_train_step_matches_torch(mode):
+    g = torch.Generator().manual_seed(1)
+    x = torch.randn(4, 3, 64, 64, generator=g)
+    y = (torch.rand(4, 64, 64, generator=g) > 0.5).float()
+    skip = lambda n: n.endswith("bias") and "double_conv.double_conv" in n  # conv bias before train-BN: grad == 0
+    _run_pair(lambda: UNet(out_classes=1, up_sample_mode=mode), x, y, lambda o, t: bce_with_logits(o.squeeze(1), t),
+              lambda o, t: F.binary_cross_entropy_with_logits(o.squeeze(1), t), skip=skip)
+
+
+def test_unet_shapes_and_multiclass():
+    m = UNet(out_classes=2)
+    m.eval()
+    with torch.no_grad():
+        y = m(torch.randn(1, 3, 32, 32))
+        y2 = m.forward_torch(torch.randn(1, 3, 32, 32))
+    assert y.shape == (1, 2, 32, 32) == y2.shape

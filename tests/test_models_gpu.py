@@ -1,5 +1,11 @@
-"""End-to-end model numerics on the GPU: the native bf16 engine vs eager fp32 torch with the same
-parameters (forward logits, loss, every parameter gradient by cosine similarity, BN buffers)."""
+"""End-to-end model numerics on the GPU.
+
+The native engine runs bf16 activations with fp32 accumulation/master weights, like
+``torch.autocast(bfloat16)``.  Both are compared with an fp64 eager-torch oracle on the same
+parameters and data; the engine's deviation (logits, loss, every parameter gradient, BN buffers)
+must stay within a small factor of stock autocast's own deviation -- i.e. the engine is at least
+as accurate as the stock bf16 path the reference would run (BN-heavy nets amplify rounding, so
+an absolute tolerance against fp32 would be meaningless)."""
 import copy
 
 import pytest
@@ -13,69 +19,103 @@ pytestmark = pytest.mark.gpu
 DEV = "cuda"
 
 
-def _cos(a, b):
-    a, b = a.double().flatten(), b.double().flatten()
-    return (a @ b / (a.norm() * b.norm() + 1e-30)).item()
+def _err(a, ref):
+    a, ref = a.double().flatten(), ref.double().flatten()
+    return ((a - ref).norm() / ref.norm().clamp_min(1e-30)).item()
 
 
-def _compare(make, x, y, loss_e, loss_t, skip_bias_before_bn=False, min_cos=0.99):
+def _compare(make, x, y, loss_e, loss_t, skip=lambda n: False, slack=3.0, floor=2e-2):
     torch.manual_seed(0)
     m1 = make().to(DEV)
     m2 = copy.deepcopy(m1)
-    m1.train()
-    m2.train()
+    m3 = copy.deepcopy(m1).double()
+    for m in (m1, m2, m3):
+        m.train()
     o1 = m1(x)
-    l1 = loss_e(o1, y)
-    l1.backward()
-    o2 = m2.forward_torch(x)
-    l2 = loss_t(o2, y)
-    l2.backward()
+    loss_e(o1, y).backward()
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        o2 = m2.forward_torch(x)
+    loss_t(o2.float(), y).backward()
+    o3 = m3.forward_torch(x.double())
+    loss_t(o3, y.double() if y.is_floating_point() else y).backward()
     torch.cuda.synchronize()
-    assert abs(l1.item() - l2.item()) < 2e-2 * max(1.0, abs(l2.item()))
-    assert _cos(o1, o2) > 0.999
+    assert _err(o1, o3) <= slack * _err(o2, o3) + 1e-2
     bad = []
-    for (n, p1), (_, p2) in zip(m1.named_parameters(), m2.named_parameters()):
-        if skip_bias_before_bn and n.endswith("bias") and "double_conv" in n and (".0." in n or ".3." in n):
-            continue   # conv bias followed by training-mode BN: exact gradient is 0
-        c = _cos(p1.grad, p2.grad)
-        if c < min_cos:
-            bad.append((n, c))
+    for (n, p1), (_, p2), (_, p3) in zip(m1.named_parameters(), m2.named_parameters(), m3.named_parameters()):
+        if skip(n) or p3.grad.abs().max() == 0:
+            continue
+        e1, e2 = _err(p1.grad, p3.grad), _err(p2.grad, p3.grad)
+        if e1 > slack * e2 + floor:
+            bad.append((n, round(e1, 4), round(e2, 4)))
     assert not bad, bad
-    for (n, b1), (_, b2) in zip(m1.named_buffers(), m2.named_buffers()):
+    for (n, b1), (_, b3) in zip(m1.named_buffers(), m3.named_buffers()):
         if b1.is_floating_point():
-            assert _cos(b1, b2) > 0.999, n
+            assert _err(b1, b3) < 2e-2, n
     m1.eval()
-    m2.eval()
+    m3.eval()
     with torch.no_grad():
-        assert _cos(m1(x), m2.forward_torch(x)) > 0.999
+        assert _err(m1(x), m3.forward_torch(x.double())) < 5e-2
 
 
-def test_resnet18_engine_vs_torch():
-    x = torch.randn(16, 3, 64, 64, device=DEV)
-    y = torch.randint(10, (16,), device=DEV)
+def test_resnet18_engine_vs_autocast():
+    g = torch.Generator(device=DEV).manual_seed(1)
+    x = torch.randn(16, 3, 64, 64, device=DEV, generator=g)
+    y = torch.randint(10, (16,), device=DEV, generator=g)
     _compare(lambda: resnet18(num_classes=10), x, y, cross_entropy, F.cross_entropy)
 
 
-def test_resnet50_engine_vs_torch():
-    x = torch.randn(8, 3, 128, 128, device=DEV)
-    y = torch.randint(1000, (8,), device=DEV)
-    _compare(lambda: resnet50(num_classes=1000), x, y, cross_entropy, F.cross_entropy, min_cos=0.97)
+def test_resnet50_engine_vs_autocast():
+    g = torch.Generator(device=DEV).manual_seed(1)
+    x = torch.randn(8, 3, 128, 128, device=DEV, generator=g)
+    y = torch.randint(1000, (8,), device=DEV, generator=g)
+    _compare(lambda: resnet50(num_classes=1000), x, y, cross_entropy, F.cross_entropy)
 
 
 @pytest.mark.parametrize("mode", ["conv_transpose", "bilinear"])
-def test_unet_engine_vs_torch(mode):
-    x = torch.randn(2, 3, 64, 96, device=DEV)
-    y = (torch.rand(2, 64, 96, device=DEV) > 0.5).float()
+def test_unet_engine_vs_autocast(mode):
+    g = torch.Generator(device=DEV).manual_seed(1)
+    x = torch.randn(2, 3, 64, 96, device=DEV, generator=g)
+    y = (torch.rand(2, 64, 96, device=DEV, generator=g) > 0.5).float()
+    skip = lambda n: n.endswith("bias") and "double_conv.double_conv" in n   # conv bias before train-BN
     _compare(lambda: UNet(out_classes=1, up_sample_mode=mode), x, y,
              lambda o, t: bce_with_logits(o.squeeze(1), t),
-             lambda o, t: F.binary_cross_entropy_with_logits(o.squeeze(1), t), skip_bias_before_bn=True)
+             lambda o, t: F.binary_cross_entropy_with_logits(o.squeeze(1), t), skip=skip)
 
 
-def test_unet_1ch_input():
+def test_unet_1ch_input_and_training_decreases_loss():
     torch.manual_seed(0)
+    from deeplearning_mpi_amd.optim import Adam, clip_grad_norm_
+
     m = UNet(out_classes=1, in_channels=1).to(DEV)
+    opt = Adam(m.parameters(), lr=1e-3)
     x = torch.randn(2, 1, 64, 64, device=DEV)
-    out = m(x)
-    assert out.shape == (2, 1, 64, 64)
-    bce_with_logits(out.squeeze(1), (torch.rand(2, 64, 64, device=DEV) > 0.5).float()).backward()
-    assert torch.isfinite(m.arena.grad).all()
+    t = (x[:, 0] > 0).float()
+    losses = []
+    for _ in range(8):
+        out = m(x)
+        assert out.shape == (2, 1, 64, 64)
+        loss = bce_with_logits(out.squeeze(1), t)
+        opt.zero_grad()
+        loss.backward()
+        clip_grad_norm_(m.parameters(), 1.0, optimizer=opt)
+        opt.step()
+        losses.append(loss.item())
+    assert losses[-1] < losses[0]
+
+
+def test_resnet_training_decreases_loss():
+    torch.manual_seed(0)
+    from deeplearning_mpi_amd.optim import SGD
+
+    m = resnet18(num_classes=10).to(DEV)
+    opt = SGD(m.parameters(), lr=0.05, momentum=0.9, weight_decay=1e-5)
+    x = torch.randn(32, 3, 32, 32, device=DEV)
+    y = torch.randint(10, (32,), device=DEV)
+    losses = []
+    for _ in range(10):
+        opt.zero_grad()
+        loss = cross_entropy(m(x), y)
+        loss.backward()
+        opt.step()
+        losses.append(loss.item())
+    assert losses[-1] < 0.5 * losses[0]
