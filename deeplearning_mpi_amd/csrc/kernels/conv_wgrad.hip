@@ -234,10 +234,10 @@ extern "C" hipError_t dlmpi_wgrad_reduce(const float* ws, int splits, int Ko, in
   const int64_t total = (int64_t)Ko * T * Cpad;
   if (total == 0 || Ko_real == 0) return hipSuccess;
   const int G = reduce_groups(splits, total);
-  if ((int64_t)G * total > (int64_t)ws2_floats) return hipErrorInvalidValue;
   const float* src = ws;
   int Gs = splits;
   if (splits > 1) {
+    if ((int64_t)G * total > (int64_t)ws2_floats) return hipErrorInvalidValue;
     hipLaunchKernelGGL(wgrad_reduce_stage1, dim3((unsigned)((total / 4 + 255) / 256), G), dim3(256), 0, s, ws, splits,
                        total, ws2);
     src = ws2;

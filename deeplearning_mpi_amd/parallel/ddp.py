@@ -60,7 +60,9 @@ class DistributedDataParallel(nn.Module):
             from .._ext import native
 
             views = [self.arena.grad[s:e] for s, e in self.bucket_bounds]
-            self.reducer = native().Reducer(views, self.param_bucket, self.comm.bucket_comm(), True)
+            # keep the (possibly Python-implemented) bucket comm alive alongside the C++ reducer
+            self._bucket_comm = self.comm.bucket_comm()
+            self.reducer = native().Reducer(views, self.param_bucket, self._bucket_comm, True)
         self._require_sync = True
         self._queued = False
 
