@@ -20,7 +20,14 @@
 #include <rccl/rccl.h>
 
 #include <cstring>
+#include <atomic>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <deque>
+#include <mutex>
 #include <stdexcept>
+#include <thread>
 
 namespace dlmpi_ext {
 
@@ -71,7 +78,89 @@ struct RcclComm::Impl {
     next_event = (next_event + 1) % events.size();
     return e;
   }
+
+  // ---- failure detection: a watchdog thread over in-flight collectives --------------------
+  // Every collective records an event on the comm stream; if the oldest one has not completed
+  // after DLMPI_COMM_TIMEOUT seconds (default 1800, 0 = off) the watchdog reports the stuck
+  // operation and the communicator's async error, aborts the communicator and terminates the
+  // process (exit code 70) so the launcher tears the job down instead of hanging forever -- the
+  // reference has no failure detection at all.
+  struct Pending {
+    hipEvent_t ev;
+    std::chrono::steady_clock::time_point t;
+    const char* what;
+  };
+  std::mutex mu;
+  std::deque<Pending> pending;
+  std::thread wd;
+  std::atomic<bool> stop{false};
+  double timeout_s = 1800.0;
+
+  void start_watchdog() {
+    if (const char* e = std::getenv("DLMPI_COMM_TIMEOUT")) timeout_s = std::atof(e);
+    if (timeout_s <= 0) return;
+    wd = std::thread([this] { watch_loop(); });
+  }
+  void watch(const char* what) {
+    if (timeout_s <= 0) return;
+    hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(stream.stream(), &st) != hipSuccess || st != hipStreamCaptureStatusNone) return;
+    hipEvent_t ev;
+    if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) return;
+    if (hipEventRecord(ev, stream.stream()) != hipSuccess) {
+      hipEventDestroy(ev);
+      return;
+    }
+    std::lock_guard<std::mutex> g(mu);
+    pending.push_back({ev, std::chrono::steady_clock::now(), what});
+  }
+  void watch_loop() {
+    hipSetDevice(device);
+    while (!stop.load()) {
+      Pending p{};
+      bool have = false;
+      {
+        std::lock_guard<std::mutex> g(mu);
+        if (!pending.empty()) {
+          p = pending.front();
+          have = true;
+        }
+      }
+      if (!have) {
+        std::this_thread::sleep_for(std::chrono::milliseconds(50));
+        continue;
+      }
+      if (hipEventQuery(p.ev) == hipSuccess) {
+        std::lock_guard<std::mutex> g(mu);
+        pending.pop_front();
+        hipEventDestroy(p.ev);
+        continue;
+      }
+      const double waited =
+          std::chrono::duration<double>(std::chrono::steady_clock::now() - p.t).count();
+      if (waited > timeout_s) {
+        ncclResult_t ae = ncclSuccess;
+        if (comm) ncclCommGetAsyncError(comm, &ae);
+        std::fprintf(stderr,
+                     "[dlmpi watchdog] rank %d/%d: collective '%s' has not completed after %.0f s "
+                     "(RCCL async error: %s). Aborting the communicator and the process.\n",
+                     rank, size, p.what, waited, ncclGetErrorString(ae));
+        std::fflush(stderr);
+        if (comm) ncclCommAbort(comm);
+        std::_Exit(70);
+      }
+      std::this_thread::sleep_for(std::chrono::milliseconds(20));
+    }
+  }
+  void stop_watchdog() {
+    stop.store(true);
+    if (wd.joinable()) wd.join();
+    std::lock_guard<std::mutex> g(mu);
+    for (auto& p : pending) hipEventDestroy(p.ev);
+    pending.clear();
+  }
   ~Impl() {
+    stop_watchdog();
     for (auto& e : events) hipEventDestroy(e);
   }
 };
@@ -92,11 +181,13 @@ RcclComm::RcclComm(const std::string& uid, int rank, int size, int device) {
   ncclUniqueId id;
   std::memcpy(&id, uid.data(), sizeof(id));
   nccl_check(ncclCommInitRank(&impl_->comm, size, id, rank), "ncclCommInitRank");
+  impl_->start_watchdog();
 }
 
 RcclComm::~RcclComm() {
   if (impl_ && impl_->comm) {
     hipStreamSynchronize(impl_->stream.stream());
+    impl_->stop_watchdog();
     ncclCommDestroy(impl_->comm);
     impl_->comm = nullptr;
   }
@@ -105,6 +196,7 @@ RcclComm::~RcclComm() {
 void RcclComm::destroy() {
   if (impl_ && impl_->comm) {
     hip_check(hipStreamSynchronize(impl_->stream.stream()), "hipStreamSynchronize");
+    impl_->stop_watchdog();
     nccl_check(ncclCommDestroy(impl_->comm), "ncclCommDestroy");
     impl_->comm = nullptr;
   }
@@ -140,6 +232,7 @@ void RcclComm::allreduce_async(at::Tensor t, const std::string& op) {
   nccl_check(ncclAllReduce(t.data_ptr(), t.data_ptr(), (size_t)t.numel(), to_nccl(t.scalar_type()), to_op(op),
                            impl_->comm, impl_->stream.stream()),
              "ncclAllReduce");
+  impl_->watch("allreduce");
 }
 
 void RcclComm::allreduce(at::Tensor t, const std::string& op, bool async_op) {
@@ -154,6 +247,7 @@ void RcclComm::broadcast(at::Tensor t, int root, bool async_op) {
   nccl_check(ncclBroadcast(t.data_ptr(), t.data_ptr(), (size_t)t.numel(), to_nccl(t.scalar_type()), root,
                            impl_->comm, impl_->stream.stream()),
              "ncclBroadcast");
+  impl_->watch("broadcast");
   if (!async_op) fence_out();
 }
 
@@ -165,6 +259,7 @@ void RcclComm::allgather(at::Tensor out, const at::Tensor& in, bool async_op) {
   nccl_check(ncclAllGather(in.data_ptr(), out.data_ptr(), (size_t)in.numel(), to_nccl(in.scalar_type()), impl_->comm,
                            impl_->stream.stream()),
              "ncclAllGather");
+  impl_->watch("allgather");
   if (!async_op) fence_out();
 }
 
@@ -176,6 +271,7 @@ void RcclComm::reduce_scatter(at::Tensor out, const at::Tensor& in, const std::s
   nccl_check(ncclReduceScatter(in.data_ptr(), out.data_ptr(), (size_t)out.numel(), to_nccl(in.scalar_type()),
                                to_op(op), impl_->comm, impl_->stream.stream()),
              "ncclReduceScatter");
+  impl_->watch("reduce_scatter");
   if (!async_op) fence_out();
 }
 
@@ -196,6 +292,7 @@ void RcclComm::alltoall(at::Tensor out, const at::Tensor& in, bool async_op) {
                "ncclRecv");
   }
   nccl_check(ncclGroupEnd(), "ncclGroupEnd");
+  impl_->watch("alltoall");
   if (!async_op) fence_out();
 }
 
@@ -205,6 +302,7 @@ void RcclComm::send(const at::Tensor& t, int peer) {
   nccl_check(ncclSend(t.data_ptr(), (size_t)t.numel(), to_nccl(t.scalar_type()), peer, impl_->comm,
                       impl_->stream.stream()),
              "ncclSend");
+  impl_->watch("send");
   fence_out();
 }
 
@@ -214,6 +312,7 @@ void RcclComm::recv(at::Tensor t, int peer) {
   nccl_check(ncclRecv(t.data_ptr(), (size_t)t.numel(), to_nccl(t.scalar_type()), peer, impl_->comm,
                       impl_->stream.stream()),
              "ncclRecv");
+  impl_->watch("recv");
   fence_out();
 }
 

@@ -10,18 +10,28 @@
 // (call sites /root/reference/pytorch/unet/model.py:9-14, resnet main.py:40-41).
 //
 // Tile: BM (pixels) x BN (channels) x 64 (reduction), 256 threads = 4 waves in 2x2, each wave
-// (BM/2) x (BN/2) as (BM/32) x (BN/32) MFMA 16x16 tiles.  Operands are register-staged
-// (global -> VGPR -> ds_write_b128) into a double-buffered LDS image with an XOR swizzle that
-// makes the ds_read_b128 fragment reads conflict-free; the next tile's global loads are issued
-// before the current tile's MFMAs (one barrier per K-step).  Out-of-bounds im2col pieces read a
-// zero page so the staging loads stay unconditional.  The epilogue stages the fp32 tile through
-// LDS and emits 16-byte stores with fused bias / residual add / folded-BN affine / ReLU and the
-// per-channel BatchNorm partial sums of the stored (bf16-rounded) values.
+// (BM/2) x (BN/2) as (BM/32) x (BN/32) MFMA 16x16 tiles.
+// Staging: global -> LDS directly with global_load_lds_dwordx4 (no VGPR round trip, no ds_write):
+// each wave instruction fills 8 LDS rows of 128 B lane-linearly; the XOR swizzle that makes the
+// ds_read_b128 fragment reads bank-conflict-free is applied on the per-lane SOURCE address
+// (cdna_hip_programming.md §5.4 rule 21).  Out-of-image im2col pieces read a zero page.  The
+// next K-tile's loads are issued before the current tile's MFMAs into the other LDS buffer
+// (one barrier per K-step).  Channel counts >= 64: the tap (r, s) and channel base are
+// wave-uniform scalars and the per-row source pointers are rebuilt only when the tap changes.
+// Epilogue: the fp32 tile is staged through LDS for 16-byte stores with fused bias / residual
+// add / folded-BN affine / ReLU and the per-channel BatchNorm partial sums of the stored
+// (bf16-rounded) values.
 #include "common.h"
 
 namespace dlmpi {
 
-template <int BM, int BN>
+typedef __attribute__((address_space(3))) void lds_void;
+
+__device__ __forceinline__ void glds16(const void* g, char* lds_wave_base) {
+  __builtin_amdgcn_global_load_lds(g, (lds_void*)lds_wave_base, 16, 0, 0);
+}
+
+template <int BM, int BN, bool SMALLC>
 __global__ __launch_bounds__(256) void conv_igemm_kernel(const ConvArgs a) {
   constexpr int BK = 64;
   constexpr int WM = BM / 2, WN = BN / 2;
@@ -34,7 +44,7 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(const ConvArgs a) {
   constexpr int SMEM = STAGE_BYTES > EPI_BYTES ? STAGE_BYTES : EPI_BYTES;
   __shared__ __attribute__((aligned(16))) char smem[SMEM];
 
-  const ConvPhase& ph = a.ph[blockIdx.z];
+  const ConvPhase ph = a.ph[blockIdx.z];
   const uint32_t nwg = (uint32_t)ph.mtiles * (uint32_t)a.ntiles;
   if (blockIdx.x >= nwg) return;
   const uint32_t bid = xcd_remap(blockIdx.x, nwg);
@@ -43,17 +53,19 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(const ConvArgs a) {
   const int PQ = ph.P * ph.Q;
   const int M = a.Nimg * PQ;
 
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wid >> 1, wn = wid & 1;
-  const int j = tid & 7;          // 16-byte chunk of the 64-wide K slice
-  const int rbase = tid >> 3;     // 0..31
+  const int lrow = tid >> 3;                          // staging row (+32 i)
+  const int jc = (tid & 7) ^ ((tid >> 4) & 7);        // swizzled 16-B chunk this lane fetches
+  const char* zp = reinterpret_cast<const char*>(g_zero_page);
 
   // ---- per-thread row state -------------------------------------------------------------
-  int a_h[AL], a_w[AL], a_img[AL];
+  int a_h[AL], a_w[AL], a_pix[AL];
   bool a_ok[AL];
 #pragma unroll
   for (int i = 0; i < AL; ++i) {
-    const int m = m0 + rbase + 32 * i;
+    const int m = m0 + lrow + 32 * i;
     a_ok[i] = m < M;
     const uint32_t mm = a_ok[i] ? (uint32_t)m : 0u;
     const uint32_t n_img = fdiv(mm, ph.fdPQ);
@@ -62,59 +74,79 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(const ConvArgs a) {
     const uint32_t q = rem - p * ph.Q;
     a_h[i] = (int)p * a.sa;
     a_w[i] = (int)q * a.sa;
-    a_img[i] = (int)n_img * a.H;
+    a_pix[i] = ((int)n_img * a.H + a_h[i]) * a.W + a_w[i];
   }
-  const uint16_t* b_row[BL];
+  const char* xlane = reinterpret_cast<const char*>(a.x) + 2 * ((int64_t)a.xoff + 8 * jc);
+  const char* b_row[BL];
   bool b_ok[BL];
 #pragma unroll
   for (int i = 0; i < BL; ++i) {
-    const int n = n0 + rbase + 32 * i;
+    const int n = n0 + lrow + 32 * i;
     b_ok[i] = n < a.Kout;
-    b_row[i] = a.w + (int64_t)(b_ok[i] ? n : 0) * a.ldw;
+    b_row[i] = reinterpret_cast<const char*>(a.w) + 2 * ((int64_t)(b_ok[i] ? n : 0) * a.ldw + 8 * jc);
   }
 
   const int C = a.C;
   const int T = ph.Tr * ph.Ts;
-  int t_cur, c_cur;
-  if (C >= 64) { t_cur = 0; c_cur = 8 * j; }
-  else { t_cur = (8 * j) / C; c_cur = (8 * j) - t_cur * C; }
+  const int nk = ph.ksteps;
+  const int ldx2 = a.ldx * 2;
 
-  u32x4 ra[AL], rb[BL];
-
-  auto load_tile = [&](int t, int c) {
-    const bool tv = t < T;
-    const int tt = tv ? t : 0;
-    const int tr = (int)fdiv((uint32_t)tt, ph.fdTs);
-    const int ts = tt - tr * ph.Ts;
+  // ---- staging ------------------------------------------------------------------------------
+  // Regular path (C % 64 == 0): the tap t and channel base c are wave-uniform.
+  const char* a_src[AL];
+  int t_cur = 0, c_cur = 0, wtC2 = 0;
+  auto tap_setup = [&](int t) {
+    const int tr = (int)fdiv((uint32_t)t, ph.fdTs);
+    const int ts = t - tr * ph.Ts;
     const int dh = ph.dh0 + tr * ph.dhs, dw = ph.dw0 + ts * ph.dws;
     const int wt = (ph.wr0 + tr * ph.wrs) * a.S + (ph.ws0 + ts * ph.wss);
+    wtC2 = wt * C * 2;
+    const int doff = dh * a.W + dw;
 #pragma unroll
     for (int i = 0; i < AL; ++i) {
       const int ih = a_h[i] + dh, iw = a_w[i] + dw;
-      const bool ok = tv && a_ok[i] && (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W;
-      const int64_t off = ((int64_t)(a_img[i] + ih) * a.W + iw) * a.ldx + a.xoff + c;
-      const u32x4* src = ok ? reinterpret_cast<const u32x4*>(a.x + off) : g_zero_page;
-      ra[i] = *src;
-    }
-#pragma unroll
-    for (int i = 0; i < BL; ++i) {
-      const bool ok = tv && b_ok[i];
-      const u32x4* src = ok ? reinterpret_cast<const u32x4*>(b_row[i] + (int64_t)wt * C + c) : g_zero_page;
-      rb[i] = *src;
+      const bool ok = a_ok[i] && (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W;
+      a_src[i] = ok ? xlane + (int64_t)(a_pix[i] + doff) * ldx2 : nullptr;
     }
   };
-  auto store_tile = [&](int buf) {
+
+  auto issue = [&](int buf, int ks) {
     char* As = smem + buf * (A_BYTES + B_BYTES);
     char* Bs = As + A_BYTES;
+    if constexpr (!SMALLC) {
 #pragma unroll
-    for (int i = 0; i < AL; ++i) {
-      const int r = rbase + 32 * i;
-      *reinterpret_cast<u32x4*>(As + r * 128 + ((j ^ ((r >> 1) & 7)) << 4)) = ra[i];
-    }
+      for (int i = 0; i < AL; ++i) {
+        const char* s = a_src[i] ? a_src[i] + 2 * c_cur : zp;
+        glds16(s, As + (32 * i + 8 * wid) * 128);
+      }
 #pragma unroll
-    for (int i = 0; i < BL; ++i) {
-      const int r = rbase + 32 * i;
-      *reinterpret_cast<u32x4*>(Bs + r * 128 + ((j ^ ((r >> 1) & 7)) << 4)) = rb[i];
+      for (int i = 0; i < BL; ++i) {
+        const char* s = b_ok[i] ? b_row[i] + wtC2 + 2 * c_cur : zp;
+        glds16(s, Bs + (32 * i + 8 * wid) * 128);
+      }
+    } else {
+      // small C (8/16/32; stem & first UNet layer): every 16-B piece is its own tap
+      const int kk = ks * BK + 8 * jc;
+      const int t = kk / C, c = kk - t * C;
+      const bool tv = t < T;
+      const int tt = tv ? t : 0;
+      const int tr = (int)fdiv((uint32_t)tt, ph.fdTs);
+      const int ts = tt - tr * ph.Ts;
+      const int dh = ph.dh0 + tr * ph.dhs, dw = ph.dw0 + ts * ph.dws;
+      const int wt = (ph.wr0 + tr * ph.wrs) * a.S + (ph.ws0 + ts * ph.wss);
+      const char* xs = reinterpret_cast<const char*>(a.x) + 2 * ((int64_t)a.xoff + c);
+#pragma unroll
+      for (int i = 0; i < AL; ++i) {
+        const int ih = a_h[i] + dh, iw = a_w[i] + dw;
+        const bool ok = tv && a_ok[i] && (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W;
+        const char* s = ok ? xs + (int64_t)(a_pix[i] + dh * a.W + dw) * ldx2 : zp;
+        glds16(s, As + (32 * i + 8 * wid) * 128);
+      }
+#pragma unroll
+      for (int i = 0; i < BL; ++i) {
+        const char* s = (tv && b_ok[i]) ? b_row[i] - 2 * 8 * jc + 2 * (wt * C + c) : zp;
+        glds16(s, Bs + (32 * i + 8 * wid) * 128);
+      }
     }
   };
 
@@ -124,21 +156,24 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(const ConvArgs a) {
 #pragma unroll
     for (int ni = 0; ni < TN; ++ni) acc[mi][ni] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  const int nk = ph.ksteps;
   if (nk > 0) {
-    load_tile(t_cur, c_cur);
-    store_tile(0);
+    if constexpr (!SMALLC) tap_setup(0);
+    issue(0, 0);
     __syncthreads();
   }
   const int fr = lane & 15, fg = lane >> 4;
   for (int ks = 0; ks < nk; ++ks) {
     const int cur = ks & 1;
-    const bool more = ks + 1 < nk;
-    if (more) {
-      c_cur += a.cstep;
-      t_cur += a.tstep;
-      if (c_cur >= C) { c_cur -= C; t_cur += 1; }
-      load_tile(t_cur, c_cur);
+    if (ks + 1 < nk) {
+      if constexpr (!SMALLC) {
+        c_cur += 64;
+        if (c_cur >= C) {
+          c_cur = 0;
+          ++t_cur;
+          tap_setup(t_cur);
+        }
+      }
+      issue(cur ^ 1, ks + 1);
     }
     const char* As = smem + cur * (A_BYTES + B_BYTES);
     const char* Bs = As + A_BYTES;
@@ -162,8 +197,7 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(const ConvArgs a) {
         for (int ni = 0; ni < TN; ++ni)
           acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[mi], bfr[ni], acc[mi][ni], 0, 0, 0);
     }
-    if (more) store_tile(cur ^ 1);
-    __syncthreads();
+    __syncthreads();   // (waits for this wave's glds of tile ks+1, then all waves) -> buffers swap
   }
 
   // ---- epilogue ------------------------------------------------------------------------------
@@ -278,15 +312,21 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(const ConvArgs a) {
 
 using namespace dlmpi;
 
+template <int BM, int BN>
+static void launch_tile(const ConvArgs* a, dim3 grid, hipStream_t s) {
+  if (a->C < 64) hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, true>), grid, dim3(256), 0, s, *a);
+  else hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, false>), grid, dim3(256), 0, s, *a);
+}
+
 extern "C" hipError_t dlmpi_conv_igemm(const ConvArgs* a, int bm, int bn, hipStream_t s) {
   int maxt = 0;
   for (int i = 0; i < a->nphase; ++i) maxt = a->ph[i].mtiles > maxt ? a->ph[i].mtiles : maxt;
   dim3 grid((unsigned)(maxt * a->ntiles), 1, (unsigned)a->nphase);
   if (grid.x == 0) return hipSuccess;
-  if (bm == 128 && bn == 128) hipLaunchKernelGGL((conv_igemm_kernel<128, 128>), grid, dim3(256), 0, s, *a);
-  else if (bm == 128 && bn == 64) hipLaunchKernelGGL((conv_igemm_kernel<128, 64>), grid, dim3(256), 0, s, *a);
-  else if (bm == 64 && bn == 128) hipLaunchKernelGGL((conv_igemm_kernel<64, 128>), grid, dim3(256), 0, s, *a);
-  else if (bm == 64 && bn == 64) hipLaunchKernelGGL((conv_igemm_kernel<64, 64>), grid, dim3(256), 0, s, *a);
+  if (bm == 128 && bn == 128) launch_tile<128, 128>(a, grid, s);
+  else if (bm == 128 && bn == 64) launch_tile<128, 64>(a, grid, s);
+  else if (bm == 64 && bn == 128) launch_tile<64, 128>(a, grid, s);
+  else if (bm == 64 && bn == 64) launch_tile<64, 64>(a, grid, s);
   else return hipErrorInvalidValue;
   return hipGetLastError();
 }
