@@ -87,6 +87,7 @@ static void fill_epilogue(ConvArgs& a, at::Tensor& y, int ldy, int yoff, const c
   a.shift = optr<float>(shift);
   a.relu = relu ? 1 : 0;
   a.stats = optr<float>(stats);
+  a.nstat = 2;
 }
 
 // y[n, p, q, yoff + k] = epilogue( sum_{r,s,c} x[n, p*stride - pad + r, q*stride - pad + s, xoff + c] * w[k][r][s][c] )
@@ -136,9 +137,16 @@ int conv2d_fwd_mtiles(int N, int H, int W, int K, int R, int S, int stride, int 
 
 // dx[n, h, w, dxoff + c] = sum_{r,s,k} dy[n, (h+pad-r)/stride, (w+pad-s)/stride, k] * wT[c][r][s][k]  (+ res)
 // as stride^2 dense sub-pixel phases.
-void conv2d_dgrad(const at::Tensor& dy, int N, int P, int Q, int K, int lddy, int dyoff, const at::Tensor& wT, int C,
-                  int R, int S, int stride, int pad, int H, int W, at::Tensor dx, int lddx, int dxoff,
-                  const c10::optional<at::Tensor>& res, int ldres, int resoff) {
+//
+// Optional BN-backward fusion (dx is the gradient of y = relu(BN(z)) [+ BN2(z2)]): the epilogue
+// applies the ReLU mask [y > 0] before storing and emits per-tile partials
+// [tiles][2|3][C] = {sum dx, sum dx*z [, sum dx*z2]}, returned (None without z).
+c10::optional<at::Tensor> conv2d_dgrad(const at::Tensor& dy, int N, int P, int Q, int K, int lddy, int dyoff,
+                                       const at::Tensor& wT, int C, int R, int S, int stride, int pad, int H, int W,
+                                       at::Tensor dx, int lddx, int dxoff, const c10::optional<at::Tensor>& res,
+                                       int ldres, int resoff, const c10::optional<at::Tensor>& mask, int ldmask,
+                                       int maskoff, const c10::optional<at::Tensor>& z, int ldz, int zoff,
+                                       const c10::optional<at::Tensor>& z2, int ldz2, int z2off) {
   require_gpu(dy, "dy");
   if (stride > 2) throw std::runtime_error("conv2d_dgrad: stride <= 2 supported");
   ConvArgs a{};
@@ -152,11 +160,22 @@ void conv2d_dgrad(const at::Tensor& dy, int N, int P, int Q, int K, int lddy, in
   a.Nimg = N; a.Kout = C;
   fill_epilogue(a, dx, lddx, dxoff, c10::nullopt, res, ldres, resoff, c10::nullopt, c10::nullopt, false, c10::nullopt);
   a.vec_store = ((lddx % 8) == 0 && (dxoff % 8) == 0) ? 1 : 0;
+  a.mask = optr<uint16_t>(mask);
+  a.ldmask = ldmask; a.maskoff = maskoff;
+  a.z = optr<uint16_t>(z);
+  a.ldz = ldz; a.zoff = zoff;
+  a.z2 = optr<uint16_t>(z2);
+  a.ldz2 = ldz2; a.z2off = z2off;
+  a.nstat = a.z2 ? 3 : 2;
+  if (a.z && !a.mask) throw std::runtime_error("conv2d_dgrad: fused BN statistics need the ReLU mask");
+  if (a.mask && ((ldmask | maskoff | ldz | zoff | ldz2 | z2off) % 8 != 0 || !a.vec_store))
+    throw std::runtime_error("conv2d_dgrad: fused BN tensors must be 8-channel aligned");
   set_kstep(a, K);
   int bm, bn;
   pick_tiles((int64_t)N * H * W / (stride * stride), C, bm, bn);
   a.ntiles = ceil_div(C, bn);
   a.nphase = stride * stride;
+  int tiles = 0;
   for (int ph = 0; ph < stride; ++ph) {
     for (int pw = 0; pw < stride; ++pw) {
       ConvPhase& p = a.ph[ph * stride + pw];
@@ -170,9 +189,17 @@ void conv2d_dgrad(const at::Tensor& dy, int N, int P, int Q, int K, int lddy, in
       p.wr0 = r0; p.wrs = stride; p.ws0 = s0; p.wss = stride;
       p.oh0 = ph; p.ow0 = pw;
       finish_phase(p, N, K, bm);
+      p.tile_base = tiles;
+      tiles += p.mtiles;
     }
   }
+  c10::optional<at::Tensor> stats;
+  if (a.z) {
+    stats = at::empty({(int64_t)tiles, (int64_t)a.nstat, (int64_t)C}, dy.options().dtype(at::kFloat));
+    a.stats = ptr<float>(*stats);
+  }
   check(dlmpi_conv_igemm(&a, bm, bn, cur_stream()), "conv2d_dgrad");
+  return stats;
 }
 
 // ConvTranspose2d(k=2, s=2): y[n, 2h+i, 2w+j, yoff + co] = bias[co] + sum_ci x[n,h,w,ci] * wf[co][i][j][ci]
@@ -301,6 +328,20 @@ void bn_bwd_finalize(const at::Tensor& partial, int nblk, int C, double count, c
                               optr<float>(invstd), optr<float>(dgamma), optr<float>(dbeta), optr<float>(coef),
                               ptr<double>(ws), cur_stream()),
         "bn_bwd_finalize");
+}
+
+// Finalize from the fused dgrad-epilogue partials [tiles][ns][C] (rows 0 and k2 = {sum dyr, sum dyr*z}).
+void bn_bwd_finalize_fused(const at::Tensor& partial, int k2, int C, double count,
+                           const c10::optional<at::Tensor>& gamma, const at::Tensor& mean, const at::Tensor& invstd,
+                           const c10::optional<at::Tensor>& dgamma, const c10::optional<at::Tensor>& dbeta,
+                           const c10::optional<at::Tensor>& coef) {
+  const int T = (int)partial.size(0), ns = (int)partial.size(1);
+  if (partial.size(2) != C) throw std::runtime_error("bn_bwd_finalize_fused: channel mismatch");
+  at::Tensor ws = colsum_ws(partial, T, C);
+  check(dlmpi_bn_bwd_finalize_ex(ptr<float>(partial), T, ns, k2, 1, C, count, optr<float>(gamma), ptr<float>(mean),
+                                 ptr<float>(invstd), optr<float>(dgamma), optr<float>(dbeta), optr<float>(coef),
+                                 ptr<double>(ws), cur_stream()),
+        "bn_bwd_finalize_fused");
 }
 
 void bn_bwd_apply(const at::Tensor& dy, int lddy, int dyoff, const c10::optional<at::Tensor>& ymask, int ldym,
@@ -436,6 +477,7 @@ void register_ops(pybind11::module& m) {
   m.def("bn_apply", &bn_apply);
   m.def("bn_bwd_reduce", &bn_bwd_reduce);
   m.def("bn_bwd_finalize", &bn_bwd_finalize);
+  m.def("bn_bwd_finalize_fused", &bn_bwd_finalize_fused);
   m.def("bn_bwd_apply", &bn_bwd_apply);
   m.def("channel_sum", &channel_sum);
   m.def("maxpool_fwd", &maxpool_fwd);

@@ -68,8 +68,10 @@ __global__ __launch_bounds__(256) void bn_stats_kernel(const uint16_t* __restric
 // Stage 1 of every per-channel column reduction over [T][2][C] fp32 partials:
 // dpart[s][k][c] = sum of partial[t][k][c] over row slice s (double).  Grid (ceil(C/64), S) so the
 // whole chip works on it (the partial tensors are up to 6272 x 2 x 2048); fixed summation order.
-__global__ __launch_bounds__(256) void colsum2_kernel(const float* __restrict__ partial, int T, int C,
-                                                      double* __restrict__ dpart) {
+// Sums rows 0 and k2 of per-tile partials laid out [T][ns][C] (fwd stats: ns = 2, k2 = 1; fused
+// backward stats from a GEMM epilogue: ns = 2 or 3 with the second BN consumer at k2 = 2).
+__global__ __launch_bounds__(256) void colsum2_kernel(const float* __restrict__ partial, int T, int C, int ns,
+                                                      int k2, double* __restrict__ dpart) {
   __shared__ double r[2][4][64];
   const int lc = threadIdx.x & 63, rl = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + lc;
@@ -79,8 +81,8 @@ __global__ __launch_bounds__(256) void colsum2_kernel(const float* __restrict__ 
   double a = 0.0, b = 0.0;
   if (c < C) {
     for (int t = t0 + rl; t < t1; t += 4) {
-      a += (double)partial[(int64_t)t * 2 * C + c];
-      b += (double)partial[(int64_t)t * 2 * C + C + c];
+      a += (double)partial[(int64_t)t * ns * C + c];
+      b += (double)partial[(int64_t)t * ns * C + k2 * C + c];
     }
   }
   r[0][rl][lc] = a;
@@ -223,11 +225,13 @@ __global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(const double* __re
                                                               double count, const float* gamma,
                                                               const float* __restrict__ mean,
                                                               const float* __restrict__ invstd, float* dgamma,
-                                                              float* dbeta, float* coef) {
+                                                              float* dbeta, float* coef, int raw_z) {
   const int c = blockIdx.x * 256 + threadIdx.x;
   if (c < C) {
     double s1, s2;
     colsum2_final(dpart, S, C, c, s1, s2);
+    // raw_z: the second sum is sum dyr*z (BN input), not sum dyr*xhat
+    if (raw_z) s2 = (double)invstd[c] * (s2 - (double)mean[c] * s1);
     if (dbeta) dbeta[c] += (float)s1;
     if (dgamma) dgamma[c] += (float)s2;
     if (coef) {
@@ -312,7 +316,7 @@ extern "C" hipError_t dlmpi_bn_finalize(const float* partial, int ntiles, int C,
                                         float eps, float* scale, float* shift, float* save_mean, float* save_invstd,
                                         double* ws, hipStream_t s) {
   const int S = colsum_slices(ntiles);
-  hipLaunchKernelGGL(colsum2_kernel, dim3((C + 63) / 64, S), dim3(256), 0, s, partial, ntiles, C, ws);
+  hipLaunchKernelGGL(colsum2_kernel, dim3((C + 63) / 64, S), dim3(256), 0, s, partial, ntiles, C, 2, 1, ws);
   hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, s, ws, S, C, count, gamma, beta,
                      running_mean, running_var, momentum, eps, scale, shift, save_mean, save_invstd);
   return hipGetLastError();
@@ -338,14 +342,22 @@ extern "C" hipError_t dlmpi_bn_bwd_reduce(const uint16_t* dy, int lddy, int dyof
   return hipGetLastError();
 }
 
+extern "C" hipError_t dlmpi_bn_bwd_finalize_ex(const float* partial, int nblk, int ns, int k2, int raw_z, int C,
+                                               double count, const float* gamma, const float* mean,
+                                               const float* invstd, float* dgamma, float* dbeta, float* coef,
+                                               double* ws, hipStream_t s) {
+  if (ns < 2 || ns > 3 || k2 < 1 || k2 >= ns) return hipErrorInvalidValue;
+  const int S = colsum_slices(nblk);
+  hipLaunchKernelGGL(colsum2_kernel, dim3((C + 63) / 64, S), dim3(256), 0, s, partial, nblk, C, ns, k2, ws);
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, s, ws, S, C, count, gamma, mean,
+                     invstd, dgamma, dbeta, coef, raw_z);
+  return hipGetLastError();
+}
+
 extern "C" hipError_t dlmpi_bn_bwd_finalize(const float* partial, int nblk, int C, double count, const float* gamma,
                                             const float* mean, const float* invstd, float* dgamma, float* dbeta,
                                             float* coef, double* ws, hipStream_t s) {
-  const int S = colsum_slices(nblk);
-  hipLaunchKernelGGL(colsum2_kernel, dim3((C + 63) / 64, S), dim3(256), 0, s, partial, nblk, C, ws);
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, s, ws, S, C, count, gamma, mean,
-                     invstd, dgamma, dbeta, coef);
-  return hipGetLastError();
+  return dlmpi_bn_bwd_finalize_ex(partial, nblk, 2, 1, 0, C, count, gamma, mean, invstd, dgamma, dbeta, coef, ws, s);
 }
 
 extern "C" hipError_t dlmpi_bn_bwd_apply(const uint16_t* dy, int lddy, int dyoff, const uint16_t* ymask, int ldym,

@@ -7,26 +7,57 @@
 
 namespace dlmpi {
 
-__global__ __launch_bounds__(256) void cast_weights_kernel(const CastEntry* __restrict__ ent, int n, int64_t total) {
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
-    int lo = 0, hi = n - 1;
-    while (lo < hi) {   // last entry with start <= i
-      const int mid = (lo + hi + 1) >> 1;
-      if (ent[mid].start <= i) lo = mid;
-      else hi = mid - 1;
+// blockIdx.y = entry.  Two paths:
+//  * transpose (source unit stride on destination dim 0, e.g. [K][R][S][C] -> [C][R][S][K] for the
+//    data-gradient copy): 64x64 tiles through LDS, coalesced reads along d0 and writes along d3;
+//  * direct (anything else, e.g. the forward copy whose innermost dim is contiguous in the source):
+//    one destination element per thread, grid-stride over the entry.
+__global__ __launch_bounds__(256) void cast_weights_kernel(const CastEntry* __restrict__ ent) {
+  __shared__ float tile[64][65];
+  const CastEntry& e = ent[blockIdx.y];
+  const int D0 = e.d[0], D1 = e.d[1], D2 = e.d[2], D3 = e.d[3];
+  const int64_t n = (int64_t)D0 * D1 * D2 * D3;
+  if (e.st[0] == 1 && e.st[3] != 1 && D0 >= 16 && D3 >= 16) {
+    const int t0n = (D0 + 63) / 64, t3n = (D3 + 63) / 64;
+    const int64_t ntiles = (int64_t)D1 * D2 * t0n * t3n;
+    const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;   // 64 x 4
+    for (int64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+      int64_t r = t;
+      const int b3 = (int)(r % t3n); r /= t3n;
+      const int b0 = (int)(r % t0n); r /= t0n;
+      const int i2 = (int)(r % D2);
+      const int i1 = (int)(r / D2);
+      const bool v12 = i1 < e.valid[1] && i2 < e.valid[2];
+      // read: i0 = b0*64 + tx (unit stride in the source), i3 = b3*64 + ty + 4k
+      for (int k = 0; k < 16; ++k) {
+        const int i0 = b0 * 64 + tx, i3 = b3 * 64 + ty + 4 * k;
+        float v = 0.f;
+        if (v12 && i0 < e.valid[0] && i3 < e.valid[3])
+          v = e.src[i0 * e.st[0] + i1 * e.st[1] + i2 * e.st[2] + i3 * e.st[3]];
+        tile[ty + 4 * k][tx] = v;
+      }
+      __syncthreads();
+      for (int k = 0; k < 16; ++k) {
+        const int i3 = b3 * 64 + tx, i0 = b0 * 64 + ty + 4 * k;
+        if (i0 < D0 && i3 < D3)
+          e.dst[(((int64_t)i0 * D1 + i1) * D2 + i2) * D3 + i3] = f2bf(tile[tx][ty + 4 * k]);
+      }
+      __syncthreads();
     }
-    const CastEntry& e = ent[lo];
-    int64_t r = i - e.start;
-    const int i3 = (int)(r % e.d[3]);
-    r /= e.d[3];
-    const int i2 = (int)(r % e.d[2]);
-    r /= e.d[2];
-    const int i1 = (int)(r % e.d[1]);
-    const int i0 = (int)(r / e.d[1]);
+    return;
+  }
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    int64_t r = i;
+    const int i3 = (int)(r % D3);
+    r /= D3;
+    const int i2 = (int)(r % D2);
+    r /= D2;
+    const int i1 = (int)(r % D1);
+    const int i0 = (int)(r / D1);
     float v = 0.f;
     if (i0 < e.valid[0] && i1 < e.valid[1] && i2 < e.valid[2] && i3 < e.valid[3])
       v = e.src[i0 * e.st[0] + i1 * e.st[1] + i2 * e.st[2] + i3 * e.st[3]];
-    e.dst[i - e.start] = f2bf(v);
+    e.dst[i] = f2bf(v);
   }
 }
 
@@ -48,10 +79,9 @@ __global__ void pack_kernel(const void* const* __restrict__ srcs, const int64_t*
 using namespace dlmpi;
 
 extern "C" hipError_t dlmpi_cast_weights(const CastEntry* entries_dev, int n, int64_t total, hipStream_t s) {
-  if (total == 0) return hipSuccess;
-  int64_t b = (total + 255) / 256;
-  if (b > 8192) b = 8192;
-  hipLaunchKernelGGL(cast_weights_kernel, dim3((unsigned)b), dim3(256), 0, s, entries_dev, n, total);
+  if (total == 0 || n == 0) return hipSuccess;
+  // gaps between entries (alignment padding) are zeroed once at allocation and never written
+  hipLaunchKernelGGL(cast_weights_kernel, dim3(64, (unsigned)n), dim3(256), 0, s, entries_dev);
   return hipGetLastError();
 }
 

@@ -229,9 +229,10 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(const ConvArgs a) {
       for (int e = 0; e < 8; ++e) { scl[e] = a.scale[c0 + e]; sft[e] = a.shift[c0 + e]; }
     }
   }
-  float s1[8], s2[8];
+  float s1[8], s2[8], s3[8];
 #pragma unroll
-  for (int e = 0; e < 8; ++e) { s1[e] = 0.f; s2[e] = 0.f; }
+  for (int e = 0; e < 8; ++e) { s1[e] = 0.f; s2[e] = 0.f; s3[e] = 0.f; }
+  const bool bwd = a.mask != nullptr;   // gradient of a BN+ReLU output: mask, then {sum dy, sum dy*z}
 
   for (int r = rg; r < BM; r += RG) {
     const int m = m0 + r;
@@ -241,7 +242,7 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(const ConvArgs a) {
     const f32x4 v1 = *reinterpret_cast<const f32x4*>(Cs + r * CS_LD + cg * 8 + 4);
 #pragma unroll
     for (int e = 0; e < 4; ++e) { v[e] = v0[e] + bias[e]; v[e + 4] = v1[e] + bias[e + 4]; }
-    if (a.stats) {
+    if (a.stats && !bwd) {
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
         const float rv = bf2f(f2bf(v[e]));
@@ -268,6 +269,27 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(const ConvArgs a) {
 #pragma unroll
       for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.f);
     }
+    if (bwd) {
+      float yy[8];
+      unpack8(*reinterpret_cast<const u32x4*>(a.mask + pix * a.ldmask + a.maskoff + c0), yy);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = yy[e] > 0.f ? v[e] : 0.f;
+      if (a.stats) {
+        float zz[8];
+        unpack8(*reinterpret_cast<const u32x4*>(a.z + pix * a.ldz + a.zoff + c0), zz);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float rv = bf2f(f2bf(v[e]));   // statistics of the stored (bf16) gradient
+          s1[e] += rv;
+          s2[e] += rv * zz[e];
+        }
+        if (a.z2) {
+          unpack8(*reinterpret_cast<const u32x4*>(a.z2 + pix * a.ldz2 + a.z2off + c0), zz);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) s3[e] += bf2f(f2bf(v[e])) * zz[e];
+        }
+      }
+    }
     if (a.vec_store) {
       if (a.out_f32) {
         float* yp = reinterpret_cast<float*>(a.y) + pix * a.ldy + a.yoff + c0;
@@ -290,20 +312,25 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(const ConvArgs a) {
   if (a.stats) {
     __syncthreads();
     float* red = reinterpret_cast<float*>(smem);
+    const int ns = a.nstat;
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
-      red[rg * 2 * BN + cg * 8 + e] = s1[e];
-      red[rg * 2 * BN + BN + cg * 8 + e] = s2[e];
+      red[(rg * 3 + 0) * BN + cg * 8 + e] = s1[e];
+      red[(rg * 3 + 1) * BN + cg * 8 + e] = s2[e];
+      red[(rg * 3 + 2) * BN + cg * 8 + e] = s3[e];
     }
     __syncthreads();
     if (tid < BN && n0 + tid < a.Kout) {
-      float t1 = 0.f, t2 = 0.f;
+      float t1 = 0.f, t2 = 0.f, t3 = 0.f;
       for (int g = 0; g < RG; ++g) {
-        t1 += red[g * 2 * BN + tid];
-        t2 += red[g * 2 * BN + BN + tid];
+        t1 += red[(g * 3 + 0) * BN + tid];
+        t2 += red[(g * 3 + 1) * BN + tid];
+        t3 += red[(g * 3 + 2) * BN + tid];
       }
-      a.stats[(int64_t)mt * 2 * a.Kout + n0 + tid] = t1;
-      a.stats[(int64_t)mt * 2 * a.Kout + a.Kout + n0 + tid] = t2;
+      float* st = a.stats + (int64_t)(ph.tile_base + mt) * ns * a.Kout + n0 + tid;
+      st[0] = t1;
+      st[a.Kout] = t2;
+      if (ns > 2) st[2 * a.Kout] = t3;
     }
   }
 }

@@ -41,6 +41,7 @@ struct ConvPhase {
   int oh0, ow0;
   int mtiles;   // ceil(N*P*Q / BM)
   int ksteps;   // ceil(Tr*Ts*C / 64)
+  int tile_base;  // first stats row of this phase (phases' tiles are numbered consecutively)
   FastDiv fdPQ, fdQ, fdTs;
 };
 
@@ -62,7 +63,17 @@ struct ConvArgs {
   const float* scale;              // per-channel affine after bias (folded eval BN) or null
   const float* shift;
   int relu;
-  float* stats;                    // BN partial sums [mtiles][2][Kout] of the (bf16-rounded) output, or null
+  float* stats;                    // BN partial sums [tiles][nstat][Kout] of the (bf16-rounded) output, or null
+  // Backward fusion (the GEMM produces the gradient dy of a BatchNorm+ReLU output y):
+  //   v := v * [mask > 0] (ReLU derivative) before the store, and the stats become
+  //   {sum v, sum v*z [, sum v*z2]} with z (z2) the BN input(s) that consume this gradient.
+  const uint16_t* mask;
+  int ldmask, maskoff;
+  const uint16_t* z;
+  int ldz, zoff;
+  const uint16_t* z2;
+  int ldz2, z2off;
+  int nstat;                       // 2 (fwd: sum v, sum v^2; bwd: sum v, sum v*z) or 3 (bwd with z2)
   int ntiles;
   int nphase;
   int cstep, tstep;                // K-iteration: c += cstep, t += tstep per 64-wide step
@@ -113,6 +124,10 @@ hipError_t dlmpi_bn_bwd_reduce(const uint16_t* dy, int lddy, int dyoff, const ui
 hipError_t dlmpi_bn_bwd_finalize(const float* partial, int nblk, int C, double count, const float* gamma,
                                  const float* mean, const float* invstd, float* dgamma, float* dbeta,
                                  float* coef, double* ws, hipStream_t s);
+// partials [nblk][ns][C]: rows 0 (sum dyr) and k2 (sum dyr*xhat, or sum dyr*z when raw_z)
+hipError_t dlmpi_bn_bwd_finalize_ex(const float* partial, int nblk, int ns, int k2, int raw_z, int C, double count,
+                                    const float* gamma, const float* mean, const float* invstd, float* dgamma,
+                                    float* dbeta, float* coef, double* ws, hipStream_t s);
 hipError_t dlmpi_bn_bwd_apply(const uint16_t* dy, int lddy, int dyoff, const uint16_t* ymask, int ldym, int ymoff,
                               const uint16_t* x, int ldx, int xoff, int64_t M, int C, const float* coef,
                               uint16_t* dx, uint16_t* dyr_out, hipStream_t s);

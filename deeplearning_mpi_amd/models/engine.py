@@ -19,6 +19,8 @@ One ``torch.autograd.Function`` bridges the engine to autograd (loss.backward() 
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.nn as nn
 
@@ -109,17 +111,34 @@ class ConvUnit:
                     shift=shift.contiguous(), relu=self.relu)
         return y, None
 
+    @staticmethod
+    def fuse_spec(ctx):
+        """(ReLU output y, BN input z) of a trained BN+ReLU unit: what a producer of dy needs to
+        fuse this unit's BN-backward reduction into its data-gradient epilogue."""
+        x, z, y, mean, invstd = ctx
+        return y, z
+
     def bwd(self, be, ctx, dy: Act, need_dx=True, dx_res: Act = None, dyr_out: Act = None, ymask: Act = None,
-            use_own_mask=True):
+            use_own_mask=True, pre=None, k2=1, fuse_next=None):
+        """Backward of the unit.
+
+        pre:       BN-backward partials already produced by the dgrad epilogue that wrote ``dy``
+                   (then ``dy`` is already ReLU-masked; row ``k2`` holds sum dy*z for this BN).
+        fuse_next: (mask, z, z2) of the consumer of this unit's dx -- the dgrad epilogue masks dx and
+                   emits that consumer's partials; returns (dx, partials) instead of dx.
+        """
         ar = self.arena
         bn = self.bn
         if bn is not None:
             x, z, y, mean, invstd = ctx
-            mask = ymask if ymask is not None else (y if (self.relu and use_own_mask) else None)
+            if pre is not None:
+                mask = None
+            else:
+                mask = ymask if ymask is not None else (y if (self.relu and use_own_mask) else None)
             dz = Act.empty(z.N, z.H, z.W, z.C, be.act_dtype, z.device)
             be.bn_bwd(dy, mask, z, mean, invstd, bn.weight.data if bn.affine else None,
                       ar.grad_flat(bn.weight) if bn.affine else None, ar.grad_flat(bn.bias) if bn.affine else None,
-                      dz, dyr_out)
+                      dz, dyr_out, pre=pre, k2=k2)
             if bn.affine:
                 ar.ready(bn.weight, bn.bias)
             if self.bias is not None:
@@ -142,8 +161,9 @@ class ConvUnit:
         if not need_dx:
             return None
         dx = Act.empty(x.N, x.H, x.W, self.Cp, be.act_dtype, x.device)
-        be.conv_dgrad(dz, ar.get_compute(self.h_dg), self.Cp, self.R, self.S, self.stride, self.pad, dx, res=dx_res)
-        return dx
+        part = be.conv_dgrad(dz, ar.get_compute(self.h_dg), self.Cp, self.R, self.S, self.stride, self.pad, dx,
+                             res=dx_res, fuse=fuse_next)
+        return (dx, part) if fuse_next is not None else dx
 
 
 class ConvTUnit:
@@ -204,6 +224,8 @@ class EngineModule(nn.Module):
         self._arena = None
         self._be = None
         self._anchor = torch.zeros(0, requires_grad=True)
+        # BN-backward reductions fused into the producing dgrad epilogue (DLMPI_FUSE_BN_BWD=0: off)
+        self.fuse_bn_bwd = os.environ.get("DLMPI_FUSE_BN_BWD", "1") != "0"
 
     def engine_setup(self, device=None):
         if device is None:

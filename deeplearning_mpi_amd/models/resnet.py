@@ -103,23 +103,43 @@ class _BlockExec:
         ctxs.append(c)
         return y, (ctxs, cd)
 
-    def bwd(self, be, st, dy: Act):
+    def fuse_spec(self, st):
+        """(block output y, BN input of the last conv, BN input of the downsample conv | None): the
+        previous schedule step fuses this block's BN-backward reductions into its dgrad epilogue."""
+        ctxs, cd = st
+        y, z = ConvUnit.fuse_spec(ctxs[-1])
+        return y, z, (cd[1] if cd is not None else None)
+
+    def bwd(self, be, st, dy: Act, pre=None, fuse_prev=None):
+        """dy: gradient of the block output.  With ``pre`` (partials from the producer's dgrad
+        epilogue) dy is already ReLU-masked.  With ``fuse_prev`` the block-input gradient is
+        produced masked for the previous block and returned with its partials."""
         ctxs, cd = st
         ylast = ctxs[-1][2]
+        n = len(self.u)
+        spec = lambda k: ConvUnit.fuse_spec(ctxs[k]) + (None,)   # noqa: E731
+        if pre is not None:
+            dh, part = self.u[-1].bwd(be, ctxs[-1], dy, pre=pre, k2=1, fuse_next=spec(n - 2))
+            for k in range(n - 2, 0, -1):
+                dh, part = self.u[k].bwd(be, ctxs[k], dh, pre=part, fuse_next=spec(k - 1))
+            # the masked dy is the identity-path gradient; the downsample BN reads row 2 of `pre`
+            dres = self.ud.bwd(be, cd, dy, pre=pre, k2=2) if self.ud is not None else dy
+            return self.u[0].bwd(be, ctxs[0], dh, dx_res=dres, pre=part, fuse_next=fuse_prev)
         if self.ud is None:
             dyr = Act.empty(dy.N, dy.H, dy.W, dy.C, be.act_dtype, dy.device)   # identity-path grad
             dh = self.u[-1].bwd(be, ctxs[-1], dy, dyr_out=dyr)
         else:
             dyr = None
             dh = self.u[-1].bwd(be, ctxs[-1], dy)
-        for k in range(len(self.u) - 2, 0, -1):
+        for k in range(n - 2, 0, -1):
             dh = self.u[k].bwd(be, ctxs[k], dh)
         if self.ud is not None:
             # downsample BN sees the same relu-masked output grad as the main branch
             dres = self.ud.bwd(be, cd, dy, ymask=ylast)
         else:
             dres = dyr
-        return self.u[0].bwd(be, ctxs[0], dh, dx_res=dres)
+        out = self.u[0].bwd(be, ctxs[0], dh, dx_res=dres, fuse_next=fuse_prev)
+        return out
 
 
 class ResNet(EngineModule):
@@ -205,8 +225,11 @@ class ResNet(EngineModule):
         dpool = self.u_fc.bwd(be, (x_fc, None), dl)
         da = Act.empty(a.N, a.H, a.W, a.C, be.act_dtype, a.device)
         be.avgpool_bwd(dpool, da)
-        for blk, st in zip(reversed(self.blocks), reversed(st_blocks)):
-            da = blk.bwd(be, st, da)
+        pre = None
+        for i in range(len(self.blocks) - 1, -1, -1):
+            fuse_prev = self.blocks[i - 1].fuse_spec(st_blocks[i - 1]) if (i > 0 and self.fuse_bn_bwd) else None
+            out = self.blocks[i].bwd(be, st_blocks[i], da, pre=pre, fuse_prev=fuse_prev)
+            da, pre = out if fuse_prev is not None else (out, None)
         dh = Act.empty(h.N, h.H, h.W, h.C, be.act_dtype, h.device)
         be.maxpool_bwd(da, idx, h, 3, 2, 1, dh)
         self.u_stem.bwd(be, cs, dh, need_dx=False)

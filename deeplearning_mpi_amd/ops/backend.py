@@ -40,10 +40,16 @@ class NativeBackend:
                           bias, res.buf if res is not None else None, res.ld if res is not None else 0,
                           res.off if res is not None else 0, scale, shift, bool(relu), stats, 0, int(kvalid))
 
-    def conv_dgrad(self, dy: Act, wT, C, R, S, stride, pad, dx: Act, res: Act = None):
-        self.C.conv2d_dgrad(dy.buf, dy.N, dy.H, dy.W, dy.C, dy.ld, dy.off, wT, C, R, S, stride, pad, dx.H, dx.W,
-                            dx.buf, dx.ld, dx.off, res.buf if res is not None else None,
-                            res.ld if res is not None else 0, res.off if res is not None else 0)
+    def conv_dgrad(self, dy: Act, wT, C, R, S, stride, pad, dx: Act, res: Act = None, fuse=None):
+        """fuse = (mask, z, z2|None): dx is the gradient of relu(BN(z) [+ BN2(z2)]) = mask; the
+        epilogue applies the ReLU mask and returns BN-backward partials [tiles][2|3][C]."""
+        m, z, z2 = fuse if fuse is not None else (None, None, None)
+
+        def t(a):
+            return (a.buf, a.ld, a.off) if a is not None else (None, 0, 0)
+
+        return self.C.conv2d_dgrad(dy.buf, dy.N, dy.H, dy.W, dy.C, dy.ld, dy.off, wT, C, R, S, stride, pad, dx.H,
+                                   dx.W, dx.buf, dx.ld, dx.off, *t(res), *t(m), *t(z), *t(z2))
 
     def convT_fwd(self, x: Act, wf, Cout, y: Act, bias=None):
         self.C.convT2x2_fwd(x.buf, x.N, x.H, x.W, x.C, x.ld, x.off, wf, Cout, y.buf, y.ld, y.off, bias)
@@ -69,15 +75,20 @@ class NativeBackend:
                         res.ld if res is not None else 0, res.off if res is not None else 0, bool(relu), y.buf, y.ld,
                         y.off)
 
-    def bn_bwd(self, dy: Act, ymask: Act, x: Act, mean, invstd, gamma, dgamma, dbeta, dx: Act, dyr_out: Act = None):
+    def bn_bwd(self, dy: Act, ymask: Act, x: Act, mean, invstd, gamma, dgamma, dbeta, dx: Act, dyr_out: Act = None,
+               pre=None, k2=1):
         M, Cc = x.rows, x.C
-        nblk = self.C.reduce_blocks(M, Cc)
-        part = torch.empty(nblk, 2, Cc, dtype=torch.float32, device=x.device)
-        self.C.bn_bwd_reduce(dy.buf, dy.ld, dy.off, ymask.buf if ymask is not None else None,
-                             ymask.ld if ymask is not None else 0, ymask.off if ymask is not None else 0, x.buf, x.ld,
-                             x.off, M, Cc, mean, invstd, part, nblk)
         coef = torch.empty(3, Cc, dtype=torch.float32, device=x.device)
-        self.C.bn_bwd_finalize(part, nblk, Cc, float(M), gamma, mean, invstd, dgamma, dbeta, coef)
+        if pre is not None:   # partials {sum dyr, sum dyr*z} came from the producer's dgrad epilogue
+            assert ymask is None
+            self.C.bn_bwd_finalize_fused(pre, k2, Cc, float(M), gamma, mean, invstd, dgamma, dbeta, coef)
+        else:
+            nblk = self.C.reduce_blocks(M, Cc)
+            part = torch.empty(nblk, 2, Cc, dtype=torch.float32, device=x.device)
+            self.C.bn_bwd_reduce(dy.buf, dy.ld, dy.off, ymask.buf if ymask is not None else None,
+                                 ymask.ld if ymask is not None else 0, ymask.off if ymask is not None else 0, x.buf,
+                                 x.ld, x.off, M, Cc, mean, invstd, part, nblk)
+            self.C.bn_bwd_finalize(part, nblk, Cc, float(M), gamma, mean, invstd, dgamma, dbeta, coef)
         assert dx.ld == Cc and dx.off == 0
         if dyr_out is not None:
             assert dyr_out.ld == Cc and dyr_out.off == 0
@@ -220,13 +231,23 @@ class RefBackend:
             out = F.relu(out)
         self._store(y, out)
 
-    def conv_dgrad(self, dy: Act, wT, C, R, S, stride, pad, dx: Act, res=None):
+    def conv_dgrad(self, dy: Act, wT, C, R, S, stride, pad, dx: Act, res=None, fuse=None):
         K = dy.C
         wk = wT.view(C, R, S, K).permute(3, 0, 1, 2).to(self.dt)
         g = torch.nn.grad.conv2d_input((dx.N, C, dx.H, dx.W), wk, dy.nchw().to(self.dt), stride, pad)
         if res is not None:
             g = g + res.nchw().to(self.dt)
+        if fuse is None:
+            self._store(dx, g)
+            return None
+        m, z, z2 = fuse
+        g = g * (m.nchw() > 0)
         self._store(dx, g)
+        v = dx.nhwc().to(self.dt)
+        rows = [v.sum((0, 1, 2)), (v * z.nhwc().to(self.dt)).sum((0, 1, 2))]
+        if z2 is not None:
+            rows.append((v * z2.nhwc().to(self.dt)).sum((0, 1, 2)))
+        return torch.stack(rows).unsqueeze(0)
 
     def convT_fwd(self, x: Act, wf, Cout, y: Act, bias=None):
         Cin = x.C
@@ -273,14 +294,21 @@ class RefBackend:
             v = F.relu(v)
         y.nhwc().copy_(v)
 
-    def bn_bwd(self, dy: Act, ymask, x: Act, mean, invstd, gamma, dgamma, dbeta, dx: Act, dyr_out=None):
+    def bn_bwd(self, dy: Act, ymask, x: Act, mean, invstd, gamma, dgamma, dbeta, dx: Act, dyr_out=None, pre=None,
+               k2=1):
         g = dy.nhwc().to(self.dt)
         if ymask is not None:
             g = g * (ymask.nhwc() > 0)
         M = x.rows
         xhat = (x.nhwc().to(self.dt) - mean) * invstd
-        s1 = g.sum((0, 1, 2))
-        s2 = (g * xhat).sum((0, 1, 2))
+        if pre is not None:
+            assert ymask is None
+            ps = pre.sum(0)
+            s1 = ps[0]
+            s2 = invstd * (ps[k2] - mean * s1)
+        else:
+            s1 = g.sum((0, 1, 2))
+            s2 = (g * xhat).sum((0, 1, 2))
         if dbeta is not None:
             dbeta.add_(s1)
         if dgamma is not None:

@@ -107,3 +107,20 @@ def test_unet_shapes_and_multiclass():
         y = m(torch.randn(1, 3, 32, 32))
         y2 = m.forward_torch(torch.randn(1, 3, 32, 32))
     assert y.shape == (1, 2, 32, 32) == y2.shape
+
+
+def test_resnet50_fused_bn_backward_matches_torch_and_unfused():
+    """BN-backward reductions fused into the dgrad epilogue (incl. the 3-statistic downsample
+    variant) reproduce fp64 autograd and the unfused schedule."""
+    g = torch.Generator().manual_seed(2)
+    x = torch.randn(4, 3, 64, 64, generator=g)
+    y = torch.randint(10, (4,), generator=g)
+    m1 = _run_pair(lambda: resnet50(num_classes=10), x, y, cross_entropy, F.cross_entropy)
+    assert m1.fuse_bn_bwd
+    torch.manual_seed(0)
+    m2 = resnet50(num_classes=10).double()
+    m2.fuse_bn_bwd = False
+    m2.train()
+    cross_entropy(m2(x.double()), y).backward()
+    for (n, p1), (_, p2) in zip(m1.named_parameters(), m2.named_parameters()):
+        assert _err(p1.grad, p2.grad) < 1e-9, n

@@ -90,6 +90,49 @@ def test_conv_dgrad(shape):
     assert _rel(dx.buf, dxr.buf) < 1e-2
 
 
+@pytest.mark.parametrize("shape", [CONV_SHAPES[1], CONV_SHAPES[2], CONV_SHAPES[3], CONV_SHAPES[5]])
+@pytest.mark.parametrize("two", [False, True])
+def test_conv_dgrad_fused_bn_backward(shape, two):
+    """dgrad epilogue: + residual, ReLU mask of the consumer, BN-backward partials
+    {sum dx, sum dx*z [, sum dx*z2]} (multi-phase tile numbering for stride 2), then the
+    finalize/apply path that consumes them."""
+    nb, rb = _be()
+    N, H, W, Cin, K, R, s, p = shape
+    Cp, Kp = pad8(Cin), pad8(K)
+    P, Q = (H + 2 * p - R) // s + 1, (W + 2 * p - R) // s + 1
+    dy, dyr = _act(N, P, Q, Kp)
+    wT = (torch.randn(Cp, R, R, Kp, device=DEV) / (R * R * K) ** 0.5).to(torch.bfloat16)
+    res, resr = _act(N, H, W, Cp)
+    m, mr = _act(N, H, W, Cp)
+    z, zr = _act(N, H, W, Cp)
+    z2, z2r = _act(N, H, W, Cp) if two else (None, None)
+    dx = _empty(N, H, W, Cp)
+    dxr = _empty(N, H, W, Cp, torch.float32)
+    part = nb.conv_dgrad(dy, wT, Cp, R, R, s, p, dx, res=res, fuse=(m, z, z2))
+    rb.conv_dgrad(dyr, wT.float(), Cp, R, R, s, p, dxr, res=resr, fuse=(mr, zr, z2r))
+    torch.cuda.synchronize()
+    assert part.shape[1] == (3 if two else 2) and part.shape[2] == Cp
+    assert _rel(dx.buf, dxr.buf) < 1e-2
+    assert torch.equal(dx.buf == 0, (m.buf <= 0) | (dx.buf == 0))   # masked lanes are exactly zero
+    # partials are sums of the stored bf16 gradient: compare against the same sums in fp64
+    v = dx.buf.double()
+    ref = [v.sum(0), (v * z.buf.double()).sum(0)] + ([(v * z2.buf.double()).sum(0)] if two else [])
+    got = part.double().sum(0)
+    for k, r in enumerate(ref):
+        assert ((got[k] - r).abs().max() / r.abs().max()).item() < 1e-4, k
+    # consumer side: finalize from the fused partials == unfused reduction of the masked grad
+    C = Cp
+    mean, invstd = torch.randn(C, device=DEV) * 0.1, torch.rand(C, device=DEV) + 0.5
+    gamma = torch.rand(C, device=DEV) + 0.5
+    dg1, db1, dg2, db2 = (torch.zeros(C, device=DEV) for _ in range(4))
+    o1, o2 = _empty(N, H, W, C), _empty(N, H, W, C)
+    nb.bn_bwd(dx, None, z, mean, invstd, gamma, dg1, db1, o1, pre=part, k2=1)
+    nb.bn_bwd(dx, None, z, mean, invstd, gamma, dg2, db2, o2)
+    torch.cuda.synchronize()
+    assert _rel(db1, db2) < 1e-4 and _rel(dg1, dg2) < 1e-3
+    assert _rel(o1.buf, o2.buf) < 1e-2
+
+
 @pytest.mark.parametrize("shape", CONV_SHAPES)
 def test_conv_wgrad(shape):
     nb, rb = _be()
