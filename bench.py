@@ -1,12 +1,21 @@
-"""Headline benchmark: ResNet-50 DDP training throughput, images/sec for the whole job.
+"""Benchmark harness: DDP training throughput, images/sec for the whole job.
 
-Config (BASELINE.json): ResNet-50, bs=256 per GPU, 3x224x224 synthetic ImageNet-shaped data,
-random-init weights, bf16 compute (fp32 master weights, fp32 gradient all-reduce), SGD momentum
-0.9 / wd 1e-5 (the reference optimizer, /root/reference/pytorch/resnet/main.py:114), one process
-per GPU over RCCL.  Every timed step is a full training step: forward, loss, backward with
-bucketed gradient all-reduce, optimizer update.
+Default = the headline config of BASELINE.json: ResNet-50, bs=256 per GPU, 3x224x224 synthetic
+ImageNet-shaped data, random-init weights, bf16 compute (fp32 master weights, fp32 gradient
+all-reduce), SGD momentum 0.9 / wd 1e-5 (the reference optimizer,
+/root/reference/pytorch/resnet/main.py:114), one process per GPU over RCCL.  Every timed step is
+a full training step: forward, loss, backward with bucketed gradient all-reduce, optimizer update.
 
-Usage:  python bench.py [--gpus N] [--steps K] [--warmup W]
+The other BASELINE.json configs are presets (``--config``):
+  resnet50        ResNet-50  bs=256/GPU 3x224x224, SGD, CE            (headline, default)
+  resnet152       ResNet-152 bs=128/GPU 3x224x224, SGD, CE            (config 4)
+  unet512         UNet bs=16/GPU 3x512x512 binary masks, Adam + BCE + clip 1.0  (config 3;
+                  /root/reference/pytorch/unet/train.py:160-194, batch default :319)
+  unet1024        UNet in_channels=1 bs=16/GPU 1x1024x1024, Adam + BCE + clip  (config 5)
+  resnet18_cifar  ResNet-18 bs=128/GPU 3x32x32, 10 classes (the reference's own CIFAR run,
+                  /root/reference/pytorch/resnet/main.py:36-54,164)
+
+Usage:  python bench.py [--gpus N] [--steps K] [--warmup W] [--config NAME] [--graph 1]
         (N > 1: launched by torch.distributed.run / torchrun or mpirun, one rank per GPU)
 Prints ONE JSON line on rank 0.
 """
@@ -24,45 +33,83 @@ if ROOT not in sys.path:
 
 BASELINE_VALUE = None   # the reference publishes no number
 
+PRESETS = {
+    "resnet50": dict(task="cls", arch="resnet50", batch=256, image=224, classes=1000, cin=3,
+                     metric="images/sec (whole node) ResNet-50 DDP bs=256/GPU"),
+    "resnet152": dict(task="cls", arch="resnet152", batch=128, image=224, classes=1000, cin=3,
+                      metric="images/sec (whole node) ResNet-152 DDP bs=128/GPU"),
+    "resnet18_cifar": dict(task="cls", arch="resnet18", batch=128, image=32, classes=10, cin=3,
+                           metric="images/sec (whole node) ResNet-18 CIFAR-10 DDP bs=128/GPU"),
+    "unet512": dict(task="seg", arch="unet", batch=16, image=512, classes=1, cin=3,
+                    metric="images/sec (whole node) UNet-2D 3x512x512 DDP bs=16/GPU"),
+    "unet1024": dict(task="seg", arch="unet", batch=16, image=1024, classes=1, cin=1,
+                     metric="images/sec (whole node) UNet-2D 1x1024x1024 DDP bs=16/GPU"),
+}
+
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--arch", default="resnet50")
-    ap.add_argument("--batch", type=int, default=256, help="per-GPU batch")
-    ap.add_argument("--image", type=int, default=224)
-    ap.add_argument("--classes", type=int, default=1000)
+    ap.add_argument("--config", default="resnet50", choices=sorted(PRESETS))
+    ap.add_argument("--arch", default=None, help="override the preset's model")
+    ap.add_argument("--batch", type=int, default=None, help="per-GPU batch (override)")
+    ap.add_argument("--image", type=int, default=None)
+    ap.add_argument("--classes", type=int, default=None)
     ap.add_argument("--bucket_mb", type=float, default=None)
-    ap.add_argument("--profile_steps", type=int, default=0, help="print a per-phase breakdown")
+    ap.add_argument("--graph", type=int, default=0, help="1: replay the whole step from a captured hipGraph")
     args = ap.parse_args()
+    cfg = dict(PRESETS[args.config])
+    for k in ("arch", "batch", "image", "classes"):
+        if getattr(args, k) is not None:
+            cfg[k] = getattr(args, k)
 
     import torch
 
     import deeplearning_mpi_amd as dl
     from deeplearning_mpi_amd.data import device_batch
-    from deeplearning_mpi_amd.models import ARCHS
-    from deeplearning_mpi_amd.ops import CrossEntropyLoss
-    from deeplearning_mpi_amd.optim import SGD
+    from deeplearning_mpi_amd.models import ARCHS, UNet
+    from deeplearning_mpi_amd.ops import BCEWithLogitsLoss, CrossEntropyLoss
+    from deeplearning_mpi_amd.optim import SGD, Adam, clip_grad_norm_
 
     comm = dl.init_distributed("rccl")
     world = comm.world_size
     dev = comm.device
     torch.manual_seed(0)
-    model = ARCHS[args.arch](num_classes=args.classes).to(dev)
+    shape = (cfg["cin"], cfg["image"], cfg["image"])
+    if cfg["task"] == "cls":
+        model = ARCHS[cfg["arch"]](num_classes=cfg["classes"]).to(dev)
+        opt = SGD(model.parameters(), lr=0.1, momentum=0.9, weight_decay=1e-5)
+        crit = CrossEntropyLoss()
+        x, y = device_batch("classification", cfg["batch"], dev, shape, cfg["classes"], seed=1234 + comm.rank)
+        optname = "SGD(momentum=0.9, wd=1e-5)"
+    else:
+        model = UNet(out_classes=1, in_channels=cfg["cin"]).to(dev)
+        opt = Adam(model.parameters(), lr=1e-4)
+        crit = BCEWithLogitsLoss()
+        x, y = device_batch("segmentation", cfg["batch"], dev, shape, seed=1234 + comm.rank)
+        optname = "Adam(lr=1e-4) + clip_grad_norm(1.0)"
     ddp = dl.DistributedDataParallel(model, bucket_cap_mb=args.bucket_mb)
-    opt = SGD(model.parameters(), lr=0.1, momentum=0.9, weight_decay=1e-5)
-    crit = CrossEntropyLoss()
-    x, y = device_batch("classification", args.batch, dev, (3, args.image, args.image), args.classes,
-                        seed=1234 + comm.rank)
 
     def step():
         opt.zero_grad()
-        loss = crit(ddp(x), y)
-        loss.backward()
+        out = ddp(x)
+        if cfg["task"] == "cls":
+            loss = crit(out, y)
+            loss.backward()
+        else:
+            loss = crit(out.squeeze(1), y)
+            loss.backward()
+            clip_grad_norm_(model.parameters(), 1.0, optimizer=opt)
         opt.step()
         return loss
+
+    if args.graph:
+        from deeplearning_mpi_amd.utils.graphs import CapturedStep
+
+        step = CapturedStep(step, warmup=2, inputs=(x, y))
+        args.warmup = max(args.warmup, 3)   # 2 eager warmup calls + the capturing call stay untimed
 
     for _ in range(args.warmup):
         step()
@@ -78,11 +125,12 @@ def main():
     comm.allreduce(tmax, "max")
     dt = float(tmax.item())
     lossv = float(loss.item())
-    global_batch = args.batch * world
+    global_batch = cfg["batch"] * world
     ips = global_batch * args.steps / dt
     if comm.rank == 0:
+        headline = args.config == "resnet50" and cfg == PRESETS["resnet50"]
         print(json.dumps({
-            "metric": "images/sec (whole node) ResNet-50 DDP bs=256/GPU",
+            "metric": cfg["metric"],
             "value": round(ips, 2),
             "unit": "images/sec",
             "n_gpus": world,
@@ -91,12 +139,13 @@ def main():
             "ms_per_step": round(dt / args.steps * 1000, 3),
             "higher_is_better": True,
             "scaling": "weak",
-            "vs_baseline": (round(ips / BASELINE_VALUE, 4) if BASELINE_VALUE else None),
+            "vs_baseline": (round(ips / BASELINE_VALUE, 4) if (BASELINE_VALUE and headline) else None),
             "dtype": "bf16",
-            "data": "synthetic (random 3x224x224 images / labels generated on device, random-init weights)",
-            "config": {"model": args.arch, "global_batch": global_batch, "seq_len": None,
-                       "image": args.image, "per_gpu_batch": args.batch,
-                       "parallelism": f"dp{world}", "optimizer": "SGD(momentum=0.9, wd=1e-5)",
+            "data": f"synthetic (random {'x'.join(map(str, shape))} inputs / "
+                    f"{'labels' if cfg['task'] == 'cls' else 'binary masks'} generated on device, random-init weights)",
+            "config": {"model": cfg["arch"], "global_batch": global_batch, "seq_len": None,
+                       "image": cfg["image"], "in_channels": cfg["cin"], "per_gpu_batch": cfg["batch"],
+                       "parallelism": f"dp{world}", "optimizer": optname, "hipgraph": bool(args.graph),
                        "final_loss": round(lossv, 4)},
         }), flush=True)
     dl.destroy_distributed()

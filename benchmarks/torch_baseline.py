@@ -1,10 +1,11 @@
-"""Stock PyTorch-ROCm baseline for the headline config (the "reference on MI355X" bar of
-BASELINE.md): the same torchvision-identical ResNet-50 parameters run through eager torch.nn
-(MIOpen convs, channels_last, torch.autocast bf16), torch DDP over the nccl(=RCCL) backend,
-torch.optim.SGD(momentum=0.9, weight_decay=1e-5) -- i.e. what /root/reference/pytorch/resnet/main.py
-does, at bs=256/GPU on 224x224 synthetic data.
+"""Stock PyTorch-ROCm baseline for the bench.py configs (the "reference on MI355X" bar of
+BASELINE.md): the same parameters run through eager torch.nn (MIOpen convs, channels_last,
+torch.autocast bf16), torch DDP over the nccl(=RCCL) backend, and the reference optimizers --
+torch.optim.SGD(momentum=0.9, weight_decay=1e-5) for ResNet (/root/reference/pytorch/resnet/main.py:114),
+torch.optim.Adam + BCEWithLogits + clip_grad_norm_(1.0) for UNet (/root/reference/pytorch/unet/train.py:160-194).
 
-python benchmarks/torch_baseline.py [--steps K] [--warmup W] [--batch B]   (torchrun for N > 1)
+python benchmarks/torch_baseline.py [--config resnet50|resnet152|resnet18_cifar|unet512|unet1024]
+                                    [--steps K] [--warmup W] [--batch B]      (torchrun for N > 1)
 """
 import argparse
 import json
@@ -12,22 +13,29 @@ import os
 import sys
 import time
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
 
 
 def main():
+    from bench import PRESETS
+
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--batch", type=int, default=256)
-    ap.add_argument("--arch", default="resnet50")
+    ap.add_argument("--config", default="resnet50", choices=sorted(PRESETS))
+    ap.add_argument("--batch", type=int, default=None)
     ap.add_argument("--no_channels_last", action="store_true")
     args = ap.parse_args()
+    cfg = dict(PRESETS[args.config])
+    if args.batch:
+        cfg["batch"] = args.batch
     import torch
     import torch.distributed as dist
     import torch.nn as nn
+    import torch.nn.functional as F
 
-    from deeplearning_mpi_amd.models import ARCHS
+    from deeplearning_mpi_amd.models import ARCHS, UNet
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -36,8 +44,13 @@ def main():
     dev = torch.device("cuda", lrank)
     if world > 1:
         dist.init_process_group("nccl")
-    torch.backends.cudnn.benchmark = True
-    model = ARCHS[args.arch](num_classes=1000).to(dev)
+    # MIOpen exhaustive find (benchmark=True) on the UNet's 512^2 / 1024^2 shapes runs for many
+    # minutes; the classification nets use it (as the reference's main.py:31 does)
+    torch.backends.cudnn.benchmark = cfg["task"] == "cls"
+    torch.manual_seed(0)
+    seg = cfg["task"] == "seg"
+    model = (UNet(out_classes=1, in_channels=cfg["cin"]) if seg else ARCHS[cfg["arch"]](num_classes=cfg["classes"]))
+    model = model.to(dev)
 
     class Eager(nn.Module):
         def __init__(self, m):
@@ -48,28 +61,40 @@ def main():
             return self.m.forward_torch(x)
 
     net = Eager(model)
-    if not args.no_channels_last:
+    cl = not args.no_channels_last
+    if cl:
         net = net.to(memory_format=torch.channels_last)
     if world > 1:
         net = nn.parallel.DistributedDataParallel(net, device_ids=[lrank])
-    opt = torch.optim.SGD(net.parameters(), lr=0.1, momentum=0.9, weight_decay=1e-5)
-    crit = nn.CrossEntropyLoss()
-    x = torch.randn(args.batch, 3, 224, 224, device=dev)
-    if not args.no_channels_last:
+    B, S, C = cfg["batch"], cfg["image"], cfg["cin"]
+    x = torch.randn(B, C, S, S, device=dev)
+    if cl:
         x = x.to(memory_format=torch.channels_last)
-    y = torch.randint(1000, (args.batch,), device=dev)
+    if seg:
+        opt = torch.optim.Adam(net.parameters(), lr=1e-4)
+        y = (torch.rand(B, S, S, device=dev) > 0.5).float()
+    else:
+        opt = torch.optim.SGD(net.parameters(), lr=0.1, momentum=0.9, weight_decay=1e-5)
+        y = torch.randint(cfg["classes"], (B,), device=dev)
 
     def step():
         opt.zero_grad()
         with torch.autocast("cuda", dtype=torch.bfloat16):
             out = net(x)
-            loss = crit(out, y)
-        loss.backward()
+        if seg:
+            loss = F.binary_cross_entropy_with_logits(out.float().squeeze(1), y)
+            loss.backward()
+            torch.nn.utils.clip_grad_norm_(net.parameters(), 1.0)
+        else:
+            loss = F.cross_entropy(out.float(), y)
+            loss.backward()
         opt.step()
         return loss
 
-    for _ in range(args.warmup):
+    for i in range(args.warmup):
         step()
+        torch.cuda.synchronize()
+        print(f"warmup step {i} done", file=sys.stderr, flush=True)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -81,10 +106,10 @@ def main():
         dist.barrier()
     dt = time.perf_counter() - t0
     if rank == 0:
-        print(json.dumps({"metric": "images/sec stock PyTorch DDP (MIOpen, autocast bf16, channels_last)",
-                          "value": round(args.batch * world * args.steps / dt, 2), "n_gpus": world,
-                          "ms_per_step": round(dt / args.steps * 1000, 3), "arch": args.arch,
-                          "per_gpu_batch": args.batch, "loss": round(float(loss.item()), 4)}), flush=True)
+        print(json.dumps({"metric": "stock PyTorch DDP (MIOpen, autocast bf16, channels_last): " + cfg["metric"],
+                          "value": round(B * world * args.steps / dt, 2), "n_gpus": world,
+                          "ms_per_step": round(dt / args.steps * 1000, 3), "config": args.config,
+                          "per_gpu_batch": B, "loss": round(float(loss.item()), 4)}), flush=True)
     if world > 1:
         dist.destroy_process_group()
 

@@ -56,9 +56,15 @@ __device__ __forceinline__ void adam_elem(float& p, float g, float& m, float& v,
 __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, const float* __restrict__ g,
                                                    float* __restrict__ m, float* __restrict__ v, int64_t n, float lr,
                                                    float b1, float b2, float eps, float wd, int adamw, float bc1,
-                                                   float bc2, const float* __restrict__ clip_coef) {
+                                                   float bc2, const float* __restrict__ clip_coef,
+                                                   const float* __restrict__ tstep) {
   const float coef = clip_coef ? clip_coef[0] : 1.f;
   if (clip_coef && clip_coef[1] != 0.f) return;   // non-finite gradient norm: collective skip
+  if (tstep) {   // step count on the device: bias corrections stay correct under hipGraph replay
+    const float t = *tstep;
+    bc1 = 1.f - powf(b1, t);
+    bc2 = 1.f - powf(b2, t);
+  }
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     float pv = p[i], mv = m[i], vv = v[i];
     adam_elem(pv, g[i], mv, vv, lr, b1, b2, eps, wd, adamw, bc1, bc2, coef);
@@ -129,9 +135,9 @@ extern "C" hipError_t dlmpi_sgd(float* p, const float* g, float* m, int64_t n, f
 }
 extern "C" hipError_t dlmpi_adam(float* p, const float* g, float* m, float* v, int64_t n, float lr, float b1, float b2,
                                  float eps, float wd, int adamw, float bc1, float bc2, const float* clip_coef,
-                                 hipStream_t s) {
+                                 const float* tstep, hipStream_t s) {
   hipLaunchKernelGGL(adam_kernel, dim3(blocks_for(n)), dim3(256), 0, s, p, g, m, v, n, lr, b1, b2, eps, wd, adamw,
-                     bc1, bc2, clip_coef);
+                     bc1, bc2, clip_coef, tstep);
   return hipGetLastError();
 }
 extern "C" hipError_t dlmpi_sumsq(const float* x, int64_t n, float* partial, int nblk, hipStream_t s) {

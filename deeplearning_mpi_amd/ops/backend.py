@@ -186,8 +186,8 @@ class NativeBackend:
     def sgd(self, p, g, m, lr, momentum, dampening, wd, nesterov, first, skip_flag=None):
         self.C.sgd_step(p, g, m, lr, momentum, dampening, wd, nesterov, first, skip_flag)
 
-    def adam(self, p, g, m, v, lr, b1, b2, eps, wd, adamw, bc1, bc2, clip=None):
-        self.C.adam_step(p, g, m, v, lr, b1, b2, eps, wd, adamw, bc1, bc2, clip)
+    def adam(self, p, g, m, v, lr, b1, b2, eps, wd, adamw, bc1, bc2, clip=None, tstep=None):
+        self.C.adam_step(p, g, m, v, lr, b1, b2, eps, wd, adamw, bc1, bc2, clip, tstep)
 
     def grad_norm(self, g, max_norm, norm_out, coef_out):
         self.C.grad_norm(g, max_norm, norm_out, coef_out)
@@ -400,12 +400,15 @@ class RefBackend:
             d = d + momentum * m if nesterov else m
         p.add_(d, alpha=-lr)
 
-    def adam(self, p, g, m, v, lr, b1, b2, eps, wd, adamw, bc1, bc2, clip=None):
+    def adam(self, p, g, m, v, lr, b1, b2, eps, wd, adamw, bc1, bc2, clip=None, tstep=None):
         coef = 1.0
         if clip is not None:
             if float(clip[1]) != 0:
                 return
             coef = clip[0]
+        if tstep is not None:
+            t = float(tstep.reshape(-1)[0])
+            bc1, bc2 = 1 - b1 ** t, 1 - b2 ** t
         g = g * coef
         if wd != 0:
             if adamw:

@@ -107,8 +107,14 @@ class Adam(_FusedBase):
             b1, b2 = g["betas"]
             m = self._buf(key, "exp_avg", p)
             v = self._buf(key, "exp_avg_sq", p)
+            # the step count also lives on the device (read by the kernel), so a captured step
+            # replayed from a hipGraph keeps correct bias corrections
+            st = self.state[key] if not isinstance(key, str) else self.state.setdefault(key, {})
+            if "step" not in st:
+                st["step"] = torch.zeros(1, dtype=torch.float32, device=p.device)
+            st["step"].add_(1)
             self._be.adam(p, gr, m, v, g["lr"], b1, b2, g["eps"], g["weight_decay"], self.decoupled,
-                          1 - b1 ** t, 1 - b2 ** t, self.clip)
+                          1 - b1 ** t, 1 - b2 ** t, self.clip, st["step"])
         if self._arena is not None:
             self._arena.mark_updated()
         return loss
@@ -143,6 +149,6 @@ def clip_grad_norm_(parameters, max_norm: float, norm_type: float = 2.0, optimiz
             be.scale_(p.grad.view(-1), coef)
     if optimizer is not None and hasattr(optimizer, "clip"):
         c = coef.clone()
-        c[0] = 1.0 if a is not None else 1.0   # grads already scaled in place; keep only the skip flag
+        c[:1].fill_(1.0)   # grads already scaled in place; keep only the skip flag (a kernel: capturable)
         optimizer.clip = c
     return norm[0]
