@@ -44,6 +44,26 @@ def resnet50_shapes(N, img=224):
     return Counter(shapes)
 
 
+def unet_shapes(N, img=512, cin=3):
+    """3x3 convs of the reference UNet (/root/reference/pytorch/unet/model.py:51-81) + the 1x1 head."""
+    sh = Counter()
+    h, c = img, cin
+    for co in (64, 128, 256, 512):
+        sh[(N, h, h, c, co, 3, 1, 1)] += 1
+        sh[(N, h, h, co, co, 3, 1, 1)] += 1
+        c, h = co, h // 2
+    sh[(N, h, h, 512, 1024, 3, 1, 1)] += 1
+    sh[(N, h, h, 1024, 1024, 3, 1, 1)] += 1
+    c = 1024
+    for co in (512, 256, 128, 64):
+        h *= 2
+        sh[(N, h, h, c, co, 3, 1, 1)] += 1    # after concat: (c - co) up + co skip = c channels
+        sh[(N, h, h, co, co, 3, 1, 1)] += 1
+        c = co
+    sh[(N, h, h, 64, 1, 1, 1, 0)] += 1
+    return sh
+
+
 def timeit(fn, iters):
     for _ in range(3):
         fn()
@@ -63,7 +83,13 @@ def main():
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--only", default=None)
     ap.add_argument("--no_miopen", action="store_true")
+    ap.add_argument("--net", default="resnet50", choices=["resnet50", "unet512"])
+    ap.add_argument("--stages", type=int, default=None, help="DLMPI_CONV_STAGES for our kernels")
     args = ap.parse_args()
+    if args.stages:
+        os.environ["DLMPI_CONV_STAGES"] = str(args.stages)
+    if args.net == "unet512" and args.batch == 256:
+        args.batch = 16
     from deeplearning_mpi_amd.ops.act import Act, padc
     from deeplearning_mpi_amd.ops.backend import NativeBackend
 
@@ -71,7 +97,8 @@ def main():
     dev = "cuda"
     torch.backends.cudnn.benchmark = True
     tot = Counter()
-    for shape, cnt in sorted(resnet50_shapes(args.batch).items(), key=lambda kv: -kv[1]):
+    shapes = resnet50_shapes(args.batch) if args.net == "resnet50" else unet_shapes(args.batch)
+    for shape, cnt in sorted(shapes.items(), key=lambda kv: -kv[1]):
         N, H, W, Cin, K, R, s, p = shape
         Cp, Kp = padc(Cin), padc(K)
         P = (H + 2 * p - R) // s + 1

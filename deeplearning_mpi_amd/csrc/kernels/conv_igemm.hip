@@ -21,6 +21,8 @@
 // Epilogue: the fp32 tile is staged through LDS for 16-byte stores with fused bias / residual
 // add / folded-BN affine / ReLU and the per-channel BatchNorm partial sums of the stored
 // (bf16-rounded) values.
+#include <cstdlib>
+
 #include "common.h"
 
 namespace dlmpi {
@@ -31,17 +33,23 @@ __device__ __forceinline__ void glds16(const void* g, char* lds_wave_base) {
   __builtin_amdgcn_global_load_lds(g, (lds_void*)lds_wave_base, 16, 0, 0);
 }
 
-template <int BM, int BN, bool SMALLC>
-__global__ __launch_bounds__(256) void conv_igemm_kernel(const ConvArgs a) {
+// STAGES = 2: double-buffered K loop (one barrier per K-step, 2 blocks/CU at 128x128);
+// STAGES = 1: single buffer, two barriers per K-step, 34 KB of LDS -> 4 blocks/CU (latency hidden
+// across blocks instead of inside one).  The epilogue stages the fp32 tile through LDS in two
+// row halves so it never needs more LDS than one stage.
+template <int BM, int BN, bool SMALLC, int STAGES>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(STAGES == 1 ? 3 : 2, 8))) void conv_igemm_kernel(const ConvArgs a) {
   constexpr int BK = 64;
   constexpr int WM = BM / 2, WN = BN / 2;
   constexpr int TM = WM / 16, TN = WN / 16;
   constexpr int AL = BM / 32, BL = BN / 32;   // 16-byte pieces per thread per tile
   constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2;
-  constexpr int STAGE_BYTES = 2 * (A_BYTES + B_BYTES);
+  constexpr int STAGE_BYTES = STAGES * (A_BYTES + B_BYTES);
   constexpr int CS_LD = BN + 4;
-  constexpr int EPI_BYTES = BM * CS_LD * 4;
-  constexpr int SMEM = STAGE_BYTES > EPI_BYTES ? STAGE_BYTES : EPI_BYTES;
+  constexpr int EPI_BYTES = (BM / 2) * CS_LD * 4;
+  constexpr int RED_BYTES = (256 / (BN / 8)) * 3 * BN * 4;   // stats combine
+  constexpr int SMEM0 = STAGE_BYTES > EPI_BYTES ? STAGE_BYTES : EPI_BYTES;
+  constexpr int SMEM = SMEM0 > RED_BYTES ? SMEM0 : RED_BYTES;
   __shared__ __attribute__((aligned(16))) char smem[SMEM];
 
   const ConvPhase ph = a.ph[blockIdx.z];
@@ -156,24 +164,34 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(const ConvArgs a) {
 #pragma unroll
     for (int ni = 0; ni < TN; ++ni) acc[mi][ni] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+  const int fr = lane & 15, fg = lane >> 4;
+  auto advance = [&]() {
+    if constexpr (!SMALLC) {
+      c_cur += 64;
+      if (c_cur >= C) {
+        c_cur = 0;
+        ++t_cur;
+        tap_setup(t_cur);
+      }
+    }
+  };
   if (nk > 0) {
     if constexpr (!SMALLC) tap_setup(0);
     issue(0, 0);
     __syncthreads();
   }
-  const int fr = lane & 15, fg = lane >> 4;
   for (int ks = 0; ks < nk; ++ks) {
-    const int cur = ks & 1;
-    if (ks + 1 < nk) {
-      if constexpr (!SMALLC) {
-        c_cur += 64;
-        if (c_cur >= C) {
-          c_cur = 0;
-          ++t_cur;
-          tap_setup(t_cur);
-        }
+    int cur = 0;
+    if constexpr (STAGES == 2) {
+      cur = ks & 1;
+      if (ks + 1 < nk) {
+        advance();
+        issue(cur ^ 1, ks + 1);
       }
-      issue(cur ^ 1, ks + 1);
+    } else if (ks > 0) {
+      advance();
+      issue(0, ks);
+      __syncthreads();   // this stage landed (vmcnt(0) + barrier)
     }
     const char* As = smem + cur * (A_BYTES + B_BYTES);
     const char* Bs = As + A_BYTES;
@@ -197,49 +215,52 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(const ConvArgs a) {
         for (int ni = 0; ni < TN; ++ni)
           acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[mi], bfr[ni], acc[mi][ni], 0, 0, 0);
     }
-    __syncthreads();   // (waits for this wave's glds of tile ks+1, then all waves) -> buffers swap
+    // STAGES 2: waits for this wave's glds of tile ks+1, then all waves -> buffers swap;
+    // STAGES 1: every wave is done reading the stage before it is overwritten
+    __syncthreads();
   }
 
   // ---- epilogue ------------------------------------------------------------------------------
   float* Cs = reinterpret_cast<float*>(smem);
-#pragma unroll
-  for (int mi = 0; mi < TM; ++mi)
-#pragma unroll
-    for (int ni = 0; ni < TN; ++ni)
-#pragma unroll
-      for (int r = 0; r < 4; ++r)
-        Cs[(wm * WM + mi * 16 + fg * 4 + r) * CS_LD + wn * WN + ni * 16 + fr] = acc[mi][ni][r];
-  __syncthreads();
 
   constexpr int CG = BN / 8;       // channel groups of 8
   constexpr int RG = 256 / CG;     // row groups
   const int cg = tid % CG, rg = tid / CG;
   const int c0 = n0 + cg * 8;
   const bool cvalid = c0 < a.Kout;
-  float bias[8], scl[8], sft[8];
+  float bias[8];
 #pragma unroll
-  for (int e = 0; e < 8; ++e) { bias[e] = 0.f; scl[e] = 1.f; sft[e] = 0.f; }
-  if (cvalid) {
-    if (a.bias) {
+  for (int e = 0; e < 8; ++e) bias[e] = 0.f;
+  if (cvalid && a.bias) {
 #pragma unroll
-      for (int e = 0; e < 8; ++e) bias[e] = a.bias[c0 + e];
-    }
-    if (a.scale) {
-#pragma unroll
-      for (int e = 0; e < 8; ++e) { scl[e] = a.scale[c0 + e]; sft[e] = a.shift[c0 + e]; }
-    }
+    for (int e = 0; e < 8; ++e) bias[e] = a.bias[c0 + e];
   }
   float s1[8], s2[8], s3[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) { s1[e] = 0.f; s2[e] = 0.f; s3[e] = 0.f; }
   const bool bwd = a.mask != nullptr;   // gradient of a BN+ReLU output: mask, then {sum dy, sum dy*z}
 
-  for (int r = rg; r < BM; r += RG) {
+  // Two passes over row halves: in pass h every wave dumps its fragments mi in
+  // [h*TM/2, (h+1)*TM/2), i.e. tile rows wm*WM + h*WM/2 + [0, WM/2), into a BM/2-row buffer.
+  constexpr int HM = WM / 2, HT = TM / 2;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+  if (h) __syncthreads();         // every thread is done with pass 0
+#pragma unroll
+  for (int mi = 0; mi < HT; ++mi)
+#pragma unroll
+    for (int ni = 0; ni < TN; ++ni)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        Cs[(wm * HM + mi * 16 + fg * 4 + r) * CS_LD + wn * WN + ni * 16 + fr] = acc[h * HT + mi][ni][r];
+  __syncthreads();
+  for (int rr = rg; rr < BM / 2; rr += RG) {
+    const int r = (rr / HM) * WM + h * HM + (rr % HM);
     const int m = m0 + r;
     if (m >= M || !cvalid) continue;
     float v[8];
-    const f32x4 v0 = *reinterpret_cast<const f32x4*>(Cs + r * CS_LD + cg * 8);
-    const f32x4 v1 = *reinterpret_cast<const f32x4*>(Cs + r * CS_LD + cg * 8 + 4);
+    const f32x4 v0 = *reinterpret_cast<const f32x4*>(Cs + rr * CS_LD + cg * 8);
+    const f32x4 v1 = *reinterpret_cast<const f32x4*>(Cs + rr * CS_LD + cg * 8 + 4);
 #pragma unroll
     for (int e = 0; e < 4; ++e) { v[e] = v0[e] + bias[e]; v[e + 4] = v1[e] + bias[e + 4]; }
     if (a.stats && !bwd) {
@@ -252,7 +273,7 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(const ConvArgs a) {
     }
     if (a.scale) {
 #pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] = v[e] * scl[e] + sft[e];
+      for (int e = 0; e < 8; ++e) v[e] = v[e] * a.scale[c0 + e] + a.shift[c0 + e];
     }
     const uint32_t n_img = fdiv((uint32_t)m, ph.fdPQ);
     const uint32_t rem = (uint32_t)m - n_img * PQ;
@@ -308,6 +329,7 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(const ConvArgs a) {
       }
     }
   }
+  }
 
   if (a.stats) {
     __syncthreads();
@@ -339,10 +361,24 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(const ConvArgs a) {
 
 using namespace dlmpi;
 
+static int stages_choice() {
+  static int v = [] {
+    const char* e = getenv("DLMPI_CONV_STAGES");
+    return e ? atoi(e) : 1;
+  }();
+  return v;
+}
+
 template <int BM, int BN>
 static void launch_tile(const ConvArgs* a, dim3 grid, hipStream_t s) {
-  if (a->C < 64) hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, true>), grid, dim3(256), 0, s, *a);
-  else hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, false>), grid, dim3(256), 0, s, *a);
+  const bool one = stages_choice() == 1;
+  if (a->C < 64) {
+    if (one) hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, true, 1>), grid, dim3(256), 0, s, *a);
+    else hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, true, 2>), grid, dim3(256), 0, s, *a);
+  } else {
+    if (one) hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, false, 1>), grid, dim3(256), 0, s, *a);
+    else hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, false, 2>), grid, dim3(256), 0, s, *a);
+  }
 }
 
 extern "C" hipError_t dlmpi_conv_igemm(const ConvArgs* a, int bm, int bn, hipStream_t s) {
