@@ -85,9 +85,13 @@ def main():
     ap.add_argument("--no_miopen", action="store_true")
     ap.add_argument("--net", default="resnet50", choices=["resnet50", "unet512"])
     ap.add_argument("--stages", type=int, default=None, help="DLMPI_CONV_STAGES for our kernels")
+    ap.add_argument("--bm256_min_tiles", type=int, default=None, help="DLMPI_CONV_BM256_MIN_TILES")
     args = ap.parse_args()
     if args.stages:
         os.environ["DLMPI_CONV_STAGES"] = str(args.stages)
+        os.environ["DLMPI_WGRAD_STAGES"] = str(args.stages)
+    if args.bm256_min_tiles is not None:
+        os.environ["DLMPI_CONV_BM256_MIN_TILES"] = str(args.bm256_min_tiles)
     if args.net == "unet512" and args.batch == 256:
         args.batch = 16
     from deeplearning_mpi_amd.ops.act import Act, padc
@@ -110,7 +114,7 @@ def main():
         dx = Act.empty(N, H, W, Cp, torch.bfloat16, dev)
         wT = (torch.randn(Cp, R, R, Kp, device=dev) * 0.05).to(torch.bfloat16)
         g = torch.zeros(K * R * R * Cin, device=dev)
-        mt = be.conv_mtiles(N, H, W, Kp, R, R, s, p)
+        mt = be.conv_mtiles(N, H, W, Cp, Kp, R, R, s, p)
         st = torch.empty(mt, 2, Kp, device=dev)
         ours = {
             "fwd": lambda: be.conv_fwd(x, w, Kp, R, R, s, p, y, stats=st),

@@ -54,11 +54,25 @@ static void set_kstep(ConvArgs& a, int C) {
   }
 }
 
-static void pick_tiles(int64_t M, int Kout, int& bm, int& bn) {
+// Tile choice.  256x128 (per-wave 128x64: 25 % less LDS traffic per MFMA than 128x128) wins on
+// long reductions into wide outputs (UNet 3x3 convs with >= 256 channels: up to 1.3x, measured by
+// benchmarks/conv_bench.py) and loses on the short / memory-bound ResNet GEMMs; 64-row tiles for
+// small grids.  `red` = GEMM reduction length (R*S*C).
+static int bm256_min_tiles() {
+  static int v = [] {
+    const char* e = getenv("DLMPI_CONV_BM256_MIN_TILES");
+    return e ? atoi(e) : 256;
+  }();
+  return v;
+}
+
+static void pick_tiles(int64_t M, int Kout, int64_t red, int& bm, int& bn) {
   bn = Kout <= 64 ? 64 : 128;
   bm = 128;
-  const int64_t tiles = ((M + 127) / 128) * ((Kout + bn - 1) / bn);
-  if (tiles < 512) bm = 64;
+  const int64_t nt = (Kout + bn - 1) / bn;
+  const int64_t tiles = ((M + 127) / 128) * nt;
+  if (Kout >= 256 && red >= 2304 && ((M + 255) / 256) * nt >= bm256_min_tiles()) bm = 256;
+  else if (tiles < 512) bm = 64;
 }
 
 static void finish_phase(ConvPhase& p, int Nimg, int C, int bm) {
@@ -112,7 +126,7 @@ int conv2d_fwd(const at::Tensor& x, int N, int H, int W, int C, int ldx, int xof
   a.vec_store = (a.kvalid == a.Kout && (ldy % 8) == 0 && (yoff % 8) == 0) ? 1 : 0;
   set_kstep(a, C);
   int bm, bn;
-  pick_tiles((int64_t)N * P * Q, K, bm, bn);
+  pick_tiles((int64_t)N * P * Q, K, (int64_t)R * S * C, bm, bn);
   if (bm_req > 0) bm = bm_req;
   a.ntiles = ceil_div(K, bn);
   a.nphase = 1;
@@ -127,10 +141,10 @@ int conv2d_fwd(const at::Tensor& x, int N, int H, int W, int C, int ldx, int xof
 }
 
 // Number of BN-stat partial rows conv2d_fwd will produce (so the caller can size `stats`).
-int conv2d_fwd_mtiles(int N, int H, int W, int K, int R, int S, int stride, int pad, int bm_req) {
+int conv2d_fwd_mtiles(int N, int H, int W, int C, int K, int R, int S, int stride, int pad, int bm_req) {
   const int P = (H + 2 * pad - R) / stride + 1, Q = (W + 2 * pad - S) / stride + 1;
   int bm, bn;
-  pick_tiles((int64_t)N * P * Q, K, bm, bn);
+  pick_tiles((int64_t)N * P * Q, K, (int64_t)R * S * C, bm, bn);
   if (bm_req > 0) bm = bm_req;
   return ceil_div((int64_t)N * P * Q, bm);
 }
@@ -172,7 +186,7 @@ c10::optional<at::Tensor> conv2d_dgrad(const at::Tensor& dy, int N, int P, int Q
     throw std::runtime_error("conv2d_dgrad: fused BN tensors must be 8-channel aligned");
   set_kstep(a, K);
   int bm, bn;
-  pick_tiles((int64_t)N * H * W / (stride * stride), C, bm, bn);
+  pick_tiles((int64_t)N * H * W / (stride * stride), C, (int64_t)R * S * K / (stride * stride), bm, bn);
   a.ntiles = ceil_div(C, bn);
   a.nphase = stride * stride;
   int tiles = 0;
@@ -219,7 +233,7 @@ void convT2x2_fwd(const at::Tensor& x, int N, int H, int W, int Cin, int ldx, in
   a.vec_store = ((ldy % 8) == 0 && (yoff % 8) == 0) ? 1 : 0;
   set_kstep(a, Cin);
   int bm, bn;
-  pick_tiles((int64_t)N * H * W, Cout, bm, bn);
+  pick_tiles((int64_t)N * H * W, Cout, Cin, bm, bn);
   a.ntiles = ceil_div(Cout, bn);
   a.nphase = 4;
   for (int i = 0; i < 2; ++i)

@@ -80,6 +80,7 @@ __global__ __launch_bounds__(256) void colsum2_kernel(const float* __restrict__ 
   const int t0 = s * per, t1 = min(T, t0 + per);
   double a = 0.0, b = 0.0;
   if (c < C) {
+#pragma unroll 8
     for (int t = t0 + rl; t < t1; t += 4) {
       a += (double)partial[(int64_t)t * ns * C + c];
       b += (double)partial[(int64_t)t * ns * C + k2 * C + c];
@@ -99,6 +100,7 @@ __device__ __forceinline__ void colsum2_final(const double* __restrict__ dpart, 
                                               double& s2) {
   s1 = 0.0;
   s2 = 0.0;
+#pragma unroll 8
   for (int s = 0; s < S; ++s) {
     s1 += dpart[(int64_t)s * 2 * C + c];
     s2 += dpart[(int64_t)s * 2 * C + C + c];

@@ -38,7 +38,7 @@ __device__ __forceinline__ void glds16(const void* g, char* lds_wave_base) {
 // across blocks instead of inside one).  The epilogue stages the fp32 tile through LDS in two
 // row halves so it never needs more LDS than one stage.
 template <int BM, int BN, bool SMALLC, int STAGES>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(STAGES == 1 ? 3 : 2, 8))) void conv_igemm_kernel(const ConvArgs a) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(STAGES == 1 && BM * BN <= 16384 ? 3 : 2, 8))) void conv_igemm_kernel(const ConvArgs a) {
   constexpr int BK = 64;
   constexpr int WM = BM / 2, WN = BN / 2;
   constexpr int TM = WM / 16, TN = WN / 16;
@@ -46,7 +46,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(STAGES == 1
   constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2;
   constexpr int STAGE_BYTES = STAGES * (A_BYTES + B_BYTES);
   constexpr int CS_LD = BN + 4;
-  constexpr int EPI_BYTES = (BM / 2) * CS_LD * 4;
+  constexpr int NP = BM >= 128 ? BM / 64 : 1;            // epilogue passes of <= 64 tile rows
+  constexpr int EPI_BYTES = (BM / NP) * CS_LD * 4;
   constexpr int RED_BYTES = (256 / (BN / 8)) * 3 * BN * 4;   // stats combine
   constexpr int SMEM0 = STAGE_BYTES > EPI_BYTES ? STAGE_BYTES : EPI_BYTES;
   constexpr int SMEM = SMEM0 > RED_BYTES ? SMEM0 : RED_BYTES;
@@ -68,31 +69,30 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(STAGES == 1
   const int jc = (tid & 7) ^ ((tid >> 4) & 7);        // swizzled 16-B chunk this lane fetches
   const char* zp = reinterpret_cast<const char*>(g_zero_page);
 
-  // ---- per-thread row state -------------------------------------------------------------
-  int a_h[AL], a_w[AL], a_pix[AL];
-  bool a_ok[AL];
+  // ---- per-thread row state (kept compact: the 256-row tile has 8 rows per thread) ----------
+  int a_hw[AL], a_pix[AL];                            // (h << 16) | w of the row's input origin
+  uint32_t a_okm = 0;                                 // bit i: GEMM row valid
 #pragma unroll
   for (int i = 0; i < AL; ++i) {
     const int m = m0 + lrow + 32 * i;
-    a_ok[i] = m < M;
-    const uint32_t mm = a_ok[i] ? (uint32_t)m : 0u;
+    if (m < M) a_okm |= 1u << i;
+    const uint32_t mm = m < M ? (uint32_t)m : 0u;
     const uint32_t n_img = fdiv(mm, ph.fdPQ);
     const uint32_t rem = mm - n_img * PQ;
     const uint32_t p = fdiv(rem, ph.fdQ);
     const uint32_t q = rem - p * ph.Q;
-    a_h[i] = (int)p * a.sa;
-    a_w[i] = (int)q * a.sa;
-    a_pix[i] = ((int)n_img * a.H + a_h[i]) * a.W + a_w[i];
+    const int h = (int)p * a.sa, w = (int)q * a.sa;
+    a_hw[i] = (h << 16) | w;
+    a_pix[i] = ((int)n_img * a.H + h) * a.W + w;
   }
   const char* xlane = reinterpret_cast<const char*>(a.x) + 2 * ((int64_t)a.xoff + 8 * jc);
-  const char* b_row[BL];
-  bool b_ok[BL];
+  // B rows n0 + lrow + 32 i: one base pointer + validity bits
+  const char* b_base = reinterpret_cast<const char*>(a.w) + 2 * ((int64_t)(n0 + lrow) * a.ldw + 8 * jc);
+  const int64_t b_step = (int64_t)64 * a.ldw;          // bytes between rows 32 apart
+  uint32_t b_okm = 0;
 #pragma unroll
-  for (int i = 0; i < BL; ++i) {
-    const int n = n0 + lrow + 32 * i;
-    b_ok[i] = n < a.Kout;
-    b_row[i] = reinterpret_cast<const char*>(a.w) + 2 * ((int64_t)(b_ok[i] ? n : 0) * a.ldw + 8 * jc);
-  }
+  for (int i = 0; i < BL; ++i)
+    if (n0 + lrow + 32 * i < a.Kout) b_okm |= 1u << i;
 
   const int C = a.C;
   const int T = ph.Tr * ph.Ts;
@@ -101,7 +101,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(STAGES == 1
 
   // ---- staging ------------------------------------------------------------------------------
   // Regular path (C % 64 == 0): the tap t and channel base c are wave-uniform.
-  const char* a_src[AL];
+  uint32_t a_off[AL];                                 // element offset of the row's input pixel
+  uint32_t a_vm = 0;                                  // bit i: (row, tap) inside the image
   int t_cur = 0, c_cur = 0, wtC2 = 0;
   auto tap_setup = [&](int t) {
     const int tr = (int)fdiv((uint32_t)t, ph.fdTs);
@@ -110,11 +111,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(STAGES == 1
     const int wt = (ph.wr0 + tr * ph.wrs) * a.S + (ph.ws0 + ts * ph.wss);
     wtC2 = wt * C * 2;
     const int doff = dh * a.W + dw;
+    a_vm = 0;
 #pragma unroll
     for (int i = 0; i < AL; ++i) {
-      const int ih = a_h[i] + dh, iw = a_w[i] + dw;
-      const bool ok = a_ok[i] && (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W;
-      a_src[i] = ok ? xlane + (int64_t)(a_pix[i] + doff) * ldx2 : nullptr;
+      const int ih = (a_hw[i] >> 16) + dh, iw = (a_hw[i] & 0xffff) + dw;
+      const bool ok = ((a_okm >> i) & 1) && (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W;
+      if (ok) a_vm |= 1u << i;
+      a_off[i] = (uint32_t)(a_pix[i] + doff) * (uint32_t)a.ldx;
     }
   };
 
@@ -124,12 +127,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(STAGES == 1
     if constexpr (!SMALLC) {
 #pragma unroll
       for (int i = 0; i < AL; ++i) {
-        const char* s = a_src[i] ? a_src[i] + 2 * c_cur : zp;
+        const char* s = ((a_vm >> i) & 1) ? xlane + 2 * ((uint64_t)a_off[i] + c_cur) : zp;
         glds16(s, As + (32 * i + 8 * wid) * 128);
       }
 #pragma unroll
       for (int i = 0; i < BL; ++i) {
-        const char* s = b_ok[i] ? b_row[i] + wtC2 + 2 * c_cur : zp;
+        const char* s = ((b_okm >> i) & 1) ? b_base + i * b_step + wtC2 + 2 * c_cur : zp;
         glds16(s, Bs + (32 * i + 8 * wid) * 128);
       }
     } else {
@@ -145,14 +148,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(STAGES == 1
       const char* xs = reinterpret_cast<const char*>(a.x) + 2 * ((int64_t)a.xoff + c);
 #pragma unroll
       for (int i = 0; i < AL; ++i) {
-        const int ih = a_h[i] + dh, iw = a_w[i] + dw;
-        const bool ok = tv && a_ok[i] && (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W;
+        const int ih = (a_hw[i] >> 16) + dh, iw = (a_hw[i] & 0xffff) + dw;
+        const bool ok = tv && ((a_okm >> i) & 1) && (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W;
         const char* s = ok ? xs + (int64_t)(a_pix[i] + dh * a.W + dw) * ldx2 : zp;
         glds16(s, As + (32 * i + 8 * wid) * 128);
       }
 #pragma unroll
       for (int i = 0; i < BL; ++i) {
-        const char* s = (tv && b_ok[i]) ? b_row[i] - 2 * 8 * jc + 2 * (wt * C + c) : zp;
+        const char* s = (tv && ((b_okm >> i) & 1)) ? b_base + i * b_step - 2 * 8 * jc + 2 * (wt * C + c) : zp;
         glds16(s, Bs + (32 * i + 8 * wid) * 128);
       }
     }
@@ -240,11 +243,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(STAGES == 1
   for (int e = 0; e < 8; ++e) { s1[e] = 0.f; s2[e] = 0.f; s3[e] = 0.f; }
   const bool bwd = a.mask != nullptr;   // gradient of a BN+ReLU output: mask, then {sum dy, sum dy*z}
 
-  // Two passes over row halves: in pass h every wave dumps its fragments mi in
-  // [h*TM/2, (h+1)*TM/2), i.e. tile rows wm*WM + h*WM/2 + [0, WM/2), into a BM/2-row buffer.
-  constexpr int HM = WM / 2, HT = TM / 2;
+  // NP passes over row slices: in pass h every wave dumps its fragments mi in
+  // [h*TM/NP, (h+1)*TM/NP), i.e. tile rows wm*WM + h*HM + [0, HM), into a BM/NP-row buffer.
+  constexpr int HM = WM / NP, HT = TM / NP;
 #pragma unroll
-  for (int h = 0; h < 2; ++h) {
+  for (int h = 0; h < NP; ++h) {
   if (h) __syncthreads();         // every thread is done with pass 0
 #pragma unroll
   for (int mi = 0; mi < HT; ++mi)
@@ -254,7 +257,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(STAGES == 1
       for (int r = 0; r < 4; ++r)
         Cs[(wm * HM + mi * 16 + fg * 4 + r) * CS_LD + wn * WN + ni * 16 + fr] = acc[h * HT + mi][ni][r];
   __syncthreads();
-  for (int rr = rg; rr < BM / 2; rr += RG) {
+  for (int rr = rg; rr < BM / NP; rr += RG) {
     const int r = (rr / HM) * WM + h * HM + (rr % HM);
     const int m = m0 + r;
     if (m >= M || !cvalid) continue;
@@ -386,7 +389,8 @@ extern "C" hipError_t dlmpi_conv_igemm(const ConvArgs* a, int bm, int bn, hipStr
   for (int i = 0; i < a->nphase; ++i) maxt = a->ph[i].mtiles > maxt ? a->ph[i].mtiles : maxt;
   dim3 grid((unsigned)(maxt * a->ntiles), 1, (unsigned)a->nphase);
   if (grid.x == 0) return hipSuccess;
-  if (bm == 128 && bn == 128) launch_tile<128, 128>(a, grid, s);
+  if (bm == 256 && bn == 128) launch_tile<256, 128>(a, grid, s);
+  else if (bm == 128 && bn == 128) launch_tile<128, 128>(a, grid, s);
   else if (bm == 128 && bn == 64) launch_tile<128, 64>(a, grid, s);
   else if (bm == 64 && bn == 128) launch_tile<64, 128>(a, grid, s);
   else if (bm == 64 && bn == 64) launch_tile<64, 64>(a, grid, s);

@@ -11,6 +11,8 @@
 //
 // Also used for ConvTranspose2d(k2,s2) weight-grad (roles of X and dY swapped, stride 2) and for
 // Linear weight-grad (1x1 "conv" on a 1x1 image).
+#include <cstdlib>
+
 #include "common.h"
 
 namespace dlmpi {
@@ -46,15 +48,33 @@ __device__ __forceinline__ bf16x8 tr_frag(const char* tile, int k0, int cb, int 
   return __builtin_bit_cast(bf16x8, r);
 }
 
-template <int BM>
-__global__ __launch_bounds__(256) void conv_wgrad_kernel(const WgradArgs a) {
+typedef __attribute__((address_space(3))) void lds_void;
+
+__device__ __forceinline__ void glds16(const void* g, char* lds_wave_base) {
+  __builtin_amdgcn_global_load_lds(g, (lds_void*)lds_wave_base, 16, 0, 0);
+}
+
+// Inverse of tr_off within a row: the chunk that lives at 16-B slot `pos` of row `row`.
+template <int ROW_BYTES>
+__device__ __forceinline__ int tr_chunk(int row, int pos) {
+  if constexpr (ROW_BYTES == 256) return pos ^ (((row & 3) << 2) | ((row >> 2) & 3));
+  else return pos ^ ((((row >> 1) & 1) << 1) | (((row >> 3) & 1) << 2));
+}
+
+// Operands are staged global -> LDS with global_load_lds (no VGPR round trip): piece i of thread
+// tid fills the 16-B LDS slot 16*(256 i + tid), i.e. each wave writes 1 KB contiguously, and the
+// lane fetches whichever (pixel row, 16-B chunk) the swizzled layout puts there.  STAGES = 1:
+// single stage, two barriers per K-step, 32 KB LDS at BM = 128 -> several blocks per CU hide
+// the load latency of one another.
+template <int BM, int STAGES>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(STAGES == 1 ? 3 : 2, 8)))
+void conv_wgrad_kernel(const WgradArgs a) {
   constexpr int BN = 128, BK = 64;
   constexpr int WM = BM / 2, WN = BN / 2, TM = WM / 16, TN = WN / 16;
   constexpr int A_ROW = BM * 2, B_ROW = BN * 2;          // bytes per LDS row
-  constexpr int CA = BM / 8, CB = BN / 8;                 // 16-B chunks per row
-  constexpr int AL = BK * CA / 256, BL = BK * CB / 256;   // pieces per thread
+  constexpr int AL = BK * A_ROW / 4096, BL = BK * B_ROW / 4096;   // 16-B pieces per thread
   constexpr int A_BYTES = BK * A_ROW, B_BYTES = BK * B_ROW;
-  __shared__ __attribute__((aligned(16))) char smem[2 * (A_BYTES + B_BYTES)];
+  __shared__ __attribute__((aligned(16))) char smem[STAGES * (A_BYTES + B_BYTES)];
 
   const uint32_t ntile = (uint32_t)a.mtiles * a.ntiles;
   const uint32_t nwg = ntile * a.splits;
@@ -67,59 +87,72 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(const WgradArgs a) {
   const int pend = min(a.npix, pbeg + a.pix_per_split);
   const int nk = pend > pbeg ? (pend - pbeg + BK - 1) / BK : 0;
 
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wid >> 1, wn = wid & 1;
   const int PQ = a.P * a.Q;
+  const char* zp = reinterpret_cast<const char*>(g_zero_page);
 
-  // A (dY) pieces: chunk ja of row ra + (256/CA)*i
-  const int ja = tid % CA, ra = tid / CA;
-  const bool a_colok = (m0 + 8 * ja) < a.Ko;
-  // B (X gathered) pieces: column chunk jb is a fixed (tap, channel) for the whole block
-  const int jb = tid % CB, rbb = tid / CB;
-  const int col = n0 + 8 * jb;
-  const bool b_colok = col < a.TC;
-  const uint32_t colc = b_colok ? (uint32_t)col : 0u;
-  const int t = (int)fdiv(colc, a.fdC);
-  const int cch = (int)colc - t * a.C;
-  const int tr = (int)fdiv((uint32_t)t, a.fdS);
-  const int ts = t - tr * a.S;
-  const int dh = tr - a.pad_h, dw = ts - a.pad_w;
+  // Piece i of this lane: 16-B LDS slot o = 256 i + tid -> (pixel row, swizzled chunk).  Rows and
+  // chunks are recomputed from (i, tid) (a few bit ops); only the gather tap of B is kept.
+  auto piece = [&](int i, int ROW, int& row, int& ch) {
+    const int o = 256 * i + tid;
+    row = (o * 16) / ROW;
+    const int pos = (o * 16 % ROW) / 16;
+    ch = ROW == 256 ? tr_chunk<256>(row, pos) : tr_chunk<128>(row, pos);
+  };
+  // B column chunk = (tap, channel): packed cch | (dh + 64) << 16 | (dw + 64) << 24, -1 = outside
+  int b_pack[BL];
+#pragma unroll
+  for (int i = 0; i < BL; ++i) {
+    int row, ch;
+    piece(i, B_ROW, row, ch);
+    const int col = n0 + 8 * ch;
+    if (col < a.TC) {
+      const int t = (int)fdiv((uint32_t)col, a.fdC);
+      const int cch = col - t * a.C;
+      const int tr = (int)fdiv((uint32_t)t, a.fdS);
+      const int ts = t - tr * a.S;
+      b_pack[i] = cch | ((tr - a.pad_h + 64) << 16) | ((ts - a.pad_w + 64) << 24);   // < 2^31
+    } else {
+      b_pack[i] = -1;
+    }
+  }
+  const uint16_t* dyb = a.dy + a.dyoff;
+  const uint16_t* xb = a.x + a.xoff;
 
-  u32x4 va[AL], vb[BL];
-  auto load_tile = [&](int pix0) {
+  auto issue = [&](int buf, int pix0) {
+    char* As = smem + buf * (A_BYTES + B_BYTES);
+    char* Bs = As + A_BYTES;
 #pragma unroll
     for (int i = 0; i < AL; ++i) {
-      const int pix = pix0 + ra + (256 / CA) * i;
-      const bool ok = a_colok && pix < pend;
-      const u32x4* src =
-          ok ? reinterpret_cast<const u32x4*>(a.dy + (int64_t)pix * a.ldy + a.dyoff + m0 + 8 * ja) : g_zero_page;
-      va[i] = *src;
+      int row, ch;
+      piece(i, A_ROW, row, ch);
+      const int pix = pix0 + row, col = m0 + 8 * ch;
+      const char* s = (pix < pend && col < a.Ko)
+                          ? reinterpret_cast<const char*>(dyb + (int64_t)pix * a.ldy + col) : zp;
+      glds16(s, As + 16 * (256 * i + 64 * wid));
     }
 #pragma unroll
     for (int i = 0; i < BL; ++i) {
-      const int pix = pix0 + rbb + (256 / CB) * i;
-      bool ok = b_colok && pix < pend;
+      int row, ch;
+      piece(i, B_ROW, row, ch);
+      const int pix = pix0 + row;
+      const int bp = b_pack[i];
+      bool ok = pix < pend && bp >= 0;
       const uint32_t pp = ok ? (uint32_t)pix : 0u;
       const uint32_t n_img = fdiv(pp, a.fdPQ);
       const uint32_t rem = pp - n_img * PQ;
       const uint32_t p = fdiv(rem, a.fdQ);
       const uint32_t q = rem - p * a.Q;
-      const int ih = (int)p * a.stride_h + dh, iw = (int)q * a.stride_w + dw;
+      const int ih = (int)p * a.stride_h + ((bp >> 16) & 255) - 64;
+      const int iw = (int)q * a.stride_w + ((bp >> 24) & 255) - 64;
       ok = ok && (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W;
-      const int64_t off = (((int64_t)n_img * a.H + ih) * a.W + iw) * a.ldx + a.xoff + cch;
-      const u32x4* src = ok ? reinterpret_cast<const u32x4*>(a.x + off) : g_zero_page;
-      vb[i] = *src;
+      const char* s = ok ? reinterpret_cast<const char*>(
+                               xb + (((int64_t)n_img * a.H + ih) * a.W + iw) * a.ldx + (bp & 0xffff))
+                         : zp;
+      glds16(s, Bs + 16 * (256 * i + 64 * wid));
     }
-  };
-  auto store_tile = [&](int buf) {
-    char* As = smem + buf * (A_BYTES + B_BYTES);
-    char* Bs = As + A_BYTES;
-#pragma unroll
-    for (int i = 0; i < AL; ++i)
-      *reinterpret_cast<u32x4*>(As + tr_off<A_ROW>(ra + (256 / CA) * i, ja)) = va[i];
-#pragma unroll
-    for (int i = 0; i < BL; ++i)
-      *reinterpret_cast<u32x4*>(Bs + tr_off<B_ROW>(rbb + (256 / CB) * i, jb)) = vb[i];
   };
 
   f32x4 acc[TM][TN];
@@ -129,14 +162,18 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(const WgradArgs a) {
     for (int ni = 0; ni < TN; ++ni) acc[mi][ni] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   if (nk > 0) {
-    load_tile(pbeg);
-    store_tile(0);
+    issue(0, pbeg);
     __syncthreads();
   }
   for (int ks = 0; ks < nk; ++ks) {
-    const int cur = ks & 1;
-    const bool more = ks + 1 < nk;
-    if (more) load_tile(pbeg + (ks + 1) * BK);
+    int cur = 0;
+    if constexpr (STAGES == 2) {
+      cur = ks & 1;
+      if (ks + 1 < nk) issue(cur ^ 1, pbeg + (ks + 1) * BK);
+    } else if (ks > 0) {
+      issue(0, pbeg + ks * BK);
+      __syncthreads();
+    }
     const char* As = smem + cur * (A_BYTES + B_BYTES);
     const char* Bs = As + A_BYTES;
 #pragma unroll
@@ -152,7 +189,6 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(const WgradArgs a) {
         for (int ni = 0; ni < TN; ++ni)
           acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[mi], bfr[ni], acc[mi][ni], 0, 0, 0);
     }
-    if (more) store_tile(cur ^ 1);
     __syncthreads();
   }
 
@@ -182,6 +218,7 @@ __global__ __launch_bounds__(256) void wgrad_reduce_stage1(const float* __restri
   const int64_t i4 = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) * 4;
   if (i4 >= total) return;
   f32x4 s = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll 8
   for (int z = z0; z < z1; ++z) s += *reinterpret_cast<const f32x4*>(ws + (int64_t)z * total + i4);
   *reinterpret_cast<f32x4*>(ws2 + (int64_t)g * total + i4) = s;
 }
@@ -200,6 +237,7 @@ __global__ __launch_bounds__(256) void wgrad_reduce_stage2(const float* __restri
     const int c = (int)(rem - tt * Cpad);
     if (c >= Creal) continue;
     float s = 0.f;
+#pragma unroll 8
     for (int g = 0; g < G; ++g) s += src[g * gstride + idx];
     out[(ko * T + tt) * Creal + c] += s;
   }
@@ -220,9 +258,19 @@ using namespace dlmpi;
 extern "C" hipError_t dlmpi_conv_wgrad(const WgradArgs* a, int bm, hipStream_t s) {
   const unsigned nwg = (unsigned)(a->mtiles * a->ntiles * a->splits);
   if (nwg == 0) return hipSuccess;
-  if (bm == 128) hipLaunchKernelGGL((conv_wgrad_kernel<128>), dim3(nwg), dim3(256), 0, s, *a);
-  else if (bm == 64) hipLaunchKernelGGL((conv_wgrad_kernel<64>), dim3(nwg), dim3(256), 0, s, *a);
-  else return hipErrorInvalidValue;
+  static const int stages = [] {
+    const char* e = getenv("DLMPI_WGRAD_STAGES");
+    return e ? atoi(e) : 1;
+  }();
+  if (bm == 128) {
+    if (stages == 1) hipLaunchKernelGGL((conv_wgrad_kernel<128, 1>), dim3(nwg), dim3(256), 0, s, *a);
+    else hipLaunchKernelGGL((conv_wgrad_kernel<128, 2>), dim3(nwg), dim3(256), 0, s, *a);
+  } else if (bm == 64) {
+    if (stages == 1) hipLaunchKernelGGL((conv_wgrad_kernel<64, 1>), dim3(nwg), dim3(256), 0, s, *a);
+    else hipLaunchKernelGGL((conv_wgrad_kernel<64, 2>), dim3(nwg), dim3(256), 0, s, *a);
+  } else {
+    return hipErrorInvalidValue;
+  }
   return hipGetLastError();
 }
 

@@ -86,7 +86,7 @@ class ConvUnit:
             return y, ((x, y) if save else None)
         if train:
             z = Act.empty(N, P, Q, self.Kp, be.act_dtype, dev)
-            mt = be.conv_mtiles(N, x.H, x.W, self.Kp, self.R, self.S, self.stride, self.pad)
+            mt = be.conv_mtiles(N, x.H, x.W, x.C, self.Kp, self.R, self.S, self.stride, self.pad)
             stats = torch.empty(mt, 2, self.Kp, dtype=be.dt, device=dev)
             be.conv_fwd(x, wf, self.Kp, self.R, self.S, self.stride, self.pad, z, bias=self._bias_vec(), stats=stats)
             vec = torch.empty(4, self.Kp, dtype=be.dt, device=dev)

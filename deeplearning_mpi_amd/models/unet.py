@@ -164,15 +164,29 @@ class UNet(EngineModule):
         return logits, state
 
     def _engine_backward(self, state, gout):
+        """Reverse schedule.  With ``fuse_bn_bwd`` every data-gradient GEMM whose output is the
+        gradient of a BN+ReLU output (inside each DoubleConv, and the 1x1 head into the last
+        decoder DoubleConv) masks it and emits that BN's backward partials in its epilogue."""
         be = self._be
+        fuse = self.fuse_bn_bwd
         cats, ctx_enc, idxs, skips, (cba, cbb), ctx_dec, cl = state
+
+        def spec(ctx):
+            return ConvUnit.fuse_spec(ctx) + (None,) if fuse else None
+
+        def double_bwd(units, ca, cb, dy, pre=None, need_dx=True):
+            ua, ub = units
+            out = ub.bwd(be, cb, dy, pre=pre, fuse_next=spec(ca))
+            dt_, part = out if fuse else (out, None)
+            return ua.bwd(be, ca, dt_, pre=part, need_dx=need_dx)
+
         dl = be.nchw_to_nhwc(gout, self.u_last.Kp)
-        da = self.u_last.bwd(be, (cl[0], None), dl)
+        out = self.u_last.bwd(be, (cl[0], None), dl, fuse_next=spec(ctx_dec[0][2]))
+        da, pre = out if fuse else (out, None)
         for k in range(4):                    # decoder, level 1 (last executed) first
             below, ca, cb = ctx_dec[k]
-            ua, ub = self.dec[k]
-            dt_ = ub.bwd(be, cb, da)
-            dcat = ua.bwd(be, ca, dt_)
+            dcat = double_bwd(self.dec[k], ca, cb, da, pre=pre)
+            pre = None
             dup = dcat.slice(0, self.up_ch[k])
             if self.upT[k] is not None:
                 da = self.upT[k].bwd(be, below, dup)
@@ -180,14 +194,11 @@ class UNet(EngineModule):
                 da = Act.empty(below.N, below.H, below.W, below.C, be.act_dtype, below.device)
                 be.upsample_bwd(dup, da)
             ctx_dec[k] = dcat                 # keep the skip-slice gradient for the encoder
-        ua, ub = self.bott
-        da = ua.bwd(be, cba, ub.bwd(be, cbb, da))
+        da = double_bwd(self.bott, cba, cbb, da)
         for k in range(3, -1, -1):
             skip = skips[k]
             dskip = Act.empty(skip.N, skip.H, skip.W, skip.C, be.act_dtype, skip.device)
             be.maxpool_bwd(da, idxs[k], skip, 2, 2, 0, dskip,
                            add=ctx_dec[k].slice(self.up_ch[k], self.skip_ch[k]))
             ca, cb = ctx_enc[k]
-            ua, ub = self.enc[k]
-            dt_ = ub.bwd(be, cb, dskip)
-            da = ua.bwd(be, ca, dt_, need_dx=k != 0)
+            da = double_bwd(self.enc[k], ca, cb, dskip, need_dx=k != 0)

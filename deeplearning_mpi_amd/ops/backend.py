@@ -31,8 +31,8 @@ class NativeBackend:
         self._cast_cache = {}
 
     # ---------------- conv family ----------------
-    def conv_mtiles(self, N, H, W, K, R, S, stride, pad):
-        return self.C.conv2d_fwd_mtiles(N, H, W, K, R, S, stride, pad, 0)
+    def conv_mtiles(self, N, H, W, C, K, R, S, stride, pad):
+        return self.C.conv2d_fwd_mtiles(N, H, W, C, K, R, S, stride, pad, 0)
 
     def conv_fwd(self, x: Act, w, K, R, S, stride, pad, y: Act, bias=None, res: Act = None, scale=None,
                  shift=None, relu=False, stats=None, kvalid=0):
@@ -211,7 +211,7 @@ class RefBackend:
     def _store(y: Act, v_nchw):
         y.nhwc().copy_(v_nchw[:, :y.C].permute(0, 2, 3, 1))
 
-    def conv_mtiles(self, N, H, W, K, R, S, stride, pad):
+    def conv_mtiles(self, N, H, W, C, K, R, S, stride, pad):
         return 1
 
     def conv_fwd(self, x: Act, w, K, R, S, stride, pad, y: Act, bias=None, res=None, scale=None, shift=None,

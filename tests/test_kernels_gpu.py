@@ -57,7 +57,7 @@ def test_conv_fwd(shape):
     res, resr = _act(N, P, Q, Kp)
     y = _empty(N, P, Q, Kp)
     yr = _empty(N, P, Q, Kp, torch.float32)
-    mt = nb.conv_mtiles(N, H, W, Kp, R, R, s, p)
+    mt = nb.conv_mtiles(N, H, W, Cp, Kp, R, R, s, p)
     st = torch.zeros(mt, 2, Kp, device=DEV)
     str_ = torch.zeros(1, 2, Kp, device=DEV)
     nb.conv_fwd(x, w, Kp, R, R, s, p, y, bias=bias, stats=st)
@@ -88,6 +88,31 @@ def test_conv_dgrad(shape):
     rb.conv_dgrad(dyr, wT.float(), Cp, R, R, s, p, dxr, res=resr)
     torch.cuda.synchronize()
     assert _rel(dx.buf, dxr.buf) < 1e-2
+
+
+@pytest.mark.parametrize("shape", [(2, 20, 20, 64, 128, 3, 1, 1), (3, 9, 11, 256, 256, 1, 1, 0),
+                                   (2, 16, 16, 128, 384, 3, 2, 1)])
+def test_conv_fwd_256_row_tile(shape):
+    """The 256x128 tile (chosen automatically for large grids) forced on small shapes, incl. BN
+    statistics partials and row/column remainders."""
+    nb, rb = _be()
+    N, H, W, Cin, K, R, s, p = shape
+    Cp, Kp = pad8(Cin), pad8(K)
+    P, Q = (H + 2 * p - R) // s + 1, (W + 2 * p - R) // s + 1
+    x, xr = _act(N, H, W, Cp)
+    w = (torch.randn(Kp, R, R, Cp, device=DEV) / (R * R * Cin) ** 0.5).to(torch.bfloat16)
+    y = _empty(N, P, Q, Kp)
+    yr = _empty(N, P, Q, Kp, torch.float32)
+    mt = (N * P * Q + 255) // 256
+    st = torch.empty(mt, 2, Kp, device=DEV)
+    rows = nb.C.conv2d_fwd(x.buf, N, H, W, Cp, Cp, 0, w, Kp, R, R, s, p, y.buf, Kp, 0, None, None, 0, 0, None, None,
+                           False, st, 256, 0)
+    assert rows == mt
+    str_ = torch.empty(1, 2, Kp, device=DEV)
+    rb.conv_fwd(xr, w.float(), Kp, R, R, s, p, yr, stats=str_)
+    torch.cuda.synchronize()
+    assert _rel(y.buf, yr.buf) < 1e-2
+    assert _rel(st.sum(0), str_.sum(0)) < 2e-2
 
 
 @pytest.mark.parametrize("shape", [CONV_SHAPES[1], CONV_SHAPES[2], CONV_SHAPES[3], CONV_SHAPES[5]])
