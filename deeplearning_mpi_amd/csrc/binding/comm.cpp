@@ -15,6 +15,8 @@
 // goes out as soon as it and all earlier buckets are complete.
 #include "comm.h"
 
+#include "../kernels/dlmpi_kernels.h"
+
 #include <c10/hip/HIPCachingAllocator.h>
 #include <c10/hip/HIPStream.h>
 #include <rccl/rccl.h>
@@ -96,7 +98,17 @@ struct RcclComm::Impl {
   std::atomic<bool> stop{false};
   double timeout_s = 1800.0;
 
+  // fault injection (tests): DLMPI_FAULT_COMM_DELAY_MS=x delays the first all-reduce by x ms
+  double inject_ms = 0.0;
+  void maybe_inject() {
+    if (inject_ms > 0) {
+      hip_check(dlmpi_delay(inject_ms, stream.stream()), "dlmpi_delay");
+      inject_ms = 0.0;
+    }
+  }
+
   void start_watchdog() {
+    if (const char* e = std::getenv("DLMPI_FAULT_COMM_DELAY_MS")) inject_ms = std::atof(e);
     if (const char* e = std::getenv("DLMPI_COMM_TIMEOUT")) timeout_s = std::atof(e);
     if (timeout_s <= 0) return;
     wd = std::thread([this] { watch_loop(); });
@@ -146,7 +158,13 @@ struct RcclComm::Impl {
                      "(RCCL async error: %s). Aborting the communicator and the process.\n",
                      rank, size, p.what, waited, ncclGetErrorString(ae));
         std::fflush(stderr);
-        if (comm) ncclCommAbort(comm);
+        // abort in a helper thread (it can block on the stuck kernel) and exit after a bounded grace
+        std::atomic<bool> aborted{false};
+        std::thread([this, &aborted] {
+          if (comm) ncclCommAbort(comm);
+          aborted.store(true);
+        }).detach();
+        for (int i = 0; i < 100 && !aborted.load(); ++i) std::this_thread::sleep_for(std::chrono::milliseconds(100));
         std::_Exit(70);
       }
       std::this_thread::sleep_for(std::chrono::milliseconds(20));
@@ -229,6 +247,7 @@ void RcclComm::record(const at::Tensor& t) {
 void RcclComm::allreduce_async(at::Tensor t, const std::string& op) {
   if (!t.is_contiguous()) throw std::runtime_error("allreduce: tensor must be contiguous");
   record(t);
+  impl_->maybe_inject();
   nccl_check(ncclAllReduce(t.data_ptr(), t.data_ptr(), (size_t)t.numel(), to_nccl(t.scalar_type()), to_op(op),
                            impl_->comm, impl_->stream.stream()),
              "ncclAllReduce");

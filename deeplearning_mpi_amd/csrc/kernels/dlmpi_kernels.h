@@ -188,6 +188,9 @@ hipError_t dlmpi_clip_coef(const float* partial, int nblk, float max_norm, float
                            hipStream_t s);
 hipError_t dlmpi_scale_f32(float* x, int64_t n, const float* coef, hipStream_t s);
 
+// fault injection: keep stream s busy for `ms` milliseconds (bounded; tests of the watchdog)
+hipError_t dlmpi_delay(double ms, hipStream_t s);
+
 // comm helpers
 hipError_t dlmpi_pack(const void* const* srcs, const int64_t* offs, int n, int64_t total_bytes, void* dst,
                       hipStream_t s);

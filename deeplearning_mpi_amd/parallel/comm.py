@@ -296,11 +296,26 @@ def _resolve_backend(backend: str) -> str:
     raise ValueError(f"unknown backend {backend!r}")
 
 
-def init_distributed(backend: str = "auto", timeout_s: float = 1800.0) -> Communicator:
-    """Bring up ranks and the communicator. Safe to call once per process."""
+def init_distributed(backend: str = "auto", timeout_s: float = 1800.0, check: bool | None = None) -> Communicator:
+    """Bring up ranks and the communicator. Safe to call once per process.
+
+    check: wrap the communicator in the collective desync detector (parallel/debug.py); default
+    from ``DLMPI_DESYNC_CHECK``.  timeout_s: control-plane timeout (a dead peer raises instead of
+    hanging); the RCCL data plane has its own watchdog (``DLMPI_COMM_TIMEOUT``)."""
     global _CURRENT
     if _CURRENT is not None:
         return _CURRENT
+    if check is None:
+        check = os.environ.get("DLMPI_DESYNC_CHECK", "0") not in ("", "0")
+    _CURRENT = _init(backend, timeout_s)
+    if check and _CURRENT.world_size > 1:
+        from .debug import CheckedCommunicator
+
+        _CURRENT = CheckedCommunicator(_CURRENT)
+    return _CURRENT
+
+
+def _init(backend: str, timeout_s: float) -> Communicator:
     info = detect_launcher()
     if info.launcher == "mpi":
         info = mpi_bring_up()
@@ -313,25 +328,28 @@ def init_distributed(backend: str = "auto", timeout_s: float = 1800.0) -> Commun
     else:
         device = torch.device("cpu")
     if info.world_size == 1:
-        _CURRENT = SingleCommunicator(info, device)
-        return _CURRENT
+        return SingleCommunicator(info, device)
     if be == "mpi":
-        _CURRENT = MPICommunicator(info, "cpu")
-        return _CURRENT
+        return MPICommunicator(info, "cpu")
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     dist.init_process_group("gloo", rank=info.rank, world_size=info.world_size,
                             timeout=datetime.timedelta(seconds=timeout_s))
     if be == "gloo":
-        _CURRENT = TorchCommunicator(info, device)
-        return _CURRENT
+        return TorchCommunicator(info, device)
     from .._ext import native
 
     C = native()
-    uid = [C.RcclComm.unique_id() if info.rank == 0 else None]
-    dist.broadcast_object_list(uid, src=0)
-    nc = C.RcclComm(uid[0], info.rank, info.world_size, info.local_rank)
-    _CURRENT = RcclCommunicator(info, device, nc)
-    return _CURRENT
+    if info.launcher == "mpi":
+        # mpirun: the RCCL unique id travels by MPI_Bcast
+        from .._ext import mpi
+
+        uid = mpi().bcast_bytes(C.RcclComm.unique_id() if info.rank == 0 else b"", 0)
+    else:
+        box = [C.RcclComm.unique_id() if info.rank == 0 else None]
+        dist.broadcast_object_list(box, src=0)
+        uid = box[0]
+    nc = C.RcclComm(uid, info.rank, info.world_size, info.local_rank)
+    return RcclCommunicator(info, device, nc)
 
 
 def get_comm() -> Communicator:

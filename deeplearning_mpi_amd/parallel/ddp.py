@@ -65,6 +65,7 @@ class DistributedDataParallel(nn.Module):
             self.reducer = native().Reducer(views, self.param_bucket, self._bucket_comm, True)
         self._require_sync = True
         self._queued = False
+        self._steps = 0
 
     # ---------------------------------------------------------------- construction collectives
     def _verify_params(self):
@@ -114,7 +115,11 @@ class DistributedDataParallel(nn.Module):
     def _finalize(self):
         self._queued = False
         if self.reducer is not None:
+            launched = self.reducer.launched()
             self.reducer.finalize()
+            self._steps += 1
+            if hasattr(self.comm, "check_step"):   # desync detector (parallel/debug.py)
+                self.comm.check_step(launched, self._steps)
         self.arena.hook = None
         self.arena.backward_end = None
 
