@@ -3,7 +3,7 @@
 Flags keep the reference names and defaults: --num_epochs, --batch_size (per
 process), --learning_rate, --random_seed, --model_dir, --model_filename, --resume.  Non-breaking
 additions: --arch, --num_classes, --synthetic, --data_root, --image_size, --backend, --device,
---bucket_mb, --workers, --eval_every, --steps_per_epoch.
+--bucket_mb, --workers, --eval_every, --steps_per_epoch, --precision, --graph, --benchmark_steps.
 
 Deliberate fixes of reference quirks (SURVEY.md §7.3): the sampler's epoch is advanced every epoch;
 evaluation runs on the unwrapped module (no stray rank-0-only collective, K8) with a non-augmenting
@@ -27,6 +27,7 @@ from ..models import ARCHS
 from ..ops import CrossEntropyLoss, top1_correct
 from ..optim import SGD
 from ..utils.checkpoint import load_checkpoint, save_checkpoint
+from ..utils.graphs import CapturedStep
 
 
 def build_argparser(variant: str = "main") -> argparse.ArgumentParser:
@@ -55,6 +56,11 @@ def build_argparser(variant: str = "main") -> argparse.ArgumentParser:
     p.add_argument("--steps_per_epoch", type=int, default=0, help="cap steps per epoch (0 = full epoch)")
     p.add_argument("--eval_before_train", action="store_true", default=variant != "main",
                    help="resnet.py variant: evaluate/save before training on eval epochs")
+    p.add_argument("--precision", default="bf16", choices=["bf16", "fp32"],
+                   help="bf16: native gfx950 kernels; fp32: the same schedules on fp32 torch ops")
+    p.add_argument("--graph", action="store_true", help="replay each training step from a captured hipGraph")
+    p.add_argument("--benchmark_steps", type=int, default=0,
+                   help="time this many steps on a synthetic device batch, print images/sec and exit")
     return p
 
 
@@ -83,6 +89,7 @@ def run(args) -> dict:
     device = comm.device if args.device == "auto" else torch.device(args.device)
     set_random_seeds(args.random_seed)
     model = ARCHS[args.arch](num_classes=args.num_classes).to(device)
+    model.precision = args.precision
     ddp = parallel.DistributedDataParallel(model, bucket_cap_mb=args.bucket_mb)
     model_filepath = os.path.join(args.model_dir, args.model_filename)
     if args.resume:
@@ -104,6 +111,25 @@ def run(args) -> dict:
                              num_workers=args.workers, pin_memory=pin)
     criterion = CrossEntropyLoss()
     optimizer = SGD(model.parameters(), lr=args.learning_rate, momentum=0.9, weight_decay=1e-5)
+
+    # the training step reads its batch from fixed tensors so that it can be captured (--graph)
+    x_static = torch.empty((args.batch_size, 3, args.image_size, args.image_size) if args.synthetic else
+                           (args.batch_size, 3, 32, 32), device=device)
+    y_static = torch.zeros(args.batch_size, dtype=torch.int64, device=device)
+
+    def train_step(x, y):
+        optimizer.zero_grad()
+        loss = criterion(ddp(x), y)
+        loss.backward()
+        optimizer.step()
+        return loss
+
+    captured = None
+    if args.graph and device.type == "cuda":
+        captured = CapturedStep(lambda: train_step(x_static, y_static), warmup=2, inputs=(x_static, y_static))
+
+    if args.benchmark_steps:
+        return benchmark(args, train_step, captured, x_static, y_static, comm, device)
 
     history = {"loss": [], "accuracy": [], "images_per_sec": []}
 
@@ -128,10 +154,11 @@ def run(args) -> dict:
             for inputs, labels in train_loader:
                 inputs = inputs.to(device, non_blocking=True)
                 labels = labels.to(device, non_blocking=True)
-                optimizer.zero_grad()
-                loss = criterion(ddp(inputs), labels)
-                loss.backward()
-                optimizer.step()
+                if captured is not None and inputs.shape[0] == args.batch_size:
+                    captured.set_inputs(inputs, labels)
+                    loss = captured()
+                else:   # eager step (also the ragged last batch of a graph run)
+                    loss = train_step(inputs, labels)
                 loss_sum += loss.detach()
                 nb += 1
                 if args.steps_per_epoch and nb >= args.steps_per_epoch:
@@ -147,6 +174,33 @@ def run(args) -> dict:
     finally:
         parallel.destroy_distributed()
     return history
+
+
+def benchmark(args, train_step, captured, x, y, comm, device) -> dict:
+    """--benchmark_steps: synthetic device batch, 3 warm-up steps, timed steps, images/sec."""
+    g = torch.Generator(device=device).manual_seed(1234 + comm.rank)
+    x.copy_(torch.randn(x.shape, generator=g, device=device))
+    y.copy_(torch.randint(args.num_classes, y.shape, generator=g, device=device))
+    step = captured if captured is not None else (lambda: train_step(x, y))
+    for _ in range(3):
+        step()
+    comm.barrier()
+    if device.type == "cuda":
+        torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.benchmark_steps):
+        loss = step()
+    comm.barrier()
+    if device.type == "cuda":
+        torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    ips = args.batch_size * comm.world_size * args.benchmark_steps / dt
+    if comm.rank == 0:
+        print(f"benchmark: {args.arch} bs={args.batch_size}/rank x {comm.world_size} ranks, "
+              f"{args.benchmark_steps} steps: {ips:.1f} images/sec ({dt / args.benchmark_steps * 1e3:.2f} ms/step), "
+              f"loss {float(loss.detach()):.4f}")
+    parallel.destroy_distributed()
+    return {"images_per_sec": ips}
 
 
 def main(variant="main", argv=None):

@@ -29,6 +29,7 @@ from ..data import CarvanaDataset, DistributedSampler, SyntheticMasks
 from ..models import UNet
 from ..ops import BCEWithLogitsLoss, dice_per_sample
 from ..optim import Adam, clip_grad_norm_
+from ..utils.graphs import CapturedStep
 from ..utils.checkpoint import load_checkpoint, save_checkpoint
 
 
@@ -55,6 +56,12 @@ def build_argparser() -> argparse.ArgumentParser:
     p.add_argument("--workers", type=int, default=max(1, (os.cpu_count() or 2) // 2))
     p.add_argument("--log_dir", default="logs")
     p.add_argument("--eval_every", type=int, default=10)
+    p.add_argument("--bucket_mb", type=float, default=None)
+    p.add_argument("--precision", default="bf16", choices=["bf16", "fp32"],
+                   help="bf16: native gfx950 kernels; fp32: the same schedules on fp32 torch ops")
+    p.add_argument("--graph", action="store_true", help="replay each training step from a captured hipGraph")
+    p.add_argument("--benchmark_steps", type=int, default=0,
+                   help="time this many steps on a synthetic device batch, print images/sec and exit")
     return p
 
 
@@ -111,6 +118,33 @@ def build_data_loaders(args, device):
     return (DataLoader(train_ds, sampler=sampler, **kw), DataLoader(test_ds, shuffle=False, **kw), sampler)
 
 
+def benchmark(args, train_step, captured, x, y, comm, device) -> dict:
+    """--benchmark_steps: synthetic device batch, 3 warm-up steps, timed steps, images/sec."""
+    g = torch.Generator(device=device).manual_seed(1234 + comm.rank)
+    x.copy_(torch.randn(x.shape, generator=g, device=device))
+    y.copy_((torch.rand(y.shape, generator=g, device=device) > 0.5).float())
+    step = captured if captured is not None else (lambda: train_step(x, y))
+    for _ in range(3):
+        step()
+    comm.barrier()
+    if device.type == "cuda":
+        torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.benchmark_steps):
+        loss = step()
+    comm.barrier()
+    if device.type == "cuda":
+        torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    ips = args.batch_size * comm.world_size * args.benchmark_steps / dt
+    if comm.rank == 0:
+        print(f"benchmark: UNet {args.in_channels}x{args.image_size}^2 bs={args.batch_size}/rank x {comm.world_size} "
+              f"ranks, {args.benchmark_steps} steps: {ips:.2f} images/sec ({dt / args.benchmark_steps * 1e3:.1f} "
+              f"ms/step), loss {float(loss.detach()):.4f}")
+    parallel.destroy_distributed()
+    return {"images_per_sec": ips}
+
+
 def run(args) -> dict:
     comm = parallel.init_distributed(args.backend)
     rank, world, local_rank = comm.rank, comm.world_size, comm.local_rank
@@ -126,12 +160,32 @@ def run(args) -> dict:
 
     train_loader, test_loader, sampler = build_data_loaders(args, device)
     model = UNet(out_classes=1, up_sample_mode=args.up_sample_mode, in_channels=args.in_channels).to(device)
-    ddp = parallel.DistributedDataParallel(model)
+    model.precision = args.precision
+    ddp = parallel.DistributedDataParallel(model, bucket_cap_mb=args.bucket_mb)
     model_filepath = os.path.join(args.model_dir, args.model_filename)
     if args.resume:
         load_checkpoint(ddp, model_filepath, map_location=device)
     optimizer = Adam(model.parameters(), lr=args.learning_rate)
     criterion = BCEWithLogitsLoss()
+
+    def train_step(images, masks):
+        pred = ddp(images).squeeze(1)
+        loss = criterion(pred, masks)
+        optimizer.zero_grad()
+        loss.backward()
+        # collective NaN/Inf guard: a non-finite all-reduced grad norm skips the step on all ranks
+        clip_grad_norm_(model.parameters(), max_norm=args.max_norm, optimizer=optimizer)
+        optimizer.step()
+        return loss
+
+    S = args.image_size
+    x_static = torch.zeros(args.batch_size, args.in_channels, S, S, device=device)
+    y_static = torch.zeros(args.batch_size, S, S, device=device)
+    captured = None
+    if args.graph and device.type == "cuda":
+        captured = CapturedStep(lambda: train_step(x_static, y_static), warmup=2, inputs=(x_static, y_static))
+    if args.benchmark_steps:
+        return benchmark(args, train_step, captured, x_static, y_static, comm, device)
     history = {"loss": [], "dice": []}
     if rank == 0:
         print(f"Logging training progress to: {log.path}")
@@ -146,13 +200,11 @@ def run(args) -> dict:
             for batch in train_loader:
                 images = batch["image"].to(device, dtype=torch.float32, non_blocking=True)
                 masks = batch["mask"].to(device, dtype=torch.float32, non_blocking=True)
-                pred = ddp(images).squeeze(1)
-                loss = criterion(pred, masks)
-                optimizer.zero_grad()
-                loss.backward()
-                # collective NaN/Inf guard: a non-finite all-reduced grad norm skips the step on all ranks
-                clip_grad_norm_(model.parameters(), max_norm=args.max_norm, optimizer=optimizer)
-                optimizer.step()
+                if captured is not None and images.shape == x_static.shape:
+                    captured.set_inputs(images, masks)
+                    loss = captured()
+                else:
+                    loss = train_step(images, masks)
                 loss_sum += torch.nan_to_num(loss.detach(), nan=0.0, posinf=0.0, neginf=0.0)
                 nb += 1
                 if args.steps_per_epoch and nb >= args.steps_per_epoch:

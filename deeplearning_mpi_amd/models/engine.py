@@ -226,6 +226,7 @@ class EngineModule(nn.Module):
         self._anchor = torch.zeros(0, requires_grad=True)
         # BN-backward reductions fused into the producing dgrad epilogue (DLMPI_FUSE_BN_BWD=0: off)
         self.fuse_bn_bwd = os.environ.get("DLMPI_FUSE_BN_BWD", "1") != "0"
+        self.precision = "bf16"    # "fp32": run the schedules on fp32 torch ops (set before first use)
 
     def engine_setup(self, device=None):
         if device is None:
@@ -233,7 +234,7 @@ class EngineModule(nn.Module):
         device = torch.device(device)
         if self._arena is not None and self._arena.device == device and self._arena.valid():
             return self._arena
-        self._be = make_backend(device, next(self.parameters()).dtype)
+        self._be = make_backend(device, next(self.parameters()).dtype, self.precision)
         self._arena = ParamArena(self, device, self._be)
         self._build_units(self._arena)
         self._arena.refresh(force=True)

@@ -430,8 +430,15 @@ class RefBackend:
         x.mul_(coef[0])
 
 
-def make_backend(device, dtype=torch.float32) -> "NativeBackend | RefBackend":
+def make_backend(device, dtype=torch.float32, precision: str = "bf16") -> "NativeBackend | RefBackend":
+    """GPU + bf16 (default): the native gfx950 kernels.  GPU + ``precision='fp32'``: the same engine
+    schedules on fp32 torch ops (the ``--precision fp32`` option of the apps; a numerics reference,
+    not a fast path).  CPU: the reference backend in the parameters' dtype."""
     device = torch.device(device)
     if device.type == "cuda":
+        if precision == "fp32":
+            return RefBackend(device, torch.float32)
+        if precision != "bf16":
+            raise ValueError(f"precision must be bf16 or fp32, got {precision!r}")
         return NativeBackend(device)
     return RefBackend(device, dtype)
