@@ -102,6 +102,11 @@ static void fill_epilogue(ConvArgs& a, at::Tensor& y, int ldy, int yoff, const c
   a.relu = relu ? 1 : 0;
   a.stats = optr<float>(stats);
   a.nstat = 2;
+  static const int nt = [] {
+    const char* e = getenv("DLMPI_NT_STORE");
+    return e ? atoi(e) : 0;
+  }();
+  a.nt_store = nt;
 }
 
 // y[n, p, q, yoff + k] = epilogue( sum_{r,s,c} x[n, p*stride - pad + r, q*stride - pad + s, xoff + c] * w[k][r][s][c] )
@@ -160,7 +165,9 @@ c10::optional<at::Tensor> conv2d_dgrad(const at::Tensor& dy, int N, int P, int Q
                                        at::Tensor dx, int lddx, int dxoff, const c10::optional<at::Tensor>& res,
                                        int ldres, int resoff, const c10::optional<at::Tensor>& mask, int ldmask,
                                        int maskoff, const c10::optional<at::Tensor>& z, int ldz, int zoff,
-                                       const c10::optional<at::Tensor>& z2, int ldz2, int z2off) {
+                                       const c10::optional<at::Tensor>& z2, int ldz2, int z2off,
+                                       const c10::optional<at::Tensor>& mscale,
+                                       const c10::optional<at::Tensor>& mshift) {
   require_gpu(dy, "dy");
   if (stride > 2) throw std::runtime_error("conv2d_dgrad: stride <= 2 supported");
   ConvArgs a{};
@@ -180,9 +187,12 @@ c10::optional<at::Tensor> conv2d_dgrad(const at::Tensor& dy, int N, int P, int Q
   a.ldz = ldz; a.zoff = zoff;
   a.z2 = optr<uint16_t>(z2);
   a.ldz2 = ldz2; a.z2off = z2off;
+  a.mscale = optr<float>(mscale);
+  a.mshift = optr<float>(mshift);
   a.nstat = a.z2 ? 3 : 2;
-  if (a.z && !a.mask) throw std::runtime_error("conv2d_dgrad: fused BN statistics need the ReLU mask");
-  if (a.mask && ((ldmask | maskoff | ldz | zoff | ldz2 | z2off) % 8 != 0 || !a.vec_store))
+  if (a.z && !a.mask && !a.mscale) throw std::runtime_error("conv2d_dgrad: fused BN statistics need the ReLU mask");
+  if (a.mscale && (!a.z || !a.mshift)) throw std::runtime_error("conv2d_dgrad: mask from z needs z, scale, shift");
+  if ((a.mask || a.mscale) && ((ldmask | maskoff | ldz | zoff | ldz2 | z2off) % 8 != 0 || !a.vec_store))
     throw std::runtime_error("conv2d_dgrad: fused BN tensors must be 8-channel aligned");
   set_kstep(a, K);
   int bm, bn;

@@ -241,7 +241,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(STAGES == 1
   float s1[8], s2[8], s3[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) { s1[e] = 0.f; s2[e] = 0.f; s3[e] = 0.f; }
-  const bool bwd = a.mask != nullptr;   // gradient of a BN+ReLU output: mask, then {sum dy, sum dy*z}
+  // gradient of a BN+ReLU output: mask, then {sum dy, sum dy*z}
+  const bool bwd = a.mask != nullptr || a.mscale != nullptr;
 
   // NP passes over row slices: in pass h every wave dumps its fragments mi in
   // [h*TM/NP, (h+1)*TM/NP), i.e. tile rows wm*WM + h*HM + [0, HM), into a BM/NP-row buffer.
@@ -294,13 +295,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(STAGES == 1
       for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.f);
     }
     if (bwd) {
-      float yy[8];
-      unpack8(*reinterpret_cast<const u32x4*>(a.mask + pix * a.ldmask + a.maskoff + c0), yy);
+      float zz[8];
+      if (a.z) unpack8(*reinterpret_cast<const u32x4*>(a.z + pix * a.ldz + a.zoff + c0), zz);
+      if (a.mask) {
+        float yy[8];
+        unpack8(*reinterpret_cast<const u32x4*>(a.mask + pix * a.ldmask + a.maskoff + c0), yy);
 #pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] = yy[e] > 0.f ? v[e] : 0.f;
+        for (int e = 0; e < 8; ++e) v[e] = yy[e] > 0.f ? v[e] : 0.f;
+      } else {   // same fma as the forward BN-apply -> same sign as y
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = zz[e] * a.mscale[c0 + e] + a.mshift[c0 + e] > 0.f ? v[e] : 0.f;
+      }
       if (a.stats) {
-        float zz[8];
-        unpack8(*reinterpret_cast<const u32x4*>(a.z + pix * a.ldz + a.zoff + c0), zz);
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
           const float rv = bf2f(f2bf(v[e]));   // statistics of the stored (bf16) gradient
@@ -321,7 +327,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(STAGES == 1
         *reinterpret_cast<f32x4*>(yp + 4) = f32x4{v[4], v[5], v[6], v[7]};
       } else {
         uint16_t* yp = reinterpret_cast<uint16_t*>(a.y) + pix * a.ldy + a.yoff + c0;
-        *reinterpret_cast<u32x4*>(yp) = pack8(v);
+        if (a.nt_store) __builtin_nontemporal_store(pack8(v), reinterpret_cast<u32x4*>(yp));
+        else *reinterpret_cast<u32x4*>(yp) = pack8(v);
       }
     } else {   // narrow / unaligned output (e.g. the 1-channel UNet head written as fp32 [N,1,H,W])
 #pragma unroll

@@ -67,13 +67,16 @@ struct ConvArgs {
   // Backward fusion (the GEMM produces the gradient dy of a BatchNorm+ReLU output y):
   //   v := v * [mask > 0] (ReLU derivative) before the store, and the stats become
   //   {sum v, sum v*z [, sum v*z2]} with z (z2) the BN input(s) that consume this gradient.
-  const uint16_t* mask;
+  const uint16_t* mask;            // ReLU output y (mask = y > 0), or null with mscale set:
   int ldmask, maskoff;
+  const float* mscale;             //   mask = z * mscale + mshift > 0 (BN+ReLU without residual:
+  const float* mshift;             //   recomputed from z, which the stats read anyway)
   const uint16_t* z;
   int ldz, zoff;
   const uint16_t* z2;
   int ldz2, z2off;
   int nstat;                       // 2 (fwd: sum v, sum v^2; bwd: sum v, sum v*z) or 3 (bwd with z2)
+  int nt_store;                    // 1: non-temporal output stores (streaming outputs)
   int ntiles;
   int nphase;
   int cstep, tstep;                // K-iteration: c += cstep, t += tstep per 64-wide step

@@ -20,6 +20,7 @@ One ``torch.autograd.Function`` bridges the engine to autograd (loss.backward() 
 from __future__ import annotations
 
 import os
+from typing import NamedTuple, Optional
 
 import torch
 import torch.nn as nn
@@ -27,6 +28,18 @@ import torch.nn as nn
 from ..ops.act import Act, padc
 from ..ops.backend import make_backend
 from ..utils.arena import ParamArena
+
+
+class BwdFuse(NamedTuple):
+    """What a data-gradient GEMM needs to produce the gradient of a BN+ReLU output fused: the ReLU
+    mask (``mask`` = the saved output y, or -- for BN+ReLU without a residual -- recomputed from the
+    BN input as z*scale + shift > 0, saving the read of y), the BN input(s) z (z2: a second BN
+    consuming the same gradient, the ResNet downsample branch) for the backward statistics."""
+    mask: Optional[Act]
+    z: Act
+    z2: Optional[Act] = None
+    scale: Optional[torch.Tensor] = None
+    shift: Optional[torch.Tensor] = None
 
 
 class ConvUnit:
@@ -100,7 +113,7 @@ class ConvUnit:
                            bn.running_var if bn.track_running_stats else None, mom, bn.eps, scale, shift, mean,
                            invstd)
             be.bn_apply(z, scale, shift, res, self.relu, y)
-            return y, ((x, z, y, mean, invstd) if save else None)
+            return y, ((x, z, y, mean, invstd, scale, shift, res is not None) if save else None)
         # eval: fold BN (and conv bias) into the GEMM epilogue
         invstd = torch.rsqrt(bn.running_var + bn.eps)
         scale = bn.weight.data * invstd if bn.affine else invstd
@@ -112,11 +125,13 @@ class ConvUnit:
         return y, None
 
     @staticmethod
-    def fuse_spec(ctx):
-        """(ReLU output y, BN input z) of a trained BN+ReLU unit: what a producer of dy needs to
-        fuse this unit's BN-backward reduction into its data-gradient epilogue."""
-        x, z, y, mean, invstd = ctx
-        return y, z
+    def fuse_spec(ctx, z2=None) -> BwdFuse:
+        """What a producer of this (trained BN+ReLU) unit's output gradient needs to fuse the
+        unit's BN-backward reduction into its data-gradient epilogue."""
+        x, z, y, mean, invstd, scale, shift, has_res = ctx
+        if has_res or z2 is not None:
+            return BwdFuse(y, z, z2)
+        return BwdFuse(None, z, None, scale, shift)
 
     def bwd(self, be, ctx, dy: Act, need_dx=True, dx_res: Act = None, dyr_out: Act = None, ymask: Act = None,
             use_own_mask=True, pre=None, k2=1, fuse_next=None):
@@ -130,7 +145,7 @@ class ConvUnit:
         ar = self.arena
         bn = self.bn
         if bn is not None:
-            x, z, y, mean, invstd = ctx
+            x, z, y, mean, invstd = ctx[:5]
             if pre is not None:
                 mask = None
             else:

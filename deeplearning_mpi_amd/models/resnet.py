@@ -17,7 +17,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from ..ops.act import Act, padc
-from .engine import ConvUnit, EngineModule
+from .engine import BwdFuse, ConvUnit, EngineModule
 
 
 def conv3x3(i, o, stride=1):
@@ -107,8 +107,8 @@ class _BlockExec:
         """(block output y, BN input of the last conv, BN input of the downsample conv | None): the
         previous schedule step fuses this block's BN-backward reductions into its dgrad epilogue."""
         ctxs, cd = st
-        y, z = ConvUnit.fuse_spec(ctxs[-1])
-        return y, z, (cd[1] if cd is not None else None)
+        x, z, y = ctxs[-1][:3]
+        return BwdFuse(y, z, cd[1] if cd is not None else None)
 
     def bwd(self, be, st, dy: Act, pre=None, fuse_prev=None):
         """dy: gradient of the block output.  With ``pre`` (partials from the producer's dgrad
@@ -117,7 +117,7 @@ class _BlockExec:
         ctxs, cd = st
         ylast = ctxs[-1][2]
         n = len(self.u)
-        spec = lambda k: ConvUnit.fuse_spec(ctxs[k]) + (None,)   # noqa: E731
+        spec = lambda k: ConvUnit.fuse_spec(ctxs[k])   # noqa: E731
         if pre is not None:
             dh, part = self.u[-1].bwd(be, ctxs[-1], dy, pre=pre, k2=1, fuse_next=spec(n - 2))
             for k in range(n - 2, 0, -1):

@@ -172,7 +172,7 @@ class UNet(EngineModule):
         cats, ctx_enc, idxs, skips, (cba, cbb), ctx_dec, cl = state
 
         def spec(ctx):
-            return ConvUnit.fuse_spec(ctx) + (None,) if fuse else None
+            return ConvUnit.fuse_spec(ctx) if fuse else None
 
         def double_bwd(units, ca, cb, dy, pre=None, need_dx=True):
             ua, ub = units

@@ -41,15 +41,16 @@ class NativeBackend:
                           res.off if res is not None else 0, scale, shift, bool(relu), stats, 0, int(kvalid))
 
     def conv_dgrad(self, dy: Act, wT, C, R, S, stride, pad, dx: Act, res: Act = None, fuse=None):
-        """fuse = (mask, z, z2|None): dx is the gradient of relu(BN(z) [+ BN2(z2)]) = mask; the
-        epilogue applies the ReLU mask and returns BN-backward partials [tiles][2|3][C]."""
-        m, z, z2 = fuse if fuse is not None else (None, None, None)
+        """fuse = BwdFuse(mask, z, z2, scale, shift): dx is the gradient of relu(BN(z) [+ BN2(z2)]);
+        the epilogue applies the ReLU mask (y > 0, or z*scale + shift > 0 without a residual) and
+        returns BN-backward partials [tiles][2|3][C]."""
+        m, z, z2, sc, sh = fuse if fuse is not None else (None, None, None, None, None)
 
         def t(a):
             return (a.buf, a.ld, a.off) if a is not None else (None, 0, 0)
 
         return self.C.conv2d_dgrad(dy.buf, dy.N, dy.H, dy.W, dy.C, dy.ld, dy.off, wT, C, R, S, stride, pad, dx.H,
-                                   dx.W, dx.buf, dx.ld, dx.off, *t(res), *t(m), *t(z), *t(z2))
+                                   dx.W, dx.buf, dx.ld, dx.off, *t(res), *t(m), *t(z), *t(z2), sc, sh)
 
     def convT_fwd(self, x: Act, wf, Cout, y: Act, bias=None):
         self.C.convT2x2_fwd(x.buf, x.N, x.H, x.W, x.C, x.ld, x.off, wf, Cout, y.buf, y.ld, y.off, bias)
@@ -240,8 +241,12 @@ class RefBackend:
         if fuse is None:
             self._store(dx, g)
             return None
-        m, z, z2 = fuse
-        g = g * (m.nchw() > 0)
+        m, z, z2, sc, sh = fuse
+        if m is not None:
+            g = g * (m.nchw() > 0)
+        else:   # mask recomputed from the BN input, as the forward BN-apply computed y
+            keep = (z.nhwc().to(self.dt) * sc + sh) > 0
+            g = g * keep.permute(0, 3, 1, 2)
         self._store(dx, g)
         v = dx.nhwc().to(self.dt)
         rows = [v.sum((0, 1, 2)), (v * z.nhwc().to(self.dt)).sum((0, 1, 2))]

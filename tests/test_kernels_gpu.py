@@ -5,6 +5,7 @@ import pytest
 import torch
 
 from deeplearning_mpi_amd.ops.act import Act, pad8
+from deeplearning_mpi_amd.models.engine import BwdFuse
 from deeplearning_mpi_amd.ops.backend import NativeBackend, RefBackend
 
 pytestmark = pytest.mark.gpu
@@ -116,8 +117,8 @@ def test_conv_fwd_256_row_tile(shape):
 
 
 @pytest.mark.parametrize("shape", [CONV_SHAPES[1], CONV_SHAPES[2], CONV_SHAPES[3], CONV_SHAPES[5]])
-@pytest.mark.parametrize("two", [False, True])
-def test_conv_dgrad_fused_bn_backward(shape, two):
+@pytest.mark.parametrize("mode", ["mask", "two", "from_z"])
+def test_conv_dgrad_fused_bn_backward(shape, mode):
     """dgrad epilogue: + residual, ReLU mask of the consumer, BN-backward partials
     {sum dx, sum dx*z [, sum dx*z2]} (multi-phase tile numbering for stride 2), then the
     finalize/apply path that consumes them."""
@@ -130,15 +131,21 @@ def test_conv_dgrad_fused_bn_backward(shape, two):
     res, resr = _act(N, H, W, Cp)
     m, mr = _act(N, H, W, Cp)
     z, zr = _act(N, H, W, Cp)
+    two = mode == "two"
     z2, z2r = _act(N, H, W, Cp) if two else (None, None)
+    sc = sh = None
+    if mode == "from_z":   # mask recomputed from the BN input: z*scale + shift > 0
+        sc, sh = torch.rand(Cp, device=DEV) + 0.5, torch.randn(Cp, device=DEV) * 0.5
+        m = mr = None
     dx = _empty(N, H, W, Cp)
     dxr = _empty(N, H, W, Cp, torch.float32)
-    part = nb.conv_dgrad(dy, wT, Cp, R, R, s, p, dx, res=res, fuse=(m, z, z2))
-    rb.conv_dgrad(dyr, wT.float(), Cp, R, R, s, p, dxr, res=resr, fuse=(mr, zr, z2r))
+    part = nb.conv_dgrad(dy, wT, Cp, R, R, s, p, dx, res=res, fuse=BwdFuse(m, z, z2, sc, sh))
+    rb.conv_dgrad(dyr, wT.float(), Cp, R, R, s, p, dxr, res=resr, fuse=BwdFuse(mr, zr, z2r, sc, sh))
     torch.cuda.synchronize()
     assert part.shape[1] == (3 if two else 2) and part.shape[2] == Cp
     assert _rel(dx.buf, dxr.buf) < 1e-2
-    assert torch.equal(dx.buf == 0, (m.buf <= 0) | (dx.buf == 0))   # masked lanes are exactly zero
+    keep = (m.buf > 0) if m is not None else (z.buf.float() * sc + sh > 0)
+    assert (dx.buf[~keep] == 0).all()   # masked lanes are exactly zero
     # partials are sums of the stored bf16 gradient: compare against the same sums in fp64
     v = dx.buf.double()
     ref = [v.sum(0), (v * z.buf.double()).sum(0)] + ([(v * z2.buf.double()).sum(0)] if two else [])
