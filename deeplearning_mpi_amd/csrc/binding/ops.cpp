@@ -274,6 +274,7 @@ void conv2d_wgrad(const at::Tensor& dy, int lddy, int dyoff, int Ko, const at::T
   a.stride_h = stride; a.stride_w = stride; a.pad_h = pad; a.pad_w = pad;
   a.TC = R * S * C;
   a.npix = N * P * Q;
+  a.direct = (R == 1 && S == 1 && stride == 1 && pad == 0 && P == H && Q == W) ? 1 : 0;
   const int bm = Ko <= 64 ? 64 : 128;
   a.mtiles = ceil_div(Ko, bm);
   a.ntiles = ceil_div(a.TC, 128);

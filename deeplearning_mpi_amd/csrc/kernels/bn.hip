@@ -11,6 +11,8 @@
 //   dyr = dy * [y > 0];  dbeta = sum dyr;  dgamma = sum dyr * xhat;
 //   dx  = k1*dyr + k2*x + k3   (k* folded per channel by the finalize kernel).
 // All tensors may be channel slices of a wider buffer (ld*, *off) so UNet's skip concat is free.
+#include <cstdlib>
+
 #include "common.h"
 
 namespace dlmpi {
@@ -112,31 +114,135 @@ static inline int colsum_slices(int T) {
   return S < 1 ? 1 : (S > 64 ? 64 : S);
 }
 
-__global__ __launch_bounds__(256) void bn_finalize_kernel(const double* __restrict__ dpart, int S, int C,
-                                                          double count, const float* gamma, const float* beta,
-                                                          float* running_mean, float* running_var, float momentum,
-                                                          float eps, float* scale, float* shift, float* save_mean,
-                                                          float* save_invstd) {
+// Per-channel finalize bodies, shared by the two-kernel path and the fused last-arriver path.
+struct FinArgs {
+  int mode;   // 0: forward statistics -> scale/shift (+ running stats); 1: backward coefficients
+  double count;
+  const float* gamma;
+  const float* beta;
+  float* running_mean;
+  float* running_var;
+  float momentum, eps;
+  float* scale;
+  float* shift;
+  float* save_mean;
+  float* save_invstd;
+  const float* mean;     // backward
+  const float* invstd;
+  float* dgamma;
+  float* dbeta;
+  float* coef;
+  int raw_z;
+};
+
+__device__ __forceinline__ void fin_fwd(const FinArgs& f, int c, double s1, double s2) {
+  const double mean = s1 / f.count;
+  double var = s2 / f.count - mean * mean;
+  if (var < 0.0) var = 0.0;
+  const float invstd = (float)(1.0 / sqrt(var + (double)f.eps));
+  const float g = f.gamma ? f.gamma[c] : 1.f;
+  const float b = f.beta ? f.beta[c] : 0.f;
+  const float sc = g * invstd;
+  f.scale[c] = sc;
+  f.shift[c] = b - (float)mean * sc;
+  if (f.save_mean) f.save_mean[c] = (float)mean;
+  if (f.save_invstd) f.save_invstd[c] = invstd;
+  if (f.running_mean) {
+    const double unbiased = f.count > 1.0 ? var * f.count / (f.count - 1.0) : var;
+    f.running_mean[c] = (1.f - f.momentum) * f.running_mean[c] + f.momentum * (float)mean;
+    f.running_var[c] = (1.f - f.momentum) * f.running_var[c] + f.momentum * (float)unbiased;
+  }
+}
+
+// coef[0..2][C] = (k1, k2, k3) with dx = k1*dyr + k2*x + k3; dgamma/dbeta accumulate.
+__device__ __forceinline__ void fin_bwd(const FinArgs& f, int c, double s1, double s2, int C) {
+  // raw_z: the second sum is sum dyr*z (BN input), not sum dyr*xhat
+  if (f.raw_z) s2 = (double)f.invstd[c] * (s2 - (double)f.mean[c] * s1);
+  if (f.dbeta) f.dbeta[c] += (float)s1;
+  if (f.dgamma) f.dgamma[c] += (float)s2;
+  if (f.coef) {
+    const double is = f.invstd[c];
+    const double k1 = (f.gamma ? (double)f.gamma[c] : 1.0) * is;
+    const double k2 = -k1 * is * s2 / f.count;
+    const double k3 = -k1 * s1 / f.count - k2 * (double)f.mean[c];
+    f.coef[c] = (float)k1;
+    f.coef[C + c] = (float)k2;
+    f.coef[2 * C + c] = (float)k3;
+  }
+}
+
+__global__ __launch_bounds__(256) void finalize_kernel(const double* __restrict__ dpart, int S, int C, FinArgs f) {
   const int c = blockIdx.x * 256 + threadIdx.x;
   if (c < C) {
     double s1, s2;
     colsum2_final(dpart, S, C, c, s1, s2);
-    const double mean = s1 / count;
-    double var = s2 / count - mean * mean;
-    if (var < 0.0) var = 0.0;
-    const float invstd = (float)(1.0 / sqrt(var + (double)eps));
-    const float g = gamma ? gamma[c] : 1.f;
-    const float b = beta ? beta[c] : 0.f;
-    const float sc = g * invstd;
-    scale[c] = sc;
-    shift[c] = b - (float)mean * sc;
-    if (save_mean) save_mean[c] = (float)mean;
-    if (save_invstd) save_invstd[c] = invstd;
-    if (running_mean) {
-      const double unbiased = count > 1.0 ? var * count / (count - 1.0) : var;
-      running_mean[c] = (1.f - momentum) * running_mean[c] + momentum * (float)mean;
-      running_var[c] = (1.f - momentum) * running_var[c] + momentum * (float)unbiased;
+    if (f.mode == 0) fin_fwd(f, c, s1, s2);
+    else fin_bwd(f, c, s1, s2, C);
+  }
+}
+
+// Fused column reduction + finalize: colsum2 for slice s of channel group g, then the LAST block
+// of group g to finish (agent-scope release -> ticket -> acquire, cdna_hip_programming.md
+// "In-launch split-K reduction") sums the S slice partials in a fixed order and finalizes the
+// group's 64 channels.  Saves the second launch of every BN finalize.  Tickets self-reset.
+__global__ __launch_bounds__(256) void colsum_fin_kernel(const float* __restrict__ partial, int T, int C, int ns,
+                                                         int k2, double* __restrict__ dpart, int* __restrict__ tickets,
+                                                         FinArgs f) {
+  __shared__ double r[2][4][64];
+  __shared__ int last;
+  const int lc = threadIdx.x & 63, rl = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + lc;
+  const int S = gridDim.y, s = blockIdx.y;
+  const int per = (T + S - 1) / S;
+  const int t0 = s * per, t1 = min(T, t0 + per);
+  double a = 0.0, b = 0.0;
+  if (c < C) {
+#pragma unroll 8
+    for (int t = t0 + rl; t < t1; t += 4) {
+      a += (double)partial[(int64_t)t * ns * C + c];
+      b += (double)partial[(int64_t)t * ns * C + k2 * C + c];
     }
+  }
+  r[0][rl][lc] = a;
+  r[1][rl][lc] = b;
+  __syncthreads();
+  if (rl == 0 && c < C) {
+    for (int g = 1; g < 4; ++g) { a += r[0][g][lc]; b += r[1][g][lc]; }
+    dpart[(int64_t)s * 2 * C + c] = a;
+    dpart[(int64_t)s * 2 * C + C + c] = b;
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    last = __hip_atomic_fetch_add(&tickets[blockIdx.x], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == S - 1;
+  }
+  __syncthreads();
+  if (!last) return;
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __hip_atomic_store(&tickets[blockIdx.x], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+  a = 0.0;
+  b = 0.0;
+  if (c < C) {
+#pragma unroll 4
+    for (int q = rl; q < S; q += 4) {
+      a += dpart[(int64_t)q * 2 * C + c];
+      b += dpart[(int64_t)q * 2 * C + C + c];
+    }
+  }
+  __syncthreads();   // r is reused
+  r[0][rl][lc] = a;
+  r[1][rl][lc] = b;
+  __syncthreads();
+  if (rl == 0 && c < C) {
+    for (int g = 1; g < 4; ++g) { a += r[0][g][lc]; b += r[1][g][lc]; }
+    if (f.mode == 0) fin_fwd(f, c, a, b);
+    else fin_bwd(f, c, a, b, C);
   }
 }
 
@@ -221,33 +327,6 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const uint16_t* __re
   block_combine<2>(acc, rm, C, partial);
 }
 
-// Reduces the bwd partials; accumulates dgamma/dbeta into the gradient buffers; emits
-// coef[0..2][C] = (k1, k2, k3) with dx = k1*dyr + k2*x + k3.
-__global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(const double* __restrict__ dpart, int S, int C,
-                                                              double count, const float* gamma,
-                                                              const float* __restrict__ mean,
-                                                              const float* __restrict__ invstd, float* dgamma,
-                                                              float* dbeta, float* coef, int raw_z) {
-  const int c = blockIdx.x * 256 + threadIdx.x;
-  if (c < C) {
-    double s1, s2;
-    colsum2_final(dpart, S, C, c, s1, s2);
-    // raw_z: the second sum is sum dyr*z (BN input), not sum dyr*xhat
-    if (raw_z) s2 = (double)invstd[c] * (s2 - (double)mean[c] * s1);
-    if (dbeta) dbeta[c] += (float)s1;
-    if (dgamma) dgamma[c] += (float)s2;
-    if (coef) {
-      const double is = invstd[c];
-      const double k1 = (gamma ? (double)gamma[c] : 1.0) * is;
-      const double k2 = -k1 * is * s2 / count;
-      const double k3 = -k1 * s1 / count - k2 * (double)mean[c];
-      coef[c] = (float)k1;
-      coef[C + c] = (float)k2;
-      coef[2 * C + c] = (float)k3;
-    }
-  }
-}
-
 __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const uint16_t* __restrict__ dy, int lddy, int dyoff,
                                                            const uint16_t* __restrict__ ym, int ldym, int ymoff,
                                                            const uint16_t* __restrict__ x, int ldx, int xoff,
@@ -313,15 +392,61 @@ extern "C" hipError_t dlmpi_bn_stats(const uint16_t* x, int64_t M, int C, int ld
 
 extern "C" int dlmpi_colsum_ws_doubles(int T, int C) { return colsum_slices(T) * 2 * C; }
 
+// Self-resetting per-channel-group tickets of colsum_fin_kernel, one array per device, zeroed once
+// (the first use happens before any hipGraph capture: the warm-up steps run eagerly).
+static int* fin_tickets() {
+  static int* t[64] = {};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+  if (!t[dev]) {
+    int* p = nullptr;
+    if (hipMalloc(&p, 4096 * sizeof(int)) != hipSuccess) return nullptr;
+    if (hipMemset(p, 0, 4096 * sizeof(int)) != hipSuccess) return nullptr;
+    t[dev] = p;
+  }
+  return t[dev];
+}
+
+static bool fused_finalize() {
+  static const bool v = [] {
+    const char* e = getenv("DLMPI_BN_FUSED_FINALIZE");
+    return !(e && atoi(e) == 0);
+  }();
+  return v;
+}
+
+static hipError_t colsum_finalize(const float* partial, int T, int C, int ns, int k2, double* ws, const FinArgs& f,
+                                  hipStream_t s) {
+  const int S = colsum_slices(T);
+  const int G = (C + 63) / 64;
+  int* tk = fused_finalize() && G <= 4096 ? fin_tickets() : nullptr;
+  if (tk) {
+    hipLaunchKernelGGL(colsum_fin_kernel, dim3(G, S), dim3(256), 0, s, partial, T, C, ns, k2, ws, tk, f);
+  } else {
+    hipLaunchKernelGGL(colsum2_kernel, dim3(G, S), dim3(256), 0, s, partial, T, C, ns, k2, ws);
+    hipLaunchKernelGGL(finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, s, ws, S, C, f);
+  }
+  return hipGetLastError();
+}
+
 extern "C" hipError_t dlmpi_bn_finalize(const float* partial, int ntiles, int C, double count, const float* gamma,
                                         const float* beta, float* running_mean, float* running_var, float momentum,
                                         float eps, float* scale, float* shift, float* save_mean, float* save_invstd,
                                         double* ws, hipStream_t s) {
-  const int S = colsum_slices(ntiles);
-  hipLaunchKernelGGL(colsum2_kernel, dim3((C + 63) / 64, S), dim3(256), 0, s, partial, ntiles, C, 2, 1, ws);
-  hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, s, ws, S, C, count, gamma, beta,
-                     running_mean, running_var, momentum, eps, scale, shift, save_mean, save_invstd);
-  return hipGetLastError();
+  FinArgs f{};
+  f.mode = 0;
+  f.count = count;
+  f.gamma = gamma;
+  f.beta = beta;
+  f.running_mean = running_mean;
+  f.running_var = running_var;
+  f.momentum = momentum;
+  f.eps = eps;
+  f.scale = scale;
+  f.shift = shift;
+  f.save_mean = save_mean;
+  f.save_invstd = save_invstd;
+  return colsum_finalize(partial, ntiles, C, 2, 1, ws, f, s);
 }
 
 extern "C" hipError_t dlmpi_bn_apply(const uint16_t* x, int ldx, int xoff, int64_t M, int C, const float* scale,
@@ -349,11 +474,17 @@ extern "C" hipError_t dlmpi_bn_bwd_finalize_ex(const float* partial, int nblk, i
                                                const float* invstd, float* dgamma, float* dbeta, float* coef,
                                                double* ws, hipStream_t s) {
   if (ns < 2 || ns > 3 || k2 < 1 || k2 >= ns) return hipErrorInvalidValue;
-  const int S = colsum_slices(nblk);
-  hipLaunchKernelGGL(colsum2_kernel, dim3((C + 63) / 64, S), dim3(256), 0, s, partial, nblk, C, ns, k2, ws);
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, s, ws, S, C, count, gamma, mean,
-                     invstd, dgamma, dbeta, coef, raw_z);
-  return hipGetLastError();
+  FinArgs f{};
+  f.mode = 1;
+  f.count = count;
+  f.gamma = gamma;
+  f.mean = mean;
+  f.invstd = invstd;
+  f.dgamma = dgamma;
+  f.dbeta = dbeta;
+  f.coef = coef;
+  f.raw_z = raw_z;
+  return colsum_finalize(partial, nblk, C, ns, k2, ws, f, s);
 }
 
 extern "C" hipError_t dlmpi_bn_bwd_finalize(const float* partial, int nblk, int C, double count, const float* gamma,

@@ -140,6 +140,11 @@ void conv_wgrad_kernel(const WgradArgs a) {
       const int pix = pix0 + row;
       const int bp = b_pack[i];
       bool ok = pix < pend && bp >= 0;
+      if (a.direct) {   // 1x1, stride 1, no padding: the input pixel IS the output pixel
+        const char* s = ok ? reinterpret_cast<const char*>(xb + (int64_t)pix * a.ldx + (bp & 0xffff)) : zp;
+        glds16(s, Bs + 16 * (256 * i + 64 * wid));
+        continue;
+      }
       const uint32_t pp = ok ? (uint32_t)pix : 0u;
       const uint32_t n_img = fdiv(pp, a.fdPQ);
       const uint32_t rem = pp - n_img * PQ;

@@ -95,6 +95,7 @@ struct WgradArgs {
   int TC;                          // R*S*C
   int npix, pix_per_split;
   int mtiles, ntiles, splits;
+  int direct;                      // 1: 1x1 / stride 1 / pad 0 on the same grid (no gather decode)
   FastDiv fdPQ, fdQ, fdC, fdS;
   float* ws;                       // [splits][Ko][TC] fp32 partials
 };
