@@ -59,6 +59,8 @@ def main():
     ap.add_argument("--classes", type=int, default=None)
     ap.add_argument("--bucket_mb", type=float, default=None)
     ap.add_argument("--graph", type=int, default=0, help="1: replay the whole step from a captured hipGraph")
+    ap.add_argument("--backend", default="rccl", help="rccl (default); gloo + DLMPI_GLOO_DEVICE=cuda rehearses "
+                                                      "several ranks on one GPU")
     args = ap.parse_args()
     cfg = dict(PRESETS[args.config])
     for k in ("arch", "batch", "image", "classes"):
@@ -73,7 +75,7 @@ def main():
     from deeplearning_mpi_amd.ops import BCEWithLogitsLoss, CrossEntropyLoss
     from deeplearning_mpi_amd.optim import SGD, Adam, clip_grad_norm_
 
-    comm = dl.init_distributed("rccl")
+    comm = dl.init_distributed(args.backend)
     world = comm.world_size
     dev = comm.device
     torch.manual_seed(0)

@@ -320,11 +320,17 @@ def _init(backend: str, timeout_s: float) -> Communicator:
     if info.launcher == "mpi":
         info = mpi_bring_up()
     be = _resolve_backend(backend)
-    if be == "rccl":
+    # gloo with GPU compute (gloo all-reduces CUDA tensors through host staging): rehearses the
+    # multi-rank DDP path on a box with fewer GPUs than ranks, where RCCL refuses shared devices
+    gloo_gpu = be == "gloo" and os.environ.get("DLMPI_GLOO_DEVICE", "cpu") == "cuda" and torch.cuda.is_available()
+    if be == "rccl" or gloo_gpu:
+        ndev = max(1, torch.cuda.device_count())   # does not initialise the GPU
         if info.local_rank < 0:
-            info.local_rank = info.rank % max(1, torch.cuda.device_count())
-        torch.cuda.set_device(info.local_rank)
-        device = torch.device("cuda", info.local_rank)
+            info.local_rank = info.rank % ndev
+        # one process per GPU; more local ranks than GPUs share devices round-robin (rehearsals)
+        dev_idx = info.local_rank % ndev
+        torch.cuda.set_device(dev_idx)
+        device = torch.device("cuda", dev_idx)
     else:
         device = torch.device("cpu")
     if info.world_size == 1:
@@ -348,7 +354,7 @@ def _init(backend: str, timeout_s: float) -> Communicator:
         box = [C.RcclComm.unique_id() if info.rank == 0 else None]
         dist.broadcast_object_list(box, src=0)
         uid = box[0]
-    nc = C.RcclComm(uid, info.rank, info.world_size, info.local_rank)
+    nc = C.RcclComm(uid, info.rank, info.world_size, device.index)
     return RcclCommunicator(info, device, nc)
 
 
