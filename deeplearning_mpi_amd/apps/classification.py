@@ -65,9 +65,14 @@ def build_argparser(variant: str = "main") -> argparse.ArgumentParser:
 
 
 def set_random_seeds(seed: int):
+    """Seeds + the reference's cuDNN flags (C16: resnet/main.py:26-33, unet/train.py:35-41).  The
+    flags only affect stock torch ops; the engine's own kernels are deterministic by construction
+    (fixed-order reductions, no float atomics) except the bilinear up-sampling backward."""
     torch.manual_seed(seed)
     np.random.seed(seed)
     random.seed(seed)
+    torch.backends.cudnn.deterministic = True
+    torch.backends.cudnn.benchmark = True
 
 
 @torch.no_grad()

@@ -16,6 +16,7 @@ from __future__ import annotations
 
 import argparse
 import os
+import sys
 import random
 import time
 from datetime import datetime
@@ -23,6 +24,7 @@ from datetime import datetime
 import numpy as np
 import torch
 from torch.utils.data import DataLoader
+from tqdm import tqdm
 
 from .. import parallel
 from ..data import CarvanaDataset, DistributedSampler, SyntheticMasks
@@ -66,9 +68,14 @@ def build_argparser() -> argparse.ArgumentParser:
 
 
 def set_random_seeds(seed):
+    """Seeds + the reference's cuDNN flags (C16: resnet/main.py:26-33, unet/train.py:35-41).  The
+    flags only affect stock torch ops; the engine's own kernels are deterministic by construction
+    (fixed-order reductions, no float atomics) except the bilinear up-sampling backward."""
     torch.manual_seed(seed)
     np.random.seed(seed)
     random.seed(seed)
+    torch.backends.cudnn.deterministic = True
+    torch.backends.cudnn.benchmark = True
 
 
 def create_log_file(log_dir="logs") -> str:
@@ -197,7 +204,9 @@ def run(args) -> dict:
             ddp.train()
             loss_sum = torch.zeros((), device=device)
             nb = 0
-            for batch in train_loader:
+            bar = tqdm(train_loader, desc=f"Epoch {epoch + 1}/{args.num_epochs}", unit="batch",
+                       disable=rank != 0 or not sys.stderr.isatty())   # no per-step host sync for a loss postfix
+            for batch in bar:
                 images = batch["image"].to(device, dtype=torch.float32, non_blocking=True)
                 masks = batch["mask"].to(device, dtype=torch.float32, non_blocking=True)
                 if captured is not None and images.shape == x_static.shape:
