@@ -167,7 +167,8 @@ c10::optional<at::Tensor> conv2d_dgrad(const at::Tensor& dy, int N, int P, int Q
                                        int maskoff, const c10::optional<at::Tensor>& z, int ldz, int zoff,
                                        const c10::optional<at::Tensor>& z2, int ldz2, int z2off,
                                        const c10::optional<at::Tensor>& mscale,
-                                       const c10::optional<at::Tensor>& mshift) {
+                                       const c10::optional<at::Tensor>& mshift,
+                                       const c10::optional<at::Tensor>& mbits) {
   require_gpu(dy, "dy");
   if (stride > 2) throw std::runtime_error("conv2d_dgrad: stride <= 2 supported");
   ConvArgs a{};
@@ -189,10 +190,14 @@ c10::optional<at::Tensor> conv2d_dgrad(const at::Tensor& dy, int N, int P, int Q
   a.ldz2 = ldz2; a.z2off = z2off;
   a.mscale = optr<float>(mscale);
   a.mshift = optr<float>(mshift);
+  a.mbits = optr<uint8_t>(mbits);
+  if (a.mbits && (mbits->numel() != (int64_t)N * H * W * (C / 8) || C % 8))
+    throw std::runtime_error("conv2d_dgrad: mask bits must be [N*H*W][C/8]");
   a.nstat = a.z2 ? 3 : 2;
-  if (a.z && !a.mask && !a.mscale) throw std::runtime_error("conv2d_dgrad: fused BN statistics need the ReLU mask");
+  if (a.z && !a.mask && !a.mscale && !a.mbits)
+    throw std::runtime_error("conv2d_dgrad: fused BN statistics need the ReLU mask");
   if (a.mscale && (!a.z || !a.mshift)) throw std::runtime_error("conv2d_dgrad: mask from z needs z, scale, shift");
-  if ((a.mask || a.mscale) && ((ldmask | maskoff | ldz | zoff | ldz2 | z2off) % 8 != 0 || !a.vec_store))
+  if ((a.mask || a.mscale || a.mbits) && ((ldmask | maskoff | ldz | zoff | ldz2 | z2off) % 8 != 0 || !a.vec_store))
     throw std::runtime_error("conv2d_dgrad: fused BN tensors must be 8-channel aligned");
   set_kstep(a, K);
   int bm, bn;
@@ -328,9 +333,10 @@ void bn_stats(const at::Tensor& x, int64_t M, int C, int ldx, int xoff, at::Tens
 
 void bn_apply(const at::Tensor& x, int ldx, int xoff, int64_t M, int C, const at::Tensor& scale,
               const at::Tensor& shift, const c10::optional<at::Tensor>& res, int ldres, int resoff, bool relu,
-              at::Tensor y, int ldy, int yoff) {
+              at::Tensor y, int ldy, int yoff, const c10::optional<at::Tensor>& mbits) {
+  if (mbits && mbits->numel() != M * (C / 8)) throw std::runtime_error("bn_apply: mask bits must be [M][C/8]");
   check(dlmpi_bn_apply(ptr<uint16_t>(x), ldx, xoff, M, C, ptr<float>(scale), ptr<float>(shift), optr<uint16_t>(res),
-                       ldres, resoff, relu ? 1 : 0, ptr<uint16_t>(y), ldy, yoff, cur_stream()),
+                       ldres, resoff, relu ? 1 : 0, ptr<uint16_t>(y), ldy, yoff, optr<uint8_t>(mbits), cur_stream()),
         "bn_apply");
 }
 
@@ -399,6 +405,21 @@ void maxpool_bwd(const at::Tensor& dy, const at::Tensor& idx, int N, int H, int 
   check(dlmpi_maxpool_bwd(ptr<uint16_t>(dy), ptr<uint8_t>(idx), N, H, W, C, k, stride, pad, OH, OW,
                           optr<uint16_t>(add), ldadd, addoff, ptr<uint16_t>(dx), lddx, dxoff, cur_stream()),
         "maxpool_bwd");
+}
+// max-pool backward fused with the BN-backward statistics of the producing BN+ReLU (mask from z);
+// returns the partials [nblk][2][C] for bn_bwd_finalize_fused
+at::Tensor maxpool_bwd_bn(const at::Tensor& dy, const at::Tensor& idx, int N, int H, int W, int C, int k, int stride,
+                          int pad, int OH, int OW, const at::Tensor& z, const at::Tensor& mscale,
+                          const at::Tensor& mshift, at::Tensor dx) {
+  // more blocks than the generic reductions: every row is a latency-bound window gather
+  const int64_t rpb = 256 / (C / 8);
+  const int nblk = (int)std::max<int64_t>(1, std::min<int64_t>(4096, ((int64_t)N * H * W + rpb * 8 - 1) / (rpb * 8)));
+  at::Tensor part = at::empty({nblk, 2, C}, dy.options().dtype(at::kFloat));
+  check(dlmpi_maxpool_bwd_bn(ptr<uint16_t>(dy), ptr<uint8_t>(idx), N, H, W, C, k, stride, pad, OH, OW,
+                             ptr<uint16_t>(z), ptr<float>(mscale), ptr<float>(mshift), ptr<uint16_t>(dx), ptr<float>(part),
+                             nblk, cur_stream()),
+        "maxpool_bwd_bn");
+  return part;
 }
 void avgpool_fwd(const at::Tensor& x, int N, int HW, int C, at::Tensor y) {
   check(dlmpi_avgpool_fwd(ptr<uint16_t>(x), N, HW, C, ptr<uint16_t>(y), cur_stream()), "avgpool_fwd");
@@ -508,6 +529,7 @@ void register_ops(pybind11::module& m) {
   m.def("channel_sum", &channel_sum);
   m.def("maxpool_fwd", &maxpool_fwd);
   m.def("maxpool_bwd", &maxpool_bwd);
+  m.def("maxpool_bwd_bn", &maxpool_bwd_bn);
   m.def("avgpool_fwd", &avgpool_fwd);
   m.def("avgpool_bwd", &avgpool_bwd);
   m.def("nchw_to_nhwc", &nchw_to_nhwc);

@@ -52,6 +52,66 @@ __device__ void block_combine(float (*acc)[8], const RowMap& rm, int C, float* p
   }
 }
 
+// Max-pool backward (gather, no atomics) fused with the BN-backward statistics of the BN+ReLU
+// that produced the pool input (the ResNet stem): dx = [z*scale + shift > 0] * sum of the window
+// gradients that selected the element, written as the masked gradient dyr, and per-block partials
+// {sum dyr, sum dyr*z} for the fused finalize (raw_z).  Replaces maxpool_bwd + bn_bwd_reduce and
+// the mask read of bn_bwd_apply.
+__global__ __launch_bounds__(256) void maxpool_bwd_bn_kernel(const uint16_t* __restrict__ dy,
+                                                             const uint8_t* __restrict__ idx, int N, int H, int W,
+                                                             int C, int k, int stride, int pad, int OH, int OW,
+                                                             FastDiv fdW, FastDiv fdH, const uint16_t* __restrict__ z,
+                                                             const float* __restrict__ msc,
+                                                             const float* __restrict__ msh, uint16_t* __restrict__ dx,
+                                                             float* __restrict__ partial) {
+  const RowMap rm = rowmap(C);
+  float acc[2][8] = {};
+  const int64_t M = (int64_t)N * H * W;
+  if (rm.active) {
+    const int c0 = rm.cc * 8;
+    float sc[8], sh[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) { sc[e] = msc[c0 + e]; sh[e] = msh[c0 + e]; }
+    for (int64_t row = (int64_t)blockIdx.x * rm.RPB + rm.rr; row < M; row += (int64_t)gridDim.x * rm.RPB) {
+      const uint32_t pix = (uint32_t)row;
+      const uint32_t t2 = fdiv(pix, fdW);
+      const int iw = (int)(pix - t2 * W);
+      const uint32_t n = fdiv(t2, fdH);
+      const int ih = (int)(t2 - n * H);
+      float g[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+      int oh_lo = ih + pad - k + 1;
+      oh_lo = oh_lo <= 0 ? 0 : (oh_lo + stride - 1) / stride;
+      const int oh_hi = min((ih + pad) / stride, OH - 1);
+      int ow_lo = iw + pad - k + 1;
+      ow_lo = ow_lo <= 0 ? 0 : (ow_lo + stride - 1) / stride;
+      const int ow_hi = min((iw + pad) / stride, OW - 1);
+      for (int oh = oh_lo; oh <= oh_hi; ++oh) {
+        for (int ow = ow_lo; ow <= ow_hi; ++ow) {
+          const uint8_t want = (uint8_t)((ih - (oh * stride - pad)) * k + (iw - (ow * stride - pad)));
+          const int64_t op = ((int64_t)n * OH + oh) * OW + ow;
+          const uint64_t id = *reinterpret_cast<const uint64_t*>(idx + op * C + c0);
+          float d[8];
+          unpack8(*reinterpret_cast<const u32x4*>(dy + op * C + c0), d);
+#pragma unroll
+          for (int e = 0; e < 8; ++e)
+            if (((id >> (8 * e)) & 0xff) == want) g[e] += d[e];
+        }
+      }
+      float zz[8];
+      unpack8(*reinterpret_cast<const u32x4*>(z + row * C + c0), zz);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) g[e] = zz[e] * sc[e] + sh[e] > 0.f ? g[e] : 0.f;
+      const u32x4 pk = pack8(g);
+      *reinterpret_cast<u32x4*>(dx + row * C + c0) = pk;
+      float r[8];
+      unpack8(pk, r);   // statistics of the stored (bf16) gradient
+#pragma unroll
+      for (int e = 0; e < 8; ++e) { acc[0][e] += r[e]; acc[1][e] += r[e] * zz[e]; }
+    }
+  }
+  block_combine<2>(acc, rm, C, partial);
+}
+
 __global__ __launch_bounds__(256) void bn_stats_kernel(const uint16_t* __restrict__ x, int64_t M, int C, int ldx,
                                                        int xoff, float* __restrict__ partial) {
   const RowMap rm = rowmap(C);
@@ -250,7 +310,8 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const uint16_t* __restric
                                                        int C, FastDiv fdCC, const float* __restrict__ scale,
                                                        const float* __restrict__ shift,
                                                        const uint16_t* __restrict__ res, int ldres, int resoff,
-                                                       int relu, uint16_t* __restrict__ y, int ldy, int yoff) {
+                                                       int relu, uint16_t* __restrict__ y, int ldy, int yoff,
+                                                       uint8_t* __restrict__ mbits) {
   const int CC = C >> 3;
   const int64_t total = M * CC;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
@@ -283,7 +344,17 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const uint16_t* __restric
 #pragma unroll
       for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.f);
     }
-    *reinterpret_cast<u32x4*>(y + row * ldy + yoff + c0) = pack8(v);
+    const u32x4 pk = pack8(v);
+    *reinterpret_cast<u32x4*>(y + row * ldy + yoff + c0) = pk;
+    if (mbits) {   // ReLU mask bits of the stored bf16 values (bit e: y[c0 + e] > 0), 1/16 of y's bytes
+      uint32_t b = 0;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        b |= (uint32_t)((pk[k] & 0xffffu) != 0u && !(pk[k] & 0x8000u)) << (2 * k);
+        b |= (uint32_t)((pk[k] >> 16) != 0u && !(pk[k] & 0x80000000u)) << (2 * k + 1);
+      }
+      mbits[row * CC + cc] = (uint8_t)b;
+    }
   }
 }
 
@@ -451,11 +522,11 @@ extern "C" hipError_t dlmpi_bn_finalize(const float* partial, int ntiles, int C,
 
 extern "C" hipError_t dlmpi_bn_apply(const uint16_t* x, int ldx, int xoff, int64_t M, int C, const float* scale,
                                      const float* shift, const uint16_t* res, int ldres, int resoff, int relu,
-                                     uint16_t* y, int ldy, int yoff, hipStream_t s) {
+                                     uint16_t* y, int ldy, int yoff, uint8_t* mbits, hipStream_t s) {
   if (C % 8) return hipErrorInvalidValue;
   const int64_t total = M * (C / 8);
   hipLaunchKernelGGL(bn_apply_kernel, dim3(ew_blocks(total)), dim3(256), 0, s, x, ldx, xoff, M, C,
-                     make_fastdiv(C / 8), scale, shift, res, ldres, resoff, relu, y, ldy, yoff);
+                     make_fastdiv(C / 8), scale, shift, res, ldres, resoff, relu, y, ldy, yoff, mbits);
   return hipGetLastError();
 }
 
@@ -510,4 +581,14 @@ extern "C" hipError_t dlmpi_channel_sum(const uint16_t* x, int64_t M, int C, int
   if (e != hipSuccess) return e;
   return dlmpi_bn_bwd_finalize(partial, nblk, C, (double)M, nullptr, nullptr, nullptr, nullptr, out_acc, nullptr, ws,
                                s);
+}
+
+extern "C" hipError_t dlmpi_maxpool_bwd_bn(const uint16_t* dy, const uint8_t* idx, int N, int H, int W, int C, int k,
+                                           int stride, int pad, int OH, int OW, const uint16_t* z, const float* mscale,
+                                           const float* mshift, uint16_t* dx, float* partial, int nblk,
+                                           hipStream_t s) {
+  if (C % 8 || C > 2048 || (int64_t)N * H * W >= (1ll << 31)) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(maxpool_bwd_bn_kernel, dim3(nblk), dim3(256), 0, s, dy, idx, N, H, W, C, k, stride, pad, OH, OW,
+                     make_fastdiv(W), make_fastdiv(H), z, mscale, mshift, dx, partial);
+  return hipGetLastError();
 }

@@ -242,7 +242,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(STAGES == 1
 #pragma unroll
   for (int e = 0; e < 8; ++e) { s1[e] = 0.f; s2[e] = 0.f; s3[e] = 0.f; }
   // gradient of a BN+ReLU output: mask, then {sum dy, sum dy*z}
-  const bool bwd = a.mask != nullptr || a.mscale != nullptr;
+  const bool bwd = a.mask != nullptr || a.mscale != nullptr || a.mbits != nullptr;
 
   // NP passes over row slices: in pass h every wave dumps its fragments mi in
   // [h*TM/NP, (h+1)*TM/NP), i.e. tile rows wm*WM + h*HM + [0, HM), into a BM/NP-row buffer.
@@ -258,6 +258,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(STAGES == 1
       for (int r = 0; r < 4; ++r)
         Cs[(wm * HM + mi * 16 + fg * 4 + r) * CS_LD + wn * WN + ni * 16 + fr] = acc[h * HT + mi][ni][r];
   __syncthreads();
+  constexpr int EPI_UNROLL = BM >= 256 ? 1 : 2;   // two rows' loads in flight (memory-bound epilogues)
+#pragma unroll EPI_UNROLL
   for (int rr = rg; rr < BM / NP; rr += RG) {
     const int r = (rr / HM) * WM + h * HM + (rr % HM);
     const int m = m0 + r;
@@ -297,7 +299,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(STAGES == 1
     if (bwd) {
       float zz[8];
       if (a.z) unpack8(*reinterpret_cast<const u32x4*>(a.z + pix * a.ldz + a.zoff + c0), zz);
-      if (a.mask) {
+      if (a.mbits) {
+        const uint32_t b = a.mbits[pix * (a.Kout >> 3) + (c0 >> 3)];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = (b >> e) & 1u ? v[e] : 0.f;
+      } else if (a.mask) {
         float yy[8];
         unpack8(*reinterpret_cast<const u32x4*>(a.mask + pix * a.ldmask + a.maskoff + c0), yy);
 #pragma unroll

@@ -71,6 +71,7 @@ struct ConvArgs {
   int ldmask, maskoff;
   const float* mscale;             //   mask = z * mscale + mshift > 0 (BN+ReLU without residual:
   const float* mshift;             //   recomputed from z, which the stats read anyway)
+  const uint8_t* mbits;            //   or mask bits written by the forward BN-apply ([pix][Kout/8])
   const uint16_t* z;
   int ldz, zoff;
   const uint16_t* z2;
@@ -119,9 +120,10 @@ hipError_t dlmpi_bn_finalize(const float* partial, int ntiles, int C, double cou
 int dlmpi_colsum_ws_doubles(int T, int C);
 hipError_t dlmpi_bn_stats(const uint16_t* x, int64_t M, int C, int ldx, int xoff, float* partial, int nblk,
                           hipStream_t s);
+// mbits (optional): [M][C/8] bytes, bit e of byte (row, g) = y[row][8g + e] > 0 (ReLU mask for backward)
 hipError_t dlmpi_bn_apply(const uint16_t* x, int ldx, int xoff, int64_t M, int C, const float* scale,
                           const float* shift, const uint16_t* res, int ldres, int resoff, int relu, uint16_t* y,
-                          int ldy, int yoff, hipStream_t s);
+                          int ldy, int yoff, uint8_t* mbits, hipStream_t s);
 hipError_t dlmpi_bn_bwd_reduce(const uint16_t* dy, int lddy, int dyoff, const uint16_t* ymask, int ldym, int ymoff,
                                const uint16_t* x, int ldx, int xoff, int64_t M, int C, const float* mean,
                                const float* invstd, float* partial, int nblk, hipStream_t s);
@@ -145,6 +147,11 @@ hipError_t dlmpi_maxpool_fwd(const uint16_t* x, int N, int H, int W, int C, int 
 hipError_t dlmpi_maxpool_bwd(const uint16_t* dy, const uint8_t* idx, int N, int H, int W, int C, int k, int stride,
                              int pad, int OH, int OW, const uint16_t* add, int ldadd, int addoff, uint16_t* dx,
                              int lddx, int dxoff, hipStream_t s);
+// max-pool backward into the gradient of a BN+ReLU output (mask z*scale+shift > 0), with the BN
+// backward partials [nblk][2][C] = {sum dyr, sum dyr*z}; dx/z dense [N*H*W][C]
+hipError_t dlmpi_maxpool_bwd_bn(const uint16_t* dy, const uint8_t* idx, int N, int H, int W, int C, int k, int stride,
+                                int pad, int OH, int OW, const uint16_t* z, const float* mscale, const float* mshift,
+                                uint16_t* dx, float* partial, int nblk, hipStream_t s);
 hipError_t dlmpi_avgpool_fwd(const uint16_t* x, int N, int HW, int C, uint16_t* y, hipStream_t s);
 hipError_t dlmpi_avgpool_bwd(const uint16_t* dy, int N, int HW, int C, uint16_t* dx, hipStream_t s);
 hipError_t dlmpi_nchw_to_nhwc(const float* x, int N, int C, int H, int W, int Cpad, uint16_t* y, hipStream_t s);

@@ -57,16 +57,29 @@ __global__ void maxpool_fwd_kernel(const uint16_t* __restrict__ x, int N, int H,
 __global__ void maxpool_bwd_kernel(const uint16_t* __restrict__ dy, const uint8_t* __restrict__ idx, int N, int H,
                                    int W, int C, int k, int stride, int pad, int OH, int OW,
                                    const uint16_t* __restrict__ add, int ldadd, int addoff, uint16_t* __restrict__ dx,
-                                   int lddx, int dxoff) {
+                                   int lddx, int dxoff, FastDiv fdCC, FastDiv fdW, FastDiv fdH) {
   const int CC = C >> 3;
   const int64_t total = (int64_t)N * H * W * CC;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
-    const int cc = (int)(i % CC);
-    const int64_t pix = i / CC;
-    const int iw = (int)(pix % W);
-    const int64_t t2 = pix / W;
-    const int ih = (int)(t2 % H);
-    const int n = (int)(t2 / H);
+    int cc, iw, ih, n;
+    int64_t pix;
+    if (total < (1ll << 31)) {   // 32-bit fast division (the 64-bit divisions dominated this kernel)
+      const uint32_t q = fdiv((uint32_t)i, fdCC);
+      cc = (int)((uint32_t)i - q * CC);
+      pix = q;
+      const uint32_t t2 = fdiv(q, fdW);
+      iw = (int)(q - t2 * W);
+      const uint32_t nn = fdiv(t2, fdH);
+      ih = (int)(t2 - nn * H);
+      n = (int)nn;
+    } else {
+      cc = (int)(i % CC);
+      pix = i / CC;
+      iw = (int)(pix % W);
+      const int64_t t2 = pix / W;
+      ih = (int)(t2 % H);
+      n = (int)(t2 / H);
+    }
     float g[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     if (add) unpack8(*reinterpret_cast<const u32x4*>(add + pix * ldadd + addoff + cc * 8), g);
     // windows oh with oh*stride - pad <= ih <= oh*stride - pad + k - 1
@@ -241,7 +254,8 @@ extern "C" hipError_t dlmpi_maxpool_bwd(const uint16_t* dy, const uint8_t* idx, 
   if (C % 8) return hipErrorInvalidValue;
   const int64_t total = (int64_t)N * H * W * (C / 8);
   hipLaunchKernelGGL(maxpool_bwd_kernel, dim3(ew_blocks(total)), dim3(256), 0, s, dy, idx, N, H, W, C, k, stride, pad,
-                     OH, OW, add, ldadd, addoff, dx, lddx, dxoff);
+                     OH, OW, add, ldadd, addoff, dx, lddx, dxoff, make_fastdiv(C / 8), make_fastdiv(W),
+                     make_fastdiv(H));
   return hipGetLastError();
 }
 

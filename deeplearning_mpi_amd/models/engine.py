@@ -40,6 +40,7 @@ class BwdFuse(NamedTuple):
     z2: Optional[Act] = None
     scale: Optional[torch.Tensor] = None
     shift: Optional[torch.Tensor] = None
+    mbits: Optional[torch.Tensor] = None   # [pixels][C/8] ReLU mask bits from the forward BN-apply
 
 
 class ConvUnit:
@@ -112,8 +113,13 @@ class ConvUnit:
                            bn.running_mean if bn.track_running_stats else None,
                            bn.running_var if bn.track_running_stats else None, mom, bn.eps, scale, shift, mean,
                            invstd)
-            be.bn_apply(z, scale, shift, res, self.relu, y)
-            return y, ((x, z, y, mean, invstd, scale, shift, res is not None) if save else None)
+            # residual units: the backward mask (y > 0) cannot be recomputed from z alone, so keep it
+            # as bits (1/16 of y's bytes) for the fused data-gradient epilogue
+            mbits = None
+            if save and res is not None and self.relu and self.Kp % 8 == 0:
+                mbits = torch.empty(y.rows, self.Kp // 8, dtype=torch.uint8, device=dev)
+            be.bn_apply(z, scale, shift, res, self.relu, y, mbits=mbits)
+            return y, ((x, z, y, mean, invstd, scale, shift, res is not None, mbits) if save else None)
         # eval: fold BN (and conv bias) into the GEMM epilogue
         invstd = torch.rsqrt(bn.running_var + bn.eps)
         scale = bn.weight.data * invstd if bn.affine else invstd
@@ -128,9 +134,9 @@ class ConvUnit:
     def fuse_spec(ctx, z2=None) -> BwdFuse:
         """What a producer of this (trained BN+ReLU) unit's output gradient needs to fuse the
         unit's BN-backward reduction into its data-gradient epilogue."""
-        x, z, y, mean, invstd, scale, shift, has_res = ctx
+        x, z, y, mean, invstd, scale, shift, has_res, mbits = ctx
         if has_res or z2 is not None:
-            return BwdFuse(y, z, z2)
+            return BwdFuse(None if mbits is not None else y, z, z2, mbits=mbits)
         return BwdFuse(None, z, None, scale, shift)
 
     def bwd(self, be, ctx, dy: Act, need_dx=True, dx_res: Act = None, dyr_out: Act = None, ymask: Act = None,

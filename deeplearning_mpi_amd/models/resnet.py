@@ -107,8 +107,7 @@ class _BlockExec:
         """(block output y, BN input of the last conv, BN input of the downsample conv | None): the
         previous schedule step fuses this block's BN-backward reductions into its dgrad epilogue."""
         ctxs, cd = st
-        x, z, y = ctxs[-1][:3]
-        return BwdFuse(y, z, cd[1] if cd is not None else None)
+        return ConvUnit.fuse_spec(ctxs[-1], z2=cd[1] if cd is not None else None)
 
     def bwd(self, be, st, dy: Act, pre=None, fuse_prev=None):
         """dy: gradient of the block output.  With ``pre`` (partials from the producer's dgrad
@@ -231,8 +230,12 @@ class ResNet(EngineModule):
             out = self.blocks[i].bwd(be, st_blocks[i], da, pre=pre, fuse_prev=fuse_prev)
             da, pre = out if fuse_prev is not None else (out, None)
         dh = Act.empty(h.N, h.H, h.W, h.C, be.act_dtype, h.device)
-        be.maxpool_bwd(da, idx, h, 3, 2, 1, dh)
-        self.u_stem.bwd(be, cs, dh, need_dx=False)
+        if self.fuse_bn_bwd:   # stem BN-backward statistics in the max-pool backward (mask from z)
+            part = be.maxpool_bwd(da, idx, h, 3, 2, 1, dh, fuse=ConvUnit.fuse_spec(cs))
+            self.u_stem.bwd(be, cs, dh, need_dx=False, pre=part)
+        else:
+            be.maxpool_bwd(da, idx, h, 3, 2, 1, dh)
+            self.u_stem.bwd(be, cs, dh, need_dx=False)
 
 
 def resnet18(num_classes=1000, **kw):

@@ -44,13 +44,13 @@ class NativeBackend:
         """fuse = BwdFuse(mask, z, z2, scale, shift): dx is the gradient of relu(BN(z) [+ BN2(z2)]);
         the epilogue applies the ReLU mask (y > 0, or z*scale + shift > 0 without a residual) and
         returns BN-backward partials [tiles][2|3][C]."""
-        m, z, z2, sc, sh = fuse if fuse is not None else (None, None, None, None, None)
+        m, z, z2, sc, sh, mb = fuse if fuse is not None else (None, None, None, None, None, None)
 
         def t(a):
             return (a.buf, a.ld, a.off) if a is not None else (None, 0, 0)
 
         return self.C.conv2d_dgrad(dy.buf, dy.N, dy.H, dy.W, dy.C, dy.ld, dy.off, wT, C, R, S, stride, pad, dx.H,
-                                   dx.W, dx.buf, dx.ld, dx.off, *t(res), *t(m), *t(z), *t(z2), sc, sh)
+                                   dx.W, dx.buf, dx.ld, dx.off, *t(res), *t(m), *t(z), *t(z2), sc, sh, mb)
 
     def convT_fwd(self, x: Act, wf, Cout, y: Act, bias=None):
         self.C.convT2x2_fwd(x.buf, x.N, x.H, x.W, x.C, x.ld, x.off, wf, Cout, y.buf, y.ld, y.off, bias)
@@ -71,10 +71,10 @@ class NativeBackend:
         self.C.bn_stats(x.buf, x.rows, x.C, x.ld, x.off, part, nblk)
         return part, nblk
 
-    def bn_apply(self, x: Act, scale, shift, res: Act, relu, y: Act):
+    def bn_apply(self, x: Act, scale, shift, res: Act, relu, y: Act, mbits=None):
         self.C.bn_apply(x.buf, x.ld, x.off, x.rows, x.C, scale, shift, res.buf if res is not None else None,
                         res.ld if res is not None else 0, res.off if res is not None else 0, bool(relu), y.buf, y.ld,
-                        y.off)
+                        y.off, mbits)
 
     def bn_bwd(self, dy: Act, ymask: Act, x: Act, mean, invstd, gamma, dgamma, dbeta, dx: Act, dyr_out: Act = None,
                pre=None, k2=1):
@@ -107,7 +107,14 @@ class NativeBackend:
         self.C.maxpool_fwd(x.buf, x.N, x.H, x.W, x.C, x.ld, x.off, k, s, p, y.buf, idx, y.H, y.W)
         return idx
 
-    def maxpool_bwd(self, dy: Act, idx, x: Act, k, s, p, dx: Act, add: Act = None):
+    def maxpool_bwd(self, dy: Act, idx, x: Act, k, s, p, dx: Act, add: Act = None, fuse=None):
+        """fuse = BwdFuse(None, z, scale=, shift=): dx is the gradient of relu(BN(z)); it is written
+        masked and the BN-backward partials are returned (for bn_bwd(pre=...))."""
+        if fuse is not None:
+            assert add is None and fuse.scale is not None and dx.ld == dx.C and fuse.z.ld == fuse.z.C
+            assert dy.ld == dy.C and dy.off == 0 and dx.off == 0 and fuse.z.off == 0
+            return self.C.maxpool_bwd_bn(dy.buf, idx, x.N, x.H, x.W, x.C, k, s, p, dy.H, dy.W, fuse.z.buf,
+                                         fuse.scale, fuse.shift, dx.buf)
         self.C.maxpool_bwd(dy.buf, idx, x.N, x.H, x.W, x.C, k, s, p, dy.H, dy.W, add.buf if add is not None else None,
                            add.ld if add is not None else 0, add.off if add is not None else 0, dx.buf, dx.ld, dx.off)
 
@@ -241,8 +248,10 @@ class RefBackend:
         if fuse is None:
             self._store(dx, g)
             return None
-        m, z, z2, sc, sh = fuse
-        if m is not None:
+        m, z, z2, sc, sh, mb = fuse
+        if mb is not None:
+            g = g * self._unpack_bits(mb, z).permute(0, 3, 1, 2)
+        elif m is not None:
             g = g * (m.nchw() > 0)
         else:   # mask recomputed from the BN input, as the forward BN-apply computed y
             keep = (z.nhwc().to(self.dt) * sc + sh) > 0
@@ -291,13 +300,23 @@ class RefBackend:
         part = torch.stack([v.sum((0, 1, 2)), (v * v).sum((0, 1, 2))]).unsqueeze(0)
         return part, 1
 
-    def bn_apply(self, x: Act, scale, shift, res, relu, y: Act):
+    def bn_apply(self, x: Act, scale, shift, res, relu, y: Act, mbits=None):
         v = x.nhwc().to(self.dt) * scale + shift
         if res is not None:
             v = v + res.nhwc().to(self.dt)
         if relu:
             v = F.relu(v)
         y.nhwc().copy_(v)
+        if mbits is not None:   # bit e of byte (row, g): y[row][8g + e] > 0
+            pos = (y.nhwc().reshape(-1, y.C // 8, 8) > 0).to(torch.uint8)
+            w = (2 ** torch.arange(8, device=pos.device, dtype=torch.uint8))
+            mbits.copy_((pos * w).sum(-1).to(torch.uint8).view(mbits.shape))
+
+    @staticmethod
+    def _unpack_bits(mbits, like: Act):
+        b = mbits.view(-1, like.C // 8, 1).to(torch.int32)
+        bits = (b >> torch.arange(8, device=b.device, dtype=torch.int32)) & 1
+        return bits.view(like.N, like.H, like.W, like.C).bool()
 
     def bn_bwd(self, dy: Act, ymask, x: Act, mean, invstd, gamma, dgamma, dbeta, dx: Act, dyr_out=None, pre=None,
                k2=1):
@@ -331,12 +350,19 @@ class RefBackend:
         self._store(y, out)
         return idx
 
-    def maxpool_bwd(self, dy: Act, idx, x: Act, k, s, p, dx: Act, add=None):
+    def maxpool_bwd(self, dy: Act, idx, x: Act, k, s, p, dx: Act, add=None, fuse=None):
         g = torch.ops.aten.max_pool2d_with_indices_backward(dy.nchw().to(self.dt).contiguous(), x.nchw().to(self.dt), [k, k],
                                                             [s, s], [p, p], [1, 1], False, idx)
         if add is not None:
             g = g + add.nchw().to(self.dt)
-        self._store(dx, g)
+        if fuse is None:
+            self._store(dx, g)
+            return None
+        zz = fuse.z.nhwc().to(self.dt)
+        keep = (zz * fuse.scale + fuse.shift) > 0
+        self._store(dx, g * keep.permute(0, 3, 1, 2))
+        v = dx.nhwc().to(self.dt)
+        return torch.stack([v.sum((0, 1, 2)), (v * zz).sum((0, 1, 2))]).unsqueeze(0)
 
     def avgpool_fwd(self, x: Act, y: Act):
         y.nhwc().copy_(x.nhwc().to(self.dt).mean((1, 2), keepdim=True))

@@ -117,7 +117,7 @@ def test_conv_fwd_256_row_tile(shape):
 
 
 @pytest.mark.parametrize("shape", [CONV_SHAPES[1], CONV_SHAPES[2], CONV_SHAPES[3], CONV_SHAPES[5]])
-@pytest.mark.parametrize("mode", ["mask", "two", "from_z"])
+@pytest.mark.parametrize("mode", ["mask", "two", "from_z", "bits"])
 def test_conv_dgrad_fused_bn_backward(shape, mode):
     """dgrad epilogue: + residual, ReLU mask of the consumer, BN-backward partials
     {sum dx, sum dx*z [, sum dx*z2]} (multi-phase tile numbering for stride 2), then the
@@ -134,12 +134,17 @@ def test_conv_dgrad_fused_bn_backward(shape, mode):
     two = mode == "two"
     z2, z2r = _act(N, H, W, Cp) if two else (None, None)
     sc = sh = None
+    mb = None
     if mode == "from_z":   # mask recomputed from the BN input: z*scale + shift > 0
         sc, sh = torch.rand(Cp, device=DEV) + 0.5, torch.randn(Cp, device=DEV) * 0.5
         m = mr = None
+    if mode == "bits":     # mask bits of y as written by the forward BN-apply
+        pos = (m.buf.float() > 0).view(-1, Cp // 8, 8).to(torch.uint8)
+        mb = (pos * (2 ** torch.arange(8, device=DEV, dtype=torch.uint8))).sum(-1).to(torch.uint8).contiguous()
     dx = _empty(N, H, W, Cp)
     dxr = _empty(N, H, W, Cp, torch.float32)
-    part = nb.conv_dgrad(dy, wT, Cp, R, R, s, p, dx, res=res, fuse=BwdFuse(m, z, z2, sc, sh))
+    part = nb.conv_dgrad(dy, wT, Cp, R, R, s, p, dx, res=res,
+                         fuse=BwdFuse(None if mb is not None else m, z, z2, sc, sh, mb))
     rb.conv_dgrad(dyr, wT.float(), Cp, R, R, s, p, dxr, res=resr, fuse=BwdFuse(mr, zr, z2r, sc, sh))
     torch.cuda.synchronize()
     assert part.shape[1] == (3 if two else 2) and part.shape[2] == Cp
@@ -246,9 +251,12 @@ def test_bn_family():
     v = outs[0][0]
     y = _empty(N, H, W, C)
     yr = _empty(N, H, W, C, torch.float32)
-    nb.bn_apply(x, v[0], v[1], res, True, y)
+    bits = torch.empty(N * H * W, C // 8, dtype=torch.uint8, device=DEV)
+    nb.bn_apply(x, v[0], v[1], res, True, y, mbits=bits)
     rb.bn_apply(xr, v[0], v[1], resr, True, yr)
     assert _rel(y.buf, yr.buf) < 1e-2
+    unpacked = RefBackend._unpack_bits(bits, y).reshape(-1, C)
+    assert torch.equal(unpacked, y.buf.float() > 0)   # bit e == (stored y > 0)
     dy, dyr = _act(N, H, W, C)
     dg, db = torch.zeros(C, device=DEV), torch.zeros(C, device=DEV)
     dgr, dbr = torch.zeros(C, device=DEV), torch.zeros(C, device=DEV)
@@ -300,6 +308,33 @@ def test_pools_and_layout():
     nb.upsample_bwd(y, dx)
     rb.upsample_bwd(Act(y.buf.float(), 2, 16, 12, 64), dxr)
     assert _rel(dx.buf, dxr.buf) < 1e-2
+
+
+def test_maxpool_bwd_fused_bn_stats():
+    """ResNet stem: max-pool backward + ReLU mask (from z) + BN-backward partials in one kernel."""
+    nb, rb = _be()
+    N, H, W, C = 2, 16, 16, 64
+    z, zr = _act(N, H, W, C)
+    sc, sh = torch.rand(C, device=DEV) + 0.5, torch.randn(C, device=DEV) * 0.3
+    y = _empty(N, H, W, C)
+    nb.bn_apply(z, sc, sh, None, True, y)
+    OH = OW = 8
+    p = _empty(N, OH, OW, C)
+    idx = nb.maxpool_fwd(y, 3, 2, 1, p)
+    dy, dyr = _act(N, OH, OW, C)
+    dx, dxr = _empty(N, H, W, C), _empty(N, H, W, C, torch.float32)
+    part = nb.maxpool_bwd(dy, idx, y, 3, 2, 1, dx, fuse=BwdFuse(None, z, None, sc, sh))
+    # reference: plain gather backward, then the mask and the sums
+    plain = _empty(N, H, W, C)
+    nb.maxpool_bwd(dy, idx, y, 3, 2, 1, plain)
+    keep = z.buf.float() * sc + sh > 0
+    want = torch.where(keep, plain.buf.float(), torch.zeros_like(plain.buf, dtype=torch.float32))
+    torch.cuda.synchronize()
+    assert torch.equal(dx.buf.float(), want)
+    ps = part.double().sum(0)
+    v = dx.buf.double()
+    assert torch.allclose(ps[0], v.sum(0), rtol=1e-4, atol=1e-3)
+    assert torch.allclose(ps[1], (v * z.buf.double()).sum(0), rtol=1e-4, atol=1e-3)
 
 
 def test_losses_eval_optim():
