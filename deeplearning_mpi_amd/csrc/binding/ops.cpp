@@ -282,7 +282,8 @@ void conv2d_wgrad(const at::Tensor& dy, int lddy, int dyoff, int Ko, const at::T
   a.direct = (R == 1 && S == 1 && stride == 1 && pad == 0 && P == H && Q == W) ? 1 : 0;
   const int bm = Ko <= 64 ? 64 : 128;
   a.mtiles = ceil_div(Ko, bm);
-  a.ntiles = ceil_div(a.TC, 128);
+  const int bn = 128;
+  a.ntiles = ceil_div(a.TC, bn);
   const int tiles = a.mtiles * a.ntiles;
   // split the pixel reduction so the grid covers the chip ~4 blocks deep, but keep each split at
   // least 8 K-steps (512 pixels) so the fp32 slab traffic stays small next to the MFMA work
@@ -301,7 +302,7 @@ void conv2d_wgrad(const at::Tensor& dy, int lddy, int dyoff, int Ko, const at::T
   const int G = splits > 1 ? dlmpi_wgrad_reduce_groups(splits, wsz) : 0;
   at::Tensor ws = at::empty({(int64_t)(splits + G) * wsz}, dy.options().dtype(at::kFloat));
   a.ws = ptr<float>(ws);
-  check(dlmpi_conv_wgrad(&a, bm, cur_stream()), "conv2d_wgrad");
+  check(dlmpi_conv_wgrad(&a, bm, bn, cur_stream()), "conv2d_wgrad");
   check(dlmpi_wgrad_reduce(a.ws, splits, Ko, R * S, C, Creal, Ko_real, ptr<float>(grad), a.ws + (int64_t)splits * wsz,
                            (int)std::min<int64_t>(INT32_MAX, (int64_t)G * wsz), cur_stream()),
         "wgrad_reduce");

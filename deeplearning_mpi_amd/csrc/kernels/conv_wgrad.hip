@@ -22,13 +22,19 @@ typedef __attribute__((address_space(3))) i16x4 lds_i16x4;
 // Byte offset of 16-B chunk `ch` of LDS row `row` in a tile with 256-B rows (16 chunks) or 128-B
 // rows (8 chunks).  Both XORs make the 8 rows x 32 bytes touched by one half-wave of transposed
 // reads land on 16 distinct 16-byte bank slots.
+// 512-B rows (32 chunks): one transposed read touches rows k0 + 8g + q (+4), g, q in 0..3, chunks
+// 2cb + {0,1}; XOR-ing the chunk pair index with (q | g << 2) spreads the 16 rows over all 32
+// chunk slots = both 256-B bank rows exactly once each.
+template <int ROW_BYTES>
+__device__ __forceinline__ int tr_swz(int row) {
+  if constexpr (ROW_BYTES == 512) return (((row & 3) | (((row >> 3) & 3) << 2)) << 1);
+  else if constexpr (ROW_BYTES == 256) return ((row & 3) << 2) | ((row >> 2) & 3);
+  else return (((row >> 1) & 1) << 1) | (((row >> 3) & 1) << 2);
+}
+
 template <int ROW_BYTES>
 __device__ __forceinline__ int tr_off(int row, int ch) {
-  if constexpr (ROW_BYTES == 256) {
-    return row * 256 + ((ch ^ (((row & 3) << 2) | ((row >> 2) & 3))) << 4);
-  } else {
-    return row * 128 + ((ch ^ ((((row >> 1) & 1) << 1) | (((row >> 3) & 1) << 2))) << 4);
-  }
+  return row * ROW_BYTES + ((ch ^ tr_swz<ROW_BYTES>(row)) << 4);
 }
 
 // 16x32 MFMA operand (16 columns starting at column 16*cb, 32 reduction rows starting at k0)
@@ -57,8 +63,7 @@ __device__ __forceinline__ void glds16(const void* g, char* lds_wave_base) {
 // Inverse of tr_off within a row: the chunk that lives at 16-B slot `pos` of row `row`.
 template <int ROW_BYTES>
 __device__ __forceinline__ int tr_chunk(int row, int pos) {
-  if constexpr (ROW_BYTES == 256) return pos ^ (((row & 3) << 2) | ((row >> 2) & 3));
-  else return pos ^ ((((row >> 1) & 1) << 1) | (((row >> 3) & 1) << 2));
+  return pos ^ tr_swz<ROW_BYTES>(row);
 }
 
 // Operands are staged global -> LDS with global_load_lds (no VGPR round trip): piece i of thread
@@ -66,10 +71,10 @@ __device__ __forceinline__ int tr_chunk(int row, int pos) {
 // lane fetches whichever (pixel row, 16-B chunk) the swizzled layout puts there.  STAGES = 1:
 // single stage, two barriers per K-step, 32 KB LDS at BM = 128 -> several blocks per CU hide
 // the load latency of one another.
-template <int BM, int STAGES>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(STAGES == 1 ? 3 : 2, 8)))
+template <int BM, int BN, int STAGES>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(STAGES == 1 && BN == 128 ? 3 : 2, 8)))
 void conv_wgrad_kernel(const WgradArgs a) {
-  constexpr int BN = 128, BK = 64;
+  constexpr int BK = 64;
   constexpr int WM = BM / 2, WN = BN / 2, TM = WM / 16, TN = WN / 16;
   constexpr int A_ROW = BM * 2, B_ROW = BN * 2;          // bytes per LDS row
   constexpr int AL = BK * A_ROW / 4096, BL = BK * B_ROW / 4096;   // 16-B pieces per thread
@@ -99,7 +104,7 @@ void conv_wgrad_kernel(const WgradArgs a) {
     const int o = 256 * i + tid;
     row = (o * 16) / ROW;
     const int pos = (o * 16 % ROW) / 16;
-    ch = ROW == 256 ? tr_chunk<256>(row, pos) : tr_chunk<128>(row, pos);
+    ch = ROW == 512 ? tr_chunk<512>(row, pos) : ROW == 256 ? tr_chunk<256>(row, pos) : tr_chunk<128>(row, pos);
   };
   // B column chunk = (tap, channel): packed cch | (dh + 64) << 16 | (dw + 64) << 24, -1 = outside
   int b_pack[BL];
@@ -260,19 +265,25 @@ static inline int reduce_groups(int splits, int64_t total) {
 
 using namespace dlmpi;
 
-extern "C" hipError_t dlmpi_conv_wgrad(const WgradArgs* a, int bm, hipStream_t s) {
+extern "C" hipError_t dlmpi_conv_wgrad(const WgradArgs* a, int bm, int bn, hipStream_t s) {
   const unsigned nwg = (unsigned)(a->mtiles * a->ntiles * a->splits);
   if (nwg == 0) return hipSuccess;
   static const int stages = [] {
     const char* e = getenv("DLMPI_WGRAD_STAGES");
     return e ? atoi(e) : 1;
   }();
-  if (bm == 128) {
-    if (stages == 1) hipLaunchKernelGGL((conv_wgrad_kernel<128, 1>), dim3(nwg), dim3(256), 0, s, *a);
-    else hipLaunchKernelGGL((conv_wgrad_kernel<128, 2>), dim3(nwg), dim3(256), 0, s, *a);
-  } else if (bm == 64) {
-    if (stages == 1) hipLaunchKernelGGL((conv_wgrad_kernel<64, 1>), dim3(nwg), dim3(256), 0, s, *a);
-    else hipLaunchKernelGGL((conv_wgrad_kernel<64, 2>), dim3(nwg), dim3(256), 0, s, *a);
+  const dim3 g(nwg), b(256);
+  // (a 256-column variant was measured 1.3-1.9x slower: 2 waves/SIMD and register spills)
+  if (bn == 128) {
+    if (bm == 128) {
+      if (stages == 1) hipLaunchKernelGGL((conv_wgrad_kernel<128, 128, 1>), g, b, 0, s, *a);
+      else hipLaunchKernelGGL((conv_wgrad_kernel<128, 128, 2>), g, b, 0, s, *a);
+    } else if (bm == 64) {
+      if (stages == 1) hipLaunchKernelGGL((conv_wgrad_kernel<64, 128, 1>), g, b, 0, s, *a);
+      else hipLaunchKernelGGL((conv_wgrad_kernel<64, 128, 2>), g, b, 0, s, *a);
+    } else {
+      return hipErrorInvalidValue;
+    }
   } else {
     return hipErrorInvalidValue;
   }

@@ -106,7 +106,7 @@ struct WgradArgs {
 extern "C" {
 // conv / gemm
 hipError_t dlmpi_conv_igemm(const dlmpi::ConvArgs* a, int bm, int bn, hipStream_t s);
-hipError_t dlmpi_conv_wgrad(const dlmpi::WgradArgs* a, int bm, hipStream_t s);
+hipError_t dlmpi_conv_wgrad(const dlmpi::WgradArgs* a, int bm, int bn, hipStream_t s);   // bn: 128 | 256
 // sum of split partials -> grad (accumulated), with channel un-padding and row limit
 hipError_t dlmpi_wgrad_reduce(const float* ws, int splits, int Ko, int T, int Cpad, int Creal,
                               int Ko_real, float* out, float* ws2, int ws2_floats, hipStream_t s);
