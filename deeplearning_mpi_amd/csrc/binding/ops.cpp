@@ -66,12 +66,48 @@ static int bm256_min_tiles() {
   return v;
 }
 
-static void pick_tiles(int64_t M, int Kout, int64_t red, int& bm, int& bn) {
+static int bm_override() {   // experiments: force the M tile (64 | 128 | 256)
+  static int v = [] {
+    const char* e = getenv("DLMPI_CONV_BM");
+    return e ? atoi(e) : 0;
+  }();
+  return v;
+}
+
+static int sq256_min_tiles() {
+  static int v = [] {
+    const char* e = getenv("DLMPI_CONV_256SQ_MIN_TILES");
+    return e ? atoi(e) : 256;
+  }();
+  return v;
+}
+
+// cin: channel count of the GEMM's gathered operand (the 8-wave 256x256 kernel needs cin % 64 == 0)
+static void pick_tiles(int64_t M, int Kout, int64_t red, int cin, int& bm, int& bn) {
   bn = Kout <= 64 ? 64 : 128;
   bm = 128;
+  if (bm_override()) {
+    bm = bm_override();
+    if (bm == 256 && bn != 128) bm = 128;
+    return;
+  }
+  // long reductions into >= 256 output channels: 8-wave 256x256 tiles while the grid still gives
+  // every CU a block (UNet levels 3-5, the wide 3x3 layers)
+  if (Kout >= 256 && red >= 2304 && cin % 64 == 0 && ((M + 255) / 256) * ((Kout + 255) / 256) >= sq256_min_tiles()) {
+    bm = bn = 256;
+    return;
+  }
   const int64_t nt = (Kout + bn - 1) / bn;
   const int64_t tiles = ((M + 127) / 128) * nt;
-  if (Kout >= 256 && red >= 2304 && ((M + 255) / 256) * nt >= bm256_min_tiles()) bm = 256;
+  static const int n64 = [] {
+    const char* e = getenv("DLMPI_CONV_BM256_N64");
+    return e ? atoi(e) : 1;
+  }();
+  // 64-channel outputs: 256 x 64 tiles (4 x 1 waves of 64 x 64).  Measured (conv_bench): wins for
+  // the small-channel stems (-13 % ResNet 7x7, -10 % UNet first conv) and the 4M-row UNet level-1
+  // 3x3s (-4 %), loses 3-8 % on the 0.8M-row ResNet layer1 GEMMs -> only there.
+  if (bn == 64 && n64 && (M + 255) / 256 >= 512 && (cin < 64 || (M >= (2 << 20) && red >= 576))) bm = 256;
+  else if (Kout >= 256 && red >= 2304 && ((M + 255) / 256) * nt >= bm256_min_tiles()) bm = 256;
   else if (tiles < 512) bm = 64;
 }
 
@@ -114,7 +150,7 @@ int conv2d_fwd(const at::Tensor& x, int N, int H, int W, int C, int ldx, int xof
                int S, int stride, int pad, at::Tensor y, int ldy, int yoff, const c10::optional<at::Tensor>& bias,
                const c10::optional<at::Tensor>& res, int ldres, int resoff, const c10::optional<at::Tensor>& scale,
                const c10::optional<at::Tensor>& shift, bool relu, const c10::optional<at::Tensor>& stats, int bm_req,
-               int kvalid) {
+               int kvalid, int bn_req) {
   require_gpu(x, "x");
   const int P = (H + 2 * pad - R) / stride + 1, Q = (W + 2 * pad - S) / stride + 1;
   ConvArgs a{};
@@ -131,8 +167,9 @@ int conv2d_fwd(const at::Tensor& x, int N, int H, int W, int C, int ldx, int xof
   a.vec_store = (a.kvalid == a.Kout && (ldy % 8) == 0 && (yoff % 8) == 0) ? 1 : 0;
   set_kstep(a, C);
   int bm, bn;
-  pick_tiles((int64_t)N * P * Q, K, (int64_t)R * S * C, bm, bn);
-  if (bm_req > 0) bm = bm_req;
+  pick_tiles((int64_t)N * P * Q, K, (int64_t)R * S * C, C, bm, bn);
+  if (bm_req > 0) bm = bm_req;   // tests / experiments: force a tile shape
+  if (bn_req > 0) bn = bn_req;
   a.ntiles = ceil_div(K, bn);
   a.nphase = 1;
   ConvPhase& p = a.ph[0];
@@ -149,7 +186,7 @@ int conv2d_fwd(const at::Tensor& x, int N, int H, int W, int C, int ldx, int xof
 int conv2d_fwd_mtiles(int N, int H, int W, int C, int K, int R, int S, int stride, int pad, int bm_req) {
   const int P = (H + 2 * pad - R) / stride + 1, Q = (W + 2 * pad - S) / stride + 1;
   int bm, bn;
-  pick_tiles((int64_t)N * P * Q, K, (int64_t)R * S * C, bm, bn);
+  pick_tiles((int64_t)N * P * Q, K, (int64_t)R * S * C, C, bm, bn);
   if (bm_req > 0) bm = bm_req;
   return ceil_div((int64_t)N * P * Q, bm);
 }
@@ -201,7 +238,7 @@ c10::optional<at::Tensor> conv2d_dgrad(const at::Tensor& dy, int N, int P, int Q
     throw std::runtime_error("conv2d_dgrad: fused BN tensors must be 8-channel aligned");
   set_kstep(a, K);
   int bm, bn;
-  pick_tiles((int64_t)N * H * W / (stride * stride), C, (int64_t)R * S * K / (stride * stride), bm, bn);
+  pick_tiles((int64_t)N * H * W / (stride * stride), C, (int64_t)R * S * K / (stride * stride), K, bm, bn);
   a.ntiles = ceil_div(C, bn);
   a.nphase = stride * stride;
   int tiles = 0;
@@ -248,7 +285,7 @@ void convT2x2_fwd(const at::Tensor& x, int N, int H, int W, int Cin, int ldx, in
   a.vec_store = ((ldy % 8) == 0 && (yoff % 8) == 0) ? 1 : 0;
   set_kstep(a, Cin);
   int bm, bn;
-  pick_tiles((int64_t)N * H * W, Cout, Cin, bm, bn);
+  pick_tiles((int64_t)N * H * W, Cout, Cin, Cin, bm, bn);
   a.ntiles = ceil_div(Cout, bn);
   a.nphase = 4;
   for (int i = 0; i < 2; ++i)

@@ -37,18 +37,27 @@ __device__ __forceinline__ void glds16(const void* g, char* lds_wave_base) {
 // STAGES = 1: single buffer, two barriers per K-step, 34 KB of LDS -> 4 blocks/CU (latency hidden
 // across blocks instead of inside one).  The epilogue stages the fp32 tile through LDS in two
 // row halves so it never needs more LDS than one stage.
-template <int BM, int BN, bool SMALLC, int STAGES>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(STAGES == 1 && BM * BN <= 16384 ? 3 : 2, 8))) void conv_igemm_kernel(const ConvArgs a) {
+// NW = 8 (512 threads, waves 2 x 4, per-wave 128 x 64 at 256 x 256): 25 % less LDS traffic per
+// MFMA than 64 x 64 per wave, double-buffered (128 KB LDS, one block per CU) so that a whole
+// K-step of MFMA work (2048 SIMD cycles) covers the next step's loads.
+// WGM = wave rows (WGM x NW/WGM wave grid): 4 x 1 for the 256 x 64 tile of 64-channel layers
+// (per-wave 64 x 64 instead of 64 x 32: a third less LDS traffic per MFMA).
+template <int BM, int BN, bool SMALLC, int STAGES, int NW, int WGM>
+__global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(STAGES == 1 && BM * BN <= 16384 ? 3 : 2, 8))) void conv_igemm_kernel(const ConvArgs a) {
+  constexpr int NT = 64 * NW;                 // threads
+  constexpr int WGN = NW / WGM;               // wave grid WGM x WGN
   constexpr int BK = 64;
-  constexpr int WM = BM / 2, WN = BN / 2;
+  constexpr int WM = BM / WGM, WN = BN / WGN;
   constexpr int TM = WM / 16, TN = WN / 16;
-  constexpr int AL = BM / 32, BL = BN / 32;   // 16-byte pieces per thread per tile
+  constexpr int RP = NT / 8;                  // tile rows staged per pass (8 lanes per 128-B row)
+  constexpr int AL = BM / RP, BL = BN / RP;   // 16-byte pieces per thread per tile
   constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2;
   constexpr int STAGE_BYTES = STAGES * (A_BYTES + B_BYTES);
   constexpr int CS_LD = BN + 4;
   constexpr int NP = BM >= 128 ? BM / 64 : 1;            // epilogue passes of <= 64 tile rows
+  static_assert(WM % (16 * NP) == 0 || NP == 1, "epilogue pass must split every wave's rows evenly");
   constexpr int EPI_BYTES = (BM / NP) * CS_LD * 4;
-  constexpr int RED_BYTES = (256 / (BN / 8)) * 3 * BN * 4;   // stats combine
+  constexpr int RED_BYTES = (NT / (BN / 8)) * 3 * BN * 4;    // stats combine
   constexpr int SMEM0 = STAGE_BYTES > EPI_BYTES ? STAGE_BYTES : EPI_BYTES;
   constexpr int SMEM = SMEM0 > RED_BYTES ? SMEM0 : RED_BYTES;
   __shared__ __attribute__((aligned(16))) char smem[SMEM];
@@ -64,8 +73,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(STAGES == 1
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wid >> 1, wn = wid & 1;
-  const int lrow = tid >> 3;                          // staging row (+32 i)
+  const int wm = wid / WGN, wn = wid % WGN;
+  const int lrow = tid >> 3;                          // staging row (+RP i)
   const int jc = (tid & 7) ^ ((tid >> 4) & 7);        // swizzled 16-B chunk this lane fetches
   const char* zp = reinterpret_cast<const char*>(g_zero_page);
 
@@ -74,7 +83,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(STAGES == 1
   uint32_t a_okm = 0;                                 // bit i: GEMM row valid
 #pragma unroll
   for (int i = 0; i < AL; ++i) {
-    const int m = m0 + lrow + 32 * i;
+    const int m = m0 + lrow + RP * i;
     if (m < M) a_okm |= 1u << i;
     const uint32_t mm = m < M ? (uint32_t)m : 0u;
     const uint32_t n_img = fdiv(mm, ph.fdPQ);
@@ -86,13 +95,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(STAGES == 1
     a_pix[i] = ((int)n_img * a.H + h) * a.W + w;
   }
   const char* xlane = reinterpret_cast<const char*>(a.x) + 2 * ((int64_t)a.xoff + 8 * jc);
-  // B rows n0 + lrow + 32 i: one base pointer + validity bits
+  // B rows n0 + lrow + RP i: one base pointer + validity bits
   const char* b_base = reinterpret_cast<const char*>(a.w) + 2 * ((int64_t)(n0 + lrow) * a.ldw + 8 * jc);
-  const int64_t b_step = (int64_t)64 * a.ldw;          // bytes between rows 32 apart
+  const int64_t b_step = (int64_t)2 * RP * a.ldw;      // bytes between rows RP apart
   uint32_t b_okm = 0;
 #pragma unroll
   for (int i = 0; i < BL; ++i)
-    if (n0 + lrow + 32 * i < a.Kout) b_okm |= 1u << i;
+    if (n0 + lrow + RP * i < a.Kout) b_okm |= 1u << i;
 
   const int C = a.C;
   const int T = ph.Tr * ph.Ts;
@@ -128,12 +137,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(STAGES == 1
 #pragma unroll
       for (int i = 0; i < AL; ++i) {
         const char* s = ((a_vm >> i) & 1) ? xlane + 2 * ((uint64_t)a_off[i] + c_cur) : zp;
-        glds16(s, As + (32 * i + 8 * wid) * 128);
+        glds16(s, As + (RP * i + 8 * wid) * 128);
       }
 #pragma unroll
       for (int i = 0; i < BL; ++i) {
         const char* s = ((b_okm >> i) & 1) ? b_base + i * b_step + wtC2 + 2 * c_cur : zp;
-        glds16(s, Bs + (32 * i + 8 * wid) * 128);
+        glds16(s, Bs + (RP * i + 8 * wid) * 128);
       }
     } else {
       // small C (8/16/32; stem & first UNet layer): every 16-B piece is its own tap
@@ -151,12 +160,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(STAGES == 1
         const int ih = (a_hw[i] >> 16) + dh, iw = (a_hw[i] & 0xffff) + dw;
         const bool ok = tv && ((a_okm >> i) & 1) && (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W;
         const char* s = ok ? xs + (int64_t)(a_pix[i] + dh * a.W + dw) * ldx2 : zp;
-        glds16(s, As + (32 * i + 8 * wid) * 128);
+        glds16(s, As + (RP * i + 8 * wid) * 128);
       }
 #pragma unroll
       for (int i = 0; i < BL; ++i) {
         const char* s = (tv && ((b_okm >> i) & 1)) ? b_base + i * b_step - 2 * 8 * jc + 2 * (wt * C + c) : zp;
-        glds16(s, Bs + (32 * i + 8 * wid) * 128);
+        glds16(s, Bs + (RP * i + 8 * wid) * 128);
       }
     }
   };
@@ -227,7 +236,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(STAGES == 1
   float* Cs = reinterpret_cast<float*>(smem);
 
   constexpr int CG = BN / 8;       // channel groups of 8
-  constexpr int RG = 256 / CG;     // row groups
+  constexpr int RG = NT / CG;      // row groups
   const int cg = tid % CG, rg = tid / CG;
   const int c0 = n0 + cg * 8;
   const bool cvalid = c0 < a.Kout;
@@ -389,11 +398,11 @@ template <int BM, int BN>
 static void launch_tile(const ConvArgs* a, dim3 grid, hipStream_t s) {
   const bool one = stages_choice() == 1;
   if (a->C < 64) {
-    if (one) hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, true, 1>), grid, dim3(256), 0, s, *a);
-    else hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, true, 2>), grid, dim3(256), 0, s, *a);
+    if (one) hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, true, 1, 4, 2>), grid, dim3(256), 0, s, *a);
+    else hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, true, 2, 4, 2>), grid, dim3(256), 0, s, *a);
   } else {
-    if (one) hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, false, 1>), grid, dim3(256), 0, s, *a);
-    else hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, false, 2>), grid, dim3(256), 0, s, *a);
+    if (one) hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, false, 1, 4, 2>), grid, dim3(256), 0, s, *a);
+    else hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, false, 2, 4, 2>), grid, dim3(256), 0, s, *a);
   }
 }
 
@@ -402,7 +411,13 @@ extern "C" hipError_t dlmpi_conv_igemm(const ConvArgs* a, int bm, int bn, hipStr
   for (int i = 0; i < a->nphase; ++i) maxt = a->ph[i].mtiles > maxt ? a->ph[i].mtiles : maxt;
   dim3 grid((unsigned)(maxt * a->ntiles), 1, (unsigned)a->nphase);
   if (grid.x == 0) return hipSuccess;
-  if (bm == 256 && bn == 128) launch_tile<256, 128>(a, grid, s);
+  if (bm == 256 && bn == 256) {   // 8 waves, double-buffered; regular channel counts only
+    if (a->C < 64) return hipErrorInvalidValue;
+    hipLaunchKernelGGL((conv_igemm_kernel<256, 256, false, 2, 8, 2>), grid, dim3(512), 0, s, *a);
+  } else if (bm == 256 && bn == 64) {   // 64-channel layers: 4 x 1 waves of 64 x 64
+    if (a->C < 64) hipLaunchKernelGGL((conv_igemm_kernel<256, 64, true, 1, 4, 4>), grid, dim3(256), 0, s, *a);
+    else hipLaunchKernelGGL((conv_igemm_kernel<256, 64, false, 1, 4, 4>), grid, dim3(256), 0, s, *a);
+  } else if (bm == 256 && bn == 128) launch_tile<256, 128>(a, grid, s);
   else if (bm == 128 && bn == 128) launch_tile<128, 128>(a, grid, s);
   else if (bm == 128 && bn == 64) launch_tile<128, 64>(a, grid, s);
   else if (bm == 64 && bn == 128) launch_tile<64, 128>(a, grid, s);

@@ -38,7 +38,7 @@ class NativeBackend:
                  shift=None, relu=False, stats=None, kvalid=0):
         self.C.conv2d_fwd(x.buf, x.N, x.H, x.W, x.C, x.ld, x.off, w, K, R, S, stride, pad, y.buf, y.ld, y.off,
                           bias, res.buf if res is not None else None, res.ld if res is not None else 0,
-                          res.off if res is not None else 0, scale, shift, bool(relu), stats, 0, int(kvalid))
+                          res.off if res is not None else 0, scale, shift, bool(relu), stats, 0, int(kvalid), 0)
 
     def conv_dgrad(self, dy: Act, wT, C, R, S, stride, pad, dx: Act, res: Act = None, fuse=None):
         """fuse = BwdFuse(mask, z, z2, scale, shift): dx is the gradient of relu(BN(z) [+ BN2(z2)]);

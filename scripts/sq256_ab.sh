@@ -1,0 +1,11 @@
+#!/bin/bash
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+cd "$R" && mkdir -p gpurun_out
+export HSA_ENABLE_IPC_MODE_LEGACY=0
+timeout -k 10 400 python -m pytest tests/test_kernels_gpu.py -q -x > gpurun_out/kernels.log 2>&1; echo "kernels rc=$?"
+for th in 1000000 256; do
+  DLMPI_CONV_256SQ_MIN_TILES=$th timeout -k 10 400 python benchmarks/conv_bench.py --net unet512 --iters 10 --no_miopen --only fwd > gpurun_out/cbu_fwd_t$th.log 2>&1 || exit 1
+  DLMPI_CONV_256SQ_MIN_TILES=$th timeout -k 10 400 python benchmarks/conv_bench.py --net unet512 --iters 10 --no_miopen --only dgrad > gpurun_out/cbu_dgrad_t$th.log 2>&1 || exit 1
+  DLMPI_CONV_256SQ_MIN_TILES=$th timeout -k 10 400 python bench.py --config unet512 --steps 10 --warmup 3 > gpurun_out/unet_t$th.log 2>&1 || exit 1
+done
+timeout -k 10 400 python bench.py --steps 10 --warmup 3 > gpurun_out/bench.log 2>&1 || exit 1

@@ -92,12 +92,16 @@ def test_conv_dgrad(shape):
 
 
 @pytest.mark.parametrize("shape", [(2, 20, 20, 64, 128, 3, 1, 1), (3, 9, 11, 256, 256, 1, 1, 0),
-                                   (2, 16, 16, 128, 384, 3, 2, 1)])
-def test_conv_fwd_256_row_tile(shape):
-    """The 256x128 tile (chosen automatically for large grids) forced on small shapes, incl. BN
-    statistics partials and row/column remainders."""
+                                   (2, 16, 16, 128, 384, 3, 2, 1), (2, 18, 18, 256, 320, 3, 1, 1),
+                                   (2, 17, 19, 64, 64, 3, 1, 1), (2, 16, 16, 32, 64, 3, 1, 1)])
+@pytest.mark.parametrize("bn", [0, 64, 256])
+def test_conv_fwd_256_row_tile(shape, bn):
+    """The 256x128 tile and the 8-wave 256x256 tile (chosen automatically for large grids) forced
+    on small shapes, incl. BN statistics partials and row/column remainders."""
     nb, rb = _be()
     N, H, W, Cin, K, R, s, p = shape
+    if (bn == 64) != (K == 64) or (bn == 256 and Cin < 64):
+        pytest.skip("tile does not apply")
     Cp, Kp = pad8(Cin), pad8(K)
     P, Q = (H + 2 * p - R) // s + 1, (W + 2 * p - R) // s + 1
     x, xr = _act(N, H, W, Cp)
@@ -107,7 +111,7 @@ def test_conv_fwd_256_row_tile(shape):
     mt = (N * P * Q + 255) // 256
     st = torch.empty(mt, 2, Kp, device=DEV)
     rows = nb.C.conv2d_fwd(x.buf, N, H, W, Cp, Cp, 0, w, Kp, R, R, s, p, y.buf, Kp, 0, None, None, 0, 0, None, None,
-                           False, st, 256, 0)
+                           False, st, 256, 0, bn)
     assert rows == mt
     str_ = torch.empty(1, 2, Kp, device=DEV)
     rb.conv_fwd(xr, w.float(), Kp, R, R, s, p, yr, stats=str_)
