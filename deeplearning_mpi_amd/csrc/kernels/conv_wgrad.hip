@@ -71,7 +71,7 @@ __device__ __forceinline__ int tr_chunk(int row, int pos) {
 // lane fetches whichever (pixel row, 16-B chunk) the swizzled layout puts there.  STAGES = 1:
 // single stage, two barriers per K-step, 32 KB LDS at BM = 128 -> several blocks per CU hide
 // the load latency of one another.
-template <int BM, int BN, int STAGES>
+template <int BM, int BN, int STAGES, bool DIRECT>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(STAGES == 1 && BN == 128 ? 3 : 2, 8)))
 void conv_wgrad_kernel(const WgradArgs a) {
   constexpr int BK = 64;
@@ -126,6 +126,13 @@ void conv_wgrad_kernel(const WgradArgs a) {
   const uint16_t* dyb = a.dy + a.dyoff;
   const uint16_t* xb = a.x + a.xoff;
 
+  // Branch-free staging: every address is computed unconditionally (no dereference happens for
+  // invalid pieces) and the zero page is selected with v_cndmask, so the glds issue is not split
+  // into exec-masked regions.
+  auto pick = [&](bool ok, const uint16_t* p) -> const char* {
+    const uintptr_t a0 = reinterpret_cast<uintptr_t>(p), z = reinterpret_cast<uintptr_t>(zp);
+    return reinterpret_cast<const char*>(ok ? a0 : z);
+  };
   auto issue = [&](int buf, int pix0) {
     char* As = smem + buf * (A_BYTES + B_BYTES);
     char* Bs = As + A_BYTES;
@@ -134,9 +141,7 @@ void conv_wgrad_kernel(const WgradArgs a) {
       int row, ch;
       piece(i, A_ROW, row, ch);
       const int pix = pix0 + row, col = m0 + 8 * ch;
-      const char* s = (pix < pend && col < a.Ko)
-                          ? reinterpret_cast<const char*>(dyb + (int64_t)pix * a.ldy + col) : zp;
-      glds16(s, As + 16 * (256 * i + 64 * wid));
+      glds16(pick(pix < pend && col < a.Ko, dyb + (int64_t)pix * a.ldy + col), As + 16 * (256 * i + 64 * wid));
     }
 #pragma unroll
     for (int i = 0; i < BL; ++i) {
@@ -144,24 +149,21 @@ void conv_wgrad_kernel(const WgradArgs a) {
       piece(i, B_ROW, row, ch);
       const int pix = pix0 + row;
       const int bp = b_pack[i];
-      bool ok = pix < pend && bp >= 0;
-      if (a.direct) {   // 1x1, stride 1, no padding: the input pixel IS the output pixel
-        const char* s = ok ? reinterpret_cast<const char*>(xb + (int64_t)pix * a.ldx + (bp & 0xffff)) : zp;
-        glds16(s, Bs + 16 * (256 * i + 64 * wid));
-        continue;
+      const bool ok = pix < pend && bp >= 0;
+      if constexpr (DIRECT) {   // 1x1, stride 1, no padding: the input pixel IS the output pixel
+        glds16(pick(ok, xb + (int64_t)pix * a.ldx + (bp & 0xffff)), Bs + 16 * (256 * i + 64 * wid));
+      } else {
+        const uint32_t pp = ok ? (uint32_t)pix : 0u;
+        const uint32_t n_img = fdiv(pp, a.fdPQ);
+        const uint32_t rem = pp - n_img * PQ;
+        const uint32_t p = fdiv(rem, a.fdQ);
+        const uint32_t q = rem - p * a.Q;
+        const int ih = (int)p * a.stride_h + ((bp >> 16) & 255) - 64;
+        const int iw = (int)q * a.stride_w + ((bp >> 24) & 255) - 64;
+        const bool in = ok && (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W;
+        const int64_t off = (((int64_t)n_img * a.H + ih) * a.W + iw) * a.ldx + (bp & 0xffff);
+        glds16(pick(in, xb + off), Bs + 16 * (256 * i + 64 * wid));
       }
-      const uint32_t pp = ok ? (uint32_t)pix : 0u;
-      const uint32_t n_img = fdiv(pp, a.fdPQ);
-      const uint32_t rem = pp - n_img * PQ;
-      const uint32_t p = fdiv(rem, a.fdQ);
-      const uint32_t q = rem - p * a.Q;
-      const int ih = (int)p * a.stride_h + ((bp >> 16) & 255) - 64;
-      const int iw = (int)q * a.stride_w + ((bp >> 24) & 255) - 64;
-      ok = ok && (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W;
-      const char* s = ok ? reinterpret_cast<const char*>(
-                               xb + (((int64_t)n_img * a.H + ih) * a.W + iw) * a.ldx + (bp & 0xffff))
-                         : zp;
-      glds16(s, Bs + 16 * (256 * i + 64 * wid));
     }
   };
 
@@ -274,19 +276,21 @@ extern "C" hipError_t dlmpi_conv_wgrad(const WgradArgs* a, int bm, int bn, hipSt
   }();
   const dim3 g(nwg), b(256);
   // (a 256-column variant was measured 1.3-1.9x slower: 2 waves/SIMD and register spills)
-  if (bn == 128) {
-    if (bm == 128) {
-      if (stages == 1) hipLaunchKernelGGL((conv_wgrad_kernel<128, 128, 1>), g, b, 0, s, *a);
-      else hipLaunchKernelGGL((conv_wgrad_kernel<128, 128, 2>), g, b, 0, s, *a);
-    } else if (bm == 64) {
-      if (stages == 1) hipLaunchKernelGGL((conv_wgrad_kernel<64, 128, 1>), g, b, 0, s, *a);
-      else hipLaunchKernelGGL((conv_wgrad_kernel<64, 128, 2>), g, b, 0, s, *a);
-    } else {
-      return hipErrorInvalidValue;
-    }
+  if (bn != 128 || (bm != 128 && bm != 64)) return hipErrorInvalidValue;
+  const bool d = a->direct != 0;
+#define DLMPI_WG(BM_, ST_)                                                                  \
+  do {                                                                                     \
+    if (d) hipLaunchKernelGGL((conv_wgrad_kernel<BM_, 128, ST_, true>), g, b, 0, s, *a);   \
+    else hipLaunchKernelGGL((conv_wgrad_kernel<BM_, 128, ST_, false>), g, b, 0, s, *a);    \
+  } while (0)
+  if (bm == 128) {
+    if (stages == 1) DLMPI_WG(128, 1);
+    else DLMPI_WG(128, 2);
   } else {
-    return hipErrorInvalidValue;
+    if (stages == 1) DLMPI_WG(64, 1);
+    else DLMPI_WG(64, 2);
   }
+#undef DLMPI_WG
   return hipGetLastError();
 }
 
