@@ -12,6 +12,7 @@ import torch
 
 from ..ops.backend import make_backend
 from ..utils.arena import arena_of
+from ..utils.profiler import range as trace_range
 
 
 def _single_arena(params):
@@ -79,6 +80,10 @@ class SGD(_FusedBase):
 
     @torch.no_grad()
     def step(self, closure=None):
+        with trace_range("dlmpi.sgd_step"):
+            return self._step(closure)
+
+    def _step(self, closure):
         loss = closure() if closure is not None else None
         for g, p, gr, key in self._groups():
             first = "momentum_buffer" not in (self.state[key] if not isinstance(key, str) else
@@ -100,6 +105,10 @@ class Adam(_FusedBase):
 
     @torch.no_grad()
     def step(self, closure=None):
+        with trace_range("dlmpi.adam_step"):
+            return self._step(closure)
+
+    def _step(self, closure):
         loss = closure() if closure is not None else None
         self._step_count += 1
         t = self._step_count

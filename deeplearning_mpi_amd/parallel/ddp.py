@@ -27,6 +27,7 @@ import torch.nn as nn
 from ..models.engine import EngineModule
 from ..ops.backend import make_backend
 from ..utils.arena import ParamArena
+from ..utils.profiler import range as trace_range
 from .comm import get_comm
 
 DEFAULT_FIRST_BUCKET_MB = 2.0
@@ -128,7 +129,8 @@ class DistributedDataParallel(nn.Module):
         active = (self.reducer is not None and self._require_sync and torch.is_grad_enabled()
                   and self.module.training)
         if self.reducer is not None and self.module.training and self.broadcast_buffers and a.fbuf_total:
-            self.comm.broadcast(a.fbuf, 0)   # K5, one collective for every BN running stat
+            with trace_range("dlmpi.ddp_buffer_broadcast"):
+                self.comm.broadcast(a.fbuf, 0)   # K5, one collective for every BN running stat
         if active:
             self.reducer.prepare_for_backward()
             a.hook = self.reducer.mark_ready
