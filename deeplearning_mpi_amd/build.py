@@ -105,7 +105,8 @@ def build_kernels(jobs=8, force=False, verbose=False):
 
     def one(so):
         s, o = so
-        _run([hipcc, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-munsafe-fp-atomics",
+        extra = os.environ.get("DLMPI_HIPCC_FLAGS", "").split()   # experiments, e.g. -DDLMPI_SETPRIO=1
+        _run([hipcc, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-munsafe-fp-atomics", *extra,
               "-c", s, "-o", o], verbose)
         return o
 
