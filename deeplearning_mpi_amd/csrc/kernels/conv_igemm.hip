@@ -23,6 +23,10 @@
 // (bf16-rounded) values.
 #include <cstdlib>
 
+#ifndef DLMPI_W128   // waves/SIMD target of the 128x128 / 256x64 tiles (A/B builds)
+#define DLMPI_W128 3
+#endif
+
 #include "common.h"
 
 namespace dlmpi {
@@ -43,7 +47,7 @@ __device__ __forceinline__ void glds16(const void* g, char* lds_wave_base) {
 // WGM = wave rows (WGM x NW/WGM wave grid): 4 x 1 for the 256 x 64 tile of 64-channel layers
 // (per-wave 64 x 64 instead of 64 x 32: a third less LDS traffic per MFMA).
 template <int BM, int BN, bool SMALLC, int STAGES, int NW, int WGM>
-__global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(STAGES == 1 && BM * BN <= 16384 ? 3 : 2, 8))) void conv_igemm_kernel(const ConvArgs a) {
+__global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(STAGES == 1 && BM * BN <= 16384 ? (BM * BN == 16384 ? DLMPI_W128 : 3) : 2, 8))) void conv_igemm_kernel(const ConvArgs a) {
   constexpr int NT = 64 * NW;                 // threads
   constexpr int WGN = NW / WGM;               // wave grid WGM x WGN
   constexpr int BK = 64;
