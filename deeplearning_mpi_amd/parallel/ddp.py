@@ -12,8 +12,10 @@ MI355X-first differences:
   by RCCL on a dedicated stream -- no gradient copies in or out of bucket buffers;
 * bucket order = flat order = reverse registration, launched in index order by the C++ reducer
   as soon as each bucket's last gradient is written by the engine's backward;
-* bucket sizes default to a small first bucket (start communicating early) then large buckets
-  sized for RCCL rings over 7 point-to-point xGMI links (per-collective latency amortised);
+* bucket sizes default to a small first bucket (start communicating early), then large buckets
+  sized for RCCL rings over 7 point-to-point xGMI links (per-collective latency amortised), and a
+  small last bucket (the stem / first-stage gradients, written last) so that little all-reduce
+  work is left exposed once the backward pass ends;
 * the per-step buffer broadcast is ONE collective over the flat BatchNorm buffer.
 """
 from __future__ import annotations
@@ -32,12 +34,13 @@ from .comm import get_comm
 
 DEFAULT_FIRST_BUCKET_MB = 2.0
 DEFAULT_BUCKET_MB = 32.0
+DEFAULT_LAST_BUCKET_MB = 4.0
 
 
 class DistributedDataParallel(nn.Module):
     def __init__(self, module: nn.Module, device_ids=None, output_device=None, broadcast_buffers=True,
                  bucket_cap_mb=None, first_bucket_cap_mb=None, comm=None, find_unused_parameters=False,
-                 gradient_as_bucket_view=True):
+                 gradient_as_bucket_view=True, last_bucket_cap_mb=None):
         super().__init__()
         self.module = module
         self.comm = comm if comm is not None else get_comm()
@@ -55,7 +58,8 @@ class DistributedDataParallel(nn.Module):
         self._sync_module_states()
         first = (first_bucket_cap_mb or DEFAULT_FIRST_BUCKET_MB) * 2 ** 20
         cap = (bucket_cap_mb or DEFAULT_BUCKET_MB) * 2 ** 20
-        self.bucket_bounds, self.param_bucket = self.arena.buckets(int(first), int(cap))
+        last = (last_bucket_cap_mb or DEFAULT_LAST_BUCKET_MB) * 2 ** 20
+        self.bucket_bounds, self.param_bucket = self.arena.buckets(int(first), int(cap), int(last))
         self.reducer = None
         if self.world_size > 1:
             from .._ext import native

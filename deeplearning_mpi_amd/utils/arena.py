@@ -212,18 +212,24 @@ class ParamArena:
         self._synced_version = None
 
     # ------------------------------------------------------------------ buckets
-    def buckets(self, first_cap_bytes, cap_bytes):
+    def buckets(self, first_cap_bytes, cap_bytes, last_cap_bytes=None):
         """Contiguous gradient buckets over the flat buffer (in flat = reverse-registration order).
-        Returns (list of (start, end) element ranges, param -> bucket index list)."""
+        Returns (list of (start, end) element ranges, param -> bucket index list).
+
+        first_cap_bytes: the first bucket closes early (its all-reduce starts while most of the
+        backward is still ahead).  last_cap_bytes: the tail of the flat order (the network's first
+        layers, whose gradients are written last) is split off into a bucket of at most this size,
+        so the collective left exposed after the backward pass ends is small."""
         bounds = []
         pb = [0] * len(self.params)
         start = 0
         cur = 0
         cap = first_cap_bytes
+        ends = []
         for i in self.order:
             end = self.offsets[i] + self.params[i].numel()
             end = (end + self.ALIGN - 1) // self.ALIGN * self.ALIGN
-            pb[i] = len(bounds)
+            ends.append((i, end))
             cur = end
             if (cur - start) * 4 >= cap:
                 bounds.append((start, cur))
@@ -231,7 +237,17 @@ class ParamArena:
                 cap = cap_bytes
         if cur > start or not bounds:
             bounds.append((start, max(cur, start)))
-        # params assigned after the last closed bucket belong to the final one
-        for i in range(len(pb)):
-            pb[i] = min(pb[i], len(bounds) - 1)
+        if last_cap_bytes and len(ends) > 1:
+            s0, e0 = bounds[-1]
+            if (e0 - s0) * 4 > last_cap_bytes:
+                # smallest parameter boundary inside the last bucket leaving <= last_cap behind it
+                cut = next((e for _, e in ends if s0 < e < e0 and (e0 - e) * 4 <= last_cap_bytes), None)
+                if cut is not None:
+                    bounds[-1] = (s0, cut)
+                    bounds.append((cut, e0))
+        b = 0
+        for i, end in ends:   # bucket of a parameter = the bucket holding its (aligned) end
+            while end > bounds[b][1] and b + 1 < len(bounds):
+                b += 1
+            pb[i] = b
         return bounds, pb

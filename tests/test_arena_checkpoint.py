@@ -41,6 +41,16 @@ def test_arena_rehomes_and_buckets():
     assert max(pb) == len(bounds) - 1
     # fc is registered last -> first in the flat buffer -> first bucket
     assert pb[ar.index[id(m.fc.weight)]] == 0
+    # small tail bucket: the stem (registered first -> end of the flat buffer) goes out in a last
+    # bucket of <= 4 MB instead of at the end of a 32 MB one
+    b2, pb2 = ar.buckets(2 * 2 ** 20, 32 * 2 ** 20, 4 * 2 ** 20)
+    assert len(b2) == len(bounds) + 1 and b2[:-2] == bounds[:-1]
+    assert b2[-2][1] == b2[-1][0] and b2[-1][1] == bounds[-1][1]
+    assert 0 < (b2[-1][1] - b2[-1][0]) * 4 <= 4 * 2 ** 20
+    assert pb2[ar.index[id(m.conv1.weight)]] == len(b2) - 1
+    for i, p in enumerate(ar.params):   # every parameter lies inside its bucket
+        s, e = b2[pb2[i]]
+        assert s <= ar.offsets[i] and ar.offsets[i] + p.numel() <= e
 
 
 def test_compute_copy_refresh():
