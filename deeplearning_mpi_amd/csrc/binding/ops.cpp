@@ -468,6 +468,9 @@ void avgpool_bwd(const at::Tensor& dy, int N, int HW, int C, at::Tensor dx) {
 void nchw_to_nhwc(const at::Tensor& x, int N, int C, int H, int W, int Cpad, at::Tensor y) {
   check(dlmpi_nchw_to_nhwc(ptr<float>(x), N, C, H, W, Cpad, ptr<uint16_t>(y), cur_stream()), "nchw_to_nhwc");
 }
+void s2d_nchw(const at::Tensor& x, int N, int C, int H, int W, int pad, int U, int V, int CS, at::Tensor y) {
+  check(dlmpi_s2d_nchw(ptr<float>(x), N, C, H, W, pad, U, V, CS, ptr<uint16_t>(y), cur_stream()), "s2d_nchw");
+}
 void upsample2x_fwd(const at::Tensor& x, int N, int H, int W, int C, int ldx, int xoff, at::Tensor y, int ldy,
                     int yoff) {
   check(dlmpi_upsample2x_fwd(ptr<uint16_t>(x), N, H, W, C, ldx, xoff, ptr<uint16_t>(y), ldy, yoff, cur_stream()),
@@ -571,6 +574,7 @@ void register_ops(pybind11::module& m) {
   m.def("avgpool_fwd", &avgpool_fwd);
   m.def("avgpool_bwd", &avgpool_bwd);
   m.def("nchw_to_nhwc", &nchw_to_nhwc);
+  m.def("s2d_nchw", &s2d_nchw);
   m.def("upsample2x_fwd", &upsample2x_fwd);
   m.def("upsample2x_bwd", &upsample2x_bwd);
   m.def("cast_weights", &cast_weights);

@@ -155,6 +155,9 @@ hipError_t dlmpi_maxpool_bwd_bn(const uint16_t* dy, const uint8_t* idx, int N, i
 hipError_t dlmpi_avgpool_fwd(const uint16_t* x, int N, int HW, int C, uint16_t* y, hipStream_t s);
 hipError_t dlmpi_avgpool_bwd(const uint16_t* dy, int N, int HW, int C, uint16_t* dx, hipStream_t s);
 hipError_t dlmpi_nchw_to_nhwc(const float* x, int N, int C, int H, int W, int Cpad, uint16_t* y, hipStream_t s);
+// 2x2 space-to-depth of the zero-padded image: y [N][U][V][4*CS] bf16, slot (vh*2+vw) holds CS channels
+hipError_t dlmpi_s2d_nchw(const float* x, int N, int C, int H, int W, int pad, int U, int V, int CS, uint16_t* y,
+                          hipStream_t s);
 hipError_t dlmpi_upsample2x_fwd(const uint16_t* x, int N, int H, int W, int C, int ldx, int xoff, uint16_t* y,
                                 int ldy, int yoff, hipStream_t s);
 hipError_t dlmpi_upsample2x_bwd(const uint16_t* dy, int N, int H, int W, int C, int lddy, int dyoff, float* ws,

@@ -162,6 +162,32 @@ __global__ void nchw_to_nhwc_kernel(const float* __restrict__ x, int N, int C, i
   }
 }
 
+// 2x2 space-to-depth of a zero-padded fp32 NCHW image into bf16 NHWC (the strided-stem layout,
+// models/engine.py:S2DConvUnit): y[n][u][v][(vh*2 + vw)*CS + c] = x[n][c][2u+vh-pad][2v+vw-pad]
+// (zero outside the image and for c >= C).  One thread = 8 output channels of one pixel.
+__global__ void s2d_nchw_kernel(const float* __restrict__ x, int N, int C, int H, int W, int pad, int U, int V, int CS,
+                                uint16_t* __restrict__ y) {
+  const int CT = 4 * CS, CC = CT >> 3;
+  const int64_t total = (int64_t)N * U * V * CC;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t pix = i / CC;
+    const int g = (int)(i - pix * CC);
+    const int v = (int)(pix % V);
+    const int64_t t = pix / V;
+    const int u = (int)(t % U);
+    const int64_t n = t / U;
+    float o[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int j = g * 8 + e, slot = j / CS, c = j - slot * CS;
+      const int h = 2 * u + (slot >> 1) - pad, w = 2 * v + (slot & 1) - pad;
+      o[e] = (c < C && (unsigned)h < (unsigned)H && (unsigned)w < (unsigned)W) ? x[((n * C + c) * H + h) * W + w]
+                                                                               : 0.f;
+    }
+    *reinterpret_cast<u32x4*>(y + pix * CT + g * 8) = pack8(o);
+  }
+}
+
 // Bilinear x2 upsample, align_corners=True: src = o * (in-1)/(out-1).
 __global__ void upsample2x_fwd_kernel(const uint16_t* __restrict__ x, int N, int H, int W, int C, int ldx, int xoff,
                                       uint16_t* __restrict__ y, int ldy, int yoff) {
@@ -276,6 +302,14 @@ extern "C" hipError_t dlmpi_nchw_to_nhwc(const float* x, int N, int C, int H, in
   if (Cpad % 8 || Cpad < C) return hipErrorInvalidValue;
   const int64_t total = (int64_t)N * H * W * (Cpad / 8);
   hipLaunchKernelGGL(nchw_to_nhwc_kernel, dim3(ew_blocks(total)), dim3(256), 0, s, x, N, C, H, W, Cpad, y);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t dlmpi_s2d_nchw(const float* x, int N, int C, int H, int W, int pad, int U, int V, int CS,
+                                     uint16_t* y, hipStream_t s) {
+  if ((4 * CS) % 8 || C > CS) return hipErrorInvalidValue;
+  const int64_t total = (int64_t)N * U * V * (CS / 2);
+  hipLaunchKernelGGL(s2d_nchw_kernel, dim3(ew_blocks(total)), dim3(256), 0, s, x, N, C, H, W, pad, U, V, CS, y);
   return hipGetLastError();
 }
 

@@ -77,6 +77,17 @@ class ConvUnit:
     def out_hw(self, H, W):
         return ((H + 2 * self.pad - self.R) // self.stride + 1, (W + 2 * self.pad - self.S) // self.stride + 1)
 
+    def _weight_fwd(self):
+        return self.arena.get_compute(self.h_fwd)
+
+    def prep_input(self, be, x: torch.Tensor) -> Act:
+        """The network input (fp32 NCHW) in this unit's input layout."""
+        return be.nchw_to_nhwc(x, self.Cp)
+
+    def _wgrad(self, be, dz: Act, x: Act):
+        be.conv_wgrad(dz, x, self.R, self.S, self.stride, self.pad, self.arena.grad_flat(self.conv.weight),
+                      self.Cin, self.K)
+
     def _bias_vec(self):
         if self.bias is None:
             return None
@@ -91,7 +102,7 @@ class ConvUnit:
         assert x.C == self.Cp, (x, self.Cp)
         P, Q = self.out_hw(x.H, x.W)
         N, dev = x.N, x.device
-        wf = self.arena.get_compute(self.h_fwd)
+        wf = self._weight_fwd()
         y = out if out is not None else Act.empty(N, P, Q, self.Kp, be.act_dtype, dev)
         bn = self.bn
         if bn is None:
@@ -178,7 +189,7 @@ class ConvUnit:
                     be.channel_sum(dz, tmp)
                     ar.grad_flat(self.bias).add_(tmp[:self.K])
                 ar.ready(self.bias)
-        be.conv_wgrad(dz, x, self.R, self.S, self.stride, self.pad, ar.grad_flat(self.conv.weight), self.Cin, self.K)
+        self._wgrad(be, dz, x)
         ar.ready(self.conv.weight)
         if not need_dx:
             return None
@@ -186,6 +197,84 @@ class ConvUnit:
         part = be.conv_dgrad(dz, ar.get_compute(self.h_dg), self.Cp, self.R, self.S, self.stride, self.pad, dx,
                              res=dx_res, fuse=fuse_next)
         return (dx, part) if fuse_next is not None else dx
+
+
+class S2DConvUnit(ConvUnit):
+    """A stride-2 convolution with few input channels (the ResNet 7x7/s2/p3 stem) computed as a
+    dense stride-1 convolution over a 2x2 space-to-depth image of the zero-padded input.
+
+    With u = p + a, slot (vh, vw) = (r % 2, s % 2) and a = r // 2, b = s // 2:
+        y[p, q] = sum_{r,s,c} x[2p + r - pad, 2q + s - pad, c] w[r, s, c]
+                = sum_{a,b,slot,c} X2[p + a, q + b, slot, c] w[2a + vh, 2b + vw, c]
+    where X2[u, v, slot, c] = x[2u + vh - pad, 2v + vw - pad, c].  For the 7x7 stem over 3 channels
+    the GEMM reduction becomes 4x4 taps x 16 channels = 256 (4 K-steps) instead of 7x7 taps x 8
+    padded channels = 392 (7 K-steps), the im2col gather has no out-of-image taps (the padding is
+    in the image), and the bf16 input image is half the bytes.  The weight is re-laid out as
+    W2[k][a][b][slot * CS + c] (zero for 2a + vh >= R); the weight gradient is computed in that
+    layout and scattered back into the [K][R][S][C] gradient slot.  Only the forward and the
+    weight gradient exist (the stem's input needs no gradient)."""
+
+    CS = 4   # channels per sub-pixel slot (input channels <= 4)
+
+    def __init__(self, arena: ParamArena, conv, bn=None, relu=True):
+        w = conv.weight
+        K, Cin, R, S = w.shape
+        assert conv.stride == (2, 2) and conv.padding[0] == conv.padding[1] and conv.groups == 1
+        assert Cin <= self.CS and conv.dilation == (1, 1)
+        self.arena, self.conv, self.bn, self.relu = arena, conv, bn, relu
+        self.linear = False
+        self.K, self.Cin, self.R0, self.S0, self.pad0 = K, Cin, R, S, conv.padding[0]
+        self.R, self.S = (R + 1) // 2, (S + 1) // 2   # taps of the stride-1 conv
+        self.stride, self.pad = 1, 0
+        self.Cp = 4 * self.CS
+        self.Kp = padc(K)
+        self.bias = conv.bias
+        self._bias_pad = None
+        self.h_dg = None
+        # one forward compute copy per sub-pixel slot: w[:, :, vh::2, vw::2] -> [Kp][R][S][CS]
+        self.h_slots = []
+        for vh in (0, 1):
+            for vw in (0, 1):
+                v = w.data[:, :, vh::2, vw::2]
+                self.h_slots.append(arena.add_compute(v, (self.Kp, self.R, self.S, self.CS),
+                                                      (K, v.shape[2], v.shape[3], Cin), (0, 2, 3, 1)))
+        self.w2 = None
+        arena.post_refresh.append(self._build_w2)
+        self._gidx = None
+
+    def _build_w2(self):
+        ar = self.arena
+        slots = [ar.get_compute(h).view(self.Kp, self.R, self.S, self.CS) for h in self.h_slots]
+        w2 = torch.stack(slots, dim=3)   # [Kp][R][S][slot][CS]
+        if self.w2 is None or self.w2.device != w2.device or self.w2.dtype != w2.dtype:
+            self.w2 = torch.empty(self.Kp, self.R, self.S, 4 * self.CS, dtype=w2.dtype, device=w2.device)
+        self.w2.view_as(w2).copy_(w2)
+
+    def prep_input(self, be, x: torch.Tensor) -> Act:
+        N, _, H, W = x.shape
+        P = (H + 2 * self.pad0 - self.R0) // 2 + 1
+        Q = (W + 2 * self.pad0 - self.S0) // 2 + 1
+        return be.s2d(x, self.pad0, P + self.R - 1, Q + self.S - 1, self.CS)
+
+    def fwd(self, be, x: Act, train: bool, res: Act = None, out: Act = None, save=True):
+        if self.w2 is None:
+            self._build_w2()
+        return super().fwd(be, x, train, res=res, out=out, save=save)
+
+    def _weight_fwd(self):
+        return self.w2.view(-1)
+
+    def _wgrad(self, be, dz: Act, x: Act):
+        K, R, S, CT = self.K, self.R, self.S, 4 * self.CS
+        g2 = torch.zeros(K * R * S * CT, dtype=torch.float32, device=dz.device)
+        be.conv_wgrad(dz, x, R, S, 1, 0, g2, CT, K)
+        if self._gidx is None or self._gidx.device != dz.device:
+            # grad[k][r][s][c] <- g2[k][r // 2][s // 2][((r % 2) * 2 + s % 2) * CS + c]
+            k, r, s_, c = torch.meshgrid(torch.arange(K), torch.arange(self.R0), torch.arange(self.S0),
+                                         torch.arange(self.Cin), indexing="ij")
+            idx = (((k * R + r // 2) * S + s_ // 2) * CT + ((r % 2) * 2 + s_ % 2) * self.CS + c)
+            self._gidx = idx.reshape(-1).to(dz.device)
+        self.arena.grad_flat(self.conv.weight).add_(g2[self._gidx])
 
 
 class ConvTUnit:

@@ -12,12 +12,14 @@ path of the same parameters (stock PyTorch baseline and test oracle).
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
 from ..ops.act import Act, padc
-from .engine import BwdFuse, ConvUnit, EngineModule
+from .engine import BwdFuse, ConvUnit, EngineModule, S2DConvUnit
 
 
 def conv3x3(i, o, stride=1):
@@ -186,7 +188,11 @@ class ResNet(EngineModule):
     # ------------------------------------------------------------------ engine
     def _build_units(self, ar):
         self.cin_pad = padc(self.in_channels)
-        self.u_stem = ConvUnit(ar, self.conv1, self.bn1, relu=True, cin_pad=self.cin_pad, need_dgrad=False)
+        if self.in_channels <= S2DConvUnit.CS and os.environ.get("DLMPI_STEM_S2D", "1") != "0":
+            # 7x7/s2 stem as a 4x4/s1 conv over a 2x2 space-to-depth image (engine.py:S2DConvUnit)
+            self.u_stem = S2DConvUnit(ar, self.conv1, self.bn1, relu=True)
+        else:
+            self.u_stem = ConvUnit(ar, self.conv1, self.bn1, relu=True, cin_pad=self.cin_pad, need_dgrad=False)
         self.blocks = []
         for layer in (self.layer1, self.layer2, self.layer3, self.layer4):
             for b in layer:
@@ -196,7 +202,7 @@ class ResNet(EngineModule):
     def _engine_forward(self, x, train, save):
         be = self._be
         N = x.shape[0]
-        a0 = be.nchw_to_nhwc(x, self.cin_pad)
+        a0 = self.u_stem.prep_input(be, x)
         h, cs = self.u_stem.fwd(be, a0, train, save=save)
         OH, OW = (h.H + 2 - 3) // 2 + 1, (h.W + 2 - 3) // 2 + 1
         p = Act.empty(N, OH, OW, h.C, be.act_dtype, x.device)

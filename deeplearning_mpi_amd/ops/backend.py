@@ -131,6 +131,14 @@ class NativeBackend:
         self.C.nchw_to_nhwc(x, N, Cc, H, W, Cpad, y.buf)
         return y
 
+    def s2d(self, x: torch.Tensor, pad, U, V, CS) -> Act:
+        """2x2 space-to-depth of the zero-padded NCHW image -> [N, U, V, 4*CS] NHWC."""
+        N, Cc, H, W = x.shape
+        x = x.contiguous().to(self.dt)
+        y = Act.empty(N, U, V, 4 * CS, torch.bfloat16, x.device)
+        self.C.s2d_nchw(x, N, Cc, H, W, pad, U, V, CS, y.buf)
+        return y
+
     def upsample_fwd(self, x: Act, y: Act):
         self.C.upsample2x_fwd(x.buf, x.N, x.H, x.W, x.C, x.ld, x.off, y.buf, y.ld, y.off)
 
@@ -375,6 +383,15 @@ class RefBackend:
         y = Act.zeros(N, H, W, Cpad, self.dt, x.device)
         y.nhwc()[..., :Cc].copy_(x.permute(0, 2, 3, 1))
         return y
+
+    def s2d(self, x: torch.Tensor, pad, U, V, CS) -> Act:
+        N, Cc, H, W = x.shape
+        xp = torch.zeros(N, CS, 2 * U, 2 * V, dtype=self.dt, device=x.device)
+        hh, ww = min(H, 2 * U - pad), min(W, 2 * V - pad)
+        xp[:, :Cc, pad:pad + hh, pad:pad + ww] = x[:, :, :hh, :ww].to(self.dt)
+        # [N, CS, U, vh, V, vw] -> [N, U, V, vh, vw, CS]
+        y = xp.view(N, CS, U, 2, V, 2).permute(0, 2, 4, 3, 5, 1).reshape(N * U * V, 4 * CS)
+        return Act(y.contiguous(), N, U, V, 4 * CS)
 
     def upsample_fwd(self, x: Act, y: Act):
         out = F.interpolate(x.nchw().to(self.dt), scale_factor=2, mode="bilinear", align_corners=True)

@@ -115,6 +115,7 @@ class ParamArena:
         self._compute_total = 0
         self.compute = None
         self._synced_version = None
+        self.post_refresh = []      # callables run after every recast (derived weight layouts)
         self.hook = None            # reducer.mark_ready(param_index) during backward
         self.backward_end = None    # reducer.finalize() at the end of the engine backward
         self.zero_pending = False
@@ -206,6 +207,8 @@ class ParamArena:
         v = self._version()
         if force or v != self._synced_version:
             self.backend.cast_weights(self._entries, self._compute_total, self.compute)
+            for fn in self.post_refresh:   # derived layouts built from the compute copies
+                fn()
             self._synced_version = v
 
     def mark_updated(self):

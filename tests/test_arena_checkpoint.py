@@ -56,14 +56,34 @@ def test_arena_rehomes_and_buckets():
 def test_compute_copy_refresh():
     m = resnet18(num_classes=10)
     ar = m.engine_setup("cpu")
-    w = ar.get_compute(m.u_stem.h_fwd).view(64, 7, 7, 8).clone()
+    u = m.blocks[0].u[0]                   # layer1.0.conv1 (3x3, 64 -> 64)
+    w = ar.get_compute(u.h_fwd).view(64, 3, 3, 64).clone()
     with torch.no_grad():
-        m.conv1.weight.add_(1.0)
+        m.layer1[0].conv1.weight.add_(1.0)
     ar.refresh()
-    w2 = ar.get_compute(m.u_stem.h_fwd).view(64, 7, 7, 8)
-    assert torch.allclose(w2[..., :3].permute(0, 3, 1, 2), m.conv1.weight)
-    assert torch.all(w2[..., 3:] == 0)
+    w2 = ar.get_compute(u.h_fwd).view(64, 3, 3, 64)
+    assert torch.allclose(w2.permute(0, 3, 1, 2), m.layer1[0].conv1.weight)
     assert not torch.equal(w, w2)
+
+
+def test_s2d_stem_weight_layout():
+    """7x7/s2 stem as a 4x4/s1 conv over the 2x2 space-to-depth image: W2[k][a][b][slot*4 + c] =
+    w[k][c][2a + vh][2b + vw] (slot = 2 vh + vw), zero past the 7x7 window and for c = 3; refreshed
+    with the other compute copies."""
+    m = resnet18(num_classes=10)
+    ar = m.engine_setup("cpu")
+    assert type(m.u_stem).__name__ == "S2DConvUnit"
+    with torch.no_grad():
+        m.conv1.weight.add_(0.5)
+    ar.refresh()
+    w = m.conv1.weight.detach()
+    w2 = m.u_stem.w2.view(64, 4, 4, 4, 4)   # [k][a][b][slot][c]
+    ref = torch.zeros(64, 4, 4, 4, 4)
+    for vh in (0, 1):
+        for vw in (0, 1):
+            blk = w[:, :, vh::2, vw::2].permute(0, 2, 3, 1)   # [k][a][b][c]
+            ref[:, :blk.shape[1], :blk.shape[2], vh * 2 + vw, :3] = blk
+    assert torch.equal(w2, ref)
 
 
 def test_checkpoint_roundtrip(tmp_path):

@@ -281,6 +281,13 @@ def test_pools_and_layout():
     a = nb.nchw_to_nhwc(x, 8)
     ar = rb.nchw_to_nhwc(x, 8)
     assert _rel(a.buf, ar.buf) < 1e-2
+    # 2x2 space-to-depth of the padded image (S2D stem input), odd sizes included
+    for (H, W, pad) in [(20, 18, 3), (23, 17, 3), (8, 8, 1)]:
+        x = torch.randn(2, 3, H, W, device=DEV)
+        U, V = (H + 2 * pad + 1) // 2, (W + 2 * pad + 1) // 2
+        a, ar = nb.s2d(x, pad, U, V, 4), rb.s2d(x, pad, U, V, 4)
+        assert a.buf.shape == ar.buf.shape == (2 * U * V, 16)
+        assert torch.equal(a.buf.float(), ar.buf.to(torch.bfloat16).float())
     for (k, s, p, H, W, C) in [(3, 2, 1, 16, 16, 64), (2, 2, 0, 16, 24, 128)]:
         xa, xr = _act(2, H, W, C)
         OH, OW = (H + 2 * p - k) // s + 1, (W + 2 * p - k) // s + 1
