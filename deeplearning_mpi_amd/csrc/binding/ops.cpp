@@ -432,9 +432,10 @@ void channel_sum(const at::Tensor& x, int64_t M, int C, int ldx, int xoff, at::T
 
 // --------------------------------- pooling / layout ----------------------------------------
 void maxpool_fwd(const at::Tensor& x, int N, int H, int W, int C, int ldx, int xoff, int k, int stride, int pad,
-                 at::Tensor y, at::Tensor idx, int OH, int OW) {
+                 at::Tensor y, at::Tensor idx, int OH, int OW, const c10::optional<at::Tensor>& scale,
+                 const c10::optional<at::Tensor>& shift) {
   check(dlmpi_maxpool_fwd(ptr<uint16_t>(x), N, H, W, C, ldx, xoff, k, stride, pad, ptr<uint16_t>(y),
-                          ptr<uint8_t>(idx), OH, OW, cur_stream()),
+                          ptr<uint8_t>(idx), OH, OW, optr<float>(scale), optr<float>(shift), cur_stream()),
         "maxpool_fwd");
 }
 void maxpool_bwd(const at::Tensor& dy, const at::Tensor& idx, int N, int H, int W, int C, int k, int stride, int pad,

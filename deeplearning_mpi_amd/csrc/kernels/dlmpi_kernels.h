@@ -142,8 +142,10 @@ hipError_t dlmpi_channel_sum(const uint16_t* x, int64_t M, int C, int ldx, int x
 int dlmpi_reduce_blocks(int64_t M, int C);
 
 // pooling / layout
+// scale/shift (optional): pool relu(x * scale + shift) (bf16-rounded), i.e. BN-apply + ReLU fused
 hipError_t dlmpi_maxpool_fwd(const uint16_t* x, int N, int H, int W, int C, int ldx, int xoff, int k, int stride,
-                             int pad, uint16_t* y, uint8_t* idx, int OH, int OW, hipStream_t s);
+                             int pad, uint16_t* y, uint8_t* idx, int OH, int OW, const float* scale,
+                             const float* shift, hipStream_t s);
 hipError_t dlmpi_maxpool_bwd(const uint16_t* dy, const uint8_t* idx, int N, int H, int W, int C, int k, int stride,
                              int pad, int OH, int OW, const uint16_t* add, int ldadd, int addoff, uint16_t* dx,
                              int lddx, int dxoff, hipStream_t s);

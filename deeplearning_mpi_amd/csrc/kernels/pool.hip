@@ -15,9 +15,12 @@ static inline unsigned ew_blocks(int64_t total) {
 
 // Max pool forward; idx stores the winning window position (kh*k + kw) per channel, first max
 // in scan order wins (torch semantics).  Padding never wins.
+// scale/shift (optional): the pooled input is relu(x * scale + shift) rounded to bf16, i.e. the
+// training-mode BN-apply + ReLU of the ResNet stem fused into the pool -- the stem's BN output is
+// never written or re-read (identical values and argmax to pooling the materialised bf16 tensor).
 __global__ void maxpool_fwd_kernel(const uint16_t* __restrict__ x, int N, int H, int W, int C, int ldx, int xoff,
                                    int k, int stride, int pad, uint16_t* __restrict__ y, uint8_t* __restrict__ idx,
-                                   int OH, int OW) {
+                                   int OH, int OW, const float* __restrict__ scale, const float* __restrict__ shift) {
   const int CC = C >> 3;
   const int64_t total = (int64_t)N * OH * OW * CC;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
@@ -27,10 +30,14 @@ __global__ void maxpool_fwd_kernel(const uint16_t* __restrict__ x, int N, int H,
     const int64_t t2 = pix / OW;
     const int oh = (int)(t2 % OH);
     const int n = (int)(t2 / OH);
-    float best[8];
+    float best[8], sc[8], sh[8];
     uint8_t bi[8];
 #pragma unroll
     for (int e = 0; e < 8; ++e) { best[e] = -INFINITY; bi[e] = 0; }
+    if (scale) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) { sc[e] = scale[cc * 8 + e]; sh[e] = shift[cc * 8 + e]; }
+    }
     for (int kh = 0; kh < k; ++kh) {
       const int ih = oh * stride - pad + kh;
       if ((unsigned)ih >= (unsigned)H) continue;
@@ -39,6 +46,10 @@ __global__ void maxpool_fwd_kernel(const uint16_t* __restrict__ x, int N, int H,
         if ((unsigned)iw >= (unsigned)W) continue;
         float v[8];
         unpack8(*reinterpret_cast<const u32x4*>(x + (((int64_t)n * H + ih) * W + iw) * ldx + xoff + cc * 8), v);
+        if (scale) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] = bf2f(f2bf(fmaxf(v[e] * sc[e] + sh[e], 0.f)));
+        }
 #pragma unroll
         for (int e = 0; e < 8; ++e)
           if (v[e] > best[e] || (v[e] != v[e] && best[e] == best[e])) { best[e] = v[e]; bi[e] = (uint8_t)(kh * k + kw); }
@@ -266,11 +277,11 @@ using namespace dlmpi;
 
 extern "C" hipError_t dlmpi_maxpool_fwd(const uint16_t* x, int N, int H, int W, int C, int ldx, int xoff, int k,
                                         int stride, int pad, uint16_t* y, uint8_t* idx, int OH, int OW,
-                                        hipStream_t s) {
+                                        const float* scale, const float* shift, hipStream_t s) {
   if (C % 8) return hipErrorInvalidValue;
   const int64_t total = (int64_t)N * OH * OW * (C / 8);
   hipLaunchKernelGGL(maxpool_fwd_kernel, dim3(ew_blocks(total)), dim3(256), 0, s, x, N, H, W, C, ldx, xoff, k, stride,
-                     pad, y, idx, OH, OW);
+                     pad, y, idx, OH, OW, scale, shift);
   return hipGetLastError();
 }
 

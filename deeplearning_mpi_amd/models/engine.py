@@ -98,7 +98,10 @@ class ConvUnit:
         self._bias_pad[:self.K].copy_(self.bias.data)
         return self._bias_pad
 
-    def fwd(self, be, x: Act, train: bool, res: Act = None, out: Act = None, save=True):
+    def fwd(self, be, x: Act, train: bool, res: Act = None, out: Act = None, save=True, defer_apply=False):
+        """Returns (output, saved context).  defer_apply (training BN, no residual): skip the
+        BN-apply + ReLU and return the BN input z -- the consumer applies scale/shift (ctx[5:7])
+        itself (the ResNet stem's max-pool), so the BN output is never materialised."""
         assert x.C == self.Cp, (x, self.Cp)
         P, Q = self.out_hw(x.H, x.W)
         N, dev = x.N, x.device
@@ -125,6 +128,8 @@ class ConvUnit:
                            bn.running_mean if bn.track_running_stats else None,
                            bn.running_var if bn.track_running_stats else None, mom, bn.eps, scale, shift, mean,
                            invstd)
+            if defer_apply and save and res is None:
+                return z, (x, z, None, mean, invstd, scale, shift, False, None)
             # residual units: the backward mask (y > 0) cannot be recomputed from z alone, so keep it
             # as bits (1/16 of y's bytes) for the fused data-gradient epilogue
             mbits = None
@@ -256,10 +261,10 @@ class S2DConvUnit(ConvUnit):
         Q = (W + 2 * self.pad0 - self.S0) // 2 + 1
         return be.s2d(x, self.pad0, P + self.R - 1, Q + self.S - 1, self.CS)
 
-    def fwd(self, be, x: Act, train: bool, res: Act = None, out: Act = None, save=True):
+    def fwd(self, be, x: Act, train: bool, res: Act = None, out: Act = None, save=True, defer_apply=False):
         if self.w2 is None:
             self._build_w2()
-        return super().fwd(be, x, train, res=res, out=out, save=save)
+        return super().fwd(be, x, train, res=res, out=out, save=save, defer_apply=defer_apply)
 
     def _weight_fwd(self):
         return self.w2.view(-1)

@@ -203,10 +203,13 @@ class ResNet(EngineModule):
         be = self._be
         N = x.shape[0]
         a0 = self.u_stem.prep_input(be, x)
-        h, cs = self.u_stem.fwd(be, a0, train, save=save)
+        # training with the fused BN backward: the stem BN-apply + ReLU runs inside the max-pool
+        # (h is then the BN input z; the backward needs only z, scale and shift)
+        defer = train and save and self.fuse_bn_bwd and self.bn1 is not None
+        h, cs = self.u_stem.fwd(be, a0, train, save=save, defer_apply=defer)
         OH, OW = (h.H + 2 - 3) // 2 + 1, (h.W + 2 - 3) // 2 + 1
         p = Act.empty(N, OH, OW, h.C, be.act_dtype, x.device)
-        idx = be.maxpool_fwd(h, 3, 2, 1, p)
+        idx = be.maxpool_fwd(h, 3, 2, 1, p, bn=(cs[5], cs[6]) if defer else None)
         st_blocks = []
         a = p
         for blk in self.blocks:

@@ -332,6 +332,12 @@ def test_maxpool_bwd_fused_bn_stats():
     OH = OW = 8
     p = _empty(N, OH, OW, C)
     idx = nb.maxpool_fwd(y, 3, 2, 1, p)
+    # BN-apply + ReLU fused into the pool (the stem's BN output never materialised): same values
+    # and the same argmax as pooling the stored bf16 output
+    p2 = _empty(N, OH, OW, C)
+    idx2 = nb.maxpool_fwd(z, 3, 2, 1, p2, bn=(sc, sh))
+    torch.cuda.synchronize()
+    assert torch.equal(p2.buf, p.buf) and torch.equal(idx2, idx)
     dy, dyr = _act(N, OH, OW, C)
     dx, dxr = _empty(N, H, W, C), _empty(N, H, W, C, torch.float32)
     part = nb.maxpool_bwd(dy, idx, y, 3, 2, 1, dx, fuse=BwdFuse(None, z, None, sc, sh))
