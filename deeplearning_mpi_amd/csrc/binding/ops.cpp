@@ -182,6 +182,51 @@ int conv2d_fwd(const at::Tensor& x, int N, int H, int W, int C, int ldx, int xof
   return p.mtiles;   // rows of the stats partial buffer
 }
 
+// Forward conv whose output is the gradient of y = relu(BN(z)) (a BN+ReLU without residual): the
+// epilogue applies the ReLU mask [z * mscale + mshift > 0] before the store and emits that BN's
+// backward partials [tiles][2][K] = {sum v, sum v*z}, returned.  (UNet: the ConvTranspose2d
+// data-gradient -- a 2x2/s2 conv -- into the DoubleConv output below it.)
+at::Tensor conv2d_fwd_bnbwd(const at::Tensor& x, int N, int H, int W, int C, int ldx, int xoff, const at::Tensor& w,
+                            int K, int R, int S, int stride, int pad, at::Tensor y, int ldy, int yoff,
+                            const at::Tensor& z, int ldz, int zoff, const at::Tensor& mscale,
+                            const at::Tensor& mshift) {
+  require_gpu(x, "x");
+  const int P = (H + 2 * pad - R) / stride + 1, Q = (W + 2 * pad - S) / stride + 1;
+  ConvArgs a{};
+  a.x = ptr<uint16_t>(x);
+  a.H = H; a.W = W; a.C = C; a.ldx = ldx; a.xoff = xoff;
+  a.w = ptr<uint16_t>(w);
+  a.ldw = R * S * C;
+  a.S = S;
+  a.OH = P; a.OW = Q;
+  a.so = 1; a.sa = stride;
+  a.Nimg = N; a.Kout = K;
+  fill_epilogue(a, y, ldy, yoff, c10::nullopt, c10::nullopt, 0, 0, c10::nullopt, c10::nullopt, false, c10::nullopt);
+  a.vec_store = ((ldy % 8) == 0 && (yoff % 8) == 0) ? 1 : 0;
+  a.z = ptr<uint16_t>(z);
+  a.ldz = ldz; a.zoff = zoff;
+  a.mscale = ptr<float>(mscale);
+  a.mshift = ptr<float>(mshift);
+  a.nstat = 2;
+  if ((ldz | zoff) % 8 != 0 || !a.vec_store || K % 8)
+    throw std::runtime_error("conv2d_fwd_bnbwd: fused BN tensors must be 8-channel aligned");
+  set_kstep(a, C);
+  int bm, bn;
+  pick_tiles((int64_t)N * P * Q, K, (int64_t)R * S * C, C, bm, bn);
+  a.ntiles = ceil_div(K, bn);
+  a.nphase = 1;
+  ConvPhase& p = a.ph[0];
+  p.P = P; p.Q = Q; p.Tr = R; p.Ts = S;
+  p.dh0 = -pad; p.dhs = 1; p.dw0 = -pad; p.dws = 1;
+  p.wr0 = 0; p.wrs = 1; p.ws0 = 0; p.wss = 1;
+  p.oh0 = 0; p.ow0 = 0;
+  finish_phase(p, N, C, bm);
+  at::Tensor stats = at::empty({(int64_t)p.mtiles, 2, (int64_t)K}, x.options().dtype(at::kFloat));
+  a.stats = ptr<float>(stats);
+  check(dlmpi_conv_igemm(&a, bm, bn, cur_stream()), "conv2d_fwd_bnbwd");
+  return stats;
+}
+
 // Number of BN-stat partial rows conv2d_fwd will produce (so the caller can size `stats`).
 int conv2d_fwd_mtiles(int N, int H, int W, int C, int K, int R, int S, int stride, int pad, int bm_req) {
   const int P = (H + 2 * pad - R) / stride + 1, Q = (W + 2 * pad - S) / stride + 1;
@@ -449,13 +494,15 @@ void maxpool_bwd(const at::Tensor& dy, const at::Tensor& idx, int N, int H, int 
 // returns the partials [nblk][2][C] for bn_bwd_finalize_fused
 at::Tensor maxpool_bwd_bn(const at::Tensor& dy, const at::Tensor& idx, int N, int H, int W, int C, int k, int stride,
                           int pad, int OH, int OW, const at::Tensor& z, const at::Tensor& mscale,
-                          const at::Tensor& mshift, at::Tensor dx) {
+                          const at::Tensor& mshift, const c10::optional<at::Tensor>& add, int ldadd, int addoff,
+                          at::Tensor dx) {
   // more blocks than the generic reductions: every row is a latency-bound window gather
   const int64_t rpb = 256 / (C / 8);
   const int nblk = (int)std::max<int64_t>(1, std::min<int64_t>(4096, ((int64_t)N * H * W + rpb * 8 - 1) / (rpb * 8)));
   at::Tensor part = at::empty({nblk, 2, C}, dy.options().dtype(at::kFloat));
   check(dlmpi_maxpool_bwd_bn(ptr<uint16_t>(dy), ptr<uint8_t>(idx), N, H, W, C, k, stride, pad, OH, OW,
-                             ptr<uint16_t>(z), ptr<float>(mscale), ptr<float>(mshift), ptr<uint16_t>(dx), ptr<float>(part),
+                             ptr<uint16_t>(z), ptr<float>(mscale), ptr<float>(mshift), optr<uint16_t>(add), ldadd,
+                             addoff, ptr<uint16_t>(dx), ptr<float>(part),
                              nblk, cur_stream()),
         "maxpool_bwd_bn");
   return part;
@@ -557,6 +604,7 @@ void register_ops(pybind11::module& m) {
   namespace py = pybind11;
   m.def("conv2d_fwd", &conv2d_fwd);
   m.def("conv2d_fwd_mtiles", &conv2d_fwd_mtiles);
+  m.def("conv2d_fwd_bnbwd", &conv2d_fwd_bnbwd);
   m.def("conv2d_dgrad", &conv2d_dgrad);
   m.def("convT2x2_fwd", &convT2x2_fwd);
   m.def("conv2d_wgrad", &conv2d_wgrad);

@@ -56,14 +56,16 @@ __device__ void block_combine(float (*acc)[8], const RowMap& rm, int C, float* p
 // that produced the pool input (the ResNet stem): dx = [z*scale + shift > 0] * sum of the window
 // gradients that selected the element, written as the masked gradient dyr, and per-block partials
 // {sum dyr, sum dyr*z} for the fused finalize (raw_z).  Replaces maxpool_bwd + bn_bwd_reduce and
-// the mask read of bn_bwd_apply.
+// the mask read of bn_bwd_apply.  `add` (optional): a second gradient of the pool input summed in
+// before the mask (the UNet encoder output also feeds the decoder's skip concat).
 __global__ __launch_bounds__(256) void maxpool_bwd_bn_kernel(const uint16_t* __restrict__ dy,
                                                              const uint8_t* __restrict__ idx, int N, int H, int W,
                                                              int C, int k, int stride, int pad, int OH, int OW,
                                                              FastDiv fdW, FastDiv fdH, const uint16_t* __restrict__ z,
                                                              const float* __restrict__ msc,
-                                                             const float* __restrict__ msh, uint16_t* __restrict__ dx,
-                                                             float* __restrict__ partial) {
+                                                             const float* __restrict__ msh,
+                                                             const uint16_t* __restrict__ add, int ldadd, int addoff,
+                                                             uint16_t* __restrict__ dx, float* __restrict__ partial) {
   const RowMap rm = rowmap(C);
   float acc[2][8] = {};
   const int64_t M = (int64_t)N * H * W;
@@ -96,6 +98,12 @@ __global__ __launch_bounds__(256) void maxpool_bwd_bn_kernel(const uint16_t* __r
           for (int e = 0; e < 8; ++e)
             if (((id >> (8 * e)) & 0xff) == want) g[e] += d[e];
         }
+      }
+      if (add) {   // second gradient source of the pool input (UNet: its skip-concat slice)
+        float a2[8];
+        unpack8(*reinterpret_cast<const u32x4*>(add + row * ldadd + addoff + c0), a2);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) g[e] += a2[e];
       }
       float zz[8];
       unpack8(*reinterpret_cast<const u32x4*>(z + row * C + c0), zz);
@@ -585,10 +593,10 @@ extern "C" hipError_t dlmpi_channel_sum(const uint16_t* x, int64_t M, int C, int
 
 extern "C" hipError_t dlmpi_maxpool_bwd_bn(const uint16_t* dy, const uint8_t* idx, int N, int H, int W, int C, int k,
                                            int stride, int pad, int OH, int OW, const uint16_t* z, const float* mscale,
-                                           const float* mshift, uint16_t* dx, float* partial, int nblk,
-                                           hipStream_t s) {
+                                           const float* mshift, const uint16_t* add, int ldadd, int addoff,
+                                           uint16_t* dx, float* partial, int nblk, hipStream_t s) {
   if (C % 8 || C > 2048 || (int64_t)N * H * W >= (1ll << 31)) return hipErrorInvalidValue;
   hipLaunchKernelGGL(maxpool_bwd_bn_kernel, dim3(nblk), dim3(256), 0, s, dy, idx, N, H, W, C, k, stride, pad, OH, OW,
-                     make_fastdiv(W), make_fastdiv(H), z, mscale, mshift, dx, partial);
+                     make_fastdiv(W), make_fastdiv(H), z, mscale, mshift, add, ldadd, addoff, dx, partial);
   return hipGetLastError();
 }

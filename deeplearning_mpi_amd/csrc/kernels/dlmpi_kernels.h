@@ -150,10 +150,12 @@ hipError_t dlmpi_maxpool_bwd(const uint16_t* dy, const uint8_t* idx, int N, int 
                              int pad, int OH, int OW, const uint16_t* add, int ldadd, int addoff, uint16_t* dx,
                              int lddx, int dxoff, hipStream_t s);
 // max-pool backward into the gradient of a BN+ReLU output (mask z*scale+shift > 0), with the BN
-// backward partials [nblk][2][C] = {sum dyr, sum dyr*z}; dx/z dense [N*H*W][C]
+// backward partials [nblk][2][C] = {sum dyr, sum dyr*z}; dx/z dense [N*H*W][C]; add (optional): a second
+// gradient of the pool input (channel slice of a [N*H*W][ldadd] buffer) summed in before the mask
 hipError_t dlmpi_maxpool_bwd_bn(const uint16_t* dy, const uint8_t* idx, int N, int H, int W, int C, int k, int stride,
                                 int pad, int OH, int OW, const uint16_t* z, const float* mscale, const float* mshift,
-                                uint16_t* dx, float* partial, int nblk, hipStream_t s);
+                                const uint16_t* add, int ldadd, int addoff, uint16_t* dx, float* partial, int nblk,
+                                hipStream_t s);
 hipError_t dlmpi_avgpool_fwd(const uint16_t* x, int N, int HW, int C, uint16_t* y, hipStream_t s);
 hipError_t dlmpi_avgpool_bwd(const uint16_t* dy, int N, int HW, int C, uint16_t* dx, hipStream_t s);
 hipError_t dlmpi_nchw_to_nhwc(const float* x, int N, int C, int H, int W, int Cpad, uint16_t* y, hipStream_t s);

@@ -301,7 +301,9 @@ class ConvTUnit:
                      self.m.bias.data if self.m.bias is not None else None)
         return x
 
-    def bwd(self, be, x: Act, dout: Act):
+    def bwd(self, be, x: Act, dout: Act, fuse_next=None):
+        """fuse_next (BwdFuse of the BN+ReLU unit that produced x): the data gradient is written
+        ReLU-masked with that BN's backward partials -> returns (dx, partials)."""
         ar = self.arena
         if self.m.bias is not None:
             be.channel_sum(dout, ar.grad_flat(self.m.bias))
@@ -310,6 +312,8 @@ class ConvTUnit:
         be.conv_wgrad(x, dout, 2, 2, 2, 0, ar.grad_flat(self.m.weight), self.Cout, self.Cin)
         ar.ready(self.m.weight)
         dx = Act.empty(x.N, x.H, x.W, self.Cip, be.act_dtype, x.device)
+        if fuse_next is not None:
+            return dx, be.conv_fwd_bnbwd(dout, ar.get_compute(self.h_dg), self.Cip, 2, 2, 2, 0, dx, fuse_next)
         be.conv_fwd(dout, ar.get_compute(self.h_dg), self.Cip, 2, 2, 2, 0, dx)
         return dx
 

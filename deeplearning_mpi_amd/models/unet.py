@@ -189,16 +189,22 @@ class UNet(EngineModule):
             pre = None
             dup = dcat.slice(0, self.up_ch[k])
             if self.upT[k] is not None:
-                da = self.upT[k].bwd(be, below, dup)
+                # the ConvTranspose data-gradient is the gradient of the BN+ReLU output below it
+                # (the next decoder level's, or the bottleneck's, second conv): masked + partials
+                below_ctx = ctx_dec[k + 1][2] if k < 3 else cbb
+                out = self.upT[k].bwd(be, below, dup, fuse_next=spec(below_ctx))
+                da, pre = out if fuse else (out, None)
             else:
                 da = Act.empty(below.N, below.H, below.W, below.C, be.act_dtype, below.device)
                 be.upsample_bwd(dup, da)
             ctx_dec[k] = dcat                 # keep the skip-slice gradient for the encoder
-        da = double_bwd(self.bott, cba, cbb, da)
+        da = double_bwd(self.bott, cba, cbb, da, pre=pre)
         for k in range(3, -1, -1):
             skip = skips[k]
             dskip = Act.empty(skip.N, skip.H, skip.W, skip.C, be.act_dtype, skip.device)
-            be.maxpool_bwd(da, idxs[k], skip, 2, 2, 0, dskip,
-                           add=ctx_dec[k].slice(self.up_ch[k], self.skip_ch[k]))
             ca, cb = ctx_enc[k]
-            da = double_bwd(self.enc[k], ca, cb, dskip, need_dx=k != 0)
+            # gradient of the encoder output = pool backward + its skip-concat slice; with the
+            # fusion the pool backward also masks it and emits the encoder BN's partials
+            part = be.maxpool_bwd(da, idxs[k], skip, 2, 2, 0, dskip,
+                                  add=ctx_dec[k].slice(self.up_ch[k], self.skip_ch[k]), fuse=spec(cb))
+            da = double_bwd(self.enc[k], ca, cb, dskip, pre=part, need_dx=k != 0)

@@ -40,6 +40,13 @@ class NativeBackend:
                           bias, res.buf if res is not None else None, res.ld if res is not None else 0,
                           res.off if res is not None else 0, scale, shift, bool(relu), stats, 0, int(kvalid), 0)
 
+    def conv_fwd_bnbwd(self, x: Act, w, K, R, S, stride, pad, y: Act, fuse):
+        """Forward conv producing the gradient of relu(BN(z)) (fuse = BwdFuse(None, z, None, scale,
+        shift)): masked in the epilogue, BN-backward partials [tiles][2][K] returned."""
+        z = fuse.z
+        return self.C.conv2d_fwd_bnbwd(x.buf, x.N, x.H, x.W, x.C, x.ld, x.off, w, K, R, S, stride, pad, y.buf, y.ld,
+                                       y.off, z.buf, z.ld, z.off, fuse.scale, fuse.shift)
+
     def conv_dgrad(self, dy: Act, wT, C, R, S, stride, pad, dx: Act, res: Act = None, fuse=None):
         """fuse = BwdFuse(mask, z, z2, scale, shift): dx is the gradient of relu(BN(z) [+ BN2(z2)]);
         the epilogue applies the ReLU mask (y > 0, or z*scale + shift > 0 without a residual) and
@@ -111,12 +118,15 @@ class NativeBackend:
 
     def maxpool_bwd(self, dy: Act, idx, x: Act, k, s, p, dx: Act, add: Act = None, fuse=None):
         """fuse = BwdFuse(None, z, scale=, shift=): dx is the gradient of relu(BN(z)); it is written
-        masked and the BN-backward partials are returned (for bn_bwd(pre=...))."""
+        masked and the BN-backward partials are returned (for bn_bwd(pre=...)).  add: a second
+        gradient of the pool input, summed in before the mask."""
         if fuse is not None:
-            assert add is None and fuse.scale is not None and dx.ld == dx.C and fuse.z.ld == fuse.z.C
+            assert fuse.scale is not None and dx.ld == dx.C and fuse.z.ld == fuse.z.C
             assert dy.ld == dy.C and dy.off == 0 and dx.off == 0 and fuse.z.off == 0
             return self.C.maxpool_bwd_bn(dy.buf, idx, x.N, x.H, x.W, x.C, k, s, p, dy.H, dy.W, fuse.z.buf,
-                                         fuse.scale, fuse.shift, dx.buf)
+                                         fuse.scale, fuse.shift, add.buf if add is not None else None,
+                                         add.ld if add is not None else 0, add.off if add is not None else 0,
+                                         dx.buf)
         self.C.maxpool_bwd(dy.buf, idx, x.N, x.H, x.W, x.C, k, s, p, dy.H, dy.W, add.buf if add is not None else None,
                            add.ld if add is not None else 0, add.off if add is not None else 0, dx.buf, dx.ld, dx.off)
 
@@ -272,6 +282,15 @@ class RefBackend:
         if z2 is not None:
             rows.append((v * z2.nhwc().to(self.dt)).sum((0, 1, 2)))
         return torch.stack(rows).unsqueeze(0)
+
+    def conv_fwd_bnbwd(self, x: Act, w, K, R, S, stride, pad, y: Act, fuse):
+        wk = w.view(K, R, S, x.C).permute(0, 3, 1, 2).to(self.dt)
+        out = F.conv2d(x.nchw().to(self.dt), wk, None, stride, pad)
+        zz = fuse.z.nhwc().to(self.dt)
+        keep = (zz * fuse.scale + fuse.shift) > 0
+        self._store(y, out * keep.permute(0, 3, 1, 2))
+        v = y.nhwc().to(self.dt)
+        return torch.stack([v.sum((0, 1, 2)), (v * zz).sum((0, 1, 2))]).unsqueeze(0)
 
     def convT_fwd(self, x: Act, wf, Cout, y: Act, bias=None):
         Cin = x.C

@@ -354,6 +354,52 @@ def test_maxpool_bwd_fused_bn_stats():
     assert torch.allclose(ps[1], (v * z.buf.double()).sum(0), rtol=1e-4, atol=1e-3)
 
 
+def test_maxpool_bwd_add_fused_bn_stats():
+    """UNet encoder output: pool backward + skip-concat gradient slice + ReLU mask + BN partials."""
+    nb, rb = _be()
+    N, H, W, C, CAT = 2, 16, 16, 64, 192
+    z, zr = _act(N, H, W, C)
+    sc, sh = torch.rand(C, device=DEV) + 0.5, torch.randn(C, device=DEV) * 0.3
+    y = _empty(N, H, W, C)
+    nb.bn_apply(z, sc, sh, None, True, y)
+    p = _empty(N, H // 2, W // 2, C)
+    idx = nb.maxpool_fwd(y, 2, 2, 0, p)
+    dy, _ = _act(N, H // 2, W // 2, C)
+    cat, _ = _act(N, H, W, CAT)
+    add = cat.slice(CAT - C, C)
+    dx = _empty(N, H, W, C)
+    part = nb.maxpool_bwd(dy, idx, y, 2, 2, 0, dx, add=add, fuse=BwdFuse(None, z, None, sc, sh))
+    plain = _empty(N, H, W, C)
+    nb.maxpool_bwd(dy, idx, y, 2, 2, 0, plain, add=add)
+    keep = z.buf.float() * sc + sh > 0
+    torch.cuda.synchronize()
+    assert torch.equal(dx.buf.float(), torch.where(keep, plain.buf.float(), torch.zeros_like(keep, dtype=torch.float32)))
+    ps, v = part.double().sum(0), dx.buf.double()
+    assert torch.allclose(ps[0], v.sum(0), rtol=1e-4, atol=1e-3)
+    assert torch.allclose(ps[1], (v * z.buf.double()).sum(0), rtol=1e-4, atol=1e-3)
+
+
+def test_conv_fwd_bnbwd():
+    """ConvTranspose data-gradient (2x2/s2 conv) producing the gradient of a BN+ReLU output: masked
+    store + BN-backward partials in the GEMM epilogue == plain conv, then mask, then sums."""
+    nb, rb = _be()
+    N, H, W, Cin, K = 2, 16, 16, 128, 64
+    x, _ = _act(N, H, W, Cin)
+    w = (torch.randn(K, 2, 2, Cin, device=DEV) * 0.05).to(torch.bfloat16)
+    z, _ = _act(N, H // 2, W // 2, K)
+    sc, sh = torch.rand(K, device=DEV) + 0.5, torch.randn(K, device=DEV) * 0.3
+    y = _empty(N, H // 2, W // 2, K)
+    part = nb.conv_fwd_bnbwd(x, w, K, 2, 2, 2, 0, y, BwdFuse(None, z, None, sc, sh))
+    plain = _empty(N, H // 2, W // 2, K)
+    nb.conv_fwd(x, w, K, 2, 2, 2, 0, plain)
+    keep = z.buf.float() * sc + sh > 0
+    torch.cuda.synchronize()
+    assert torch.equal(y.buf.float(), torch.where(keep, plain.buf.float(), torch.zeros_like(keep, dtype=torch.float32)))
+    ps, v = part.double().sum(0), y.buf.double()
+    assert torch.allclose(ps[0], v.sum(0), rtol=1e-4, atol=1e-3)
+    assert torch.allclose(ps[1], (v * z.buf.double()).sum(0), rtol=1e-4, atol=1e-3)
+
+
 def test_losses_eval_optim():
     nb, rb = _be()
     logits = torch.randn(64, 1000, device=DEV)
