@@ -3,7 +3,8 @@
 Flags keep the reference names and defaults: --num_epochs, --batch_size (per
 process), --learning_rate, --random_seed, --model_dir, --model_filename, --resume.  Non-breaking
 additions: --arch, --num_classes, --synthetic, --data_root, --image_size, --backend, --device,
---bucket_mb, --workers, --eval_every, --steps_per_epoch, --precision, --graph, --benchmark_steps.
+--bucket_mb, --workers, --eval_every, --steps_per_epoch, --precision, --graph, --data_on_device,
+--benchmark_steps.
 
 Deliberate fixes of reference quirks (SURVEY.md §7.3): the sampler's epoch is advanced every epoch;
 evaluation runs on the unwrapped module (no stray rank-0-only collective, K8) with a non-augmenting
@@ -22,7 +23,7 @@ import torch
 from torch.utils.data import DataLoader
 
 from .. import parallel
-from ..data import CIFAR10, CifarTransform, DistributedSampler, SyntheticImages
+from ..data import CIFAR10, CifarTransform, DeviceBatches, DeviceImageDataset, DistributedSampler, SyntheticImages
 from ..models import ARCHS
 from ..ops import CrossEntropyLoss, top1_correct
 from ..optim import SGD
@@ -59,6 +60,9 @@ def build_argparser(variant: str = "main") -> argparse.ArgumentParser:
     p.add_argument("--precision", default="bf16", choices=["bf16", "fp32"],
                    help="bf16: native gfx950 kernels; fp32: the same schedules on fp32 torch ops")
     p.add_argument("--graph", action="store_true", help="replay each training step from a captured hipGraph")
+    p.add_argument("--data_on_device", default="auto", choices=["auto", "0", "1"],
+                   help="keep CIFAR-10 resident in GPU memory and build each augmented batch with one kernel "
+                        "(data/device.py); auto = on for GPU training on real data")
     p.add_argument("--benchmark_steps", type=int, default=0,
                    help="time this many steps on a synthetic device batch, print images/sec and exit")
     return p
@@ -100,27 +104,38 @@ def run(args) -> dict:
     if args.resume:
         load_checkpoint(ddp, model_filepath, map_location=device)
 
+    # the training step reads its batch from fixed tensors so that it can be captured (--graph)
+    x_static = torch.empty((args.batch_size, 3, args.image_size, args.image_size) if args.synthetic else
+                           (args.batch_size, 3, 32, 32), device=device)
+    y_static = torch.zeros(args.batch_size, dtype=torch.int64, device=device)
+    on_device = (args.data_on_device == "1" or
+                 (args.data_on_device == "auto" and device.type == "cuda" and not args.synthetic))
+    test_bs = args.test_batch_size or args.batch_size
     if args.synthetic:
         shape = (3, args.image_size, args.image_size)
         train_set = SyntheticImages(args.synthetic_size, shape, args.num_classes, seed=1)
         test_set = SyntheticImages(max(64, args.synthetic_size // 8), shape, args.num_classes, seed=2)
+    elif on_device:
+        # the whole dataset in HBM; one kernel per batch does gather + crop/flip + normalize
+        train_set = DeviceImageDataset.cifar10(args.data_root, True, device, seed=args.random_seed)
+        test_set = DeviceImageDataset.cifar10(args.data_root, False, device, augment=False)
     else:
         # download=False semantics: the data must already be under data_root (see download.py)
         train_set = CIFAR10(args.data_root, train=True, transform=CifarTransform(True), seed=args.random_seed + rank)
         test_set = CIFAR10(args.data_root, train=False, transform=CifarTransform(False))
     sampler = DistributedSampler(train_set, seed=0)
-    pin = device.type == "cuda"
-    train_loader = DataLoader(train_set, batch_size=args.batch_size, sampler=sampler, num_workers=args.workers,
-                              pin_memory=pin, persistent_workers=args.workers > 0)
-    test_loader = DataLoader(test_set, batch_size=args.test_batch_size or args.batch_size, shuffle=False,
-                             num_workers=args.workers, pin_memory=pin)
+    if on_device and not args.synthetic:
+        train_loader = DeviceBatches(train_set, args.batch_size, sampler,
+                                     out=(x_static, y_static) if args.graph else None)
+        test_loader = DeviceBatches(test_set, test_bs)
+    else:
+        pin = device.type == "cuda"
+        train_loader = DataLoader(train_set, batch_size=args.batch_size, sampler=sampler, num_workers=args.workers,
+                                  pin_memory=pin, persistent_workers=args.workers > 0)
+        test_loader = DataLoader(test_set, batch_size=test_bs, shuffle=False, num_workers=args.workers,
+                                 pin_memory=pin)
     criterion = CrossEntropyLoss()
     optimizer = SGD(model.parameters(), lr=args.learning_rate, momentum=0.9, weight_decay=1e-5)
-
-    # the training step reads its batch from fixed tensors so that it can be captured (--graph)
-    x_static = torch.empty((args.batch_size, 3, args.image_size, args.image_size) if args.synthetic else
-                           (args.batch_size, 3, 32, 32), device=device)
-    y_static = torch.zeros(args.batch_size, dtype=torch.int64, device=device)
 
     def train_step(x, y):
         optimizer.zero_grad()
@@ -173,6 +188,8 @@ def run(args) -> dict:
             history["loss"].append(mean_loss)
             history["images_per_sec"].append(nb * args.batch_size * world / dt)
             print("Local Rank: {}, Epoch: {}, Loss: {}".format(local_rank, epoch, mean_loss))
+            if rank == 0:
+                print(f"Epoch {epoch} throughput: {history['images_per_sec'][-1]:.1f} images/sec ({nb} steps)")
             if not args.eval_before_train and epoch % args.eval_every == 0 and rank == 0:
                 eval_and_save(epoch)
             print(f"Epoch {epoch} completed")

@@ -27,7 +27,7 @@ from torch.utils.data import DataLoader
 from tqdm import tqdm
 
 from .. import parallel
-from ..data import CarvanaDataset, DistributedSampler, SyntheticMasks
+from ..data import CarvanaDataset, DeviceBatches, DeviceCachedDataset, DistributedSampler, SyntheticMasks
 from ..models import UNet
 from ..ops import BCEWithLogitsLoss, dice_per_sample
 from ..optim import Adam, clip_grad_norm_
@@ -56,6 +56,9 @@ def build_argparser() -> argparse.ArgumentParser:
     p.add_argument("--max_norm", type=float, default=1.0)
     p.add_argument("--steps_per_epoch", type=int, default=0)
     p.add_argument("--workers", type=int, default=max(1, (os.cpu_count() or 2) // 2))
+    p.add_argument("--data_on_device", default="auto", choices=["auto", "0", "1"],
+                   help="decode the dataset once and keep it in GPU memory; batches are device-side gathers "
+                        "(auto: on for GPU runs when it needs < 1/4 of the GPU memory)")
     p.add_argument("--log_dir", default="logs")
     p.add_argument("--eval_every", type=int, default=10)
     p.add_argument("--bucket_mb", type=float, default=None)
@@ -120,9 +123,26 @@ def build_data_loaders(args, device):
     # same split on every rank (seeded generator rather than the global RNG)
     train_ds, test_ds = torch.utils.data.random_split(ds, [train_size, test_size],
                                                       generator=torch.Generator().manual_seed(args.random_seed))
+    if _use_device_data(args, device, ds):
+        # the reference dataset is deterministic (no augmentation): decode / resize once, keep the
+        # tensors in HBM, and serve every batch as an index gather on the device
+        train_c, test_c = DeviceCachedDataset(train_ds, device), DeviceCachedDataset(test_ds, device)
+        sampler = DistributedSampler(train_c)
+        return DeviceBatches(train_c, args.batch_size, sampler), DeviceBatches(test_c, args.batch_size), sampler
     kw = dict(batch_size=args.batch_size, num_workers=args.workers, pin_memory=device.type == "cuda")
     sampler = DistributedSampler(train_ds)
     return (DataLoader(train_ds, sampler=sampler, **kw), DataLoader(test_ds, shuffle=False, **kw), sampler)
+
+
+def _use_device_data(args, device, ds) -> bool:
+    """--data_on_device auto: on for GPU runs whose decoded dataset needs < 1/4 of the GPU memory."""
+    if args.data_on_device != "auto":
+        return args.data_on_device == "1"
+    if device.type != "cuda":
+        return False
+    s = ds[0]
+    per = sum(torch.as_tensor(v).numel() * 4 for v in s.values())
+    return per * len(ds) < torch.cuda.get_device_properties(device).total_memory // 4
 
 
 def benchmark(args, train_step, captured, x, y, comm, device) -> dict:

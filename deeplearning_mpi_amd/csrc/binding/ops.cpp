@@ -600,6 +600,24 @@ void scale_(at::Tensor x, const at::Tensor& coef) {
   check(dlmpi_scale_f32(ptr<float>(x), x.numel(), ptr<float>(coef), cur_stream()), "scale");
 }
 
+// --------------------------------- device-resident input pipeline ---------------------------
+void image_batch(const at::Tensor& data, const at::Tensor& labels, const at::Tensor& idx, int H, int W, int C,
+                 int pad, bool augment, int64_t seed, int64_t epoch, std::vector<double> mean, std::vector<double> sd,
+                 at::Tensor out, const c10::optional<at::Tensor>& out_labels) {
+  require_gpu(data, "data");
+  if (mean.size() != (size_t)C || sd.size() != (size_t)C) throw std::runtime_error("image_batch: mean/std per channel");
+  if (data.scalar_type() != at::kByte || idx.scalar_type() != at::kLong || out.scalar_type() != at::kFloat)
+    throw std::runtime_error("image_batch: uint8 data, int64 indices, fp32 output");
+  float m3[3] = {0.f, 0.f, 0.f}, s3[3] = {1.f, 1.f, 1.f};
+  for (int c = 0; c < C; ++c) { m3[c] = (float)mean[c]; s3[c] = (float)sd[c]; }
+  const int B = (int)idx.numel();
+  if (out.numel() != (int64_t)B * C * H * W) throw std::runtime_error("image_batch: output size");
+  check(dlmpi_image_batch(ptr<uint8_t>(data), ptr<int64_t>(labels), ptr<int64_t>(idx), B, H, W, C, pad, augment ? 1 : 0,
+                          (uint32_t)seed, (uint32_t)epoch, m3, s3, ptr<float>(out), optr<int64_t>(out_labels),
+                          cur_stream()),
+        "image_batch");
+}
+
 void register_ops(pybind11::module& m) {
   namespace py = pybind11;
   m.def("conv2d_fwd", &conv2d_fwd);
@@ -624,6 +642,7 @@ void register_ops(pybind11::module& m) {
   m.def("avgpool_bwd", &avgpool_bwd);
   m.def("nchw_to_nhwc", &nchw_to_nhwc);
   m.def("s2d_nchw", &s2d_nchw);
+  m.def("image_batch", &image_batch);
   m.def("upsample2x_fwd", &upsample2x_fwd);
   m.def("upsample2x_bwd", &upsample2x_bwd);
   m.def("cast_weights", &cast_weights);

@@ -206,6 +206,11 @@ hipError_t dlmpi_clip_coef(const float* partial, int nblk, float max_norm, float
                            hipStream_t s);
 hipError_t dlmpi_scale_f32(float* x, int64_t n, const float* coef, hipStream_t s);
 
+// device-resident input pipeline: out[b] = normalize(augment(data[idx[b]])), [B][C][H][W] fp32 (C <= 3)
+hipError_t dlmpi_image_batch(const uint8_t* data, const int64_t* labels, const int64_t* idx, int B, int H, int W,
+                             int C, int pad, int augment, uint32_t seed, uint32_t epoch, const float* mean3,
+                             const float* std3, float* out, int64_t* out_labels, hipStream_t s);
+
 // fault injection: keep stream s busy for `ms` milliseconds (bounded; tests of the watchdog)
 hipError_t dlmpi_delay(double ms, hipStream_t s);
 

@@ -38,7 +38,8 @@ class CapturedStep:
     def set_inputs(self, *tensors):
         """Copy a new batch into the captured input tensors (same shapes / dtypes)."""
         for dst, src in zip(self.inputs, tensors):
-            dst.copy_(src, non_blocking=True)
+            if dst.data_ptr() != src.data_ptr():   # device pipelines may write the inputs in place
+                dst.copy_(src, non_blocking=True)
 
     def recapture(self):
         self.graph = None
