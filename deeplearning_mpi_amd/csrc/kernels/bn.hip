@@ -473,17 +473,31 @@ extern "C" int dlmpi_colsum_ws_doubles(int T, int C) { return colsum_slices(T) *
 
 // Self-resetting per-channel-group tickets of colsum_fin_kernel, one array per device, zeroed once
 // (the first use happens before any hipGraph capture: the warm-up steps run eagerly).
-static int* fin_tickets() {
-  static int* t[64] = {};
+// Last-arriver tickets of the fused finalize: one self-resetting array per device and stream
+// ROLE.  Launches on one stream are serialised, so they can share an array; the engine's
+// weight-gradient side stream (models/engine.py:grad_side) runs colsum_fin launches (bias sums)
+// concurrently with the main stream's BN finalizes, so it gets its own.  (Per stream role rather
+// than per stream: a graph capture runs the main role on a fresh capture stream, where no
+// allocation may happen.)
+static int* g_tickets[64] = {};
+static hipStream_t g_side_stream[64] = {};
+
+static int* tickets_for_device(int dev) {
+  if (!g_tickets[dev]) {
+    int* p = nullptr;
+    if (hipMalloc(&p, 2 * 4096 * sizeof(int)) != hipSuccess) return nullptr;
+    if (hipMemset(p, 0, 2 * 4096 * sizeof(int)) != hipSuccess) return nullptr;
+    g_tickets[dev] = p;
+  }
+  return g_tickets[dev];
+}
+
+static int* fin_tickets(hipStream_t s) {
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
-  if (!t[dev]) {
-    int* p = nullptr;
-    if (hipMalloc(&p, 4096 * sizeof(int)) != hipSuccess) return nullptr;
-    if (hipMemset(p, 0, 4096 * sizeof(int)) != hipSuccess) return nullptr;
-    t[dev] = p;
-  }
-  return t[dev];
+  int* t = tickets_for_device(dev);
+  if (!t) return nullptr;
+  return s != nullptr && s == g_side_stream[dev] ? t + 4096 : t;
 }
 
 static bool fused_finalize() {
@@ -498,7 +512,7 @@ static hipError_t colsum_finalize(const float* partial, int T, int C, int ns, in
                                   hipStream_t s) {
   const int S = colsum_slices(T);
   const int G = (C + 63) / 64;
-  int* tk = fused_finalize() && G <= 4096 ? fin_tickets() : nullptr;
+  int* tk = fused_finalize() && G <= 4096 ? fin_tickets(s) : nullptr;
   if (tk) {
     hipLaunchKernelGGL(colsum_fin_kernel, dim3(G, S), dim3(256), 0, s, partial, T, C, ns, k2, ws, tk, f);
   } else {
@@ -506,6 +520,15 @@ static hipError_t colsum_finalize(const float* partial, int T, int C, int ns, in
     hipLaunchKernelGGL(finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, s, ws, S, C, f);
   }
   return hipGetLastError();
+}
+
+extern "C" hipError_t dlmpi_set_side_stream(hipStream_t s) {
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return e;
+  if (dev < 0 || dev >= 64 || !tickets_for_device(dev)) return hipErrorInvalidValue;   // allocate outside any capture
+  g_side_stream[dev] = s;
+  return hipSuccess;
 }
 
 extern "C" hipError_t dlmpi_bn_finalize(const float* partial, int ntiles, int C, double count, const float* gamma,

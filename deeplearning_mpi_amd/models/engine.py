@@ -19,6 +19,7 @@ One ``torch.autograd.Function`` bridges the engine to autograd (loss.backward() 
 """
 from __future__ import annotations
 
+import contextlib
 import os
 from typing import NamedTuple, Optional
 
@@ -29,6 +30,28 @@ from ..ops.act import Act, padc
 from ..ops.backend import make_backend
 from ..utils.arena import ParamArena
 from ..utils.profiler import range as trace_range
+
+
+@contextlib.contextmanager
+def grad_side(be, *tensors):
+    """Run parameter-gradient work -- weight-gradient GEMMs, their split reductions, bias sums and
+    the DDP ``ready`` announcements that launch bucket all-reduces -- on the backend's side stream,
+    ordered after everything issued so far on the current stream.  Only the data-gradient chain
+    (dgrad -> BN backward -> dgrad ...) stays on the main stream, so weight gradients fill the
+    GPU beside it (tails of under-filled grids, the small BN finalize launches).  Every ``ready``
+    is issued here, so a bucket's all-reduce always fences on the side stream, which has waited
+    for the main stream's BN-parameter gradients.  ``tensors``: buffers read on the side stream
+    (kept alive for it in the caching allocator).  The engine backward joins the side stream
+    before the optimizer (``_EngineFn.backward``)."""
+    side = getattr(be, "side_stream", None)
+    if side is None:
+        yield
+        return
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        yield
+    for t in tensors:
+        t.record_stream(side)
 
 
 class BwdFuse(NamedTuple):
@@ -177,25 +200,29 @@ class ConvUnit:
             be.bn_bwd(dy, mask, z, mean, invstd, bn.weight.data if bn.affine else None,
                       ar.grad_flat(bn.weight) if bn.affine else None, ar.grad_flat(bn.bias) if bn.affine else None,
                       dz, dyr_out, pre=pre, k2=k2)
-            if bn.affine:
-                ar.ready(bn.weight, bn.bias)
-            if self.bias is not None:
-                # d(bias) of a conv followed by training-mode BN is exactly zero (BN removes the mean)
-                ar.ready(self.bias)
+            with grad_side(be, dz.buf, x.buf):
+                if bn.affine:
+                    ar.ready(bn.weight, bn.bias)
+                if self.bias is not None:
+                    # d(bias) of a conv followed by training-mode BN is exactly zero (BN removes the mean)
+                    ar.ready(self.bias)
+                self._wgrad(be, dz, x)
+                ar.ready(self.conv.weight)
         else:
             x, y = ctx
             assert not self.relu, "ReLU without BN is not used by the engine models"
             dz = dy
-            if self.bias is not None:
-                if self.Kp == self.K:
-                    be.channel_sum(dz, ar.grad_flat(self.bias))
-                else:
-                    tmp = torch.zeros(self.Kp, dtype=be.dt, device=dz.device)
-                    be.channel_sum(dz, tmp)
-                    ar.grad_flat(self.bias).add_(tmp[:self.K])
-                ar.ready(self.bias)
-        self._wgrad(be, dz, x)
-        ar.ready(self.conv.weight)
+            with grad_side(be, dz.buf, x.buf):
+                if self.bias is not None:
+                    if self.Kp == self.K:
+                        be.channel_sum(dz, ar.grad_flat(self.bias))
+                    else:
+                        tmp = torch.zeros(self.Kp, dtype=be.dt, device=dz.device)
+                        be.channel_sum(dz, tmp)
+                        ar.grad_flat(self.bias).add_(tmp[:self.K])
+                    ar.ready(self.bias)
+                self._wgrad(be, dz, x)
+                ar.ready(self.conv.weight)
         if not need_dx:
             return None
         dx = Act.empty(x.N, x.H, x.W, self.Cp, be.act_dtype, x.device)
@@ -305,12 +332,13 @@ class ConvTUnit:
         """fuse_next (BwdFuse of the BN+ReLU unit that produced x): the data gradient is written
         ReLU-masked with that BN's backward partials -> returns (dx, partials)."""
         ar = self.arena
-        if self.m.bias is not None:
-            be.channel_sum(dout, ar.grad_flat(self.m.bias))
-            ar.ready(self.m.bias)
-        # dW[ci][i][j][co] = sum_pix x[pix][ci] * dout[2p+i, 2q+j][co]: the wgrad of a stride-2 2x2 conv
-        be.conv_wgrad(x, dout, 2, 2, 2, 0, ar.grad_flat(self.m.weight), self.Cout, self.Cin)
-        ar.ready(self.m.weight)
+        with grad_side(be, dout.buf, x.buf):
+            if self.m.bias is not None:
+                be.channel_sum(dout, ar.grad_flat(self.m.bias))
+                ar.ready(self.m.bias)
+            # dW[ci][i][j][co] = sum_pix x[pix][ci] * dout[2p+i, 2q+j][co]: the wgrad of a 2x2/s2 conv
+            be.conv_wgrad(x, dout, 2, 2, 2, 0, ar.grad_flat(self.m.weight), self.Cout, self.Cin)
+            ar.ready(self.m.weight)
         dx = Act.empty(x.N, x.H, x.W, self.Cip, be.act_dtype, x.device)
         if fuse_next is not None:
             return dx, be.conv_fwd_bnbwd(dout, ar.get_compute(self.h_dg), self.Cip, 2, 2, 2, 0, dx, fuse_next)
@@ -337,6 +365,9 @@ class _EngineFn(torch.autograd.Function):
         ctx.state = None
         with trace_range(f"dlmpi.backward[{type(mod).__name__}]"):
             mod._engine_backward(state, gout)
+            side = getattr(mod._be, "side_stream", None)
+            if side is not None:   # every parameter gradient is final before the optimizer runs
+                torch.cuda.current_stream().wait_stream(side)
         with trace_range("dlmpi.ddp_finalize"):
             mod._arena.end_backward()
         return None, None, None

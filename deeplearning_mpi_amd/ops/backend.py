@@ -9,6 +9,7 @@ Both expose the same methods; the engine (models/*) is written once against this
 """
 from __future__ import annotations
 
+import os
 import struct
 
 import torch
@@ -18,6 +19,21 @@ from .act import Act
 
 
 # --------------------------------------------------------------------------------------------
+_SIDE_STREAMS = {}
+
+
+def _side_stream(device, C):
+    """One weight-gradient side stream per device, shared by every backend instance (the kernels
+    keep one last-arriver ticket array for it: bn.hip:fin_tickets)."""
+    idx = device.index if device.index is not None else torch.cuda.current_device()
+    st = _SIDE_STREAMS.get(idx)
+    if st is None:
+        st = _SIDE_STREAMS[idx] = torch.cuda.Stream(device=idx)
+        with torch.cuda.device(idx):
+            C.set_side_stream(st.cuda_stream)
+    return st
+
+
 class NativeBackend:
     name = "native"
     act_dtype = torch.bfloat16
@@ -29,6 +45,11 @@ class NativeBackend:
         self.C = native()
         self.device = torch.device(device)
         self._cast_cache = {}
+        # parameter-gradient work (weight-gradient GEMMs + split reductions, DDP bucket launches)
+        # runs on this side stream, off the data-gradient critical path (models/engine.py:grad_side);
+        # DLMPI_WGRAD_STREAM=0 keeps everything on the current stream
+        self.side_stream = _side_stream(self.device, self.C) if os.environ.get("DLMPI_WGRAD_STREAM", "1") != "0" \
+            else None
 
     # ---------------- conv family ----------------
     def conv_mtiles(self, N, H, W, C, K, R, S, stride, pad):
