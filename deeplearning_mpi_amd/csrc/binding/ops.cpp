@@ -627,7 +627,9 @@ void register_ops(pybind11::module& m) {
   m.def("convT2x2_fwd", &convT2x2_fwd);
   m.def("conv2d_wgrad", &conv2d_wgrad);
   m.def("bn_finalize", &bn_finalize);
-  m.def("set_side_stream", [](int64_t h) { check(dlmpi_set_side_stream(reinterpret_cast<hipStream_t>(h)), "set_side_stream"); });
+  m.def("set_aux_stream", [](int64_t h, int role) {
+    check(dlmpi_set_aux_stream(reinterpret_cast<hipStream_t>(h), role), "set_aux_stream");
+  });
   m.def("reduce_blocks", &reduce_blocks);
   m.def("bn_stats", &bn_stats);
   m.def("bn_apply", &bn_apply);

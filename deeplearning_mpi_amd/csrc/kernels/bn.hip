@@ -474,19 +474,20 @@ extern "C" int dlmpi_colsum_ws_doubles(int T, int C) { return colsum_slices(T) *
 // Self-resetting per-channel-group tickets of colsum_fin_kernel, one array per device, zeroed once
 // (the first use happens before any hipGraph capture: the warm-up steps run eagerly).
 // Last-arriver tickets of the fused finalize: one self-resetting array per device and stream
-// ROLE.  Launches on one stream are serialised, so they can share an array; the engine's
-// weight-gradient side stream (models/engine.py:grad_side) runs colsum_fin launches (bias sums)
-// concurrently with the main stream's BN finalizes, so it gets its own.  (Per stream role rather
-// than per stream: a graph capture runs the main role on a fresh capture stream, where no
-// allocation may happen.)
+// ROLE.  Launches on one stream are serialised, so they can share an array; the engine's auxiliary
+// streams (models/engine.py: the weight-gradient side stream and the residual-branch stream) run
+// colsum_fin launches concurrently with the main stream's, so each role gets its own array.
+// (Per role rather than per stream: a graph capture runs the main role on a fresh capture stream,
+// where no allocation may happen.)
+constexpr int kTicketRoles = 4;   // 0 = main (any unregistered stream), 1..3 = registered aux streams
 static int* g_tickets[64] = {};
-static hipStream_t g_side_stream[64] = {};
+static hipStream_t g_aux_stream[64][kTicketRoles] = {};
 
 static int* tickets_for_device(int dev) {
   if (!g_tickets[dev]) {
     int* p = nullptr;
-    if (hipMalloc(&p, 2 * 4096 * sizeof(int)) != hipSuccess) return nullptr;
-    if (hipMemset(p, 0, 2 * 4096 * sizeof(int)) != hipSuccess) return nullptr;
+    if (hipMalloc(&p, kTicketRoles * 4096 * sizeof(int)) != hipSuccess) return nullptr;
+    if (hipMemset(p, 0, kTicketRoles * 4096 * sizeof(int)) != hipSuccess) return nullptr;
     g_tickets[dev] = p;
   }
   return g_tickets[dev];
@@ -497,7 +498,9 @@ static int* fin_tickets(hipStream_t s) {
   if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
   int* t = tickets_for_device(dev);
   if (!t) return nullptr;
-  return s != nullptr && s == g_side_stream[dev] ? t + 4096 : t;
+  for (int r = 1; r < kTicketRoles; ++r)
+    if (s != nullptr && s == g_aux_stream[dev][r]) return t + r * 4096;
+  return t;
 }
 
 static bool fused_finalize() {
@@ -522,12 +525,13 @@ static hipError_t colsum_finalize(const float* partial, int T, int C, int ns, in
   return hipGetLastError();
 }
 
-extern "C" hipError_t dlmpi_set_side_stream(hipStream_t s) {
+extern "C" hipError_t dlmpi_set_aux_stream(hipStream_t s, int role) {
   int dev = 0;
   hipError_t e = hipGetDevice(&dev);
   if (e != hipSuccess) return e;
-  if (dev < 0 || dev >= 64 || !tickets_for_device(dev)) return hipErrorInvalidValue;   // allocate outside any capture
-  g_side_stream[dev] = s;
+  if (dev < 0 || dev >= 64 || role < 1 || role >= kTicketRoles || !tickets_for_device(dev))
+    return hipErrorInvalidValue;   // (allocates outside any capture)
+  g_aux_stream[dev][role] = s;
   return hipSuccess;
 }
 

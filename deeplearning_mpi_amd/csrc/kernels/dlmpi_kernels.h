@@ -118,8 +118,8 @@ hipError_t dlmpi_bn_finalize(const float* partial, int ntiles, int C, double cou
                              float eps, float* scale, float* shift, float* save_mean, float* save_invstd,
                              double* ws, hipStream_t s);
 int dlmpi_colsum_ws_doubles(int T, int C);
-// register the weight-gradient side stream of the current device (own last-arriver ticket array)
-hipError_t dlmpi_set_side_stream(hipStream_t s);
+// register an auxiliary stream (role 1..3) of the current device: own last-arriver ticket array
+hipError_t dlmpi_set_aux_stream(hipStream_t s, int role);
 hipError_t dlmpi_bn_stats(const uint16_t* x, int64_t M, int C, int ldx, int xoff, float* partial, int nblk,
                           hipStream_t s);
 // mbits (optional): [M][C/8] bytes, bit e of byte (row, g) = y[row][8g + e] > 0 (ReLU mask for backward)

@@ -54,6 +54,21 @@ def grad_side(be, *tensors):
         t.record_stream(side)
 
 
+def record_on(stream, *objs):
+    """Mark every tensor (or Act buffer) inside ``objs`` (nested tuples / lists allowed) as used on
+    ``stream``, so the caching allocator does not recycle it before that stream's work is done."""
+    for o in objs:
+        if o is None:
+            continue
+        if isinstance(o, torch.Tensor):
+            if o.is_cuda:
+                o.record_stream(stream)
+        elif hasattr(o, "buf") and isinstance(getattr(o, "buf"), torch.Tensor):
+            record_on(stream, o.buf)
+        elif isinstance(o, (tuple, list)):
+            record_on(stream, *o)
+
+
 class BwdFuse(NamedTuple):
     """What a data-gradient GEMM needs to produce the gradient of a BN+ReLU output fused: the ReLU
     mask (``mask`` = the saved output y, or -- for BN+ReLU without a residual -- recomputed from the

@@ -19,7 +19,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from ..ops.act import Act, padc
-from .engine import BwdFuse, ConvUnit, EngineModule, S2DConvUnit
+from .engine import BwdFuse, ConvUnit, EngineModule, S2DConvUnit, record_on
 
 
 def conv3x3(i, o, stride=1):
@@ -92,12 +92,24 @@ class _BlockExec:
         self.u, self.ud = units, ds
 
     def fwd(self, be, x: Act, train, save):
+        """The downsample branch (1x1 conv + BN) depends only on the block input: with a branch
+        stream it runs beside conv1 -> conv2 and joins before the residual add of conv3's BN."""
         ctxs = []
+        br = getattr(be, "branch_stream", None) if self.ud is not None else None
+        if br is not None:
+            main = torch.cuda.current_stream()
+            br.wait_stream(main)
+            with torch.cuda.stream(br):
+                idn, cd = self.ud.fwd(be, x, train, save=save)
+            record_on(br, x)
         h = x
         for k, u in enumerate(self.u[:-1]):
             h, c = u.fwd(be, h, train, save=save)
             ctxs.append(c)
-        if self.ud is not None:
+        if br is not None:
+            main.wait_stream(br)
+            record_on(main, idn, cd)
+        elif self.ud is not None:
             idn, cd = self.ud.fwd(be, x, train, save=save)
         else:
             idn, cd = x, None
@@ -120,11 +132,26 @@ class _BlockExec:
         n = len(self.u)
         spec = lambda k: ConvUnit.fuse_spec(ctxs[k])   # noqa: E731
         if pre is not None:
+            # the masked dy is the identity-path gradient; the downsample BN reads row 2 of `pre`.
+            # With a branch stream the downsample backward (BN backward + 1x1 data gradient) runs
+            # beside the main branch and joins before conv1's data gradient adds it.
+            br = getattr(be, "branch_stream", None) if self.ud is not None else None
+            if br is not None:
+                main = torch.cuda.current_stream()
+                br.wait_stream(main)
+                with torch.cuda.stream(br):
+                    dres = self.ud.bwd(be, cd, dy, pre=pre, k2=2)
+                record_on(br, dy, pre)
             dh, part = self.u[-1].bwd(be, ctxs[-1], dy, pre=pre, k2=1, fuse_next=spec(n - 2))
             for k in range(n - 2, 0, -1):
                 dh, part = self.u[k].bwd(be, ctxs[k], dh, pre=part, fuse_next=spec(k - 1))
-            # the masked dy is the identity-path gradient; the downsample BN reads row 2 of `pre`
-            dres = self.ud.bwd(be, cd, dy, pre=pre, k2=2) if self.ud is not None else dy
+            if br is not None:
+                main.wait_stream(br)
+                record_on(main, dres)
+            elif self.ud is not None:
+                dres = self.ud.bwd(be, cd, dy, pre=pre, k2=2)
+            else:
+                dres = dy
             return self.u[0].bwd(be, ctxs[0], dh, dx_res=dres, pre=part, fuse_next=fuse_prev)
         if self.ud is None:
             dyr = Act.empty(dy.N, dy.H, dy.W, dy.C, be.act_dtype, dy.device)   # identity-path grad

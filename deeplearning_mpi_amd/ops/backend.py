@@ -19,18 +19,19 @@ from .act import Act
 
 
 # --------------------------------------------------------------------------------------------
-_SIDE_STREAMS = {}
+_AUX_STREAMS = {}
 
 
-def _side_stream(device, C):
-    """One weight-gradient side stream per device, shared by every backend instance (the kernels
-    keep one last-arriver ticket array for it: bn.hip:fin_tickets)."""
+def _aux_stream(device, C, role):
+    """Auxiliary streams, one per (device, role), shared by every backend instance: role 1 = the
+    weight-gradient side stream, role 2 = the residual-branch stream.  The kernels keep a separate
+    last-arriver ticket array per role (bn.hip:fin_tickets)."""
     idx = device.index if device.index is not None else torch.cuda.current_device()
-    st = _SIDE_STREAMS.get(idx)
+    st = _AUX_STREAMS.get((idx, role))
     if st is None:
-        st = _SIDE_STREAMS[idx] = torch.cuda.Stream(device=idx)
+        st = _AUX_STREAMS[(idx, role)] = torch.cuda.Stream(device=idx)
         with torch.cuda.device(idx):
-            C.set_side_stream(st.cuda_stream)
+            C.set_aux_stream(st.cuda_stream, role)
     return st
 
 
@@ -48,8 +49,12 @@ class NativeBackend:
         # parameter-gradient work (weight-gradient GEMMs + split reductions, DDP bucket launches)
         # runs on this side stream, off the data-gradient critical path (models/engine.py:grad_side);
         # DLMPI_WGRAD_STREAM=0 keeps everything on the current stream
-        self.side_stream = _side_stream(self.device, self.C) if os.environ.get("DLMPI_WGRAD_STREAM", "1") != "0" \
+        self.side_stream = _aux_stream(self.device, self.C, 1) if os.environ.get("DLMPI_WGRAD_STREAM", "1") != "0" \
             else None
+        # independent residual branches (the ResNet downsample conv + BN) run on this stream beside
+        # the main branch, forward and backward (models/resnet.py:_BlockExec); DLMPI_BRANCH_STREAM=0: off
+        self.branch_stream = _aux_stream(self.device, self.C, 2) \
+            if os.environ.get("DLMPI_BRANCH_STREAM", "1") != "0" else None
 
     # ---------------- conv family ----------------
     def conv_mtiles(self, N, H, W, C, K, R, S, stride, pad):
