@@ -250,7 +250,7 @@ c10::optional<at::Tensor> conv2d_dgrad(const at::Tensor& dy, int N, int P, int Q
                                        const c10::optional<at::Tensor>& z2, int ldz2, int z2off,
                                        const c10::optional<at::Tensor>& mscale,
                                        const c10::optional<at::Tensor>& mshift,
-                                       const c10::optional<at::Tensor>& mbits) {
+                                       const c10::optional<at::Tensor>& mbits, bool colsum) {
   require_gpu(dy, "dy");
   if (stride > 2) throw std::runtime_error("conv2d_dgrad: stride <= 2 supported");
   ConvArgs a{};
@@ -305,7 +305,9 @@ c10::optional<at::Tensor> conv2d_dgrad(const at::Tensor& dy, int N, int P, int Q
     }
   }
   c10::optional<at::Tensor> stats;
-  if (a.z) {
+  if (a.z || colsum) {
+    // colsum without BN fusion: per-tile {sum dx, sum dx^2} of the stored gradient (UNet: the
+    // column sums of the up-sampling slice are the ConvTranspose2d bias gradient)
     stats = at::empty({(int64_t)tiles, (int64_t)a.nstat, (int64_t)C}, dy.options().dtype(at::kFloat));
     a.stats = ptr<float>(*stats);
   }

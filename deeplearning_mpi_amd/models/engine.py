@@ -195,13 +195,15 @@ class ConvUnit:
         return BwdFuse(None, z, None, scale, shift)
 
     def bwd(self, be, ctx, dy: Act, need_dx=True, dx_res: Act = None, dyr_out: Act = None, ymask: Act = None,
-            use_own_mask=True, pre=None, k2=1, fuse_next=None):
+            use_own_mask=True, pre=None, k2=1, fuse_next=None, colsum=False):
         """Backward of the unit.
 
         pre:       BN-backward partials already produced by the dgrad epilogue that wrote ``dy``
                    (then ``dy`` is already ReLU-masked; row ``k2`` holds sum dy*z for this BN).
         fuse_next: (mask, z, z2) of the consumer of this unit's dx -- the dgrad epilogue masks dx and
                    emits that consumer's partials; returns (dx, partials) instead of dx.
+        colsum:    (without fuse_next) the dgrad epilogue also emits per-tile column sums of dx;
+                   returns (dx, partials [tiles][2][C]).
         """
         ar = self.arena
         bn = self.bn
@@ -242,8 +244,8 @@ class ConvUnit:
             return None
         dx = Act.empty(x.N, x.H, x.W, self.Cp, be.act_dtype, x.device)
         part = be.conv_dgrad(dz, ar.get_compute(self.h_dg), self.Cp, self.R, self.S, self.stride, self.pad, dx,
-                             res=dx_res, fuse=fuse_next)
-        return (dx, part) if fuse_next is not None else dx
+                             res=dx_res, fuse=fuse_next, colsum=colsum)
+        return (dx, part) if (fuse_next is not None or colsum) else dx
 
 
 class S2DConvUnit(ConvUnit):
@@ -343,13 +345,18 @@ class ConvTUnit:
                      self.m.bias.data if self.m.bias is not None else None)
         return x
 
-    def bwd(self, be, x: Act, dout: Act, fuse_next=None):
+    def bwd(self, be, x: Act, dout: Act, fuse_next=None, bias_part=None):
         """fuse_next (BwdFuse of the BN+ReLU unit that produced x): the data gradient is written
-        ReLU-masked with that BN's backward partials -> returns (dx, partials)."""
+        ReLU-masked with that BN's backward partials -> returns (dx, partials).  bias_part: per-tile
+        column sums of ``dout`` already produced by the GEMM that wrote it ([tiles][Cout] view);
+        the bias gradient is then their sum instead of another pass over ``dout``."""
         ar = self.arena
-        with grad_side(be, dout.buf, x.buf):
+        with grad_side(be, dout.buf, x.buf, bias_part):
             if self.m.bias is not None:
-                be.channel_sum(dout, ar.grad_flat(self.m.bias))
+                if bias_part is not None:
+                    ar.grad_flat(self.m.bias).add_(bias_part[:, :self.Cout].sum(0))
+                else:
+                    be.channel_sum(dout, ar.grad_flat(self.m.bias))
                 ar.ready(self.m.bias)
             # dW[ci][i][j][co] = sum_pix x[pix][ci] * dout[2p+i, 2q+j][co]: the wgrad of a 2x2/s2 conv
             be.conv_wgrad(x, dout, 2, 2, 2, 0, ar.grad_flat(self.m.weight), self.Cout, self.Cin)

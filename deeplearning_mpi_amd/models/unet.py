@@ -174,25 +174,30 @@ class UNet(EngineModule):
         def spec(ctx):
             return ConvUnit.fuse_spec(ctx) if fuse else None
 
-        def double_bwd(units, ca, cb, dy, pre=None, need_dx=True):
+        def double_bwd(units, ca, cb, dy, pre=None, need_dx=True, colsum=False):
             ua, ub = units
             out = ub.bwd(be, cb, dy, pre=pre, fuse_next=spec(ca))
             dt_, part = out if fuse else (out, None)
-            return ua.bwd(be, ca, dt_, pre=part, need_dx=need_dx)
+            return ua.bwd(be, ca, dt_, pre=part, need_dx=need_dx, colsum=colsum)
 
         dl = be.nchw_to_nhwc(gout, self.u_last.Kp)
         out = self.u_last.bwd(be, (cl[0], None), dl, fuse_next=spec(ctx_dec[0][2]))
         da, pre = out if fuse else (out, None)
         for k in range(4):                    # decoder, level 1 (last executed) first
             below, ca, cb = ctx_dec[k]
-            dcat = double_bwd(self.dec[k], ca, cb, da, pre=pre)
+            up_t = self.upT[k]
+            # with a ConvTranspose2d up-sampling, the concat-gradient GEMM also emits its column sums:
+            # those of the up-sampling slice are the ConvTranspose bias gradient (no extra pass)
+            out = double_bwd(self.dec[k], ca, cb, da, pre=pre, colsum=up_t is not None and up_t.m.bias is not None)
+            dcat, cpart = out if isinstance(out, tuple) else (out, None)
             pre = None
             dup = dcat.slice(0, self.up_ch[k])
-            if self.upT[k] is not None:
+            if up_t is not None:
                 # the ConvTranspose data-gradient is the gradient of the BN+ReLU output below it
                 # (the next decoder level's, or the bottleneck's, second conv): masked + partials
                 below_ctx = ctx_dec[k + 1][2] if k < 3 else cbb
-                out = self.upT[k].bwd(be, below, dup, fuse_next=spec(below_ctx))
+                out = up_t.bwd(be, below, dup, fuse_next=spec(below_ctx),
+                               bias_part=cpart[:, 0] if cpart is not None else None)
                 da, pre = out if fuse else (out, None)
             else:
                 da = Act.empty(below.N, below.H, below.W, below.C, be.act_dtype, below.device)

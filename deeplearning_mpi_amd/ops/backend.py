@@ -73,17 +73,19 @@ class NativeBackend:
         return self.C.conv2d_fwd_bnbwd(x.buf, x.N, x.H, x.W, x.C, x.ld, x.off, w, K, R, S, stride, pad, y.buf, y.ld,
                                        y.off, z.buf, z.ld, z.off, fuse.scale, fuse.shift)
 
-    def conv_dgrad(self, dy: Act, wT, C, R, S, stride, pad, dx: Act, res: Act = None, fuse=None):
+    def conv_dgrad(self, dy: Act, wT, C, R, S, stride, pad, dx: Act, res: Act = None, fuse=None, colsum=False):
         """fuse = BwdFuse(mask, z, z2, scale, shift): dx is the gradient of relu(BN(z) [+ BN2(z2)]);
         the epilogue applies the ReLU mask (y > 0, or z*scale + shift > 0 without a residual) and
-        returns BN-backward partials [tiles][2|3][C]."""
+        returns BN-backward partials [tiles][2|3][C].  colsum (no fuse): returns per-tile
+        {sum dx, sum dx^2} [tiles][2][C] of the stored dx instead."""
         m, z, z2, sc, sh, mb = fuse if fuse is not None else (None, None, None, None, None, None)
 
         def t(a):
             return (a.buf, a.ld, a.off) if a is not None else (None, 0, 0)
 
         return self.C.conv2d_dgrad(dy.buf, dy.N, dy.H, dy.W, dy.C, dy.ld, dy.off, wT, C, R, S, stride, pad, dx.H,
-                                   dx.W, dx.buf, dx.ld, dx.off, *t(res), *t(m), *t(z), *t(z2), sc, sh, mb)
+                                   dx.W, dx.buf, dx.ld, dx.off, *t(res), *t(m), *t(z), *t(z2), sc, sh, mb,
+                                   bool(colsum and fuse is None))
 
     def convT_fwd(self, x: Act, wf, Cout, y: Act, bias=None):
         self.C.convT2x2_fwd(x.buf, x.N, x.H, x.W, x.C, x.ld, x.off, wf, Cout, y.buf, y.ld, y.off, bias)
@@ -285,7 +287,7 @@ class RefBackend:
             out = F.relu(out)
         self._store(y, out)
 
-    def conv_dgrad(self, dy: Act, wT, C, R, S, stride, pad, dx: Act, res=None, fuse=None):
+    def conv_dgrad(self, dy: Act, wT, C, R, S, stride, pad, dx: Act, res=None, fuse=None, colsum=False):
         K = dy.C
         wk = wT.view(C, R, S, K).permute(3, 0, 1, 2).to(self.dt)
         g = torch.nn.grad.conv2d_input((dx.N, C, dx.H, dx.W), wk, dy.nchw().to(self.dt), stride, pad)
@@ -293,6 +295,9 @@ class RefBackend:
             g = g + res.nchw().to(self.dt)
         if fuse is None:
             self._store(dx, g)
+            if colsum:
+                v = dx.nhwc().to(self.dt)
+                return torch.stack([v.sum((0, 1, 2)), (v * v).sum((0, 1, 2))]).unsqueeze(0)
             return None
         m, z, z2, sc, sh, mb = fuse
         if mb is not None:
