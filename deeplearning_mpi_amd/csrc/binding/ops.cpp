@@ -534,8 +534,9 @@ void upsample2x_bwd(const at::Tensor& dy, int N, int H, int W, int C, int lddy, 
 }
 
 // entries: int64 tensor [n][16] on the host: src_ptr, dst_ptr, d0..d3, v0..v3, s0..s3, start
-void cast_weights(const at::Tensor& entries_dev, int n, int64_t total) {
-  check(dlmpi_cast_weights(reinterpret_cast<const CastEntry*>(entries_dev.data_ptr()), n, total, cur_stream()),
+void cast_weights(const at::Tensor& entries_dev, const at::Tensor& block_map_dev) {
+  check(dlmpi_cast_weights(reinterpret_cast<const CastEntry*>(entries_dev.data_ptr()), block_map_dev.data_ptr(),
+                           (int)(block_map_dev.numel() / 4), cur_stream()),
         "cast_weights");
 }
 

@@ -7,21 +7,26 @@
 
 namespace dlmpi {
 
-// blockIdx.y = entry.  Two paths:
+// Work distribution: block b handles entry map[b].x as slice map[b].y of map[b].z blocks; the host
+// gives each entry ~1 block per 4096 destination elements (= one 64x64 transpose tile), so the
+// large tensors are not left to a fixed handful of blocks while the small ones finish.  Two paths:
 //  * transpose (source unit stride on destination dim 0, e.g. [K][R][S][C] -> [C][R][S][K] for the
 //    data-gradient copy): 64x64 tiles through LDS, coalesced reads along d0 and writes along d3;
 //  * direct (anything else, e.g. the forward copy whose innermost dim is contiguous in the source):
 //    one destination element per thread, grid-stride over the entry.
-__global__ __launch_bounds__(256) void cast_weights_kernel(const CastEntry* __restrict__ ent) {
+__global__ __launch_bounds__(256) void cast_weights_kernel(const CastEntry* __restrict__ ent,
+                                                           const int4* __restrict__ map) {
   __shared__ float tile[64][65];
-  const CastEntry& e = ent[blockIdx.y];
+  const int4 mb = map[blockIdx.x];
+  const CastEntry& e = ent[mb.x];
+  const int sub = mb.y, nsub = mb.z;
   const int D0 = e.d[0], D1 = e.d[1], D2 = e.d[2], D3 = e.d[3];
   const int64_t n = (int64_t)D0 * D1 * D2 * D3;
   if (e.st[0] == 1 && e.st[3] != 1 && D0 >= 16 && D3 >= 16) {
     const int t0n = (D0 + 63) / 64, t3n = (D3 + 63) / 64;
     const int64_t ntiles = (int64_t)D1 * D2 * t0n * t3n;
     const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;   // 64 x 4
-    for (int64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+    for (int64_t t = sub; t < ntiles; t += nsub) {
       int64_t r = t;
       const int b3 = (int)(r % t3n); r /= t3n;
       const int b0 = (int)(r % t0n); r /= t0n;
@@ -46,7 +51,7 @@ __global__ __launch_bounds__(256) void cast_weights_kernel(const CastEntry* __re
     }
     return;
   }
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+  for (int64_t i = sub * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)nsub * blockDim.x) {
     int64_t r = i;
     const int i3 = (int)(r % D3);
     r /= D3;
@@ -78,10 +83,12 @@ __global__ void pack_kernel(const void* const* __restrict__ srcs, const int64_t*
 
 using namespace dlmpi;
 
-extern "C" hipError_t dlmpi_cast_weights(const CastEntry* entries_dev, int n, int64_t total, hipStream_t s) {
-  if (total == 0 || n == 0) return hipSuccess;
+extern "C" hipError_t dlmpi_cast_weights(const CastEntry* entries_dev, const void* block_map_dev, int nblocks,
+                                         hipStream_t s) {
+  if (nblocks <= 0) return hipSuccess;
   // gaps between entries (alignment padding) are zeroed once at allocation and never written
-  hipLaunchKernelGGL(cast_weights_kernel, dim3(64, (unsigned)n), dim3(256), 0, s, entries_dev);
+  hipLaunchKernelGGL(cast_weights_kernel, dim3((unsigned)nblocks), dim3(256), 0, s, entries_dev,
+                     reinterpret_cast<const int4*>(block_map_dev));
   return hipGetLastError();
 }
 

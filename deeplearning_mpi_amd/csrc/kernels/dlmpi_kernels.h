@@ -178,7 +178,8 @@ struct CastEntry {
   int64_t st[4];   // source strides (elements)
   int64_t start;   // first destination element of this entry in the global enumeration
 };
-hipError_t dlmpi_cast_weights(const CastEntry* entries_dev, int n, int64_t total, hipStream_t s);
+// block_map_dev: int4 per block {entry, slice, slices of that entry, 0}
+hipError_t dlmpi_cast_weights(const CastEntry* entries_dev, const void* block_map_dev, int nblocks, hipStream_t s);
 
 // losses (forward saves what the backward needs; backward reads the upstream grad from device)
 hipError_t dlmpi_softmax_ce_fwd(const float* logits, int ldl, const int64_t* labels, int N, int K, float* loss_rows,

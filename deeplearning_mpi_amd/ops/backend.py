@@ -189,18 +189,21 @@ class NativeBackend:
     # ---------------- weights ----------------
     def cast_weights(self, entries, total, dst_flat):
         """entries: list of (src fp32 tensor view, dst offset, dims[4], valid[4], src strides[4])."""
-        key = id(entries)
+        key = (id(entries), len(entries), dst_flat.data_ptr())
         ent = self._cast_cache.get(key)
         if ent is None or ent[0] is not entries:
             blob = bytearray()
             base = dst_flat.data_ptr()
-            start = 0
-            for (src, doff, d, v, st) in entries:
+            bmap = []
+            for k, (src, doff, d, v, st) in enumerate(entries):
                 blob += struct.pack("<QQ4i4i4qq", src.data_ptr(), base + 2 * doff, *d, *v, *st, doff)
-                start += d[0] * d[1] * d[2] * d[3]
+                # ~one block per 4096 destination elements (one 64x64 tile of the transpose path)
+                nb = max(1, min(1024, -(-d[0] * d[1] * d[2] * d[3] // 4096)))
+                bmap += [(k, j, nb, 0) for j in range(nb)]
             dev = torch.frombuffer(bytearray(blob), dtype=torch.uint8).to(self.device)
-            self._cast_cache[key] = ent = (entries, dev)
-        self.C.cast_weights(ent[1], len(entries), int(total))
+            bm = torch.tensor(bmap, dtype=torch.int32).to(self.device)
+            self._cast_cache[key] = ent = (entries, dev, bm)
+        self.C.cast_weights(ent[1], ent[2])
 
     # ---------------- losses / eval ----------------
     def ce_fwd(self, logits, labels):
