@@ -13,6 +13,8 @@ import os
 import sys
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+if os.environ.get("DLMPI_AB_ROOT"):   # A/B against another build of the package (e.g. a saved copy)
+    sys.path.insert(0, os.path.abspath(os.environ["DLMPI_AB_ROOT"]))
 
 import torch  # noqa: E402
 
