@@ -119,3 +119,38 @@ def test_resnet_training_decreases_loss():
         opt.step()
         losses.append(loss.item())
     assert losses[-1] < 0.5 * losses[0]
+
+
+@pytest.mark.parametrize("make,loss", [
+    (lambda: resnet50(num_classes=10), "ce"),
+    (lambda: UNet(out_classes=1), "bce"),
+])
+def test_auxiliary_streams_bitwise_equal_single_stream(make, loss):
+    """Weight gradients on the side stream and the ResNet downsample branch on the branch stream
+    change only WHEN kernels run, not what they compute: one training step with the auxiliary
+    streams must give bit-identical gradients and BN statistics to the same step on one stream
+    (a missing stream dependency would show up as a mismatch)."""
+    torch.manual_seed(0)
+    m1 = make().to(DEV)
+    m2 = copy.deepcopy(m1)
+    g = torch.Generator(device=DEV).manual_seed(5)
+    if loss == "ce":
+        x = torch.randn(32, 3, 64, 64, device=DEV, generator=g)
+        y = torch.randint(10, (32,), device=DEV, generator=g)
+        fn = lambda m: cross_entropy(m(x), y)   # noqa: E731
+    else:
+        x = torch.randn(2, 3, 64, 64, device=DEV, generator=g)
+        y = (torch.rand(2, 64, 64, device=DEV, generator=g) > 0.5).float()
+        fn = lambda m: bce_with_logits(m(x).squeeze(1), y)   # noqa: E731
+    m1.engine_setup(DEV)
+    m2.engine_setup(DEV)
+    assert m1._be.side_stream is not None
+    m2._be.side_stream = None       # everything on the current stream
+    m2._be.branch_stream = None
+    for m in (m1, m2):
+        m.arena.zero_grad()
+        fn(m).backward()
+    torch.cuda.synchronize()
+    assert torch.equal(m1.arena.grad, m2.arena.grad)
+    for (n, b1), (_, b2) in zip(m1.named_buffers(), m2.named_buffers()):
+        assert torch.equal(b1, b2), n
