@@ -369,10 +369,16 @@ void conv2d_wgrad(const at::Tensor& dy, int lddy, int dyoff, int Ko, const at::T
   const int bn = 128;
   a.ntiles = ceil_div(a.TC, bn);
   const int tiles = a.mtiles * a.ntiles;
-  // split the pixel reduction so the grid covers the chip ~4 blocks deep, but keep each split at
-  // least 8 K-steps (512 pixels) so the fp32 slab traffic stays small next to the MFMA work
+  // split the pixel reduction so the grid covers the chip ~2 blocks deep, but keep each split at
+  // least 8 K-steps (512 pixels) so the fp32 slab traffic stays small next to the MFMA work.
+  // DLMPI_WGRAD_BLOCKS: target grid size (the weight gradients share the GPU with the data-gradient
+  // chain on another stream, so they need not fill it alone)
+  static const int target_blocks = [] {
+    const char* e = getenv("DLMPI_WGRAD_BLOCKS");
+    return e ? std::max(64, atoi(e)) : 512;
+  }();
   const int maxsplit = std::max(1, ceil_div(a.npix, 512));
-  int splits = std::max(1, std::min(maxsplit, ceil_div(1024, tiles)));
+  int splits = std::max(1, std::min(maxsplit, ceil_div(target_blocks, tiles)));
   int pps = ceil_div(a.npix, splits);
   pps = ceil_div(pps, 64) * 64;
   splits = ceil_div(a.npix, pps);
