@@ -57,7 +57,9 @@ def unet_shapes(N, img=512, cin=3):
     c = 1024
     for co in (512, 256, 128, 64):
         h *= 2
-        sh[(N, h, h, c, co, 3, 1, 1)] += 1    # after concat: (c - co) up + co skip = c channels
+        # after concat: c up-sampled (ConvTranspose2d keeps the channel count) + co skip channels
+        # (UpBlock(c + co, co), /root/reference/pytorch/unet/model.py:36-47, 66-69)
+        sh[(N, h, h, c + co, co, 3, 1, 1)] += 1
         sh[(N, h, h, co, co, 3, 1, 1)] += 1
         c = co
     sh[(N, h, h, 64, 1, 1, 1, 0)] += 1

@@ -85,6 +85,9 @@ static int sq256_min_tiles() {
 // cin: channel count of the GEMM's gathered operand (the 8-wave 256x256 kernel needs cin % 64 == 0)
 static void pick_tiles(int64_t M, int Kout, int64_t red, int cin, int& bm, int& bn) {
   bn = Kout <= 64 ? 64 : 128;
+  // 64 (mod 128) channels above 128 (the UNet's 192-channel top concat gradient): 64-wide tiles
+  // cover them exactly instead of a half-empty last 128-wide tile (a third more MFMA work)
+  if (Kout > 128 && Kout % 128 == 64) bn = 64;
   bm = 128;
   if (bm_override()) {
     bm = bm_override();
