@@ -58,6 +58,11 @@ __device__ void block_combine(float (*acc)[8], const RowMap& rm, int C, float* p
 // {sum dyr, sum dyr*z} for the fused finalize (raw_z).  Replaces maxpool_bwd + bn_bwd_reduce and
 // the mask read of bn_bwd_apply.  `add` (optional): a second gradient of the pool input summed in
 // before the mask (the UNet encoder output also feeds the decoder's skip concat).
+// NWIN > 0: at most NWIN x NWIN windows hold an input pixel (ceil(k / stride): 2 for the ResNet
+// stem's 3x3/s2, 1 for the UNet's 2x2/s2); the candidate loop is unrolled with predication so all
+// window loads (index + gradient) are in flight at once instead of one dependent round trip per
+// window.  Same summation order as the generic loop (oh, then ow, ascending) -> identical results.
+template <int NWIN>
 __global__ __launch_bounds__(256) void maxpool_bwd_bn_kernel(const uint16_t* __restrict__ dy,
                                                              const uint8_t* __restrict__ idx, int N, int H, int W,
                                                              int C, int k, int stride, int pad, int OH, int OW,
@@ -87,16 +92,42 @@ __global__ __launch_bounds__(256) void maxpool_bwd_bn_kernel(const uint16_t* __r
       int ow_lo = iw + pad - k + 1;
       ow_lo = ow_lo <= 0 ? 0 : (ow_lo + stride - 1) / stride;
       const int ow_hi = min((iw + pad) / stride, OW - 1);
-      for (int oh = oh_lo; oh <= oh_hi; ++oh) {
-        for (int ow = ow_lo; ow <= ow_hi; ++ow) {
-          const uint8_t want = (uint8_t)((ih - (oh * stride - pad)) * k + (iw - (ow * stride - pad)));
-          const int64_t op = ((int64_t)n * OH + oh) * OW + ow;
-          const uint64_t id = *reinterpret_cast<const uint64_t*>(idx + op * C + c0);
-          float d[8];
-          unpack8(*reinterpret_cast<const u32x4*>(dy + op * C + c0), d);
+      if constexpr (NWIN > 0) {
+        uint64_t id[NWIN * NWIN];
+        u32x4 dv[NWIN * NWIN];
 #pragma unroll
-          for (int e = 0; e < 8; ++e)
-            if (((id >> (8 * e)) & 0xff) == want) g[e] += d[e];
+        for (int a = 0; a < NWIN; ++a)
+#pragma unroll
+          for (int b = 0; b < NWIN; ++b) {
+            const bool ok = oh_lo + a <= oh_hi && ow_lo + b <= ow_hi;
+            const int64_t op = ok ? ((int64_t)n * OH + oh_lo + a) * OW + ow_lo + b : 0;   // 0: a valid address
+            id[a * NWIN + b] = *reinterpret_cast<const uint64_t*>(idx + op * C + c0);
+            dv[a * NWIN + b] = *reinterpret_cast<const u32x4*>(dy + op * C + c0);
+          }
+#pragma unroll
+        for (int a = 0; a < NWIN; ++a)
+#pragma unroll
+          for (int b = 0; b < NWIN; ++b) {
+            const bool ok = oh_lo + a <= oh_hi && ow_lo + b <= ow_hi;
+            const int want = ok ? (ih - ((oh_lo + a) * stride - pad)) * k + (iw - ((ow_lo + b) * stride - pad)) : 256;
+            float d[8];
+            unpack8(dv[a * NWIN + b], d);
+#pragma unroll
+            for (int e = 0; e < 8; ++e)
+              if ((int)((id[a * NWIN + b] >> (8 * e)) & 0xff) == want) g[e] += d[e];
+          }
+      } else {
+        for (int oh = oh_lo; oh <= oh_hi; ++oh) {
+          for (int ow = ow_lo; ow <= ow_hi; ++ow) {
+            const uint8_t want = (uint8_t)((ih - (oh * stride - pad)) * k + (iw - (ow * stride - pad)));
+            const int64_t op = ((int64_t)n * OH + oh) * OW + ow;
+            const uint64_t id = *reinterpret_cast<const uint64_t*>(idx + op * C + c0);
+            float d[8];
+            unpack8(*reinterpret_cast<const u32x4*>(dy + op * C + c0), d);
+#pragma unroll
+            for (int e = 0; e < 8; ++e)
+              if (((id >> (8 * e)) & 0xff) == want) g[e] += d[e];
+          }
         }
       }
       if (add) {   // second gradient source of the pool input (UNet: its skip-concat slice)
@@ -660,7 +691,17 @@ extern "C" hipError_t dlmpi_maxpool_bwd_bn(const uint16_t* dy, const uint8_t* id
                                            const float* mshift, const uint16_t* add, int ldadd, int addoff,
                                            uint16_t* dx, float* partial, int nblk, hipStream_t s) {
   if (C % 8 || C > 2048 || (int64_t)N * H * W >= (1ll << 31)) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(maxpool_bwd_bn_kernel, dim3(nblk), dim3(256), 0, s, dy, idx, N, H, W, C, k, stride, pad, OH, OW,
-                     make_fastdiv(W), make_fastdiv(H), z, mscale, mshift, add, ldadd, addoff, dx, partial);
+  const int nw = (k + stride - 1) / stride;
+  static const bool generic = [] {   // DLMPI_POOL_BWD_GENERIC=1: the dependent window loop (A/B)
+    const char* e = getenv("DLMPI_POOL_BWD_GENERIC");
+    return e && atoi(e) != 0;
+  }();
+#define DLMPI_MPB(NW)                                                                                          \
+  hipLaunchKernelGGL(maxpool_bwd_bn_kernel<NW>, dim3(nblk), dim3(256), 0, s, dy, idx, N, H, W, C, k, stride, pad, \
+                     OH, OW, make_fastdiv(W), make_fastdiv(H), z, mscale, mshift, add, ldadd, addoff, dx, partial)
+  if (!generic && nw == 1) DLMPI_MPB(1);
+  else if (!generic && nw == 2) DLMPI_MPB(2);
+  else DLMPI_MPB(0);
+#undef DLMPI_MPB
   return hipGetLastError();
 }
