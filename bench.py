@@ -15,7 +15,7 @@ The other BASELINE.json configs are presets (``--config``):
   resnet18_cifar  ResNet-18 bs=128/GPU 3x32x32, 10 classes (the reference's own CIFAR run,
                   /root/reference/pytorch/resnet/main.py:36-54,164)
 
-Usage:  python bench.py [--gpus N] [--steps K] [--warmup W] [--config NAME] [--graph 1]
+Usage:  python bench.py [--gpus N] [--steps K] [--warmup W] [--config NAME] [--graph 1] [--breakdown N]
         (N > 1: launched by torch.distributed.run / torchrun or mpirun, one rank per GPU)
 Prints ONE JSON line on rank 0.
 """
@@ -59,6 +59,9 @@ def main():
     ap.add_argument("--classes", type=int, default=None)
     ap.add_argument("--bucket_mb", type=float, default=None)
     ap.add_argument("--graph", type=int, default=0, help="1: replay the whole step from a captured hipGraph")
+    ap.add_argument("--breakdown", type=int, default=0,
+                    help="N > 0: after the timed steps, N more steps with HIP-event phase timing (forward / "
+                         "backward / exposed all-reduce wait / optimizer), printed to stderr")
     ap.add_argument("--backend", default="rccl", help="rccl (default); gloo + DLMPI_GLOO_DEVICE=cuda rehearses "
                                                       "several ranks on one GPU")
     args = ap.parse_args()
@@ -129,6 +132,33 @@ def main():
     lossv = float(loss.item())
     global_batch = cfg["batch"] * world
     ips = global_batch * args.steps / dt
+    if args.breakdown > 0 and not args.graph:
+        # untimed extra steps: per-phase GPU time from HIP events (no host sync inside a step)
+        from deeplearning_mpi_amd.utils.profiler import StepTimer
+
+        tm = StepTimer()
+        ddp.timer = tm
+        for _ in range(args.breakdown):
+            with tm.phase("step"):
+                opt.zero_grad()
+                with tm.phase("forward"):
+                    out = ddp(x)
+                    loss = crit(out, y) if cfg["task"] == "cls" else crit(out.squeeze(1), y)
+                with tm.phase("backward"):   # includes comm_exposed
+                    loss.backward()
+                with tm.phase("optimizer"):
+                    if cfg["task"] == "seg":
+                        clip_grad_norm_(model.parameters(), 1.0, optimizer=opt)
+                    opt.step()
+        ddp.timer = None
+        bd = {k: round(v, 3) for k, v in tm.summary().items()}
+        bd.setdefault("comm_exposed", 0.0)
+        bdt = torch.tensor([bd["comm_exposed"], bd["step"]], dtype=torch.float64, device=dev)
+        comm.allreduce(bdt, "max")
+        if comm.rank == 0:
+            print(json.dumps({"breakdown_ms_per_step": bd, "max_over_ranks": {"comm_exposed": float(bdt[0]),
+                                                                             "step": float(bdt[1])},
+                              "n_gpus": world, "config": args.config}), file=sys.stderr, flush=True)
     if comm.rank == 0:
         headline = args.config == "resnet50" and cfg == PRESETS["resnet50"]
         print(json.dumps({

@@ -71,6 +71,7 @@ class DistributedDataParallel(nn.Module):
         self._require_sync = True
         self._queued = False
         self._steps = 0
+        self.timer = None   # optional utils.profiler.StepTimer: times the exposed all-reduce wait
 
     # ---------------------------------------------------------------- construction collectives
     def _verify_params(self):
@@ -121,7 +122,11 @@ class DistributedDataParallel(nn.Module):
         self._queued = False
         if self.reducer is not None:
             launched = self.reducer.launched()
-            self.reducer.finalize()
+            if self.timer is not None:   # exposed communication: the stream's wait for the last buckets
+                with self.timer.phase("comm_exposed"):
+                    self.reducer.finalize()
+            else:
+                self.reducer.finalize()
             self._steps += 1
             if hasattr(self.comm, "check_step"):   # desync detector (parallel/debug.py)
                 self.comm.check_step(launched, self._steps)
