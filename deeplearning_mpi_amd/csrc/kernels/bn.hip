@@ -209,8 +209,17 @@ __device__ __forceinline__ void colsum2_final(const double* __restrict__ dpart, 
 }
 
 static inline int colsum_slices(int T) {
-  int S = (T + 31) / 32;
-  return S < 1 ? 1 : (S > 64 ? 64 : S);
+  // tiles per slice / slice cap (DLMPI_COLSUM_TPS / DLMPI_COLSUM_SMAX: A/B knobs)
+  static const int tps = [] {
+    const char* e = getenv("DLMPI_COLSUM_TPS");
+    return e && atoi(e) > 0 ? atoi(e) : 32;
+  }();
+  static const int smax = [] {
+    const char* e = getenv("DLMPI_COLSUM_SMAX");
+    return e && atoi(e) > 0 ? atoi(e) : 64;
+  }();
+  int S = (T + tps - 1) / tps;
+  return S < 1 ? 1 : (S > smax ? smax : S);
 }
 
 // Per-channel finalize bodies, shared by the two-kernel path and the fused last-arriver path.
