@@ -117,7 +117,16 @@ def _w_ddp(rank, world, port, out, arch):
         cross_entropy(ddp(x.double()), y).backward()
     cross_entropy(ddp(x.double()), y).backward()
     acc = {n: p.grad.clone() for n, p in model.named_parameters()}
-    torch.save({"init": init, "grads": grads, "acc": acc, "nb": len(ddp.bucket_bounds)}, f"{out}/r{rank}.pt")
+    # exposed-communication timer (bench.py --breakdown): the reducer's finalize is timed per step
+    from deeplearning_mpi_amd.utils.profiler import StepTimer
+
+    tm = StepTimer()
+    ddp.timer = tm
+    cross_entropy(ddp(x.double()), y).backward()
+    ddp.timer = None
+    bd = tm.summary()
+    torch.save({"init": init, "grads": grads, "acc": acc, "nb": len(ddp.bucket_bounds), "bd": bd},
+               f"{out}/r{rank}.pt")
     dl.destroy_distributed()
 
 
@@ -128,6 +137,7 @@ def test_ddp_matches_mean_of_local_grads(tmp_path, arch):
 
     res = _spawn(_w_ddp, 2, tmp_path, arch)
     assert res[0]["nb"] > 2
+    assert all("comm_exposed" in r["bd"] and r["bd"]["comm_exposed"] >= 0.0 for r in res)
     # construction broadcast: both ranks start from rank 0's weights
     for k in res[0]["init"]:
         assert torch.equal(res[0]["init"][k], res[1]["init"][k]), k
