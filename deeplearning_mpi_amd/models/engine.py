@@ -378,6 +378,7 @@ class _EngineFn(torch.autograd.Function):
             out, state = mod._engine_forward(x, train=True, save=True)
         ctx.mod = mod
         ctx.state = state
+        ctx.aux_on = getattr(mod._be, "aux_on", None)   # the backward uses the forward's stream plan
         return out
 
     @staticmethod
@@ -385,6 +386,8 @@ class _EngineFn(torch.autograd.Function):
         mod = ctx.mod
         state = ctx.state
         ctx.state = None
+        if ctx.aux_on is not None:
+            mod._be.aux_on = ctx.aux_on
         with trace_range(f"dlmpi.backward[{type(mod).__name__}]"):
             mod._engine_backward(state, gout)
             side = getattr(mod._be, "side_stream", None)
@@ -428,6 +431,9 @@ class EngineModule(nn.Module):
 
     def forward(self, x):
         self.engine_setup(x.device)
+        be = self._be
+        if hasattr(be, "aux_min_pixels"):   # auxiliary streams only for steps big enough to use them
+            be.aux_on = x.shape[0] * x.shape[-2] * x.shape[-1] >= be.aux_min_pixels
         self._arena.refresh()
         if self.training and torch.is_grad_enabled():
             self._arena.attach_grads()

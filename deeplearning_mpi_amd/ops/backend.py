@@ -49,12 +49,36 @@ class NativeBackend:
         # parameter-gradient work (weight-gradient GEMMs + split reductions, DDP bucket launches)
         # runs on this side stream, off the data-gradient critical path (models/engine.py:grad_side);
         # DLMPI_WGRAD_STREAM=0 keeps everything on the current stream
-        self.side_stream = _aux_stream(self.device, self.C, 1) if os.environ.get("DLMPI_WGRAD_STREAM", "1") != "0" \
+        self._side = _aux_stream(self.device, self.C, 1) if os.environ.get("DLMPI_WGRAD_STREAM", "1") != "0" \
             else None
         # independent residual branches (the ResNet downsample conv + BN) run on this stream beside
         # the main branch, forward and backward (models/resnet.py:_BlockExec); DLMPI_BRANCH_STREAM=0: off
-        self.branch_stream = _aux_stream(self.device, self.C, 2) \
+        self._branch = _aux_stream(self.device, self.C, 2) \
             if os.environ.get("DLMPI_BRANCH_STREAM", "1") != "0" else None
+        # The auxiliary streams pay off when kernels are long enough to leave idle CUs beside each
+        # other; a launch-bound step (ResNet-18 on 32x32 CIFAR: ~300 kernels of a few us) only pays
+        # their per-launch event traffic (measured 31-36k vs 58-60k img/s eager).  The engine turns
+        # them on per step when the input has >= aux_min_pixels (N*H*W) pixels
+        # (EngineModule.forward; DLMPI_AUX_MIN_PIXELS, default 1M: on for ResNet-50 bs 256 at 224^2 and
+        # UNet bs 16 at 512^2, off for CIFAR).
+        self.aux_min_pixels = int(os.environ.get("DLMPI_AUX_MIN_PIXELS", str(1 << 20)))
+        self.aux_on = True
+
+    @property
+    def side_stream(self):
+        return self._side if self.aux_on else None
+
+    @side_stream.setter
+    def side_stream(self, s):
+        self._side = s
+
+    @property
+    def branch_stream(self):
+        return self._branch if self.aux_on else None
+
+    @branch_stream.setter
+    def branch_stream(self, s):
+        self._branch = s
 
     # ---------------- conv family ----------------
     def conv_mtiles(self, N, H, W, C, K, R, S, stride, pad):

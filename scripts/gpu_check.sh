@@ -21,7 +21,7 @@ for s in $STEPS; do
       for c in ${CONFIGS:-resnet18_cifar resnet152 unet512 unet1024}; do
         run "cfg_${c}_ours" 600 python bench.py --config $c --steps 10 --warmup 3
         run "cfg_${c}_graph" 600 python bench.py --config $c --steps 10 --warmup 3 --graph 1
-        [ -z "$SKIP_TORCH" ] && run "cfg_${c}_torch" 600 python benchmarks/torch_baseline.py --config $c --steps 10 --warmup 3
+        if [ -z "$SKIP_TORCH" ]; then run "cfg_${c}_torch" 600 python benchmarks/torch_baseline.py --config $c --steps 10 --warmup 3; fi
       done ;;
     prof)
       ( cd /tmp && export TMPDIR=/tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/prof" -o bench --output-format csv -- python "$R/bench.py" --steps 5 --warmup 2 > "$R/gpurun_out/prof.log" 2>&1 ); echo "prof rc=$?" ;;

@@ -144,6 +144,7 @@ def test_auxiliary_streams_bitwise_equal_single_stream(make, loss):
         fn = lambda m: bce_with_logits(m(x).squeeze(1), y)   # noqa: E731
     m1.engine_setup(DEV)
     m2.engine_setup(DEV)
+    m1._be.aux_min_pixels = 0       # small test inputs: force the auxiliary streams on
     assert m1._be.side_stream is not None
     m2._be.side_stream = None       # everything on the current stream
     m2._be.branch_stream = None
