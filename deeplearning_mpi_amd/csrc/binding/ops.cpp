@@ -501,6 +501,20 @@ void maxpool_bwd(const at::Tensor& dy, const at::Tensor& idx, int N, int H, int 
                           optr<uint16_t>(add), ldadd, addoff, ptr<uint16_t>(dx), lddx, dxoff, cur_stream()),
         "maxpool_bwd");
 }
+// data gradient of a 1x1 convolution with one output channel (UNet head) fused with the BN backward of
+// the layer below; returns the partials [nblk][2][C] for bn_bwd_finalize_fused
+at::Tensor outer_dgrad_bn(const at::Tensor& dy, int lddy, int64_t M, int C, const at::Tensor& w, int ldw,
+                          const at::Tensor& z, const at::Tensor& mscale, const at::Tensor& mshift, at::Tensor dx) {
+  require_gpu(dy, "dy");
+  const int64_t rpb = 256 / (C / 8);
+  const int nblk = (int)std::max<int64_t>(1, std::min<int64_t>(4096, (M + rpb * 8 - 1) / (rpb * 8)));
+  at::Tensor part = at::empty({nblk, 2, C}, dy.options().dtype(at::kFloat));
+  check(dlmpi_outer_dgrad_bn(ptr<uint16_t>(dy), lddy, M, C, ptr<uint16_t>(w), ldw, ptr<uint16_t>(z),
+                             ptr<float>(mscale), ptr<float>(mshift), ptr<uint16_t>(dx), ptr<float>(part), nblk,
+                             cur_stream()),
+        "outer_dgrad_bn");
+  return part;
+}
 // max-pool backward fused with the BN-backward statistics of the producing BN+ReLU (mask from z);
 // returns the partials [nblk][2][C] for bn_bwd_finalize_fused
 at::Tensor maxpool_bwd_bn(const at::Tensor& dy, const at::Tensor& idx, int N, int H, int W, int C, int k, int stride,
@@ -653,6 +667,7 @@ void register_ops(pybind11::module& m) {
   m.def("maxpool_fwd", &maxpool_fwd);
   m.def("maxpool_bwd", &maxpool_bwd);
   m.def("maxpool_bwd_bn", &maxpool_bwd_bn);
+  m.def("outer_dgrad_bn", &outer_dgrad_bn);
   m.def("avgpool_fwd", &avgpool_fwd);
   m.def("avgpool_bwd", &avgpool_bwd);
   m.def("nchw_to_nhwc", &nchw_to_nhwc);

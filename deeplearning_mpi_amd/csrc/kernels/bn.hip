@@ -151,6 +151,45 @@ __global__ __launch_bounds__(256) void maxpool_bwd_bn_kernel(const uint16_t* __r
   block_combine<2>(acc, rm, C, partial);
 }
 
+// Data gradient of a 1x1 convolution with ONE output channel (the UNet head, reference
+// model.py:68) into the gradient of the BN+ReLU output below it: dx[m, c] = dy[m] * w[c] -- an
+// outer product, so a streaming kernel instead of a GEMM tile with 63 of 64 reduction lanes zero
+// -- masked by [z*scale + shift > 0], stored, and the BN-backward partials {sum dx, sum dx*z} per
+// block.  The bf16 x bf16 product is exact in fp32, as in the GEMM path: identical dx.
+__global__ __launch_bounds__(256) void outer_dgrad_bn_kernel(const uint16_t* __restrict__ dy, int lddy, int64_t M,
+                                                             int C, const uint16_t* __restrict__ w, int ldw,
+                                                             const uint16_t* __restrict__ z,
+                                                             const float* __restrict__ msc,
+                                                             const float* __restrict__ msh,
+                                                             uint16_t* __restrict__ dx, float* __restrict__ partial) {
+  const RowMap rm = rowmap(C);
+  float acc[2][8] = {};
+  if (rm.active) {
+    const int c0 = rm.cc * 8;
+    float wv[8], sc[8], sh[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      wv[e] = bf2f(w[(int64_t)(c0 + e) * ldw]);
+      sc[e] = msc[c0 + e];
+      sh[e] = msh[c0 + e];
+    }
+    for (int64_t row = (int64_t)blockIdx.x * rm.RPB + rm.rr; row < M; row += (int64_t)gridDim.x * rm.RPB) {
+      const float d = bf2f(dy[row * lddy]);
+      float zz[8], g[8];
+      unpack8(*reinterpret_cast<const u32x4*>(z + row * C + c0), zz);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) g[e] = zz[e] * sc[e] + sh[e] > 0.f ? d * wv[e] : 0.f;
+      const u32x4 pk = pack8(g);
+      *reinterpret_cast<u32x4*>(dx + row * C + c0) = pk;
+      float r[8];
+      unpack8(pk, r);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) { acc[0][e] += r[e]; acc[1][e] += r[e] * zz[e]; }
+    }
+  }
+  block_combine<2>(acc, rm, C, partial);
+}
+
 __global__ __launch_bounds__(256) void bn_stats_kernel(const uint16_t* __restrict__ x, int64_t M, int C, int ldx,
                                                        int xoff, float* __restrict__ partial) {
   const RowMap rm = rowmap(C);
@@ -599,6 +638,15 @@ static hipError_t colsum_finalize(const float* partial, int T, int C, int ns, in
     hipLaunchKernelGGL(colsum2_kernel, dim3(G, S), dim3(256), 0, s, partial, T, C, ns, k2, ws);
     hipLaunchKernelGGL(finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, s, ws, S, C, f);
   }
+  return hipGetLastError();
+}
+
+extern "C" hipError_t dlmpi_outer_dgrad_bn(const uint16_t* dy, int lddy, int64_t M, int C, const uint16_t* w, int ldw,
+                                         const uint16_t* z, const float* mscale, const float* mshift, uint16_t* dx,
+                                         float* partial, int nblk, hipStream_t s) {
+  if (C % 8 || C > 2048 || M <= 0) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(outer_dgrad_bn_kernel, dim3(nblk), dim3(256), 0, s, dy, lddy, M, C, w, ldw, z, mscale, mshift,
+                     dx, partial);
   return hipGetLastError();
 }
 

@@ -158,6 +158,11 @@ hipError_t dlmpi_maxpool_bwd_bn(const uint16_t* dy, const uint8_t* idx, int N, i
                                 int pad, int OH, int OW, const uint16_t* z, const float* mscale, const float* mshift,
                                 const uint16_t* add, int ldadd, int addoff, uint16_t* dx, float* partial, int nblk,
                                 hipStream_t s);
+// data gradient of a 1x1 conv with one output channel (dx[m,c] = dy[m*lddy] * w[c*ldw]) into the
+// gradient of a BN+ReLU output (mask z*scale+shift > 0), BN-backward partials [nblk][2][C]
+hipError_t dlmpi_outer_dgrad_bn(const uint16_t* dy, int lddy, int64_t M, int C, const uint16_t* w, int ldw,
+                                const uint16_t* z, const float* mscale, const float* mshift, uint16_t* dx,
+                                float* partial, int nblk, hipStream_t s);
 hipError_t dlmpi_avgpool_fwd(const uint16_t* x, int N, int HW, int C, uint16_t* y, hipStream_t s);
 hipError_t dlmpi_avgpool_bwd(const uint16_t* dy, int N, int HW, int C, uint16_t* dx, hipStream_t s);
 hipError_t dlmpi_nchw_to_nhwc(const float* x, int N, int C, int H, int W, int Cpad, uint16_t* y, hipStream_t s);

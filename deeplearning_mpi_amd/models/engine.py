@@ -69,6 +69,10 @@ def record_on(stream, *objs):
             record_on(stream, *o)
 
 
+# DLMPI_OUTER_DGRAD=0: one-output-channel 1x1 data gradients through the GEMM kernel (A/B)
+_OUTER_DGRAD = os.environ.get("DLMPI_OUTER_DGRAD", "1") != "0"
+
+
 class BwdFuse(NamedTuple):
     """What a data-gradient GEMM needs to produce the gradient of a BN+ReLU output fused: the ReLU
     mask (``mask`` = the saved output y, or -- for BN+ReLU without a residual -- recomputed from the
@@ -243,6 +247,12 @@ class ConvUnit:
         if not need_dx:
             return None
         dx = Act.empty(x.N, x.H, x.W, self.Cp, be.act_dtype, x.device)
+        if (self.K == 1 and self.R == 1 and self.S == 1 and self.stride == 1 and dx_res is None and not colsum
+                and fuse_next is not None and fuse_next.scale is not None and fuse_next.z2 is None
+                and hasattr(be, "outer_dgrad_bn") and _OUTER_DGRAD):
+            # one output channel (the UNet head): the data gradient is an outer product
+            part = be.outer_dgrad_bn(dz, ar.get_compute(self.h_dg), self.Kp, dx, fuse_next)
+            return dx, part
         part = be.conv_dgrad(dz, ar.get_compute(self.h_dg), self.Cp, self.R, self.S, self.stride, self.pad, dx,
                              res=dx_res, fuse=fuse_next, colsum=colsum)
         return (dx, part) if (fuse_next is not None or colsum) else dx

@@ -182,6 +182,15 @@ class NativeBackend:
         self.C.maxpool_bwd(dy.buf, idx, x.N, x.H, x.W, x.C, k, s, p, dy.H, dy.W, add.buf if add is not None else None,
                            add.ld if add is not None else 0, add.off if add is not None else 0, dx.buf, dx.ld, dx.off)
 
+    def outer_dgrad_bn(self, dy: Act, wT, ldw, dx: Act, fuse):
+        """Data gradient of a 1x1 conv with one output channel: dx[m, c] = dy[m, 0] * wT[c * ldw],
+        as the masked gradient of relu(BN(z)) (fuse = BwdFuse(None, z, None, scale, shift)); returns
+        the BN-backward partials [blocks][2][C]."""
+        assert fuse.scale is not None and fuse.z2 is None and fuse.mask is None and fuse.mbits is None
+        assert dx.ld == dx.C and dx.off == 0 and fuse.z.ld == fuse.z.C and fuse.z.off == 0
+        return self.C.outer_dgrad_bn(dy.buf[:, dy.off:], dy.ld, dx.rows, dx.C, wT, ldw, fuse.z.buf, fuse.scale,
+                                     fuse.shift, dx.buf)
+
     def avgpool_fwd(self, x: Act, y: Act):
         self.C.avgpool_fwd(x.buf, x.N, x.H * x.W, x.C, y.buf)
 

@@ -354,6 +354,29 @@ def test_maxpool_bwd_fused_bn_stats():
     assert torch.allclose(ps[1], (v * z.buf.double()).sum(0), rtol=1e-4, atol=1e-3)
 
 
+def test_outer_dgrad_fused_bn_matches_gemm_path():
+    """UNet head (1x1 conv, one output channel): the outer-product data gradient with the BN-backward
+    fusion gives the same masked dx as the GEMM kernel's fused epilogue, and the same partial sums."""
+    nb, rb = _be()
+    N, H, W, C, Kp = 2, 24, 20, 64, 8
+    z, zr = _act(N, H, W, C)
+    sc, sh = torch.rand(C, device=DEV) + 0.5, torch.randn(C, device=DEV) * 0.3
+    dy, _ = _act(N, H, W, Kp)
+    dy.buf[:, 1:] = 0                                    # channels >= K are padding
+    wT = torch.zeros(C, 1, 1, Kp, device=DEV, dtype=torch.bfloat16)
+    wT[..., 0] = (torch.randn(C, 1, 1, device=DEV) * 0.2).to(torch.bfloat16)
+    fuse = BwdFuse(None, z, None, sc, sh)
+    dx1, dx2 = _empty(N, H, W, C), _empty(N, H, W, C)
+    p1 = nb.conv_dgrad(dy, wT, C, 1, 1, 1, 0, dx1, fuse=fuse)
+    p2 = nb.outer_dgrad_bn(dy, wT.view(-1), Kp, dx2, fuse)
+    torch.cuda.synchronize()
+    assert torch.equal(dx1.buf, dx2.buf)
+    assert torch.allclose(p1.double().sum(0), p2.double().sum(0), rtol=1e-5, atol=1e-4)
+    keep = z.buf.float() * sc + sh > 0
+    want = torch.where(keep, dy.buf[:, :1].float() * wT.view(C, Kp)[:, 0].float(), torch.zeros(1, device=DEV))
+    assert torch.equal(dx2.buf.float(), want.to(torch.bfloat16).float())
+
+
 def test_maxpool_bwd_add_fused_bn_stats():
     """UNet encoder output: pool backward + skip-concat gradient slice + ReLU mask + BN partials."""
     nb, rb = _be()
