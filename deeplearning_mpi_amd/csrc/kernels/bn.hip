@@ -610,6 +610,51 @@ static int* fin_tickets(hipStream_t s) {
   return t;
 }
 
+static int role_of(hipStream_t s, int dev) {
+  for (int r = 1; r < kTicketRoles; ++r)
+    if (s != nullptr && s == g_aux_stream[dev][r]) return r;
+  return 0;
+}
+
+// Split-K workspaces of the conv kernel (conv_igemm.hip), per device and stream role like the
+// finalize tickets.  The slab grows on demand outside graph captures (the eager warm-up steps
+// size it); inside a capture a too-small slab makes the launcher fall back to no split.
+static float* g_sk_slab[64][kTicketRoles] = {};
+static size_t g_sk_slab_floats[64][kTicketRoles] = {};
+static int* g_sk_tk[64][kTicketRoles] = {};
+constexpr int kSplitTickets = 4096;
+
+extern "C" float* dlmpi_splitk_slab(hipStream_t s, size_t floats) {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+  const int r = role_of(s, dev);
+  if (g_sk_slab_floats[dev][r] >= floats) return g_sk_slab[dev][r];
+  hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(s, &st) != hipSuccess || st != hipStreamCaptureStatusNone) return nullptr;
+  // the old slab is never freed: a captured hipGraph may still reference it (a few MB, kept)
+  const size_t n = floats + floats / 2;   // head room
+  float* p = nullptr;
+  if (hipMalloc(&p, n * sizeof(float)) != hipSuccess) return nullptr;
+  g_sk_slab[dev][r] = p;
+  g_sk_slab_floats[dev][r] = n;
+  return p;
+}
+
+extern "C" int* dlmpi_splitk_tickets(hipStream_t s, int n) {
+  int dev = 0;
+  if (n > kSplitTickets || hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+  const int r = role_of(s, dev);
+  if (!g_sk_tk[dev][r]) {
+    hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(s, &st) != hipSuccess || st != hipStreamCaptureStatusNone) return nullptr;
+    int* p = nullptr;
+    if (hipMalloc(&p, kSplitTickets * sizeof(int)) != hipSuccess) return nullptr;
+    if (hipMemsetAsync(p, 0, kSplitTickets * sizeof(int), s) != hipSuccess) return nullptr;   // ordered before the kernel
+    g_sk_tk[dev][r] = p;
+  }
+  return g_sk_tk[dev][r];
+}
+
 static bool fused_finalize() {
   static const bool v = [] {
     const char* e = getenv("DLMPI_BN_FUSED_FINALIZE");

@@ -191,20 +191,32 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(STAGES 
       }
     }
   };
-  if (nk > 0) {
-    if constexpr (!SMALLC) tap_setup(0);
-    issue(0, 0);
+  // split-K (small grids): block y of a.splitk reduces K-steps [kbeg, kend)
+  int kbeg = 0, kend = nk;
+  if (a.splitk > 1) {
+    const int per = (nk + a.splitk - 1) / a.splitk;
+    kbeg = min(nk, (int)blockIdx.y * per);
+    kend = min(nk, kbeg + per);
+  }
+  if (kend > kbeg) {
+    if constexpr (!SMALLC) {
+      const int cps = C >> 6;   // K-steps per tap
+      t_cur = kbeg / cps;
+      c_cur = (kbeg - t_cur * cps) * 64;
+      tap_setup(t_cur);
+    }
+    issue(0, kbeg);
     __syncthreads();
   }
-  for (int ks = 0; ks < nk; ++ks) {
+  for (int ks = kbeg; ks < kend; ++ks) {
     int cur = 0;
     if constexpr (STAGES == 2) {
-      cur = ks & 1;
-      if (ks + 1 < nk) {
+      cur = (ks - kbeg) & 1;
+      if (ks + 1 < kend) {
         advance();
         issue(cur ^ 1, ks + 1);
       }
-    } else if (ks > 0) {
+    } else if (ks > kbeg) {
       advance();
       issue(0, ks);
       __syncthreads();   // this stage landed (vmcnt(0) + barrier)
@@ -234,6 +246,43 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(STAGES 
     // STAGES 2: waits for this wave's glds of tile ks+1, then all waves -> buffers swap;
     // STAGES 1: every wave is done reading the stage before it is overwritten
     __syncthreads();
+  }
+
+  // ---- split-K combine (cdna_hip_programming.md "In-launch split-K reduction") --------------
+  // Every slice stores its fp32 accumulators (fragment layout) to its slab, publishes with an
+  // agent-scope release + ticket; the tile's last arriver acquires and sums ALL slices' slabs in
+  // slice order (deterministic whichever block arrives last), then runs the normal epilogue.
+  if (a.splitk > 1) {
+    constexpr int NF = TM * TN;
+    const int S = a.splitk;
+    // unique over phases (blockIdx.z): ConvTranspose phases all have tile_base 0
+    const int64_t tile = (int64_t)blockIdx.z * gridDim.x + (int64_t)mt * a.ntiles + nt;
+    f32x4* slab = reinterpret_cast<f32x4*>(a.sk_slab) + (tile * S + blockIdx.y) * NF * NT + tid;
+#pragma unroll
+    for (int i = 0; i < NF; ++i) slab[(int64_t)i * NT] = acc[i / TN][i % TN];
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    int* flag = reinterpret_cast<int*>(smem);   // the one LDS array (no second __shared__ object)
+    if (tid == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      flag[0] = __hip_atomic_fetch_add(a.sk_tk + tile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == S - 1;
+    }
+    __syncthreads();
+    if (!flag[0]) return;
+    if (tid == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __hip_atomic_store(a.sk_tk + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+    const f32x4* base = reinterpret_cast<const f32x4*>(a.sk_slab) + tile * S * NF * NT + tid;
+#pragma unroll
+    for (int i = 0; i < NF; ++i) acc[i / TN][i % TN] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int sp = 0; sp < S; ++sp)
+#pragma unroll
+      for (int i = 0; i < NF; ++i) acc[i / TN][i % TN] += base[((int64_t)sp * NF + i) * NT];
+    __syncthreads();   // flag (LDS) is reused by the epilogue staging
   }
 
   // ---- epilogue ------------------------------------------------------------------------------
@@ -410,10 +459,44 @@ static void launch_tile(const ConvArgs* a, dim3 grid, hipStream_t s) {
   }
 }
 
-extern "C" hipError_t dlmpi_conv_igemm(const ConvArgs* a, int bm, int bn, hipStream_t s) {
-  int maxt = 0;
-  for (int i = 0; i < a->nphase; ++i) maxt = a->ph[i].mtiles > maxt ? a->ph[i].mtiles : maxt;
-  dim3 grid((unsigned)(maxt * a->ntiles), 1, (unsigned)a->nphase);
+// Split-K plan for small grids (ResNet-18 on 32x32 CIFAR: layer4 is 1x1 pixels, 8 tiles x 72
+// K-steps): slices so that tiles x slices reaches ~256 blocks, >= 4 K-steps per slice, <= 8 slices.
+// DLMPI_CONV_SPLITK=0 disables.  Slabs (fp32) and tickets come per stream role (bn.hip), so the
+// main and the branch stream can run split convolutions concurrently.
+static int splitk_plan(int tiles, int nk) {
+  static const int on = [] {
+    const char* e = getenv("DLMPI_CONV_SPLITK");
+    return e ? atoi(e) : 1;
+  }();
+  if (!on || tiles >= 256 || nk < 8) return 1;
+  int S = (256 + tiles - 1) / tiles;
+  S = S < nk / 4 ? S : nk / 4;
+  S = S < 8 ? S : 8;
+  return S < 2 ? 1 : S;
+}
+
+extern "C" hipError_t dlmpi_conv_igemm(const ConvArgs* a_in, int bm, int bn, hipStream_t s) {
+  int maxt = 0, tiles = 0, maxk = 0;
+  for (int i = 0; i < a_in->nphase; ++i) {
+    maxt = a_in->ph[i].mtiles > maxt ? a_in->ph[i].mtiles : maxt;
+    tiles += a_in->ph[i].mtiles * a_in->ntiles;
+    maxk = a_in->ph[i].ksteps > maxk ? a_in->ph[i].ksteps : maxk;
+  }
+  ConvArgs ab = *a_in;
+  const ConvArgs* a = &ab;
+  ab.splitk = 1;
+  const int S = splitk_plan(tiles, maxk);
+  if (S > 1) {
+    const int ntile_ids = maxt * a_in->ntiles * a_in->nphase;   // kernel: z * gridDim.x + mt * ntiles + nt
+    float* slab = dlmpi_splitk_slab(s, (size_t)ntile_ids * S * bm * bn);
+    int* tk = dlmpi_splitk_tickets(s, ntile_ids);
+    if (slab && tk) {
+      ab.splitk = S;
+      ab.sk_slab = slab;
+      ab.sk_tk = tk;
+    }
+  }
+  dim3 grid((unsigned)(maxt * a->ntiles), (unsigned)ab.splitk, (unsigned)a->nphase);
   if (grid.x == 0) return hipSuccess;
   if (bm == 256 && bn == 256) {   // 8 waves, double-buffered; regular channel counts only
     if (a->C < 64) return hipErrorInvalidValue;

@@ -80,6 +80,9 @@ struct ConvArgs {
   int nt_store;                    // 1: non-temporal output stores (streaming outputs)
   int ntiles;
   int nphase;
+  int splitk;                      // > 1: K split over blockIdx.y, last-arriver combine (set by the launcher)
+  float* sk_slab;                  // [tile][slice][TM*TN][threads] f32x4 fragment slabs
+  int* sk_tk;                      // [tile] self-resetting arrival tickets
   int cstep, tstep;                // K-iteration: c += cstep, t += tstep per 64-wide step
   ConvPhase ph[4];
 };
@@ -163,6 +166,11 @@ hipError_t dlmpi_maxpool_bwd_bn(const uint16_t* dy, const uint8_t* idx, int N, i
 hipError_t dlmpi_outer_dgrad_bn(const uint16_t* dy, int lddy, int64_t M, int C, const uint16_t* w, int ldw,
                                 const uint16_t* z, const float* mscale, const float* mshift, uint16_t* dx,
                                 float* partial, int nblk, hipStream_t s);
+// per-(device, stream role) split-K workspaces for the conv kernel (bn.hip): an fp32 slab of at least
+// `floats` elements and `n` zeroed self-resetting tickets; null if unavailable (e.g. would have to
+// grow during a graph capture)
+float* dlmpi_splitk_slab(hipStream_t s, size_t floats);
+int* dlmpi_splitk_tickets(hipStream_t s, int n);
 hipError_t dlmpi_avgpool_fwd(const uint16_t* x, int N, int HW, int C, uint16_t* y, hipStream_t s);
 hipError_t dlmpi_avgpool_bwd(const uint16_t* dy, int N, int HW, int C, uint16_t* dx, hipStream_t s);
 hipError_t dlmpi_nchw_to_nhwc(const float* x, int N, int C, int H, int W, int Cpad, uint16_t* y, hipStream_t s);

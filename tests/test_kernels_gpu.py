@@ -43,6 +43,8 @@ CONV_SHAPES = [
     (2, 14, 14, 256, 512, 1, 2, 0),    # downsample 1x1 stride 2
     (1, 16, 24, 192, 64, 3, 1, 1),     # UNet decoder level-1 concat width
     (2, 15, 20, 512, 1024, 3, 1, 1),   # UNet bottleneck at the reference 240x320 scale
+    (2, 4, 4, 512, 512, 3, 1, 1),      # tiny grid, 72 K-steps: in-launch split-K (8 slices)
+    (4, 4, 4, 256, 256, 3, 2, 1),      # split-K with stride-2 data-gradient phases
 ]
 
 
@@ -221,9 +223,9 @@ def test_unet_head_1ch():
     assert _rel(o, orf) < 1e-2
 
 
-def test_convT():
+@pytest.mark.parametrize("N,H,W,Ci,Co", [(2, 8, 12, 256, 256), (2, 4, 4, 1024, 512)])   # 2nd: split-K
+def test_convT(N, H, W, Ci, Co):
     nb, rb = _be()
-    N, H, W, Ci, Co = 2, 8, 12, 256, 256
     x, xr = _act(N, H, W, Ci)
     wf = (torch.randn(Co, 2, 2, Ci, device=DEV) / Ci ** 0.5).to(torch.bfloat16)
     bias = torch.randn(Co, device=DEV)
