@@ -62,6 +62,8 @@ def main():
     ap.add_argument("--breakdown", type=int, default=0,
                     help="N > 0: after the timed steps, N more steps with HIP-event phase timing (forward / "
                          "backward / exposed all-reduce wait / optimizer), printed to stderr")
+    ap.add_argument("--mem", type=int, default=0, help="1: print caching-allocator statistics (peak allocated / "
+                                                       "reserved GB, allocation retries) to stderr")
     ap.add_argument("--backend", default="rccl", help="rccl (default); gloo + DLMPI_GLOO_DEVICE=cuda rehearses "
                                                       "several ranks on one GPU")
     args = ap.parse_args()
@@ -159,6 +161,14 @@ def main():
             print(json.dumps({"breakdown_ms_per_step": bd, "max_over_ranks": {"comm_exposed": float(bdt[0]),
                                                                              "step": float(bdt[1])},
                               "n_gpus": world, "config": args.config}), file=sys.stderr, flush=True)
+    if args.mem and comm.rank == 0:
+        ms = torch.cuda.memory_stats(dev)
+        print(json.dumps({"mem": {"peak_allocated_gb": round(ms.get("allocated_bytes.all.peak", 0) / 2 ** 30, 2),
+                                  "peak_reserved_gb": round(ms.get("reserved_bytes.all.peak", 0) / 2 ** 30, 2),
+                                  "alloc_retries": ms.get("num_alloc_retries", 0),
+                                  "ooms": ms.get("num_ooms", 0),
+                                  "device_total_gb": round(torch.cuda.get_device_properties(dev).total_memory / 2 ** 30, 1)}}),
+              file=sys.stderr, flush=True)
     if comm.rank == 0:
         headline = args.config == "resnet50" and cfg == PRESETS["resnet50"]
         print(json.dumps({
