@@ -42,7 +42,15 @@ def grad_side(be, *tensors):
     is issued here, so a bucket's all-reduce always fences on the side stream, which has waited
     for the main stream's BN-parameter gradients.  ``tensors``: buffers read on the side stream
     (kept alive for it in the caching allocator).  The engine backward joins the side stream
-    before the optimizer (``_EngineFn.backward``)."""
+    before the optimizer (``_EngineFn.backward``).
+
+    Keeping them alive: by default (``DLMPI_STREAM_HOLD=1``) the buffers are held in ``be.held``
+    until that join and then dropped, so their blocks go back to the main stream's pool already
+    ordered after the side-stream work.  ``record_stream`` instead defers each block's reuse to an
+    event the host polls only at the next allocation; the host runs a whole backward ahead of the
+    GPU, so during backward nearly every freed block was still pending, every allocation took fresh
+    memory, and at UNet 1024^2 the cache grew to 170-272 GB reserved for 53 GB allocated with
+    step times from 146 to 871 ms (profiles/r1_stream_hold)."""
     side = getattr(be, "side_stream", None)
     if side is None:
         yield
@@ -50,13 +58,25 @@ def grad_side(be, *tensors):
     side.wait_stream(torch.cuda.current_stream())
     with torch.cuda.stream(side):
         yield
+    if _STREAM_HOLD:
+        be.held.extend(t for t in tensors if t is not None)
+        return
     for t in tensors:
-        t.record_stream(side)
+        if t is not None:
+            t.record_stream(side)
 
 
 def record_on(stream, *objs):
     """Mark every tensor (or Act buffer) inside ``objs`` (nested tuples / lists allowed) as used on
-    ``stream``, so the caching allocator does not recycle it before that stream's work is done."""
+    ``stream``, so the caching allocator does not recycle it before that stream's work is done.
+
+    With ``DLMPI_STREAM_HOLD=1`` (default) this is a no-op: its callers (the ResNet downsample
+    branch, models/resnet.py:_BlockExec) keep the main-pool tensors they hand to the branch stream
+    referenced until the main stream has waited for it, and the branch stream waits for the main
+    stream every time it is entered, so a branch-pool block freed after a main-stream read is only
+    reused by branch work ordered after that read."""
+    if _STREAM_HOLD:
+        return
     for o in objs:
         if o is None:
             continue
@@ -68,6 +88,9 @@ def record_on(stream, *objs):
         elif isinstance(o, (tuple, list)):
             record_on(stream, *o)
 
+
+# DLMPI_STREAM_HOLD=0: cross-stream buffer lifetimes through record_stream instead (A/B; grad_side)
+_STREAM_HOLD = os.environ.get("DLMPI_STREAM_HOLD", "1") != "0"
 
 # DLMPI_OUTER_DGRAD=0: one-output-channel 1x1 data gradients through the GEMM kernel (A/B)
 _OUTER_DGRAD = os.environ.get("DLMPI_OUTER_DGRAD", "1") != "0"
@@ -403,6 +426,9 @@ class _EngineFn(torch.autograd.Function):
             side = getattr(mod._be, "side_stream", None)
             if side is not None:   # every parameter gradient is final before the optimizer runs
                 torch.cuda.current_stream().wait_stream(side)
+            held = getattr(mod._be, "held", None)
+            if held:   # buffers read on the side stream: freed now, ordered after it (grad_side)
+                held.clear()
         with trace_range("dlmpi.ddp_finalize"):
             mod._arena.end_backward()
         return None, None, None

@@ -46,6 +46,7 @@ class NativeBackend:
         self.C = native()
         self.device = torch.device(device)
         self._cast_cache = {}
+        self.held = []   # buffers read on the side stream, dropped at the backward's join (engine.grad_side)
         # parameter-gradient work (weight-gradient GEMMs + split reductions, DDP bucket launches)
         # runs on this side stream, off the data-gradient critical path (models/engine.py:grad_side);
         # DLMPI_WGRAD_STREAM=0 keeps everything on the current stream
