@@ -138,9 +138,11 @@ def clip_grad_norm_(parameters, max_norm: float, norm_type: float = 2.0, optimiz
     """L2 gradient clipping without a host synchronisation.  Returns the total norm as a device
     tensor.  With ``optimizer`` (our Adam) the clip coefficient is also handed to it so a
     non-finite norm skips the update (the same decision on every rank, because gradients are
-    identical after the all-reduce)."""
-    if norm_type != 2.0:
-        raise NotImplementedError("only the L2 norm is fused")
+    identical after the all-reduce).
+
+    ``norm_type`` 2 runs the fused single-pass kernel; any other p (including ``inf``) is the
+    torch.nn.utils.clip_grad_norm_ contract computed with device-side torch reductions (still no
+    host synchronisation, still capturable)."""
     params = [p for p in parameters if p.grad is not None] if not isinstance(parameters, torch.Tensor) \
         else [parameters]
     a = _single_arena(params)
@@ -148,7 +150,19 @@ def clip_grad_norm_(parameters, max_norm: float, norm_type: float = 2.0, optimiz
     be = a.backend if a is not None else make_backend(dev)
     norm = torch.empty(1, dtype=torch.float32, device=dev)
     coef = torch.empty(2, dtype=torch.float32, device=dev)
-    if a is not None:
+    if float(norm_type) != 2.0:
+        grads = [a.grad] if a is not None else [p.grad.reshape(-1) for p in params]
+        p = float(norm_type)
+        if p == float("inf"):
+            n = torch.stack([g.float().abs().max() for g in grads]).max()
+        else:
+            n = torch.stack([g.double().abs().pow(p).sum() for g in grads]).sum().pow(1.0 / p).float()
+        norm.copy_(n.reshape(1))
+        coef[0] = torch.clamp(max_norm / (n + 1e-6), max=1.0)
+        coef[1] = (~torch.isfinite(n)).float()
+        for g in grads:
+            g.mul_(coef[0].to(g.dtype))
+    elif a is not None:
         be.grad_norm(a.grad, float(max_norm), norm, coef)
         be.scale_(a.grad, coef)
     else:

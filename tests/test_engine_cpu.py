@@ -124,3 +124,25 @@ def test_resnet50_fused_bn_backward_matches_torch_and_unfused():
     cross_entropy(m2(x.double()), y).backward()
     for (n, p1), (_, p2) in zip(m1.named_parameters(), m2.named_parameters()):
         assert _err(p1.grad, p2.grad) < 1e-9, n
+
+
+@pytest.mark.parametrize("norm_type", [1.0, 2.0, 3.0, float("inf")])
+def test_clip_grad_norm_matches_torch(norm_type):
+    """clip_grad_norm_ for every p against torch.nn.utils.clip_grad_norm_ (arena-backed model)."""
+    from deeplearning_mpi_amd.models import resnet18
+    from deeplearning_mpi_amd.ops import cross_entropy
+    from deeplearning_mpi_amd.optim import clip_grad_norm_
+
+    torch.manual_seed(0)
+    m = resnet18(num_classes=10)
+    loss = cross_entropy(m(torch.randn(2, 3, 32, 32)), torch.tensor([1, 7]))
+    loss.backward()
+    ref = [p.grad.detach().clone().requires_grad_(False) for p in m.parameters()]
+    shadows = [torch.zeros_like(g, requires_grad=True) for g in ref]
+    for s, g in zip(shadows, ref):
+        s.grad = g.clone()
+    want = torch.nn.utils.clip_grad_norm_(shadows, 0.5, norm_type=norm_type)
+    got = clip_grad_norm_(m.parameters(), 0.5, norm_type=norm_type)
+    torch.testing.assert_close(got.double(), want.double(), rtol=1e-4, atol=1e-6)
+    for p, s in zip(m.parameters(), shadows):
+        torch.testing.assert_close(p.grad, s.grad, rtol=1e-4, atol=1e-7)
