@@ -22,30 +22,40 @@ __global__ __launch_bounds__(256) void cast_weights_kernel(const CastEntry* __re
   const int sub = mb.y, nsub = mb.z;
   const int D0 = e.d[0], D1 = e.d[1], D2 = e.d[2], D3 = e.d[3];
   const int64_t n = (int64_t)D0 * D1 * D2 * D3;
-  if (e.st[0] == 1 && e.st[3] != 1 && D0 >= 16 && D3 >= 16) {
-    const int t0n = (D0 + 63) / 64, t3n = (D3 + 63) / 64;
-    const int64_t ntiles = (int64_t)D1 * D2 * t0n * t3n;
+  // Transpose path.  Besides the 1x1 case (source unit stride on d0) it takes any destination
+  // whose d0..d2 are jointly contiguous in the source, e.g. the 3x3 data-gradient copy
+  // [K][C][R][S] -> [C][R][S][K], which is a plain [K][C*R*S] -> [C*R*S][K] transpose: the merged
+  // rows are tiled 64x64 like the 1x1 case instead of gathered at a C*R*S stride per lane.
+  const bool merged = e.st[2] == 1 && e.st[1] == D2 && e.st[0] == (int64_t)D1 * D2 && D1 * D2 > 1 &&
+                      e.valid[1] == D1 && e.valid[2] == D2;
+  if (((e.st[0] == 1 && D0 >= 16) || (merged && D0 * D1 * D2 >= 16)) && e.st[3] != 1 && D3 >= 16) {
+    const int M0 = merged ? D0 * D1 * D2 : D0, M1 = merged ? 1 : D1, M2 = merged ? 1 : D2;
+    const int V0 = merged ? e.valid[0] * D1 * D2 : e.valid[0];
+    const int V1 = merged ? 1 : e.valid[1], V2 = merged ? 1 : e.valid[2];
+    const int64_t S0 = 1, S1 = merged ? 0 : e.st[1], S2 = merged ? 0 : e.st[2];
+    const int t0n = (M0 + 63) / 64, t3n = (D3 + 63) / 64;
+    const int64_t ntiles = (int64_t)M1 * M2 * t0n * t3n;
     const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;   // 64 x 4
     for (int64_t t = sub; t < ntiles; t += nsub) {
       int64_t r = t;
       const int b3 = (int)(r % t3n); r /= t3n;
       const int b0 = (int)(r % t0n); r /= t0n;
-      const int i2 = (int)(r % D2);
-      const int i1 = (int)(r / D2);
-      const bool v12 = i1 < e.valid[1] && i2 < e.valid[2];
+      const int i2 = (int)(r % M2);
+      const int i1 = (int)(r / M2);
+      const bool v12 = i1 < V1 && i2 < V2;
       // read: i0 = b0*64 + tx (unit stride in the source), i3 = b3*64 + ty + 4k
       for (int k = 0; k < 16; ++k) {
         const int i0 = b0 * 64 + tx, i3 = b3 * 64 + ty + 4 * k;
         float v = 0.f;
-        if (v12 && i0 < e.valid[0] && i3 < e.valid[3])
-          v = e.src[i0 * e.st[0] + i1 * e.st[1] + i2 * e.st[2] + i3 * e.st[3]];
+        if (v12 && i0 < V0 && i3 < e.valid[3])
+          v = e.src[i0 * S0 + i1 * S1 + i2 * S2 + i3 * e.st[3]];
         tile[ty + 4 * k][tx] = v;
       }
       __syncthreads();
       for (int k = 0; k < 16; ++k) {
         const int i3 = b3 * 64 + tx, i0 = b0 * 64 + ty + 4 * k;
-        if (i0 < D0 && i3 < D3)
-          e.dst[(((int64_t)i0 * D1 + i1) * D2 + i2) * D3 + i3] = f2bf(tile[tx][ty + 4 * k]);
+        if (i0 < M0 && i3 < D3)
+          e.dst[(((int64_t)i0 * M1 + i1) * M2 + i2) * D3 + i3] = f2bf(tile[tx][ty + 4 * k]);
       }
       __syncthreads();
     }

@@ -460,3 +460,21 @@ def test_losses_eval_optim():
     nb.grad_norm(g, 1.0, nrm, coef)
     rb.grad_norm(g, 1.0, nrm2, coef2)
     assert _rel(nrm, nrm2) < 1e-5 and _rel(coef, coef2) < 1e-5
+
+
+@pytest.mark.parametrize("model", ["resnet50", "unet1"])
+def test_cast_weights_all_layouts(model):
+    """Multi-tensor weight re-layout + cast (cast.hip) for every entry of a real model -- 1x1,
+    3x3 and 7x7 forward / data-gradient copies, transposed-conv copies, the 1-channel UNet input
+    conv (merged-row transpose path) -- bit-exact against the torch reference re-layout."""
+    from deeplearning_mpi_amd.models import UNet, resnet50
+
+    torch.manual_seed(0)
+    m = (resnet50(num_classes=1000) if model == "resnet50" else UNet(out_classes=1, in_channels=1)).to(DEV)
+    a = m.arena
+    a.refresh(force=True)
+    torch.cuda.synchronize()
+    got = a.compute.clone()
+    want = torch.zeros_like(a.compute)
+    RefBackend(DEV, torch.float32).cast_weights(a._entries, a._compute_total, want)
+    assert torch.equal(got, want)
