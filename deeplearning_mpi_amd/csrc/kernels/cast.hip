@@ -61,6 +61,33 @@ __global__ __launch_bounds__(256) void cast_weights_kernel(const CastEntry* __re
     }
     return;
   }
+  // Direct path.  When the entry's destination and source extents fit 32-bit indices (every
+  // conv / linear weight does) and rows are a multiple of 4 wide, each lane produces 4
+  // consecutive destination elements with one 8-byte store and one 32-bit index decomposition
+  // (instead of three 64-bit divisions per element).
+  const int64_t smax = (int64_t)(e.valid[0] - 1) * e.st[0] + (int64_t)(e.valid[1] - 1) * e.st[1] +
+                       (int64_t)(e.valid[2] - 1) * e.st[2] + (int64_t)(e.valid[3] - 1) * e.st[3];
+  if ((D3 & 3) == 0 && n < (1ll << 31) && smax < (1ll << 31) && ((uintptr_t)e.dst & 7) == 0) {
+    const uint32_t nq = (uint32_t)(n >> 2);
+    const int s0 = (int)e.st[0], s1 = (int)e.st[1], s2 = (int)e.st[2], s3 = (int)e.st[3];
+    const uint32_t uD3 = D3, uD2 = D2, uD1 = D1;
+    for (uint32_t q = sub * blockDim.x + threadIdx.x; q < nq; q += nsub * blockDim.x) {
+      const uint32_t i = q * 4u;
+      uint32_t r = i / uD3;
+      const int i3 = (int)(i - r * uD3);
+      const uint32_t r2 = r / uD2;
+      const int i2 = (int)(r - r2 * uD2);
+      const int i0 = (int)(r2 / uD1);
+      const int i1 = (int)(r2 - (uint32_t)i0 * uD1);
+      const bool v012 = i0 < e.valid[0] && i1 < e.valid[1] && i2 < e.valid[2];
+      const int base = i0 * s0 + i1 * s1 + i2 * s2 + i3 * s3;
+      float v[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v[j] = (v012 && i3 + j < e.valid[3]) ? e.src[base + j * s3] : 0.f;
+      *reinterpret_cast<u32x2*>(e.dst + i) = u32x2{pack2bf(v[0], v[1]), pack2bf(v[2], v[3])};
+    }
+    return;
+  }
   for (int64_t i = sub * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)nsub * blockDim.x) {
     int64_t r = i;
     const int i3 = (int)(r % D3);
