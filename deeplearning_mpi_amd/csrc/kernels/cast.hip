@@ -22,17 +22,11 @@ __global__ __launch_bounds__(256) void cast_weights_kernel(const CastEntry* __re
   const int sub = mb.y, nsub = mb.z;
   const int D0 = e.d[0], D1 = e.d[1], D2 = e.d[2], D3 = e.d[3];
   const int64_t n = (int64_t)D0 * D1 * D2 * D3;
-  // Transpose path.  Besides the 1x1 case (source unit stride on d0) it takes any destination
-  // whose d0..d2 are jointly contiguous in the source, e.g. the 3x3 data-gradient copy
-  // [K][C][R][S] -> [C][R][S][K], which is a plain [K][C*R*S] -> [C*R*S][K] transpose: the merged
-  // rows are tiled 64x64 like the 1x1 case instead of gathered at a C*R*S stride per lane.
-  const bool merged = e.st[2] == 1 && e.st[1] == D2 && e.st[0] == (int64_t)D1 * D2 && D1 * D2 > 1 &&
-                      e.valid[1] == D1 && e.valid[2] == D2;
-  if (((e.st[0] == 1 && D0 >= 16) || (merged && D0 * D1 * D2 >= 16)) && e.st[3] != 1 && D3 >= 16) {
-    const int M0 = merged ? D0 * D1 * D2 : D0, M1 = merged ? 1 : D1, M2 = merged ? 1 : D2;
-    const int V0 = merged ? e.valid[0] * D1 * D2 : e.valid[0];
-    const int V1 = merged ? 1 : e.valid[1], V2 = merged ? 1 : e.valid[2];
-    const int64_t S0 = 1, S1 = merged ? 0 : e.st[1], S2 = merged ? 0 : e.st[2];
+  // Transpose path (source unit stride on d0, e.g. the KRSC -> CRSK data-gradient copy).
+  if (e.st[0] == 1 && e.st[3] != 1 && D0 >= 16 && D3 >= 16) {
+    const int M0 = D0, M1 = D1, M2 = D2;
+    const int V0 = e.valid[0], V1 = e.valid[1], V2 = e.valid[2];
+    const int64_t S0 = 1, S1 = e.st[1], S2 = e.st[2];
     const int t0n = (M0 + 63) / 64, t3n = (D3 + 63) / 64;
     const int64_t ntiles = (int64_t)M1 * M2 * t0n * t3n;
     const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;   // 64 x 4
