@@ -12,7 +12,9 @@ if [ -n "$TESTS" ]; then
 fi
 for i in $(seq 1 ${AB_REPS:-3}); do
   for c in ${AB_CONFIGS:-resnet50}; do
-    for v in old new; do
+    # alternate which build runs first: a fixed order biases the A/B by ~0.4 % (profiles/r1_cast_transpose)
+    order="old new"; [ $((i % 2)) -eq 0 ] && order="new old"
+    for v in $order; do
       b=bench.py; [ $v = old ] && b=ab_old/bench.py
       timeout -k 10 300 python $b --config $c --steps ${AB_STEPS:-10} --warmup 3 > gpurun_out/bab/${c}_${v}_$i.log 2>&1 || { echo "bench $c $v rc=$?"; tail -20 gpurun_out/bab/${c}_${v}_$i.log; exit 1; }
       echo "$c $v #$i $(grep -o '"value": [0-9.]*' gpurun_out/bab/${c}_${v}_$i.log)"
