@@ -16,7 +16,15 @@ The other BASELINE.json configs are presets (``--config``):
                   /root/reference/pytorch/resnet/main.py:36-54,164)
 
 Usage:  python bench.py [--gpus N] [--steps K] [--warmup W] [--config NAME] [--graph 1] [--breakdown N]
-        (N > 1: launched by torch.distributed.run / torchrun or mpirun, one rank per GPU)
+
+Launch: one rank per GPU.  Under torch.distributed.run / torchrun or mpirun the ranks come from the
+launcher's environment and ``--gpus`` must equal the world size (checked; a mismatch exits 2).
+Without a launcher environment and N > 1, this process starts the N ranks itself BEFORE importing
+torch or touching a GPU (``--launcher torchrun`` (default) or ``mpirun``, rendezvous at 127.0.0.1,
+``HSA_ENABLE_IPC_MODE_LEGACY=0`` exported for dmabuf-only hosts), waits for them and exits with the
+first non-zero return code -- the reference's launcher likewise spawns ``nproc_per_node`` workers
+itself (/root/reference/pytorch/unet/run.sh:100-112).  ``--backend gloo`` is a CPU dry run of the
+same multi-rank path (gloo all-reduce, CPU reference backend).
 Prints ONE JSON line on rank 0.
 """
 from __future__ import annotations
@@ -24,8 +32,14 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import shutil
+import socket
+import subprocess
 import sys
 import time
+
+# multi-process RCCL on dmabuf-only hosts (read by the HSA runtime at its first use, which is later)
+os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 if ROOT not in sys.path:
@@ -47,6 +61,35 @@ PRESETS = {
 }
 
 
+_LAUNCH_ENV = ("RANK", "WORLD_SIZE", "OMPI_COMM_WORLD_RANK", "PMI_RANK", "PMIX_RANK", "MV2_COMM_WORLD_RANK")
+
+
+def _under_launcher() -> bool:
+    return any(os.environ.get(k) not in (None, "") for k in _LAUNCH_ENV)
+
+
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n: int, launcher: str, argv) -> int:
+    """Start ``n`` ranks of this script as child processes (no torch import, no GPU touched in this
+    process) and return the first non-zero exit code (0 if all ranks succeeded)."""
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", MASTER_ADDR="127.0.0.1")
+    env["PYTHONPATH"] = ROOT + (os.pathsep + env["PYTHONPATH"] if env.get("PYTHONPATH") else "")
+    script = os.path.abspath(__file__)
+    if launcher == "mpirun":
+        mpirun = shutil.which("mpirun") or "/opt/conda/bin/mpirun"
+        cmd = [mpirun, "-n", str(n), sys.executable, script, *argv]
+    else:
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", str(n),
+               "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), script, *argv]
+    print(f"[bench] launching {n} ranks: {' '.join(cmd)}", file=sys.stderr, flush=True)
+    return subprocess.call(cmd, env=env)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -64,9 +107,13 @@ def main():
                          "backward / exposed all-reduce wait / optimizer), printed to stderr")
     ap.add_argument("--mem", type=int, default=0, help="1: print caching-allocator statistics (peak allocated / "
                                                        "reserved GB, allocation retries) to stderr")
-    ap.add_argument("--backend", default="rccl", help="rccl (default); gloo + DLMPI_GLOO_DEVICE=cuda rehearses "
-                                                      "several ranks on one GPU")
+    ap.add_argument("--backend", default="rccl", help="rccl (default); gloo: CPU dry run of the multi-rank path "
+                                                      "(gloo + DLMPI_GLOO_DEVICE=cuda rehearses several ranks on one GPU)")
+    ap.add_argument("--launcher", default="torchrun", choices=("torchrun", "mpirun"),
+                    help="how --gpus N > 1 starts its ranks when not already under a launcher")
     args = ap.parse_args()
+    if args.gpus > 1 and not _under_launcher():
+        sys.exit(launch_ranks(args.gpus, args.launcher, sys.argv[1:]))
     cfg = dict(PRESETS[args.config])
     for k in ("arch", "batch", "image", "classes"):
         if getattr(args, k) is not None:
@@ -83,6 +130,16 @@ def main():
     comm = dl.init_distributed(args.backend)
     world = comm.world_size
     dev = comm.device
+    if world != args.gpus:
+        print(f"[bench] --gpus {args.gpus} but the launcher started {world} ranks", file=sys.stderr, flush=True)
+        sys.exit(2)
+    if world > 1 and args.backend in ("rccl", "nccl") and "rccl" not in comm.backend:
+        print(f"[bench] expected the RCCL data plane, got {comm.backend}", file=sys.stderr, flush=True)
+        sys.exit(2)
+
+    def sync():
+        if dev.type == "cuda":
+            torch.cuda.synchronize()
     torch.manual_seed(0)
     shape = (cfg["cin"], cfg["image"], cfg["image"])
     if cfg["task"] == "cls":
@@ -121,12 +178,12 @@ def main():
     for _ in range(args.warmup):
         step()
     comm.barrier()
-    torch.cuda.synchronize()
+    sync()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         loss = step()
     comm.barrier()
-    torch.cuda.synchronize()
+    sync()
     dt = time.perf_counter() - t0
     tmax = torch.tensor([dt], dtype=torch.float64, device=dev)
     comm.allreduce(tmax, "max")
@@ -161,7 +218,7 @@ def main():
             print(json.dumps({"breakdown_ms_per_step": bd, "max_over_ranks": {"comm_exposed": float(bdt[0]),
                                                                              "step": float(bdt[1])},
                               "n_gpus": world, "config": args.config}), file=sys.stderr, flush=True)
-    if args.mem and comm.rank == 0:
+    if args.mem and comm.rank == 0 and dev.type == "cuda":
         ms = torch.cuda.memory_stats(dev)
         print(json.dumps({"mem": {"peak_allocated_gb": round(ms.get("allocated_bytes.all.peak", 0) / 2 ** 30, 2),
                                   "peak_reserved_gb": round(ms.get("reserved_bytes.all.peak", 0) / 2 ** 30, 2),
@@ -182,12 +239,13 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": (round(ips / BASELINE_VALUE, 4) if (BASELINE_VALUE and headline) else None),
-            "dtype": "bf16",
+            "dtype": "bf16" if model._be.act_dtype == torch.bfloat16 else str(model._be.act_dtype).replace("torch.", ""),
             "data": f"synthetic (random {'x'.join(map(str, shape))} inputs / "
                     f"{'labels' if cfg['task'] == 'cls' else 'binary masks'} generated on device, random-init weights)",
             "config": {"model": cfg["arch"], "global_batch": global_batch, "seq_len": None,
                        "image": cfg["image"], "in_channels": cfg["cin"], "per_gpu_batch": cfg["batch"],
-                       "parallelism": f"dp{world}", "optimizer": optname, "hipgraph": bool(args.graph),
+                       "parallelism": f"dp{world}", "backend": comm.backend, "device": dev.type,
+                       "optimizer": optname, "hipgraph": bool(args.graph),
                        "final_loss": round(lossv, 4)},
         }), flush=True)
     dl.destroy_distributed()

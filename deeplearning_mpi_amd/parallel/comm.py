@@ -2,7 +2,7 @@
 
 * :class:`RcclCommunicator` -- the GPU data plane: our native RCCL communicator (``_C.RcclComm``)
   over xGMI with its own comm stream; RCCL unique id distributed by MPI_Bcast (mpirun) or the
-  gloo control plane (torchrun).
+  launcher's TCPStore (torchrun).  No torch process group exists on this path.
 * :class:`TorchCommunicator` -- ``torch.distributed`` gloo group (CPU tensors; tests, plumbing).
 * :class:`MPICommunicator` -- host MPI collectives through ``_mpi`` (the CPU hello-world path).
 * :class:`SingleCommunicator` -- world size 1, all collectives are no-ops.
@@ -142,8 +142,7 @@ class RcclCommunicator(Communicator):
 
     def destroy(self):
         self.c.destroy()
-        if dist.is_initialized():
-            dist.destroy_process_group()
+        self.control = None
 
 
 def _make_torch_bucket_comm(group, world_size):
@@ -316,6 +315,9 @@ def init_distributed(backend: str = "auto", timeout_s: float = 1800.0, check: bo
 
 
 def _init(backend: str, timeout_s: float) -> Communicator:
+    # cross-process GPU memory sharing on dmabuf-only hosts; must be set before the HSA runtime
+    # starts (the first GPU call below)
+    os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
     info = detect_launcher()
     if info.launcher == "mpi":
         info = mpi_bring_up()
@@ -337,25 +339,43 @@ def _init(backend: str, timeout_s: float) -> Communicator:
         return SingleCommunicator(info, device)
     if be == "mpi":
         return MPICommunicator(info, "cpu")
-    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-    dist.init_process_group("gloo", rank=info.rank, world_size=info.world_size,
-                            timeout=datetime.timedelta(seconds=timeout_s))
-    if be == "gloo":
+    if be == "gloo" or gloo_gpu:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("gloo", rank=info.rank, world_size=info.world_size,
+                                timeout=datetime.timedelta(seconds=timeout_s))
         return TorchCommunicator(info, device)
+    # RCCL data plane: no torch process group at all, only the 128-byte unique id has to reach
+    # every rank before ncclCommInitRank
     from .._ext import native
 
     C = native()
+    store = None
     if info.launcher == "mpi":
-        # mpirun: the RCCL unique id travels by MPI_Bcast
+        # mpirun: the id travels by MPI_Bcast
         from .._ext import mpi
 
         uid = mpi().bcast_bytes(C.RcclComm.unique_id() if info.rank == 0 else b"", 0)
     else:
-        box = [C.RcclComm.unique_id() if info.rank == 0 else None]
-        dist.broadcast_object_list(box, src=0)
-        uid = box[0]
+        uid, store = uid_via_store(info, C.RcclComm.unique_id, timeout_s)
     nc = C.RcclComm(uid, info.rank, info.world_size, device.index)
-    return RcclCommunicator(info, device, nc)
+    return RcclCommunicator(info, device, nc, control_group=store)
+
+
+def uid_via_store(info, make_uid, timeout_s=1800.0):
+    """torchrun / env:// launch: the RCCL unique id goes through the launcher's c10d TCPStore (the
+    elastic agent's store when torchrun shares it), obtained with the same env:// rendezvous
+    ``init_process_group`` would use -- but no gloo/NCCL process group is created on top of it."""
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    store, _, _ = next(dist.rendezvous("env://", rank=info.rank, world_size=info.world_size,
+                                       timeout=datetime.timedelta(seconds=timeout_s)))
+    store.set_timeout(datetime.timedelta(seconds=timeout_s))
+    key = f"dlmpi/rccl_uid/{os.environ.get('TORCHELASTIC_RESTART_COUNT', '0')}"
+    if info.rank == 0:
+        uid = make_uid()
+        store.set(key, uid)
+    else:
+        uid = store.get(key)
+    return bytes(uid), store
 
 
 def get_comm() -> Communicator:
