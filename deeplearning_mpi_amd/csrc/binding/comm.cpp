@@ -2,8 +2,7 @@
 //
 // RcclComm: one RCCL communicator per process (one process per GPU, xGMI), bootstrapped from a
 // 128-byte ncclUniqueId that the launcher layer distributes (MPI_Bcast under mpirun, the c10d
-// TCPStore under torchrun).  Every collective is enqueued on a dedicated high-priority comm HIP
-// stream, ordered after the compute stream with an event, so bucket all-reduces overlap the rest
+// TCPStore under torchrun).  Every collective is enqueued on a dedicated comm HIP stream, ordered after the compute stream with an event, so bucket all-reduces overlap the rest
 // of the backward pass; wait() makes the compute stream wait on the comm stream (no host block).
 // Replaces c10d ProcessGroupNCCL of the reference (SURVEY.md §2.4, K1-K8 call sites §2.6).
 //
@@ -192,7 +191,12 @@ pybind11::bytes RcclComm::unique_id() {
 RcclComm::RcclComm(const std::string& uid, int rank, int size, int device) {
   if (uid.size() != sizeof(ncclUniqueId)) throw std::runtime_error("RcclComm: bad unique id size");
   hip_check(hipSetDevice(device), "hipSetDevice");
-  impl_ = std::make_unique<Impl>(c10::hip::getStreamFromPool(/*isHighPriority=*/true, (c10::DeviceIndex)device));
+  // Default priority: a high-priority stream inside a hipGraph capture was seen to segfault in
+  // capture_end on this ROCm build (profiles/r1_hipri_rejected), and the comm stream joins every
+  // captured DDP step.  DLMPI_COMM_HIPRI=1 opts back in.
+  const char* hp = std::getenv("DLMPI_COMM_HIPRI");
+  const bool hipri = hp != nullptr && std::atoi(hp) != 0;
+  impl_ = std::make_unique<Impl>(c10::hip::getStreamFromPool(hipri, (c10::DeviceIndex)device));
   impl_->rank = rank;
   impl_->size = size;
   impl_->device = device;

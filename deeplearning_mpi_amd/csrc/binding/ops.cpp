@@ -610,7 +610,7 @@ void adam_step(at::Tensor p, const at::Tensor& g, at::Tensor m, at::Tensor v, do
                const c10::optional<at::Tensor>& tstep) {
   check(dlmpi_adam(ptr<float>(p), ptr<float>(g), ptr<float>(m), ptr<float>(v), p.numel(), (float)lr, (float)b1,
                    (float)b2, (float)eps, (float)wd, adamw ? 1 : 0, (float)bc1, (float)bc2, optr<float>(clip),
-                   optr<float>(tstep), cur_stream()),
+                   optr<float>(tstep), cur_stream()),   // advanced in place unless skipped
         "adam");
 }
 // total L2 norm of a flat fp32 buffer -> norm_out[0]; coef_out = {min(1, max_norm/(norm+1e-6)), nonfinite}

@@ -216,7 +216,7 @@ hipError_t dlmpi_sgd(float* p, const float* g, float* m, int64_t n, float lr, fl
                      float wd, int nesterov, int first, const float* skip_flag, hipStream_t s);
 hipError_t dlmpi_adam(float* p, const float* g, float* m, float* v, int64_t n, float lr, float b1, float b2,
                       float eps, float wd, int adamw, float bc1, float bc2, const float* clip_coef,
-                      const float* tstep, hipStream_t s);   // tstep (device step count) overrides bc1/bc2
+                      float* tstep, hipStream_t s);   // tstep (device step count) overrides bc1/bc2
 hipError_t dlmpi_sumsq(const float* x, int64_t n, float* partial, int nblk, hipStream_t s);
 hipError_t dlmpi_clip_coef(const float* partial, int nblk, float max_norm, float* norm_out, float* coef_out,
                            hipStream_t s);

@@ -58,10 +58,11 @@ __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, const 
                                                    float b1, float b2, float eps, float wd, int adamw, float bc1,
                                                    float bc2, const float* __restrict__ clip_coef,
                                                    const float* __restrict__ tstep) {
+  // tstep = number of updates applied so far (device scalar): this update is number tstep + 1
   const float coef = clip_coef ? clip_coef[0] : 1.f;
   if (clip_coef && clip_coef[1] != 0.f) return;   // non-finite gradient norm: collective skip
   if (tstep) {   // step count on the device: bias corrections stay correct under hipGraph replay
-    const float t = *tstep;
+    const float t = *tstep + 1.f;
     bc1 = 1.f - powf(b1, t);
     bc2 = 1.f - powf(b2, t);
   }
@@ -72,6 +73,12 @@ __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, const 
     m[i] = mv;
     v[i] = vv;
   }
+}
+
+// After adam_kernel: count the update only if it was applied, so a collectively skipped step
+// (non-finite gradient norm) leaves every later bias correction exactly as if it never happened.
+__global__ void adam_step_advance_kernel(float* __restrict__ tstep, const float* __restrict__ clip_coef) {
+  if (threadIdx.x == 0 && !(clip_coef && clip_coef[1] != 0.f)) *tstep += 1.f;
 }
 
 __global__ __launch_bounds__(256) void sumsq_kernel(const float* __restrict__ x, int64_t n,
@@ -135,9 +142,10 @@ extern "C" hipError_t dlmpi_sgd(float* p, const float* g, float* m, int64_t n, f
 }
 extern "C" hipError_t dlmpi_adam(float* p, const float* g, float* m, float* v, int64_t n, float lr, float b1, float b2,
                                  float eps, float wd, int adamw, float bc1, float bc2, const float* clip_coef,
-                                 const float* tstep, hipStream_t s) {
+                                 float* tstep, hipStream_t s) {
   hipLaunchKernelGGL(adam_kernel, dim3(blocks_for(n)), dim3(256), 0, s, p, g, m, v, n, lr, b1, b2, eps, wd, adamw,
                      bc1, bc2, clip_coef, tstep);
+  if (tstep) hipLaunchKernelGGL(adam_step_advance_kernel, dim3(1), dim3(64), 0, s, tstep, clip_coef);
   return hipGetLastError();
 }
 extern "C" hipError_t dlmpi_sumsq(const float* x, int64_t n, float* partial, int nblk, hipStream_t s) {

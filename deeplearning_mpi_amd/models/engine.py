@@ -185,6 +185,7 @@ class ConvUnit:
             be.conv_fwd(x, wf, self.Kp, self.R, self.S, self.stride, self.pad, z, bias=self._bias_vec(), stats=stats)
             vec = torch.empty(4, self.Kp, dtype=be.dt, device=dev)
             scale, shift, mean, invstd = vec[0], vec[1], vec[2], vec[3]
+            self.arena.wait_buffers()   # DDP's asynchronous buffer broadcast must land first
             mom = bn.momentum
             if mom is None:   # cumulative moving average
                 mom = 1.0 / float(bn.num_batches_tracked.item())
@@ -453,7 +454,7 @@ class EngineModule(nn.Module):
         if self._arena is not None and self._arena.device == device and self._arena.valid():
             return self._arena
         self._be = make_backend(device, next(self.parameters()).dtype, self.precision)
-        self._arena = ParamArena(self, device, self._be)
+        self._arena = ParamArena(self, device, self._be, order_names=self._grad_ready_names())
         self._build_units(self._arena)
         self._arena.refresh(force=True)
         return self._arena
@@ -464,6 +465,20 @@ class EngineModule(nn.Module):
 
     def _build_units(self, arena):
         raise NotImplementedError
+
+    def _grad_ready_names(self):
+        """Parameter names in the order the engine backward announces them ready (the flat
+        gradient layout, hence the DDP bucket order).  None: reverse registration order."""
+        return None
+
+    @staticmethod
+    def unit_ready_names(conv: str, bn: str = None, conv_bias=False):
+        """The ``ready`` order of one ConvUnit (ConvUnit.bwd): BN weight, BN bias, conv bias, conv
+        weight; a ConvTUnit / bias-only unit: bias, weight."""
+        out = [f"{bn}.weight", f"{bn}.bias"] if bn else []
+        if conv_bias:
+            out.append(f"{conv}.bias")
+        return out + [f"{conv}.weight"]
 
     def forward(self, x):
         self.engine_setup(x.device)

@@ -213,6 +213,24 @@ class ResNet(EngineModule):
         return self.fc(x)
 
     # ------------------------------------------------------------------ engine
+    def _grad_ready_names(self):
+        """Backward order (_BlockExec.bwd): fc, then per block (last first) its last conv unit,
+        the middle units, the downsample branch (joined before conv1's data gradient), conv1;
+        finally the stem."""
+        un = self.unit_ready_names
+        names = un("fc", None, conv_bias=self.fc.bias is not None)
+        for li in (4, 3, 2, 1):
+            layer = getattr(self, f"layer{li}")
+            for bi in range(len(layer) - 1, -1, -1):
+                p = f"layer{li}.{bi}"
+                nconv = 3 if isinstance(layer[bi], Bottleneck) else 2
+                for k in range(nconv, 1, -1):
+                    names += un(f"{p}.conv{k}", f"{p}.bn{k}")
+                if layer[bi].downsample is not None:
+                    names += un(f"{p}.downsample.0", f"{p}.downsample.1")
+                names += un(f"{p}.conv1", f"{p}.bn1")
+        return names + un("conv1", "bn1")
+
     def _build_units(self, ar):
         self.cin_pad = padc(self.in_channels)
         if self.in_channels <= S2DConvUnit.CS and os.environ.get("DLMPI_STEM_S2D", "1") != "0":

@@ -104,6 +104,26 @@ class UNet(EngineModule):
         return self.conv_last(x)
 
     # ------------------------------------------------------------------ engine
+    def _grad_ready_names(self):
+        """Backward order (_engine_backward): the head, each decoder level from the top (its
+        DoubleConv's second then first unit, then its ConvTranspose2d), the bottleneck, the
+        encoder from the bottom."""
+        un = self.unit_ready_names
+
+        def dc(prefix):
+            b = f"{prefix}.double_conv"
+            return un(f"{b}.3", f"{b}.4", conv_bias=True) + un(f"{b}.0", f"{b}.1", conv_bias=True)
+
+        names = un("conv_last", None, conv_bias=self.conv_last.bias is not None)
+        for k in (1, 2, 3, 4):
+            names += dc(f"up_conv{k}.double_conv")
+            if self.up_sample_mode == "conv_transpose":
+                names += un(f"up_conv{k}.up_sample", None, conv_bias=True)
+        names += dc("double_conv")
+        for k in (4, 3, 2, 1):
+            names += dc(f"down_conv{k}.double_conv")
+        return names
+
     def _build_units(self, ar):
         self.cin_pad = padc(self.in_channels)
         downs = [self.down_conv1, self.down_conv2, self.down_conv3, self.down_conv4]

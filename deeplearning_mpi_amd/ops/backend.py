@@ -546,9 +546,10 @@ class RefBackend:
             if float(clip[1]) != 0:
                 return
             coef = clip[0]
-        if tstep is not None:
-            t = float(tstep.reshape(-1)[0])
+        if tstep is not None:   # tstep = updates applied so far; advanced only when this one is applied
+            t = float(tstep.reshape(-1)[0]) + 1
             bc1, bc2 = 1 - b1 ** t, 1 - b2 ** t
+            tstep.add_(1)
         g = g * coef
         if wd != 0:
             if adamw:

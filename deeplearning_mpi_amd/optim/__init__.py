@@ -116,12 +116,12 @@ class Adam(_FusedBase):
             b1, b2 = g["betas"]
             m = self._buf(key, "exp_avg", p)
             v = self._buf(key, "exp_avg_sq", p)
-            # the step count also lives on the device (read by the kernel), so a captured step
-            # replayed from a hipGraph keeps correct bias corrections
+            # the step count lives on the device: the kernel uses step + 1 and advances it only when
+            # the update is applied (a collective NaN/Inf skip leaves it unchanged), so a captured
+            # step replayed from a hipGraph keeps correct bias corrections
             st = self.state[key] if not isinstance(key, str) else self.state.setdefault(key, {})
             if "step" not in st:
                 st["step"] = torch.zeros(1, dtype=torch.float32, device=p.device)
-            st["step"].add_(1)
             self._be.adam(p, gr, m, v, g["lr"], b1, b2, g["eps"], g["weight_decay"], self.decoupled,
                           1 - b1 ** t, 1 - b2 ** t, self.clip, st["step"])
         if self._arena is not None:

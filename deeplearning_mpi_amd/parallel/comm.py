@@ -40,6 +40,12 @@ class Communicator:
     def broadcast(self, t, src=0):
         raise NotImplementedError
 
+    def broadcast_async(self, t, src=0):
+        """Start a broadcast; returns a callable that makes the caller's current stream wait for
+        it (None when the broadcast already completed, as on host backends)."""
+        self.broadcast(t, src)
+        return None
+
     def allgather(self, out, t):
         raise NotImplementedError
 
@@ -112,6 +118,12 @@ class RcclCommunicator(Communicator):
     def broadcast(self, t, src=0):
         self.c.broadcast(t, src, False)
         return t
+
+    def broadcast_async(self, t, src=0):
+        # enqueued on the comm stream behind the compute stream's prior work; the returned fence
+        # joins it back (no host block, capturable)
+        self.c.broadcast(t, src, True)
+        return self.c.wait
 
     def allgather(self, out, t):
         self.c.allgather(out, t.contiguous(), False)

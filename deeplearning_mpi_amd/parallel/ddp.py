@@ -16,7 +16,10 @@ MI355X-first differences:
   sized for RCCL rings over 7 point-to-point xGMI links (per-collective latency amortised), and a
   small last bucket (the stem / first-stage gradients, written last) so that little all-reduce
   work is left exposed once the backward pass ends;
-* the per-step buffer broadcast is ONE collective over the flat BatchNorm buffer.
+* the per-step buffer broadcast is ONE collective over the flat BatchNorm buffer, issued
+  asynchronously on the comm stream: the compute stream waits for it only right before the first
+  BatchNorm finalize reads the running statistics (``ParamArena.wait_buffers``), so the stem
+  convolution runs meanwhile instead of behind a latency-bound collective.
 """
 from __future__ import annotations
 
@@ -40,7 +43,7 @@ DEFAULT_LAST_BUCKET_MB = 4.0
 class DistributedDataParallel(nn.Module):
     def __init__(self, module: nn.Module, device_ids=None, output_device=None, broadcast_buffers=True,
                  bucket_cap_mb=None, first_bucket_cap_mb=None, comm=None, find_unused_parameters=False,
-                 gradient_as_bucket_view=True, last_bucket_cap_mb=None):
+                 gradient_as_bucket_view=True, last_bucket_cap_mb=None, _force_reducer=False):
         super().__init__()
         self.module = module
         self.comm = comm if comm is not None else get_comm()
@@ -61,7 +64,8 @@ class DistributedDataParallel(nn.Module):
         last = (last_bucket_cap_mb or DEFAULT_LAST_BUCKET_MB) * 2 ** 20
         self.bucket_bounds, self.param_bucket = self.arena.buckets(int(first), int(cap), int(last))
         self.reducer = None
-        if self.world_size > 1:
+        # _force_reducer (tests): run the bucketed all-reduce path even with one rank
+        if self.world_size > 1 or _force_reducer:
             from .._ext import native
 
             views = [self.arena.grad[s:e] for s, e in self.bucket_bounds]
@@ -120,6 +124,7 @@ class DistributedDataParallel(nn.Module):
     # ---------------------------------------------------------------- step
     def _finalize(self):
         self._queued = False
+        self.arena.wait_buffers()   # a forward without BatchNorm finalize never joined the K5 broadcast
         if self.reducer is not None:
             launched = self.reducer.launched()
             if self.timer is not None:   # exposed communication: the stream's wait for the last buckets
@@ -139,7 +144,11 @@ class DistributedDataParallel(nn.Module):
                   and self.module.training)
         if self.reducer is not None and self.module.training and self.broadcast_buffers and a.fbuf_total:
             with trace_range("dlmpi.ddp_buffer_broadcast"):
-                self.comm.broadcast(a.fbuf, 0)   # K5, one collective for every BN running stat
+                # K5, one collective for every BN running stat
+                if self._engine:
+                    a.buffer_fence = self.comm.broadcast_async(a.fbuf, 0)
+                else:
+                    self.comm.broadcast(a.fbuf, 0)
         if active:
             self.reducer.prepare_for_backward()
             a.hook = self.reducer.mark_ready

@@ -86,6 +86,10 @@ class CheckedCommunicator(Communicator):
         self._check("broadcast", t, src=src)
         return self.inner.broadcast(t, src)
 
+    def broadcast_async(self, t, src=0):
+        self._check("broadcast", t, src=src)
+        return self.inner.broadcast_async(t, src)
+
     def allgather(self, out, t):
         self._check("allgather", t)
         return self.inner.allgather(out, t)

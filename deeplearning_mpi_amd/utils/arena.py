@@ -1,8 +1,10 @@
 """ParamArena: flat, device-resident parameter / gradient / buffer storage.
 
 Every parameter of a model is re-homed into ONE fp32 buffer (and its gradient into ONE fp32
-gradient buffer) laid out in *reverse registration order* -- roughly the order in which the
-backward pass produces gradients.  Consequences (MI355X-first design):
+gradient buffer) laid out in the order in which the backward pass produces the gradients: the
+engine models declare that order (``EngineModule._grad_ready_names``, checked against the
+recorded ``ready`` sequence by tests/test_engine_cpu.py), other modules get reverse registration
+order.  Consequences (MI355X-first design):
 
 * DDP gradient buckets are contiguous slices of the flat gradient: all-reduced in place over RCCL,
   no pack/unpack (the reference's torch DDP Reducer copies grads into bucket buffers);
@@ -39,7 +41,7 @@ def _conv_like(m):
 class ParamArena:
     ALIGN = 16   # elements (64 bytes): every tensor starts on a 64-B boundary
 
-    def __init__(self, module: nn.Module, device, backend=None):
+    def __init__(self, module: nn.Module, device, backend=None, order_names=None):
         self.device = torch.device(device)
         self.backend = backend
         named = []
@@ -60,8 +62,15 @@ class ParamArena:
             elif isinstance(m, nn.ConvTranspose2d):
                 layout[id(m.weight)] = "convT"         # [Cin,Cout,kh,kw] stored as [Cin][kh][kw][Cout]
 
-        # flat layout in reverse registration order
+        # flat layout in gradient-ready order: declared names first, the rest in reverse registration
         order = list(range(len(self.params)))[::-1]
+        if order_names:
+            pos = {n: i for i, n in enumerate(self.names)}
+            first = [pos[n] for n in order_names if n in pos]
+            if len(set(first)) != len(first):
+                raise ValueError("ParamArena: duplicate names in order_names")
+            taken = set(first)
+            order = first + [i for i in order if i not in taken]
         self.offsets = [0] * len(self.params)
         off = 0
         for i in order:
@@ -118,6 +127,7 @@ class ParamArena:
         self.post_refresh = []      # callables run after every recast (derived weight layouts)
         self.hook = None            # reducer.mark_ready(param_index) during backward
         self.backward_end = None    # reducer.finalize() at the end of the engine backward
+        self.buffer_fence = None    # joins an in-flight broadcast of fbuf (DDP K5) before its first use
         self.zero_pending = False
 
     @staticmethod
@@ -172,6 +182,13 @@ class ParamArena:
             for p in ps:
                 if p is not None:
                     self.hook(self.index[id(p)])
+
+    def wait_buffers(self):
+        """Make the current stream wait for an in-flight update of the BN buffers (once)."""
+        f = self.buffer_fence
+        if f is not None:
+            self.buffer_fence = None
+            f()
 
     def end_backward(self):
         if self.backward_end is not None:

@@ -146,3 +146,31 @@ def test_clip_grad_norm_matches_torch(norm_type):
     torch.testing.assert_close(got.double(), want.double(), rtol=1e-4, atol=1e-6)
     for p, s in zip(m.parameters(), shadows):
         torch.testing.assert_close(p.grad, s.grad, rtol=1e-4, atol=1e-7)
+
+
+@pytest.mark.parametrize("name", ["resnet18", "resnet50", "resnet152", "unet", "unet_bilinear"])
+def test_flat_gradient_layout_follows_backward_ready_order(name):
+    """The DDP reducer launches buckets strictly in index order, so a bucket whose last gradient
+    arrives after a later bucket's would hold that later all-reduce back.  The flat layout (hence
+    the bucket order) must be exactly the order in which the engine backward announces gradients
+    ready -- recorded here through the reducer hook -- for every bucket split."""
+    from deeplearning_mpi_amd.models import ARCHS, UNet
+
+    torch.manual_seed(0)
+    if name.startswith("unet"):
+        m = UNet(out_classes=1, up_sample_mode="bilinear" if "bilinear" in name else "conv_transpose")
+        x = torch.randn(1, 3, 32, 32)
+    else:
+        m = ARCHS[name](num_classes=10)
+        x = torch.randn(2, 3, 32, 32)
+    a = m.arena
+    seq = []
+    out = m(x)
+    a.hook = seq.append
+    out.float().mean().backward()
+    a.hook = None
+    assert seq == a.order
+    for caps in ((2 << 20, 32 << 20, 4 << 20), (1 << 18, 1 << 20, 1 << 18)):
+        _, pb = a.buckets(*caps)
+        bseq = [pb[i] for i in seq]
+        assert bseq == sorted(bseq)
