@@ -27,7 +27,7 @@ from ..data import CIFAR10, CifarTransform, DeviceBatches, DeviceImageDataset, D
 from ..models import ARCHS
 from ..ops import CrossEntropyLoss, top1_correct
 from ..optim import SGD
-from ..utils.checkpoint import load_checkpoint, save_checkpoint
+from ..utils.checkpoint import load_checkpoint, resume_state, save_checkpoint, set_rng_state
 from ..utils.graphs import CapturedStep
 
 
@@ -59,13 +59,25 @@ def build_argparser(variant: str = "main") -> argparse.ArgumentParser:
                    help="resnet.py variant: evaluate/save before training on eval epochs")
     p.add_argument("--precision", default="bf16", choices=["bf16", "fp32"],
                    help="bf16: native gfx950 kernels; fp32: the same schedules on fp32 torch ops")
-    p.add_argument("--graph", action="store_true", help="replay each training step from a captured hipGraph")
+    p.add_argument("--graph", nargs="?", const="1", default="auto", choices=["auto", "0", "1"],
+                   help="replay each full-size training step from a captured hipGraph (ragged last batches run "
+                        "eagerly); auto = on for bf16 training on a GPU")
     p.add_argument("--data_on_device", default="auto", choices=["auto", "0", "1"],
                    help="keep CIFAR-10 resident in GPU memory and build each augmented batch with one kernel "
                         "(data/device.py); auto = on for GPU training on real data")
     p.add_argument("--benchmark_steps", type=int, default=0,
                    help="time this many steps on a synthetic device batch, print images/sec and exit")
     return p
+
+
+def use_graph(args, device) -> bool:
+    """--graph auto: capture the step when it runs on the native bf16 kernels of a GPU (the fp32
+    option runs stock torch ops, captured only on request)."""
+    if args.graph in (True, "1"):
+        return device.type == "cuda"
+    if args.graph in (False, "0"):
+        return False
+    return device.type == "cuda" and args.precision == "bf16"
 
 
 def set_random_seeds(seed: int):
@@ -101,8 +113,7 @@ def run(args) -> dict:
     model.precision = args.precision
     ddp = parallel.DistributedDataParallel(model, bucket_cap_mb=args.bucket_mb)
     model_filepath = os.path.join(args.model_dir, args.model_filename)
-    if args.resume:
-        load_checkpoint(ddp, model_filepath, map_location=device)
+    args.graph = use_graph(args, device)
 
     # the training step reads its batch from fixed tensors so that it can be captured (--graph)
     x_static = torch.empty((args.batch_size, 3, args.image_size, args.image_size) if args.synthetic else
@@ -136,6 +147,12 @@ def run(args) -> dict:
                                  pin_memory=pin)
     criterion = CrossEntropyLoss()
     optimizer = SGD(model.parameters(), lr=args.learning_rate, momentum=0.9, weight_decay=1e-5)
+    start_epoch = 0
+    if args.resume:
+        # weights (reference layout) + the sidecar: optimizer state, next epoch, RNG states
+        meta = load_checkpoint(ddp, model_filepath, map_location=device, optimizer=optimizer)
+        start_epoch = int(meta.get("next_epoch", 0))
+        set_rng_state(meta.get("rng"))
 
     def train_step(x, y):
         optimizer.zero_grad()
@@ -153,19 +170,19 @@ def run(args) -> dict:
 
     history = {"loss": [], "accuracy": [], "images_per_sec": []}
 
-    def eval_and_save(epoch):
+    def eval_and_save(epoch, next_epoch):
         accuracy = evaluate(model, device, test_loader)
-        save_checkpoint(ddp, model_filepath, rank=rank)
+        save_checkpoint(ddp, model_filepath, optimizer=optimizer, extra=resume_state(next_epoch), rank=rank)
         print("-" * 75)
         print("Epoch: {}, Accuracy: {}".format(epoch, accuracy))
         print("-" * 75)
         history["accuracy"].append(accuracy)
 
     try:
-        for epoch in range(args.num_epochs):
+        for epoch in range(start_epoch, args.num_epochs):
             sampler.set_epoch(epoch)
             if args.eval_before_train and epoch % args.eval_every == 0 and rank == 0:
-                eval_and_save(epoch)
+                eval_and_save(epoch, epoch)
             print("Local Rank: {}, Epoch: {}, Training ...".format(local_rank, epoch))
             ddp.train()
             loss_sum = torch.zeros((), device=device)
@@ -191,7 +208,7 @@ def run(args) -> dict:
             if rank == 0:
                 print(f"Epoch {epoch} throughput: {history['images_per_sec'][-1]:.1f} images/sec ({nb} steps)")
             if not args.eval_before_train and epoch % args.eval_every == 0 and rank == 0:
-                eval_and_save(epoch)
+                eval_and_save(epoch, epoch + 1)
             print(f"Epoch {epoch} completed")
     finally:
         parallel.destroy_distributed()

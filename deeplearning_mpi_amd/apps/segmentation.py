@@ -32,7 +32,8 @@ from ..models import UNet
 from ..ops import BCEWithLogitsLoss, dice_per_sample
 from ..optim import Adam, clip_grad_norm_
 from ..utils.graphs import CapturedStep
-from ..utils.checkpoint import load_checkpoint, save_checkpoint
+from ..utils.checkpoint import load_checkpoint, resume_state, save_checkpoint, set_rng_state
+from .classification import use_graph
 
 
 def build_argparser() -> argparse.ArgumentParser:
@@ -64,7 +65,9 @@ def build_argparser() -> argparse.ArgumentParser:
     p.add_argument("--bucket_mb", type=float, default=None)
     p.add_argument("--precision", default="bf16", choices=["bf16", "fp32"],
                    help="bf16: native gfx950 kernels; fp32: the same schedules on fp32 torch ops")
-    p.add_argument("--graph", action="store_true", help="replay each training step from a captured hipGraph")
+    p.add_argument("--graph", nargs="?", const="1", default="auto", choices=["auto", "0", "1"],
+                   help="replay each full-size training step from a captured hipGraph (ragged last batches run "
+                        "eagerly); auto = on for bf16 training on a GPU")
     p.add_argument("--benchmark_steps", type=int, default=0,
                    help="time this many steps on a synthetic device batch, print images/sec and exit")
     return p
@@ -190,10 +193,15 @@ def run(args) -> dict:
     model.precision = args.precision
     ddp = parallel.DistributedDataParallel(model, bucket_cap_mb=args.bucket_mb)
     model_filepath = os.path.join(args.model_dir, args.model_filename)
-    if args.resume:
-        load_checkpoint(ddp, model_filepath, map_location=device)
     optimizer = Adam(model.parameters(), lr=args.learning_rate)
     criterion = BCEWithLogitsLoss()
+    start_epoch = 0
+    if args.resume:
+        # weights (reference layout) + the sidecar: Adam moments and step, next epoch, RNG states
+        meta = load_checkpoint(ddp, model_filepath, map_location=device, optimizer=optimizer)
+        start_epoch = int(meta.get("next_epoch", 0))
+        set_rng_state(meta.get("rng"))
+    args.graph = use_graph(args, device)
 
     def train_step(images, masks):
         pred = ddp(images).squeeze(1)
@@ -218,7 +226,7 @@ def run(args) -> dict:
         print(f"Logging training progress to: {log.path}")
     log(f"Started training at {datetime.now()}")
     try:
-        for epoch in range(args.num_epochs):
+        for epoch in range(start_epoch, args.num_epochs):
             sampler.set_epoch(epoch)
             t0 = time.time()
             ddp.train()
@@ -244,7 +252,7 @@ def run(args) -> dict:
             log(f"Epoch {epoch + 1} | Loss: {avg_loss:.4f} | Duration: {time.time() - t0:.2f}s")
             if (epoch + 1) % args.eval_every == 0 and rank == 0:
                 dice = evaluate_model(model, device, test_loader)
-                save_checkpoint(ddp, model_filepath, rank=rank)
+                save_checkpoint(ddp, model_filepath, optimizer=optimizer, extra=resume_state(epoch + 1), rank=rank)
                 print("-" * 75)
                 print(f"Epoch {epoch + 1} Dice Score: {dice:.4f}")
                 print("-" * 75)
@@ -253,7 +261,7 @@ def run(args) -> dict:
         if rank == 0:
             print("\n" + "=" * 80 + "\nTRAINING COMPLETED - FINAL EVALUATION\n" + "=" * 80)
             final = evaluate_model(model, device, test_loader)
-            save_checkpoint(ddp, model_filepath, rank=rank)
+            save_checkpoint(ddp, model_filepath, optimizer=optimizer, extra=resume_state(args.num_epochs), rank=rank)
             print(f"FINAL DICE COEFFICIENT: {final:.4f}\n" + "=" * 80 + "\n")
             log("=" * 80)
             log("FINAL TRAINING RESULTS")

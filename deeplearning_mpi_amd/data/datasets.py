@@ -8,16 +8,14 @@ image/mask segmentation dataset of the reference UNet.
   ``torchvision.datasets.CIFAR10(download=False)`` (/root/reference/pytorch/resnet/main.py:89-92).
   Transforms identical to the reference: RandomCrop(32, padding=4), RandomHorizontalFlip,
   ToTensor, Normalize((0.4914, 0.4822, 0.4465), (0.2023, 0.1994, 0.2010)).
-* ``SegmentationDataset`` (alias ``CarvanaDataset``) -- same semantics as
-  /root/reference/pytorch/unet/data_loading.py:52-134: images/masks matched by stem, resized by
-  ``scale`` (bicubic / nearest), HWC->CHW, /255 when >1, mask values mapped to indices and
-  binarised (>0) to float32; returns ``{'image', 'mask'}``.
+* ``SegmentationDataset`` (alias ``CarvanaDataset``) -- the training targets of
+  /root/reference/pytorch/unet/data_loading.py:52-134 (see the class docstring for how they are
+  produced here); returns ``{'image', 'mask'}``.
 """
 from __future__ import annotations
 
 import os
 import pickle
-from os import listdir
 from os.path import isfile, join, splitext
 
 import numpy as np
@@ -129,85 +127,174 @@ class CIFAR10(Dataset):
 
 
 # ----------------------------------------------------------------------------- segmentation
-def load_image(filename):
+_ARRAY_EXT = {".npy", ".pt", ".pth"}
+
+
+def read_array(path) -> np.ndarray:
+    """Decode one image or mask file to a numpy array (HW or HWC).  ``.npy`` through numpy without
+    pickles, ``.pt``/``.pth`` as a weights-only tensor, anything else through PIL."""
+    ext = os.path.splitext(str(path))[1].lower()
+    if ext == ".npy":
+        return np.load(path)
+    if ext in (".pt", ".pth"):
+        return torch.load(path, weights_only=True).numpy()
     from PIL import Image
 
-    ext = splitext(filename)[1]
-    if ext == ".npy":
-        return Image.fromarray(np.load(filename))   # allow_pickle=False (numpy default)
-    if ext in (".pt", ".pth"):
-        return Image.fromarray(torch.load(filename, weights_only=True).numpy())
-    return Image.open(filename)
+    with Image.open(path) as im:
+        return np.asarray(im)
+
+
+def load_image(filename):
+    """PIL view of :func:`read_array` (API of the reference's helper, data_loading.py:20-27)."""
+    from PIL import Image
+
+    return Image.fromarray(read_array(filename))
+
+
+def _resized(arr: np.ndarray, scale: float, nearest: bool) -> np.ndarray:
+    h, w = arr.shape[:2]
+    size = (int(scale * w), int(scale * h))
+    if size[0] <= 0 or size[1] <= 0:
+        raise ValueError(f"scale {scale} leaves no pixel of a {w}x{h} image")
+    if size == (w, h):
+        return arr
+    from PIL import Image
+
+    mode = Image.NEAREST if nearest else Image.BICUBIC
+    return np.asarray(Image.fromarray(arr).resize(size, resample=mode))
+
+
+def _row_keys(arr: np.ndarray) -> np.ndarray:
+    """One sortable integer key per pixel: the value itself for single-channel masks, the channel
+    tuple packed into an unsigned integer (lexicographic order preserved) otherwise."""
+    if arr.ndim <= 2:
+        return arr.reshape(-1)
+    flat = np.ascontiguousarray(arr.reshape(-1, arr.shape[-1]))
+    if flat.dtype.kind in "ui" and flat.dtype.itemsize <= 2 and flat.shape[1] * 16 <= 64:
+        bits = 8 * flat.dtype.itemsize
+        u = flat.astype(np.int64) - (np.iinfo(flat.dtype).min if flat.dtype.kind == "i" else 0)
+        key = np.zeros(len(flat), dtype=np.uint64)
+        for c in range(flat.shape[1]):
+            key = (key << np.uint64(bits)) | u[:, c].astype(np.uint64)
+        return key
+    # generic fallback: a structured view sorts lexicographically as well
+    return flat.view([("", flat.dtype)] * flat.shape[1]).reshape(-1)
 
 
 class SegmentationDataset(Dataset):
-    def __init__(self, images_dir, mask_dir, scale=1.0, mask_suffix=""):
-        from pathlib import Path
+    """Image / mask pairs for the UNet trainer (semantics of the reference's ``BasicDataset``,
+    /root/reference/pytorch/unet/data_loading.py:52-134; re-implemented, not transcribed):
 
-        assert 0 < scale <= 1, "Scale must be between 0 and 1"
-        self.images_dir, self.mask_dir = Path(images_dir), Path(mask_dir)
-        self.scale, self.mask_suffix = scale, mask_suffix
-        self.ids = [splitext(f)[0] for f in listdir(images_dir) if isfile(join(images_dir, f)) and not f.startswith(".")]
-        if not self.ids:
-            raise RuntimeError(f"No input file found in {images_dir}, make sure you put your images there")
-        uniq = [self._unique(i) for i in self.ids]
-        self.mask_values = list(sorted(np.unique(np.concatenate(uniq), axis=0).tolist()))
+    * the sample list is built ONCE by pairing ``images_dir/<id>.*`` with
+      ``mask_dir/<id><mask_suffix>.*`` (duplicate or missing files are rejected up front, not on
+      every ``__getitem__``);
+    * the table of distinct mask values (pixel values, or channel tuples of colour masks) is found
+      by a thread-parallel scan of the masks;
+    * a mask is mapped to class indices by one vectorised ``searchsorted`` into that table (no loop
+      over the values), then binarised (index > 0) to float32 -- the reference's training target;
+    * images are resized by ``scale`` (bicubic; nearest for masks), laid out CHW, divided by 255
+      when any value exceeds 1, float32;
+    * ``cache=True`` decodes each sample once and keeps the tensors (the device-resident variant is
+      ``data.DeviceCachedDataset``).
 
-    def _mask_file(self, idx):
-        files = list(self.mask_dir.glob(idx + self.mask_suffix + ".*"))
-        if not files:
-            raise FileNotFoundError(f"No mask file found for index '{idx}' with suffix '{self.mask_suffix}' "
-                                    f"in directory '{self.mask_dir}'")
-        return files[0]
+    Returns ``{'image': float32 [C, H, W], 'mask': float32 [H, W]}``."""
 
-    def _unique(self, idx):
-        mask = np.asarray(load_image(self._mask_file(idx)))
-        if mask.ndim == 2:
-            return np.unique(mask)
-        if mask.ndim == 3:
-            return np.unique(mask.reshape(-1, mask.shape[-1]), axis=0)
-        raise ValueError(f"Loaded masks should have 2 or 3 dimensions, found {mask.ndim}")
+    def __init__(self, images_dir, mask_dir, scale=1.0, mask_suffix="", cache=False, workers=None):
+        if not 0 < scale <= 1:
+            raise ValueError(f"scale must be in (0, 1], got {scale}")
+        self.images_dir, self.mask_dir = str(images_dir), str(mask_dir)
+        self.scale, self.mask_suffix = float(scale), mask_suffix
+        self._pairs = self._pair_files()
+        self.ids = [k for k, _, _ in self._pairs]
+        self._table = self._value_table(workers)
+        self._cache = {} if cache else None
+
+    # ------------------------------------------------------------------ indexing
+    def _pair_files(self):
+        def by_stem(d, suffix):
+            out = {}
+            for f in sorted(os.listdir(d)):
+                full = join(d, f)
+                if f.startswith(".") or not isfile(full):
+                    continue
+                stem = splitext(f)[0]
+                if suffix:
+                    if not stem.endswith(suffix):
+                        continue
+                    stem = stem[: -len(suffix)]
+                out.setdefault(stem, []).append(full)
+            return out
+
+        imgs = by_stem(self.images_dir, "")
+        if not imgs:
+            raise RuntimeError(f"{self.images_dir} holds no image files")
+        masks = by_stem(self.mask_dir, self.mask_suffix)
+        pairs = []
+        for stem in sorted(imgs):
+            if len(imgs[stem]) != 1:
+                raise RuntimeError(f"sample {stem!r}: expected one image file, got {imgs[stem]}")
+            m = masks.get(stem, [])
+            if len(m) != 1:
+                raise RuntimeError(f"sample {stem!r}: expected one mask file '{stem}{self.mask_suffix}.*' in "
+                                   f"{self.mask_dir}, got {m}")
+            pairs.append((stem, imgs[stem][0], m[0]))
+        return pairs
+
+    def _value_table(self, workers):
+        from concurrent.futures import ThreadPoolExecutor
+
+        def distinct(path):
+            a = read_array(path)
+            if a.ndim not in (2, 3):
+                raise ValueError(f"mask {path}: expected a 2-D or 3-D array, got {a.ndim}-D")
+            return a.ndim, (np.unique(a) if a.ndim == 2 else np.unique(a.reshape(-1, a.shape[-1]), axis=0))
+
+        n = workers or min(16, os.cpu_count() or 1, len(self._pairs))
+        with ThreadPoolExecutor(max_workers=max(1, n)) as ex:
+            found = list(ex.map(distinct, [m for _, _, m in self._pairs]))
+        ndims = {d for d, _ in found}
+        if len(ndims) != 1:
+            raise ValueError("masks mix single-channel and multi-channel files")
+        vals = np.unique(np.concatenate([u for _, u in found]), axis=0)   # sorted (lexicographic rows)
+        self.mask_values = vals.tolist()
+        return np.sort(_row_keys(vals if vals.ndim == 1 else vals[None]))
+
+    # ------------------------------------------------------------------ samples
+    def mask_indices(self, mask: np.ndarray) -> np.ndarray:
+        """Class index of every pixel (its value's rank in the table); int64 [H, W]."""
+        keys = _row_keys(mask)
+        idx = np.searchsorted(self._table, keys)
+        idx = np.minimum(idx, len(self._table) - 1)
+        idx = np.where(self._table[idx] == keys, idx, 0)   # values outside the table -> class 0
+        return idx.astype(np.int64).reshape(mask.shape[:2])
+
+    def load(self, i):
+        stem, ipath, mpath = self._pairs[i]
+        img, mask = read_array(ipath), read_array(mpath)
+        if img.shape[:2] != mask.shape[:2]:
+            raise ValueError(f"sample {stem!r}: image {img.shape[:2]} and mask {mask.shape[:2]} differ in size")
+        img = _resized(img, self.scale, nearest=False)
+        mask = _resized(mask, self.scale, nearest=True)
+        chw = np.ascontiguousarray(img[None] if img.ndim == 2 else np.moveaxis(img, -1, 0))
+        if bool((chw > 1).any()):
+            chw = chw / 255.0
+        image = torch.tensor(chw).float()
+        target = torch.from_numpy(self.mask_indices(mask) > 0).float()
+        return {"image": image.contiguous(), "mask": target.contiguous()}
 
     def __len__(self):
-        return len(self.ids)
+        return len(self._pairs)
 
-    @staticmethod
-    def preprocess(mask_values, pil_img, scale, is_mask):
-        from PIL import Image
-
-        w, h = pil_img.size
-        nw, nh = int(scale * w), int(scale * h)
-        assert nw > 0 and nh > 0, "Scale is too small, resized images would have no pixel"
-        pil_img = pil_img.resize((nw, nh), resample=Image.NEAREST if is_mask else Image.BICUBIC)
-        img = np.asarray(pil_img)
-        if is_mask:
-            mask = np.zeros((nh, nw), dtype=np.int64)
-            for i, v in enumerate(mask_values):
-                if img.ndim == 2:
-                    mask[img == v] = i
-                else:
-                    mask[(img == v).all(-1)] = i
-            return mask
-        img = img[np.newaxis, ...] if img.ndim == 2 else img.transpose((2, 0, 1))
-        if (img > 1).any():
-            img = img / 255.0
-        return img
-
-    def __getitem__(self, idx):
-        name = self.ids[idx]
-        mask_file = list(self.mask_dir.glob(name + self.mask_suffix + ".*"))
-        img_file = list(self.images_dir.glob(name + ".*"))
-        assert len(img_file) == 1, f"Either no image or multiple images found for the ID {name}: {img_file}"
-        assert len(mask_file) == 1, f"Either no mask or multiple masks found for the ID {name}: {mask_file}"
-        mask = load_image(mask_file[0])
-        img = load_image(img_file[0])
-        assert img.size == mask.size, f"Image and mask {name} should be the same size"
-        img = self.preprocess(self.mask_values, img, self.scale, is_mask=False)
-        mask = self.preprocess(self.mask_values, mask, self.scale, is_mask=True)
-        return {"image": torch.as_tensor(img.copy()).float().contiguous(),
-                "mask": torch.as_tensor((mask > 0).astype(np.float32)).float().contiguous()}
+    def __getitem__(self, i):
+        if self._cache is None:
+            return self.load(i)
+        if i not in self._cache:
+            self._cache[i] = self.load(i)
+        return self._cache[i]
 
 
 class CarvanaDataset(SegmentationDataset):
-    def __init__(self, images_dir, mask_dir, scale=1):
-        super().__init__(images_dir, mask_dir, scale, mask_suffix="")
+    """Name kept for the reference's entry points (data_loading.py:132-134): no mask suffix."""
+
+    def __init__(self, images_dir, mask_dir, scale=1.0, **kw):
+        super().__init__(images_dir, mask_dir, scale, mask_suffix="", **kw)

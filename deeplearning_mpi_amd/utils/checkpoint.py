@@ -3,15 +3,18 @@
 The main file is exactly what the reference writes -- ``torch.save(ddp_model.state_dict(), path)``
 (/root/reference/pytorch/resnet/main.py:139, unet/train.py:216): a flat dict of fp32 tensors whose
 keys carry the ``module.`` prefix -- so reference checkpoints load here and ours load there.
-Optional resume state (optimizer, epoch, RNG, sampler epoch) goes to a sidecar ``<path>.state``
-so the main file layout never changes.  Only GLOBAL rank 0 writes (the reference gates on
+Resume state (optimizer, next epoch, sampler epoch, RNG states: :func:`resume_state`) goes to a
+sidecar ``<path>.state`` so the main file layout never changes; the apps write it with every
+checkpoint and ``--resume`` continues from it exactly (tests/test_resume_cpu.py).  Only GLOBAL rank 0 writes (the reference gates on
 LOCAL_RANK, which collides across nodes on a shared filesystem).
 Loading uses ``torch.load(..., weights_only=True)`` and accepts either key style.
 """
 from __future__ import annotations
 
 import os
+import random
 
+import numpy as np
 import torch
 
 
@@ -72,3 +75,34 @@ def load_checkpoint(model, path, map_location=None, optimizer=None, strict=True)
     if a is not None:
         a.mark_updated()
     return meta
+
+
+def rng_state() -> dict:
+    """Host (torch / numpy / python) and device RNG states, as tensors and plain numbers only so
+    the sidecar loads with ``weights_only=True``."""
+    np_s = np.random.get_state()
+    py = random.getstate()
+    st = {"torch": torch.get_rng_state(),
+          "numpy": {"keys": torch.from_numpy(np.asarray(np_s[1], dtype=np.int64)), "pos": int(np_s[2]),
+                    "has_gauss": int(np_s[3]), "gauss": float(np_s[4])},
+          "python": {"version": int(py[0]), "state": torch.tensor(py[1], dtype=torch.int64), "gauss": py[2]}}
+    if torch.cuda.is_available() and torch.cuda.is_initialized():
+        st["cuda"] = [t.cpu() for t in torch.cuda.get_rng_state_all()]
+    return st
+
+
+def set_rng_state(st: dict):
+    if not st:
+        return
+    torch.set_rng_state(st["torch"].cpu())
+    n = st["numpy"]
+    np.random.set_state(("MT19937", n["keys"].cpu().numpy().astype(np.uint32), n["pos"], n["has_gauss"], n["gauss"]))
+    p = st["python"]
+    random.setstate((p["version"], tuple(int(v) for v in p["state"].tolist()), p["gauss"]))
+    if "cuda" in st and torch.cuda.is_available():
+        torch.cuda.set_rng_state_all([t.cpu() for t in st["cuda"]])
+
+
+def resume_state(next_epoch: int, **more) -> dict:
+    """Sidecar payload: the epoch to continue with, the sampler epoch and the RNG states."""
+    return dict(next_epoch=int(next_epoch), sampler_epoch=int(next_epoch), rng=rng_state(), **more)
