@@ -393,6 +393,34 @@ void conv2d_wgrad(const at::Tensor& dy, int lddy, int dyoff, int Ko, const at::T
   a.fdS = make_fastdiv((uint32_t)S);
   const int64_t wsz = (int64_t)Ko * a.TC;
   const int G = splits > 1 ? dlmpi_wgrad_reduce_groups(splits, wsz) : 0;
+  // In-launch split reduction for few splits (DLMPI_WGRAD_INLAUNCH = max splits, default 8; 0 = off):
+  // the tile's last arriver reads all S slabs itself, a serial tail of S x 32-64 KB.  Most ResNet /
+  // UNet weight gradients split the pixel axis 15-500 ways (tiny Ko x R*S*C output, huge pixel
+  // reduction), where that tail costs far more than the two reduction launches it saves (all
+  // splits in-launch: ResNet-50 11,770 -> 7,630 img/s, profiles/r2_wgrad_inlaunch); those keep the
+  // slab workspace + two parallel reduction kernels.
+  static const int inlaunch_max = [] {
+    const char* e = getenv("DLMPI_WGRAD_INLAUNCH");
+    return e ? atoi(e) : 8;
+  }();
+  if (splits <= inlaunch_max) {
+    hipStream_t st = cur_stream();
+    const int tiles_n = a.mtiles * a.ntiles;
+    float* slab = splits > 1 ? dlmpi_splitk_slab(st, (size_t)tiles_n * splits * bm * bn) : nullptr;
+    int* tk = splits > 1 ? dlmpi_splitk_tickets(st, tiles_n) : nullptr;
+    if (splits == 1 || (slab && tk)) {
+      a.ws = nullptr;
+      a.slab = slab;
+      a.tk = tk;
+      a.out = ptr<float>(grad);
+      a.T = R * S;
+      a.Creal = Creal;
+      a.Ko_real = Ko_real;
+      a.groups = std::max(1, G);
+      check(dlmpi_conv_wgrad(&a, bm, bn, st), "conv2d_wgrad");
+      return;
+    }
+  }
   at::Tensor ws = at::empty({(int64_t)(splits + G) * wsz}, dy.options().dtype(at::kFloat));
   a.ws = ptr<float>(ws);
   check(dlmpi_conv_wgrad(&a, bm, bn, cur_stream()), "conv2d_wgrad");

@@ -101,7 +101,14 @@ struct WgradArgs {
   int mtiles, ntiles, splits;
   int direct;                      // 1: 1x1 / stride 1 / pad 0 on the same grid (no gather decode)
   FastDiv fdPQ, fdQ, fdC, fdS;
-  float* ws;                       // [splits][Ko][TC] fp32 partials
+  float* ws;                       // [splits][Ko][TC] fp32 partials (two-kernel path)
+  // in-launch reduction (ws == nullptr): per (tile, split) fp32 fragment slabs + per-tile tickets;
+  // the tile's last-arriving split sums the slabs in split order (in `groups` consecutive groups,
+  // the association of the two-kernel path) and accumulates out[ko][t][c] (c < Creal, ko < Ko_real)
+  float* slab;
+  int* tk;
+  float* out;
+  int T, Creal, Ko_real, groups;
 };
 
 }  // namespace dlmpi

@@ -478,3 +478,47 @@ def test_cast_weights_all_layouts(model):
     want = torch.zeros_like(a.compute)
     RefBackend(DEV, torch.float32).cast_weights(a._entries, a._compute_total, want)
     assert torch.equal(got, want)
+
+
+_WG_SCRIPT = r"""
+import sys, torch
+sys.path.insert(0, {root!r})
+from deeplearning_mpi_amd.ops.act import Act, pad8
+from deeplearning_mpi_amd.ops.backend import NativeBackend
+nb = NativeBackend("cuda")
+out = {{}}
+for i, (N, H, W, Cin, K, R, s, p) in enumerate({shapes!r}):
+    g = torch.Generator(device="cuda").manual_seed(100 + i)
+    Cp, Kp = pad8(Cin), pad8(K)
+    P, Q = (H + 2 * p - R) // s + 1, (W + 2 * p - R) // s + 1
+    x = Act(torch.randn(N * H * W, Cp, device="cuda", generator=g).to(torch.bfloat16), N, H, W, Cp)
+    dy = Act(torch.randn(N * P * Q, Kp, device="cuda", generator=g).to(torch.bfloat16), N, P, Q, Kp)
+    gr = torch.randn(K * R * R * Cin, device="cuda", generator=g)
+    nb.conv_wgrad(dy, x, R, R, s, p, gr, Cin, K)
+    out[i] = gr.cpu()
+torch.save(out, sys.argv[1])
+"""
+
+
+def test_wgrad_in_launch_reduction_bit_identical_to_two_kernel_path(tmp_path):
+    """The last-arriver split reduction inside the weight-gradient kernel sums the split slabs in
+    the association of the former slab + two-kernel reduction: bit-identical results, incl. a
+    ResNet-50 bench-scale layer (many splits) and split-free small grids."""
+    import os
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    shapes = CONV_SHAPES + [(256, 14, 14, 256, 256, 3, 1, 1), (256, 56, 56, 64, 256, 1, 1, 0),
+                            (256, 7, 7, 2048, 512, 1, 1, 0)]
+    script = tmp_path / "wg.py"
+    script.write_text(_WG_SCRIPT.format(root=root, shapes=shapes))
+    res = {}
+    for mode in ("100000", "0"):   # every split count in-launch vs the two-kernel path
+        env = dict(os.environ, DLMPI_WGRAD_INLAUNCH=mode)
+        r = subprocess.run([sys.executable, str(script), str(tmp_path / f"o{mode}.pt")], env=env,
+                           capture_output=True, text=True, timeout=300)
+        assert r.returncode == 0, r.stderr[-3000:]
+        res[mode] = torch.load(tmp_path / f"o{mode}.pt", weights_only=True)
+    for i in res["0"]:
+        assert torch.equal(res["100000"][i], res["0"][i]), shapes[i]
