@@ -67,15 +67,18 @@ def main():
     if world > 1:
         net = nn.parallel.DistributedDataParallel(net, device_ids=[lrank])
     B, S, C = cfg["batch"], cfg["image"], cfg["cin"]
-    x = torch.randn(B, C, S, S, device=dev)
+    # the same fixed device batch as bench.py (device_batch, seed 1234 + rank), so the two final
+    # losses are comparable
+    from deeplearning_mpi_amd.data import device_batch
+
+    x, y = device_batch("segmentation" if seg else "classification", B, dev, (C, S, S), cfg["classes"],
+                        seed=1234 + rank)
     if cl:
         x = x.to(memory_format=torch.channels_last)
     if seg:
         opt = torch.optim.Adam(net.parameters(), lr=1e-4)
-        y = (torch.rand(B, S, S, device=dev) > 0.5).float()
     else:
         opt = torch.optim.SGD(net.parameters(), lr=0.1, momentum=0.9, weight_decay=1e-5)
-        y = torch.randint(cfg["classes"], (B,), device=dev)
 
     def step():
         opt.zero_grad()

@@ -75,7 +75,26 @@ class DistributedDataParallel(nn.Module):
         self._require_sync = True
         self._queued = False
         self._steps = 0
+        self.streams_per_step = self._check_queue_budget()
         self.timer = None   # optional utils.profiler.StepTimer: times the exposed all-reduce wait
+
+    def _check_queue_budget(self) -> int:
+        """HIP streams one training step keeps busy: the compute stream, the engine's weight-gradient
+        side stream and residual-branch stream, and the RCCL comm stream.  HIP maps streams onto
+        GPU_MAX_HW_QUEUES hardware queues (4 by default, and on the MI355X pool); beyond that,
+        streams share queues and their kernels serialise behind each other (correct, slower), so
+        the design keeps the set at 4 and warns if a configuration exceeds it."""
+        import os
+        import warnings
+
+        be = self.arena.backend
+        n = 1 + sum(getattr(be, a, None) is not None for a in ("_side", "_branch"))
+        n += 1 if (self.reducer is not None and getattr(self.comm, "backend", "") == "rccl") else 0
+        cap = int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4)
+        if n > cap:
+            warnings.warn(f"DistributedDataParallel: {n} HIP streams per step > GPU_MAX_HW_QUEUES={cap}: "
+                          "streams will share hardware queues")
+        return n
 
     # ---------------------------------------------------------------- construction collectives
     def _verify_params(self):
