@@ -70,14 +70,23 @@ def build_argparser(variant: str = "main") -> argparse.ArgumentParser:
     return p
 
 
-def use_graph(args, device) -> bool:
-    """--graph auto: capture the step when it runs on the native bf16 kernels of a GPU (the fp32
-    option runs stock torch ops, captured only on request)."""
+def use_graph(args, device, pixels=None) -> bool:
+    """--graph auto: capture the step when it is launch-bound -- native bf16 kernels on a GPU and a
+    step smaller than the auxiliary-stream threshold (N*H*W < DLMPI_AUX_MIN_PIXELS, default 1M:
+    the reference's ResNet-18 on CIFAR, 46k -> 85k img/s).  Larger steps run their weight-gradient
+    and residual-branch streams concurrently, which a replayed graph loses (measured: ResNet-50
+    bs 256 -7 %, ResNet-152 -13 %, UNet 512 -2 %, profiles/r2_graph_ab).  The fp32 option runs
+    stock torch ops, captured only on request."""
     if args.graph in (True, "1"):
         return device.type == "cuda"
     if args.graph in (False, "0"):
         return False
-    return device.type == "cuda" and args.precision == "bf16"
+    if device.type != "cuda" or args.precision != "bf16":
+        return False
+    if pixels is None:
+        side = args.image_size if getattr(args, "synthetic", False) else 32
+        pixels = args.batch_size * side * side
+    return pixels < int(os.environ.get("DLMPI_AUX_MIN_PIXELS", str(1 << 20)))
 
 
 def set_random_seeds(seed: int):

@@ -201,7 +201,7 @@ def run(args) -> dict:
         meta = load_checkpoint(ddp, model_filepath, map_location=device, optimizer=optimizer)
         start_epoch = int(meta.get("next_epoch", 0))
         set_rng_state(meta.get("rng"))
-    args.graph = use_graph(args, device)
+    args.graph = use_graph(args, device, pixels=args.batch_size * args.image_size * args.image_size)
 
     def train_step(images, masks):
         pred = ddp(images).squeeze(1)

@@ -83,7 +83,7 @@ static int sq256_min_tiles() {
 }
 
 // cin: channel count of the GEMM's gathered operand (the 8-wave 256x256 kernel needs cin % 64 == 0)
-static void pick_tiles(int64_t M, int Kout, int64_t red, int cin, int& bm, int& bn) {
+static void pick_tiles(int64_t M, int Kout, int64_t red, int cin, int& bm, int& bn, bool pro = false) {
   bn = Kout <= 64 ? 64 : 128;
   // 64 (mod 128) channels above 128 (the UNet's 192-channel top concat gradient): 64-wide tiles
   // cover them exactly instead of a half-empty last 128-wide tile (a third more MFMA work)
@@ -96,7 +96,9 @@ static void pick_tiles(int64_t M, int Kout, int64_t red, int cin, int& bm, int& 
   }
   // long reductions into >= 256 output channels: 8-wave 256x256 tiles while the grid still gives
   // every CU a block (UNet levels 3-5, the wide 3x3 layers)
-  if (Kout >= 256 && red >= 2304 && cin % 64 == 0 && ((M + 255) / 256) * ((Kout + 255) / 256) >= sq256_min_tiles()) {
+  // (the operand prologue exists for the single-stage kernels only)
+  if (!pro && Kout >= 256 && red >= 2304 && cin % 64 == 0 &&
+      ((M + 255) / 256) * ((Kout + 255) / 256) >= sq256_min_tiles()) {
     bm = bn = 256;
     return;
   }
@@ -148,12 +150,37 @@ static void fill_epilogue(ConvArgs& a, at::Tensor& y, int ldy, int yoff, const c
   a.nt_store = nt;
 }
 
+// Operand prologue of the gathered operand (ConvArgs::pro): pro 1 = (k0 scale, k1 shift) of a deferred
+// BN-apply + ReLU; pro 2 = (k0 coef [3][C], pz = Z) of a deferred BN-backward apply.
+static void set_prologue(ConvArgs& a, int pro, const c10::optional<at::Tensor>& k0, const c10::optional<at::Tensor>& k1,
+                         const c10::optional<at::Tensor>& pz, int ldpz, int pzoff) {
+  a.pro = pro;
+  if (pro == 0) return;
+  if (a.C < 64 || a.C % 64) throw std::runtime_error("conv prologue: channel count must be a multiple of 64");
+  if (pro == 1) {
+    a.pscale = optr<float>(k0);
+    a.pshift = optr<float>(k1);
+    if (!a.pscale || !a.pshift || k0->numel() < a.C || k1->numel() < a.C)
+      throw std::runtime_error("conv prologue 1: scale / shift of C channels required");
+  } else if (pro == 2) {
+    a.pcoef = optr<float>(k0);
+    a.pz = optr<uint16_t>(pz);
+    a.ldpz = ldpz;
+    a.pzoff = pzoff;
+    if (!a.pcoef || !a.pz || k0->numel() < 3 * a.C || (ldpz | pzoff) % 8)
+      throw std::runtime_error("conv prologue 2: coef [3][C] and an 8-channel aligned Z required");
+  } else {
+    throw std::runtime_error("conv prologue: mode 1 or 2");
+  }
+}
+
 // y[n, p, q, yoff + k] = epilogue( sum_{r,s,c} x[n, p*stride - pad + r, q*stride - pad + s, xoff + c] * w[k][r][s][c] )
-int conv2d_fwd(const at::Tensor& x, int N, int H, int W, int C, int ldx, int xoff, const at::Tensor& w, int K, int R,
+int conv2d_fwd_pro(const at::Tensor& x, int N, int H, int W, int C, int ldx, int xoff, const at::Tensor& w, int K, int R,
                int S, int stride, int pad, at::Tensor y, int ldy, int yoff, const c10::optional<at::Tensor>& bias,
                const c10::optional<at::Tensor>& res, int ldres, int resoff, const c10::optional<at::Tensor>& scale,
                const c10::optional<at::Tensor>& shift, bool relu, const c10::optional<at::Tensor>& stats, int bm_req,
-               int kvalid, int bn_req) {
+               int kvalid, int bn_req, int pro, const c10::optional<at::Tensor>& pk0,
+               const c10::optional<at::Tensor>& pk1, const c10::optional<at::Tensor>& pz, int ldpz, int pzoff) {
   require_gpu(x, "x");
   const int P = (H + 2 * pad - R) / stride + 1, Q = (W + 2 * pad - S) / stride + 1;
   ConvArgs a{};
@@ -169,8 +196,9 @@ int conv2d_fwd(const at::Tensor& x, int N, int H, int W, int C, int ldx, int xof
   if (kvalid > 0 && kvalid < K) a.kvalid = kvalid;
   a.vec_store = (a.kvalid == a.Kout && (ldy % 8) == 0 && (yoff % 8) == 0) ? 1 : 0;
   set_kstep(a, C);
+  set_prologue(a, pro, pk0, pk1, pz, ldpz, pzoff);
   int bm, bn;
-  pick_tiles((int64_t)N * P * Q, K, (int64_t)R * S * C, C, bm, bn);
+  pick_tiles((int64_t)N * P * Q, K, (int64_t)R * S * C, C, bm, bn, pro != 0);
   if (bm_req > 0) bm = bm_req;   // tests / experiments: force a tile shape
   if (bn_req > 0) bn = bn_req;
   a.ntiles = ceil_div(K, bn);
@@ -183,6 +211,16 @@ int conv2d_fwd(const at::Tensor& x, int N, int H, int W, int C, int ldx, int xof
   finish_phase(p, N, C, bm);
   check(dlmpi_conv_igemm(&a, bm, bn, cur_stream()), "conv2d_fwd");
   return p.mtiles;   // rows of the stats partial buffer
+}
+
+int conv2d_fwd(const at::Tensor& x, int N, int H, int W, int C, int ldx, int xoff, const at::Tensor& w, int K, int R,
+               int S, int stride, int pad, at::Tensor y, int ldy, int yoff, const c10::optional<at::Tensor>& bias,
+               const c10::optional<at::Tensor>& res, int ldres, int resoff, const c10::optional<at::Tensor>& scale,
+               const c10::optional<at::Tensor>& shift, bool relu, const c10::optional<at::Tensor>& stats, int bm_req,
+               int kvalid, int bn_req) {
+  return conv2d_fwd_pro(x, N, H, W, C, ldx, xoff, w, K, R, S, stride, pad, y, ldy, yoff, bias, res, ldres, resoff,
+                        scale, shift, relu, stats, bm_req, kvalid, bn_req, 0, c10::nullopt, c10::nullopt,
+                        c10::nullopt, 0, 0);
 }
 
 // Forward conv whose output is the gradient of y = relu(BN(z)) (a BN+ReLU without residual): the
@@ -231,12 +269,15 @@ at::Tensor conv2d_fwd_bnbwd(const at::Tensor& x, int N, int H, int W, int C, int
 }
 
 // Number of BN-stat partial rows conv2d_fwd will produce (so the caller can size `stats`).
-int conv2d_fwd_mtiles(int N, int H, int W, int C, int K, int R, int S, int stride, int pad, int bm_req) {
+int conv2d_fwd_mtiles_pro(int N, int H, int W, int C, int K, int R, int S, int stride, int pad, int bm_req, int pro) {
   const int P = (H + 2 * pad - R) / stride + 1, Q = (W + 2 * pad - S) / stride + 1;
   int bm, bn;
-  pick_tiles((int64_t)N * P * Q, K, (int64_t)R * S * C, C, bm, bn);
+  pick_tiles((int64_t)N * P * Q, K, (int64_t)R * S * C, C, bm, bn, pro != 0);
   if (bm_req > 0) bm = bm_req;
   return ceil_div((int64_t)N * P * Q, bm);
+}
+int conv2d_fwd_mtiles(int N, int H, int W, int C, int K, int R, int S, int stride, int pad, int bm_req) {
+  return conv2d_fwd_mtiles_pro(N, H, W, C, K, R, S, stride, pad, bm_req, 0);
 }
 
 // dx[n, h, w, dxoff + c] = sum_{r,s,k} dy[n, (h+pad-r)/stride, (w+pad-s)/stride, k] * wT[c][r][s][k]  (+ res)
@@ -245,7 +286,7 @@ int conv2d_fwd_mtiles(int N, int H, int W, int C, int K, int R, int S, int strid
 // Optional BN-backward fusion (dx is the gradient of y = relu(BN(z)) [+ BN2(z2)]): the epilogue
 // applies the ReLU mask [y > 0] before storing and emits per-tile partials
 // [tiles][2|3][C] = {sum dx, sum dx*z [, sum dx*z2]}, returned (None without z).
-c10::optional<at::Tensor> conv2d_dgrad(const at::Tensor& dy, int N, int P, int Q, int K, int lddy, int dyoff,
+c10::optional<at::Tensor> conv2d_dgrad_pro(const at::Tensor& dy, int N, int P, int Q, int K, int lddy, int dyoff,
                                        const at::Tensor& wT, int C, int R, int S, int stride, int pad, int H, int W,
                                        at::Tensor dx, int lddx, int dxoff, const c10::optional<at::Tensor>& res,
                                        int ldres, int resoff, const c10::optional<at::Tensor>& mask, int ldmask,
@@ -253,7 +294,9 @@ c10::optional<at::Tensor> conv2d_dgrad(const at::Tensor& dy, int N, int P, int Q
                                        const c10::optional<at::Tensor>& z2, int ldz2, int z2off,
                                        const c10::optional<at::Tensor>& mscale,
                                        const c10::optional<at::Tensor>& mshift,
-                                       const c10::optional<at::Tensor>& mbits, bool colsum) {
+                                       const c10::optional<at::Tensor>& mbits, bool colsum, int pro,
+                                       const c10::optional<at::Tensor>& pk0, const c10::optional<at::Tensor>& pk1,
+                                       const c10::optional<at::Tensor>& pz, int ldpz, int pzoff) {
   require_gpu(dy, "dy");
   if (stride > 2) throw std::runtime_error("conv2d_dgrad: stride <= 2 supported");
   ConvArgs a{};
@@ -285,8 +328,9 @@ c10::optional<at::Tensor> conv2d_dgrad(const at::Tensor& dy, int N, int P, int Q
   if ((a.mask || a.mscale || a.mbits) && ((ldmask | maskoff | ldz | zoff | ldz2 | z2off) % 8 != 0 || !a.vec_store))
     throw std::runtime_error("conv2d_dgrad: fused BN tensors must be 8-channel aligned");
   set_kstep(a, K);
+  set_prologue(a, pro, pk0, pk1, pz, ldpz, pzoff);
   int bm, bn;
-  pick_tiles((int64_t)N * H * W / (stride * stride), C, (int64_t)R * S * K / (stride * stride), K, bm, bn);
+  pick_tiles((int64_t)N * H * W / (stride * stride), C, (int64_t)R * S * K / (stride * stride), K, bm, bn, pro != 0);
   a.ntiles = ceil_div(C, bn);
   a.nphase = stride * stride;
   int tiles = 0;
@@ -316,6 +360,20 @@ c10::optional<at::Tensor> conv2d_dgrad(const at::Tensor& dy, int N, int P, int Q
   }
   check(dlmpi_conv_igemm(&a, bm, bn, cur_stream()), "conv2d_dgrad");
   return stats;
+}
+
+c10::optional<at::Tensor> conv2d_dgrad(const at::Tensor& dy, int N, int P, int Q, int K, int lddy, int dyoff,
+                                       const at::Tensor& wT, int C, int R, int S, int stride, int pad, int H, int W,
+                                       at::Tensor dx, int lddx, int dxoff, const c10::optional<at::Tensor>& res,
+                                       int ldres, int resoff, const c10::optional<at::Tensor>& mask, int ldmask,
+                                       int maskoff, const c10::optional<at::Tensor>& z, int ldz, int zoff,
+                                       const c10::optional<at::Tensor>& z2, int ldz2, int z2off,
+                                       const c10::optional<at::Tensor>& mscale,
+                                       const c10::optional<at::Tensor>& mshift,
+                                       const c10::optional<at::Tensor>& mbits, bool colsum) {
+  return conv2d_dgrad_pro(dy, N, P, Q, K, lddy, dyoff, wT, C, R, S, stride, pad, H, W, dx, lddx, dxoff, res, ldres,
+                          resoff, mask, ldmask, maskoff, z, ldz, zoff, z2, ldz2, z2off, mscale, mshift, mbits, colsum,
+                          0, c10::nullopt, c10::nullopt, c10::nullopt, 0, 0);
 }
 
 // ConvTranspose2d(k=2, s=2): y[n, 2h+i, 2w+j, yoff + co] = bias[co] + sum_ci x[n,h,w,ci] * wf[co][i][j][ci]
@@ -352,12 +410,32 @@ void convT2x2_fwd(const at::Tensor& x, int N, int H, int W, int Cin, int ldx, in
 
 // grad[ko][t][c] += sum_pix dy[pix][dyoff + ko] * x[gather(pix, t)][xoff + c]   (c < Creal, ko < Ko_real)
 // dy is over the P x Q output grid of a conv (R x S, stride, pad) applied to x (H x W).
-void conv2d_wgrad(const at::Tensor& dy, int lddy, int dyoff, int Ko, const at::Tensor& x, int N, int H, int W, int C,
-                  int ldx, int xoff, int R, int S, int stride, int pad, int P, int Q, at::Tensor grad, int Creal,
-                  int Ko_real) {
+// Operand prologues: pro_a 2 -> the dy operand is dz = pcoef[0] dy + pcoef[1] Z + pcoef[2] (a deferred
+// BN-backward apply, Z = the BN input); pro_b 1 -> the x operand is relu(x * pscale + pshift).
+void conv2d_wgrad_pro(const at::Tensor& dy, int lddy, int dyoff, int Ko, const at::Tensor& x, int N, int H, int W,
+                      int C, int ldx, int xoff, int R, int S, int stride, int pad, int P, int Q, at::Tensor grad,
+                      int Creal, int Ko_real, int pro_a, const c10::optional<at::Tensor>& pcoef,
+                      const c10::optional<at::Tensor>& pz, int ldpz, int pzoff, int pro_b,
+                      const c10::optional<at::Tensor>& pscale, const c10::optional<at::Tensor>& pshift) {
   require_gpu(dy, "dy");
   if (C % 8 != 0 || Ko % 8 != 0) throw std::runtime_error("conv2d_wgrad: channels must be multiples of 8");
   WgradArgs a{};
+  a.pro_a = pro_a;
+  a.pro_b = pro_b;
+  if (pro_a) {
+    a.pcoef = optr<float>(pcoef);
+    a.pz = optr<uint16_t>(pz);
+    a.ldpz = ldpz;
+    a.pzoff = pzoff;
+    if (pro_a != 2 || !a.pcoef || !a.pz || pcoef->numel() < 3 * Ko || (ldpz | pzoff) % 8)
+      throw std::runtime_error("conv2d_wgrad: prologue a needs coef [3][Ko] and an aligned Z");
+  }
+  if (pro_b) {
+    a.pscale = optr<float>(pscale);
+    a.pshift = optr<float>(pshift);
+    if (pro_b != 1 || !a.pscale || !a.pshift || pscale->numel() < C || pshift->numel() < C)
+      throw std::runtime_error("conv2d_wgrad: prologue b needs scale / shift of C channels");
+  }
   a.dy = ptr<uint16_t>(dy);
   a.ldy = lddy; a.dyoff = dyoff; a.Ko = Ko;
   a.x = ptr<uint16_t>(x);
@@ -427,6 +505,13 @@ void conv2d_wgrad(const at::Tensor& dy, int lddy, int dyoff, int Ko, const at::T
   check(dlmpi_wgrad_reduce(a.ws, splits, Ko, R * S, C, Creal, Ko_real, ptr<float>(grad), a.ws + (int64_t)splits * wsz,
                            (int)std::min<int64_t>(INT32_MAX, (int64_t)G * wsz), cur_stream()),
         "wgrad_reduce");
+}
+
+void conv2d_wgrad(const at::Tensor& dy, int lddy, int dyoff, int Ko, const at::Tensor& x, int N, int H, int W, int C,
+                  int ldx, int xoff, int R, int S, int stride, int pad, int P, int Q, at::Tensor grad, int Creal,
+                  int Ko_real) {
+  conv2d_wgrad_pro(dy, lddy, dyoff, Ko, x, N, H, W, C, ldx, xoff, R, S, stride, pad, P, Q, grad, Creal, Ko_real, 0,
+                   c10::nullopt, c10::nullopt, 0, 0, 0, c10::nullopt, c10::nullopt);
 }
 
 static at::Tensor colsum_ws(const at::Tensor& like, int T, int C) {
@@ -675,11 +760,15 @@ void image_batch(const at::Tensor& data, const at::Tensor& labels, const at::Ten
 void register_ops(pybind11::module& m) {
   namespace py = pybind11;
   m.def("conv2d_fwd", &conv2d_fwd);
+  m.def("conv2d_fwd_pro", &conv2d_fwd_pro);
   m.def("conv2d_fwd_mtiles", &conv2d_fwd_mtiles);
+  m.def("conv2d_fwd_mtiles_pro", &conv2d_fwd_mtiles_pro);
   m.def("conv2d_fwd_bnbwd", &conv2d_fwd_bnbwd);
   m.def("conv2d_dgrad", &conv2d_dgrad);
+  m.def("conv2d_dgrad_pro", &conv2d_dgrad_pro);
   m.def("convT2x2_fwd", &convT2x2_fwd);
   m.def("conv2d_wgrad", &conv2d_wgrad);
+  m.def("conv2d_wgrad_pro", &conv2d_wgrad_pro);
   m.def("bn_finalize", &bn_finalize);
   m.def("set_aux_stream", [](int64_t h, int role) {
     check(dlmpi_set_aux_stream(reinterpret_cast<hipStream_t>(h), role), "set_aux_stream");

@@ -446,8 +446,9 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const uint16_t* __restric
     const f32x4 h0 = *reinterpret_cast<const f32x4*>(shift + c0), h1 = *reinterpret_cast<const f32x4*>(shift + c0 + 4);
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
-      v[e] = v[e] * s0[e] + h0[e];
-      v[e + 4] = v[e + 4] * s1[e] + h1[e];
+      // explicit fma: the conv prologue (conv_igemm.hip, pro 1) recomputes exactly this value
+      v[e] = __builtin_fmaf(v[e], s0[e], h0[e]);
+      v[e + 4] = __builtin_fmaf(v[e + 4], s1[e], h1[e]);
     }
     if (res) {
       float r[8];
@@ -544,7 +545,8 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const uint16_t* __res
     unpack8(*reinterpret_cast<const u32x4*>(x + row * ldx + xoff + c0), xv);
     float o[8];
 #pragma unroll
-    for (int e = 0; e < 8; ++e) o[e] = coef[c0 + e] * g[e] + coef[C + c0 + e] * xv[e] + coef[2 * C + c0 + e];
+    for (int e = 0; e < 8; ++e)   // this fma order is shared with the conv prologues (pro 2 / PA 2)
+      o[e] = __builtin_fmaf(coef[c0 + e], g[e], __builtin_fmaf(coef[C + c0 + e], xv[e], coef[2 * C + c0 + e]));
     *reinterpret_cast<u32x4*>(dx + row * C + c0) = pack8(o);
   }
 }

@@ -46,7 +46,7 @@ __device__ __forceinline__ void glds16(const void* g, char* lds_wave_base) {
 // K-step of MFMA work (2048 SIMD cycles) covers the next step's loads.
 // WGM = wave rows (WGM x NW/WGM wave grid): 4 x 1 for the 256 x 64 tile of 64-channel layers
 // (per-wave 64 x 64 instead of 64 x 32: a third less LDS traffic per MFMA).
-template <int BM, int BN, bool SMALLC, int STAGES, int NW, int WGM>
+template <int BM, int BN, bool SMALLC, int STAGES, int NW, int WGM, int PRO = 0>
 __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(STAGES == 1 && BM * BN <= 16384 ? (BM * BN == 16384 ? DLMPI_W128 : 3) : 2, 8))) void conv_igemm_kernel(const ConvArgs a) {
   constexpr int NT = 64 * NW;                 // threads
   constexpr int WGN = NW / WGM;               // wave grid WGM x WGN
@@ -56,7 +56,10 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(STAGES 
   constexpr int RP = NT / 8;                  // tile rows staged per pass (8 lanes per 128-B row)
   constexpr int AL = BM / RP, BL = BN / RP;   // 16-byte pieces per thread per tile
   constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2;
-  constexpr int STAGE_BYTES = STAGES * (A_BYTES + B_BYTES);
+  static_assert(PRO == 0 || (!SMALLC && STAGES == 1), "operand prologue: regular channels, single stage");
+  constexpr int Z_BYTES = PRO == 2 ? A_BYTES : 0;   // the second prologue operand, staged like A
+  constexpr int SB = A_BYTES + B_BYTES + Z_BYTES;   // bytes per stage: [A | B | Z]
+  constexpr int STAGE_BYTES = STAGES * SB;
   constexpr int CS_LD = BN + 4;
   constexpr int NP = BM >= 128 ? BM / 64 : 1;            // epilogue passes of <= 64 tile rows
   static_assert(WM % (16 * NP) == 0 || NP == 1, "epilogue pass must split every wave's rows evenly");
@@ -115,6 +118,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(STAGES 
   // ---- staging ------------------------------------------------------------------------------
   // Regular path (C % 64 == 0): the tap t and channel base c are wave-uniform.
   uint32_t a_off[AL];                                 // element offset of the row's input pixel
+  uint32_t z_off[PRO == 2 ? AL : 1];                  // the same pixel in the prologue's Z
   uint32_t a_vm = 0;                                  // bit i: (row, tap) inside the image
   int t_cur = 0, c_cur = 0, wtC2 = 0;
   auto tap_setup = [&](int t) {
@@ -131,17 +135,27 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(STAGES 
       const bool ok = ((a_okm >> i) & 1) && (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W;
       if (ok) a_vm |= 1u << i;
       a_off[i] = (uint32_t)(a_pix[i] + doff) * (uint32_t)a.ldx;
+      if constexpr (PRO == 2) z_off[i] = (uint32_t)(a_pix[i] + doff) * (uint32_t)a.ldpz;
     }
   };
+  const char* zlane = PRO == 2 ? reinterpret_cast<const char*>(a.pz) + 2 * ((int64_t)a.pzoff + 8 * jc) : nullptr;
 
   auto issue = [&](int buf, int ks) {
-    char* As = smem + buf * (A_BYTES + B_BYTES);
+    char* As = smem + buf * SB;
     char* Bs = As + A_BYTES;
     if constexpr (!SMALLC) {
 #pragma unroll
       for (int i = 0; i < AL; ++i) {
         const char* s = ((a_vm >> i) & 1) ? xlane + 2 * ((uint64_t)a_off[i] + c_cur) : zp;
         glds16(s, As + (RP * i + 8 * wid) * 128);
+      }
+      if constexpr (PRO == 2) {
+        char* Zs = Bs + B_BYTES;
+#pragma unroll
+        for (int i = 0; i < AL; ++i) {
+          const char* s = ((a_vm >> i) & 1) ? zlane + 2 * ((uint64_t)z_off[i] + c_cur) : zp;
+          glds16(s, Zs + (RP * i + 8 * wid) * 128);
+        }
       }
 #pragma unroll
       for (int i = 0; i < BL; ++i) {
@@ -171,6 +185,56 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(STAGES 
         const char* s = (tv && ((b_okm >> i) & 1)) ? b_base + i * b_step - 2 * 8 * jc + 2 * (wt * C + c) : zp;
         glds16(s, Bs + (RP * i + 8 * wid) * 128);
       }
+    }
+  };
+
+  // Operand prologue: this lane's own staged A pieces (row lrow + RP i, chunk jc = channels
+  // c_cur + 8 jc of the current tap) are rewritten in place once the stage has landed; pieces of
+  // out-of-image taps / rows past M hold zeros and are left alone.  Same fma order and bf16
+  // rounding as the standalone kernels it replaces (bn_apply_kernel / bn_bwd_apply_kernel), so the
+  // fused and the unfused schedules are bit-identical.
+  auto prologue = [&](int buf) {
+    if constexpr (PRO != 0) {
+      char* As = smem + buf * SB;
+      const int c = c_cur + 8 * jc;
+      f32x4 k0a, k0b, k1a, k1b, k2a, k2b;
+      if constexpr (PRO == 1) {
+        k0a = *reinterpret_cast<const f32x4*>(a.pscale + c);
+        k0b = *reinterpret_cast<const f32x4*>(a.pscale + c + 4);
+        k1a = *reinterpret_cast<const f32x4*>(a.pshift + c);
+        k1b = *reinterpret_cast<const f32x4*>(a.pshift + c + 4);
+      } else {
+        k0a = *reinterpret_cast<const f32x4*>(a.pcoef + c);
+        k0b = *reinterpret_cast<const f32x4*>(a.pcoef + c + 4);
+        k1a = *reinterpret_cast<const f32x4*>(a.pcoef + C + c);
+        k1b = *reinterpret_cast<const f32x4*>(a.pcoef + C + c + 4);
+        k2a = *reinterpret_cast<const f32x4*>(a.pcoef + 2 * C + c);
+        k2b = *reinterpret_cast<const f32x4*>(a.pcoef + 2 * C + c + 4);
+      }
+#pragma unroll
+      for (int i = 0; i < AL; ++i) {
+        if (!((a_vm >> i) & 1)) continue;
+        u32x4* pa = reinterpret_cast<u32x4*>(As + RP * i * 128 + tid * 16);
+        float v[8];
+        unpack8(*pa, v);
+        if constexpr (PRO == 1) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            v[e] = fmaxf(__builtin_fmaf(v[e], k0a[e], k1a[e]), 0.f);
+            v[e + 4] = fmaxf(__builtin_fmaf(v[e + 4], k0b[e], k1b[e]), 0.f);
+          }
+        } else {
+          float zv[8];
+          unpack8(*reinterpret_cast<const u32x4*>(As + A_BYTES + B_BYTES + RP * i * 128 + tid * 16), zv);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            v[e] = __builtin_fmaf(k0a[e], v[e], __builtin_fmaf(k1a[e], zv[e], k2a[e]));
+            v[e + 4] = __builtin_fmaf(k0b[e], v[e + 4], __builtin_fmaf(k1b[e], zv[e + 4], k2b[e]));
+          }
+        }
+        *pa = pack8(v);
+      }
+      __syncthreads();   // every wave's pieces are rewritten before any fragment read
     }
   };
 
@@ -207,6 +271,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(STAGES 
     }
     issue(0, kbeg);
     __syncthreads();
+    prologue(0);
   }
   for (int ks = kbeg; ks < kend; ++ks) {
     int cur = 0;
@@ -220,8 +285,9 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(STAGES 
       advance();
       issue(0, ks);
       __syncthreads();   // this stage landed (vmcnt(0) + barrier)
+      prologue(0);
     }
-    const char* As = smem + cur * (A_BYTES + B_BYTES);
+    const char* As = smem + cur * SB;
     const char* Bs = As + A_BYTES;
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
@@ -450,6 +516,14 @@ static int stages_choice() {
 template <int BM, int BN>
 static void launch_tile(const ConvArgs* a, dim3 grid, hipStream_t s) {
   const bool one = stages_choice() == 1;
+  if (a->pro == 1) {
+    hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, false, 1, 4, 2, 1>), grid, dim3(256), 0, s, *a);
+    return;
+  }
+  if (a->pro == 2) {
+    hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, false, 1, 4, 2, 2>), grid, dim3(256), 0, s, *a);
+    return;
+  }
   if (a->C < 64) {
     if (one) hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, true, 1, 4, 2>), grid, dim3(256), 0, s, *a);
     else hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, true, 2, 4, 2>), grid, dim3(256), 0, s, *a);
@@ -498,11 +572,14 @@ extern "C" hipError_t dlmpi_conv_igemm(const ConvArgs* a_in, int bm, int bn, hip
   }
   dim3 grid((unsigned)(maxt * a->ntiles), (unsigned)ab.splitk, (unsigned)a->nphase);
   if (grid.x == 0) return hipSuccess;
+  if (a->pro != 0 && (a->C < 64 || a->C % 64 != 0 || (bm == 256 && bn == 256))) return hipErrorInvalidValue;
   if (bm == 256 && bn == 256) {   // 8 waves, double-buffered; regular channel counts only
     if (a->C < 64) return hipErrorInvalidValue;
     hipLaunchKernelGGL((conv_igemm_kernel<256, 256, false, 2, 8, 2>), grid, dim3(512), 0, s, *a);
   } else if (bm == 256 && bn == 64) {   // 64-channel layers: 4 x 1 waves of 64 x 64
-    if (a->C < 64) hipLaunchKernelGGL((conv_igemm_kernel<256, 64, true, 1, 4, 4>), grid, dim3(256), 0, s, *a);
+    if (a->pro == 1) hipLaunchKernelGGL((conv_igemm_kernel<256, 64, false, 1, 4, 4, 1>), grid, dim3(256), 0, s, *a);
+    else if (a->pro == 2) hipLaunchKernelGGL((conv_igemm_kernel<256, 64, false, 1, 4, 4, 2>), grid, dim3(256), 0, s, *a);
+    else if (a->C < 64) hipLaunchKernelGGL((conv_igemm_kernel<256, 64, true, 1, 4, 4>), grid, dim3(256), 0, s, *a);
     else hipLaunchKernelGGL((conv_igemm_kernel<256, 64, false, 1, 4, 4>), grid, dim3(256), 0, s, *a);
   } else if (bm == 256 && bn == 128) launch_tile<256, 128>(a, grid, s);
   else if (bm == 128 && bn == 128) launch_tile<128, 128>(a, grid, s);

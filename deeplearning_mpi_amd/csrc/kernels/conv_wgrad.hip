@@ -72,7 +72,11 @@ __device__ __forceinline__ int tr_chunk(int row, int pos) {
 // lane fetches whichever (pixel row, 16-B chunk) the swizzled layout puts there.  STAGES = 1:
 // single stage, two barriers per K-step, 32 KB LDS at BM = 128 -> several blocks per CU hide
 // the load latency of one another.
-template <int BM, int BN, int STAGES, bool DIRECT>
+// PA = 2: the dy operand is a deferred BN-backward apply (dz = k1 dy + k2 Z + k3, Z staged beside
+// dy); PB = 1: the x operand is a deferred BN-apply + ReLU (relu(x * scale + shift)).  Both are
+// rewritten in LDS once a stage has landed, in-range pieces only (padding / tails stay zero), with
+// the arithmetic of the standalone kernels they replace (bit-identical results).
+template <int BM, int BN, int STAGES, bool DIRECT, int PA = 0, int PB = 0>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(STAGES == 1 && BN == 128 ? 3 : 2, 8)))
 void conv_wgrad_kernel(const WgradArgs a) {
   constexpr int BK = 64;
@@ -80,7 +84,10 @@ void conv_wgrad_kernel(const WgradArgs a) {
   constexpr int A_ROW = BM * 2, B_ROW = BN * 2;          // bytes per LDS row
   constexpr int AL = BK * A_ROW / 4096, BL = BK * B_ROW / 4096;   // 16-B pieces per thread
   constexpr int A_BYTES = BK * A_ROW, B_BYTES = BK * B_ROW;
-  __shared__ __attribute__((aligned(16))) char smem[STAGES * (A_BYTES + B_BYTES)];
+  static_assert((PA == 0 && PB == 0) || STAGES == 1, "operand prologues: single-stage kernels");
+  constexpr int Z_BYTES = PA == 2 ? A_BYTES : 0;
+  constexpr int SB = A_BYTES + B_BYTES + Z_BYTES;        // per stage: [A | B | Z]
+  __shared__ __attribute__((aligned(16))) char smem[STAGES * SB];
 
   const uint32_t ntile = (uint32_t)a.mtiles * a.ntiles;
   const uint32_t nwg = ntile * a.splits;
@@ -134,8 +141,9 @@ void conv_wgrad_kernel(const WgradArgs a) {
     const uintptr_t a0 = reinterpret_cast<uintptr_t>(p), z = reinterpret_cast<uintptr_t>(zp);
     return reinterpret_cast<const char*>(ok ? a0 : z);
   };
+  const uint16_t* zb = PA == 2 ? a.pz + a.pzoff : nullptr;
   auto issue = [&](int buf, int pix0) {
-    char* As = smem + buf * (A_BYTES + B_BYTES);
+    char* As = smem + buf * SB;
     char* Bs = As + A_BYTES;
 #pragma unroll
     for (int i = 0; i < AL; ++i) {
@@ -143,6 +151,9 @@ void conv_wgrad_kernel(const WgradArgs a) {
       piece(i, A_ROW, row, ch);
       const int pix = pix0 + row, col = m0 + 8 * ch;
       glds16(pick(pix < pend && col < a.Ko, dyb + (int64_t)pix * a.ldy + col), As + 16 * (256 * i + 64 * wid));
+      if constexpr (PA == 2)
+        glds16(pick(pix < pend && col < a.Ko, zb + (int64_t)pix * a.ldpz + col),
+               As + A_BYTES + B_BYTES + 16 * (256 * i + 64 * wid));
     }
 #pragma unroll
     for (int i = 0; i < BL; ++i) {
@@ -168,6 +179,81 @@ void conv_wgrad_kernel(const WgradArgs a) {
     }
   };
 
+  // Prologue work split: thread t rewrites 16-B chunk t % 16 (BM = 64: t % 8) of tile rows
+  // t / 16 + 16 j, so its channel chunk -- and the coefficients -- are fixed per thread.
+  auto prologue = [&](int buf, int pix0) {
+    if constexpr (PA != 0 || PB != 0) {
+      char* As = smem + buf * SB;
+      if constexpr (PA == 2) {
+        constexpr int CH = BM / 8, RS = 256 / CH;
+        const int cq = tid % CH, r0 = tid / CH;
+        const int col = m0 + 8 * cq;
+        if (col < a.Ko) {
+          const f32x4 k0a = *reinterpret_cast<const f32x4*>(a.pcoef + col);
+          const f32x4 k0b = *reinterpret_cast<const f32x4*>(a.pcoef + col + 4);
+          const f32x4 k1a = *reinterpret_cast<const f32x4*>(a.pcoef + a.Ko + col);
+          const f32x4 k1b = *reinterpret_cast<const f32x4*>(a.pcoef + a.Ko + col + 4);
+          const f32x4 k2a = *reinterpret_cast<const f32x4*>(a.pcoef + 2 * a.Ko + col);
+          const f32x4 k2b = *reinterpret_cast<const f32x4*>(a.pcoef + 2 * a.Ko + col + 4);
+#pragma unroll
+          for (int r = r0; r < BK; r += RS) {
+            if (pix0 + r >= pend) break;
+            const int off = tr_off<A_ROW>(r, cq);
+            u32x4* pa = reinterpret_cast<u32x4*>(As + off);
+            float v[8], zv[8];
+            unpack8(*pa, v);
+            unpack8(*reinterpret_cast<const u32x4*>(As + A_BYTES + B_BYTES + off), zv);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              v[e] = __builtin_fmaf(k0a[e], v[e], __builtin_fmaf(k1a[e], zv[e], k2a[e]));
+              v[e + 4] = __builtin_fmaf(k0b[e], v[e + 4], __builtin_fmaf(k1b[e], zv[e + 4], k2b[e]));
+            }
+            *pa = pack8(v);
+          }
+        }
+      }
+      if constexpr (PB == 1) {
+        constexpr int CH = BN / 8, RS = 256 / CH;
+        const int cq = tid % CH, r0 = tid / CH;
+        const int col = n0 + 8 * cq;
+        if (col < a.TC) {
+          const int t = (int)fdiv((uint32_t)col, a.fdC);
+          const int cch = col - t * a.C;
+          const int tr = (int)fdiv((uint32_t)t, a.fdS);
+          const int dh = tr - a.pad_h, dw = (t - tr * a.S) - a.pad_w;
+          const f32x4 s0 = *reinterpret_cast<const f32x4*>(a.pscale + cch);
+          const f32x4 s1 = *reinterpret_cast<const f32x4*>(a.pscale + cch + 4);
+          const f32x4 h0 = *reinterpret_cast<const f32x4*>(a.pshift + cch);
+          const f32x4 h1 = *reinterpret_cast<const f32x4*>(a.pshift + cch + 4);
+          char* Bs = As + A_BYTES;
+#pragma unroll
+          for (int r = r0; r < BK; r += RS) {
+            const int pix = pix0 + r;
+            if (pix >= pend) break;
+            if constexpr (!DIRECT) {   // out-of-image taps were staged as zeros: leave them
+              const uint32_t n_img = fdiv((uint32_t)pix, a.fdPQ);
+              const uint32_t rem = (uint32_t)pix - n_img * (uint32_t)(a.P * a.Q);
+              const uint32_t p = fdiv(rem, a.fdQ);
+              const uint32_t q = rem - p * a.Q;
+              const int ih = (int)p * a.stride_h + dh, iw = (int)q * a.stride_w + dw;
+              if ((unsigned)ih >= (unsigned)a.H || (unsigned)iw >= (unsigned)a.W) continue;
+            }
+            u32x4* pb = reinterpret_cast<u32x4*>(Bs + tr_off<B_ROW>(r, cq));
+            float v[8];
+            unpack8(*pb, v);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              v[e] = fmaxf(__builtin_fmaf(v[e], s0[e], h0[e]), 0.f);
+              v[e + 4] = fmaxf(__builtin_fmaf(v[e + 4], s1[e], h1[e]), 0.f);
+            }
+            *pb = pack8(v);
+          }
+        }
+      }
+      __syncthreads();
+    }
+  };
+
   f32x4 acc[TM][TN];
 #pragma unroll
   for (int mi = 0; mi < TM; ++mi)
@@ -177,6 +263,7 @@ void conv_wgrad_kernel(const WgradArgs a) {
   if (nk > 0) {
     issue(0, pbeg);
     __syncthreads();
+    prologue(0, pbeg);
   }
   for (int ks = 0; ks < nk; ++ks) {
     int cur = 0;
@@ -186,8 +273,9 @@ void conv_wgrad_kernel(const WgradArgs a) {
     } else if (ks > 0) {
       issue(0, pbeg + ks * BK);
       __syncthreads();
+      prologue(0, pbeg + ks * BK);
     }
-    const char* As = smem + cur * (A_BYTES + B_BYTES);
+    const char* As = smem + cur * SB;
     const char* Bs = As + A_BYTES;
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
@@ -345,6 +433,25 @@ extern "C" hipError_t dlmpi_conv_wgrad(const WgradArgs* a, int bm, int bn, hipSt
   // (a 256-column variant was measured 1.3-1.9x slower: 2 waves/SIMD and register spills)
   if (bn != 128 || (bm != 128 && bm != 64)) return hipErrorInvalidValue;
   const bool d = a->direct != 0;
+  if (a->pro_a != 0 || a->pro_b != 0) {
+    if ((a->pro_a != 0 && a->pro_a != 2) || (a->pro_b != 0 && a->pro_b != 1)) return hipErrorInvalidValue;
+    const int m = (a->pro_a ? 2 : 0) | (a->pro_b ? 1 : 0);
+#define DLMPI_WGP(BM_, D_)                                                                             \
+  do {                                                                                                \
+    if (m == 2) hipLaunchKernelGGL((conv_wgrad_kernel<BM_, 128, 1, D_, 2, 0>), g, b, 0, s, *a);      \
+    else if (m == 1) hipLaunchKernelGGL((conv_wgrad_kernel<BM_, 128, 1, D_, 0, 1>), g, b, 0, s, *a); \
+    else hipLaunchKernelGGL((conv_wgrad_kernel<BM_, 128, 1, D_, 2, 1>), g, b, 0, s, *a);             \
+  } while (0)
+    if (bm == 128) {
+      if (d) DLMPI_WGP(128, true);
+      else DLMPI_WGP(128, false);
+    } else {
+      if (d) DLMPI_WGP(64, true);
+      else DLMPI_WGP(64, false);
+    }
+#undef DLMPI_WGP
+    return hipGetLastError();
+  }
 #define DLMPI_WG(BM_, ST_)                                                                  \
   do {                                                                                     \
     if (d) hipLaunchKernelGGL((conv_wgrad_kernel<BM_, 128, ST_, true>), g, b, 0, s, *a);   \

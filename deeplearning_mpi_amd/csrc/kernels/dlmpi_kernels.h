@@ -84,6 +84,17 @@ struct ConvArgs {
   float* sk_slab;                  // [tile][slice][TM*TN][threads] f32x4 fragment slabs
   int* sk_tk;                      // [tile] self-resetting arrival tickets
   int cstep, tstep;                // K-iteration: c += cstep, t += tstep per 64-wide step
+  // Operand prologue (regular channel counts, single-stage kernels): every staged A piece of an
+  // in-image tap is rewritten in LDS before the MFMAs (out-of-image taps stay zero):
+  //   pro 1: A := bf16(relu(A * pscale[c] + pshift[c]))   (a deferred forward BN-apply + ReLU)
+  //   pro 2: A := bf16(pcoef[c] * A + pcoef[C + c] * Z + pcoef[2C + c])   (a deferred BN-backward
+  //          apply: A = the masked output gradient dy, Z = the BN input, same pixel grid / C)
+  int pro;
+  const float* pscale;
+  const float* pshift;
+  const float* pcoef;
+  const uint16_t* pz;
+  int ldpz, pzoff;
   ConvPhase ph[4];
 };
 
@@ -109,6 +120,15 @@ struct WgradArgs {
   int* tk;
   float* out;
   int T, Creal, Ko_real, groups;
+  // Operand prologues (conv_igemm's pro modes, applied in LDS to in-range pieces only):
+  //   dy side (A): pro_a 2 -> dz = pcoef[k] * dy + pcoef[Ko + k] * Z + pcoef[2 Ko + k]
+  //   x side  (B): pro_b 1 -> x := relu(x * pscale[c] + pshift[c])
+  int pro_a, pro_b;
+  const float* pcoef;
+  const uint16_t* pz;
+  int ldpz, pzoff;
+  const float* pscale;
+  const float* pshift;
 };
 
 }  // namespace dlmpi

@@ -26,7 +26,7 @@ from typing import NamedTuple, Optional
 import torch
 import torch.nn as nn
 
-from ..ops.act import Act, padc
+from ..ops.act import Act, Deferred, padc
 from ..ops.backend import make_backend
 from ..utils.arena import ParamArena
 from ..utils.profiler import range as trace_range
@@ -94,6 +94,34 @@ _STREAM_HOLD = os.environ.get("DLMPI_STREAM_HOLD", "1") != "0"
 
 # DLMPI_OUTER_DGRAD=0: one-output-channel 1x1 data gradients through the GEMM kernel (A/B)
 _OUTER_DGRAD = os.environ.get("DLMPI_OUTER_DGRAD", "1") != "0"
+
+# Deferred BatchNorm elementwise passes (ops.act.Deferred), off by default:
+# DLMPI_DEFER_BN_FWD=1: never store a BN-apply + ReLU output without residual; the consumer
+#                       convolution rebuilds it in its operand prologue (forward GEMM and weight
+#                       gradient);
+# DLMPI_DEFER_BN_BWD=1: never store dz = BN-backward(dy); the unit's own weight-gradient and
+#                       data-gradient GEMMs rebuild it in their operand prologues.
+# Bit-identical results either way, but measured slower (ResNet-50 bs 256 9,924 vs 11,655 img/s,
+# UNet 512 266 vs 421, profiles/r2_defer_bn_rejected): a consumer re-transforms every element once
+# per tap and per output tile, with an extra LDS round trip and barrier in every K-step, which
+# costs more than the single elementwise pass it removes.
+DEFER_BN_FWD = os.environ.get("DLMPI_DEFER_BN_FWD", "0") != "0"
+DEFER_BN_BWD = os.environ.get("DLMPI_DEFER_BN_BWD", "0") != "0"
+
+
+def bufs(*objs):
+    """The storage tensors behind Acts / Deferred operands (None skipped)."""
+    out = []
+    for o in objs:
+        if o is None:
+            continue
+        if isinstance(o, Deferred):
+            out.extend(o.bufs())
+        elif isinstance(o, Act):
+            out.append(o.buf)
+        else:
+            out.append(o)
+    return out
 
 
 class BwdFuse(NamedTuple):
@@ -163,15 +191,20 @@ class ConvUnit:
         self._bias_pad[:self.K].copy_(self.bias.data)
         return self._bias_pad
 
-    def fwd(self, be, x: Act, train: bool, res: Act = None, out: Act = None, save=True, defer_apply=False):
-        """Returns (output, saved context).  defer_apply (training BN, no residual): skip the
-        BN-apply + ReLU and return the BN input z -- the consumer applies scale/shift (ctx[5:7])
-        itself (the ResNet stem's max-pool), so the BN output is never materialised."""
+    def fwd(self, be, x, train: bool, res: Act = None, out: Act = None, save=True, defer_apply=False):
+        """Returns (output, saved context).  x: an Act or a Deferred operand (rebuilt by the GEMM's
+        operand prologue).  defer_apply (training BN + ReLU, no residual): skip the BN-apply + ReLU;
+        True returns the BN input z -- the consumer applies scale/shift (ctx[5:7]) itself (the ResNet
+        stem's max-pool) --, "act" returns Deferred.affine(z, scale, shift) for the next
+        convolution.  Either way the BN output is never materialised."""
         assert x.C == self.Cp, (x, self.Cp)
         P, Q = self.out_hw(x.H, x.W)
         N, dev = x.N, x.device
         wf = self._weight_fwd()
-        y = out if out is not None else Act.empty(N, P, Q, self.Kp, be.act_dtype, dev)
+        if defer_apply == "act" and not (train and save and res is None and self.relu and self.bn is not None):
+            defer_apply = False
+        y = None if defer_apply and out is None else (
+            out if out is not None else Act.empty(N, P, Q, self.Kp, be.act_dtype, dev))
         bn = self.bn
         if bn is None:
             assert not self.relu or res is None or True
@@ -180,7 +213,8 @@ class ConvUnit:
             return y, ((x, y) if save else None)
         if train:
             z = Act.empty(N, P, Q, self.Kp, be.act_dtype, dev)
-            mt = be.conv_mtiles(N, x.H, x.W, x.C, self.Kp, self.R, self.S, self.stride, self.pad)
+            mt = be.conv_mtiles(N, x.H, x.W, x.C, self.Kp, self.R, self.S, self.stride, self.pad,
+                                pro=isinstance(x, Deferred))
             stats = torch.empty(mt, 2, self.Kp, dtype=be.dt, device=dev)
             be.conv_fwd(x, wf, self.Kp, self.R, self.S, self.stride, self.pad, z, bias=self._bias_vec(), stats=stats)
             vec = torch.empty(4, self.Kp, dtype=be.dt, device=dev)
@@ -195,7 +229,8 @@ class ConvUnit:
                            bn.running_var if bn.track_running_stats else None, mom, bn.eps, scale, shift, mean,
                            invstd)
             if defer_apply and save and res is None:
-                return z, (x, z, None, mean, invstd, scale, shift, False, None)
+                ctx = (x, z, None, mean, invstd, scale, shift, False, None)
+                return (Deferred.affine(z, scale, shift) if defer_apply == "act" else z), ctx
             # residual units: the backward mask (y > 0) cannot be recomputed from z alone, so keep it
             # as bits (1/16 of y's bytes) for the fused data-gradient epilogue
             mbits = None
@@ -241,11 +276,16 @@ class ConvUnit:
                 mask = None
             else:
                 mask = ymask if ymask is not None else (y if (self.relu and use_own_mask) else None)
-            dz = Act.empty(z.N, z.H, z.W, z.C, be.act_dtype, z.device)
-            be.bn_bwd(dy, mask, z, mean, invstd, bn.weight.data if bn.affine else None,
-                      ar.grad_flat(bn.weight) if bn.affine else None, ar.grad_flat(bn.bias) if bn.affine else None,
-                      dz, dyr_out, pre=pre, k2=k2)
-            with grad_side(be, dz.buf, x.buf):
+            gam = bn.weight.data if bn.affine else None
+            dgam = ar.grad_flat(bn.weight) if bn.affine else None
+            dbet = ar.grad_flat(bn.bias) if bn.affine else None
+            if pre is not None and mask is None and dyr_out is None and DEFER_BN_BWD:
+                # finalize only: dz = k1 dy + k2 z + k3 is rebuilt inside the wgrad / dgrad GEMMs
+                dz = be.bn_bwd_deferred(dy, z, mean, invstd, gam, dgam, dbet, pre=pre, k2=k2)
+            else:
+                dz = Act.empty(z.N, z.H, z.W, z.C, be.act_dtype, z.device)
+                be.bn_bwd(dy, mask, z, mean, invstd, gam, dgam, dbet, dz, dyr_out, pre=pre, k2=k2)
+            with grad_side(be, *bufs(dz, x)):
                 if bn.affine:
                     ar.ready(bn.weight, bn.bias)
                 if self.bias is not None:
@@ -257,7 +297,7 @@ class ConvUnit:
             x, y = ctx
             assert not self.relu, "ReLU without BN is not used by the engine models"
             dz = dy
-            with grad_side(be, dz.buf, x.buf):
+            with grad_side(be, *bufs(dz, x)):
                 if self.bias is not None:
                     if self.Kp == self.K:
                         be.channel_sum(dz, ar.grad_flat(self.bias))
@@ -275,7 +315,7 @@ class ConvUnit:
                 and fuse_next is not None and fuse_next.scale is not None and fuse_next.z2 is None
                 and hasattr(be, "outer_dgrad_bn") and _OUTER_DGRAD):
             # one output channel (the UNet head): the data gradient is an outer product
-            part = be.outer_dgrad_bn(dz, ar.get_compute(self.h_dg), self.Kp, dx, fuse_next)
+            part = be.outer_dgrad_bn(be.materialize(dz), ar.get_compute(self.h_dg), self.Kp, dx, fuse_next)
             return dx, part
         part = be.conv_dgrad(dz, ar.get_compute(self.h_dg), self.Cp, self.R, self.S, self.stride, self.pad, dx,
                              res=dx_res, fuse=fuse_next, colsum=colsum)

@@ -19,6 +19,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from ..ops.act import Act, padc
+from . import engine as _engine
 from .engine import BwdFuse, ConvUnit, EngineModule, S2DConvUnit, record_on
 
 
@@ -91,9 +92,11 @@ class _BlockExec:
     def __init__(self, units, ds):
         self.u, self.ud = units, ds
 
-    def fwd(self, be, x: Act, train, save):
+    def fwd(self, be, x: Act, train, save, defer=False):
         """The downsample branch (1x1 conv + BN) depends only on the block input: with a branch
-        stream it runs beside conv1 -> conv2 and joins before the residual add of conv3's BN."""
+        stream it runs beside conv1 -> conv2 and joins before the residual add of conv3's BN.
+        defer: the inner BN + ReLU outputs (bn1, bn2 of a bottleneck) are never stored -- the next
+        convolution rebuilds them in its operand prologue (ops.act.Deferred)."""
         ctxs = []
         br = getattr(be, "branch_stream", None) if self.ud is not None else None
         if br is not None:
@@ -104,7 +107,7 @@ class _BlockExec:
             record_on(br, x)
         h = x
         for k, u in enumerate(self.u[:-1]):
-            h, c = u.fwd(be, h, train, save=save)
+            h, c = u.fwd(be, h, train, save=save, defer_apply="act" if defer else False)
             ctxs.append(c)
         if br is not None:
             main.wait_stream(br)
@@ -123,7 +126,7 @@ class _BlockExec:
         ctxs, cd = st
         return ConvUnit.fuse_spec(ctxs[-1], z2=cd[1] if cd is not None else None)
 
-    def bwd(self, be, st, dy: Act, pre=None, fuse_prev=None):
+    def bwd(self, be, st, dy: Act, pre=None, fuse_prev=None, fuse_inner=False):
         """dy: gradient of the block output.  With ``pre`` (partials from the producer's dgrad
         epilogue) dy is already ReLU-masked.  With ``fuse_prev`` the block-input gradient is
         produced masked for the previous block and returned with its partials."""
@@ -153,20 +156,30 @@ class _BlockExec:
             else:
                 dres = dy
             return self.u[0].bwd(be, ctxs[0], dh, dx_res=dres, pre=part, fuse_next=fuse_prev)
+        # fused BN-backward partials for the inner units also when the block's output gradient comes
+        # without them (the last block, behind the average-pool backward); required when their BN +
+        # ReLU output was deferred (never stored: ctx y is None), so the mask is recomputed from z
+        inner = fuse_inner or any(c[2] is None for c in ctxs[:-1])
         if self.ud is None:
             dyr = Act.empty(dy.N, dy.H, dy.W, dy.C, be.act_dtype, dy.device)   # identity-path grad
-            dh = self.u[-1].bwd(be, ctxs[-1], dy, dyr_out=dyr)
+            dh = self.u[-1].bwd(be, ctxs[-1], dy, dyr_out=dyr, fuse_next=spec(n - 2) if inner else None)
         else:
             dyr = None
-            dh = self.u[-1].bwd(be, ctxs[-1], dy)
+            dh = self.u[-1].bwd(be, ctxs[-1], dy, fuse_next=spec(n - 2) if inner else None)
+        part = None
+        if inner:
+            dh, part = dh
         for k in range(n - 2, 0, -1):
-            dh = self.u[k].bwd(be, ctxs[k], dh)
+            if inner:
+                dh, part = self.u[k].bwd(be, ctxs[k], dh, pre=part, fuse_next=spec(k - 1))
+            else:
+                dh = self.u[k].bwd(be, ctxs[k], dh)
         if self.ud is not None:
             # downsample BN sees the same relu-masked output grad as the main branch
             dres = self.ud.bwd(be, cd, dy, ymask=ylast)
         else:
             dres = dyr
-        out = self.u[0].bwd(be, ctxs[0], dh, dx_res=dres, fuse_next=fuse_prev)
+        out = self.u[0].bwd(be, ctxs[0], dh, dx_res=dres, pre=part, fuse_next=fuse_prev)
         return out
 
 
@@ -257,8 +270,9 @@ class ResNet(EngineModule):
         idx = be.maxpool_fwd(h, 3, 2, 1, p, bn=(cs[5], cs[6]) if defer else None)
         st_blocks = []
         a = p
+        dfr = train and save and self.fuse_bn_bwd and _engine.DEFER_BN_FWD
         for blk in self.blocks:
-            a, st = blk.fwd(be, a, train, save)
+            a, st = blk.fwd(be, a, train, save, defer=dfr)
             st_blocks.append(st)
         pooled = Act.empty(N, 1, 1, a.C, be.act_dtype, x.device)
         be.avgpool_fwd(a, pooled)
@@ -281,7 +295,7 @@ class ResNet(EngineModule):
         pre = None
         for i in range(len(self.blocks) - 1, -1, -1):
             fuse_prev = self.blocks[i - 1].fuse_spec(st_blocks[i - 1]) if (i > 0 and self.fuse_bn_bwd) else None
-            out = self.blocks[i].bwd(be, st_blocks[i], da, pre=pre, fuse_prev=fuse_prev)
+            out = self.blocks[i].bwd(be, st_blocks[i], da, pre=pre, fuse_prev=fuse_prev, fuse_inner=self.fuse_bn_bwd)
             da, pre = out if fuse_prev is not None else (out, None)
         dh = Act.empty(h.N, h.H, h.W, h.C, be.act_dtype, h.device)
         if self.fuse_bn_bwd:   # stem BN-backward statistics in the max-pool backward (mask from z)

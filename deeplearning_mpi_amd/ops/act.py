@@ -57,6 +57,48 @@ class Act:
         return f"Act(N={self.N},H={self.H},W={self.W},C={self.C},ld={self.ld},off={self.off},{self.dtype})"
 
 
+class Deferred:
+    """A GEMM operand that is never stored: the convolution kernels rebuild it from ``src`` in their
+    operand prologue (in LDS, right after the tile lands), which removes a full elementwise pass
+    (read + write) over the tensor and its re-read by the consumer.
+
+    * ``Deferred.affine(z, scale, shift)`` = relu(z * scale + shift): a training BatchNorm-apply +
+      ReLU without residual (the ResNet bottleneck's bn1 / bn2, the first BN of a UNet DoubleConv),
+      consumed by the next convolution's forward and weight gradient;
+    * ``Deferred.bnbwd(dy, z, coef)`` = coef[0] * dy + coef[1] * z + coef[2]: the BatchNorm-backward
+      apply, consumed by the unit's own weight-gradient and data-gradient GEMMs.
+
+    Backends without operand prologues call ``materialize`` (same values)."""
+
+    __slots__ = ("kind", "src", "z", "k0", "k1")
+
+    def __init__(self, kind, src: Act, z: Act = None, k0=None, k1=None):
+        self.kind, self.src, self.z, self.k0, self.k1 = kind, src, z, k0, k1
+
+    @staticmethod
+    def affine(z: Act, scale, shift) -> "Deferred":
+        return Deferred("affine", z, None, scale, shift)
+
+    @staticmethod
+    def bnbwd(dy: Act, z: Act, coef) -> "Deferred":
+        return Deferred("bnbwd", dy, z, coef)
+
+    N = property(lambda self: self.src.N)
+    H = property(lambda self: self.src.H)
+    W = property(lambda self: self.src.W)
+    C = property(lambda self: self.src.C)
+    rows = property(lambda self: self.src.rows)
+    dtype = property(lambda self: self.src.dtype)
+    device = property(lambda self: self.src.device)
+
+    def bufs(self):
+        """Storage the deferred value is computed from (kept alive across streams by the engine)."""
+        return (self.src.buf,) + ((self.z.buf,) if self.z is not None else ())
+
+    def __repr__(self):
+        return f"Deferred({self.kind}, {self.src!r})"
+
+
 def pad8(c: int) -> int:
     return (c + 7) // 8 * 8
 

@@ -15,7 +15,7 @@ import struct
 import torch
 import torch.nn.functional as F
 
-from .act import Act
+from .act import Act, Deferred
 
 
 # --------------------------------------------------------------------------------------------
@@ -82,14 +82,40 @@ class NativeBackend:
         self._branch = s
 
     # ---------------- conv family ----------------
-    def conv_mtiles(self, N, H, W, C, K, R, S, stride, pad):
-        return self.C.conv2d_fwd_mtiles(N, H, W, C, K, R, S, stride, pad, 0)
+    prologue = True   # the GEMM kernels consume ops.act.Deferred operands directly
 
-    def conv_fwd(self, x: Act, w, K, R, S, stride, pad, y: Act, bias=None, res: Act = None, scale=None,
+    @staticmethod
+    def _pro(op):
+        """(source Act, prologue mode, k0, k1, Z buffer, Z ld, Z offset) of a GEMM operand."""
+        if not isinstance(op, Deferred):
+            return op, 0, None, None, None, 0, 0
+        if op.kind == "affine":
+            return op.src, 1, op.k0, op.k1, None, 0, 0
+        return op.src, 2, op.k0, None, op.z.buf, op.z.ld, op.z.off
+
+    def materialize(self, d) -> Act:
+        """The stored form of a Deferred operand (one elementwise pass)."""
+        if not isinstance(d, Deferred):
+            return d
+        src = d.src
+        out = Act.empty(src.N, src.H, src.W, src.C, self.act_dtype, src.device)
+        if d.kind == "affine":
+            self.bn_apply(src, d.k0, d.k1, None, True, out)
+        else:
+            self.C.bn_bwd_apply(src.buf, src.ld, src.off, None, 0, 0, d.z.buf, d.z.ld, d.z.off, src.rows, src.C,
+                                d.k0, out.buf, None)
+        return out
+
+    def conv_mtiles(self, N, H, W, C, K, R, S, stride, pad, pro=False):
+        return self.C.conv2d_fwd_mtiles_pro(N, H, W, C, K, R, S, stride, pad, 0, int(bool(pro)))
+
+    def conv_fwd(self, x, w, K, R, S, stride, pad, y: Act, bias=None, res: Act = None, scale=None,
                  shift=None, relu=False, stats=None, kvalid=0):
-        self.C.conv2d_fwd(x.buf, x.N, x.H, x.W, x.C, x.ld, x.off, w, K, R, S, stride, pad, y.buf, y.ld, y.off,
-                          bias, res.buf if res is not None else None, res.ld if res is not None else 0,
-                          res.off if res is not None else 0, scale, shift, bool(relu), stats, 0, int(kvalid), 0)
+        x, pm, k0, k1, zb, zld, zoff = self._pro(x)
+        self.C.conv2d_fwd_pro(x.buf, x.N, x.H, x.W, x.C, x.ld, x.off, w, K, R, S, stride, pad, y.buf, y.ld, y.off,
+                              bias, res.buf if res is not None else None, res.ld if res is not None else 0,
+                              res.off if res is not None else 0, scale, shift, bool(relu), stats, 0, int(kvalid), 0,
+                              pm, k0, k1, zb, zld, zoff)
 
     def conv_fwd_bnbwd(self, x: Act, w, K, R, S, stride, pad, y: Act, fuse):
         """Forward conv producing the gradient of relu(BN(z)) (fuse = BwdFuse(None, z, None, scale,
@@ -108,16 +134,20 @@ class NativeBackend:
         def t(a):
             return (a.buf, a.ld, a.off) if a is not None else (None, 0, 0)
 
-        return self.C.conv2d_dgrad(dy.buf, dy.N, dy.H, dy.W, dy.C, dy.ld, dy.off, wT, C, R, S, stride, pad, dx.H,
-                                   dx.W, dx.buf, dx.ld, dx.off, *t(res), *t(m), *t(z), *t(z2), sc, sh, mb,
-                                   bool(colsum and fuse is None))
+        dy, pm, k0, k1, zb, zld, zoff = self._pro(dy)
+        return self.C.conv2d_dgrad_pro(dy.buf, dy.N, dy.H, dy.W, dy.C, dy.ld, dy.off, wT, C, R, S, stride, pad, dx.H,
+                                       dx.W, dx.buf, dx.ld, dx.off, *t(res), *t(m), *t(z), *t(z2), sc, sh, mb,
+                                       bool(colsum and fuse is None), pm, k0, k1, zb, zld, zoff)
 
     def convT_fwd(self, x: Act, wf, Cout, y: Act, bias=None):
         self.C.convT2x2_fwd(x.buf, x.N, x.H, x.W, x.C, x.ld, x.off, wf, Cout, y.buf, y.ld, y.off, bias)
 
-    def conv_wgrad(self, dy: Act, x: Act, R, S, stride, pad, grad, Creal, Ko_real):
-        self.C.conv2d_wgrad(dy.buf, dy.ld, dy.off, dy.C, x.buf, x.N, x.H, x.W, x.C, x.ld, x.off, R, S, stride, pad,
-                            dy.H, dy.W, grad, Creal, Ko_real)
+    def conv_wgrad(self, dy, x, R, S, stride, pad, grad, Creal, Ko_real):
+        dy, pa, ca, _, zb, zld, zoff = self._pro(dy)
+        x, pb, sb, hb, _, _, _ = self._pro(x)
+        assert pa in (0, 2) and pb in (0, 1)
+        self.C.conv2d_wgrad_pro(dy.buf, dy.ld, dy.off, dy.C, x.buf, x.N, x.H, x.W, x.C, x.ld, x.off, R, S, stride,
+                                pad, dy.H, dy.W, grad, Creal, Ko_real, pa, ca, zb, zld, zoff, pb, sb, hb)
 
     # ---------------- batch norm ----------------
     def bn_finalize(self, stats, ntiles, C, count, gamma, beta, rm, rv, momentum, eps, scale, shift, save_mean,
@@ -135,6 +165,13 @@ class NativeBackend:
         self.C.bn_apply(x.buf, x.ld, x.off, x.rows, x.C, scale, shift, res.buf if res is not None else None,
                         res.ld if res is not None else 0, res.off if res is not None else 0, bool(relu), y.buf, y.ld,
                         y.off, mbits)
+
+    def bn_bwd_deferred(self, dy: Act, x: Act, mean, invstd, gamma, dgamma, dbeta, pre, k2=1) -> Deferred:
+        """BN backward from the producer's fused partials (``pre``): finalize only (dgamma, dbeta and
+        the apply coefficients); dz stays a Deferred operand of the unit's wgrad / dgrad GEMMs."""
+        coef = torch.empty(3, x.C, dtype=torch.float32, device=x.device)
+        self.C.bn_bwd_finalize_fused(pre, k2, x.C, float(x.rows), gamma, mean, invstd, dgamma, dbeta, coef)
+        return Deferred.bnbwd(dy, x, coef)
 
     def bn_bwd(self, dy: Act, ymask: Act, x: Act, mean, invstd, gamma, dgamma, dbeta, dx: Act, dyr_out: Act = None,
                pre=None, k2=1):
@@ -304,11 +341,42 @@ class RefBackend:
     def _store(y: Act, v_nchw):
         y.nhwc().copy_(v_nchw[:, :y.C].permute(0, 2, 3, 1))
 
-    def conv_mtiles(self, N, H, W, C, K, R, S, stride, pad):
+    prologue = False   # Deferred operands are materialized (same values) before each consumer
+
+    def materialize(self, d) -> Act:
+        if not isinstance(d, Deferred):
+            return d
+        src = d.src
+        out = Act.empty(src.N, src.H, src.W, src.C, self.act_dtype, src.device)
+        if d.kind == "affine":
+            self.bn_apply(src, d.k0, d.k1, None, True, out)
+        else:
+            c = d.k0.to(self.dt)
+            out.nhwc().copy_(c[0] * src.nhwc().to(self.dt) + c[1] * d.z.nhwc().to(self.dt) + c[2])
+        return out
+
+    def bn_bwd_deferred(self, dy: Act, x: Act, mean, invstd, gamma, dgamma, dbeta, pre, k2=1) -> Deferred:
+        """bn_bwd's result as coefficients: dz = k1*(dy - s1/M - xhat*s2/M) = c0*dy + c1*x + c2."""
+        ps = pre.sum(0)
+        s1 = ps[0]
+        s2 = invstd * (ps[k2] - mean * s1)
+        if dbeta is not None:
+            dbeta.add_(s1)
+        if dgamma is not None:
+            dgamma.add_(s2)
+        M = x.rows
+        k1 = (gamma if gamma is not None else torch.ones_like(mean)) * invstd
+        c0 = k1
+        c1 = -k1 * invstd * s2 / M
+        c2 = -k1 * s1 / M + k1 * mean * invstd * s2 / M
+        return Deferred.bnbwd(dy, x, torch.stack([c0, c1, c2]).to(self.dt))
+
+    def conv_mtiles(self, N, H, W, C, K, R, S, stride, pad, pro=False):
         return 1
 
-    def conv_fwd(self, x: Act, w, K, R, S, stride, pad, y: Act, bias=None, res=None, scale=None, shift=None,
+    def conv_fwd(self, x, w, K, R, S, stride, pad, y: Act, bias=None, res=None, scale=None, shift=None,
                  relu=False, stats=None, kvalid=0):
+        x = self.materialize(x)
         wk = w.view(K, R, S, x.C).permute(0, 3, 1, 2).to(self.dt)
         out = F.conv2d(x.nchw().to(self.dt), wk, None, stride, pad)
         if bias is not None:
@@ -324,7 +392,8 @@ class RefBackend:
             out = F.relu(out)
         self._store(y, out)
 
-    def conv_dgrad(self, dy: Act, wT, C, R, S, stride, pad, dx: Act, res=None, fuse=None, colsum=False):
+    def conv_dgrad(self, dy, wT, C, R, S, stride, pad, dx: Act, res=None, fuse=None, colsum=False):
+        dy = self.materialize(dy)
         K = dy.C
         wk = wT.view(C, R, S, K).permute(3, 0, 1, 2).to(self.dt)
         g = torch.nn.grad.conv2d_input((dx.N, C, dx.H, dx.W), wk, dy.nchw().to(self.dt), stride, pad)
@@ -366,7 +435,8 @@ class RefBackend:
         out = F.conv_transpose2d(x.nchw().to(self.dt), wk, bias, stride=2)
         self._store(y, out)
 
-    def conv_wgrad(self, dy: Act, x: Act, R, S, stride, pad, grad, Creal, Ko_real):
+    def conv_wgrad(self, dy, x, R, S, stride, pad, grad, Creal, Ko_real):
+        dy, x = self.materialize(dy), self.materialize(x)
         Ko, Cc = dy.C, x.C
         gw = torch.nn.grad.conv2d_weight(x.nchw().to(self.dt), (Ko, Cc, R, S), dy.nchw().to(self.dt), stride, pad)
         gw = gw.permute(0, 2, 3, 1)[:Ko_real, :, :, :Creal]

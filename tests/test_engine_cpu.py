@@ -174,3 +174,28 @@ def test_flat_gradient_layout_follows_backward_ready_order(name):
         _, pb = a.buckets(*caps)
         bseq = [pb[i] for i in seq]
         assert bseq == sorted(bseq)
+
+
+@pytest.mark.parametrize("arch", ["resnet50", "resnet18", "unet", "unet_bilinear"])
+def test_deferred_bn_passes_match_torch(arch, monkeypatch):
+    """The schedules with deferred BatchNorm elementwise passes (ops.act.Deferred: forward BN-apply
+    rebuilt by the next conv, BN-backward apply rebuilt by the unit's wgrad / dgrad) are exact
+    against fp64 autograd too (the reference backend materializes the deferred operands)."""
+    import deeplearning_mpi_amd.models.engine as E
+
+    monkeypatch.setattr(E, "DEFER_BN_FWD", True)
+    monkeypatch.setattr(E, "DEFER_BN_BWD", True)
+    g = torch.Generator().manual_seed(4)
+    if arch.startswith("unet"):
+        mode = "bilinear" if "bilinear" in arch else "conv_transpose"
+        x = torch.randn(2, 3, 32, 32, generator=g)
+        y = (torch.rand(2, 32, 32, generator=g) > 0.5).float()
+        skip = lambda n: n.endswith("bias") and "double_conv.double_conv" in n  # noqa: E731 (grad == 0)
+        _run_pair(lambda: UNet(out_classes=1, up_sample_mode=mode), x, y,
+                  lambda o, t: bce_with_logits(o.squeeze(1), t),
+                  lambda o, t: F.binary_cross_entropy_with_logits(o.squeeze(1), t), skip=skip)
+    else:
+        x = torch.randn(8, 3, 64, 64, generator=g)
+        y = torch.randint(10, (8,), generator=g)
+        make = resnet50 if arch == "resnet50" else resnet18
+        _run_pair(lambda: make(num_classes=10), x, y, cross_entropy, F.cross_entropy)

@@ -522,3 +522,119 @@ def test_wgrad_in_launch_reduction_bit_identical_to_two_kernel_path(tmp_path):
         res[mode] = torch.load(tmp_path / f"o{mode}.pt", weights_only=True)
     for i in res["0"]:
         assert torch.equal(res["100000"][i], res["0"][i]), shapes[i]
+
+
+# ------------------------------------------------------------------ operand prologues (Deferred)
+PRO_SHAPES = [
+    # N, H, W, Cin, Cout, R, stride, pad
+    (2, 14, 14, 64, 64, 3, 1, 1),
+    (3, 7, 7, 256, 64, 1, 1, 0),        # row remainders
+    (2, 16, 16, 128, 256, 3, 2, 1),     # stride 2: dgrad phases
+    (2, 14, 14, 256, 512, 1, 2, 0),
+    (1, 16, 24, 192, 64, 3, 1, 1),      # UNet concat width
+    (8, 64, 64, 64, 64, 3, 1, 1),       # 256-row tiles
+    (2, 4, 4, 512, 512, 3, 1, 1),       # split-K
+]
+
+
+def _deferred_pair(N, H, W, C):
+    """(affine Deferred, its materialized Act) and (bnbwd Deferred, materialized)."""
+    from deeplearning_mpi_amd.ops.act import Deferred
+
+    nb = NativeBackend(DEV)
+    z, _ = _act(N, H, W, C)
+    sc, sh = torch.rand(C, device=DEV) + 0.5, torch.randn(C, device=DEV) * 0.5
+    aff = Deferred.affine(z, sc, sh)
+    dy, _ = _act(N, H, W, C)
+    coef = torch.stack([torch.rand(C, device=DEV) + 0.5, torch.randn(C, device=DEV) * 0.1,
+                        torch.randn(C, device=DEV) * 0.1])
+    bwd = Deferred.bnbwd(dy, z, coef)
+    return (aff, nb.materialize(aff)), (bwd, nb.materialize(bwd))
+
+
+@pytest.mark.parametrize("shape", PRO_SHAPES)
+def test_conv_prologues_bit_identical_to_materialized_operands(shape):
+    """Forward with a deferred BN-apply+ReLU operand, data gradient with a deferred BN-backward
+    operand, weight gradient with either or both: every result bit-identical to the same kernels
+    on the materialized tensors (incl. zero padding taps, row tails, stride-2 phases, split-K)."""
+    nb = NativeBackend(DEV)
+    N, H, W, Cin, K, R, s, p = shape
+    Cp, Kp = pad8(Cin), pad8(K)
+    P, Q = (H + 2 * p - R) // s + 1, (W + 2 * p - R) // s + 1
+    (aff, affm), _ = _deferred_pair(N, H, W, Cp)
+    w = (torch.randn(Kp, R, R, Cp, device=DEV) / (R * R * Cin) ** 0.5).to(torch.bfloat16)
+    # forward + BN stats
+    ys = [_empty(N, P, Q, Kp) for _ in range(2)]
+    sts = [torch.zeros(nb.conv_mtiles(N, H, W, Cp, Kp, R, R, s, p, pro=pro), 2, Kp, device=DEV) for pro in (1, 0)]
+    nb.conv_fwd(aff, w, Kp, R, R, s, p, ys[0], stats=sts[0])
+    nb.conv_fwd(affm, w, Kp, R, R, s, p, ys[1], stats=sts[1])
+    torch.cuda.synchronize()
+    assert torch.equal(ys[0].buf, ys[1].buf)
+    assert torch.allclose(sts[0].sum(0), sts[1].sum(0), rtol=1e-5, atol=1e-3)
+    # data gradient: dy operand deferred (BN backward of the layer above)
+    _, (bwd, bwdm) = _deferred_pair(N, P, Q, Kp)
+    wT = (torch.randn(Cp, R, R, Kp, device=DEV) / (R * R * K) ** 0.5).to(torch.bfloat16)
+    dxs = [_empty(N, H, W, Cp) for _ in range(2)]
+    nb.conv_dgrad(bwd, wT, Cp, R, R, s, p, dxs[0])
+    nb.conv_dgrad(bwdm, wT, Cp, R, R, s, p, dxs[1])
+    torch.cuda.synchronize()
+    assert torch.equal(dxs[0].buf, dxs[1].buf)
+    # weight gradient: dy deferred, x deferred, both
+    for dyo, xo in ((bwd, affm), (bwdm, aff), (bwd, aff)):
+        g1 = torch.zeros(K * R * R * Cin, device=DEV)
+        g2 = torch.zeros_like(g1)
+        nb.conv_wgrad(dyo, xo, R, R, s, p, g1, Cin, K)
+        nb.conv_wgrad(bwdm, affm, R, R, s, p, g2, Cin, K)
+        torch.cuda.synchronize()
+        assert torch.equal(g1, g2), (type(dyo).__name__, type(xo).__name__)
+
+
+@pytest.mark.parametrize("model", ["resnet50", "unet"])
+def test_deferred_bn_passes_bit_identical_training(model):
+    """Three training steps with the deferred BN elementwise passes (forward BN-apply rebuilt in the
+    next conv, BN-backward apply rebuilt in the wgrad/dgrad GEMMs) equal the materialized schedule
+    bit for bit: losses, parameters, BN buffers."""
+    import copy
+
+    import deeplearning_mpi_amd.models.engine as E
+    from deeplearning_mpi_amd.models import UNet, resnet50
+    from deeplearning_mpi_amd.ops import bce_with_logits, cross_entropy
+    from deeplearning_mpi_amd.optim import SGD
+
+    g = torch.Generator(device=DEV).manual_seed(11)
+    if model == "resnet50":
+        make = lambda: resnet50(num_classes=100)   # noqa: E731
+        x = torch.randn(8, 3, 96, 96, device=DEV, generator=g)
+        y = torch.randint(100, (8,), device=DEV, generator=g)
+        lossf = lambda o: cross_entropy(o, y)   # noqa: E731
+    else:
+        make = lambda: UNet(out_classes=1)   # noqa: E731
+        x = torch.randn(2, 3, 64, 64, device=DEV, generator=g)
+        y = (torch.rand(2, 64, 64, device=DEV, generator=g) > 0.5).float()
+        lossf = lambda o: bce_with_logits(o.squeeze(1), y)   # noqa: E731
+    torch.manual_seed(0)
+    m0 = make().to(DEV)
+    res = []
+    old = (E.DEFER_BN_FWD, E.DEFER_BN_BWD)
+    try:
+        for flag in (True, False):
+            E.DEFER_BN_FWD = E.DEFER_BN_BWD = flag
+            m = copy.deepcopy(m0)
+            m.engine_setup(DEV)
+            m._be.aux_min_pixels = 0
+            opt = SGD(m.parameters(), lr=0.05, momentum=0.9)
+            ls = []
+            for _ in range(3):
+                opt.zero_grad()
+                loss = lossf(m(x))
+                loss.backward()
+                opt.step()
+                ls.append(loss.detach().clone())
+            torch.cuda.synchronize()
+            res.append((torch.stack(ls), [p.detach().clone() for p in m.parameters()],
+                        [b.detach().clone() for b in m.buffers()]))
+    finally:
+        E.DEFER_BN_FWD, E.DEFER_BN_BWD = old
+    assert torch.equal(res[0][0], res[1][0])
+    for a, b in zip(res[0][1] + res[0][2], res[1][1] + res[1][2]):
+        assert torch.equal(a, b)
