@@ -124,7 +124,7 @@ def main():
     import deeplearning_mpi_amd as dl
     from deeplearning_mpi_amd.data import device_batch
     from deeplearning_mpi_amd.models import ARCHS, UNet
-    from deeplearning_mpi_amd.ops import BCEWithLogitsLoss, CrossEntropyLoss
+    from deeplearning_mpi_amd.ops import BCEWithLogitsLoss, CrossEntropyLoss, backward
     from deeplearning_mpi_amd.optim import SGD, Adam, clip_grad_norm_
 
     comm = dl.init_distributed(args.backend)
@@ -161,10 +161,10 @@ def main():
         out = ddp(x)
         if cfg["task"] == "cls":
             loss = crit(out, y)
-            loss.backward()
+            backward(loss)
         else:
             loss = crit(out.squeeze(1), y)
-            loss.backward()
+            backward(loss)
             clip_grad_norm_(model.parameters(), 1.0, optimizer=opt)
         opt.step()
         return loss
@@ -204,7 +204,7 @@ def main():
                     out = ddp(x)
                     loss = crit(out, y) if cfg["task"] == "cls" else crit(out.squeeze(1), y)
                 with tm.phase("backward"):   # includes comm_exposed
-                    loss.backward()
+                    backward(loss)
                 with tm.phase("optimizer"):
                     if cfg["task"] == "seg":
                         clip_grad_norm_(model.parameters(), 1.0, optimizer=opt)

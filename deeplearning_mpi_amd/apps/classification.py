@@ -25,7 +25,7 @@ from torch.utils.data import DataLoader
 from .. import parallel
 from ..data import CIFAR10, CifarTransform, DeviceBatches, DeviceImageDataset, DistributedSampler, SyntheticImages
 from ..models import ARCHS
-from ..ops import CrossEntropyLoss, top1_correct
+from ..ops import CrossEntropyLoss, backward, top1_correct
 from ..optim import SGD
 from ..utils.checkpoint import load_checkpoint, resume_state, save_checkpoint, set_rng_state
 from ..utils.graphs import CapturedStep
@@ -58,10 +58,11 @@ def build_argparser(variant: str = "main") -> argparse.ArgumentParser:
     p.add_argument("--eval_before_train", action="store_true", default=variant != "main",
                    help="resnet.py variant: evaluate/save before training on eval epochs")
     p.add_argument("--precision", default="bf16", choices=["bf16", "fp32"],
-                   help="bf16: native gfx950 kernels; fp32: the same schedules on fp32 torch ops")
+                   help="bf16: native gfx950 kernels on bf16 activations; fp32: the same kernels on fp32 "
+                        "activations and weights (fp32 MFMA)")
     p.add_argument("--graph", nargs="?", const="1", default="auto", choices=["auto", "0", "1"],
                    help="replay each full-size training step from a captured hipGraph (ragged last batches run "
-                        "eagerly); auto = on for bf16 training on a GPU")
+                        "eagerly); auto = on for launch-bound GPU training")
     p.add_argument("--data_on_device", default="auto", choices=["auto", "0", "1"],
                    help="keep CIFAR-10 resident in GPU memory and build each augmented batch with one kernel "
                         "(data/device.py); auto = on for GPU training on real data")
@@ -75,13 +76,12 @@ def use_graph(args, device, pixels=None) -> bool:
     step smaller than the auxiliary-stream threshold (N*H*W < DLMPI_AUX_MIN_PIXELS, default 1M:
     the reference's ResNet-18 on CIFAR, 46k -> 85k img/s).  Larger steps run their weight-gradient
     and residual-branch streams concurrently, which a replayed graph loses (measured: ResNet-50
-    bs 256 -7 %, ResNet-152 -13 %, UNet 512 -2 %, profiles/r2_graph_ab).  The fp32 option runs
-    stock torch ops, captured only on request."""
+    bs 256 -7 %, ResNet-152 -13 %, UNet 512 -2 %, profiles/r2_graph_ab)."""
     if args.graph in (True, "1"):
         return device.type == "cuda"
     if args.graph in (False, "0"):
         return False
-    if device.type != "cuda" or args.precision != "bf16":
+    if device.type != "cuda":
         return False
     if pixels is None:
         side = args.image_size if getattr(args, "synthetic", False) else 32
@@ -92,7 +92,7 @@ def use_graph(args, device, pixels=None) -> bool:
 def set_random_seeds(seed: int):
     """Seeds + the reference's cuDNN flags (C16: resnet/main.py:26-33, unet/train.py:35-41).  The
     flags only affect stock torch ops; the engine's own kernels are deterministic by construction
-    (fixed-order reductions, no float atomics) except the bilinear up-sampling backward."""
+    (fixed-order reductions, no float atomics; the bilinear up-sampling backward is a gather)."""
     torch.manual_seed(seed)
     np.random.seed(seed)
     random.seed(seed)
@@ -166,7 +166,7 @@ def run(args) -> dict:
     def train_step(x, y):
         optimizer.zero_grad()
         loss = criterion(ddp(x), y)
-        loss.backward()
+        backward(loss)
         optimizer.step()
         return loss
 

@@ -29,7 +29,7 @@ from tqdm import tqdm
 from .. import parallel
 from ..data import CarvanaDataset, DeviceBatches, DeviceCachedDataset, DistributedSampler, SyntheticMasks
 from ..models import UNet
-from ..ops import BCEWithLogitsLoss, dice_per_sample
+from ..ops import BCEWithLogitsLoss, backward, dice_per_sample
 from ..optim import Adam, clip_grad_norm_
 from ..utils.graphs import CapturedStep
 from ..utils.checkpoint import load_checkpoint, resume_state, save_checkpoint, set_rng_state
@@ -64,10 +64,11 @@ def build_argparser() -> argparse.ArgumentParser:
     p.add_argument("--eval_every", type=int, default=10)
     p.add_argument("--bucket_mb", type=float, default=None)
     p.add_argument("--precision", default="bf16", choices=["bf16", "fp32"],
-                   help="bf16: native gfx950 kernels; fp32: the same schedules on fp32 torch ops")
+                   help="bf16: native gfx950 kernels on bf16 activations; fp32: the same kernels on fp32 "
+                        "activations and weights (fp32 MFMA)")
     p.add_argument("--graph", nargs="?", const="1", default="auto", choices=["auto", "0", "1"],
                    help="replay each full-size training step from a captured hipGraph (ragged last batches run "
-                        "eagerly); auto = on for bf16 training on a GPU")
+                        "eagerly); auto = on for launch-bound GPU training")
     p.add_argument("--benchmark_steps", type=int, default=0,
                    help="time this many steps on a synthetic device batch, print images/sec and exit")
     return p
@@ -76,7 +77,7 @@ def build_argparser() -> argparse.ArgumentParser:
 def set_random_seeds(seed):
     """Seeds + the reference's cuDNN flags (C16: resnet/main.py:26-33, unet/train.py:35-41).  The
     flags only affect stock torch ops; the engine's own kernels are deterministic by construction
-    (fixed-order reductions, no float atomics) except the bilinear up-sampling backward."""
+    (fixed-order reductions, no float atomics; the bilinear up-sampling backward is a gather)."""
     torch.manual_seed(seed)
     np.random.seed(seed)
     random.seed(seed)
@@ -207,7 +208,7 @@ def run(args) -> dict:
         pred = ddp(images).squeeze(1)
         loss = criterion(pred, masks)
         optimizer.zero_grad()
-        loss.backward()
+        backward(loss)
         # collective NaN/Inf guard: a non-finite all-reduced grad norm skips the step on all ranks
         clip_grad_norm_(model.parameters(), max_norm=args.max_norm, optimizer=optimizer)
         optimizer.step()

@@ -40,9 +40,30 @@ static inline void require_gpu(const at::Tensor& t, const char* name) {
 
 static inline int ceil_div(int64_t a, int64_t b) { return (int)((a + b - 1) / b); }
 
-// K-iteration constants: the 64-wide reduction step walks channels (C % 64 == 0) or taps (64 % C == 0)
+// Activation storage type: bf16 (the product path) or fp32 (the fp32 precision path).  Every
+// activation operand of one launch must share it; the kernels are instantiated for both.
+static inline int act_f32(const at::Tensor& t, const char* what) {
+  if (t.scalar_type() == at::kFloat) return 1;
+  if (t.scalar_type() == at::kBFloat16) return 0;
+  throw std::runtime_error(std::string(what) + ": activations must be bf16 or fp32");
+}
+static inline void same_type(const at::Tensor& ref, const c10::optional<at::Tensor>& t, const char* what) {
+  if (t.has_value() && t->defined() && t->scalar_type() != ref.scalar_type())
+    throw std::runtime_error(std::string(what) + ": operand dtype differs from the activations'");
+}
+static inline void same_type(const at::Tensor& ref, const at::Tensor& t, const char* what) {
+  same_type(ref, c10::optional<at::Tensor>(t), what);
+}
+
+// K-iteration constants: the reduction step (64 bf16 / 32 fp32 elements = one 128-byte LDS row)
+// walks channels (C a multiple of it) or, for small C, every 16-byte piece is its own tap
 static void set_kstep(ConvArgs& a, int C) {
   if (C % 8 != 0) throw std::runtime_error("conv: channel count must be a multiple of 8 (pad it)");
+  if (a.f32) {   // conv_igemm.hip launch_f32: C < 32 or C % 32 != 0 -> small-channel staging
+    a.cstep = C % 32 == 0 ? 32 : 0;
+    a.tstep = 0;
+    return;
+  }
   if (C >= 64) {
     if (C % 64 != 0) throw std::runtime_error("conv: channels >= 64 must be a multiple of 64");
     a.cstep = 64;
@@ -116,9 +137,15 @@ static void pick_tiles(int64_t M, int Kout, int64_t red, int cin, int& bm, int& 
   else if (tiles < 512) bm = 64;
 }
 
-static void finish_phase(ConvPhase& p, int Nimg, int C, int bm) {
+// fp32: single-stage 4-wave tiles only, at most 128 x 128 (launch_f32)
+static void f32_tiles(int& bm, int& bn) {
+  bm = std::min(bm, 128);
+  bn = std::min(bn, 128);
+}
+
+static void finish_phase(ConvPhase& p, int Nimg, int C, int bm, bool f32 = false) {
   p.mtiles = ceil_div((int64_t)Nimg * p.P * p.Q, bm);
-  p.ksteps = ceil_div((int64_t)p.Tr * p.Ts * C, 64);
+  p.ksteps = ceil_div((int64_t)p.Tr * p.Ts * C, f32 ? 32 : 64);
   if (p.Tr * p.Ts == 0) p.ksteps = 0;
   p.fdPQ = make_fastdiv((uint32_t)std::max(1, p.P * p.Q));
   p.fdQ = make_fastdiv((uint32_t)std::max(1, p.Q));
@@ -184,6 +211,9 @@ int conv2d_fwd_pro(const at::Tensor& x, int N, int H, int W, int C, int ldx, int
   require_gpu(x, "x");
   const int P = (H + 2 * pad - R) / stride + 1, Q = (W + 2 * pad - S) / stride + 1;
   ConvArgs a{};
+  a.f32 = act_f32(x, "conv2d_fwd");
+  same_type(x, w, "conv2d_fwd w");
+  same_type(x, res, "conv2d_fwd res");
   a.x = ptr<uint16_t>(x);
   a.H = H; a.W = W; a.C = C; a.ldx = ldx; a.xoff = xoff;
   a.w = ptr<uint16_t>(w);
@@ -199,6 +229,7 @@ int conv2d_fwd_pro(const at::Tensor& x, int N, int H, int W, int C, int ldx, int
   set_prologue(a, pro, pk0, pk1, pz, ldpz, pzoff);
   int bm, bn;
   pick_tiles((int64_t)N * P * Q, K, (int64_t)R * S * C, C, bm, bn, pro != 0);
+  if (a.f32) f32_tiles(bm, bn);
   if (bm_req > 0) bm = bm_req;   // tests / experiments: force a tile shape
   if (bn_req > 0) bn = bn_req;
   a.ntiles = ceil_div(K, bn);
@@ -208,7 +239,7 @@ int conv2d_fwd_pro(const at::Tensor& x, int N, int H, int W, int C, int ldx, int
   p.dh0 = -pad; p.dhs = 1; p.dw0 = -pad; p.dws = 1;
   p.wr0 = 0; p.wrs = 1; p.ws0 = 0; p.wss = 1;
   p.oh0 = 0; p.ow0 = 0;
-  finish_phase(p, N, C, bm);
+  finish_phase(p, N, C, bm, a.f32);
   check(dlmpi_conv_igemm(&a, bm, bn, cur_stream()), "conv2d_fwd");
   return p.mtiles;   // rows of the stats partial buffer
 }
@@ -234,6 +265,10 @@ at::Tensor conv2d_fwd_bnbwd(const at::Tensor& x, int N, int H, int W, int C, int
   require_gpu(x, "x");
   const int P = (H + 2 * pad - R) / stride + 1, Q = (W + 2 * pad - S) / stride + 1;
   ConvArgs a{};
+  a.f32 = act_f32(x, "conv2d_fwd_bnbwd");
+  same_type(x, w, "conv2d_fwd_bnbwd w");
+  same_type(x, z, "conv2d_fwd_bnbwd z");
+  same_type(x, y, "conv2d_fwd_bnbwd y");
   a.x = ptr<uint16_t>(x);
   a.H = H; a.W = W; a.C = C; a.ldx = ldx; a.xoff = xoff;
   a.w = ptr<uint16_t>(w);
@@ -254,6 +289,7 @@ at::Tensor conv2d_fwd_bnbwd(const at::Tensor& x, int N, int H, int W, int C, int
   set_kstep(a, C);
   int bm, bn;
   pick_tiles((int64_t)N * P * Q, K, (int64_t)R * S * C, C, bm, bn);
+  if (a.f32) f32_tiles(bm, bn);
   a.ntiles = ceil_div(K, bn);
   a.nphase = 1;
   ConvPhase& p = a.ph[0];
@@ -261,7 +297,7 @@ at::Tensor conv2d_fwd_bnbwd(const at::Tensor& x, int N, int H, int W, int C, int
   p.dh0 = -pad; p.dhs = 1; p.dw0 = -pad; p.dws = 1;
   p.wr0 = 0; p.wrs = 1; p.ws0 = 0; p.wss = 1;
   p.oh0 = 0; p.ow0 = 0;
-  finish_phase(p, N, C, bm);
+  finish_phase(p, N, C, bm, a.f32);
   at::Tensor stats = at::empty({(int64_t)p.mtiles, 2, (int64_t)K}, x.options().dtype(at::kFloat));
   a.stats = ptr<float>(stats);
   check(dlmpi_conv_igemm(&a, bm, bn, cur_stream()), "conv2d_fwd_bnbwd");
@@ -269,15 +305,17 @@ at::Tensor conv2d_fwd_bnbwd(const at::Tensor& x, int N, int H, int W, int C, int
 }
 
 // Number of BN-stat partial rows conv2d_fwd will produce (so the caller can size `stats`).
-int conv2d_fwd_mtiles_pro(int N, int H, int W, int C, int K, int R, int S, int stride, int pad, int bm_req, int pro) {
+int conv2d_fwd_mtiles_pro(int N, int H, int W, int C, int K, int R, int S, int stride, int pad, int bm_req, int pro,
+                          int f32) {
   const int P = (H + 2 * pad - R) / stride + 1, Q = (W + 2 * pad - S) / stride + 1;
   int bm, bn;
   pick_tiles((int64_t)N * P * Q, K, (int64_t)R * S * C, C, bm, bn, pro != 0);
+  if (f32) f32_tiles(bm, bn);
   if (bm_req > 0) bm = bm_req;
   return ceil_div((int64_t)N * P * Q, bm);
 }
 int conv2d_fwd_mtiles(int N, int H, int W, int C, int K, int R, int S, int stride, int pad, int bm_req) {
-  return conv2d_fwd_mtiles_pro(N, H, W, C, K, R, S, stride, pad, bm_req, 0);
+  return conv2d_fwd_mtiles_pro(N, H, W, C, K, R, S, stride, pad, bm_req, 0, 0);
 }
 
 // dx[n, h, w, dxoff + c] = sum_{r,s,k} dy[n, (h+pad-r)/stride, (w+pad-s)/stride, k] * wT[c][r][s][k]  (+ res)
@@ -300,6 +338,13 @@ c10::optional<at::Tensor> conv2d_dgrad_pro(const at::Tensor& dy, int N, int P, i
   require_gpu(dy, "dy");
   if (stride > 2) throw std::runtime_error("conv2d_dgrad: stride <= 2 supported");
   ConvArgs a{};
+  a.f32 = act_f32(dy, "conv2d_dgrad");
+  same_type(dy, wT, "conv2d_dgrad wT");
+  same_type(dy, dx, "conv2d_dgrad dx");
+  same_type(dy, res, "conv2d_dgrad res");
+  same_type(dy, mask, "conv2d_dgrad mask");
+  same_type(dy, z, "conv2d_dgrad z");
+  same_type(dy, z2, "conv2d_dgrad z2");
   a.x = ptr<uint16_t>(dy);
   a.H = P; a.W = Q; a.C = K; a.ldx = lddy; a.xoff = dyoff;
   a.w = ptr<uint16_t>(wT);
@@ -331,6 +376,7 @@ c10::optional<at::Tensor> conv2d_dgrad_pro(const at::Tensor& dy, int N, int P, i
   set_prologue(a, pro, pk0, pk1, pz, ldpz, pzoff);
   int bm, bn;
   pick_tiles((int64_t)N * H * W / (stride * stride), C, (int64_t)R * S * K / (stride * stride), K, bm, bn, pro != 0);
+  if (a.f32) f32_tiles(bm, bn);
   a.ntiles = ceil_div(C, bn);
   a.nphase = stride * stride;
   int tiles = 0;
@@ -346,7 +392,7 @@ c10::optional<at::Tensor> conv2d_dgrad_pro(const at::Tensor& dy, int N, int P, i
       p.dw0 = (pw + pad - s0) / stride; p.dws = -1;
       p.wr0 = r0; p.wrs = stride; p.ws0 = s0; p.wss = stride;
       p.oh0 = ph; p.ow0 = pw;
-      finish_phase(p, N, K, bm);
+      finish_phase(p, N, K, bm, a.f32);
       p.tile_base = tiles;
       tiles += p.mtiles;
     }
@@ -381,6 +427,9 @@ void convT2x2_fwd(const at::Tensor& x, int N, int H, int W, int Cin, int ldx, in
                   at::Tensor y, int ldy, int yoff, const c10::optional<at::Tensor>& bias) {
   require_gpu(x, "x");
   ConvArgs a{};
+  a.f32 = act_f32(x, "convT2x2_fwd");
+  same_type(x, wf, "convT2x2_fwd w");
+  same_type(x, y, "convT2x2_fwd y");
   a.x = ptr<uint16_t>(x);
   a.H = H; a.W = W; a.C = Cin; a.ldx = ldx; a.xoff = xoff;
   a.w = ptr<uint16_t>(wf);
@@ -394,6 +443,7 @@ void convT2x2_fwd(const at::Tensor& x, int N, int H, int W, int Cin, int ldx, in
   set_kstep(a, Cin);
   int bm, bn;
   pick_tiles((int64_t)N * H * W, Cout, Cin, Cin, bm, bn);
+  if (a.f32) f32_tiles(bm, bn);
   a.ntiles = ceil_div(Cout, bn);
   a.nphase = 4;
   for (int i = 0; i < 2; ++i)
@@ -403,7 +453,7 @@ void convT2x2_fwd(const at::Tensor& x, int N, int H, int W, int Cin, int ldx, in
       p.dh0 = 0; p.dhs = 0; p.dw0 = 0; p.dws = 0;
       p.wr0 = i; p.wrs = 0; p.ws0 = j; p.wss = 0;
       p.oh0 = i; p.ow0 = j;
-      finish_phase(p, N, Cin, bm);
+      finish_phase(p, N, Cin, bm, a.f32);
     }
   check(dlmpi_conv_igemm(&a, bm, bn, cur_stream()), "convT2x2_fwd");
 }
@@ -420,6 +470,9 @@ void conv2d_wgrad_pro(const at::Tensor& dy, int lddy, int dyoff, int Ko, const a
   require_gpu(dy, "dy");
   if (C % 8 != 0 || Ko % 8 != 0) throw std::runtime_error("conv2d_wgrad: channels must be multiples of 8");
   WgradArgs a{};
+  a.f32 = act_f32(dy, "conv2d_wgrad");
+  same_type(dy, x, "conv2d_wgrad x");
+  if (a.f32 && (pro_a || pro_b)) throw std::runtime_error("conv2d_wgrad: operand prologues are bf16 only");
   a.pro_a = pro_a;
   a.pro_b = pro_b;
   if (pro_a) {
@@ -445,9 +498,9 @@ void conv2d_wgrad_pro(const at::Tensor& dy, int lddy, int dyoff, int Ko, const a
   a.TC = R * S * C;
   a.npix = N * P * Q;
   a.direct = (R == 1 && S == 1 && stride == 1 && pad == 0 && P == H && Q == W) ? 1 : 0;
-  const int bm = Ko <= 64 ? 64 : 128;
+  const int bm = a.f32 || Ko <= 64 ? 64 : 128;   // fp32: conv_wgrad_f32_kernel's 64 x 64 tile
   a.mtiles = ceil_div(Ko, bm);
-  const int bn = 128;
+  const int bn = a.f32 ? 64 : 128;
   a.ntiles = ceil_div(a.TC, bn);
   const int tiles = a.mtiles * a.ntiles;
   // split the pixel reduction so the grid covers the chip ~2 blocks deep, but keep each split at
@@ -481,7 +534,7 @@ void conv2d_wgrad_pro(const at::Tensor& dy, int lddy, int dyoff, int Ko, const a
     const char* e = getenv("DLMPI_WGRAD_INLAUNCH");
     return e ? atoi(e) : 8;
   }();
-  if (splits <= inlaunch_max) {
+  if (splits <= inlaunch_max && !a.f32) {
     hipStream_t st = cur_stream();
     const int tiles_n = a.mtiles * a.ntiles;
     float* slab = splits > 1 ? dlmpi_splitk_slab(st, (size_t)tiles_n * splits * bm * bn) : nullptr;
@@ -535,15 +588,19 @@ void bn_finalize(const at::Tensor& partial, int ntiles, int C, double count, con
 int reduce_blocks(int64_t M, int C) { return dlmpi_reduce_blocks(M, C); }
 
 void bn_stats(const at::Tensor& x, int64_t M, int C, int ldx, int xoff, at::Tensor partial, int nblk) {
-  check(dlmpi_bn_stats(ptr<uint16_t>(x), M, C, ldx, xoff, ptr<float>(partial), nblk, cur_stream()), "bn_stats");
+  check(dlmpi_bn_stats(x.data_ptr(), M, C, ldx, xoff, ptr<float>(partial), nblk, act_f32(x, "bn_stats"), cur_stream()),
+        "bn_stats");
 }
 
 void bn_apply(const at::Tensor& x, int ldx, int xoff, int64_t M, int C, const at::Tensor& scale,
               const at::Tensor& shift, const c10::optional<at::Tensor>& res, int ldres, int resoff, bool relu,
               at::Tensor y, int ldy, int yoff, const c10::optional<at::Tensor>& mbits) {
   if (mbits && mbits->numel() != M * (C / 8)) throw std::runtime_error("bn_apply: mask bits must be [M][C/8]");
-  check(dlmpi_bn_apply(ptr<uint16_t>(x), ldx, xoff, M, C, ptr<float>(scale), ptr<float>(shift), optr<uint16_t>(res),
-                       ldres, resoff, relu ? 1 : 0, ptr<uint16_t>(y), ldy, yoff, optr<uint8_t>(mbits), cur_stream()),
+  same_type(x, y, "bn_apply y");
+  same_type(x, res, "bn_apply res");
+  check(dlmpi_bn_apply(x.data_ptr(), ldx, xoff, M, C, ptr<float>(scale), ptr<float>(shift), optr<uint16_t>(res), ldres,
+                       resoff, relu ? 1 : 0, y.data_ptr(), ldy, yoff, optr<uint8_t>(mbits), act_f32(x, "bn_apply"),
+                       cur_stream()),
         "bn_apply");
 }
 
@@ -551,9 +608,11 @@ void bn_bwd_reduce(const at::Tensor& dy, int lddy, int dyoff, const c10::optiona
                    int ymoff, const c10::optional<at::Tensor>& x, int ldx, int xoff, int64_t M, int C,
                    const c10::optional<at::Tensor>& mean, const c10::optional<at::Tensor>& invstd, at::Tensor partial,
                    int nblk) {
-  check(dlmpi_bn_bwd_reduce(ptr<uint16_t>(dy), lddy, dyoff, optr<uint16_t>(ymask), ldym, ymoff, optr<uint16_t>(x), ldx,
+  same_type(dy, ymask, "bn_bwd_reduce ymask");
+  same_type(dy, x, "bn_bwd_reduce x");
+  check(dlmpi_bn_bwd_reduce(dy.data_ptr(), lddy, dyoff, optr<uint16_t>(ymask), ldym, ymoff, optr<uint16_t>(x), ldx,
                             xoff, M, C, optr<float>(mean), optr<float>(invstd), ptr<float>(partial), nblk,
-                            cur_stream()),
+                            act_f32(dy, "bn_bwd_reduce"), cur_stream()),
         "bn_bwd_reduce");
 }
 
@@ -585,8 +644,13 @@ void bn_bwd_finalize_fused(const at::Tensor& partial, int k2, int C, double coun
 void bn_bwd_apply(const at::Tensor& dy, int lddy, int dyoff, const c10::optional<at::Tensor>& ymask, int ldym,
                   int ymoff, const at::Tensor& x, int ldx, int xoff, int64_t M, int C, const at::Tensor& coef,
                   at::Tensor dx, const c10::optional<at::Tensor>& dyr_out) {
-  check(dlmpi_bn_bwd_apply(ptr<uint16_t>(dy), lddy, dyoff, optr<uint16_t>(ymask), ldym, ymoff, ptr<uint16_t>(x), ldx,
-                           xoff, M, C, ptr<float>(coef), ptr<uint16_t>(dx), optr<uint16_t>(dyr_out), cur_stream()),
+  same_type(dy, ymask, "bn_bwd_apply ymask");
+  same_type(dy, x, "bn_bwd_apply x");
+  same_type(dy, dx, "bn_bwd_apply dx");
+  same_type(dy, dyr_out, "bn_bwd_apply dyr_out");
+  check(dlmpi_bn_bwd_apply(dy.data_ptr(), lddy, dyoff, optr<uint16_t>(ymask), ldym, ymoff, x.data_ptr(), ldx, xoff, M,
+                           C, ptr<float>(coef), dx.data_ptr(), optr<uint16_t>(dyr_out), act_f32(dy, "bn_bwd_apply"),
+                           cur_stream()),
         "bn_bwd_apply");
 }
 
@@ -594,8 +658,8 @@ void channel_sum(const at::Tensor& x, int64_t M, int C, int ldx, int xoff, at::T
   const int nblk = dlmpi_reduce_blocks(M, C);
   at::Tensor partial = at::empty({(int64_t)nblk * 2 * C}, x.options().dtype(at::kFloat));
   at::Tensor ws = colsum_ws(partial, nblk, C);
-  check(dlmpi_channel_sum(ptr<uint16_t>(x), M, C, ldx, xoff, ptr<float>(out_acc), ptr<float>(partial), nblk,
-                          ptr<double>(ws), cur_stream()),
+  check(dlmpi_channel_sum(x.data_ptr(), M, C, ldx, xoff, ptr<float>(out_acc), ptr<float>(partial), nblk,
+                          ptr<double>(ws), act_f32(x, "channel_sum"), cur_stream()),
         "channel_sum");
 }
 
@@ -603,15 +667,18 @@ void channel_sum(const at::Tensor& x, int64_t M, int C, int ldx, int xoff, at::T
 void maxpool_fwd(const at::Tensor& x, int N, int H, int W, int C, int ldx, int xoff, int k, int stride, int pad,
                  at::Tensor y, at::Tensor idx, int OH, int OW, const c10::optional<at::Tensor>& scale,
                  const c10::optional<at::Tensor>& shift) {
-  check(dlmpi_maxpool_fwd(ptr<uint16_t>(x), N, H, W, C, ldx, xoff, k, stride, pad, ptr<uint16_t>(y),
-                          ptr<uint8_t>(idx), OH, OW, optr<float>(scale), optr<float>(shift), cur_stream()),
+  same_type(x, y, "maxpool_fwd y");
+  check(dlmpi_maxpool_fwd(x.data_ptr(), N, H, W, C, ldx, xoff, k, stride, pad, y.data_ptr(), ptr<uint8_t>(idx), OH, OW,
+                          optr<float>(scale), optr<float>(shift), act_f32(x, "maxpool_fwd"), cur_stream()),
         "maxpool_fwd");
 }
 void maxpool_bwd(const at::Tensor& dy, const at::Tensor& idx, int N, int H, int W, int C, int k, int stride, int pad,
                  int OH, int OW, const c10::optional<at::Tensor>& add, int ldadd, int addoff, at::Tensor dx, int lddx,
                  int dxoff) {
-  check(dlmpi_maxpool_bwd(ptr<uint16_t>(dy), ptr<uint8_t>(idx), N, H, W, C, k, stride, pad, OH, OW,
-                          optr<uint16_t>(add), ldadd, addoff, ptr<uint16_t>(dx), lddx, dxoff, cur_stream()),
+  same_type(dy, add, "maxpool_bwd add");
+  same_type(dy, dx, "maxpool_bwd dx");
+  check(dlmpi_maxpool_bwd(dy.data_ptr(), ptr<uint8_t>(idx), N, H, W, C, k, stride, pad, OH, OW, optr<uint16_t>(add),
+                          ldadd, addoff, dx.data_ptr(), lddx, dxoff, act_f32(dy, "maxpool_bwd"), cur_stream()),
         "maxpool_bwd");
 }
 // data gradient of a 1x1 convolution with one output channel (UNet head) fused with the BN backward of
@@ -622,8 +689,11 @@ at::Tensor outer_dgrad_bn(const at::Tensor& dy, int lddy, int64_t M, int C, cons
   const int64_t rpb = 256 / (C / 8);
   const int nblk = (int)std::max<int64_t>(1, std::min<int64_t>(4096, (M + rpb * 8 - 1) / (rpb * 8)));
   at::Tensor part = at::empty({nblk, 2, C}, dy.options().dtype(at::kFloat));
-  check(dlmpi_outer_dgrad_bn(ptr<uint16_t>(dy), lddy, M, C, ptr<uint16_t>(w), ldw, ptr<uint16_t>(z),
-                             ptr<float>(mscale), ptr<float>(mshift), ptr<uint16_t>(dx), ptr<float>(part), nblk,
+  same_type(dy, w, "outer_dgrad_bn w");
+  same_type(dy, z, "outer_dgrad_bn z");
+  same_type(dy, dx, "outer_dgrad_bn dx");
+  check(dlmpi_outer_dgrad_bn(dy.data_ptr(), lddy, M, C, w.data_ptr(), ldw, z.data_ptr(), ptr<float>(mscale),
+                             ptr<float>(mshift), dx.data_ptr(), ptr<float>(part), nblk, act_f32(dy, "outer_dgrad_bn"),
                              cur_stream()),
         "outer_dgrad_bn");
   return part;
@@ -638,41 +708,51 @@ at::Tensor maxpool_bwd_bn(const at::Tensor& dy, const at::Tensor& idx, int N, in
   const int64_t rpb = 256 / (C / 8);
   const int nblk = (int)std::max<int64_t>(1, std::min<int64_t>(4096, ((int64_t)N * H * W + rpb * 8 - 1) / (rpb * 8)));
   at::Tensor part = at::empty({nblk, 2, C}, dy.options().dtype(at::kFloat));
-  check(dlmpi_maxpool_bwd_bn(ptr<uint16_t>(dy), ptr<uint8_t>(idx), N, H, W, C, k, stride, pad, OH, OW,
-                             ptr<uint16_t>(z), ptr<float>(mscale), ptr<float>(mshift), optr<uint16_t>(add), ldadd,
-                             addoff, ptr<uint16_t>(dx), ptr<float>(part),
-                             nblk, cur_stream()),
+  same_type(dy, z, "maxpool_bwd_bn z");
+  same_type(dy, add, "maxpool_bwd_bn add");
+  same_type(dy, dx, "maxpool_bwd_bn dx");
+  check(dlmpi_maxpool_bwd_bn(dy.data_ptr(), ptr<uint8_t>(idx), N, H, W, C, k, stride, pad, OH, OW, z.data_ptr(),
+                             ptr<float>(mscale), ptr<float>(mshift), optr<uint16_t>(add), ldadd, addoff, dx.data_ptr(),
+                             ptr<float>(part), nblk, act_f32(dy, "maxpool_bwd_bn"), cur_stream()),
         "maxpool_bwd_bn");
   return part;
 }
 void avgpool_fwd(const at::Tensor& x, int N, int HW, int C, at::Tensor y) {
-  check(dlmpi_avgpool_fwd(ptr<uint16_t>(x), N, HW, C, ptr<uint16_t>(y), cur_stream()), "avgpool_fwd");
+  same_type(x, y, "avgpool_fwd y");
+  check(dlmpi_avgpool_fwd(x.data_ptr(), N, HW, C, y.data_ptr(), act_f32(x, "avgpool_fwd"), cur_stream()), "avgpool_fwd");
 }
 void avgpool_bwd(const at::Tensor& dy, int N, int HW, int C, at::Tensor dx) {
-  check(dlmpi_avgpool_bwd(ptr<uint16_t>(dy), N, HW, C, ptr<uint16_t>(dx), cur_stream()), "avgpool_bwd");
+  same_type(dy, dx, "avgpool_bwd dx");
+  check(dlmpi_avgpool_bwd(dy.data_ptr(), N, HW, C, dx.data_ptr(), act_f32(dy, "avgpool_bwd"), cur_stream()),
+        "avgpool_bwd");
 }
 void nchw_to_nhwc(const at::Tensor& x, int N, int C, int H, int W, int Cpad, at::Tensor y) {
-  check(dlmpi_nchw_to_nhwc(ptr<float>(x), N, C, H, W, Cpad, ptr<uint16_t>(y), cur_stream()), "nchw_to_nhwc");
+  check(dlmpi_nchw_to_nhwc(ptr<float>(x), N, C, H, W, Cpad, y.data_ptr(), act_f32(y, "nchw_to_nhwc"), cur_stream()),
+        "nchw_to_nhwc");
 }
 void s2d_nchw(const at::Tensor& x, int N, int C, int H, int W, int pad, int U, int V, int CS, at::Tensor y) {
-  check(dlmpi_s2d_nchw(ptr<float>(x), N, C, H, W, pad, U, V, CS, ptr<uint16_t>(y), cur_stream()), "s2d_nchw");
+  check(dlmpi_s2d_nchw(ptr<float>(x), N, C, H, W, pad, U, V, CS, y.data_ptr(), act_f32(y, "s2d_nchw"), cur_stream()),
+        "s2d_nchw");
 }
 void upsample2x_fwd(const at::Tensor& x, int N, int H, int W, int C, int ldx, int xoff, at::Tensor y, int ldy,
                     int yoff) {
-  check(dlmpi_upsample2x_fwd(ptr<uint16_t>(x), N, H, W, C, ldx, xoff, ptr<uint16_t>(y), ldy, yoff, cur_stream()),
+  same_type(x, y, "upsample2x_fwd y");
+  check(dlmpi_upsample2x_fwd(x.data_ptr(), N, H, W, C, ldx, xoff, y.data_ptr(), ldy, yoff, act_f32(x, "upsample2x_fwd"),
+                             cur_stream()),
         "upsample2x_fwd");
 }
 void upsample2x_bwd(const at::Tensor& dy, int N, int H, int W, int C, int lddy, int dyoff, at::Tensor dx) {
-  at::Tensor ws = at::empty({(int64_t)N * H * W * C}, dy.options().dtype(at::kFloat));
-  check(dlmpi_upsample2x_bwd(ptr<uint16_t>(dy), N, H, W, C, lddy, dyoff, ptr<float>(ws), ptr<uint16_t>(dx),
+  same_type(dy, dx, "upsample2x_bwd dx");
+  check(dlmpi_upsample2x_bwd(dy.data_ptr(), N, H, W, C, lddy, dyoff, dx.data_ptr(), act_f32(dy, "upsample2x_bwd"),
                              cur_stream()),
         "upsample2x_bwd");
 }
 
 // entries: int64 tensor [n][16] on the host: src_ptr, dst_ptr, d0..d3, v0..v3, s0..s3, start
-void cast_weights(const at::Tensor& entries_dev, const at::Tensor& block_map_dev) {
+// f32: the destinations are fp32 compute copies (fp32 precision path), else bf16
+void cast_weights(const at::Tensor& entries_dev, const at::Tensor& block_map_dev, bool f32) {
   check(dlmpi_cast_weights(reinterpret_cast<const CastEntry*>(entries_dev.data_ptr()), block_map_dev.data_ptr(),
-                           (int)(block_map_dev.numel() / 4), cur_stream()),
+                           (int)(block_map_dev.numel() / 4), f32 ? 1 : 0, cur_stream()),
         "cast_weights");
 }
 
@@ -739,6 +819,25 @@ void scale_(at::Tensor x, const at::Tensor& coef) {
   check(dlmpi_scale_f32(ptr<float>(x), x.numel(), ptr<float>(coef), cur_stream()), "scale");
 }
 
+// --------------------------------- utilities -----------------------------------------------
+void fill_(at::Tensor t, double v) {
+  if (t.scalar_type() != at::kFloat || !t.is_contiguous()) throw std::runtime_error("fill_: contiguous fp32 tensor");
+  check(dlmpi_fill_f32(ptr<float>(t), t.numel(), (float)v, cur_stream()), "fill");
+}
+void add_i64_(at::Tensor t, int64_t v) {
+  if (t.scalar_type() != at::kLong || !t.is_contiguous()) throw std::runtime_error("add_i64_: contiguous int64 tensor");
+  check(dlmpi_add_i64(ptr<int64_t>(t), t.numel(), v, cur_stream()), "add_i64");
+}
+// dst.view(-1)[i] (+)= src.view(-1)[idx[i]]  (idx < 0: 0), every i < idx.numel()
+void gather_(at::Tensor dst, const at::Tensor& src, const at::Tensor& idx, bool accumulate) {
+  if (dst.scalar_type() != src.scalar_type() || !dst.is_contiguous() || !src.is_contiguous() ||
+      idx.scalar_type() != at::kLong || !idx.is_contiguous() || idx.numel() > dst.numel())
+    throw std::runtime_error("gather_: contiguous dst/src of one dtype, int64 idx no longer than dst");
+  check(dlmpi_gather(dst.data_ptr(), src.data_ptr(), ptr<int64_t>(idx), idx.numel(), (int)dst.element_size(),
+                     accumulate ? 1 : 0, cur_stream()),
+        "gather");
+}
+
 // --------------------------------- device-resident input pipeline ---------------------------
 void image_batch(const at::Tensor& data, const at::Tensor& labels, const at::Tensor& idx, int H, int W, int C,
                  int pad, bool augment, int64_t seed, int64_t epoch, std::vector<double> mean, std::vector<double> sd,
@@ -803,6 +902,9 @@ void register_ops(pybind11::module& m) {
   m.def("adam_step", &adam_step);
   m.def("grad_norm", &grad_norm);
   m.def("scale_", &scale_);
+  m.def("fill_", &fill_);
+  m.def("add_i64_", &add_i64_);
+  m.def("gather_", &gather_);
   m.attr("CAST_ENTRY_BYTES") = (int)sizeof(CastEntry);
 }
 

@@ -62,15 +62,15 @@ __device__ void block_combine(float (*acc)[8], const RowMap& rm, int C, float* p
 // stem's 3x3/s2, 1 for the UNet's 2x2/s2); the candidate loop is unrolled with predication so all
 // window loads (index + gradient) are in flight at once instead of one dependent round trip per
 // window.  Same summation order as the generic loop (oh, then ow, ascending) -> identical results.
-template <int NWIN>
-__global__ __launch_bounds__(256) void maxpool_bwd_bn_kernel(const uint16_t* __restrict__ dy,
+template <int NWIN, typename T>
+__global__ __launch_bounds__(256) void maxpool_bwd_bn_kernel(const T* __restrict__ dy,
                                                              const uint8_t* __restrict__ idx, int N, int H, int W,
                                                              int C, int k, int stride, int pad, int OH, int OW,
-                                                             FastDiv fdW, FastDiv fdH, const uint16_t* __restrict__ z,
+                                                             FastDiv fdW, FastDiv fdH, const T* __restrict__ z,
                                                              const float* __restrict__ msc,
                                                              const float* __restrict__ msh,
-                                                             const uint16_t* __restrict__ add, int ldadd, int addoff,
-                                                             uint16_t* __restrict__ dx, float* __restrict__ partial) {
+                                                             const T* __restrict__ add, int ldadd, int addoff,
+                                                             T* __restrict__ dx, float* __restrict__ partial) {
   const RowMap rm = rowmap(C);
   float acc[2][8] = {};
   const int64_t M = (int64_t)N * H * W;
@@ -94,7 +94,7 @@ __global__ __launch_bounds__(256) void maxpool_bwd_bn_kernel(const uint16_t* __r
       const int ow_hi = min((iw + pad) / stride, OW - 1);
       if constexpr (NWIN > 0) {
         uint64_t id[NWIN * NWIN];
-        u32x4 dv[NWIN * NWIN];
+        typename Vec8<T>::type dv[NWIN * NWIN];
 #pragma unroll
         for (int a = 0; a < NWIN; ++a)
 #pragma unroll
@@ -102,7 +102,7 @@ __global__ __launch_bounds__(256) void maxpool_bwd_bn_kernel(const uint16_t* __r
             const bool ok = oh_lo + a <= oh_hi && ow_lo + b <= ow_hi;
             const int64_t op = ok ? ((int64_t)n * OH + oh_lo + a) * OW + ow_lo + b : 0;   // 0: a valid address
             id[a * NWIN + b] = *reinterpret_cast<const uint64_t*>(idx + op * C + c0);
-            dv[a * NWIN + b] = *reinterpret_cast<const u32x4*>(dy + op * C + c0);
+            dv[a * NWIN + b] = raw8(dy + op * C + c0);
           }
 #pragma unroll
         for (int a = 0; a < NWIN; ++a)
@@ -123,7 +123,7 @@ __global__ __launch_bounds__(256) void maxpool_bwd_bn_kernel(const uint16_t* __r
             const int64_t op = ((int64_t)n * OH + oh) * OW + ow;
             const uint64_t id = *reinterpret_cast<const uint64_t*>(idx + op * C + c0);
             float d[8];
-            unpack8(*reinterpret_cast<const u32x4*>(dy + op * C + c0), d);
+            load8(dy + op * C + c0, d);
 #pragma unroll
             for (int e = 0; e < 8; ++e)
               if (((id >> (8 * e)) & 0xff) == want) g[e] += d[e];
@@ -132,20 +132,21 @@ __global__ __launch_bounds__(256) void maxpool_bwd_bn_kernel(const uint16_t* __r
       }
       if (add) {   // second gradient source of the pool input (UNet: its skip-concat slice)
         float a2[8];
-        unpack8(*reinterpret_cast<const u32x4*>(add + row * ldadd + addoff + c0), a2);
+        load8(add + row * ldadd + addoff + c0, a2);
 #pragma unroll
         for (int e = 0; e < 8; ++e) g[e] += a2[e];
       }
       float zz[8];
-      unpack8(*reinterpret_cast<const u32x4*>(z + row * C + c0), zz);
+      load8(z + row * C + c0, zz);
 #pragma unroll
       for (int e = 0; e < 8; ++e) g[e] = zz[e] * sc[e] + sh[e] > 0.f ? g[e] : 0.f;
-      const u32x4 pk = pack8(g);
-      *reinterpret_cast<u32x4*>(dx + row * C + c0) = pk;
-      float r[8];
-      unpack8(pk, r);   // statistics of the stored (bf16) gradient
+      store8(dx + row * C + c0, g);
 #pragma unroll
-      for (int e = 0; e < 8; ++e) { acc[0][e] += r[e]; acc[1][e] += r[e] * zz[e]; }
+      for (int e = 0; e < 8; ++e) {   // statistics of the stored gradient
+        const float r = stored<T>(g[e]);
+        acc[0][e] += r;
+        acc[1][e] += r * zz[e];
+      }
     }
   }
   block_combine<2>(acc, rm, C, partial);
@@ -156,12 +157,13 @@ __global__ __launch_bounds__(256) void maxpool_bwd_bn_kernel(const uint16_t* __r
 // outer product, so a streaming kernel instead of a GEMM tile with 63 of 64 reduction lanes zero
 // -- masked by [z*scale + shift > 0], stored, and the BN-backward partials {sum dx, sum dx*z} per
 // block.  The bf16 x bf16 product is exact in fp32, as in the GEMM path: identical dx.
-__global__ __launch_bounds__(256) void outer_dgrad_bn_kernel(const uint16_t* __restrict__ dy, int lddy, int64_t M,
-                                                             int C, const uint16_t* __restrict__ w, int ldw,
-                                                             const uint16_t* __restrict__ z,
+template <typename T>
+__global__ __launch_bounds__(256) void outer_dgrad_bn_kernel(const T* __restrict__ dy, int lddy, int64_t M,
+                                                             int C, const T* __restrict__ w, int ldw,
+                                                             const T* __restrict__ z,
                                                              const float* __restrict__ msc,
                                                              const float* __restrict__ msh,
-                                                             uint16_t* __restrict__ dx, float* __restrict__ partial) {
+                                                             T* __restrict__ dx, float* __restrict__ partial) {
   const RowMap rm = rowmap(C);
   float acc[2][8] = {};
   if (rm.active) {
@@ -169,35 +171,37 @@ __global__ __launch_bounds__(256) void outer_dgrad_bn_kernel(const uint16_t* __r
     float wv[8], sc[8], sh[8];
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
-      wv[e] = bf2f(w[(int64_t)(c0 + e) * ldw]);
+      wv[e] = load1(w + (int64_t)(c0 + e) * ldw);
       sc[e] = msc[c0 + e];
       sh[e] = msh[c0 + e];
     }
     for (int64_t row = (int64_t)blockIdx.x * rm.RPB + rm.rr; row < M; row += (int64_t)gridDim.x * rm.RPB) {
-      const float d = bf2f(dy[row * lddy]);
+      const float d = load1(dy + row * lddy);
       float zz[8], g[8];
-      unpack8(*reinterpret_cast<const u32x4*>(z + row * C + c0), zz);
+      load8(z + row * C + c0, zz);
 #pragma unroll
       for (int e = 0; e < 8; ++e) g[e] = zz[e] * sc[e] + sh[e] > 0.f ? d * wv[e] : 0.f;
-      const u32x4 pk = pack8(g);
-      *reinterpret_cast<u32x4*>(dx + row * C + c0) = pk;
-      float r[8];
-      unpack8(pk, r);
+      store8(dx + row * C + c0, g);
 #pragma unroll
-      for (int e = 0; e < 8; ++e) { acc[0][e] += r[e]; acc[1][e] += r[e] * zz[e]; }
+      for (int e = 0; e < 8; ++e) {
+        const float r = stored<T>(g[e]);
+        acc[0][e] += r;
+        acc[1][e] += r * zz[e];
+      }
     }
   }
   block_combine<2>(acc, rm, C, partial);
 }
 
-__global__ __launch_bounds__(256) void bn_stats_kernel(const uint16_t* __restrict__ x, int64_t M, int C, int ldx,
+template <typename T>
+__global__ __launch_bounds__(256) void bn_stats_kernel(const T* __restrict__ x, int64_t M, int C, int ldx,
                                                        int xoff, float* __restrict__ partial) {
   const RowMap rm = rowmap(C);
   float acc[2][8] = {};
   if (rm.active) {
     for (int64_t row = (int64_t)blockIdx.x * rm.RPB + rm.rr; row < M; row += (int64_t)gridDim.x * rm.RPB) {
       float v[8];
-      unpack8(*reinterpret_cast<const u32x4*>(x + row * ldx + xoff + rm.cc * 8), v);
+      load8(x + row * ldx + xoff + rm.cc * 8, v);
 #pragma unroll
       for (int e = 0; e < 8; ++e) { acc[0][e] += v[e]; acc[1][e] += v[e] * v[e]; }
     }
@@ -421,11 +425,12 @@ __global__ __launch_bounds__(256) void colsum_fin_kernel(const float* __restrict
   }
 }
 
-__global__ __launch_bounds__(256) void bn_apply_kernel(const uint16_t* __restrict__ x, int ldx, int xoff, int64_t M,
+template <typename T>
+__global__ __launch_bounds__(256) void bn_apply_kernel(const T* __restrict__ x, int ldx, int xoff, int64_t M,
                                                        int C, FastDiv fdCC, const float* __restrict__ scale,
                                                        const float* __restrict__ shift,
-                                                       const uint16_t* __restrict__ res, int ldres, int resoff,
-                                                       int relu, uint16_t* __restrict__ y, int ldy, int yoff,
+                                                       const T* __restrict__ res, int ldres, int resoff,
+                                                       int relu, T* __restrict__ y, int ldy, int yoff,
                                                        uint8_t* __restrict__ mbits) {
   const int CC = C >> 3;
   const int64_t total = M * CC;
@@ -441,7 +446,7 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const uint16_t* __restric
     }
     const int c0 = cc * 8;
     float v[8];
-    unpack8(*reinterpret_cast<const u32x4*>(x + row * ldx + xoff + c0), v);
+    load8(x + row * ldx + xoff + c0, v);
     const f32x4 s0 = *reinterpret_cast<const f32x4*>(scale + c0), s1 = *reinterpret_cast<const f32x4*>(scale + c0 + 4);
     const f32x4 h0 = *reinterpret_cast<const f32x4*>(shift + c0), h1 = *reinterpret_cast<const f32x4*>(shift + c0 + 4);
 #pragma unroll
@@ -452,7 +457,7 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const uint16_t* __restric
     }
     if (res) {
       float r[8];
-      unpack8(*reinterpret_cast<const u32x4*>(res + row * ldres + resoff + c0), r);
+      load8(res + row * ldres + resoff + c0, r);
 #pragma unroll
       for (int e = 0; e < 8; ++e) v[e] += r[e];
     }
@@ -460,24 +465,35 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const uint16_t* __restric
 #pragma unroll
       for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.f);
     }
-    const u32x4 pk = pack8(v);
-    *reinterpret_cast<u32x4*>(y + row * ldy + yoff + c0) = pk;
-    if (mbits) {   // ReLU mask bits of the stored bf16 values (bit e: y[c0 + e] > 0), 1/16 of y's bytes
-      uint32_t b = 0;
+    if constexpr (sizeof(T) == 2) {
+      const u32x4 pk = pack8(v);
+      *reinterpret_cast<u32x4*>(y + row * ldy + yoff + c0) = pk;
+      if (mbits) {   // ReLU mask bits of the stored bf16 values (bit e: y[c0 + e] > 0), 1/16 of y's bytes
+        uint32_t b = 0;
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        b |= (uint32_t)((pk[k] & 0xffffu) != 0u && !(pk[k] & 0x8000u)) << (2 * k);
-        b |= (uint32_t)((pk[k] >> 16) != 0u && !(pk[k] & 0x80000000u)) << (2 * k + 1);
+        for (int k = 0; k < 4; ++k) {
+          b |= (uint32_t)((pk[k] & 0xffffu) != 0u && !(pk[k] & 0x8000u)) << (2 * k);
+          b |= (uint32_t)((pk[k] >> 16) != 0u && !(pk[k] & 0x80000000u)) << (2 * k + 1);
+        }
+        mbits[row * CC + cc] = (uint8_t)b;
       }
-      mbits[row * CC + cc] = (uint8_t)b;
+    } else {
+      store8(y + row * ldy + yoff + c0, v);
+      if (mbits) {
+        uint32_t b = 0;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) b |= (uint32_t)(v[e] > 0.f) << e;
+        mbits[row * CC + cc] = (uint8_t)b;
+      }
     }
   }
 }
 
 // partial[blk][0][C] = sum dyr, partial[blk][1][C] = sum dyr * xhat  (x == null: only the first)
-__global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const uint16_t* __restrict__ dy, int lddy, int dyoff,
-                                                            const uint16_t* __restrict__ ym, int ldym, int ymoff,
-                                                            const uint16_t* __restrict__ x, int ldx, int xoff,
+template <typename T>
+__global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const T* __restrict__ dy, int lddy, int dyoff,
+                                                            const T* __restrict__ ym, int ldym, int ymoff,
+                                                            const T* __restrict__ x, int ldx, int xoff,
                                                             int64_t M, int C, const float* __restrict__ mean,
                                                             const float* __restrict__ invstd,
                                                             float* __restrict__ partial) {
@@ -493,11 +509,10 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const uint16_t* __re
     }
     for (int64_t row = (int64_t)blockIdx.x * rm.RPB + rm.rr; row < M; row += (int64_t)gridDim.x * rm.RPB) {
       float g[8];
-      unpack8(*reinterpret_cast<const u32x4*>(dy + row * lddy + dyoff + c0), g);
+      load8(dy + row * lddy + dyoff + c0, g);
       if (ym) {
-        const u32x4 mv = *reinterpret_cast<const u32x4*>(ym + row * ldym + ymoff + c0);
         float m[8];
-        unpack8(mv, m);
+        load8(ym + row * ldym + ymoff + c0, m);
 #pragma unroll
         for (int e = 0; e < 8; ++e) g[e] = m[e] > 0.f ? g[e] : 0.f;
       }
@@ -505,7 +520,7 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const uint16_t* __re
       for (int e = 0; e < 8; ++e) acc[0][e] += g[e];
       if (x) {
         float xv[8];
-        unpack8(*reinterpret_cast<const u32x4*>(x + row * ldx + xoff + c0), xv);
+        load8(x + row * ldx + xoff + c0, xv);
 #pragma unroll
         for (int e = 0; e < 8; ++e) acc[1][e] += g[e] * (xv[e] - mu[e]) * is[e];
       }
@@ -514,12 +529,13 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const uint16_t* __re
   block_combine<2>(acc, rm, C, partial);
 }
 
-__global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const uint16_t* __restrict__ dy, int lddy, int dyoff,
-                                                           const uint16_t* __restrict__ ym, int ldym, int ymoff,
-                                                           const uint16_t* __restrict__ x, int ldx, int xoff,
+template <typename T>
+__global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const T* __restrict__ dy, int lddy, int dyoff,
+                                                           const T* __restrict__ ym, int ldym, int ymoff,
+                                                           const T* __restrict__ x, int ldx, int xoff,
                                                            int64_t M, int C, FastDiv fdCC,
-                                                           const float* __restrict__ coef, uint16_t* __restrict__ dx,
-                                                           uint16_t* __restrict__ dyr_out) {
+                                                           const float* __restrict__ coef, T* __restrict__ dx,
+                                                           T* __restrict__ dyr_out) {
   const int CC = C >> 3;
   const int64_t total = M * CC;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
@@ -534,20 +550,20 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const uint16_t* __res
     }
     const int c0 = cc * 8;
     float g[8], xv[8];
-    unpack8(*reinterpret_cast<const u32x4*>(dy + row * lddy + dyoff + c0), g);
+    load8(dy + row * lddy + dyoff + c0, g);
     if (ym) {
       float m[8];
-      unpack8(*reinterpret_cast<const u32x4*>(ym + row * ldym + ymoff + c0), m);
+      load8(ym + row * ldym + ymoff + c0, m);
 #pragma unroll
       for (int e = 0; e < 8; ++e) g[e] = m[e] > 0.f ? g[e] : 0.f;
     }
-    if (dyr_out) *reinterpret_cast<u32x4*>(dyr_out + row * C + c0) = pack8(g);
-    unpack8(*reinterpret_cast<const u32x4*>(x + row * ldx + xoff + c0), xv);
+    if (dyr_out) store8(dyr_out + row * C + c0, g);
+    load8(x + row * ldx + xoff + c0, xv);
     float o[8];
 #pragma unroll
     for (int e = 0; e < 8; ++e)   // this fma order is shared with the conv prologues (pro 2 / PA 2)
       o[e] = __builtin_fmaf(coef[c0 + e], g[e], __builtin_fmaf(coef[C + c0 + e], xv[e], coef[2 * C + c0 + e]));
-    *reinterpret_cast<u32x4*>(dx + row * C + c0) = pack8(o);
+    store8(dx + row * C + c0, o);
   }
 }
 
@@ -571,10 +587,25 @@ extern "C" int dlmpi_reduce_blocks(int64_t M, int C) {
   return (int)b;
 }
 
-extern "C" hipError_t dlmpi_bn_stats(const uint16_t* x, int64_t M, int C, int ldx, int xoff, float* partial, int nblk,
-                                     hipStream_t s) {
+// Storage-type dispatch of the templated kernels: f32 = 1 -> float activations (fp32 precision
+// path), 0 -> bf16.  TA(p) casts a `const void*` / `void*` launcher argument to the chosen type.
+#define DLMPI_TLAUNCH(KER, GRID, ...)                                               \
+  do {                                                                             \
+    if (f32) {                                                                     \
+      typedef float T;                                                             \
+      hipLaunchKernelGGL(KER<T>, GRID, dim3(256), 0, s, __VA_ARGS__);              \
+    } else {                                                                       \
+      typedef uint16_t T;                                                          \
+      hipLaunchKernelGGL(KER<T>, GRID, dim3(256), 0, s, __VA_ARGS__);              \
+    }                                                                              \
+  } while (0)
+#define CT(p) static_cast<const T*>(p)
+#define MT(p) static_cast<T*>(p)
+
+extern "C" hipError_t dlmpi_bn_stats(const void* x, int64_t M, int C, int ldx, int xoff, float* partial, int nblk,
+                                     int f32, hipStream_t s) {
   if (C % 8 || C > 2048) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(bn_stats_kernel, dim3(nblk), dim3(256), 0, s, x, M, C, ldx, xoff, partial);
+  DLMPI_TLAUNCH(bn_stats_kernel, dim3(nblk), CT(x), M, C, ldx, xoff, partial);
   return hipGetLastError();
 }
 
@@ -688,12 +719,12 @@ static hipError_t colsum_finalize(const float* partial, int T, int C, int ns, in
   return hipGetLastError();
 }
 
-extern "C" hipError_t dlmpi_outer_dgrad_bn(const uint16_t* dy, int lddy, int64_t M, int C, const uint16_t* w, int ldw,
-                                         const uint16_t* z, const float* mscale, const float* mshift, uint16_t* dx,
-                                         float* partial, int nblk, hipStream_t s) {
+extern "C" hipError_t dlmpi_outer_dgrad_bn(const void* dy, int lddy, int64_t M, int C, const void* w, int ldw,
+                                         const void* z, const float* mscale, const float* mshift, void* dx,
+                                         float* partial, int nblk, int f32, hipStream_t s) {
   if (C % 8 || C > 2048 || M <= 0) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(outer_dgrad_bn_kernel, dim3(nblk), dim3(256), 0, s, dy, lddy, M, C, w, ldw, z, mscale, mshift,
-                     dx, partial);
+  DLMPI_TLAUNCH(outer_dgrad_bn_kernel, dim3(nblk), CT(dy), lddy, M, C, CT(w), ldw, CT(z), mscale, mshift, MT(dx),
+                partial);
   return hipGetLastError();
 }
 
@@ -727,23 +758,23 @@ extern "C" hipError_t dlmpi_bn_finalize(const float* partial, int ntiles, int C,
   return colsum_finalize(partial, ntiles, C, 2, 1, ws, f, s);
 }
 
-extern "C" hipError_t dlmpi_bn_apply(const uint16_t* x, int ldx, int xoff, int64_t M, int C, const float* scale,
-                                     const float* shift, const uint16_t* res, int ldres, int resoff, int relu,
-                                     uint16_t* y, int ldy, int yoff, uint8_t* mbits, hipStream_t s) {
+extern "C" hipError_t dlmpi_bn_apply(const void* x, int ldx, int xoff, int64_t M, int C, const float* scale,
+                                     const float* shift, const void* res, int ldres, int resoff, int relu,
+                                     void* y, int ldy, int yoff, uint8_t* mbits, int f32, hipStream_t s) {
   if (C % 8) return hipErrorInvalidValue;
   const int64_t total = M * (C / 8);
-  hipLaunchKernelGGL(bn_apply_kernel, dim3(ew_blocks(total)), dim3(256), 0, s, x, ldx, xoff, M, C,
-                     make_fastdiv(C / 8), scale, shift, res, ldres, resoff, relu, y, ldy, yoff, mbits);
+  DLMPI_TLAUNCH(bn_apply_kernel, dim3(ew_blocks(total)), CT(x), ldx, xoff, M, C, make_fastdiv(C / 8), scale, shift,
+                CT(res), ldres, resoff, relu, MT(y), ldy, yoff, mbits);
   return hipGetLastError();
 }
 
-extern "C" hipError_t dlmpi_bn_bwd_reduce(const uint16_t* dy, int lddy, int dyoff, const uint16_t* ymask, int ldym,
-                                          int ymoff, const uint16_t* x, int ldx, int xoff, int64_t M, int C,
+extern "C" hipError_t dlmpi_bn_bwd_reduce(const void* dy, int lddy, int dyoff, const void* ymask, int ldym,
+                                          int ymoff, const void* x, int ldx, int xoff, int64_t M, int C,
                                           const float* mean, const float* invstd, float* partial, int nblk,
-                                          hipStream_t s) {
+                                          int f32, hipStream_t s) {
   if (C % 8 || C > 2048) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3(nblk), dim3(256), 0, s, dy, lddy, dyoff, ymask, ldym, ymoff, x, ldx,
-                     xoff, M, C, mean, invstd, partial);
+  DLMPI_TLAUNCH(bn_bwd_reduce_kernel, dim3(nblk), CT(dy), lddy, dyoff, CT(ymask), ldym, ymoff, CT(x), ldx, xoff, M, C,
+                mean, invstd, partial);
   return hipGetLastError();
 }
 
@@ -771,41 +802,53 @@ extern "C" hipError_t dlmpi_bn_bwd_finalize(const float* partial, int nblk, int 
   return dlmpi_bn_bwd_finalize_ex(partial, nblk, 2, 1, 0, C, count, gamma, mean, invstd, dgamma, dbeta, coef, ws, s);
 }
 
-extern "C" hipError_t dlmpi_bn_bwd_apply(const uint16_t* dy, int lddy, int dyoff, const uint16_t* ymask, int ldym,
-                                         int ymoff, const uint16_t* x, int ldx, int xoff, int64_t M, int C,
-                                         const float* coef, uint16_t* dx, uint16_t* dyr_out, hipStream_t s) {
+extern "C" hipError_t dlmpi_bn_bwd_apply(const void* dy, int lddy, int dyoff, const void* ymask, int ldym,
+                                         int ymoff, const void* x, int ldx, int xoff, int64_t M, int C,
+                                         const float* coef, void* dx, void* dyr_out, int f32, hipStream_t s) {
   if (C % 8) return hipErrorInvalidValue;
   const int64_t total = M * (C / 8);
-  hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(ew_blocks(total)), dim3(256), 0, s, dy, lddy, dyoff, ymask, ldym, ymoff,
-                     x, ldx, xoff, M, C, make_fastdiv(C / 8), coef, dx, dyr_out);
+  DLMPI_TLAUNCH(bn_bwd_apply_kernel, dim3(ew_blocks(total)), CT(dy), lddy, dyoff, CT(ymask), ldym, ymoff, CT(x), ldx,
+                xoff, M, C, make_fastdiv(C / 8), coef, MT(dx), MT(dyr_out));
   return hipGetLastError();
 }
 
-extern "C" hipError_t dlmpi_channel_sum(const uint16_t* x, int64_t M, int C, int ldx, int xoff, float* out_acc,
-                                        float* partial, int nblk, double* ws, hipStream_t s) {
+extern "C" hipError_t dlmpi_channel_sum(const void* x, int64_t M, int C, int ldx, int xoff, float* out_acc,
+                                        float* partial, int nblk, double* ws, int f32, hipStream_t s) {
   hipError_t e = dlmpi_bn_bwd_reduce(x, ldx, xoff, nullptr, 0, 0, nullptr, 0, 0, M, C, nullptr, nullptr, partial,
-                                     nblk, s);
+                                     nblk, f32, s);
   if (e != hipSuccess) return e;
   return dlmpi_bn_bwd_finalize(partial, nblk, C, (double)M, nullptr, nullptr, nullptr, nullptr, out_acc, nullptr, ws,
                                s);
 }
 
-extern "C" hipError_t dlmpi_maxpool_bwd_bn(const uint16_t* dy, const uint8_t* idx, int N, int H, int W, int C, int k,
-                                           int stride, int pad, int OH, int OW, const uint16_t* z, const float* mscale,
-                                           const float* mshift, const uint16_t* add, int ldadd, int addoff,
-                                           uint16_t* dx, float* partial, int nblk, hipStream_t s) {
+extern "C" hipError_t dlmpi_maxpool_bwd_bn(const void* dy, const uint8_t* idx, int N, int H, int W, int C, int k,
+                                           int stride, int pad, int OH, int OW, const void* z, const float* mscale,
+                                           const float* mshift, const void* add, int ldadd, int addoff,
+                                           void* dx, float* partial, int nblk, int f32, hipStream_t s) {
   if (C % 8 || C > 2048 || (int64_t)N * H * W >= (1ll << 31)) return hipErrorInvalidValue;
   const int nw = (k + stride - 1) / stride;
   static const bool generic = [] {   // DLMPI_POOL_BWD_GENERIC=1: the dependent window loop (A/B)
     const char* e = getenv("DLMPI_POOL_BWD_GENERIC");
     return e && atoi(e) != 0;
   }();
-#define DLMPI_MPB(NW)                                                                                          \
-  hipLaunchKernelGGL(maxpool_bwd_bn_kernel<NW>, dim3(nblk), dim3(256), 0, s, dy, idx, N, H, W, C, k, stride, pad, \
-                     OH, OW, make_fastdiv(W), make_fastdiv(H), z, mscale, mshift, add, ldadd, addoff, dx, partial)
+#define DLMPI_MPB1(NW, T)                                                                                          \
+  hipLaunchKernelGGL((maxpool_bwd_bn_kernel<NW, T>), dim3(nblk), dim3(256), 0, s, CT(dy), idx, N, H, W, C, k, stride, \
+                     pad, OH, OW, make_fastdiv(W), make_fastdiv(H), CT(z), mscale, mshift, CT(add), ldadd, addoff,   \
+                     MT(dx), partial)
+#define DLMPI_MPB(NW)          \
+  do {                         \
+    if (f32) {                 \
+      typedef float T;         \
+      DLMPI_MPB1(NW, T);       \
+    } else {                   \
+      typedef uint16_t T;      \
+      DLMPI_MPB1(NW, T);       \
+    }                          \
+  } while (0)
   if (!generic && nw == 1) DLMPI_MPB(1);
   else if (!generic && nw == 2) DLMPI_MPB(2);
   else DLMPI_MPB(0);
 #undef DLMPI_MPB
+#undef DLMPI_MPB1
   return hipGetLastError();
 }

@@ -1,4 +1,5 @@
-// Multi-tensor weight re-layout + cast: fp32 master parameters -> bf16 compute copies in the
+// Multi-tensor weight re-layout + cast: fp32 master parameters -> bf16 (or, on the fp32 precision
+// path, fp32) compute copies in the
 // layouts the GEMM kernels consume (forward [K][R][S][Cpad], data-gradient [C][R][S][K],
 // transposed-conv [Cout][2][2][Cin], ...), all tensors in ONE launch.  Each entry describes a
 // 4-D destination (contiguous), per-dimension source strides and a zero-padding limit.
@@ -14,11 +15,13 @@ namespace dlmpi {
 //    data-gradient copy): 64x64 tiles through LDS, coalesced reads along d0 and writes along d3;
 //  * direct (anything else, e.g. the forward copy whose innermost dim is contiguous in the source):
 //    one destination element per thread, grid-stride over the entry.
+template <typename T>
 __global__ __launch_bounds__(256) void cast_weights_kernel(const CastEntry* __restrict__ ent,
                                                            const int4* __restrict__ map) {
   __shared__ float tile[64][65];
   const int4 mb = map[blockIdx.x];
   const CastEntry& e = ent[mb.x];
+  T* const dst = static_cast<T*>(e.dst);
   const int sub = mb.y, nsub = mb.z;
   const int D0 = e.d[0], D1 = e.d[1], D2 = e.d[2], D3 = e.d[3];
   const int64_t n = (int64_t)D0 * D1 * D2 * D3;
@@ -49,7 +52,7 @@ __global__ __launch_bounds__(256) void cast_weights_kernel(const CastEntry* __re
       for (int k = 0; k < 16; ++k) {
         const int i3 = b3 * 64 + tx, i0 = b0 * 64 + ty + 4 * k;
         if (i0 < M0 && i3 < D3)
-          e.dst[(((int64_t)i0 * M1 + i1) * M2 + i2) * D3 + i3] = f2bf(tile[tx][ty + 4 * k]);
+          store1(dst + (((int64_t)i0 * M1 + i1) * M2 + i2) * D3 + i3, tile[tx][ty + 4 * k]);
       }
       __syncthreads();
     }
@@ -57,11 +60,12 @@ __global__ __launch_bounds__(256) void cast_weights_kernel(const CastEntry* __re
   }
   // Direct path.  When the entry's destination and source extents fit 32-bit indices (every
   // conv / linear weight does) and rows are a multiple of 4 wide, each lane produces 4
-  // consecutive destination elements with one 8-byte store and one 32-bit index decomposition
+  // consecutive destination elements with one 4-element store and one 32-bit index decomposition
   // (instead of three 64-bit divisions per element).
   const int64_t smax = (int64_t)(e.valid[0] - 1) * e.st[0] + (int64_t)(e.valid[1] - 1) * e.st[1] +
                        (int64_t)(e.valid[2] - 1) * e.st[2] + (int64_t)(e.valid[3] - 1) * e.st[3];
-  if ((D3 & 3) == 0 && n < (1ll << 31) && smax < (1ll << 31) && ((uintptr_t)e.dst & 7) == 0) {
+  if ((D3 & 3) == 0 && n < (1ll << 31) && smax < (1ll << 31) &&
+      ((uintptr_t)dst & (4 * sizeof(T) - 1)) == 0) {
     const uint32_t nq = (uint32_t)(n >> 2);
     const int s0 = (int)e.st[0], s1 = (int)e.st[1], s2 = (int)e.st[2], s3 = (int)e.st[3];
     const uint32_t uD3 = D3, uD2 = D2, uD1 = D1;
@@ -78,7 +82,8 @@ __global__ __launch_bounds__(256) void cast_weights_kernel(const CastEntry* __re
       float v[4];
 #pragma unroll
       for (int j = 0; j < 4; ++j) v[j] = (v012 && i3 + j < e.valid[3]) ? e.src[base + j * s3] : 0.f;
-      *reinterpret_cast<u32x2*>(e.dst + i) = u32x2{pack2bf(v[0], v[1]), pack2bf(v[2], v[3])};
+      if constexpr (sizeof(T) == 2) *reinterpret_cast<u32x2*>(dst + i) = u32x2{pack2bf(v[0], v[1]), pack2bf(v[2], v[3])};
+      else *reinterpret_cast<f32x4*>(dst + i) = f32x4{v[0], v[1], v[2], v[3]};
     }
     return;
   }
@@ -93,7 +98,7 @@ __global__ __launch_bounds__(256) void cast_weights_kernel(const CastEntry* __re
     float v = 0.f;
     if (i0 < e.valid[0] && i1 < e.valid[1] && i2 < e.valid[2] && i3 < e.valid[3])
       v = e.src[i0 * e.st[0] + i1 * e.st[1] + i2 * e.st[2] + i3 * e.st[3]];
-    e.dst[i] = f2bf(v);
+    store1(dst + i, v);
   }
 }
 
@@ -115,11 +120,15 @@ __global__ void pack_kernel(const void* const* __restrict__ srcs, const int64_t*
 using namespace dlmpi;
 
 extern "C" hipError_t dlmpi_cast_weights(const CastEntry* entries_dev, const void* block_map_dev, int nblocks,
-                                         hipStream_t s) {
+                                         int f32, hipStream_t s) {
   if (nblocks <= 0) return hipSuccess;
   // gaps between entries (alignment padding) are zeroed once at allocation and never written
-  hipLaunchKernelGGL(cast_weights_kernel, dim3((unsigned)nblocks), dim3(256), 0, s, entries_dev,
-                     reinterpret_cast<const int4*>(block_map_dev));
+  if (f32)
+    hipLaunchKernelGGL(cast_weights_kernel<float>, dim3((unsigned)nblocks), dim3(256), 0, s, entries_dev,
+                       reinterpret_cast<const int4*>(block_map_dev));
+  else
+    hipLaunchKernelGGL(cast_weights_kernel<uint16_t>, dim3((unsigned)nblocks), dim3(256), 0, s, entries_dev,
+                       reinterpret_cast<const int4*>(block_map_dev));
   return hipGetLastError();
 }
 

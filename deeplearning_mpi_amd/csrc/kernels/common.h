@@ -1,8 +1,9 @@
 // Shared device helpers for the gfx950 (CDNA4 / MI355X) kernels.
 //
 // Conventions used by every kernel in this directory:
-//   * activations are NHWC, bf16 stored as uint16_t, channel count a multiple of 8
-//     so one 16-byte vector = 8 consecutive channels of one pixel;
+//   * activations are NHWC, bf16 stored as uint16_t (or fp32 on the fp32 precision path: the
+//     kernels are templated on the storage type), channel count a multiple of 8 so one vector
+//     = 8 consecutive channels of one pixel;
 //   * master weights / gradients / BN statistics are fp32;
 //   * all launchers are `extern "C"` and take an explicit hipStream_t so they can be
 //     captured into a hipGraph (no allocation, no synchronisation inside a launcher).
@@ -45,6 +46,45 @@ __device__ __forceinline__ u32x4 pack8(const float* f) {
 #pragma unroll
   for (int i = 0; i < 4; ++i) r[i] = pack2bf(f[2 * i], f[2 * i + 1]);
   return r;
+}
+
+// Storage-type-generic access to 8 consecutive channels (activations are bf16 -- stored as
+// uint16_t -- or, for the fp32 precision path, float).  The arithmetic is always fp32.
+__device__ __forceinline__ void load8(const uint16_t* p, float* f) { unpack8(*reinterpret_cast<const u32x4*>(p), f); }
+__device__ __forceinline__ void load8(const float* p, float* f) {
+  const f32x4 a = *reinterpret_cast<const f32x4*>(p), b = *reinterpret_cast<const f32x4*>(p + 4);
+#pragma unroll
+  for (int e = 0; e < 4; ++e) { f[e] = a[e]; f[e + 4] = b[e]; }
+}
+__device__ __forceinline__ void store8(uint16_t* p, const float* f) { *reinterpret_cast<u32x4*>(p) = pack8(f); }
+__device__ __forceinline__ void store8(float* p, const float* f) {
+  *reinterpret_cast<f32x4*>(p) = f32x4{f[0], f[1], f[2], f[3]};
+  *reinterpret_cast<f32x4*>(p + 4) = f32x4{f[4], f[5], f[6], f[7]};
+}
+__device__ __forceinline__ void store1(uint16_t* p, float v) { *p = f2bf(v); }
+__device__ __forceinline__ void store1(float* p, float v) { *p = v; }
+__device__ __forceinline__ float load1(const uint16_t* p) { return bf2f(*p); }
+__device__ __forceinline__ float load1(const float* p) { return *p; }
+// Raw 8-channel vector of storage type T (kept packed while loads are in flight).
+struct f32x4x2 {
+  f32x4 a, b;
+};
+template <typename T> struct Vec8;
+template <> struct Vec8<uint16_t> { typedef u32x4 type; };
+template <> struct Vec8<float> { typedef f32x4x2 type; };
+template <typename T>
+__device__ __forceinline__ typename Vec8<T>::type raw8(const T* p) {
+  return *reinterpret_cast<const typename Vec8<T>::type*>(p);
+}
+__device__ __forceinline__ void unpack8(const f32x4x2& v, float* f) {
+#pragma unroll
+  for (int e = 0; e < 4; ++e) { f[e] = v.a[e]; f[e + 4] = v.b[e]; }
+}
+// the value as stored in T (statistics are taken of stored values)
+template <typename T>
+__device__ __forceinline__ float stored(float v) {
+  if constexpr (sizeof(T) == 2) return bf2f(f2bf(v));
+  else return v;
 }
 
 __device__ __forceinline__ uint32_t fdiv(uint32_t n, const FastDiv& f) {

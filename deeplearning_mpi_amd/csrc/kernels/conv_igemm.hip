@@ -22,6 +22,7 @@
 // add / folded-BN affine / ReLU and the per-channel BatchNorm partial sums of the stored
 // (bf16-rounded) values.
 #include <cstdlib>
+#include <type_traits>
 
 #ifndef DLMPI_W128   // waves/SIMD target of the 128x128 / 256x64 tiles (A/B builds)
 #define DLMPI_W128 3
@@ -46,16 +47,23 @@ __device__ __forceinline__ void glds16(const void* g, char* lds_wave_base) {
 // K-step of MFMA work (2048 SIMD cycles) covers the next step's loads.
 // WGM = wave rows (WGM x NW/WGM wave grid): 4 x 1 for the 256 x 64 tile of 64-channel layers
 // (per-wave 64 x 64 instead of 64 x 32: a third less LDS traffic per MFMA).
-template <int BM, int BN, bool SMALLC, int STAGES, int NW, int WGM, int PRO = 0>
+// T: storage type of activations and weights -- uint16_t (bf16, v_mfma_f32_16x16x32_bf16) or float
+// (the fp32 precision path: v_mfma_f32_16x16x4_f32, four per 16-byte fragment; the LDS tile keeps
+// its 128-byte rows, i.e. 32 fp32 reduction elements per K-step instead of 64 bf16).
+template <int BM, int BN, bool SMALLC, int STAGES, int NW, int WGM, int PRO = 0, typename ET = uint16_t>
 __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(STAGES == 1 && BM * BN <= 16384 ? (BM * BN == 16384 ? DLMPI_W128 : 3) : 2, 8))) void conv_igemm_kernel(const ConvArgs a) {
   constexpr int NT = 64 * NW;                 // threads
   constexpr int WGN = NW / WGM;               // wave grid WGM x WGN
-  constexpr int BK = 64;
+  using T = ET;                               // element (storage) type
+  constexpr int ES = sizeof(T);               // bytes per element
+  constexpr int BK = 128 / ES;                // reduction elements per K-step (one 128-B LDS row)
+  constexpr int CPC = 16 / ES;                // channels per 16-byte chunk
+  static_assert(PRO == 0 || ES == 2, "operand prologues: bf16 only");
   constexpr int WM = BM / WGM, WN = BN / WGN;
   constexpr int TM = WM / 16, TN = WN / 16;
   constexpr int RP = NT / 8;                  // tile rows staged per pass (8 lanes per 128-B row)
   constexpr int AL = BM / RP, BL = BN / RP;   // 16-byte pieces per thread per tile
-  constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2;
+  constexpr int A_BYTES = BM * 128, B_BYTES = BN * 128;
   static_assert(PRO == 0 || (!SMALLC && STAGES == 1), "operand prologue: regular channels, single stage");
   constexpr int Z_BYTES = PRO == 2 ? A_BYTES : 0;   // the second prologue operand, staged like A
   constexpr int SB = A_BYTES + B_BYTES + Z_BYTES;   // bytes per stage: [A | B | Z]
@@ -101,19 +109,19 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(STAGES 
     a_hw[i] = (h << 16) | w;
     a_pix[i] = ((int)n_img * a.H + h) * a.W + w;
   }
-  const char* xlane = reinterpret_cast<const char*>(a.x) + 2 * ((int64_t)a.xoff + 8 * jc);
+  const char* xlane = reinterpret_cast<const char*>(a.x) + ES * ((int64_t)a.xoff + CPC * jc);
   // B rows n0 + lrow + RP i: one base pointer + validity bits
-  const char* b_base = reinterpret_cast<const char*>(a.w) + 2 * ((int64_t)(n0 + lrow) * a.ldw + 8 * jc);
-  const int64_t b_step = (int64_t)2 * RP * a.ldw;      // bytes between rows RP apart
+  const char* b_base = reinterpret_cast<const char*>(a.w) + ES * ((int64_t)(n0 + lrow) * a.ldw + CPC * jc);
+  const int64_t b_step = (int64_t)ES * RP * a.ldw;     // bytes between rows RP apart
   uint32_t b_okm = 0;
 #pragma unroll
   for (int i = 0; i < BL; ++i)
     if (n0 + lrow + RP * i < a.Kout) b_okm |= 1u << i;
 
   const int C = a.C;
-  const int T = ph.Tr * ph.Ts;
+  const int NTAP = ph.Tr * ph.Ts;
   const int nk = ph.ksteps;
-  const int ldx2 = a.ldx * 2;
+  const int ldx2 = a.ldx * ES;
 
   // ---- staging ------------------------------------------------------------------------------
   // Regular path (C % 64 == 0): the tap t and channel base c are wave-uniform.
@@ -126,7 +134,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(STAGES 
     const int ts = t - tr * ph.Ts;
     const int dh = ph.dh0 + tr * ph.dhs, dw = ph.dw0 + ts * ph.dws;
     const int wt = (ph.wr0 + tr * ph.wrs) * a.S + (ph.ws0 + ts * ph.wss);
-    wtC2 = wt * C * 2;
+    wtC2 = wt * C * ES;
     const int doff = dh * a.W + dw;
     a_vm = 0;
 #pragma unroll
@@ -138,7 +146,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(STAGES 
       if constexpr (PRO == 2) z_off[i] = (uint32_t)(a_pix[i] + doff) * (uint32_t)a.ldpz;
     }
   };
-  const char* zlane = PRO == 2 ? reinterpret_cast<const char*>(a.pz) + 2 * ((int64_t)a.pzoff + 8 * jc) : nullptr;
+  const char* zlane = PRO == 2 ? reinterpret_cast<const char*>(a.pz) + ES * ((int64_t)a.pzoff + CPC * jc) : nullptr;
 
   auto issue = [&](int buf, int ks) {
     char* As = smem + buf * SB;
@@ -146,33 +154,33 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(STAGES 
     if constexpr (!SMALLC) {
 #pragma unroll
       for (int i = 0; i < AL; ++i) {
-        const char* s = ((a_vm >> i) & 1) ? xlane + 2 * ((uint64_t)a_off[i] + c_cur) : zp;
+        const char* s = ((a_vm >> i) & 1) ? xlane + ES * ((uint64_t)a_off[i] + c_cur) : zp;
         glds16(s, As + (RP * i + 8 * wid) * 128);
       }
       if constexpr (PRO == 2) {
         char* Zs = Bs + B_BYTES;
 #pragma unroll
         for (int i = 0; i < AL; ++i) {
-          const char* s = ((a_vm >> i) & 1) ? zlane + 2 * ((uint64_t)z_off[i] + c_cur) : zp;
+          const char* s = ((a_vm >> i) & 1) ? zlane + ES * ((uint64_t)z_off[i] + c_cur) : zp;
           glds16(s, Zs + (RP * i + 8 * wid) * 128);
         }
       }
 #pragma unroll
       for (int i = 0; i < BL; ++i) {
-        const char* s = ((b_okm >> i) & 1) ? b_base + i * b_step + wtC2 + 2 * c_cur : zp;
+        const char* s = ((b_okm >> i) & 1) ? b_base + i * b_step + wtC2 + ES * c_cur : zp;
         glds16(s, Bs + (RP * i + 8 * wid) * 128);
       }
     } else {
       // small C (8/16/32; stem & first UNet layer): every 16-B piece is its own tap
-      const int kk = ks * BK + 8 * jc;
+      const int kk = ks * BK + CPC * jc;
       const int t = kk / C, c = kk - t * C;
-      const bool tv = t < T;
+      const bool tv = t < NTAP;
       const int tt = tv ? t : 0;
       const int tr = (int)fdiv((uint32_t)tt, ph.fdTs);
       const int ts = tt - tr * ph.Ts;
       const int dh = ph.dh0 + tr * ph.dhs, dw = ph.dw0 + ts * ph.dws;
       const int wt = (ph.wr0 + tr * ph.wrs) * a.S + (ph.ws0 + ts * ph.wss);
-      const char* xs = reinterpret_cast<const char*>(a.x) + 2 * ((int64_t)a.xoff + c);
+      const char* xs = reinterpret_cast<const char*>(a.x) + ES * ((int64_t)a.xoff + c);
 #pragma unroll
       for (int i = 0; i < AL; ++i) {
         const int ih = (a_hw[i] >> 16) + dh, iw = (a_hw[i] & 0xffff) + dw;
@@ -182,7 +190,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(STAGES 
       }
 #pragma unroll
       for (int i = 0; i < BL; ++i) {
-        const char* s = (tv && ((b_okm >> i) & 1)) ? b_base + i * b_step - 2 * 8 * jc + 2 * (wt * C + c) : zp;
+        const char* s = (tv && ((b_okm >> i) & 1)) ? b_base + i * b_step - 16 * jc + ES * (wt * C + c) : zp;
         glds16(s, Bs + (RP * i + 8 * wid) * 128);
       }
     }
@@ -247,7 +255,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(STAGES 
   const int fr = lane & 15, fg = lane >> 4;
   auto advance = [&]() {
     if constexpr (!SMALLC) {
-      c_cur += 64;
+      c_cur += BK;
       if (c_cur >= C) {
         c_cur = 0;
         ++t_cur;
@@ -264,9 +272,9 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(STAGES 
   }
   if (kend > kbeg) {
     if constexpr (!SMALLC) {
-      const int cps = C >> 6;   // K-steps per tap
+      const int cps = C / BK;   // K-steps per tap
       t_cur = kbeg / cps;
-      c_cur = (kbeg - t_cur * cps) * 64;
+      c_cur = (kbeg - t_cur * cps) * BK;
       tap_setup(t_cur);
     }
     issue(0, kbeg);
@@ -291,23 +299,34 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(STAGES 
     const char* Bs = As + A_BYTES;
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
-      bf16x8 af[TM], bfr[TN];
+      typedef typename std::conditional<sizeof(T) == 2, bf16x8, f32x4>::type frag_t;
+      frag_t af[TM], bfr[TN];
       const int ch = kk * 4 + fg;
 #pragma unroll
       for (int mi = 0; mi < TM; ++mi) {
         const int r = wm * WM + mi * 16 + fr;
-        af[mi] = *reinterpret_cast<const bf16x8*>(As + r * 128 + ((ch ^ ((r >> 1) & 7)) << 4));
+        af[mi] = *reinterpret_cast<const frag_t*>(As + r * 128 + ((ch ^ ((r >> 1) & 7)) << 4));
       }
 #pragma unroll
       for (int ni = 0; ni < TN; ++ni) {
         const int r = wn * WN + ni * 16 + fr;
-        bfr[ni] = *reinterpret_cast<const bf16x8*>(Bs + r * 128 + ((ch ^ ((r >> 1) & 7)) << 4));
+        bfr[ni] = *reinterpret_cast<const frag_t*>(Bs + r * 128 + ((ch ^ ((r >> 1) & 7)) << 4));
       }
 #pragma unroll
       for (int mi = 0; mi < TM; ++mi)
 #pragma unroll
-        for (int ni = 0; ni < TN; ++ni)
-          acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[mi], bfr[ni], acc[mi][ni], 0, 0, 0);
+        for (int ni = 0; ni < TN; ++ni) {
+          if constexpr (sizeof(T) == 2) {
+            acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[mi], bfr[ni], acc[mi][ni], 0, 0, 0);
+          } else {
+            // the lane's 16-byte chunk holds reduction elements 4 fg + j (j < 4) of this half-step:
+            // MFMA j reduces element j of every lane group -- a fixed permutation of the K order,
+            // identical for A and B
+#pragma unroll
+            for (int jj = 0; jj < 4; ++jj)
+              acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[mi][jj], bfr[ni][jj], acc[mi][ni], 0, 0, 0);
+          }
+        }
     }
     // STAGES 2: waits for this wave's glds of tile ks+1, then all waves -> buffers swap;
     // STAGES 1: every wave is done reading the stage before it is overwritten
@@ -400,7 +419,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(STAGES 
     if (a.stats && !bwd) {
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
-        const float rv = bf2f(f2bf(v[e]));
+        const float rv = stored<T>(v[e]);
         s1[e] += rv;
         s2[e] += rv * rv;
       }
@@ -416,7 +435,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(STAGES 
     const int64_t pix = ((int64_t)n_img * a.OH + (int)p * a.so + ph.oh0) * a.OW + (int)q * a.so + ph.ow0;
     if (a.res) {
       float rr[8];
-      unpack8(*reinterpret_cast<const u32x4*>(a.res + pix * a.ldres + a.resoff + c0), rr);
+      load8(static_cast<const T*>(a.res) + pix * a.ldres + a.resoff + c0, rr);
 #pragma unroll
       for (int e = 0; e < 8; ++e) v[e] += rr[e];
     }
@@ -426,14 +445,14 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(STAGES 
     }
     if (bwd) {
       float zz[8];
-      if (a.z) unpack8(*reinterpret_cast<const u32x4*>(a.z + pix * a.ldz + a.zoff + c0), zz);
+      if (a.z) load8(static_cast<const T*>(a.z) + pix * a.ldz + a.zoff + c0, zz);
       if (a.mbits) {
         const uint32_t b = a.mbits[pix * (a.Kout >> 3) + (c0 >> 3)];
 #pragma unroll
         for (int e = 0; e < 8; ++e) v[e] = (b >> e) & 1u ? v[e] : 0.f;
       } else if (a.mask) {
         float yy[8];
-        unpack8(*reinterpret_cast<const u32x4*>(a.mask + pix * a.ldmask + a.maskoff + c0), yy);
+        load8(static_cast<const T*>(a.mask) + pix * a.ldmask + a.maskoff + c0, yy);
 #pragma unroll
         for (int e = 0; e < 8; ++e) v[e] = yy[e] > 0.f ? v[e] : 0.f;
       } else {   // same fma as the forward BN-apply -> same sign as y
@@ -443,14 +462,14 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(STAGES 
       if (a.stats) {
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
-          const float rv = bf2f(f2bf(v[e]));   // statistics of the stored (bf16) gradient
+          const float rv = stored<T>(v[e]);   // statistics of the stored gradient
           s1[e] += rv;
           s2[e] += rv * zz[e];
         }
         if (a.z2) {
-          unpack8(*reinterpret_cast<const u32x4*>(a.z2 + pix * a.ldz2 + a.z2off + c0), zz);
+          load8(static_cast<const T*>(a.z2) + pix * a.ldz2 + a.z2off + c0, zz);
 #pragma unroll
-          for (int e = 0; e < 8; ++e) s3[e] += bf2f(f2bf(v[e])) * zz[e];
+          for (int e = 0; e < 8; ++e) s3[e] += stored<T>(v[e]) * zz[e];
         }
       }
     }
@@ -549,6 +568,26 @@ static int splitk_plan(int tiles, int nk) {
   return S < 2 ? 1 : S;
 }
 
+// fp32 precision path: single-stage 4-wave tiles up to 128 x 128 (the f32 MFMA is 1/16 of the
+// bf16 rate, so the wider bf16 tiles buy nothing here)
+static hipError_t launch_f32(const ConvArgs* a, int bm, int bn, dim3 grid, hipStream_t s) {
+  if (a->pro != 0) return hipErrorInvalidValue;
+  // the regular staging walks whole 32-channel K-steps per tap; anything else stages per 16-B piece
+  const bool small = a->C < 32 || a->C % 32 != 0;
+#define DLMPI_F32(BM_, BN_)                                                                                        \
+  do {                                                                                                            \
+    if (small) hipLaunchKernelGGL((conv_igemm_kernel<BM_, BN_, true, 1, 4, 2, 0, float>), grid, dim3(256), 0, s, *a); \
+    else hipLaunchKernelGGL((conv_igemm_kernel<BM_, BN_, false, 1, 4, 2, 0, float>), grid, dim3(256), 0, s, *a);     \
+  } while (0)
+  if (bm == 128 && bn == 128) DLMPI_F32(128, 128);
+  else if (bm == 128 && bn == 64) DLMPI_F32(128, 64);
+  else if (bm == 64 && bn == 128) DLMPI_F32(64, 128);
+  else if (bm == 64 && bn == 64) DLMPI_F32(64, 64);
+  else return hipErrorInvalidValue;
+#undef DLMPI_F32
+  return hipGetLastError();
+}
+
 extern "C" hipError_t dlmpi_conv_igemm(const ConvArgs* a_in, int bm, int bn, hipStream_t s) {
   int maxt = 0, tiles = 0, maxk = 0;
   for (int i = 0; i < a_in->nphase; ++i) {
@@ -572,6 +611,7 @@ extern "C" hipError_t dlmpi_conv_igemm(const ConvArgs* a_in, int bm, int bn, hip
   }
   dim3 grid((unsigned)(maxt * a->ntiles), (unsigned)ab.splitk, (unsigned)a->nphase);
   if (grid.x == 0) return hipSuccess;
+  if (a->f32) return launch_f32(a, bm, bn, grid, s);
   if (a->pro != 0 && (a->C < 64 || a->C % 64 != 0 || (bm == 256 && bn == 256))) return hipErrorInvalidValue;
   if (bm == 256 && bn == 256) {   // 8 waves, double-buffered; regular channel counts only
     if (a->C < 64) return hipErrorInvalidValue;

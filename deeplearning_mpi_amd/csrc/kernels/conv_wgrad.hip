@@ -131,8 +131,8 @@ void conv_wgrad_kernel(const WgradArgs a) {
       b_pack[i] = -1;
     }
   }
-  const uint16_t* dyb = a.dy + a.dyoff;
-  const uint16_t* xb = a.x + a.xoff;
+  const uint16_t* dyb = static_cast<const uint16_t*>(a.dy) + a.dyoff;
+  const uint16_t* xb = static_cast<const uint16_t*>(a.x) + a.xoff;
 
   // Branch-free staging: every address is computed unconditionally (no dereference happens for
   // invalid pieces) and the zero page is selected with v_cndmask, so the glds issue is not split
@@ -375,6 +375,93 @@ void conv_wgrad_kernel(const WgradArgs a) {
     }
 }
 
+// fp32 precision path: the same weight gradient with v_mfma_f32_16x16x4_f32.  Tile 64 (Ko) x 64
+// (R*S*C columns) x 32 pixels per K-step, 4 waves of 32 x 32; operands staged through registers
+// into pixel-major LDS rows padded to 80 floats, so the 4-byte fragment reads of the four lane
+// groups (4 consecutive pixel rows) fall on disjoint banks.  Split over pixels into fp32 slabs,
+// reduced by wgrad_reduce_stage1/2 like the bf16 path.
+template <bool DIRECT>
+__global__ __launch_bounds__(256) void conv_wgrad_f32_kernel(const WgradArgs a) {
+  constexpr int BM = 64, BN = 64, BK = 32, LDR = 80;
+  __shared__ __attribute__((aligned(16))) float As[BK * LDR], Bs[BK * LDR];
+  const uint32_t ntile = (uint32_t)a.mtiles * a.ntiles;
+  const uint32_t bid = xcd_remap(blockIdx.x, ntile * a.splits);
+  const int z = bid / ntile;
+  const int tile = bid - z * ntile;
+  const int mt = tile / a.ntiles, nt = tile - mt * a.ntiles;
+  const int m0 = mt * BM, n0 = nt * BN;
+  const int pbeg = z * a.pix_per_split;
+  const int pend = min(a.npix, pbeg + a.pix_per_split);
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid >> 1, wn = wid & 1;
+  const int fr = lane & 15, fg = lane >> 4;
+  const float* dyb = static_cast<const float*>(a.dy) + a.dyoff;
+  const float* xb = static_cast<const float*>(a.x) + a.xoff;
+  const int PQ = a.P * a.Q;
+  f32x4 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int p0 = pbeg; p0 < pend; p0 += BK) {
+    // 2 x 16-B chunks of A and of B per thread: chunk c -> row c / 16, columns 4 (c % 16) .. +3
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int c = tid + 256 * h, row = c >> 4, col = (c & 15) * 4;
+      const int pix = p0 + row;
+      f32x4 va = f32x4{0.f, 0.f, 0.f, 0.f}, vb = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (pix < pend && m0 + col < a.Ko) va = *reinterpret_cast<const f32x4*>(dyb + (int64_t)pix * a.ldy + m0 + col);
+      const int tc = n0 + col;
+      if (pix < pend && tc < a.TC) {
+        const int t = (int)fdiv((uint32_t)tc, a.fdC);
+        const int cch = tc - t * a.C;
+        if (DIRECT) {
+          vb = *reinterpret_cast<const f32x4*>(xb + (int64_t)pix * a.ldx + cch);
+        } else {
+          const int tr = (int)fdiv((uint32_t)t, a.fdS);
+          const int ts = t - tr * a.S;
+          const uint32_t n_img = fdiv((uint32_t)pix, a.fdPQ);
+          const uint32_t rem = (uint32_t)pix - n_img * PQ;
+          const uint32_t pp = fdiv(rem, a.fdQ);
+          const uint32_t qq = rem - pp * a.Q;
+          const int ih = (int)pp * a.stride_h + tr - a.pad_h, iw = (int)qq * a.stride_w + ts - a.pad_w;
+          if ((unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W)
+            vb = *reinterpret_cast<const f32x4*>(xb + (((int64_t)n_img * a.H + ih) * a.W + iw) * a.ldx + cch);
+        }
+      }
+      *reinterpret_cast<f32x4*>(As + row * LDR + col) = va;
+      *reinterpret_cast<f32x4*>(Bs + row * LDR + col) = vb;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k0 = 0; k0 < BK; k0 += 4) {
+      float af[2], bfv[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) af[i] = As[(k0 + fg) * LDR + wm * 32 + i * 16 + fr];
+#pragma unroll
+      for (int j = 0; j < 2; ++j) bfv[j] = Bs[(k0 + fg) * LDR + wn * 32 + j * 16 + fr];
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i], bfv[j], acc[i][j], 0, 0, 0);
+    }
+    __syncthreads();
+  }
+  // D[row = ko][col = tc]: lane holds col (lane & 15), rows 4 (lane >> 4) + r
+  float* wsz = a.ws + (int64_t)z * a.Ko * a.TC;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int cc = n0 + wn * 32 + j * 16 + fr;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int ko = m0 + wm * 32 + i * 16 + fg * 4 + r;
+        if (ko < a.Ko && cc < a.TC) wsz[(int64_t)ko * a.TC + cc] = acc[i][j][r];
+      }
+    }
+}
+
 // Split reduction, stage 1: grid (ceil(total/1024), G): block (x, g) sums split slabs
 // [g*per, (g+1)*per) for 1024 consecutive outputs (4 per thread, 16-byte loads) -> ws2[g][idx].
 __global__ __launch_bounds__(256) void wgrad_reduce_stage1(const float* __restrict__ ws, int splits, int64_t total,
@@ -430,6 +517,12 @@ extern "C" hipError_t dlmpi_conv_wgrad(const WgradArgs* a, int bm, int bn, hipSt
     return e ? atoi(e) : 1;
   }();
   const dim3 g(nwg), b(256);
+  if (a->f32) {
+    if (bm != 64 || bn != 64 || a->ws == nullptr || a->pro_a || a->pro_b) return hipErrorInvalidValue;
+    if (a->direct) hipLaunchKernelGGL(conv_wgrad_f32_kernel<true>, g, b, 0, s, *a);
+    else hipLaunchKernelGGL(conv_wgrad_f32_kernel<false>, g, b, 0, s, *a);
+    return hipGetLastError();
+  }
   // (a 256-column variant was measured 1.3-1.9x slower: 2 waves/SIMD and register spills)
   if (bn != 128 || (bm != 128 && bm != 64)) return hipErrorInvalidValue;
   const bool d = a->direct != 0;

@@ -46,9 +46,9 @@ struct ConvPhase {
 };
 
 struct ConvArgs {
-  const uint16_t* x;
+  const void* x;                   // bf16 (uint16_t) or, with f32 = 1, float elements
   int H, W, C, ldx, xoff;          // input NHWC, pixel stride ldx, channel offset xoff
-  const uint16_t* w;
+  const void* w;
   int ldw, S;                      // weight row stride (= R*S*C), S of the weight tap grid
   void* y;
   int OH, OW, ldy, yoff;           // output NHWC geometry
@@ -58,7 +58,7 @@ struct ConvArgs {
   int kvalid;                      // output channels actually stored (<= Kout)
   int vec_store;                   // 1: 16-byte stores legal (ldy, yoff multiples of 8 and kvalid == Kout)
   const float* bias;               // [Kout] or null
-  const uint16_t* res;             // residual added in the epilogue (same pixel grid as y) or null
+  const void* res;             // residual added in the epilogue (same pixel grid as y) or null
   int ldres, resoff;
   const float* scale;              // per-channel affine after bias (folded eval BN) or null
   const float* shift;
@@ -67,14 +67,14 @@ struct ConvArgs {
   // Backward fusion (the GEMM produces the gradient dy of a BatchNorm+ReLU output y):
   //   v := v * [mask > 0] (ReLU derivative) before the store, and the stats become
   //   {sum v, sum v*z [, sum v*z2]} with z (z2) the BN input(s) that consume this gradient.
-  const uint16_t* mask;            // ReLU output y (mask = y > 0), or null with mscale set:
+  const void* mask;            // ReLU output y (mask = y > 0), or null with mscale set:
   int ldmask, maskoff;
   const float* mscale;             //   mask = z * mscale + mshift > 0 (BN+ReLU without residual:
   const float* mshift;             //   recomputed from z, which the stats read anyway)
   const uint8_t* mbits;            //   or mask bits written by the forward BN-apply ([pix][Kout/8])
-  const uint16_t* z;
+  const void* z;
   int ldz, zoff;
-  const uint16_t* z2;
+  const void* z2;
   int ldz2, z2off;
   int nstat;                       // 2 (fwd: sum v, sum v^2; bwd: sum v, sum v*z) or 3 (bwd with z2)
   int nt_store;                    // 1: non-temporal output stores (streaming outputs)
@@ -90,10 +90,11 @@ struct ConvArgs {
   //   pro 2: A := bf16(pcoef[c] * A + pcoef[C + c] * Z + pcoef[2C + c])   (a deferred BN-backward
   //          apply: A = the masked output gradient dy, Z = the BN input, same pixel grid / C)
   int pro;
+  int f32;                         // 1: activations / weights are fp32 (the fp32 precision path)
   const float* pscale;
   const float* pshift;
   const float* pcoef;
-  const uint16_t* pz;
+  const void* pz;
   int ldpz, pzoff;
   ConvPhase ph[4];
 };
@@ -102,9 +103,9 @@ struct ConvArgs {
 // Weight gradient:  dW[ko][t][c] = sum_pix dY[pix][ko] * X[gather(pix, t)][c]   (split over pix)
 // ---------------------------------------------------------------------------------------------
 struct WgradArgs {
-  const uint16_t* dy;
+  const void* dy;                  // bf16 (uint16_t) or, with f32 = 1, float elements
   int ldy, dyoff, Ko;
-  const uint16_t* x;
+  const void* x;
   int H, W, C, ldx, xoff;
   int Nimg, P, Q, S, stride_h, stride_w, pad_h, pad_w;
   int TC;                          // R*S*C
@@ -124,6 +125,7 @@ struct WgradArgs {
   //   dy side (A): pro_a 2 -> dz = pcoef[k] * dy + pcoef[Ko + k] * Z + pcoef[2 Ko + k]
   //   x side  (B): pro_b 1 -> x := relu(x * pscale[c] + pshift[c])
   int pro_a, pro_b;
+  int f32;                         // 1: fp32 operands (conv_wgrad_f32_kernel, 64 x 64 tiles)
   const float* pcoef;
   const uint16_t* pz;
   int ldpz, pzoff;
@@ -150,15 +152,17 @@ hipError_t dlmpi_bn_finalize(const float* partial, int ntiles, int C, double cou
 int dlmpi_colsum_ws_doubles(int T, int C);
 // register an auxiliary stream (role 1..3) of the current device: own last-arriver ticket array
 hipError_t dlmpi_set_aux_stream(hipStream_t s, int role);
-hipError_t dlmpi_bn_stats(const uint16_t* x, int64_t M, int C, int ldx, int xoff, float* partial, int nblk,
+// Activation-typed launchers below take `const void*` / `void*` activations and `int f32`: 1 = fp32
+// storage (the fp32 precision path), 0 = bf16 (uint16_t).
+hipError_t dlmpi_bn_stats(const void* x, int64_t M, int C, int ldx, int xoff, float* partial, int nblk, int f32,
                           hipStream_t s);
 // mbits (optional): [M][C/8] bytes, bit e of byte (row, g) = y[row][8g + e] > 0 (ReLU mask for backward)
-hipError_t dlmpi_bn_apply(const uint16_t* x, int ldx, int xoff, int64_t M, int C, const float* scale,
-                          const float* shift, const uint16_t* res, int ldres, int resoff, int relu, uint16_t* y,
-                          int ldy, int yoff, uint8_t* mbits, hipStream_t s);
-hipError_t dlmpi_bn_bwd_reduce(const uint16_t* dy, int lddy, int dyoff, const uint16_t* ymask, int ldym, int ymoff,
-                               const uint16_t* x, int ldx, int xoff, int64_t M, int C, const float* mean,
-                               const float* invstd, float* partial, int nblk, hipStream_t s);
+hipError_t dlmpi_bn_apply(const void* x, int ldx, int xoff, int64_t M, int C, const float* scale, const float* shift,
+                          const void* res, int ldres, int resoff, int relu, void* y, int ldy, int yoff, uint8_t* mbits,
+                          int f32, hipStream_t s);
+hipError_t dlmpi_bn_bwd_reduce(const void* dy, int lddy, int dyoff, const void* ymask, int ldym, int ymoff,
+                               const void* x, int ldx, int xoff, int64_t M, int C, const float* mean,
+                               const float* invstd, float* partial, int nblk, int f32, hipStream_t s);
 hipError_t dlmpi_bn_bwd_finalize(const float* partial, int nblk, int C, double count, const float* gamma,
                                  const float* mean, const float* invstd, float* dgamma, float* dbeta,
                                  float* coef, double* ws, hipStream_t s);
@@ -166,60 +170,62 @@ hipError_t dlmpi_bn_bwd_finalize(const float* partial, int nblk, int C, double c
 hipError_t dlmpi_bn_bwd_finalize_ex(const float* partial, int nblk, int ns, int k2, int raw_z, int C, double count,
                                     const float* gamma, const float* mean, const float* invstd, float* dgamma,
                                     float* dbeta, float* coef, double* ws, hipStream_t s);
-hipError_t dlmpi_bn_bwd_apply(const uint16_t* dy, int lddy, int dyoff, const uint16_t* ymask, int ldym, int ymoff,
-                              const uint16_t* x, int ldx, int xoff, int64_t M, int C, const float* coef,
-                              uint16_t* dx, uint16_t* dyr_out, hipStream_t s);
-hipError_t dlmpi_channel_sum(const uint16_t* x, int64_t M, int C, int ldx, int xoff, float* out_acc, float* partial,
-                             int nblk, double* ws, hipStream_t s);
+hipError_t dlmpi_bn_bwd_apply(const void* dy, int lddy, int dyoff, const void* ymask, int ldym, int ymoff,
+                              const void* x, int ldx, int xoff, int64_t M, int C, const float* coef, void* dx,
+                              void* dyr_out, int f32, hipStream_t s);
+hipError_t dlmpi_channel_sum(const void* x, int64_t M, int C, int ldx, int xoff, float* out_acc, float* partial,
+                             int nblk, double* ws, int f32, hipStream_t s);
 int dlmpi_reduce_blocks(int64_t M, int C);
 
 // pooling / layout
-// scale/shift (optional): pool relu(x * scale + shift) (bf16-rounded), i.e. BN-apply + ReLU fused
-hipError_t dlmpi_maxpool_fwd(const uint16_t* x, int N, int H, int W, int C, int ldx, int xoff, int k, int stride,
-                             int pad, uint16_t* y, uint8_t* idx, int OH, int OW, const float* scale,
-                             const float* shift, hipStream_t s);
-hipError_t dlmpi_maxpool_bwd(const uint16_t* dy, const uint8_t* idx, int N, int H, int W, int C, int k, int stride,
-                             int pad, int OH, int OW, const uint16_t* add, int ldadd, int addoff, uint16_t* dx,
-                             int lddx, int dxoff, hipStream_t s);
+// scale/shift (optional): pool relu(x * scale + shift) (rounded to the storage type), i.e. BN-apply + ReLU fused
+hipError_t dlmpi_maxpool_fwd(const void* x, int N, int H, int W, int C, int ldx, int xoff, int k, int stride, int pad,
+                             void* y, uint8_t* idx, int OH, int OW, const float* scale, const float* shift, int f32,
+                             hipStream_t s);
+hipError_t dlmpi_maxpool_bwd(const void* dy, const uint8_t* idx, int N, int H, int W, int C, int k, int stride,
+                             int pad, int OH, int OW, const void* add, int ldadd, int addoff, void* dx, int lddx,
+                             int dxoff, int f32, hipStream_t s);
 // max-pool backward into the gradient of a BN+ReLU output (mask z*scale+shift > 0), with the BN
 // backward partials [nblk][2][C] = {sum dyr, sum dyr*z}; dx/z dense [N*H*W][C]; add (optional): a second
 // gradient of the pool input (channel slice of a [N*H*W][ldadd] buffer) summed in before the mask
-hipError_t dlmpi_maxpool_bwd_bn(const uint16_t* dy, const uint8_t* idx, int N, int H, int W, int C, int k, int stride,
-                                int pad, int OH, int OW, const uint16_t* z, const float* mscale, const float* mshift,
-                                const uint16_t* add, int ldadd, int addoff, uint16_t* dx, float* partial, int nblk,
+hipError_t dlmpi_maxpool_bwd_bn(const void* dy, const uint8_t* idx, int N, int H, int W, int C, int k, int stride,
+                                int pad, int OH, int OW, const void* z, const float* mscale, const float* mshift,
+                                const void* add, int ldadd, int addoff, void* dx, float* partial, int nblk, int f32,
                                 hipStream_t s);
 // data gradient of a 1x1 conv with one output channel (dx[m,c] = dy[m*lddy] * w[c*ldw]) into the
 // gradient of a BN+ReLU output (mask z*scale+shift > 0), BN-backward partials [nblk][2][C]
-hipError_t dlmpi_outer_dgrad_bn(const uint16_t* dy, int lddy, int64_t M, int C, const uint16_t* w, int ldw,
-                                const uint16_t* z, const float* mscale, const float* mshift, uint16_t* dx,
-                                float* partial, int nblk, hipStream_t s);
+hipError_t dlmpi_outer_dgrad_bn(const void* dy, int lddy, int64_t M, int C, const void* w, int ldw, const void* z,
+                                const float* mscale, const float* mshift, void* dx, float* partial, int nblk, int f32,
+                                hipStream_t s);
 // per-(device, stream role) split-K workspaces for the conv kernel (bn.hip): an fp32 slab of at least
 // `floats` elements and `n` zeroed self-resetting tickets; null if unavailable (e.g. would have to
 // grow during a graph capture)
 float* dlmpi_splitk_slab(hipStream_t s, size_t floats);
 int* dlmpi_splitk_tickets(hipStream_t s, int n);
-hipError_t dlmpi_avgpool_fwd(const uint16_t* x, int N, int HW, int C, uint16_t* y, hipStream_t s);
-hipError_t dlmpi_avgpool_bwd(const uint16_t* dy, int N, int HW, int C, uint16_t* dx, hipStream_t s);
-hipError_t dlmpi_nchw_to_nhwc(const float* x, int N, int C, int H, int W, int Cpad, uint16_t* y, hipStream_t s);
-// 2x2 space-to-depth of the zero-padded image: y [N][U][V][4*CS] bf16, slot (vh*2+vw) holds CS channels
-hipError_t dlmpi_s2d_nchw(const float* x, int N, int C, int H, int W, int pad, int U, int V, int CS, uint16_t* y,
+hipError_t dlmpi_avgpool_fwd(const void* x, int N, int HW, int C, void* y, int f32, hipStream_t s);
+hipError_t dlmpi_avgpool_bwd(const void* dy, int N, int HW, int C, void* dx, int f32, hipStream_t s);
+hipError_t dlmpi_nchw_to_nhwc(const float* x, int N, int C, int H, int W, int Cpad, void* y, int f32, hipStream_t s);
+// 2x2 space-to-depth of the zero-padded image: y [N][U][V][4*CS], slot (vh*2+vw) holds CS channels
+hipError_t dlmpi_s2d_nchw(const float* x, int N, int C, int H, int W, int pad, int U, int V, int CS, void* y, int f32,
                           hipStream_t s);
-hipError_t dlmpi_upsample2x_fwd(const uint16_t* x, int N, int H, int W, int C, int ldx, int xoff, uint16_t* y,
-                                int ldy, int yoff, hipStream_t s);
-hipError_t dlmpi_upsample2x_bwd(const uint16_t* dy, int N, int H, int W, int C, int lddy, int dyoff, float* ws,
-                                uint16_t* dx, hipStream_t s);
+hipError_t dlmpi_upsample2x_fwd(const void* x, int N, int H, int W, int C, int ldx, int xoff, void* y, int ldy,
+                                int yoff, int f32, hipStream_t s);
+// bilinear x2 (align_corners) backward as a deterministic gather: dx dense [N*H*W][C]
+hipError_t dlmpi_upsample2x_bwd(const void* dy, int N, int H, int W, int C, int lddy, int dyoff, void* dx, int f32,
+                                hipStream_t s);
 
-// weights: multi-tensor strided 4-D gather + cast fp32 -> bf16 (with zero padding)
+// weights: multi-tensor strided 4-D gather + cast fp32 -> bf16 / fp32 (f32 = 1) with zero padding
 struct CastEntry {
   const float* src;
-  uint16_t* dst;
+  void* dst;
   int d[4];        // destination dims (contiguous)
   int valid[4];    // indices >= valid are zero
   int64_t st[4];   // source strides (elements)
   int64_t start;   // first destination element of this entry in the global enumeration
 };
 // block_map_dev: int4 per block {entry, slice, slices of that entry, 0}
-hipError_t dlmpi_cast_weights(const CastEntry* entries_dev, const void* block_map_dev, int nblocks, hipStream_t s);
+hipError_t dlmpi_cast_weights(const CastEntry* entries_dev, const void* block_map_dev, int nblocks, int f32,
+                              hipStream_t s);
 
 // losses (forward saves what the backward needs; backward reads the upstream grad from device)
 hipError_t dlmpi_softmax_ce_fwd(const float* logits, int ldl, const int64_t* labels, int N, int K, float* loss_rows,
@@ -256,6 +262,13 @@ hipError_t dlmpi_image_batch(const uint8_t* data, const int64_t* labels, const i
 
 // fault injection: keep stream s busy for `ms` milliseconds (bounded; tests of the watchdog)
 hipError_t dlmpi_delay(double ms, hipStream_t s);
+
+// utilities (util.hip): fp32 fill, int64 add, indexed gather dst[i] (+)= src[idx[i]] (idx < 0: zero;
+// esize 2 | 4 bytes, accumulate: fp32 only)
+hipError_t dlmpi_fill_f32(float* p, int64_t n, float v, hipStream_t s);
+hipError_t dlmpi_add_i64(int64_t* p, int64_t n, int64_t v, hipStream_t s);
+hipError_t dlmpi_gather(void* dst, const void* src, const int64_t* idx, int64_t n, int esize, int accumulate,
+                        hipStream_t s);
 
 // comm helpers
 hipError_t dlmpi_pack(const void* const* srcs, const int64_t* offs, int n, int64_t total_bytes, void* dst,

@@ -1,4 +1,5 @@
-// Pooling / layout / resampling kernels (NHWC bf16, 8 channels per thread, 16-byte vectors).
+// Pooling / layout / resampling kernels (NHWC, 8 channels per thread; every kernel is templated on
+// the activation storage type T: uint16_t = bf16, float = the fp32 precision path).
 // Replace ATen MaxPool2d (ResNet stem 3x3/s2/p1, UNet 2x2/s2: /root/reference/pytorch/unet/model.py:25),
 // AdaptiveAvgPool2d(1) (ResNet head), the host-side NCHW fp32 -> NHWC bf16 input conversion, and
 // nn.Upsample(scale_factor=2, mode='bilinear', align_corners=True) (model.py:39-40).
@@ -18,8 +19,9 @@ static inline unsigned ew_blocks(int64_t total) {
 // scale/shift (optional): the pooled input is relu(x * scale + shift) rounded to bf16, i.e. the
 // training-mode BN-apply + ReLU of the ResNet stem fused into the pool -- the stem's BN output is
 // never written or re-read (identical values and argmax to pooling the materialised bf16 tensor).
-__global__ void maxpool_fwd_kernel(const uint16_t* __restrict__ x, int N, int H, int W, int C, int ldx, int xoff,
-                                   int k, int stride, int pad, uint16_t* __restrict__ y, uint8_t* __restrict__ idx,
+template <typename T>
+__global__ void maxpool_fwd_kernel(const T* __restrict__ x, int N, int H, int W, int C, int ldx, int xoff,
+                                   int k, int stride, int pad, T* __restrict__ y, uint8_t* __restrict__ idx,
                                    int OH, int OW, const float* __restrict__ scale, const float* __restrict__ shift) {
   const int CC = C >> 3;
   const int64_t total = (int64_t)N * OH * OW * CC;
@@ -45,17 +47,17 @@ __global__ void maxpool_fwd_kernel(const uint16_t* __restrict__ x, int N, int H,
         const int iw = ow * stride - pad + kw;
         if ((unsigned)iw >= (unsigned)W) continue;
         float v[8];
-        unpack8(*reinterpret_cast<const u32x4*>(x + (((int64_t)n * H + ih) * W + iw) * ldx + xoff + cc * 8), v);
+        load8(x + (((int64_t)n * H + ih) * W + iw) * ldx + xoff + cc * 8, v);
         if (scale) {
 #pragma unroll
-          for (int e = 0; e < 8; ++e) v[e] = bf2f(f2bf(fmaxf(v[e] * sc[e] + sh[e], 0.f)));
+          for (int e = 0; e < 8; ++e) v[e] = stored<T>(fmaxf(v[e] * sc[e] + sh[e], 0.f));
         }
 #pragma unroll
         for (int e = 0; e < 8; ++e)
           if (v[e] > best[e] || (v[e] != v[e] && best[e] == best[e])) { best[e] = v[e]; bi[e] = (uint8_t)(kh * k + kw); }
       }
     }
-    *reinterpret_cast<u32x4*>(y + pix * C + cc * 8) = pack8(best);
+    store8(y + pix * C + cc * 8, best);
     uint64_t packed = 0;
 #pragma unroll
     for (int e = 0; e < 8; ++e) packed |= (uint64_t)bi[e] << (8 * e);
@@ -65,9 +67,10 @@ __global__ void maxpool_fwd_kernel(const uint16_t* __restrict__ x, int N, int H,
 
 // Max pool backward as a gather (no atomics): each input pixel sums the gradients of the windows
 // that selected it; optionally adds a second gradient source (UNet skip-concat slice).
-__global__ void maxpool_bwd_kernel(const uint16_t* __restrict__ dy, const uint8_t* __restrict__ idx, int N, int H,
+template <typename T>
+__global__ void maxpool_bwd_kernel(const T* __restrict__ dy, const uint8_t* __restrict__ idx, int N, int H,
                                    int W, int C, int k, int stride, int pad, int OH, int OW,
-                                   const uint16_t* __restrict__ add, int ldadd, int addoff, uint16_t* __restrict__ dx,
+                                   const T* __restrict__ add, int ldadd, int addoff, T* __restrict__ dx,
                                    int lddx, int dxoff, FastDiv fdCC, FastDiv fdW, FastDiv fdH) {
   const int CC = C >> 3;
   const int64_t total = (int64_t)N * H * W * CC;
@@ -92,7 +95,7 @@ __global__ void maxpool_bwd_kernel(const uint16_t* __restrict__ dy, const uint8_
       n = (int)(t2 / H);
     }
     float g[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    if (add) unpack8(*reinterpret_cast<const u32x4*>(add + pix * ldadd + addoff + cc * 8), g);
+    if (add) load8(add + pix * ldadd + addoff + cc * 8, g);
     // windows oh with oh*stride - pad <= ih <= oh*stride - pad + k - 1
     int oh_lo = ih + pad - k + 1;
     oh_lo = oh_lo <= 0 ? 0 : (oh_lo + stride - 1) / stride;
@@ -106,18 +109,19 @@ __global__ void maxpool_bwd_kernel(const uint16_t* __restrict__ dy, const uint8_
         const int64_t op = ((int64_t)n * OH + oh) * OW + ow;
         const uint64_t id = *reinterpret_cast<const uint64_t*>(idx + op * C + cc * 8);
         float d[8];
-        unpack8(*reinterpret_cast<const u32x4*>(dy + op * C + cc * 8), d);
+        load8(dy + op * C + cc * 8, d);
 #pragma unroll
         for (int e = 0; e < 8; ++e)
           if (((id >> (8 * e)) & 0xff) == want) g[e] += d[e];
       }
     }
-    *reinterpret_cast<u32x4*>(dx + pix * lddx + dxoff + cc * 8) = pack8(g);
+    store8(dx + pix * lddx + dxoff + cc * 8, g);
   }
 }
 
 // Global average pool [N][HW][C] -> [N][C]
-__global__ void avgpool_fwd_kernel(const uint16_t* __restrict__ x, int N, int HW, int C, uint16_t* __restrict__ y) {
+template <typename T>
+__global__ void avgpool_fwd_kernel(const T* __restrict__ x, int N, int HW, int C, T* __restrict__ y) {
   const int CC = C >> 3;
   const int64_t total = (int64_t)N * CC;
   const float inv = 1.f / (float)HW;
@@ -127,17 +131,18 @@ __global__ void avgpool_fwd_kernel(const uint16_t* __restrict__ x, int N, int HW
     float s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     for (int p = 0; p < HW; ++p) {
       float v[8];
-      unpack8(*reinterpret_cast<const u32x4*>(x + ((int64_t)n * HW + p) * C + cc * 8), v);
+      load8(x + ((int64_t)n * HW + p) * C + cc * 8, v);
 #pragma unroll
       for (int e = 0; e < 8; ++e) s[e] += v[e];
     }
 #pragma unroll
     for (int e = 0; e < 8; ++e) s[e] *= inv;
-    *reinterpret_cast<u32x4*>(y + (int64_t)n * C + cc * 8) = pack8(s);
+    store8(y + (int64_t)n * C + cc * 8, s);
   }
 }
 
-__global__ void avgpool_bwd_kernel(const uint16_t* __restrict__ dy, int N, int HW, int C, uint16_t* __restrict__ dx) {
+template <typename T>
+__global__ void avgpool_bwd_kernel(const T* __restrict__ dy, int N, int HW, int C, T* __restrict__ dx) {
   const int CC = C >> 3;
   const int64_t total = (int64_t)N * HW * CC;
   const float inv = 1.f / (float)HW;
@@ -146,16 +151,17 @@ __global__ void avgpool_bwd_kernel(const uint16_t* __restrict__ dy, int N, int H
     const int64_t pix = i / CC;
     const int n = (int)(pix / HW);
     float v[8];
-    unpack8(*reinterpret_cast<const u32x4*>(dy + (int64_t)n * C + cc * 8), v);
+    load8(dy + (int64_t)n * C + cc * 8, v);
 #pragma unroll
     for (int e = 0; e < 8; ++e) v[e] *= inv;
-    *reinterpret_cast<u32x4*>(dx + pix * C + cc * 8) = pack8(v);
+    store8(dx + pix * C + cc * 8, v);
   }
 }
 
-// NCHW fp32 -> NHWC bf16 with channel zero-padding to Cpad (multiple of 8).
+// NCHW fp32 -> NHWC T with channel zero-padding to Cpad (multiple of 8).
+template <typename T>
 __global__ void nchw_to_nhwc_kernel(const float* __restrict__ x, int N, int C, int H, int W, int Cpad,
-                                    uint16_t* __restrict__ y) {
+                                    T* __restrict__ y) {
   const int CC = Cpad >> 3;
   const int64_t HW = (int64_t)H * W;
   const int64_t total = (int64_t)N * HW * CC;
@@ -169,15 +175,16 @@ __global__ void nchw_to_nhwc_kernel(const float* __restrict__ x, int N, int C, i
       const int c = cc * 8 + e;
       v[e] = c < C ? x[(n * C + c) * HW + hw] : 0.f;
     }
-    *reinterpret_cast<u32x4*>(y + pix * Cpad + cc * 8) = pack8(v);
+    store8(y + pix * Cpad + cc * 8, v);
   }
 }
 
 // 2x2 space-to-depth of a zero-padded fp32 NCHW image into bf16 NHWC (the strided-stem layout,
 // models/engine.py:S2DConvUnit): y[n][u][v][(vh*2 + vw)*CS + c] = x[n][c][2u+vh-pad][2v+vw-pad]
 // (zero outside the image and for c >= C).  One thread = 8 output channels of one pixel.
+template <typename T>
 __global__ void s2d_nchw_kernel(const float* __restrict__ x, int N, int C, int H, int W, int pad, int U, int V, int CS,
-                                uint16_t* __restrict__ y) {
+                                T* __restrict__ y) {
   const int CT = 4 * CS, CC = CT >> 3;
   const int64_t total = (int64_t)N * U * V * CC;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
@@ -195,13 +202,14 @@ __global__ void s2d_nchw_kernel(const float* __restrict__ x, int N, int C, int H
       o[e] = (c < C && (unsigned)h < (unsigned)H && (unsigned)w < (unsigned)W) ? x[((n * C + c) * H + h) * W + w]
                                                                                : 0.f;
     }
-    *reinterpret_cast<u32x4*>(y + pix * CT + g * 8) = pack8(o);
+    store8(y + pix * CT + g * 8, o);
   }
 }
 
 // Bilinear x2 upsample, align_corners=True: src = o * (in-1)/(out-1).
-__global__ void upsample2x_fwd_kernel(const uint16_t* __restrict__ x, int N, int H, int W, int C, int ldx, int xoff,
-                                      uint16_t* __restrict__ y, int ldy, int yoff) {
+template <typename T>
+__global__ void upsample2x_fwd_kernel(const T* __restrict__ x, int N, int H, int W, int C, int ldx, int xoff,
+                                      T* __restrict__ y, int ldy, int yoff) {
   const int OH = 2 * H, OW = 2 * W, CC = C >> 3;
   const float sh = OH > 1 ? (float)(H - 1) / (float)(OH - 1) : 0.f;
   const float sw = OW > 1 ? (float)(W - 1) / (float)(OW - 1) : 0.f;
@@ -219,55 +227,73 @@ __global__ void upsample2x_fwd_kernel(const uint16_t* __restrict__ x, int N, int
     const float lh = fh - h0, lw = fw - w0;
     float a[8], b[8], c[8], d[8], o[8];
     const int64_t base = (int64_t)n * H;
-    unpack8(*reinterpret_cast<const u32x4*>(x + ((base + h0) * W + w0) * ldx + xoff + cc * 8), a);
-    unpack8(*reinterpret_cast<const u32x4*>(x + ((base + h0) * W + w1) * ldx + xoff + cc * 8), b);
-    unpack8(*reinterpret_cast<const u32x4*>(x + ((base + h1) * W + w0) * ldx + xoff + cc * 8), c);
-    unpack8(*reinterpret_cast<const u32x4*>(x + ((base + h1) * W + w1) * ldx + xoff + cc * 8), d);
+    load8(x + ((base + h0) * W + w0) * ldx + xoff + cc * 8, a);
+    load8(x + ((base + h0) * W + w1) * ldx + xoff + cc * 8, b);
+    load8(x + ((base + h1) * W + w0) * ldx + xoff + cc * 8, c);
+    load8(x + ((base + h1) * W + w1) * ldx + xoff + cc * 8, d);
 #pragma unroll
     for (int e = 0; e < 8; ++e)
       o[e] = (1.f - lh) * ((1.f - lw) * a[e] + lw * b[e]) + lh * ((1.f - lw) * c[e] + lw * d[e]);
-    *reinterpret_cast<u32x4*>(y + pix * ldy + yoff + cc * 8) = pack8(o);
+    store8(y + pix * ldy + yoff + cc * 8, o);
   }
 }
 
-__global__ void upsample2x_bwd_scatter_kernel(const uint16_t* __restrict__ dy, int N, int H, int W, int C, int lddy,
-                                              int dyoff, float* __restrict__ ws) {
+// Bilinear x2 backward as a GATHER (deterministic, no atomics): input pixel (h, w) sums, in
+// ascending (oh, ow) order, the output gradients whose interpolation footprint contains it, with the
+// forward's own weights (same fh = oh * sh, h0 = (int) fh, lh = fh - h0 arithmetic).  An output row
+// oh touches input rows h0(oh) and h1(oh) = min(h0 + 1, H - 1) with h0 = floor(oh * sh) monotone in
+// oh, so h receives from h0 in {h - 1, h}: oh in [(h - 1) / sh, (h + 1) / sh), widened by one row
+// each side against rounding (sh = (H-1)/(2H-1) < 1/2: at most ~2/sh + 3 candidate rows).
+__device__ __forceinline__ void bilin_rows(int o, float s, int n_in, int& i0, int& i1, float& l) {
+  const float f = o * s;
+  i0 = (int)f;
+  i1 = min(i0 + 1, n_in - 1);
+  l = f - i0;
+}
+
+template <typename T>
+__global__ void upsample2x_bwd_kernel(const T* __restrict__ dy, int N, int H, int W, int C, int lddy, int dyoff,
+                                      T* __restrict__ dx) {
   const int OH = 2 * H, OW = 2 * W, CC = C >> 3;
   const float sh = OH > 1 ? (float)(H - 1) / (float)(OH - 1) : 0.f;
   const float sw = OW > 1 ? (float)(W - 1) / (float)(OW - 1) : 0.f;
-  const int64_t total = (int64_t)N * OH * OW * CC;
+  const int64_t total = (int64_t)N * H * W * CC;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
     const int cc = (int)(i % CC);
     const int64_t pix = i / CC;
-    const int ow = (int)(pix % OW);
-    const int64_t t2 = pix / OW;
-    const int oh = (int)(t2 % OH);
-    const int n = (int)(t2 / OH);
-    const float fh = oh * sh, fw = ow * sw;
-    const int h0 = (int)fh, w0 = (int)fw;
-    const int h1 = min(h0 + 1, H - 1), w1 = min(w0 + 1, W - 1);
-    const float lh = fh - h0, lw = fw - w0;
-    float g[8];
-    unpack8(*reinterpret_cast<const u32x4*>(dy + pix * lddy + dyoff + cc * 8), g);
-    const int64_t base = (int64_t)n * H;
-    const int64_t p00 = ((base + h0) * W + w0) * C, p01 = ((base + h0) * W + w1) * C;
-    const int64_t p10 = ((base + h1) * W + w0) * C, p11 = ((base + h1) * W + w1) * C;
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      const int c = cc * 8 + e;
-      atomicAdd(ws + p00 + c, (1.f - lh) * (1.f - lw) * g[e]);
-      atomicAdd(ws + p01 + c, (1.f - lh) * lw * g[e]);
-      atomicAdd(ws + p10 + c, lh * (1.f - lw) * g[e]);
-      atomicAdd(ws + p11 + c, lh * lw * g[e]);
+    const int w = (int)(pix % W);
+    const int64_t t2 = pix / W;
+    const int h = (int)(t2 % H);
+    const int n = (int)(t2 / H);
+    int oh_lo = 0, oh_hi = OH - 1, ow_lo = 0, ow_hi = OW - 1;
+    if (sh > 0.f) {
+      oh_lo = max(0, (int)floorf((h - 1) / sh) - 1);
+      oh_hi = min(OH - 1, (int)((h + 1) / sh) + 1);
     }
-  }
-}
-
-__global__ void f32_to_bf16_kernel(const float* __restrict__ x, int64_t n8, uint16_t* __restrict__ y) {
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n8; i += (int64_t)gridDim.x * blockDim.x) {
-    const f32x4 a = *reinterpret_cast<const f32x4*>(x + 8 * i), b = *reinterpret_cast<const f32x4*>(x + 8 * i + 4);
-    const float v[8] = {a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
-    *reinterpret_cast<u32x4*>(y + 8 * i) = pack8(v);
+    if (sw > 0.f) {
+      ow_lo = max(0, (int)floorf((w - 1) / sw) - 1);
+      ow_hi = min(OW - 1, (int)((w + 1) / sw) + 1);
+    }
+    float g[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (int oh = oh_lo; oh <= oh_hi; ++oh) {
+      int h0, h1;
+      float lh;
+      bilin_rows(oh, sh, H, h0, h1, lh);
+      const float wh = (h0 == h ? 1.f - lh : 0.f) + (h1 == h ? lh : 0.f);
+      if (h0 != h && h1 != h) continue;
+      for (int ow = ow_lo; ow <= ow_hi; ++ow) {
+        int w0, w1;
+        float lw;
+        bilin_rows(ow, sw, W, w0, w1, lw);
+        if (w0 != w && w1 != w) continue;
+        const float ww = (w0 == w ? 1.f - lw : 0.f) + (w1 == w ? lw : 0.f);
+        float d[8];
+        load8(dy + (((int64_t)n * OH + oh) * OW + ow) * lddy + dyoff + cc * 8, d);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) g[e] += wh * ww * d[e];
+      }
+    }
+    store8(dx + pix * C + cc * 8, g);
   }
 }
 
@@ -275,71 +301,92 @@ __global__ void f32_to_bf16_kernel(const float* __restrict__ x, int64_t n8, uint
 
 using namespace dlmpi;
 
-extern "C" hipError_t dlmpi_maxpool_fwd(const uint16_t* x, int N, int H, int W, int C, int ldx, int xoff, int k,
-                                        int stride, int pad, uint16_t* y, uint8_t* idx, int OH, int OW,
-                                        const float* scale, const float* shift, hipStream_t s) {
+// f32: 1 = fp32 activations (the fp32 precision path), 0 = bf16 (uint16_t storage)
+extern "C" hipError_t dlmpi_maxpool_fwd(const void* x, int N, int H, int W, int C, int ldx, int xoff, int k,
+                                        int stride, int pad, void* y, uint8_t* idx, int OH, int OW,
+                                        const float* scale, const float* shift, int f32, hipStream_t s) {
   if (C % 8) return hipErrorInvalidValue;
   const int64_t total = (int64_t)N * OH * OW * (C / 8);
-  hipLaunchKernelGGL(maxpool_fwd_kernel, dim3(ew_blocks(total)), dim3(256), 0, s, x, N, H, W, C, ldx, xoff, k, stride,
-                     pad, y, idx, OH, OW, scale, shift);
+  if (f32)
+    hipLaunchKernelGGL(maxpool_fwd_kernel<float>, dim3(ew_blocks(total)), dim3(256), 0, s, (const float*)x, N, H, W, C,
+                       ldx, xoff, k, stride, pad, (float*)y, idx, OH, OW, scale, shift);
+  else
+    hipLaunchKernelGGL(maxpool_fwd_kernel<uint16_t>, dim3(ew_blocks(total)), dim3(256), 0, s, (const uint16_t*)x, N, H,
+                       W, C, ldx, xoff, k, stride, pad, (uint16_t*)y, idx, OH, OW, scale, shift);
   return hipGetLastError();
 }
 
-extern "C" hipError_t dlmpi_maxpool_bwd(const uint16_t* dy, const uint8_t* idx, int N, int H, int W, int C, int k,
-                                        int stride, int pad, int OH, int OW, const uint16_t* add, int ldadd,
-                                        int addoff, uint16_t* dx, int lddx, int dxoff, hipStream_t s) {
+extern "C" hipError_t dlmpi_maxpool_bwd(const void* dy, const uint8_t* idx, int N, int H, int W, int C, int k,
+                                        int stride, int pad, int OH, int OW, const void* add, int ldadd,
+                                        int addoff, void* dx, int lddx, int dxoff, int f32, hipStream_t s) {
   if (C % 8) return hipErrorInvalidValue;
   const int64_t total = (int64_t)N * H * W * (C / 8);
-  hipLaunchKernelGGL(maxpool_bwd_kernel, dim3(ew_blocks(total)), dim3(256), 0, s, dy, idx, N, H, W, C, k, stride, pad,
-                     OH, OW, add, ldadd, addoff, dx, lddx, dxoff, make_fastdiv(C / 8), make_fastdiv(W),
-                     make_fastdiv(H));
+  const dim3 g(ew_blocks(total));
+  if (f32)
+    hipLaunchKernelGGL(maxpool_bwd_kernel<float>, g, dim3(256), 0, s, (const float*)dy, idx, N, H, W, C, k, stride,
+                       pad, OH, OW, (const float*)add, ldadd, addoff, (float*)dx, lddx, dxoff, make_fastdiv(C / 8),
+                       make_fastdiv(W), make_fastdiv(H));
+  else
+    hipLaunchKernelGGL(maxpool_bwd_kernel<uint16_t>, g, dim3(256), 0, s, (const uint16_t*)dy, idx, N, H, W, C, k,
+                       stride, pad, OH, OW, (const uint16_t*)add, ldadd, addoff, (uint16_t*)dx, lddx, dxoff,
+                       make_fastdiv(C / 8), make_fastdiv(W), make_fastdiv(H));
   return hipGetLastError();
 }
 
-extern "C" hipError_t dlmpi_avgpool_fwd(const uint16_t* x, int N, int HW, int C, uint16_t* y, hipStream_t s) {
-  const int64_t total = (int64_t)N * (C / 8);
-  hipLaunchKernelGGL(avgpool_fwd_kernel, dim3(ew_blocks(total)), dim3(256), 0, s, x, N, HW, C, y);
+extern "C" hipError_t dlmpi_avgpool_fwd(const void* x, int N, int HW, int C, void* y, int f32, hipStream_t s) {
+  const dim3 g(ew_blocks((int64_t)N * (C / 8)));
+  if (f32) hipLaunchKernelGGL(avgpool_fwd_kernel<float>, g, dim3(256), 0, s, (const float*)x, N, HW, C, (float*)y);
+  else hipLaunchKernelGGL(avgpool_fwd_kernel<uint16_t>, g, dim3(256), 0, s, (const uint16_t*)x, N, HW, C, (uint16_t*)y);
   return hipGetLastError();
 }
 
-extern "C" hipError_t dlmpi_avgpool_bwd(const uint16_t* dy, int N, int HW, int C, uint16_t* dx, hipStream_t s) {
-  const int64_t total = (int64_t)N * HW * (C / 8);
-  hipLaunchKernelGGL(avgpool_bwd_kernel, dim3(ew_blocks(total)), dim3(256), 0, s, dy, N, HW, C, dx);
+extern "C" hipError_t dlmpi_avgpool_bwd(const void* dy, int N, int HW, int C, void* dx, int f32, hipStream_t s) {
+  const dim3 g(ew_blocks((int64_t)N * HW * (C / 8)));
+  if (f32) hipLaunchKernelGGL(avgpool_bwd_kernel<float>, g, dim3(256), 0, s, (const float*)dy, N, HW, C, (float*)dx);
+  else hipLaunchKernelGGL(avgpool_bwd_kernel<uint16_t>, g, dim3(256), 0, s, (const uint16_t*)dy, N, HW, C,
+                          (uint16_t*)dx);
   return hipGetLastError();
 }
 
-extern "C" hipError_t dlmpi_nchw_to_nhwc(const float* x, int N, int C, int H, int W, int Cpad, uint16_t* y,
+extern "C" hipError_t dlmpi_nchw_to_nhwc(const float* x, int N, int C, int H, int W, int Cpad, void* y, int f32,
                                          hipStream_t s) {
   if (Cpad % 8 || Cpad < C) return hipErrorInvalidValue;
-  const int64_t total = (int64_t)N * H * W * (Cpad / 8);
-  hipLaunchKernelGGL(nchw_to_nhwc_kernel, dim3(ew_blocks(total)), dim3(256), 0, s, x, N, C, H, W, Cpad, y);
+  const dim3 g(ew_blocks((int64_t)N * H * W * (Cpad / 8)));
+  if (f32) hipLaunchKernelGGL(nchw_to_nhwc_kernel<float>, g, dim3(256), 0, s, x, N, C, H, W, Cpad, (float*)y);
+  else hipLaunchKernelGGL(nchw_to_nhwc_kernel<uint16_t>, g, dim3(256), 0, s, x, N, C, H, W, Cpad, (uint16_t*)y);
   return hipGetLastError();
 }
 
 extern "C" hipError_t dlmpi_s2d_nchw(const float* x, int N, int C, int H, int W, int pad, int U, int V, int CS,
-                                     uint16_t* y, hipStream_t s) {
+                                     void* y, int f32, hipStream_t s) {
   if ((4 * CS) % 8 || C > CS) return hipErrorInvalidValue;
-  const int64_t total = (int64_t)N * U * V * (CS / 2);
-  hipLaunchKernelGGL(s2d_nchw_kernel, dim3(ew_blocks(total)), dim3(256), 0, s, x, N, C, H, W, pad, U, V, CS, y);
+  const dim3 g(ew_blocks((int64_t)N * U * V * (CS / 2)));
+  if (f32) hipLaunchKernelGGL(s2d_nchw_kernel<float>, g, dim3(256), 0, s, x, N, C, H, W, pad, U, V, CS, (float*)y);
+  else hipLaunchKernelGGL(s2d_nchw_kernel<uint16_t>, g, dim3(256), 0, s, x, N, C, H, W, pad, U, V, CS, (uint16_t*)y);
   return hipGetLastError();
 }
 
-extern "C" hipError_t dlmpi_upsample2x_fwd(const uint16_t* x, int N, int H, int W, int C, int ldx, int xoff,
-                                           uint16_t* y, int ldy, int yoff, hipStream_t s) {
-  const int64_t total = (int64_t)N * 4 * H * W * (C / 8);
-  hipLaunchKernelGGL(upsample2x_fwd_kernel, dim3(ew_blocks(total)), dim3(256), 0, s, x, N, H, W, C, ldx, xoff, y, ldy,
-                     yoff);
+extern "C" hipError_t dlmpi_upsample2x_fwd(const void* x, int N, int H, int W, int C, int ldx, int xoff, void* y,
+                                           int ldy, int yoff, int f32, hipStream_t s) {
+  const dim3 g(ew_blocks((int64_t)N * 4 * H * W * (C / 8)));
+  if (f32)
+    hipLaunchKernelGGL(upsample2x_fwd_kernel<float>, g, dim3(256), 0, s, (const float*)x, N, H, W, C, ldx, xoff,
+                       (float*)y, ldy, yoff);
+  else
+    hipLaunchKernelGGL(upsample2x_fwd_kernel<uint16_t>, g, dim3(256), 0, s, (const uint16_t*)x, N, H, W, C, ldx, xoff,
+                       (uint16_t*)y, ldy, yoff);
   return hipGetLastError();
 }
 
-extern "C" hipError_t dlmpi_upsample2x_bwd(const uint16_t* dy, int N, int H, int W, int C, int lddy, int dyoff,
-                                           float* ws, uint16_t* dx, hipStream_t s) {
-  const int64_t nin = (int64_t)N * H * W * C;
-  hipError_t e = hipMemsetAsync(ws, 0, nin * sizeof(float), s);
-  if (e != hipSuccess) return e;
-  const int64_t total = (int64_t)N * 4 * H * W * (C / 8);
-  hipLaunchKernelGGL(upsample2x_bwd_scatter_kernel, dim3(ew_blocks(total)), dim3(256), 0, s, dy, N, H, W, C, lddy,
-                     dyoff, ws);
-  hipLaunchKernelGGL(f32_to_bf16_kernel, dim3(ew_blocks(nin / 8)), dim3(256), 0, s, ws, nin / 8, dx);
+extern "C" hipError_t dlmpi_upsample2x_bwd(const void* dy, int N, int H, int W, int C, int lddy, int dyoff, void* dx,
+                                           int f32, hipStream_t s) {
+  if (C % 8) return hipErrorInvalidValue;
+  const dim3 g(ew_blocks((int64_t)N * H * W * (C / 8)));
+  if (f32)
+    hipLaunchKernelGGL(upsample2x_bwd_kernel<float>, g, dim3(256), 0, s, (const float*)dy, N, H, W, C, lddy, dyoff,
+                       (float*)dx);
+  else
+    hipLaunchKernelGGL(upsample2x_bwd_kernel<uint16_t>, g, dim3(256), 0, s, (const uint16_t*)dy, N, H, W, C, lddy,
+                       dyoff, (uint16_t*)dx);
   return hipGetLastError();
 }

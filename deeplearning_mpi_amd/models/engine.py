@@ -188,7 +188,10 @@ class ConvUnit:
             return self.bias.data
         if self._bias_pad is None or self._bias_pad.device != self.bias.device:
             self._bias_pad = torch.zeros(self.Kp, dtype=self.bias.dtype, device=self.bias.device)
-        self._bias_pad[:self.K].copy_(self.bias.data)
+            idx = torch.arange(self.Kp)
+            idx[self.K:] = -1   # zero padding
+            self._bias_idx = idx.to(self.bias.device)
+        self.arena.backend.gather_(self._bias_pad, self.bias.data, self._bias_idx)   # one launch of ours
         return self._bias_pad
 
     def fwd(self, be, x, train: bool, res: Act = None, out: Act = None, save=True, defer_apply=False):
@@ -302,9 +305,12 @@ class ConvUnit:
                     if self.Kp == self.K:
                         be.channel_sum(dz, ar.grad_flat(self.bias))
                     else:
-                        tmp = torch.zeros(self.Kp, dtype=be.dt, device=dz.device)
+                        tmp = torch.empty(self.Kp, dtype=be.dt, device=dz.device)
+                        be.fill_(tmp, 0.0)
                         be.channel_sum(dz, tmp)
-                        ar.grad_flat(self.bias).add_(tmp[:self.K])
+                        if getattr(self, "_kidx", None) is None or self._kidx.device != dz.device:
+                            self._kidx = torch.arange(self.K, device=dz.device)
+                        be.gather_(ar.grad_flat(self.bias), tmp, self._kidx, accumulate=True)
                     ar.ready(self.bias)
                 self._wgrad(be, dz, x)
                 ar.ready(self.conv.weight)
@@ -362,16 +368,24 @@ class S2DConvUnit(ConvUnit):
                 self.h_slots.append(arena.add_compute(v, (self.Kp, self.R, self.S, self.CS),
                                                       (K, v.shape[2], v.shape[3], Cin), (0, 2, 3, 1)))
         self.w2 = None
+        self._w2idx = None
         arena.post_refresh.append(self._build_w2)
         self._gidx = None
 
     def _build_w2(self):
+        """w2[k][a][b][slot * CS + c] = slot copy [k][a][b][c]: one gather launch from the compute
+        copies (index map built once)."""
         ar = self.arena
-        slots = [ar.get_compute(h).view(self.Kp, self.R, self.S, self.CS) for h in self.h_slots]
-        w2 = torch.stack(slots, dim=3)   # [Kp][R][S][slot][CS]
-        if self.w2 is None or self.w2.device != w2.device or self.w2.dtype != w2.dtype:
-            self.w2 = torch.empty(self.Kp, self.R, self.S, 4 * self.CS, dtype=w2.dtype, device=w2.device)
-        self.w2.view_as(w2).copy_(w2)
+        comp = ar.compute
+        if self._w2idx is None or self._w2idx.device != comp.device:
+            k, a, b, sl, c = torch.meshgrid(torch.arange(self.Kp), torch.arange(self.R), torch.arange(self.S),
+                                            torch.arange(4), torch.arange(self.CS), indexing="ij")
+            offs = torch.tensor([h[0] for h in self.h_slots])
+            idx = offs[sl] + (((k * self.R + a) * self.S + b) * self.CS + c)
+            self._w2idx = idx.reshape(-1).to(comp.device)
+        if self.w2 is None or self.w2.device != comp.device or self.w2.dtype != comp.dtype:
+            self.w2 = torch.empty(self.Kp, self.R, self.S, 4 * self.CS, dtype=comp.dtype, device=comp.device)
+        ar.backend.gather_(self.w2, comp, self._w2idx)
 
     def prep_input(self, be, x: torch.Tensor) -> Act:
         N, _, H, W = x.shape
@@ -389,7 +403,8 @@ class S2DConvUnit(ConvUnit):
 
     def _wgrad(self, be, dz: Act, x: Act):
         K, R, S, CT = self.K, self.R, self.S, 4 * self.CS
-        g2 = torch.zeros(K * R * S * CT, dtype=torch.float32, device=dz.device)
+        g2 = torch.empty(K * R * S * CT, dtype=be.dt, device=dz.device)
+        be.fill_(g2, 0.0)
         be.conv_wgrad(dz, x, R, S, 1, 0, g2, CT, K)
         if self._gidx is None or self._gidx.device != dz.device:
             # grad[k][r][s][c] <- g2[k][r // 2][s // 2][((r % 2) * 2 + s % 2) * CS + c]
@@ -397,7 +412,7 @@ class S2DConvUnit(ConvUnit):
                                          torch.arange(self.Cin), indexing="ij")
             idx = (((k * R + r // 2) * S + s_ // 2) * CT + ((r % 2) * 2 + s_ % 2) * self.CS + c)
             self._gidx = idx.reshape(-1).to(dz.device)
-        self.arena.grad_flat(self.conv.weight).add_(g2[self._gidx])
+        be.gather_(self.arena.grad_flat(self.conv.weight), g2, self._gidx, accumulate=True)
 
 
 class ConvTUnit:
@@ -422,15 +437,25 @@ class ConvTUnit:
     def bwd(self, be, x: Act, dout: Act, fuse_next=None, bias_part=None):
         """fuse_next (BwdFuse of the BN+ReLU unit that produced x): the data gradient is written
         ReLU-masked with that BN's backward partials -> returns (dx, partials).  bias_part: per-tile
-        column sums of ``dout`` already produced by the GEMM that wrote it ([tiles][Cout] view);
-        the bias gradient is then their sum instead of another pass over ``dout``."""
+        column sums of ``dout`` already produced by the GEMM that wrote it ([tiles][ns][C] partials,
+        row 0 = sum dout, channels [0, Cout) = this up-sampling's slice); the bias gradient is then
+        their column sum (one reduction launch over tiles rows) instead of another pass over ``dout``."""
         ar = self.arena
         with grad_side(be, dout.buf, x.buf, bias_part):
             if self.m.bias is not None:
+                src = dout
                 if bias_part is not None:
-                    ar.grad_flat(self.m.bias).add_(bias_part[:, :self.Cout].sum(0))
+                    T = bias_part.shape[0]
+                    src = Act(bias_part.reshape(T, -1), T, 1, 1, self.Cop)   # ld = ns * C: row 0 per tile
+                if self.Cop == self.Cout:
+                    be.channel_sum(src, ar.grad_flat(self.m.bias))
                 else:
-                    be.channel_sum(dout, ar.grad_flat(self.m.bias))
+                    tmp = torch.empty(self.Cop, dtype=be.dt, device=dout.device)
+                    be.fill_(tmp, 0.0)
+                    be.channel_sum(src, tmp)
+                    if getattr(self, "_kidx", None) is None or self._kidx.device != dout.device:
+                        self._kidx = torch.arange(self.Cout, device=dout.device)
+                    be.gather_(ar.grad_flat(self.m.bias), tmp, self._kidx, accumulate=True)
                 ar.ready(self.m.bias)
             # dW[ci][i][j][co] = sum_pix x[pix][ci] * dout[2p+i, 2q+j][co]: the wgrad of a 2x2/s2 conv
             be.conv_wgrad(x, dout, 2, 2, 2, 0, ar.grad_flat(self.m.weight), self.Cout, self.Cin)
@@ -485,12 +510,14 @@ class EngineModule(nn.Module):
         self._anchor = torch.zeros(0, requires_grad=True)
         # BN-backward reductions fused into the producing dgrad epilogue (DLMPI_FUSE_BN_BWD=0: off)
         self.fuse_bn_bwd = os.environ.get("DLMPI_FUSE_BN_BWD", "1") != "0"
-        self.precision = "bf16"    # "fp32": run the schedules on fp32 torch ops (set before first use)
+        self.precision = "bf16"    # "fp32": fp32 activations / weights in the same kernels (set before first use)
 
     def engine_setup(self, device=None):
         if device is None:
             device = next(self.parameters()).device
         device = torch.device(device)
+        if device.type == "cuda" and device.index is None:   # "cuda" and "cuda:0" are one arena
+            device = torch.device("cuda", torch.cuda.current_device())
         if self._arena is not None and self._arena.device == device and self._arena.valid():
             return self._arena
         self._be = make_backend(device, next(self.parameters()).dtype, self.precision)
@@ -528,12 +555,12 @@ class EngineModule(nn.Module):
         self._arena.refresh()
         if self.training and torch.is_grad_enabled():
             self._arena.attach_grads()
-            if self._arena.ibuf_total:
-                self._arena.ibuf.add_(1)   # every BatchNorm's num_batches_tracked, one launch
+            if self._arena.ibuf_total:   # every BatchNorm's num_batches_tracked, one launch
+                be.add_i64_(self._arena.ibuf, 1)
             return _EngineFn.apply(self, x, self._anchor)
         with torch.no_grad():
             if self.training and self._arena.ibuf_total:
-                self._arena.ibuf.add_(1)
+                be.add_i64_(self._arena.ibuf, 1)
             out, _ = self._engine_forward(x, train=self.training, save=False)
         return out
 

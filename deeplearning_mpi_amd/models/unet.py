@@ -220,7 +220,7 @@ class UNet(EngineModule):
                 # (the next decoder level's, or the bottleneck's, second conv): masked + partials
                 below_ctx = ctx_dec[k + 1][2] if k < 3 else cbb
                 out = up_t.bwd(be, below, dup, fuse_next=spec(below_ctx),
-                               bias_part=cpart[:, 0] if cpart is not None else None)
+                               bias_part=cpart)
                 da, pre = out if fuse else (out, None)
             else:
                 da = Act.empty(below.N, below.H, below.W, below.C, be.act_dtype, below.device)

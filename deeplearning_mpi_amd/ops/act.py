@@ -93,7 +93,8 @@ class Deferred:
 
     def bufs(self):
         """Storage the deferred value is computed from (kept alive across streams by the engine)."""
-        return (self.src.buf,) + ((self.z.buf,) if self.z is not None else ())
+        return (self.src.buf,) + ((self.z.buf,) if self.z is not None else ()) + \
+            tuple(k for k in (self.k0, self.k1) if isinstance(k, torch.Tensor))   # the per-channel coefficients too
 
     def __repr__(self):
         return f"Deferred({self.kind}, {self.src!r})"

@@ -1,7 +1,9 @@
 """Compute backends of the execution engine.
 
 * :class:`NativeBackend` -- the product path: bf16 NHWC activations, every op is one of our
-  gfx950 HIP kernels (``_C``), launched on the current HIP stream (graph-capturable).
+  gfx950 HIP kernels (``_C``), launched on the current HIP stream (graph-capturable).  With
+  ``act_dtype=torch.float32`` the same kernels run instantiated for fp32 storage (fp32 MFMA
+  v_mfma_f32_16x16x4_f32 in the GEMMs): the ``--precision fp32`` path.
 * :class:`RefBackend` -- fp32 torch reference of exactly the same op set and semantics.  It runs
   on CPU (CPU test-suite, gloo multi-process tests) and is the numerics oracle for the kernels.
 
@@ -37,14 +39,19 @@ def _aux_stream(device, C, role):
 
 class NativeBackend:
     name = "native"
-    act_dtype = torch.bfloat16
     dt = torch.float32
 
-    def __init__(self, device):
+    def __init__(self, device, act_dtype=torch.bfloat16):
         from .._ext import native
 
+        if act_dtype not in (torch.bfloat16, torch.float32):
+            raise ValueError(f"native activations are bf16 or fp32, got {act_dtype}")
         self.C = native()
         self.device = torch.device(device)
+        self.act_dtype = act_dtype
+        self.f32 = act_dtype == torch.float32
+        # the GEMM operand prologues (deferred BN passes) are instantiated for bf16 only
+        self.prologue = not self.f32
         self._cast_cache = {}
         self.held = []   # buffers read on the side stream, dropped at the backward's join (engine.grad_side)
         # parameter-gradient work (weight-gradient GEMMs + split reductions, DDP bucket launches)
@@ -82,7 +89,7 @@ class NativeBackend:
         self._branch = s
 
     # ---------------- conv family ----------------
-    prologue = True   # the GEMM kernels consume ops.act.Deferred operands directly
+    prologue = True   # the GEMM kernels consume ops.act.Deferred operands directly (bf16)
 
     @staticmethod
     def _pro(op):
@@ -107,7 +114,7 @@ class NativeBackend:
         return out
 
     def conv_mtiles(self, N, H, W, C, K, R, S, stride, pad, pro=False):
-        return self.C.conv2d_fwd_mtiles_pro(N, H, W, C, K, R, S, stride, pad, 0, int(bool(pro)))
+        return self.C.conv2d_fwd_mtiles_pro(N, H, W, C, K, R, S, stride, pad, 0, int(bool(pro)), int(self.f32))
 
     def conv_fwd(self, x, w, K, R, S, stride, pad, y: Act, bias=None, res: Act = None, scale=None,
                  shift=None, relu=False, stats=None, kvalid=0):
@@ -238,7 +245,7 @@ class NativeBackend:
     def nchw_to_nhwc(self, x: torch.Tensor, Cpad) -> Act:
         N, Cc, H, W = x.shape
         x = x.contiguous().to(self.dt)
-        y = Act.empty(N, H, W, Cpad, torch.bfloat16, x.device)
+        y = Act.empty(N, H, W, Cpad, self.act_dtype, x.device)
         self.C.nchw_to_nhwc(x, N, Cc, H, W, Cpad, y.buf)
         return y
 
@@ -246,7 +253,7 @@ class NativeBackend:
         """2x2 space-to-depth of the zero-padded NCHW image -> [N, U, V, 4*CS] NHWC."""
         N, Cc, H, W = x.shape
         x = x.contiguous().to(self.dt)
-        y = Act.empty(N, U, V, 4 * CS, torch.bfloat16, x.device)
+        y = Act.empty(N, U, V, 4 * CS, self.act_dtype, x.device)
         self.C.s2d_nchw(x, N, Cc, H, W, pad, U, V, CS, y.buf)
         return y
 
@@ -264,17 +271,18 @@ class NativeBackend:
         ent = self._cast_cache.get(key)
         if ent is None or ent[0] is not entries:
             blob = bytearray()
-            base = dst_flat.data_ptr()
+            base, esz = dst_flat.data_ptr(), dst_flat.element_size()
+            assert dst_flat.dtype == self.act_dtype
             bmap = []
             for k, (src, doff, d, v, st) in enumerate(entries):
-                blob += struct.pack("<QQ4i4i4qq", src.data_ptr(), base + 2 * doff, *d, *v, *st, doff)
+                blob += struct.pack("<QQ4i4i4qq", src.data_ptr(), base + esz * doff, *d, *v, *st, doff)
                 # ~one block per 4096 destination elements (one 64x64 tile of the transpose path)
                 nb = max(1, min(1024, -(-d[0] * d[1] * d[2] * d[3] // 4096)))
                 bmap += [(k, j, nb, 0) for j in range(nb)]
             dev = torch.frombuffer(bytearray(blob), dtype=torch.uint8).to(self.device)
             bm = torch.tensor(bmap, dtype=torch.int32).to(self.device)
             self._cast_cache[key] = ent = (entries, dev, bm)
-        self.C.cast_weights(ent[1], ent[2])
+        self.C.cast_weights(ent[1], ent[2], self.f32)
 
     # ---------------- losses / eval ----------------
     def ce_fwd(self, logits, labels):
@@ -324,6 +332,17 @@ class NativeBackend:
 
     def scale_(self, x, coef):
         self.C.scale_(x, coef)
+
+    # ---------------- utilities (per-step glue on our own kernels) ----------------
+    def fill_(self, t, v):
+        self.C.fill_(t, float(v))
+
+    def add_i64_(self, t, v):
+        self.C.add_i64_(t, int(v))
+
+    def gather_(self, dst, src, idx, accumulate=False):
+        """dst.view(-1)[i] (+)= src.view(-1)[idx[i]] (idx < 0: zero)."""
+        self.C.gather_(dst, src, idx, bool(accumulate))
 
 
 # --------------------------------------------------------------------------------------------
@@ -534,6 +553,16 @@ class RefBackend:
         v = dx.nhwc().to(self.dt)
         return torch.stack([v.sum((0, 1, 2)), (v * zz).sum((0, 1, 2))]).unsqueeze(0)
 
+    def outer_dgrad_bn(self, dy: Act, wT, ldw, dx: Act, fuse):
+        """dx[m, c] = dy[m, 0] * wT[c * ldw], ReLU-masked by relu(BN(z)); BN-backward partials."""
+        d = dy.nhwc()[..., :1].to(self.dt)
+        w = wT.reshape(-1)[::ldw][:dx.C].to(self.dt)
+        zz = fuse.z.nhwc().to(self.dt)
+        keep = (zz * fuse.scale + fuse.shift) > 0
+        dx.nhwc().copy_(d * w * keep)
+        v = dx.nhwc().to(self.dt)
+        return torch.stack([v.sum((0, 1, 2)), (v * zz).sum((0, 1, 2))]).unsqueeze(0)
+
     def avgpool_fwd(self, x: Act, y: Act):
         y.nhwc().copy_(x.nhwc().to(self.dt).mean((1, 2), keepdim=True))
 
@@ -640,16 +669,32 @@ class RefBackend:
     def scale_(self, x, coef):
         x.mul_(coef[0])
 
+    def fill_(self, t, v):
+        t.fill_(v)
+
+    def add_i64_(self, t, v):
+        t.add_(v)
+
+    def gather_(self, dst, src, idx, accumulate=False):
+        d, sv = dst.view(-1)[:idx.numel()], src.reshape(-1)
+        v = torch.where(idx >= 0, sv[idx.clamp_min(0)], torch.zeros((), dtype=sv.dtype, device=sv.device))
+        if accumulate:
+            d.add_(v)
+        else:
+            d.copy_(v)
+
 
 def make_backend(device, dtype=torch.float32, precision: str = "bf16") -> "NativeBackend | RefBackend":
-    """GPU + bf16 (default): the native gfx950 kernels.  GPU + ``precision='fp32'``: the same engine
-    schedules on fp32 torch ops (the ``--precision fp32`` option of the apps; a numerics reference,
-    not a fast path).  CPU: the reference backend in the parameters' dtype."""
+    """GPU: the native gfx950 kernels with bf16 activations (default) or, ``precision='fp32'`` (the
+    apps' ``--precision fp32``), the same kernels instantiated for fp32 activations and weights.
+    ``precision='ref'`` on GPU: the torch reference backend in the parameters' dtype (numerics
+    oracle, e.g. fp64 against the fp32 kernels).  CPU: the
+    reference backend in the parameters' dtype."""
     device = torch.device(device)
     if device.type == "cuda":
-        if precision == "fp32":
-            return RefBackend(device, torch.float32)
-        if precision != "bf16":
+        if precision == "ref":
+            return RefBackend(device, dtype)
+        if precision not in ("bf16", "fp32"):
             raise ValueError(f"precision must be bf16 or fp32, got {precision!r}")
-        return NativeBackend(device)
+        return NativeBackend(device, torch.float32 if precision == "fp32" else torch.bfloat16)
     return RefBackend(device, dtype)

@@ -12,6 +12,17 @@ import torch.nn as nn
 from .backend import make_backend
 
 _BE = {}
+_ONES = {}
+
+
+def backward(loss: torch.Tensor):
+    """``loss.backward()`` with a cached unit seed gradient (autograd's own seed is an ATen fill
+    launch every step; with this the training step launches our kernels only)."""
+    key = (loss.device, loss.dtype)
+    one = _ONES.get(key)
+    if one is None:
+        one = _ONES[key] = torch.ones((), dtype=loss.dtype, device=loss.device)
+    loss.backward(one)
 
 
 def _be(device, dtype=None):

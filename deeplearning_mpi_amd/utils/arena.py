@@ -172,10 +172,15 @@ class ParamArena:
                                               self.offsets[i])
                 dropped = True
         if dropped:
-            self.grad.zero_()
+            self.zero_grad()
 
     def zero_grad(self):
-        self.grad.zero_()
+        """One launch of our fill kernel (reference backend / non-fp32: torch)."""
+        be = self.backend
+        if be is not None and hasattr(be, "fill_") and self.grad.dtype == torch.float32:
+            be.fill_(self.grad, 0.0)
+        else:
+            self.grad.zero_()
 
     def ready(self, *ps):
         if self.hook is not None:

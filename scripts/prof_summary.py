@@ -41,11 +41,16 @@ def main():
     ap.add_argument("--steps", type=float, default=1.0)
     ap.add_argument("--top", type=int, default=25)
     ap.add_argument("--window", type=float, default=None, help="(db) keep dispatches of the last N seconds")
+    ap.add_argument("--step-kernel", default=None,
+                    help="count training steps as the calls of this once-per-step kernel (overrides --steps)")
     a = ap.parse_args()
     if a.path.endswith(".db"):
         rows = rows_from_db(a.path, a.window)
     else:
         rows = list(csv.DictReader(open(a.path)))
+    if a.step_kernel:
+        a.steps = float(sum(int(r["Calls"]) for r in rows if short(r["Name"]).startswith(a.step_kernel)))
+        print(f"steps in window: {a.steps:.0f} (calls of {a.step_kernel})\n")
     tot = sum(float(r["TotalDurationNs"]) for r in rows)
     print("| kernel | calls/step | ms/step | % |\n|---|---:|---:|---:|")
     for r in sorted(rows, key=lambda r: -float(r["TotalDurationNs"]))[:a.top]:
