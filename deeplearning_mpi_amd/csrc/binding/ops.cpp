@@ -123,6 +123,19 @@ static void pick_tiles(int64_t M, int Kout, int64_t red, int cin, int& bm, int& 
     bm = bn = 256;
     return;
   }
+  // DLMPI_CONV_WIDE=<max reduction>: 128 x 256 tiles of 8 waves for short reductions into
+  // 256-multiple outputs (each input row read once, every output row written whole by one block).
+  // Off by default: measured 15-25 % SLOWER than 128 x 128 on the ResNet-50 expand / reduce 1x1
+  // shapes and -6 % on the bench (profiles/r2_wide_rejected).
+  static const int wide = [] {
+    const char* e = getenv("DLMPI_CONV_WIDE");
+    return e ? atoi(e) : 0;
+  }();
+  if (!pro && wide > 0 && Kout % 256 == 0 && red <= wide && cin % 64 == 0 && (M + 127) / 128 >= 256) {
+    bm = 128;
+    bn = 256;
+    return;
+  }
   const int64_t nt = (Kout + bn - 1) / bn;
   const int64_t tiles = ((M + 127) / 128) * nt;
   static const int n64 = [] {

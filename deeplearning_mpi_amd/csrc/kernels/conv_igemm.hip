@@ -621,6 +621,9 @@ extern "C" hipError_t dlmpi_conv_igemm(const ConvArgs* a_in, int bm, int bn, hip
     else if (a->pro == 2) hipLaunchKernelGGL((conv_igemm_kernel<256, 64, false, 1, 4, 4, 2>), grid, dim3(256), 0, s, *a);
     else if (a->C < 64) hipLaunchKernelGGL((conv_igemm_kernel<256, 64, true, 1, 4, 4>), grid, dim3(256), 0, s, *a);
     else hipLaunchKernelGGL((conv_igemm_kernel<256, 64, false, 1, 4, 4>), grid, dim3(256), 0, s, *a);
+  } else if (bm == 128 && bn == 256) {   // short reductions, wide outputs: 8 waves (2 x 4 of 64 x 64)
+    if (a->C < 64 || a->pro != 0) return hipErrorInvalidValue;
+    hipLaunchKernelGGL((conv_igemm_kernel<128, 256, false, 1, 8, 2>), grid, dim3(512), 0, s, *a);
   } else if (bm == 256 && bn == 128) launch_tile<256, 128>(a, grid, s);
   else if (bm == 128 && bn == 128) launch_tile<128, 128>(a, grid, s);
   else if (bm == 128 && bn == 64) launch_tile<128, 64>(a, grid, s);

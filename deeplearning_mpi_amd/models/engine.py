@@ -107,6 +107,7 @@ _OUTER_DGRAD = os.environ.get("DLMPI_OUTER_DGRAD", "1") != "0"
 # costs more than the single elementwise pass it removes.
 DEFER_BN_FWD = os.environ.get("DLMPI_DEFER_BN_FWD", "0") != "0"
 DEFER_BN_BWD = os.environ.get("DLMPI_DEFER_BN_BWD", "0") != "0"
+DEFER_BN_WGRAD = os.environ.get("DLMPI_DEFER_BN_WGRAD", "1") != "0"
 
 
 def bufs(*objs):
@@ -194,9 +195,11 @@ class ConvUnit:
         self.arena.backend.gather_(self._bias_pad, self.bias.data, self._bias_idx)   # one launch of ours
         return self._bias_pad
 
-    def fwd(self, be, x, train: bool, res: Act = None, out: Act = None, save=True, defer_apply=False):
+    def fwd(self, be, x, train: bool, res: Act = None, out: Act = None, save=True, defer_apply=False,
+            before_res=None):
         """Returns (output, saved context).  x: an Act or a Deferred operand (rebuilt by the GEMM's
-        operand prologue).  defer_apply (training BN + ReLU, no residual): skip the BN-apply + ReLU;
+        operand prologue).  before_res: called right before the first kernel that reads ``res`` (a
+        residual produced on another stream is joined there, after this unit's GEMM).  defer_apply (training BN + ReLU, no residual): skip the BN-apply + ReLU;
         True returns the BN input z -- the consumer applies scale/shift (ctx[5:7]) itself (the ResNet
         stem's max-pool) --, "act" returns Deferred.affine(z, scale, shift) for the next
         convolution.  Either way the BN output is never materialised."""
@@ -210,7 +213,8 @@ class ConvUnit:
             out if out is not None else Act.empty(N, P, Q, self.Kp, be.act_dtype, dev))
         bn = self.bn
         if bn is None:
-            assert not self.relu or res is None or True
+            if before_res is not None and res is not None:
+                before_res()
             be.conv_fwd(x, wf, self.Kp, self.R, self.S, self.stride, self.pad, y, bias=self._bias_vec(), res=res,
                         relu=self.relu, kvalid=y.C if y.C < self.Kp else 0)
             return y, ((x, y) if save else None)
@@ -239,9 +243,13 @@ class ConvUnit:
             mbits = None
             if save and res is not None and self.relu and self.Kp % 8 == 0:
                 mbits = torch.empty(y.rows, self.Kp // 8, dtype=torch.uint8, device=dev)
+            if before_res is not None and res is not None:
+                before_res()
             be.bn_apply(z, scale, shift, res, self.relu, y, mbits=mbits)
             return y, ((x, z, y, mean, invstd, scale, shift, res is not None, mbits) if save else None)
         # eval: fold BN (and conv bias) into the GEMM epilogue
+        if before_res is not None and res is not None:
+            before_res()
         invstd = torch.rsqrt(bn.running_var + bn.eps)
         scale = bn.weight.data * invstd if bn.affine else invstd
         shift = (bn.bias.data if bn.affine else 0.0) - bn.running_mean * scale
@@ -261,7 +269,7 @@ class ConvUnit:
         return BwdFuse(None, z, None, scale, shift)
 
     def bwd(self, be, ctx, dy: Act, need_dx=True, dx_res: Act = None, dyr_out: Act = None, ymask: Act = None,
-            use_own_mask=True, pre=None, k2=1, fuse_next=None, colsum=False):
+            use_own_mask=True, pre=None, k2=1, fuse_next=None, colsum=False, before_res=None):
         """Backward of the unit.
 
         pre:       BN-backward partials already produced by the dgrad epilogue that wrote ``dy``
@@ -270,6 +278,8 @@ class ConvUnit:
                    emits that consumer's partials; returns (dx, partials) instead of dx.
         colsum:    (without fuse_next) the dgrad epilogue also emits per-tile column sums of dx;
                    returns (dx, partials [tiles][2][C]).
+        before_res: called right before the data-gradient GEMM that adds ``dx_res`` (a residual
+                   gradient produced on another stream is joined there, after this unit's BN backward).
         """
         ar = self.arena
         bn = self.bn
@@ -282,7 +292,11 @@ class ConvUnit:
             gam = bn.weight.data if bn.affine else None
             dgam = ar.grad_flat(bn.weight) if bn.affine else None
             dbet = ar.grad_flat(bn.bias) if bn.affine else None
-            if pre is not None and mask is None and dyr_out is None and DEFER_BN_BWD:
+            # deferred: always with DLMPI_DEFER_BN_BWD; by default also when the weight gradient is
+            # dz's only consumer (need_dx False: the ResNet stem, the UNet input conv) -- then the
+            # BN-backward apply pass (read dy, z; write dz) is replaced by the wgrad reading dy and z
+            defer = DEFER_BN_BWD or (not need_dx and DEFER_BN_WGRAD and getattr(be, "prologue", False))
+            if pre is not None and mask is None and dyr_out is None and defer:
                 # finalize only: dz = k1 dy + k2 z + k3 is rebuilt inside the wgrad / dgrad GEMMs
                 dz = be.bn_bwd_deferred(dy, z, mean, invstd, gam, dgam, dbet, pre=pre, k2=k2)
             else:
@@ -316,6 +330,8 @@ class ConvUnit:
                 ar.ready(self.conv.weight)
         if not need_dx:
             return None
+        if before_res is not None:
+            before_res()
         dx = Act.empty(x.N, x.H, x.W, self.Cp, be.act_dtype, x.device)
         if (self.K == 1 and self.R == 1 and self.S == 1 and self.stride == 1 and dx_res is None and not colsum
                 and fuse_next is not None and fuse_next.scale is not None and fuse_next.z2 is None

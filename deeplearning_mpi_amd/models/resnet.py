@@ -86,6 +86,11 @@ class Bottleneck(nn.Module):
         return u, ud
 
 
+# DLMPI_LATE_JOIN=0: join the downsample branch stream before the last unit's GEMM (forward) /
+# before conv1's BN backward (backward) instead of right before the residual is read (A/B knob)
+_LATE_JOIN = os.environ.get("DLMPI_LATE_JOIN", "1") != "0"
+
+
 class _BlockExec:
     """Forward/backward schedule of one residual block (basic or bottleneck)."""
 
@@ -109,14 +114,19 @@ class _BlockExec:
         for k, u in enumerate(self.u[:-1]):
             h, c = u.fwd(be, h, train, save=save, defer_apply="act" if defer else False)
             ctxs.append(c)
+        join = None
         if br is not None:
-            main.wait_stream(br)
-            record_on(main, idn, cd)
+            def join():   # the residual is first read by the last unit's BN-apply, after its GEMM
+                main.wait_stream(br)
+                record_on(main, idn, cd)
+            if not _LATE_JOIN:
+                join()
+                join = None
         elif self.ud is not None:
             idn, cd = self.ud.fwd(be, x, train, save=save)
         else:
             idn, cd = x, None
-        y, c = self.u[-1].fwd(be, h, train, res=idn, save=save)
+        y, c = self.u[-1].fwd(be, h, train, res=idn, save=save, before_res=join)
         ctxs.append(c)
         return y, (ctxs, cd)
 
@@ -148,14 +158,19 @@ class _BlockExec:
             dh, part = self.u[-1].bwd(be, ctxs[-1], dy, pre=pre, k2=1, fuse_next=spec(n - 2))
             for k in range(n - 2, 0, -1):
                 dh, part = self.u[k].bwd(be, ctxs[k], dh, pre=part, fuse_next=spec(k - 1))
+            join = None
             if br is not None:
-                main.wait_stream(br)
-                record_on(main, dres)
+                def join():   # dres is first read by conv1's data-gradient GEMM, after its BN backward
+                    main.wait_stream(br)
+                    record_on(main, dres)
+                if not _LATE_JOIN:
+                    join()
+                    join = None
             elif self.ud is not None:
                 dres = self.ud.bwd(be, cd, dy, pre=pre, k2=2)
             else:
                 dres = dy
-            return self.u[0].bwd(be, ctxs[0], dh, dx_res=dres, pre=part, fuse_next=fuse_prev)
+            return self.u[0].bwd(be, ctxs[0], dh, dx_res=dres, pre=part, fuse_next=fuse_prev, before_res=join)
         # fused BN-backward partials for the inner units also when the block's output gradient comes
         # without them (the last block, behind the average-pool backward); required when their BN +
         # ReLU output was deferred (never stored: ctx y is None), so the mask is recomputed from z

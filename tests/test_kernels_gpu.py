@@ -122,6 +122,60 @@ def test_conv_fwd_256_row_tile(shape, bn):
     assert _rel(st.sum(0), str_.sum(0)) < 2e-2
 
 
+@pytest.mark.parametrize("shape", [(2, 20, 20, 64, 256, 1, 1, 0), (3, 9, 11, 128, 512, 1, 1, 0),
+                                   (2, 16, 16, 256, 256, 3, 2, 1), (2, 17, 19, 64, 768, 3, 1, 1)])
+def test_conv_fwd_128x256_wide_tile(shape):
+    """The 8-wave 128x256 tile (chosen for short reductions into 256-multiple outputs) forced on
+    small shapes: forward with BN partials, row remainders, 3x3 / strided taps."""
+    nb, rb = _be()
+    N, H, W, Cin, K, R, s, p = shape
+    Cp, Kp = pad8(Cin), pad8(K)
+    P, Q = (H + 2 * p - R) // s + 1, (W + 2 * p - R) // s + 1
+    x, xr = _act(N, H, W, Cp)
+    w = (torch.randn(Kp, R, R, Cp, device=DEV) / (R * R * Cin) ** 0.5).to(torch.bfloat16)
+    res, resr = _act(N, P, Q, Kp)
+    y = _empty(N, P, Q, Kp)
+    yr = _empty(N, P, Q, Kp, torch.float32)
+    mt = (N * P * Q + 127) // 128
+    st = torch.empty(mt, 2, Kp, device=DEV)
+    rows = nb.C.conv2d_fwd(x.buf, N, H, W, Cp, Cp, 0, w, Kp, R, R, s, p, y.buf, Kp, 0, None, None, 0, 0, None, None,
+                           False, st, 128, 0, 256)
+    assert rows == mt
+    str_ = torch.empty(1, 2, Kp, device=DEV)
+    rb.conv_fwd(xr, w.float(), Kp, R, R, s, p, yr, stats=str_)
+    torch.cuda.synchronize()
+    assert _rel(y.buf, yr.buf) < 1e-2
+    assert _rel(st.sum(0), str_.sum(0)) < 2e-2
+    # residual + affine + relu epilogue through the same tile
+    sc, sh = torch.rand(Kp, device=DEV) + 0.5, torch.randn(Kp, device=DEV)
+    nb.C.conv2d_fwd(x.buf, N, H, W, Cp, Cp, 0, w, Kp, R, R, s, p, y.buf, Kp, 0, None, res.buf, Kp, 0, sc, sh,
+                    True, None, 128, 0, 256)
+    rb.conv_fwd(xr, w.float(), Kp, R, R, s, p, yr, res=resr, scale=sc, shift=sh, relu=True)
+    torch.cuda.synchronize()
+    assert _rel(y.buf, yr.buf) < 1e-2
+
+
+def test_wide_tile_bit_identical_to_128x128():
+    """At a bench shape (ResNet-50 layer-1 expand, 16 images) the 128x256 tile and the default
+    128x128 tile give bit-identical outputs (same per-element K order) and equal BN partial sums
+    up to fp32 summation order."""
+    nb, rb = _be()
+    N, H, W, C, K = 16, 56, 56, 64, 256
+    x, xr = _act(N, H, W, C)
+    w = (torch.randn(K, 1, 1, C, device=DEV) / C ** 0.5).to(torch.bfloat16)
+    ys, sts = [], []
+    for bn in (256, 128):
+        y = _empty(N, H, W, K)
+        st = torch.empty((N * H * W + 127) // 128, 2, K, device=DEV)
+        nb.C.conv2d_fwd(x.buf, N, H, W, C, C, 0, w, K, 1, 1, 1, 0, y.buf, K, 0, None, None, 0, 0, None, None,
+                        False, st, 128, 0, bn)
+        ys.append(y.buf)
+        sts.append(st)
+    torch.cuda.synchronize()
+    assert torch.equal(ys[0], ys[1])
+    assert torch.allclose(sts[0].double().sum(0), sts[1].double().sum(0), rtol=1e-5, atol=1e-2)
+
+
 @pytest.mark.parametrize("shape", [CONV_SHAPES[1], CONV_SHAPES[2], CONV_SHAPES[3], CONV_SHAPES[5]])
 @pytest.mark.parametrize("mode", ["mask", "two", "from_z", "bits"])
 def test_conv_dgrad_fused_bn_backward(shape, mode):
