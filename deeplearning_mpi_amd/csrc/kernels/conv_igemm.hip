@@ -50,7 +50,11 @@ __device__ __forceinline__ void glds16(const void* g, char* lds_wave_base) {
 // T: storage type of activations and weights -- uint16_t (bf16, v_mfma_f32_16x16x32_bf16) or float
 // (the fp32 precision path: v_mfma_f32_16x16x4_f32, four per 16-byte fragment; the LDS tile keeps
 // its 128-byte rows, i.e. 32 fp32 reduction elements per K-step instead of 64 bf16).
-template <int BM, int BN, bool SMALLC, int STAGES, int NW, int WGM, int PRO = 0, typename ET = uint16_t>
+// SKM: stream-K work decomposition (ConvArgs::sk_*): a persistent grid walks the flattened
+// (phase, tile, K-step) iterations; tiles split between blocks are summed by their last-arriving
+// contributor in a fixed block order (deterministic), exactly like the split-K combine.
+template <int BM, int BN, bool SMALLC, int STAGES, int NW, int WGM, int PRO = 0, typename ET = uint16_t,
+          bool SKM = false>
 __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(STAGES == 1 && BM * BN <= 16384 ? (BM * BN == 16384 ? DLMPI_W128 : 3) : 2, 8))) void conv_igemm_kernel(const ConvArgs a) {
   constexpr int NT = 64 * NW;                 // threads
   constexpr int WGN = NW / WGM;               // wave grid WGM x WGN
@@ -77,21 +81,46 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(STAGES 
   constexpr int SMEM = SMEM0 > RED_BYTES ? SMEM0 : RED_BYTES;
   __shared__ __attribute__((aligned(16))) char smem[SMEM];
 
-  const ConvPhase ph = a.ph[blockIdx.z];
-  const uint32_t nwg = (uint32_t)ph.mtiles * (uint32_t)a.ntiles;
-  if (blockIdx.x >= nwg) return;
-  const uint32_t bid = xcd_remap(blockIdx.x, nwg);
-  const int mt = bid / a.ntiles, nt = bid - mt * a.ntiles;
-  const int m0 = mt * BM, n0 = nt * BN;
-  const int PQ = ph.P * ph.Q;
-  const int M = a.Nimg * PQ;
-
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wid / WGN, wn = wid % WGN;
   const int lrow = tid >> 3;                          // staging row (+RP i)
   const int jc = (tid & 7) ^ ((tid >> 4) & 7);        // swizzled 16-B chunk this lane fetches
   const char* zp = reinterpret_cast<const char*>(g_zero_page);
+
+  // stream-K: this block's iteration range (XCD-remapped so one XCD walks a contiguous range)
+  int sk_lb = 0, sk_it = 0, sk_end = 0;
+  if constexpr (SKM) {
+    sk_lb = (int)xcd_remap(blockIdx.x, gridDim.x);
+    sk_it = sk_lb * a.sk_per;
+    sk_end = min(a.sk_total, sk_it + a.sk_per);
+  }
+  for (;;) {   // SKM: one pass per tile segment of the range; otherwise exactly one pass
+  int zph, seg_k0 = 0, seg_k1 = 0, seg_start = 0;
+  uint32_t bid;
+  if constexpr (SKM) {
+    if (sk_it >= sk_end) break;
+    zph = 0;
+    while (zph + 1 < a.nphase && sk_it >= a.sk_base[zph + 1]) ++zph;
+    const int nkz = a.ph[zph].ksteps;
+    const int loc = sk_it - a.sk_base[zph];
+    const int tl = loc / nkz;
+    seg_k0 = loc - tl * nkz;
+    seg_k1 = min(nkz, seg_k0 + (sk_end - sk_it));
+    seg_start = sk_it;
+    sk_it += seg_k1 - seg_k0;
+    bid = (uint32_t)tl;
+  } else {
+    zph = blockIdx.z;
+    const uint32_t nwg0 = (uint32_t)a.ph[zph].mtiles * (uint32_t)a.ntiles;
+    if (blockIdx.x >= nwg0) return;
+    bid = xcd_remap(blockIdx.x, nwg0);
+  }
+  const ConvPhase ph = a.ph[zph];
+  const int mt = bid / a.ntiles, nt = bid - mt * a.ntiles;
+  const int m0 = mt * BM, n0 = nt * BN;
+  const int PQ = ph.P * ph.Q;
+  const int M = a.Nimg * PQ;
 
   // ---- per-thread row state (kept compact: the 256-row tile has 8 rows per thread) ----------
   int a_hw[AL], a_pix[AL];                            // (h << 16) | w of the row's input origin
@@ -265,7 +294,10 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(STAGES 
   };
   // split-K (small grids): block y of a.splitk reduces K-steps [kbeg, kend)
   int kbeg = 0, kend = nk;
-  if (a.splitk > 1) {
+  if constexpr (SKM) {
+    kbeg = seg_k0;
+    kend = seg_k1;
+  } else if (a.splitk > 1) {
     const int per = (nk + a.splitk - 1) / a.splitk;
     kbeg = min(nk, (int)blockIdx.y * per);
     kend = min(nk, kbeg + per);
@@ -337,7 +369,46 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(STAGES 
   // Every slice stores its fp32 accumulators (fragment layout) to its slab, publishes with an
   // agent-scope release + ticket; the tile's last arriver acquires and sums ALL slices' slabs in
   // slice order (deterministic whichever block arrives last), then runs the normal epilogue.
-  if (a.splitk > 1) {
+  if constexpr (SKM) {
+    if (kbeg != 0 || kend != nk) {
+      // partial tile: store this block's accumulators write-through (sc1) into its slab slot
+      // (0: the range's first segment, 1: its last), take a ticket; the last contributor sums the
+      // slots of every contributing block in block order (deterministic) and runs the epilogue
+      constexpr int NF = TM * TN;
+      const int slot = seg_start == sk_lb * a.sk_per ? 0 : 1;
+      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+          a.sk_slab + (int64_t)(sk_lb * 2 + slot) * NF * NT * 4, (short)0, NF * NT * 16, 0x00020000);
+#pragma unroll
+      for (int i = 0; i < NF; ++i)
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[i / TN][i % TN]), rs,
+                                               (i * NT + tid) * 16, 0, 16 /* sc1 */);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      const int s_it = a.sk_base[zph] + (int)bid * nk;       // the tile's iteration range [s_it, s_it + nk)
+      const int b_lo = s_it / a.sk_per, b_hi = (s_it + nk - 1) / a.sk_per;
+      const int gt = a.sk_tbase[zph] + (int)bid;
+      int* flag = reinterpret_cast<int*>(smem);
+      if (tid == 0)
+        flag[0] = __hip_atomic_fetch_add(a.sk_tk + gt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == b_hi - b_lo;
+      __syncthreads();
+      if (!flag[0]) continue;
+      if (tid == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __hip_atomic_store(a.sk_tk + gt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      __syncthreads();
+#pragma unroll
+      for (int i = 0; i < NF; ++i) acc[i / TN][i % TN] = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int b = b_lo; b <= b_hi; ++b) {
+        const int sl = b * a.sk_per >= s_it ? 0 : 1;
+        const f32x4* src = reinterpret_cast<const f32x4*>(a.sk_slab) + (int64_t)(b * 2 + sl) * NF * NT + tid;
+#pragma unroll
+        for (int i = 0; i < NF; ++i) acc[i / TN][i % TN] += src[(int64_t)i * NT];
+      }
+      __syncthreads();   // flag (LDS) is reused by the epilogue staging
+    }
+  } else if (a.splitk > 1) {
     constexpr int NF = TM * TN;
     const int S = a.splitk;
     // unique over phases (blockIdx.z): ConvTranspose phases all have tile_base 0
@@ -518,6 +589,9 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(STAGES 
       if (ns > 2) st[2 * a.Kout] = t3;
     }
   }
+  if constexpr (!SKM) break;
+  __syncthreads();   // LDS (epilogue staging / stats) is reused by the next segment's staging
+  }   // segment loop
 }
 
 }  // namespace dlmpi
@@ -568,6 +642,50 @@ static int splitk_plan(int tiles, int nk) {
   return S < 2 ? 1 : S;
 }
 
+// ---- stream-K planning --------------------------------------------------------------------------
+// A launch of T tiles on a chip holding `slots` resident blocks takes ceil(T / slots) tile-times; at
+// ResNet-50 bs 256 many layers sit just above a multiple (784 tiles of 14^2 x 256 channels on 768
+// slots: 2 tile-times for 1.02 tiles of work each, measured +48 % vs 248 images).  Stream-K runs
+// exactly `slots` persistent blocks over the flattened (tile, K-step) iterations instead; a tile cut
+// between two blocks costs one slab round trip + a ticket (sk_time below: + 0.15 tile-times).
+static int cu_count() {
+  static const int n = [] {
+    int d = 0, v = 0;
+    if (hipGetDevice(&d) != hipSuccess || hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, d) != hipSuccess)
+      v = 256;
+    return v > 0 ? v : 256;
+  }();
+  return n;
+}
+
+template <int BM, int BN>
+static int sk_occupancy() {   // resident blocks per CU of the stream-K instance
+  static const int occ = [] {
+    int n = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, conv_igemm_kernel<BM, BN, false, 1, 4, 2, 0, uint16_t, true>,
+                                                     256, 0) != hipSuccess || n < 1)
+      n = 2;
+    return n;
+  }();
+  return occ;
+}
+
+static int g_sk_override = -1;   // dlmpi_set_conv_sk (tests); -1: the environment decides
+static int g_sk_last = 0;        // 1 if the last conv launch ran stream-K (tests)
+// DLMPI_CONV_SK: 0 off (default), 1 auto, 2 whenever applicable (tests).  Measured slower on every
+// targeted ResNet-50 shape (profiles/r2_streamk_rejected): with ~1 iteration range per tile almost
+// every tile is cut, and the 64 KB fp32 partials per cut tile cost more than the wave tail saved.
+static int sk_mode_env() {
+  static const int v = [] {
+    const char* e = getenv("DLMPI_CONV_SK");
+    return e ? atoi(e) : 0;
+  }();
+  return g_sk_override >= 0 ? g_sk_override : v;
+}
+
+extern "C" void dlmpi_set_conv_sk(int mode) { g_sk_override = mode; }
+extern "C" int dlmpi_conv_sk_last() { return g_sk_last; }
+
 // fp32 precision path: single-stage 4-wave tiles up to 128 x 128 (the f32 MFMA is 1/16 of the
 // bf16 rate, so the wider bf16 tiles buy nothing here)
 static hipError_t launch_f32(const ConvArgs* a, int bm, int bn, dim3 grid, hipStream_t s) {
@@ -598,6 +716,7 @@ extern "C" hipError_t dlmpi_conv_igemm(const ConvArgs* a_in, int bm, int bn, hip
   ConvArgs ab = *a_in;
   const ConvArgs* a = &ab;
   ab.splitk = 1;
+  g_sk_last = 0;
   const int S = splitk_plan(tiles, maxk);
   if (S > 1) {
     const int ntile_ids = maxt * a_in->ntiles * a_in->nphase;   // kernel: z * gridDim.x + mt * ntiles + nt
@@ -612,6 +731,63 @@ extern "C" hipError_t dlmpi_conv_igemm(const ConvArgs* a_in, int bm, int bn, hip
   dim3 grid((unsigned)(maxt * a->ntiles), (unsigned)ab.splitk, (unsigned)a->nphase);
   if (grid.x == 0) return hipSuccess;
   if (a->f32) return launch_f32(a, bm, bn, grid, s);
+  // stream-K: regular channel counts, no prologue, the single-stage 4-wave tiles
+  const int skm = sk_mode_env();
+  const bool sk_tile = (bm == 128 && (bn == 128 || bn == 64)) || (bm == 64 && (bn == 128 || bn == 64)) ||
+                       (bm == 256 && bn == 128);
+  bool kzero = false;
+  int iters = 0;
+  for (int i = 0; i < a_in->nphase; ++i) {
+    kzero |= a_in->ph[i].ksteps == 0;
+    iters += a_in->ph[i].mtiles * a_in->ntiles * a_in->ph[i].ksteps;
+  }
+  if (skm && ab.splitk == 1 && sk_tile && a->pro == 0 && a->C >= 64 && stages_choice() == 1 && !kzero &&
+      tiles <= 4096 && iters > 0) {
+    int occ = 2;
+    if (bm == 128 && bn == 128) occ = sk_occupancy<128, 128>();
+    else if (bm == 128) occ = sk_occupancy<128, 64>();
+    else if (bm == 64 && bn == 128) occ = sk_occupancy<64, 128>();
+    else if (bm == 64) occ = sk_occupancy<64, 64>();
+    else occ = sk_occupancy<256, 128>();
+    const int slots = cu_count() * occ;
+    const int G = tiles < slots ? (tiles * 2 < slots ? 0 : slots) : slots;   // < half a wave: leave it
+    if (G > 0) {
+      const int per = (iters + G - 1) / G;
+      const double now = (double)((tiles + slots - 1) / slots);
+      const double sk = (double)per * tiles / iters + 0.15;
+      if (skm == 2 || sk < 0.85 * now) {
+        const int Ge = (iters + per - 1) / per;
+        float* slab = dlmpi_splitk_slab(s, (size_t)Ge * 2 * bm * bn);
+        int* tk = dlmpi_splitk_tickets(s, tiles);
+        if (slab && tk) {
+          ab.sk_mode = 1;
+          ab.sk_per = per;
+          ab.sk_total = iters;
+          ab.sk_slab = slab;
+          ab.sk_tk = tk;
+          int it = 0, tb = 0;
+          for (int i = 0; i < a_in->nphase; ++i) {
+            ab.sk_base[i] = it;
+            ab.sk_tbase[i] = tb;
+            it += a_in->ph[i].mtiles * a_in->ntiles * a_in->ph[i].ksteps;
+            tb += a_in->ph[i].mtiles * a_in->ntiles;
+          }
+          ab.sk_base[a_in->nphase] = it;
+          const dim3 g((unsigned)Ge, 1, 1);
+#define DLMPI_SK(BM_, BN_) \
+  hipLaunchKernelGGL((conv_igemm_kernel<BM_, BN_, false, 1, 4, 2, 0, uint16_t, true>), g, dim3(256), 0, s, *a)
+          if (bm == 128 && bn == 128) DLMPI_SK(128, 128);
+          else if (bm == 128) DLMPI_SK(128, 64);
+          else if (bm == 64 && bn == 128) DLMPI_SK(64, 128);
+          else if (bm == 64) DLMPI_SK(64, 64);
+          else DLMPI_SK(256, 128);
+#undef DLMPI_SK
+          g_sk_last = 1;
+          return hipGetLastError();
+        }
+      }
+    }
+  }
   if (a->pro != 0 && (a->C < 64 || a->C % 64 != 0 || (bm == 256 && bn == 256))) return hipErrorInvalidValue;
   if (bm == 256 && bn == 256) {   // 8 waves, double-buffered; regular channel counts only
     if (a->C < 64) return hipErrorInvalidValue;

@@ -83,6 +83,13 @@ struct ConvArgs {
   int splitk;                      // > 1: K split over blockIdx.y, last-arriver combine (set by the launcher)
   float* sk_slab;                  // [tile][slice][TM*TN][threads] f32x4 fragment slabs
   int* sk_tk;                      // [tile] self-resetting arrival tickets
+  // stream-K (set by the launcher): gridDim.x persistent blocks, block lb (XCD-remapped) runs the
+  // flattened (phase, tile, K-step) iterations [lb * sk_per, min(sk_total, (lb + 1) * sk_per)); a tile
+  // split between blocks is combined by its last-arriving contributor from per-block slab slots
+  int sk_mode;                     // 0: one tile (or split) per block, 1: stream-K
+  int sk_per, sk_total;
+  int sk_base[5];                  // first iteration of each phase (sk_base[nphase] = total)
+  int sk_tbase[4];                 // first global tile index of each phase (tickets)
   int cstep, tstep;                // K-iteration: c += cstep, t += tstep per 64-wide step
   // Operand prologue (regular channel counts, single-stage kernels): every staged A piece of an
   // in-image tap is rewritten in LDS before the MFMAs (out-of-image taps stay zero):
@@ -138,6 +145,10 @@ struct WgradArgs {
 extern "C" {
 // conv / gemm
 hipError_t dlmpi_conv_igemm(const dlmpi::ConvArgs* a, int bm, int bn, hipStream_t s);
+// stream-K mode override (-1: DLMPI_CONV_SK decides; 0 off, 1 auto, 2 whenever applicable) and
+// whether the last conv launch used it
+void dlmpi_set_conv_sk(int mode);
+int dlmpi_conv_sk_last();
 hipError_t dlmpi_conv_wgrad(const dlmpi::WgradArgs* a, int bm, int bn, hipStream_t s);   // bn: 128 | 256
 // sum of split partials -> grad (accumulated), with channel un-padding and row limit
 hipError_t dlmpi_wgrad_reduce(const float* ws, int splits, int Ko, int T, int Cpad, int Creal,

@@ -176,6 +176,48 @@ def test_wide_tile_bit_identical_to_128x128():
     assert torch.allclose(sts[0].double().sum(0), sts[1].double().sum(0), rtol=1e-5, atol=1e-2)
 
 
+SK_SHAPES = [(256, 14, 14, 1024, 256, 1, 1, 0), (256, 14, 14, 256, 256, 3, 1, 1), (256, 28, 28, 512, 128, 1, 1, 0),
+             (256, 7, 7, 512, 2048, 1, 1, 0), (128, 14, 14, 256, 256, 3, 2, 1), (256, 28, 28, 256, 512, 1, 2, 0)]
+
+
+@pytest.mark.parametrize("shape", SK_SHAPES, ids=lambda s: "x".join(map(str, s)))
+def test_stream_k_conv_matches_tile_per_block(shape):
+    """Stream-K (persistent blocks over the flattened (phase, tile, K-step) iterations, tiles cut
+    between blocks combined by the last contributor) forced on: forward with BN partials and the
+    data gradient (incl. stride-2 sub-pixel phases) against the one-tile-per-block launch, and
+    bit-reproducible from run to run."""
+    nb, _ = _be()
+    N, H, W, Cin, K, R, s, p = shape
+    Cp, Kp = pad8(Cin), pad8(K)
+    P, Q = (H + 2 * p - R) // s + 1, (W + 2 * p - R) // s + 1
+    torch.manual_seed(3)
+    x, _ = _act(N, H, W, Cp)
+    w = (torch.randn(Kp, R, R, Cp, device=DEV) / (R * R * Cin) ** 0.5).to(torch.bfloat16)
+    dy, _ = _act(N, P, Q, Kp)
+    wT = w.permute(3, 1, 2, 0).contiguous()
+    out = {}
+    try:
+        for mode in (0, 2, 2):
+            nb.C.set_conv_sk(mode)
+            y = _empty(N, P, Q, Kp)
+            st = torch.zeros(nb.conv_mtiles(N, H, W, Cp, Kp, R, R, s, p), 2, Kp, device=DEV)
+            nb.conv_fwd(x, w, Kp, R, R, s, p, y, stats=st)
+            used_fwd = nb.C.conv_sk_last()
+            dx = _empty(N, H, W, Cp)
+            nb.conv_dgrad(dy, wT, Cp, R, R, s, p, dx)
+            used_dg = nb.C.conv_sk_last()
+            torch.cuda.synchronize()
+            out.setdefault(mode, []).append((y.buf.clone(), st.double().sum(0), dx.buf.clone(), used_fwd, used_dg))
+    finally:
+        nb.C.set_conv_sk(-1)
+    base, sk1, sk2 = out[0][0], out[2][0], out[2][1]
+    assert base[3] == 0 and base[4] == 0
+    assert sk1[3] == 1 or sk1[4] == 1, "stream-K did not engage"
+    assert torch.equal(sk1[0], sk2[0]) and torch.equal(sk1[2], sk2[2]) and torch.equal(sk1[1], sk2[1])
+    assert _rel(sk1[0], base[0]) < 1e-2 and _rel(sk1[2], base[2]) < 1e-2
+    assert _rel(sk1[1], base[1]) < 1e-4
+
+
 @pytest.mark.parametrize("shape", [CONV_SHAPES[1], CONV_SHAPES[2], CONV_SHAPES[3], CONV_SHAPES[5]])
 @pytest.mark.parametrize("mode", ["mask", "two", "from_z", "bits"])
 def test_conv_dgrad_fused_bn_backward(shape, mode):
