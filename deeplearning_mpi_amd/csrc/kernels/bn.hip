@@ -344,6 +344,33 @@ __global__ __launch_bounds__(256) void finalize_kernel(const double* __restrict_
 typedef __attribute__((address_space(1))) unsigned long long gu64_t;
 typedef __attribute__((address_space(1))) int gi32_t;
 
+// Direct form for short partial columns (T <= DLMPI_COLSUM_DIRECT rows, default 512: the 14^2 / 7^2
+// ResNet layers): one 1024-thread block per 64-channel group walks all T rows (16 row lanes, fixed
+// order), combines them in LDS and finalizes -- no slice stores, ticket or second pass, whose
+// latency chain (~7 us) dominated these small finalizes.
+__global__ __launch_bounds__(1024) void colsum_fin_direct_kernel(const float* __restrict__ partial, int T, int C,
+                                                                 int ns, int k2, FinArgs f) {
+  __shared__ double r[2][16][64];
+  const int lc = threadIdx.x & 63, rl = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + lc;
+  double a = 0.0, b = 0.0;
+  if (c < C) {
+#pragma unroll 8
+    for (int t = rl; t < T; t += 16) {
+      a += (double)partial[(int64_t)t * ns * C + c];
+      b += (double)partial[(int64_t)t * ns * C + k2 * C + c];
+    }
+  }
+  r[0][rl][lc] = a;
+  r[1][rl][lc] = b;
+  __syncthreads();
+  if (rl == 0 && c < C) {
+    for (int g = 1; g < 16; ++g) { a += r[0][g][lc]; b += r[1][g][lc]; }
+    if (f.mode == 0) fin_fwd(f, c, a, b);
+    else fin_bwd(f, c, a, b, C);
+  }
+}
+
 template <bool SC1>
 __global__ __launch_bounds__(256) void colsum_fin_kernel(const float* __restrict__ partial, int T, int C, int ns,
                                                          int k2, double* __restrict__ dpart, int* __restrict__ tickets,
@@ -704,10 +731,22 @@ static bool fin_sc1() {   // DLMPI_FIN_SC1=0: the fenced hand-off (A/B)
   return v;
 }
 
+static int colsum_direct_max() {
+  static const int v = [] {
+    const char* e = getenv("DLMPI_COLSUM_DIRECT");
+    return e ? atoi(e) : 512;
+  }();
+  return v;
+}
+
 static hipError_t colsum_finalize(const float* partial, int T, int C, int ns, int k2, double* ws, const FinArgs& f,
                                   hipStream_t s) {
   const int S = colsum_slices(T);
   const int G = (C + 63) / 64;
+  if (T <= colsum_direct_max()) {
+    hipLaunchKernelGGL(colsum_fin_direct_kernel, dim3(G), dim3(1024), 0, s, partial, T, C, ns, k2, f);
+    return hipGetLastError();
+  }
   int* tk = fused_finalize() && G <= 4096 ? fin_tickets(s) : nullptr;
   if (tk) {
     if (fin_sc1()) hipLaunchKernelGGL(colsum_fin_kernel<true>, dim3(G, S), dim3(256), 0, s, partial, T, C, ns, k2, ws, tk, f);

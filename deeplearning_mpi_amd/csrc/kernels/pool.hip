@@ -22,16 +22,20 @@ static inline unsigned ew_blocks(int64_t total) {
 template <typename T>
 __global__ void maxpool_fwd_kernel(const T* __restrict__ x, int N, int H, int W, int C, int ldx, int xoff,
                                    int k, int stride, int pad, T* __restrict__ y, uint8_t* __restrict__ idx,
-                                   int OH, int OW, const float* __restrict__ scale, const float* __restrict__ shift) {
+                                   int OH, int OW, const float* __restrict__ scale, const float* __restrict__ shift,
+                                   FastDiv fdCC, FastDiv fdOW, FastDiv fdOH) {
   const int CC = C >> 3;
-  const int64_t total = (int64_t)N * OH * OW * CC;
+  const int64_t total = (int64_t)N * OH * OW * CC;   // < 2^31 (launcher): 32-bit magic divisions
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
-    const int cc = (int)(i % CC);
-    int64_t pix = i / CC;
-    const int ow = (int)(pix % OW);
-    const int64_t t2 = pix / OW;
-    const int oh = (int)(t2 % OH);
-    const int n = (int)(t2 / OH);
+    const uint32_t ui = (uint32_t)i;
+    const uint32_t upix = fdiv(ui, fdCC);
+    const int cc = (int)(ui - upix * CC);
+    const int64_t pix = upix;
+    const uint32_t t2 = fdiv(upix, fdOW);
+    const int ow = (int)(upix - t2 * OW);
+    const uint32_t n_ = fdiv(t2, fdOH);
+    const int oh = (int)(t2 - n_ * OH);
+    const int n = (int)n_;
     float best[8], sc[8], sh[8];
     uint8_t bi[8];
 #pragma unroll
@@ -307,12 +311,14 @@ extern "C" hipError_t dlmpi_maxpool_fwd(const void* x, int N, int H, int W, int 
                                         const float* scale, const float* shift, int f32, hipStream_t s) {
   if (C % 8) return hipErrorInvalidValue;
   const int64_t total = (int64_t)N * OH * OW * (C / 8);
+  if (total >= (1ll << 31)) return hipErrorInvalidValue;
+  const FastDiv a = make_fastdiv(C / 8), b = make_fastdiv(OW), c = make_fastdiv(OH);
   if (f32)
     hipLaunchKernelGGL(maxpool_fwd_kernel<float>, dim3(ew_blocks(total)), dim3(256), 0, s, (const float*)x, N, H, W, C,
-                       ldx, xoff, k, stride, pad, (float*)y, idx, OH, OW, scale, shift);
+                       ldx, xoff, k, stride, pad, (float*)y, idx, OH, OW, scale, shift, a, b, c);
   else
     hipLaunchKernelGGL(maxpool_fwd_kernel<uint16_t>, dim3(ew_blocks(total)), dim3(256), 0, s, (const uint16_t*)x, N, H,
-                       W, C, ldx, xoff, k, stride, pad, (uint16_t*)y, idx, OH, OW, scale, shift);
+                       W, C, ldx, xoff, k, stride, pad, (uint16_t*)y, idx, OH, OW, scale, shift, a, b, c);
   return hipGetLastError();
 }
 
