@@ -513,7 +513,16 @@ void conv2d_wgrad_pro(const at::Tensor& dy, int lddy, int dyoff, int Ko, const a
   a.direct = (R == 1 && S == 1 && stride == 1 && pad == 0 && P == H && Q == W) ? 1 : 0;
   const int bm = a.f32 || Ko <= 64 ? 64 : 128;   // fp32: conv_wgrad_f32_kernel's 64 x 64 tile
   a.mtiles = ceil_div(Ko, bm);
-  const int bn = a.f32 ? 64 : 128;
+  // Ko <= 64: 64 x 256 tiles (1 x 4 waves of 64 x 64) when the 256-column padding costs little more
+  // than the 128-column one.  DLMPI_WGRAD_WIDE: 0 off (default), 1 that rule, 2 whenever TC >= 256.
+  static const int wide = [] {
+    const char* e = getenv("DLMPI_WGRAD_WIDE");
+    return e ? atoi(e) : 0;
+  }();
+  const int64_t pad128 = ceil_div(a.TC, 128) * 128, pad256 = ceil_div(a.TC, 256) * 256;
+  const bool w256 = !a.f32 && Ko <= 64 && pro_b == 0 && a.TC >= 256 &&
+                    (wide == 2 || (wide == 1 && pad256 * 10 <= pad128 * 11));
+  const int bn = a.f32 ? 64 : (w256 ? 256 : 128);
   a.ntiles = ceil_div(a.TC, bn);
   const int tiles = a.mtiles * a.ntiles;
   // split the pixel reduction so the grid covers the chip ~2 blocks deep, but keep each split at
@@ -607,13 +616,17 @@ void bn_stats(const at::Tensor& x, int64_t M, int C, int ldx, int xoff, at::Tens
 
 void bn_apply(const at::Tensor& x, int ldx, int xoff, int64_t M, int C, const at::Tensor& scale,
               const at::Tensor& shift, const c10::optional<at::Tensor>& res, int ldres, int resoff, bool relu,
-              at::Tensor y, int ldy, int yoff, const c10::optional<at::Tensor>& mbits) {
+              at::Tensor y, int ldy, int yoff, const c10::optional<at::Tensor>& mbits,
+              const c10::optional<at::Tensor>& rscale, const c10::optional<at::Tensor>& rshift) {
   if (mbits && mbits->numel() != M * (C / 8)) throw std::runtime_error("bn_apply: mask bits must be [M][C/8]");
+  if (rscale.has_value() != rshift.has_value() || (rscale && !res))
+    throw std::runtime_error("bn_apply: rscale / rshift come together, with a residual");
+  if (rscale && (rscale->numel() < C || rshift->numel() < C)) throw std::runtime_error("bn_apply: rscale / rshift < C");
   same_type(x, y, "bn_apply y");
   same_type(x, res, "bn_apply res");
-  check(dlmpi_bn_apply(x.data_ptr(), ldx, xoff, M, C, ptr<float>(scale), ptr<float>(shift), optr<uint16_t>(res), ldres,
-                       resoff, relu ? 1 : 0, y.data_ptr(), ldy, yoff, optr<uint8_t>(mbits), act_f32(x, "bn_apply"),
-                       cur_stream()),
+  check(dlmpi_bn_apply2(x.data_ptr(), ldx, xoff, M, C, ptr<float>(scale), ptr<float>(shift), optr<uint16_t>(res), ldres,
+                        resoff, optr<float>(rscale), optr<float>(rshift), relu ? 1 : 0, y.data_ptr(), ldy, yoff,
+                        optr<uint8_t>(mbits), act_f32(x, "bn_apply"), cur_stream()),
         "bn_apply");
 }
 

@@ -476,7 +476,8 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const T* __restrict__ x, 
                                                        const float* __restrict__ shift,
                                                        const T* __restrict__ res, int ldres, int resoff,
                                                        int relu, T* __restrict__ y, int ldy, int yoff,
-                                                       uint8_t* __restrict__ mbits) {
+                                                       uint8_t* __restrict__ mbits, const float* __restrict__ rscale,
+                                                       const float* __restrict__ rshift) {
   const int CC = C >> 3;
   const int64_t total = M * CC;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
@@ -503,6 +504,16 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const T* __restrict__ x, 
     if (res) {
       float r[8];
       load8(res + row * ldres + resoff + c0, r);
+      if (rscale) {   // the residual is itself a BN output (ResNet downsample): r * rscale + rshift,
+                      // applied here instead of in a pass of its own (never rounded to bf16)
+        const f32x4 a0 = *reinterpret_cast<const f32x4*>(rscale + c0), a1 = *reinterpret_cast<const f32x4*>(rscale + c0 + 4);
+        const f32x4 b0 = *reinterpret_cast<const f32x4*>(rshift + c0), b1 = *reinterpret_cast<const f32x4*>(rshift + c0 + 4);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          r[e] = __builtin_fmaf(r[e], a0[e], b0[e]);
+          r[e + 4] = __builtin_fmaf(r[e + 4], a1[e], b1[e]);
+        }
+      }
 #pragma unroll
       for (int e = 0; e < 8; ++e) v[e] += r[e];
     }
@@ -816,14 +827,22 @@ extern "C" hipError_t dlmpi_bn_finalize(const float* partial, int ntiles, int C,
   return colsum_finalize(partial, ntiles, C, 2, 1, ws, f, s);
 }
 
+extern "C" hipError_t dlmpi_bn_apply2(const void* x, int ldx, int xoff, int64_t M, int C, const float* scale,
+                                      const float* shift, const void* res, int ldres, int resoff, const float* rscale,
+                                      const float* rshift, int relu, void* y, int ldy, int yoff, uint8_t* mbits,
+                                      int f32, hipStream_t s) {
+  if (C % 8 || ((rscale != nullptr) != (rshift != nullptr)) || (rscale && !res)) return hipErrorInvalidValue;
+  const int64_t total = M * (C / 8);
+  DLMPI_TLAUNCH(bn_apply_kernel, dim3(ew_blocks(total)), CT(x), ldx, xoff, M, C, make_fastdiv(C / 8), scale, shift,
+                CT(res), ldres, resoff, relu, MT(y), ldy, yoff, mbits, rscale, rshift);
+  return hipGetLastError();
+}
+
 extern "C" hipError_t dlmpi_bn_apply(const void* x, int ldx, int xoff, int64_t M, int C, const float* scale,
                                      const float* shift, const void* res, int ldres, int resoff, int relu,
                                      void* y, int ldy, int yoff, uint8_t* mbits, int f32, hipStream_t s) {
-  if (C % 8) return hipErrorInvalidValue;
-  const int64_t total = M * (C / 8);
-  DLMPI_TLAUNCH(bn_apply_kernel, dim3(ew_blocks(total)), CT(x), ldx, xoff, M, C, make_fastdiv(C / 8), scale, shift,
-                CT(res), ldres, resoff, relu, MT(y), ldy, yoff, mbits);
-  return hipGetLastError();
+  return dlmpi_bn_apply2(x, ldx, xoff, M, C, scale, shift, res, ldres, resoff, nullptr, nullptr, relu, y, ldy, yoff,
+                         mbits, f32, s);
 }
 
 extern "C" hipError_t dlmpi_bn_bwd_reduce(const void* dy, int lddy, int dyoff, const void* ymask, int ldym,

@@ -76,11 +76,15 @@ __device__ __forceinline__ int tr_chunk(int row, int pos) {
 // dy); PB = 1: the x operand is a deferred BN-apply + ReLU (relu(x * scale + shift)).  Both are
 // rewritten in LDS once a stage has landed, in-range pieces only (padding / tails stay zero), with
 // the arithmetic of the standalone kernels they replace (bit-identical results).
-template <int BM, int BN, int STAGES, bool DIRECT, int PA = 0, int PB = 0>
+// WR: wave-grid rows (WR x 4/WR waves).  64 x 256 (Ko <= 64 layers: the whole Ko by 256 columns)
+// runs 1 x 4 waves of 64 x 64: 16 transposed-read pairs per 16 MFMAs instead of the 64 x 128 tile's
+// 12 per 8, and every dy row is staged once per 256 instead of per 128 columns.
+template <int BM, int BN, int STAGES, bool DIRECT, int PA = 0, int PB = 0, int WR = 2>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(STAGES == 1 && BN == 128 ? 3 : 2, 8)))
 void conv_wgrad_kernel(const WgradArgs a) {
   constexpr int BK = 64;
-  constexpr int WM = BM / 2, WN = BN / 2, TM = WM / 16, TN = WN / 16;
+  constexpr int WC = 4 / WR;                               // wave-grid columns
+  constexpr int WM = BM / WR, WN = BN / WC, TM = WM / 16, TN = WN / 16;
   constexpr int A_ROW = BM * 2, B_ROW = BN * 2;          // bytes per LDS row
   constexpr int AL = BK * A_ROW / 4096, BL = BK * B_ROW / 4096;   // 16-B pieces per thread
   constexpr int A_BYTES = BK * A_ROW, B_BYTES = BK * B_ROW;
@@ -102,7 +106,7 @@ void conv_wgrad_kernel(const WgradArgs a) {
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wid >> 1, wn = wid & 1;
+  const int wm = wid / WC, wn = wid % WC;
   const int PQ = a.P * a.Q;
   const char* zp = reinterpret_cast<const char*>(g_zero_page);
 
@@ -523,9 +527,21 @@ extern "C" hipError_t dlmpi_conv_wgrad(const WgradArgs* a, int bm, int bn, hipSt
     else hipLaunchKernelGGL(conv_wgrad_f32_kernel<false>, g, b, 0, s, *a);
     return hipGetLastError();
   }
-  // (a 256-column variant was measured 1.3-1.9x slower: 2 waves/SIMD and register spills)
-  if (bn != 128 || (bm != 128 && bm != 64)) return hipErrorInvalidValue;
   const bool d = a->direct != 0;
+  // 64 x 256, 1 x 4 waves (Ko <= 64 layers); prologue a (deferred BN-backward apply) or none
+  if (bm == 64 && bn == 256) {
+    if (a->pro_b != 0 || (a->pro_a != 0 && a->pro_a != 2) || stages != 1) return hipErrorInvalidValue;
+    if (a->pro_a == 2) {
+      if (d) hipLaunchKernelGGL((conv_wgrad_kernel<64, 256, 1, true, 2, 0, 1>), g, b, 0, s, *a);
+      else hipLaunchKernelGGL((conv_wgrad_kernel<64, 256, 1, false, 2, 0, 1>), g, b, 0, s, *a);
+    } else {
+      if (d) hipLaunchKernelGGL((conv_wgrad_kernel<64, 256, 1, true, 0, 0, 1>), g, b, 0, s, *a);
+      else hipLaunchKernelGGL((conv_wgrad_kernel<64, 256, 1, false, 0, 0, 1>), g, b, 0, s, *a);
+    }
+    return hipGetLastError();
+  }
+  // (a 128 x 256 variant was measured 1.3-1.9x slower: 2 waves/SIMD and register spills)
+  if (bn != 128 || (bm != 128 && bm != 64)) return hipErrorInvalidValue;
   if (a->pro_a != 0 || a->pro_b != 0) {
     if ((a->pro_a != 0 && a->pro_a != 2) || (a->pro_b != 0 && a->pro_b != 1)) return hipErrorInvalidValue;
     const int m = (a->pro_a ? 2 : 0) | (a->pro_b ? 1 : 0);

@@ -171,6 +171,10 @@ hipError_t dlmpi_bn_stats(const void* x, int64_t M, int C, int ldx, int xoff, fl
 hipError_t dlmpi_bn_apply(const void* x, int ldx, int xoff, int64_t M, int C, const float* scale, const float* shift,
                           const void* res, int ldres, int resoff, int relu, void* y, int ldy, int yoff, uint8_t* mbits,
                           int f32, hipStream_t s);
+// as dlmpi_bn_apply; the residual is a BN output applied on the fly: res * rscale + rshift
+hipError_t dlmpi_bn_apply2(const void* x, int ldx, int xoff, int64_t M, int C, const float* scale, const float* shift,
+                           const void* res, int ldres, int resoff, const float* rscale, const float* rshift, int relu,
+                           void* y, int ldy, int yoff, uint8_t* mbits, int f32, hipStream_t s);
 hipError_t dlmpi_bn_bwd_reduce(const void* dy, int lddy, int dyoff, const void* ymask, int ldym, int ymoff,
                                const void* x, int ldx, int xoff, int64_t M, int C, const float* mean,
                                const float* invstd, float* partial, int nblk, int f32, hipStream_t s);

@@ -83,6 +83,8 @@ def record_on(stream, *objs):
         if isinstance(o, torch.Tensor):
             if o.is_cuda:
                 o.record_stream(stream)
+        elif isinstance(o, Deferred):
+            record_on(stream, *o.bufs())
         elif hasattr(o, "buf") and isinstance(getattr(o, "buf"), torch.Tensor):
             record_on(stream, o.buf)
         elif isinstance(o, (tuple, list)):
@@ -202,12 +204,16 @@ class ConvUnit:
         residual produced on another stream is joined there, after this unit's GEMM).  defer_apply (training BN + ReLU, no residual): skip the BN-apply + ReLU;
         True returns the BN input z -- the consumer applies scale/shift (ctx[5:7]) itself (the ResNet
         stem's max-pool) --, "act" returns Deferred.affine(z, scale, shift) for the next
-        convolution.  Either way the BN output is never materialised."""
+        convolution, "bn" (BN without ReLU) Deferred.bn(z, scale, shift) for a residual consumer
+        (the ResNet downsample branch, applied inside the block's last BN-apply).  Either way the BN
+        output is never materialised."""
         assert x.C == self.Cp, (x, self.Cp)
         P, Q = self.out_hw(x.H, x.W)
         N, dev = x.N, x.device
         wf = self._weight_fwd()
         if defer_apply == "act" and not (train and save and res is None and self.relu and self.bn is not None):
+            defer_apply = False
+        if defer_apply == "bn" and not (train and save and res is None and not self.relu and self.bn is not None):
             defer_apply = False
         y = None if defer_apply and out is None else (
             out if out is not None else Act.empty(N, P, Q, self.Kp, be.act_dtype, dev))
@@ -237,7 +243,11 @@ class ConvUnit:
                            invstd)
             if defer_apply and save and res is None:
                 ctx = (x, z, None, mean, invstd, scale, shift, False, None)
-                return (Deferred.affine(z, scale, shift) if defer_apply == "act" else z), ctx
+                if defer_apply == "act":
+                    return Deferred.affine(z, scale, shift), ctx
+                if defer_apply == "bn":
+                    return Deferred.bn(z, scale, shift), ctx
+                return z, ctx
             # residual units: the backward mask (y > 0) cannot be recomputed from z alone, so keep it
             # as bits (1/16 of y's bytes) for the fused data-gradient epilogue
             mbits = None

@@ -89,6 +89,9 @@ class Bottleneck(nn.Module):
 # DLMPI_LATE_JOIN=0: join the downsample branch stream before the last unit's GEMM (forward) /
 # before conv1's BN backward (backward) instead of right before the residual is read (A/B knob)
 _LATE_JOIN = os.environ.get("DLMPI_LATE_JOIN", "1") != "0"
+# DLMPI_DS_FUSE=0: store the downsample branch's BN output (a pass of its own) instead of applying
+# it inside the block's last BN-apply (A/B knob; backends without the fused residual ignore it)
+_DS_FUSE = os.environ.get("DLMPI_DS_FUSE", "1") != "0"
 
 
 class _BlockExec:
@@ -103,12 +106,15 @@ class _BlockExec:
         defer: the inner BN + ReLU outputs (bn1, bn2 of a bottleneck) are never stored -- the next
         convolution rebuilds them in its operand prologue (ops.act.Deferred)."""
         ctxs = []
+        # the downsample BN output is read once, as the residual of the last unit's BN-apply: applied
+        # there on the fly (Deferred.bn), which removes its own apply pass (read z_ds + write idn)
+        ds_defer = "bn" if (_DS_FUSE and train and save) else False
         br = getattr(be, "branch_stream", None) if self.ud is not None else None
         if br is not None:
             main = torch.cuda.current_stream()
             br.wait_stream(main)
             with torch.cuda.stream(br):
-                idn, cd = self.ud.fwd(be, x, train, save=save)
+                idn, cd = self.ud.fwd(be, x, train, save=save, defer_apply=ds_defer)
             record_on(br, x)
         h = x
         for k, u in enumerate(self.u[:-1]):
@@ -123,7 +129,7 @@ class _BlockExec:
                 join()
                 join = None
         elif self.ud is not None:
-            idn, cd = self.ud.fwd(be, x, train, save=save)
+            idn, cd = self.ud.fwd(be, x, train, save=save, defer_apply=ds_defer)
         else:
             idn, cd = x, None
         y, c = self.u[-1].fwd(be, h, train, res=idn, save=save, before_res=join)

@@ -65,6 +65,8 @@ class Deferred:
     * ``Deferred.affine(z, scale, shift)`` = relu(z * scale + shift): a training BatchNorm-apply +
       ReLU without residual (the ResNet bottleneck's bn1 / bn2, the first BN of a UNet DoubleConv),
       consumed by the next convolution's forward and weight gradient;
+    * ``Deferred.bn(z, scale, shift)`` = z * scale + shift: a training BatchNorm output without ReLU
+      used only as a residual (the ResNet downsample branch), applied inside the consumer's BN-apply;
     * ``Deferred.bnbwd(dy, z, coef)`` = coef[0] * dy + coef[1] * z + coef[2]: the BatchNorm-backward
       apply, consumed by the unit's own weight-gradient and data-gradient GEMMs.
 
@@ -78,6 +80,12 @@ class Deferred:
     @staticmethod
     def affine(z: Act, scale, shift) -> "Deferred":
         return Deferred("affine", z, None, scale, shift)
+
+    @staticmethod
+    def bn(z: Act, scale, shift) -> "Deferred":
+        """z * scale + shift (a training BatchNorm output without ReLU): the ResNet downsample
+        branch, read only as the residual of the block's last BN-apply, which applies it on the fly."""
+        return Deferred("bn", z, None, scale, shift)
 
     @staticmethod
     def bnbwd(dy: Act, z: Act, coef) -> "Deferred":

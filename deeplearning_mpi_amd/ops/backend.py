@@ -106,8 +106,8 @@ class NativeBackend:
             return d
         src = d.src
         out = Act.empty(src.N, src.H, src.W, src.C, self.act_dtype, src.device)
-        if d.kind == "affine":
-            self.bn_apply(src, d.k0, d.k1, None, True, out)
+        if d.kind in ("affine", "bn"):
+            self.bn_apply(src, d.k0, d.k1, None, d.kind == "affine", out)
         else:
             self.C.bn_bwd_apply(src.buf, src.ld, src.off, None, 0, 0, d.z.buf, d.z.ld, d.z.off, src.rows, src.C,
                                 d.k0, out.buf, None)
@@ -168,10 +168,15 @@ class NativeBackend:
         self.C.bn_stats(x.buf, x.rows, x.C, x.ld, x.off, part, nblk)
         return part, nblk
 
-    def bn_apply(self, x: Act, scale, shift, res: Act, relu, y: Act, mbits=None):
+    def bn_apply(self, x: Act, scale, shift, res, relu, y: Act, mbits=None):
+        """res: an Act, or a Deferred.bn residual (applied on the fly, never materialised)."""
+        rs = rh = None
+        if isinstance(res, Deferred):
+            assert res.kind == "bn", res
+            res, rs, rh = res.src, res.k0, res.k1
         self.C.bn_apply(x.buf, x.ld, x.off, x.rows, x.C, scale, shift, res.buf if res is not None else None,
                         res.ld if res is not None else 0, res.off if res is not None else 0, bool(relu), y.buf, y.ld,
-                        y.off, mbits)
+                        y.off, mbits, rs, rh)
 
     def bn_bwd_deferred(self, dy: Act, x: Act, mean, invstd, gamma, dgamma, dbeta, pre, k2=1) -> Deferred:
         """BN backward from the producer's fused partials (``pre``): finalize only (dgamma, dbeta and
@@ -367,8 +372,8 @@ class RefBackend:
             return d
         src = d.src
         out = Act.empty(src.N, src.H, src.W, src.C, self.act_dtype, src.device)
-        if d.kind == "affine":
-            self.bn_apply(src, d.k0, d.k1, None, True, out)
+        if d.kind in ("affine", "bn"):
+            self.bn_apply(src, d.k0, d.k1, None, d.kind == "affine", out)
         else:
             c = d.k0.to(self.dt)
             out.nhwc().copy_(c[0] * src.nhwc().to(self.dt) + c[1] * d.z.nhwc().to(self.dt) + c[2])
@@ -488,7 +493,10 @@ class RefBackend:
 
     def bn_apply(self, x: Act, scale, shift, res, relu, y: Act, mbits=None):
         v = x.nhwc().to(self.dt) * scale + shift
-        if res is not None:
+        if isinstance(res, Deferred):   # a BN output applied on the fly (no storage rounding)
+            assert res.kind == "bn", res
+            v = v + (res.src.nhwc().to(self.dt) * res.k0.to(self.dt) + res.k1.to(self.dt))
+        elif res is not None:
             v = v + res.nhwc().to(self.dt)
         if relu:
             v = F.relu(v)

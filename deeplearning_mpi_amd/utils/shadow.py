@@ -15,7 +15,7 @@ from __future__ import annotations
 
 import torch
 
-from ..ops.act import Act
+from ..ops.act import Act, Deferred
 
 # ops whose outputs the reference cannot reproduce bit-compatibly: max-pool window indices (native
 # uint8 window slots vs torch flat indices) feed maxpool_bwd; cast_weights / conv_mtiles are layout
@@ -30,6 +30,8 @@ def to64(a):
         return Act(b.double().clone() if b.is_floating_point() else b.clone(), a.N, a.H, a.W, a.C, a.off)
     if isinstance(a, torch.Tensor):
         return a.detach().double().clone() if a.is_floating_point() else a.clone()
+    if isinstance(a, Deferred):
+        return Deferred(a.kind, to64(a.src), to64(a.z), to64(a.k0), to64(a.k1))
     if isinstance(a, tuple) and hasattr(a, "_fields"):
         return type(a)(*[to64(x) for x in a])
     if isinstance(a, (list, tuple)):

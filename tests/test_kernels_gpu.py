@@ -4,7 +4,7 @@ strided / downsample, UNet concat widths, linear heads, odd tile remainders)."""
 import pytest
 import torch
 
-from deeplearning_mpi_amd.ops.act import Act, pad8
+from deeplearning_mpi_amd.ops.act import Act, Deferred, pad8
 from deeplearning_mpi_amd.models.engine import BwdFuse
 from deeplearning_mpi_amd.ops.backend import NativeBackend, RefBackend
 
@@ -359,6 +359,14 @@ def test_bn_family():
     assert _rel(y.buf, yr.buf) < 1e-2
     unpacked = RefBackend._unpack_bits(bits, y).reshape(-1, C)
     assert torch.equal(unpacked, y.buf.float() > 0)   # bit e == (stored y > 0)
+    # residual that is itself a BN output, applied on the fly (the ResNet downsample branch)
+    rs, rh = torch.rand(C, device=DEV) + 0.5, torch.randn(C, device=DEV)
+    y2, y2r = _empty(N, H, W, C), _empty(N, H, W, C, torch.float32)
+    bits2 = torch.empty_like(bits)
+    nb.bn_apply(x, v[0], v[1], Deferred.bn(res, rs, rh), True, y2, mbits=bits2)
+    rb.bn_apply(xr, v[0], v[1], Deferred.bn(resr, rs, rh), True, y2r)
+    assert _rel(y2.buf, y2r.buf) < 1e-2
+    assert torch.equal(RefBackend._unpack_bits(bits2, y2).reshape(-1, C), y2.buf.float() > 0)
     dy, dyr = _act(N, H, W, C)
     dg, db = torch.zeros(C, device=DEV), torch.zeros(C, device=DEV)
     dgr, dbr = torch.zeros(C, device=DEV), torch.zeros(C, device=DEV)
@@ -579,7 +587,7 @@ def test_cast_weights_all_layouts(model):
 _WG_SCRIPT = r"""
 import sys, torch
 sys.path.insert(0, {root!r})
-from deeplearning_mpi_amd.ops.act import Act, pad8
+from deeplearning_mpi_amd.ops.act import Act, Deferred, pad8
 from deeplearning_mpi_amd.ops.backend import NativeBackend
 nb = NativeBackend("cuda")
 out = {{}}
