@@ -513,15 +513,15 @@ void conv2d_wgrad_pro(const at::Tensor& dy, int lddy, int dyoff, int Ko, const a
   a.direct = (R == 1 && S == 1 && stride == 1 && pad == 0 && P == H && Q == W) ? 1 : 0;
   const int bm = a.f32 || Ko <= 64 ? 64 : 128;   // fp32: conv_wgrad_f32_kernel's 64 x 64 tile
   a.mtiles = ceil_div(Ko, bm);
-  // Ko <= 64: 64 x 256 tiles (1 x 4 waves of 64 x 64) when the 256-column padding costs little more
-  // than the 128-column one.  DLMPI_WGRAD_WIDE: 0 off (default), 1 that rule, 2 whenever TC >= 256.
+  // Ko <= 64 gather-form (3x3 / strided / stem) weight gradients: 64 x 256 tiles (1 x 4 waves of
+  // 64 x 64) -- each dy row staged once per 256 columns, fewer LDS reads per MFMA.  The tile holds
+  // ~200 VGPRs (2 blocks per CU), so its split count is floored to fit the grid in one round
+  // (profiles/r2_wgrad_wide).  DLMPI_WGRAD_WIDE: 0 off, 1 gather-form only (default), 2 also 1x1.
   static const int wide = [] {
     const char* e = getenv("DLMPI_WGRAD_WIDE");
-    return e ? atoi(e) : 0;
+    return e ? atoi(e) : 1;
   }();
-  const int64_t pad128 = ceil_div(a.TC, 128) * 128, pad256 = ceil_div(a.TC, 256) * 256;
-  const bool w256 = !a.f32 && Ko <= 64 && pro_b == 0 && a.TC >= 256 &&
-                    (wide == 2 || (wide == 1 && pad256 * 10 <= pad128 * 11));
+  const bool w256 = !a.f32 && Ko <= 64 && pro_b == 0 && a.TC >= 256 && (wide == 2 || (wide == 1 && !a.direct));
   const int bn = a.f32 ? 64 : (w256 ? 256 : 128);
   a.ntiles = ceil_div(a.TC, bn);
   const int tiles = a.mtiles * a.ntiles;
@@ -534,7 +534,7 @@ void conv2d_wgrad_pro(const at::Tensor& dy, int lddy, int dyoff, int Ko, const a
     return e ? std::max(64, atoi(e)) : 512;
   }();
   const int maxsplit = std::max(1, ceil_div(a.npix, 512));
-  int splits = std::max(1, std::min(maxsplit, ceil_div(target_blocks, tiles)));
+  int splits = std::max(1, std::min(maxsplit, w256 ? target_blocks / tiles : ceil_div(target_blocks, tiles)));
   int pps = ceil_div(a.npix, splits);
   pps = ceil_div(pps, 64) * 64;
   splits = ceil_div(a.npix, pps);
