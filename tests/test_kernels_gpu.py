@@ -381,6 +381,27 @@ def test_bn_family():
     assert _rel(dyo.buf, dyor.buf) < 1e-2
 
 
+@pytest.mark.parametrize("T,C", [(300, 256), (600, 64), (6272, 64), (1568, 512), (40000, 64)])
+def test_bn_finalize_column_paths(T, C):
+    """Every finalize path (single-pass T <= 512, the sliced last-arriver kernel beyond) against
+    the fp32 reference on random per-tile partials."""
+    nb, rb = _be()
+    torch.manual_seed(T + C)
+    M = T * 128
+    x = torch.randn(T, 1, C, device=DEV) * 3 + 1
+    st = torch.cat([x, x * x + torch.rand(T, 1, C, device=DEV)], 1) * 128
+    gamma, beta = torch.rand(C, device=DEV) + 0.5, torch.randn(C, device=DEV)
+    outs = []
+    for be in (nb, rb):
+        rm, rv = torch.zeros(C, device=DEV), torch.ones(C, device=DEV)
+        v = torch.empty(4, C, device=DEV)
+        be.bn_finalize(st, T, C, M, gamma, beta, rm, rv, 0.1, 1e-5, v[0], v[1], v[2], v[3])
+        outs.append((v.clone(), rm, rv))
+    torch.cuda.synchronize()
+    for a, b in zip(outs[0], outs[1]):
+        assert _rel(a, b) < 1e-5
+
+
 def test_pools_and_layout():
     nb, rb = _be()
     x = torch.randn(2, 3, 20, 18, device=DEV)
