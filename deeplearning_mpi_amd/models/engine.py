@@ -111,6 +111,62 @@ DEFER_BN_FWD = os.environ.get("DLMPI_DEFER_BN_FWD", "0") != "0"
 DEFER_BN_BWD = os.environ.get("DLMPI_DEFER_BN_BWD", "0") != "0"
 DEFER_BN_WGRAD = os.environ.get("DLMPI_DEFER_BN_WGRAD", "1") != "0"
 
+# DLMPI_CHUNK_FWD=1: run each forward BN-apply in two image chunks interleaved with its consumer's
+# GEMM on the main + side streams (PendingApply).  Off by default: measured slower (ResNet-50 bs 256
+# 11,501 vs 11,894 img/s, ResNet-152 3,963 vs 4,390; profiles/r2_chunk_fwd_rejected) -- the bn_apply
+# time with nothing beside it drops 2.1 -> 1.5 ms, but every join costs the main stream a ~40 us
+# wait for the later side-stream half before the BN finalize (1.8 ms of main-stream gaps per step)
+CHUNK_FWD = os.environ.get("DLMPI_CHUNK_FWD", "0") != "0"
+
+
+def img_rows(a, n0: int, n1: int):
+    """Images [n0, n1) of an Act (a row range of its 2-D buffer, same ld / channel offset) or of a
+    Deferred.bn operand."""
+    if a is None:
+        return None
+    if isinstance(a, Deferred):
+        return Deferred(a.kind, img_rows(a.src, n0, n1), img_rows(a.z, n0, n1), a.k0, a.k1)
+    hw = a.H * a.W
+    return Act(a.buf[n0 * hw:n1 * hw], n1 - n0, a.H, a.W, a.C, a.off)
+
+
+class PendingApply:
+    """A training BN-apply (+ residual) (+ ReLU) (+ mask bits) whose output ``y`` is allocated but
+    not yet computed.  The consuming convolution (``ConvUnit.fwd``) runs it image-chunk by
+    image-chunk interleaved with its own GEMM on two streams -- chunk 0's apply and GEMM on the
+    main stream, chunk 1's apply and GEMM on the side stream, which starts after chunk 0's apply --
+    so the memory-bound apply of one half runs beside the MFMA-bound GEMM of the other instead of
+    alone on the forward's critical path (profiles/r2_profile_v4: 2.1 ms of bn_apply with nothing
+    beside it per ResNet-50 step).  Any other consumer calls ``resolve`` (one whole apply)."""
+
+    __slots__ = ("y", "z", "scale", "shift", "res", "relu", "mbits", "done")
+
+    def __init__(self, y, z, scale, shift, res, relu, mbits):
+        self.y, self.z, self.scale, self.shift, self.res, self.relu, self.mbits = y, z, scale, shift, res, relu, mbits
+        self.done = False
+
+    N = property(lambda self: self.y.N)
+    H = property(lambda self: self.y.H)
+    W = property(lambda self: self.y.W)
+    C = property(lambda self: self.y.C)
+    device = property(lambda self: self.y.device)
+
+    def apply_images(self, be, n0, n1):
+        hw = self.y.H * self.y.W
+        mb = self.mbits[n0 * hw:n1 * hw] if self.mbits is not None else None
+        be.bn_apply(img_rows(self.z, n0, n1), self.scale, self.shift, img_rows(self.res, n0, n1), self.relu,
+                    img_rows(self.y, n0, n1), mbits=mb)
+
+    def resolve(self, be) -> Act:
+        if not self.done:
+            be.bn_apply(self.z, self.scale, self.shift, self.res, self.relu, self.y, mbits=self.mbits)
+            self.done = True
+        return self.y
+
+
+def resolve(be, a):
+    return a.resolve(be) if isinstance(a, PendingApply) else a
+
 
 def bufs(*objs):
     """The storage tensors behind Acts / Deferred operands (None skipped)."""
@@ -197,8 +253,43 @@ class ConvUnit:
         self.arena.backend.gather_(self._bias_pad, self.bias.data, self._bias_idx)   # one launch of ours
         return self._bias_pad
 
+    def _chunkable(self, be, x) -> bool:
+        """Can this unit consume a PendingApply input chunk-wise (ConvUnit._conv_chunked)?"""
+        return (CHUNK_FWD and isinstance(x, PendingApply) and self.bn is not None and x.N >= 2 and x.N % 2 == 0
+                and (getattr(be, "side_stream", None) is not None or getattr(be, "chunk_serial", False)))
+
+    def _conv_chunked(self, be, xp: PendingApply, wf, z: Act):
+        """The producer's BN-apply and this GEMM (with its BN-statistics epilogue) over two image
+        halves: apply(0) -> GEMM(0) on the current stream; the side stream starts after apply(0)
+        and runs apply(1) -> GEMM(1) beside GEMM(0); the current stream joins it before the
+        finalize.  Each half writes its own rows of the statistics partials, so the finalize sees
+        the same column sums as one whole GEMM (bit-identical outputs).  Returns (stats, rows)."""
+        N, h = xp.N, xp.N // 2
+        halves = ((0, h), (h, N))
+        mts = [be.conv_mtiles(n1 - n0, xp.H, xp.W, self.Cp, self.Kp, self.R, self.S, self.stride, self.pad)
+               for n0, n1 in halves]
+        stats = torch.empty(sum(mts), 2, self.Kp, dtype=be.dt, device=z.device)
+        bias = self._bias_vec()
+        side = getattr(be, "side_stream", None)
+        main = torch.cuda.current_stream() if side is not None else None
+        xp.apply_images(be, 0, h)
+        if side is not None:
+            side.wait_stream(main)
+        o = 0
+        for i, ((n0, n1), mt) in enumerate(zip(halves, mts)):
+            with torch.cuda.stream(side) if (i == 1 and side is not None) else contextlib.nullcontext():
+                if i == 1:
+                    xp.apply_images(be, n0, n1)
+                be.conv_fwd(img_rows(xp.y, n0, n1), wf, self.Kp, self.R, self.S, self.stride, self.pad,
+                            img_rows(z, n0, n1), bias=bias, stats=stats[o:o + mt])
+            o += mt
+        if side is not None:
+            main.wait_stream(side)
+        xp.done = True
+        return stats, o
+
     def fwd(self, be, x, train: bool, res: Act = None, out: Act = None, save=True, defer_apply=False,
-            before_res=None):
+            before_res=None, lazy=False):
         """Returns (output, saved context).  x: an Act or a Deferred operand (rebuilt by the GEMM's
         operand prologue).  before_res: called right before the first kernel that reads ``res`` (a
         residual produced on another stream is joined there, after this unit's GEMM).  defer_apply (training BN + ReLU, no residual): skip the BN-apply + ReLU;
@@ -206,7 +297,11 @@ class ConvUnit:
         stem's max-pool) --, "act" returns Deferred.affine(z, scale, shift) for the next
         convolution, "bn" (BN without ReLU) Deferred.bn(z, scale, shift) for a residual consumer
         (the ResNet downsample branch, applied inside the block's last BN-apply).  Either way the BN
-        output is never materialised."""
+        output is never materialised.  lazy (training BN, not deferred): return a PendingApply instead
+        of running the BN-apply -- for a consumer that runs it chunk-wise beside its own GEMM."""
+        chunked = train and self._chunkable(be, x)
+        if isinstance(x, PendingApply) and not chunked:
+            x = x.resolve(be)
         assert x.C == self.Cp, (x, self.Cp)
         P, Q = self.out_hw(x.H, x.W)
         N, dev = x.N, x.device
@@ -226,10 +321,15 @@ class ConvUnit:
             return y, ((x, y) if save else None)
         if train:
             z = Act.empty(N, P, Q, self.Kp, be.act_dtype, dev)
-            mt = be.conv_mtiles(N, x.H, x.W, x.C, self.Kp, self.R, self.S, self.stride, self.pad,
-                                pro=isinstance(x, Deferred))
-            stats = torch.empty(mt, 2, self.Kp, dtype=be.dt, device=dev)
-            be.conv_fwd(x, wf, self.Kp, self.R, self.S, self.stride, self.pad, z, bias=self._bias_vec(), stats=stats)
+            if chunked:
+                stats, mt = self._conv_chunked(be, x, wf, z)
+                x = x.y
+            else:
+                mt = be.conv_mtiles(N, x.H, x.W, x.C, self.Kp, self.R, self.S, self.stride, self.pad,
+                                    pro=isinstance(x, Deferred))
+                stats = torch.empty(mt, 2, self.Kp, dtype=be.dt, device=dev)
+                be.conv_fwd(x, wf, self.Kp, self.R, self.S, self.stride, self.pad, z, bias=self._bias_vec(),
+                            stats=stats)
             vec = torch.empty(4, self.Kp, dtype=be.dt, device=dev)
             scale, shift, mean, invstd = vec[0], vec[1], vec[2], vec[3]
             self.arena.wait_buffers()   # DDP's asynchronous buffer broadcast must land first
@@ -255,8 +355,11 @@ class ConvUnit:
                 mbits = torch.empty(y.rows, self.Kp // 8, dtype=torch.uint8, device=dev)
             if before_res is not None and res is not None:
                 before_res()
+            ctx = (x, z, y, mean, invstd, scale, shift, res is not None, mbits) if save else None
+            if lazy and CHUNK_FWD and out is None:
+                return PendingApply(y, z, scale, shift, res, self.relu, mbits), ctx
             be.bn_apply(z, scale, shift, res, self.relu, y, mbits=mbits)
-            return y, ((x, z, y, mean, invstd, scale, shift, res is not None, mbits) if save else None)
+            return y, ctx
         # eval: fold BN (and conv bias) into the GEMM epilogue
         if before_res is not None and res is not None:
             before_res()

@@ -20,7 +20,7 @@ import torch.nn.functional as F
 
 from ..ops.act import Act, padc
 from . import engine as _engine
-from .engine import BwdFuse, ConvUnit, EngineModule, S2DConvUnit, record_on
+from .engine import BwdFuse, ConvUnit, EngineModule, S2DConvUnit, record_on, resolve
 
 
 def conv3x3(i, o, stride=1):
@@ -106,6 +106,9 @@ class _BlockExec:
         defer: the inner BN + ReLU outputs (bn1, bn2 of a bottleneck) are never stored -- the next
         convolution rebuilds them in its operand prologue (ops.act.Deferred)."""
         ctxs = []
+        lazy = train and save and not defer   # BN-applies run chunk-wise inside their consumer (PendingApply)
+        if self.ud is not None:   # the branch reads the whole block input
+            x = resolve(be, x)
         # the downsample BN output is read once, as the residual of the last unit's BN-apply: applied
         # there on the fly (Deferred.bn), which removes its own apply pass (read z_ds + write idn)
         ds_defer = "bn" if (_DS_FUSE and train and save) else False
@@ -118,7 +121,7 @@ class _BlockExec:
             record_on(br, x)
         h = x
         for k, u in enumerate(self.u[:-1]):
-            h, c = u.fwd(be, h, train, save=save, defer_apply="act" if defer else False)
+            h, c = u.fwd(be, h, train, save=save, defer_apply="act" if defer else False, lazy=lazy)
             ctxs.append(c)
         join = None
         if br is not None:
@@ -130,9 +133,9 @@ class _BlockExec:
                 join = None
         elif self.ud is not None:
             idn, cd = self.ud.fwd(be, x, train, save=save, defer_apply=ds_defer)
-        else:
-            idn, cd = x, None
-        y, c = self.u[-1].fwd(be, h, train, res=idn, save=save, before_res=join)
+        else:   # identity: the block input, complete once conv1 has consumed it
+            idn, cd = resolve(be, x), None
+        y, c = self.u[-1].fwd(be, h, train, res=idn, save=save, before_res=join, lazy=lazy)
         ctxs.append(c)
         return y, (ctxs, cd)
 
@@ -295,6 +298,7 @@ class ResNet(EngineModule):
         for blk in self.blocks:
             a, st = blk.fwd(be, a, train, save, defer=dfr)
             st_blocks.append(st)
+        a = resolve(be, a)
         pooled = Act.empty(N, 1, 1, a.C, be.act_dtype, x.device)
         be.avgpool_fwd(a, pooled)
         K = self.fc.out_features

@@ -199,3 +199,32 @@ def test_deferred_bn_passes_match_torch(arch, monkeypatch):
         y = torch.randint(10, (8,), generator=g)
         make = resnet50 if arch == "resnet50" else resnet18
         _run_pair(lambda: make(num_classes=10), x, y, cross_entropy, F.cross_entropy)
+
+
+@pytest.mark.parametrize("arch", ["resnet18", "resnet50"])
+def test_chunked_forward_bn_apply_matches_torch(arch, monkeypatch):
+    """Forward BN-applies run in two image chunks inside their consumer convolution
+    (engine.PendingApply; serial here, main + side stream on the GPU): same fp64 results as
+    autograd, and the chunked path is really taken for every chained BN-apply."""
+    from deeplearning_mpi_amd.models import engine
+    from deeplearning_mpi_amd.models.resnet import resnet18 as r18
+    from deeplearning_mpi_amd.ops.backend import RefBackend
+
+    monkeypatch.setattr(RefBackend, "chunk_serial", True, raising=False)
+    monkeypatch.setattr(engine, "CHUNK_FWD", True)
+    calls = []
+    orig = engine.ConvUnit._conv_chunked
+
+    def counted(self, *a, **k):
+        calls.append(self)
+        return orig(self, *a, **k)
+
+    monkeypatch.setattr(engine.ConvUnit, "_conv_chunked", counted)
+    g = torch.Generator().manual_seed(3)
+    x = torch.randn(4, 3, 64, 64, generator=g)
+    y = torch.randint(10, (4,), generator=g)
+    make = (lambda: r18(num_classes=10)) if arch == "resnet18" else (lambda: resnet50(num_classes=10))
+    _run_pair(make, x, y, cross_entropy, F.cross_entropy)
+    # every conv whose input is a BN-apply output, except conv1 of blocks with a downsample branch
+    # (the branch reads the whole input): resnet18 2*8 - 3 - 1(stem pool input) = 12, resnet50 3*16 - 4
+    assert len(calls) == (12 if arch == "resnet18" else 44)

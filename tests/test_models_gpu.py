@@ -148,6 +148,7 @@ def test_auxiliary_streams_bitwise_equal_single_stream(make, loss):
     assert m1._be.side_stream is not None
     m2._be.side_stream = None       # everything on the current stream
     m2._be.branch_stream = None
+    m2._be.chunk_serial = True      # the same image-chunked forward BN-applies (engine.PendingApply), serially
     for m in (m1, m2):
         m.arena.zero_grad()
         fn(m).backward()
