@@ -347,9 +347,12 @@ c10::optional<at::Tensor> conv2d_dgrad_pro(const at::Tensor& dy, int N, int P, i
                                        const c10::optional<at::Tensor>& mshift,
                                        const c10::optional<at::Tensor>& mbits, bool colsum, int pro,
                                        const c10::optional<at::Tensor>& pk0, const c10::optional<at::Tensor>& pk1,
-                                       const c10::optional<at::Tensor>& pz, int ldpz, int pzoff) {
+                                       const c10::optional<at::Tensor>& pz, int ldpz, int pzoff,
+                                       const c10::optional<at::Tensor>& bias) {
   require_gpu(dy, "dy");
   if (stride > 2) throw std::runtime_error("conv2d_dgrad: stride <= 2 supported");
+  if (bias.has_value() && bias->defined() && (bias->scalar_type() != at::kFloat || bias->numel() < C))
+    throw std::runtime_error("conv2d_dgrad: bias must be fp32 [C]");
   ConvArgs a{};
   a.f32 = act_f32(dy, "conv2d_dgrad");
   same_type(dy, wT, "conv2d_dgrad wT");
@@ -366,7 +369,7 @@ c10::optional<at::Tensor> conv2d_dgrad_pro(const at::Tensor& dy, int N, int P, i
   a.OH = H; a.OW = W;
   a.so = stride; a.sa = 1;
   a.Nimg = N; a.Kout = C;
-  fill_epilogue(a, dx, lddx, dxoff, c10::nullopt, res, ldres, resoff, c10::nullopt, c10::nullopt, false, c10::nullopt);
+  fill_epilogue(a, dx, lddx, dxoff, bias, res, ldres, resoff, c10::nullopt, c10::nullopt, false, c10::nullopt);
   a.vec_store = ((lddx % 8) == 0 && (dxoff % 8) == 0) ? 1 : 0;
   a.mask = optr<uint16_t>(mask);
   a.ldmask = ldmask; a.maskoff = maskoff;
@@ -432,7 +435,7 @@ c10::optional<at::Tensor> conv2d_dgrad(const at::Tensor& dy, int N, int P, int Q
                                        const c10::optional<at::Tensor>& mbits, bool colsum) {
   return conv2d_dgrad_pro(dy, N, P, Q, K, lddy, dyoff, wT, C, R, S, stride, pad, H, W, dx, lddx, dxoff, res, ldres,
                           resoff, mask, ldmask, maskoff, z, ldz, zoff, z2, ldz2, z2off, mscale, mshift, mbits, colsum,
-                          0, c10::nullopt, c10::nullopt, c10::nullopt, 0, 0);
+                          0, c10::nullopt, c10::nullopt, c10::nullopt, 0, 0, c10::nullopt);
 }
 
 // ConvTranspose2d(k=2, s=2): y[n, 2h+i, 2w+j, yoff + co] = bias[co] + sum_ci x[n,h,w,ci] * wf[co][i][j][ci]
@@ -680,6 +683,17 @@ void bn_bwd_apply(const at::Tensor& dy, int lddy, int dyoff, const c10::optional
         "bn_bwd_apply");
 }
 
+// w2 [C][2K] = {wT * coef[0], wT * coef[1]}, b [C] = wT . coef[2]: the dual 1x1 data gradient (bn.hip)
+void dual_dgrad_weights(const at::Tensor& wT, int C, int K, const at::Tensor& coef, at::Tensor w2, at::Tensor b) {
+  same_type(wT, w2, "dual_dgrad_weights w2");
+  if (wT.numel() < (int64_t)C * K || w2.numel() < (int64_t)C * 2 * K || coef.numel() < 3 * (int64_t)K ||
+      b.numel() < C || b.scalar_type() != at::kFloat || coef.scalar_type() != at::kFloat)
+    throw std::runtime_error("dual_dgrad_weights: shapes / dtypes");
+  check(dlmpi_dual_dgrad_weights(wT.data_ptr(), C, K, ptr<float>(coef), w2.data_ptr(), ptr<float>(b),
+                                 act_f32(wT, "dual_dgrad_weights"), cur_stream()),
+        "dual_dgrad_weights");
+}
+
 void channel_sum(const at::Tensor& x, int64_t M, int C, int ldx, int xoff, at::Tensor out_acc) {
   const int nblk = dlmpi_reduce_blocks(M, C);
   at::Tensor partial = at::empty({(int64_t)nblk * 2 * C}, x.options().dtype(at::kFloat));
@@ -905,6 +919,7 @@ void register_ops(pybind11::module& m) {
   m.def("bn_bwd_finalize", &bn_bwd_finalize);
   m.def("bn_bwd_finalize_fused", &bn_bwd_finalize_fused);
   m.def("bn_bwd_apply", &bn_bwd_apply);
+  m.def("dual_dgrad_weights", &dual_dgrad_weights);
   m.def("channel_sum", &channel_sum);
   m.def("maxpool_fwd", &maxpool_fwd);
   m.def("maxpool_bwd", &maxpool_bwd);

@@ -623,6 +623,35 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const T* __restrict__
   }
 }
 
+
+// Weights of the "dual" data gradient of a 1x1 stride-1 convolution whose input gradient passes
+// through a training BatchNorm (models/engine.py:ConvUnit, dual path): instead of materialising
+// dz = k1*dy + k2*z + k3 (coef [3][K]) and running dx = dz . W, the GEMM reduces over [dy | z]
+// (2K channels, stored side by side) with
+//   w2[c][k] = W[c][k] * k1[k],   w2[c][K + k] = W[c][k] * k2[k]   (rounded to the storage type),
+//   b[c] = sum_k W[c][k] * k3[k]   (fp32 epilogue bias; fixed-order tree, deterministic).
+// W is the data-gradient compute copy [C][K] (CRSK of a 1x1 conv); one block per row c.
+template <typename T>
+__global__ __launch_bounds__(256) void dual_dgrad_weights_kernel(const T* __restrict__ w, int K,
+                                                                 const float* __restrict__ coef,
+                                                                 T* __restrict__ w2, float* __restrict__ b) {
+  __shared__ float red[4];
+  const int c = blockIdx.x;
+  const T* wr = w + (int64_t)c * K;
+  T* o = w2 + (int64_t)c * 2 * K;
+  float acc = 0.f;
+  for (int k = threadIdx.x; k < K; k += 256) {
+    const float wv = load1(wr + k);
+    store1(o + k, wv * coef[k]);
+    store1(o + K + k, wv * coef[K + k]);
+    acc = __builtin_fmaf(wv, coef[2 * K + k], acc);
+  }
+  acc = warp_sum(acc);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) b[c] = (red[0] + red[1]) + (red[2] + red[3]);
+}
+
 static inline unsigned ew_blocks(int64_t total) {
   int64_t b = (total + 255) / 256;
   if (b > 8192) b = 8192;
@@ -886,6 +915,14 @@ extern "C" hipError_t dlmpi_bn_bwd_apply(const void* dy, int lddy, int dyoff, co
   const int64_t total = M * (C / 8);
   DLMPI_TLAUNCH(bn_bwd_apply_kernel, dim3(ew_blocks(total)), CT(dy), lddy, dyoff, CT(ymask), ldym, ymoff, CT(x), ldx,
                 xoff, M, C, make_fastdiv(C / 8), coef, MT(dx), MT(dyr_out));
+  return hipGetLastError();
+}
+
+
+extern "C" hipError_t dlmpi_dual_dgrad_weights(const void* w, int C, int K, const float* coef, void* w2, float* b,
+                                               int f32, hipStream_t s) {
+  if (C <= 0 || K <= 0) return hipErrorInvalidValue;
+  DLMPI_TLAUNCH(dual_dgrad_weights_kernel, dim3(C), CT(w), K, coef, MT(w2), b);
   return hipGetLastError();
 }
 

@@ -188,6 +188,9 @@ hipError_t dlmpi_bn_bwd_finalize_ex(const float* partial, int nblk, int ns, int 
 hipError_t dlmpi_bn_bwd_apply(const void* dy, int lddy, int dyoff, const void* ymask, int ldym, int ymoff,
                               const void* x, int ldx, int xoff, int64_t M, int C, const float* coef, void* dx,
                               void* dyr_out, int f32, hipStream_t s);
+// [dy | z] weights of the dual 1x1 data gradient: w2 [C][2K] = {W*k1, W*k2}, b [C] = W . k3 (coef [3][K])
+hipError_t dlmpi_dual_dgrad_weights(const void* w, int C, int K, const float* coef, void* w2, float* b, int f32,
+                                    hipStream_t s);
 hipError_t dlmpi_channel_sum(const void* x, int64_t M, int C, int ldx, int xoff, float* out_acc, float* partial,
                              int nblk, double* ws, int f32, hipStream_t s);
 int dlmpi_reduce_blocks(int64_t M, int C);

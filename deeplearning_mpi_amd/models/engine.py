@@ -111,6 +111,20 @@ DEFER_BN_FWD = os.environ.get("DLMPI_DEFER_BN_FWD", "0") != "0"
 DEFER_BN_BWD = os.environ.get("DLMPI_DEFER_BN_BWD", "0") != "0"
 DEFER_BN_WGRAD = os.environ.get("DLMPI_DEFER_BN_WGRAD", "1") != "0"
 
+# Dual data gradient of 1x1 stride-1 convolutions behind a training BN (ConvUnit.dual): the forward
+# stores the BN input z in the right half of a [rows][2K] buffer whose left half later receives the
+# BN's output gradient dy, so the data gradient reduces over [dy | z] with weights {W*k1, W*k2} and
+# bias W.k3 -- dx = dz.W without dz -- and the BN-backward apply pass (dz = k1 dy + k2 z + k3, needed
+# only by the weight gradient now) moves to the side stream, off the data-gradient critical path.
+# DLMPI_DUAL_DGRAD=0: off; DLMPI_DUAL_MIN_ROWS: only layers with at least this many output pixels
+# (N*P*Q; memory-bound 1x1 GEMMs -- the doubled reduction costs MFMA time on the small deep layers).
+DUAL_DGRAD = os.environ.get("DLMPI_DUAL_DGRAD", "1") != "0"
+DUAL_MIN_ROWS = int(os.environ.get("DLMPI_DUAL_MIN_ROWS", str(256 * 28 * 28)))
+# The dual path's weight gradient rebuilds dz in its operand prologue (PA 2) from the same [dy | z]
+# buffer; DLMPI_DUAL_WGRAD_PRO=0: an apply pass materialises dz on the side stream first (measured
+# slower: that pass competes with the main stream for HBM, profiles/r2_dual_dgrad)
+DUAL_WGRAD_PRO = os.environ.get("DLMPI_DUAL_WGRAD_PRO", "1") != "0"
+
 # DLMPI_CHUNK_FWD=1: run each forward BN-apply in two image chunks interleaved with its consumer's
 # GEMM on the main + side streams (PendingApply).  Off by default: measured slower (ResNet-50 bs 256
 # 11,501 vs 11,894 img/s, ResNet-152 3,963 vs 4,390; profiles/r2_chunk_fwd_rejected) -- the bn_apply
@@ -226,6 +240,18 @@ class ConvUnit:
         self.bias = conv.bias
         self._bias_pad = None
 
+    dual = False   # set by the model for 1x1 stride-1 convs behind a training BN (DUAL_DGRAD)
+
+    def dy_slot(self, ctx) -> Optional[Act]:
+        """Where the producer of this unit's output gradient should write it: the left half of the
+        forward's [rows][2K] z buffer when the dual data gradient is on for this step, else None."""
+        if not self.dual or ctx is None:
+            return None
+        z = ctx[1]
+        if z is None or z.off != z.C or z.ld != 2 * z.C:
+            return None
+        return Act(z.buf, z.N, z.H, z.W, z.C, 0)
+
     def out_hw(self, H, W):
         return ((H + 2 * self.pad - self.R) // self.stride + 1, (W + 2 * self.pad - self.S) // self.stride + 1)
 
@@ -320,7 +346,13 @@ class ConvUnit:
                         relu=self.relu, kvalid=y.C if y.C < self.Kp else 0)
             return y, ((x, y) if save else None)
         if train:
-            z = Act.empty(N, P, Q, self.Kp, be.act_dtype, dev)
+            if (self.dual and DUAL_DGRAD and save and not defer_apply and self.stride == 1 and self.R == 1
+                    and self.S == 1 and N * P * Q >= DUAL_MIN_ROWS and hasattr(be, "dual_weights")):
+                # [dy | z]: z on the right, the BN's output gradient later on the left (dy_slot)
+                z = Act(torch.empty(N * P * Q, 2 * self.Kp, dtype=be.act_dtype, device=dev), N, P, Q, self.Kp,
+                        self.Kp)
+            else:
+                z = Act.empty(N, P, Q, self.Kp, be.act_dtype, dev)
             if chunked:
                 stats, mt = self._conv_chunked(be, x, wf, z)
                 x = x.y
@@ -382,7 +414,7 @@ class ConvUnit:
         return BwdFuse(None, z, None, scale, shift)
 
     def bwd(self, be, ctx, dy: Act, need_dx=True, dx_res: Act = None, dyr_out: Act = None, ymask: Act = None,
-            use_own_mask=True, pre=None, k2=1, fuse_next=None, colsum=False, before_res=None):
+            use_own_mask=True, pre=None, k2=1, fuse_next=None, colsum=False, before_res=None, dx_out: Act = None):
         """Backward of the unit.
 
         pre:       BN-backward partials already produced by the dgrad epilogue that wrote ``dy``
@@ -393,10 +425,33 @@ class ConvUnit:
                    returns (dx, partials [tiles][2][C]).
         before_res: called right before the data-gradient GEMM that adds ``dx_res`` (a residual
                    gradient produced on another stream is joined there, after this unit's BN backward).
+        dx_out:    where to write dx (the consumer's dy_slot), else a fresh buffer.
         """
         ar = self.arena
         bn = self.bn
-        if bn is not None:
+        dg_in, dg_w, dg_b = None, None, None   # data-gradient GEMM operand / weights / bias (dual path)
+        if bn is not None and need_dx and pre is not None and dyr_out is None and self.dual:
+            x, z = ctx[0], ctx[1]
+            if (z.off == z.C and z.ld == 2 * z.C and dy.off == 0 and dy.ld == z.ld
+                    and dy.buf.data_ptr() == z.buf.data_ptr()):
+                # dual: finalize only on this stream; dz for the weight gradient on the side stream
+                mean, invstd = ctx[3], ctx[4]
+                gam = bn.weight.data if bn.affine else None
+                dzd = be.bn_bwd_deferred(dy, z, mean, invstd, gam, ar.grad_flat(bn.weight) if bn.affine else None,
+                                         ar.grad_flat(bn.bias) if bn.affine else None, pre=pre, k2=k2)
+                with grad_side(be, *bufs(dzd, x)):
+                    if bn.affine:
+                        ar.ready(bn.weight, bn.bias)
+                    if self.bias is not None:
+                        ar.ready(self.bias)
+                    self._wgrad(be, dzd if (DUAL_WGRAD_PRO and getattr(be, "prologue", False)) else be.materialize(dzd), x)
+                    ar.ready(self.conv.weight)
+                dg_w, dg_b = be.dual_weights(ar.get_compute(self.h_dg), self.Cp, self.Kp, dzd.k0)
+                dg_in = Act(z.buf, z.N, z.H, z.W, 2 * z.C)
+                bn = None   # handled
+        if dg_in is not None:
+            x = ctx[0]
+        elif bn is not None:
             x, z, y, mean, invstd = ctx[:5]
             if pre is not None:
                 mask = None
@@ -445,7 +500,15 @@ class ConvUnit:
             return None
         if before_res is not None:
             before_res()
-        dx = Act.empty(x.N, x.H, x.W, self.Cp, be.act_dtype, x.device)
+        if dx_out is not None:
+            assert (dx_out.N, dx_out.H, dx_out.W, dx_out.C) == (x.N, x.H, x.W, self.Cp), (dx_out, x, self.Cp)
+            dx = dx_out
+        else:
+            dx = Act.empty(x.N, x.H, x.W, self.Cp, be.act_dtype, x.device)
+        if dg_in is not None:
+            part = be.conv_dgrad(dg_in, dg_w, self.Cp, 1, 1, 1, 0, dx, res=dx_res, fuse=fuse_next, colsum=colsum,
+                                 bias=dg_b)
+            return (dx, part) if (fuse_next is not None or colsum) else dx
         if (self.K == 1 and self.R == 1 and self.S == 1 and self.stride == 1 and dx_res is None and not colsum
                 and fuse_next is not None and fuse_next.scale is not None and fuse_next.z2 is None
                 and hasattr(be, "outer_dgrad_bn") and _OUTER_DGRAD):

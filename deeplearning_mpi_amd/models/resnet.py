@@ -82,6 +82,8 @@ class Bottleneck(nn.Module):
     def units(self, ar):
         u = [ConvUnit(ar, self.conv1, self.bn1, relu=True), ConvUnit(ar, self.conv2, self.bn2, relu=True),
              ConvUnit(ar, self.conv3, self.bn3, relu=True)]
+        # 1x1 stride-1 convs: data gradient over [dy | z] without materialising dz (engine.DUAL_DGRAD)
+        u[0].dual = u[2].dual = True
         ud = ConvUnit(ar, self.downsample[0], self.downsample[1], relu=False) if self.downsample is not None else None
         return u, ud
 
@@ -145,11 +147,17 @@ class _BlockExec:
         ctxs, cd = st
         return ConvUnit.fuse_spec(ctxs[-1], z2=cd[1] if cd is not None else None)
 
-    def bwd(self, be, st, dy: Act, pre=None, fuse_prev=None, fuse_inner=False):
+    def out_slot(self, st):
+        """Where the block-output gradient should be written (the last unit's dy_slot) or None."""
+        return self.u[-1].dy_slot(st[0][-1])
+
+    def bwd(self, be, st, dy: Act, pre=None, fuse_prev=None, fuse_inner=False, dx_out=None):
         """dy: gradient of the block output.  With ``pre`` (partials from the producer's dgrad
         epilogue) dy is already ReLU-masked.  With ``fuse_prev`` the block-input gradient is
-        produced masked for the previous block and returned with its partials."""
+        produced masked for the previous block and returned with its partials.  dx_out: where to
+        write the block-input gradient (the previous block's out_slot)."""
         ctxs, cd = st
+        slot = lambda k: self.u[k].dy_slot(ctxs[k])   # noqa: E731
         ylast = ctxs[-1][2]
         n = len(self.u)
         spec = lambda k: ConvUnit.fuse_spec(ctxs[k])   # noqa: E731
@@ -164,9 +172,9 @@ class _BlockExec:
                 with torch.cuda.stream(br):
                     dres = self.ud.bwd(be, cd, dy, pre=pre, k2=2)
                 record_on(br, dy, pre)
-            dh, part = self.u[-1].bwd(be, ctxs[-1], dy, pre=pre, k2=1, fuse_next=spec(n - 2))
+            dh, part = self.u[-1].bwd(be, ctxs[-1], dy, pre=pre, k2=1, fuse_next=spec(n - 2), dx_out=slot(n - 2))
             for k in range(n - 2, 0, -1):
-                dh, part = self.u[k].bwd(be, ctxs[k], dh, pre=part, fuse_next=spec(k - 1))
+                dh, part = self.u[k].bwd(be, ctxs[k], dh, pre=part, fuse_next=spec(k - 1), dx_out=slot(k - 1))
             join = None
             if br is not None:
                 def join():   # dres is first read by conv1's data-gradient GEMM, after its BN backward
@@ -179,31 +187,33 @@ class _BlockExec:
                 dres = self.ud.bwd(be, cd, dy, pre=pre, k2=2)
             else:
                 dres = dy
-            return self.u[0].bwd(be, ctxs[0], dh, dx_res=dres, pre=part, fuse_next=fuse_prev, before_res=join)
+            return self.u[0].bwd(be, ctxs[0], dh, dx_res=dres, pre=part, fuse_next=fuse_prev, before_res=join,
+                                 dx_out=dx_out)
         # fused BN-backward partials for the inner units also when the block's output gradient comes
         # without them (the last block, behind the average-pool backward); required when their BN +
         # ReLU output was deferred (never stored: ctx y is None), so the mask is recomputed from z
         inner = fuse_inner or any(c[2] is None for c in ctxs[:-1])
         if self.ud is None:
             dyr = Act.empty(dy.N, dy.H, dy.W, dy.C, be.act_dtype, dy.device)   # identity-path grad
-            dh = self.u[-1].bwd(be, ctxs[-1], dy, dyr_out=dyr, fuse_next=spec(n - 2) if inner else None)
+            dh = self.u[-1].bwd(be, ctxs[-1], dy, dyr_out=dyr, fuse_next=spec(n - 2) if inner else None,
+                                dx_out=slot(n - 2))
         else:
             dyr = None
-            dh = self.u[-1].bwd(be, ctxs[-1], dy, fuse_next=spec(n - 2) if inner else None)
+            dh = self.u[-1].bwd(be, ctxs[-1], dy, fuse_next=spec(n - 2) if inner else None, dx_out=slot(n - 2))
         part = None
         if inner:
             dh, part = dh
         for k in range(n - 2, 0, -1):
             if inner:
-                dh, part = self.u[k].bwd(be, ctxs[k], dh, pre=part, fuse_next=spec(k - 1))
+                dh, part = self.u[k].bwd(be, ctxs[k], dh, pre=part, fuse_next=spec(k - 1), dx_out=slot(k - 1))
             else:
-                dh = self.u[k].bwd(be, ctxs[k], dh)
+                dh = self.u[k].bwd(be, ctxs[k], dh, dx_out=slot(k - 1))
         if self.ud is not None:
             # downsample BN sees the same relu-masked output grad as the main branch
             dres = self.ud.bwd(be, cd, dy, ymask=ylast)
         else:
             dres = dyr
-        out = self.u[0].bwd(be, ctxs[0], dh, dx_res=dres, pre=part, fuse_next=fuse_prev)
+        out = self.u[0].bwd(be, ctxs[0], dh, dx_res=dres, pre=part, fuse_next=fuse_prev, dx_out=dx_out)
         return out
 
 
@@ -320,7 +330,8 @@ class ResNet(EngineModule):
         pre = None
         for i in range(len(self.blocks) - 1, -1, -1):
             fuse_prev = self.blocks[i - 1].fuse_spec(st_blocks[i - 1]) if (i > 0 and self.fuse_bn_bwd) else None
-            out = self.blocks[i].bwd(be, st_blocks[i], da, pre=pre, fuse_prev=fuse_prev, fuse_inner=self.fuse_bn_bwd)
+            out = self.blocks[i].bwd(be, st_blocks[i], da, pre=pre, fuse_prev=fuse_prev, fuse_inner=self.fuse_bn_bwd,
+                                     dx_out=self.blocks[i - 1].out_slot(st_blocks[i - 1]) if i > 0 else None)
             da, pre = out if fuse_prev is not None else (out, None)
         dh = Act.empty(h.N, h.H, h.W, h.C, be.act_dtype, h.device)
         if self.fuse_bn_bwd:   # stem BN-backward statistics in the max-pool backward (mask from z)

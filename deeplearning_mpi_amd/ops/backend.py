@@ -131,11 +131,13 @@ class NativeBackend:
         return self.C.conv2d_fwd_bnbwd(x.buf, x.N, x.H, x.W, x.C, x.ld, x.off, w, K, R, S, stride, pad, y.buf, y.ld,
                                        y.off, z.buf, z.ld, z.off, fuse.scale, fuse.shift)
 
-    def conv_dgrad(self, dy: Act, wT, C, R, S, stride, pad, dx: Act, res: Act = None, fuse=None, colsum=False):
+    def conv_dgrad(self, dy: Act, wT, C, R, S, stride, pad, dx: Act, res: Act = None, fuse=None, colsum=False,
+                   bias=None):
         """fuse = BwdFuse(mask, z, z2, scale, shift): dx is the gradient of relu(BN(z) [+ BN2(z2)]);
         the epilogue applies the ReLU mask (y > 0, or z*scale + shift > 0 without a residual) and
         returns BN-backward partials [tiles][2|3][C].  colsum (no fuse): returns per-tile
-        {sum dx, sum dx^2} [tiles][2][C] of the stored dx instead."""
+        {sum dx, sum dx^2} [tiles][2][C] of the stored dx instead.  bias: fp32 [C] added to the
+        GEMM result first (the dual 1x1 data gradient's W . k3 term)."""
         m, z, z2, sc, sh, mb = fuse if fuse is not None else (None, None, None, None, None, None)
 
         def t(a):
@@ -144,7 +146,15 @@ class NativeBackend:
         dy, pm, k0, k1, zb, zld, zoff = self._pro(dy)
         return self.C.conv2d_dgrad_pro(dy.buf, dy.N, dy.H, dy.W, dy.C, dy.ld, dy.off, wT, C, R, S, stride, pad, dx.H,
                                        dx.W, dx.buf, dx.ld, dx.off, *t(res), *t(m), *t(z), *t(z2), sc, sh, mb,
-                                       bool(colsum and fuse is None), pm, k0, k1, zb, zld, zoff)
+                                       bool(colsum and fuse is None), pm, k0, k1, zb, zld, zoff, bias)
+
+    def dual_weights(self, wT, C, K, coef):
+        """[dy | z] weights of the dual 1x1 data gradient (engine.ConvUnit, dual path): w2 [C][2K] =
+        {wT * coef[0], wT * coef[1]} in the storage type, b [C] = wT . coef[2] in fp32."""
+        w2 = torch.empty(C, 2 * K, dtype=self.act_dtype, device=self.device)
+        b = torch.empty(C, dtype=torch.float32, device=self.device)
+        self.C.dual_dgrad_weights(wT, C, K, coef, w2, b)
+        return w2, b
 
     def convT_fwd(self, x: Act, wf, Cout, y: Act, bias=None):
         self.C.convT2x2_fwd(x.buf, x.N, x.H, x.W, x.C, x.ld, x.off, wf, Cout, y.buf, y.ld, y.off, bias)
@@ -416,11 +426,19 @@ class RefBackend:
             out = F.relu(out)
         self._store(y, out)
 
-    def conv_dgrad(self, dy, wT, C, R, S, stride, pad, dx: Act, res=None, fuse=None, colsum=False):
+    def dual_weights(self, wT, C, K, coef):
+        w = wT.reshape(C, K).to(self.dt)
+        c = coef.to(self.dt)
+        w2 = torch.cat([w * c[0], w * c[1]], 1).to(self.act_dtype)
+        return w2, (w * c[2]).sum(1)
+
+    def conv_dgrad(self, dy, wT, C, R, S, stride, pad, dx: Act, res=None, fuse=None, colsum=False, bias=None):
         dy = self.materialize(dy)
         K = dy.C
         wk = wT.view(C, R, S, K).permute(3, 0, 1, 2).to(self.dt)
         g = torch.nn.grad.conv2d_input((dx.N, C, dx.H, dx.W), wk, dy.nchw().to(self.dt), stride, pad)
+        if bias is not None:
+            g = g + bias.to(self.dt).view(1, -1, 1, 1)
         if res is not None:
             g = g + res.nchw().to(self.dt)
         if fuse is None:

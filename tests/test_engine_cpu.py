@@ -228,3 +228,29 @@ def test_chunked_forward_bn_apply_matches_torch(arch, monkeypatch):
     # every conv whose input is a BN-apply output, except conv1 of blocks with a downsample branch
     # (the branch reads the whole input): resnet18 2*8 - 3 - 1(stem pool input) = 12, resnet50 3*16 - 4
     assert len(calls) == (12 if arch == "resnet18" else 44)
+
+
+def test_dual_dgrad_matches_torch(monkeypatch):
+    """1x1 data gradients over [dy | z] with weights {W*k1, W*k2} and bias W.k3 (engine.DUAL_DGRAD,
+    dz only materialised for the weight gradient): the fp64 engine still reproduces autograd, and
+    the dual path is taken for every eligible 1x1 conv (all but the last block's conv3, whose
+    gradient comes from the average-pool backward)."""
+    from deeplearning_mpi_amd.models import engine
+
+    monkeypatch.setattr(engine, "DUAL_DGRAD", True)
+    monkeypatch.setattr(engine, "DUAL_MIN_ROWS", 0)
+    calls = []
+    orig = engine.ConvUnit.bwd
+
+    def counted(self, be, ctx, dy, *a, **k):
+        if self.dual and ctx is not None and ctx[1] is not None and ctx[1].ld == 2 * ctx[1].C \
+                and dy.buf.data_ptr() == ctx[1].buf.data_ptr():
+            calls.append(self)
+        return orig(self, be, ctx, dy, *a, **k)
+
+    monkeypatch.setattr(engine.ConvUnit, "bwd", counted)
+    g = torch.Generator().manual_seed(4)
+    x = torch.randn(4, 3, 64, 64, generator=g)
+    y = torch.randint(10, (4,), generator=g)
+    _run_pair(lambda: resnet50(num_classes=10), x, y, cross_entropy, F.cross_entropy)
+    assert len(calls) == 2 * 16 - 1
