@@ -230,7 +230,8 @@ def test_chunked_forward_bn_apply_matches_torch(arch, monkeypatch):
     assert len(calls) == (12 if arch == "resnet18" else 44)
 
 
-def test_dual_dgrad_matches_torch(monkeypatch):
+@pytest.mark.parametrize("fused", [True, False])
+def test_dual_dgrad_matches_torch(monkeypatch, fused):
     """1x1 data gradients over [dy | z] with weights {W*k1, W*k2} and bias W.k3 (engine.DUAL_DGRAD,
     dz only materialised for the weight gradient): the fp64 engine still reproduces autograd, and
     the dual path is taken for every eligible 1x1 conv (all but the last block's conv3, whose
@@ -252,5 +253,10 @@ def test_dual_dgrad_matches_torch(monkeypatch):
     g = torch.Generator().manual_seed(4)
     x = torch.randn(4, 3, 64, 64, generator=g)
     y = torch.randint(10, (4,), generator=g)
-    _run_pair(lambda: resnet50(num_classes=10), x, y, cross_entropy, F.cross_entropy)
-    assert len(calls) == 2 * 16 - 1
+    def make():
+        m = resnet50(num_classes=10)
+        m.fuse_bn_bwd = fused   # unfused: dy still lands in the [dy | z] buffers, read with their stride
+        return m
+
+    _run_pair(make, x, y, cross_entropy, F.cross_entropy)
+    assert len(calls) == 2 * 16 - 1   # dy written into the [dy | z] buffer (dual GEMM only when fused)
