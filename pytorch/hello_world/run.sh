@@ -16,7 +16,7 @@ ask BACKEND "Backend (nccl, gloo or mpi)" gloo
 ask OP "Operation (send, allreduce, both)" both
 MPIRUN=$(command -v mpirun || echo /opt/conda/bin/mpirun)
 if [ "$LAUNCHER" = "mpirun" ]; then
-  exec "$MPIRUN" -n "$NPROC" python hello_world.py --backend "$BACKEND" --op "$OP"
+  exec "$MPIRUN" ${HOSTFILE:+-hostfile "$HOSTFILE"} -n "$NPROC" python hello_world.py --backend "$BACKEND" --op "$OP"
 else
   exec python -m torch.distributed.run --nproc_per_node="$NPROC" --nnodes="$NNODES" --node_rank="$NODE_RANK" \
        --master_addr="$MASTER_ADDR" --master_port="$MASTER_PORT" hello_world.py --backend "$BACKEND" --op "$OP"

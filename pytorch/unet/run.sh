@@ -1,6 +1,7 @@
 #!/bin/bash
 # UNet launcher (reference: pytorch/unet/run.sh -- torchrun + interactive prompts with defaults).
-# Defaults to mpirun; LAUNCHER=torchrun for the reference-style launch.  PROMPT=1 asks interactively.
+# Defaults to mpirun (HOSTFILE=<file>: ranks over several nodes, NPROC_PER_NODE * NNODES in total);
+# LAUNCHER=torchrun for the reference-style launch.  PROMPT=1 asks interactively.
 set -e
 cd "$(dirname "$0")"
 validate_ip() {
@@ -33,7 +34,7 @@ mkdir -p "$MODEL_DIR" logs
 ARGS="--num_epochs $NUM_EPOCHS --batch_size $BATCH_SIZE --learning_rate $LEARNING_RATE --random_seed $RANDOM_SEED --model_dir $MODEL_DIR --model_filename $MODEL_FILENAME $RESUME $EXTRA"
 MPIRUN=$(command -v mpirun || echo /opt/conda/bin/mpirun)
 if [ "$LAUNCHER" = "mpirun" ]; then
-  exec "$MPIRUN" -n "$((NPROC_PER_NODE * NNODES))" python train.py $ARGS
+  exec "$MPIRUN" ${HOSTFILE:+-hostfile "$HOSTFILE"} -n "$((NPROC_PER_NODE * NNODES))" python train.py $ARGS
 else
   exec python -m torch.distributed.run --nproc_per_node=$NPROC_PER_NODE --nnodes=$NNODES --node_rank=$NODE_RANK \
        --master_addr=$MASTER_ADDR --master_port=$MASTER_PORT train.py $ARGS
