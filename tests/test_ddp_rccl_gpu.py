@@ -75,8 +75,15 @@ def _check(make, make_opt, loss_fn, batches, aux):
         comm.destroy()
 
 
-def test_resnet50_rccl_reducer_eager_and_graph_match_single_process():
-    from deeplearning_mpi_amd.models import resnet50
+@pytest.mark.parametrize("dual", [False, True])
+def test_resnet50_rccl_reducer_eager_and_graph_match_single_process(dual, monkeypatch):
+    """dual: the dual 1x1 data gradient (models/engine.py DUAL_DGRAD) forced on every eligible conv
+    (at the bench size it is on for layers 1-2), so its weight kernel, the [dy | z] GEMMs and the
+    prologue weight gradients run under the reducer and inside the captured graph too."""
+    from deeplearning_mpi_amd.models import engine, resnet50
+
+    monkeypatch.setattr(engine, "DUAL_DGRAD", True)
+    monkeypatch.setattr(engine, "DUAL_MIN_ROWS", 0 if dual else 1 << 40)
     from deeplearning_mpi_amd.ops import cross_entropy
     from deeplearning_mpi_amd.optim import SGD
 
