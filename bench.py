@@ -185,12 +185,20 @@ def main():
     comm.barrier()
     sync()
     dt = time.perf_counter() - t0
-    tmax = torch.tensor([dt], dtype=torch.float64, device=dev)
-    comm.allreduce(tmax, "max")
-    dt = float(tmax.item())
+    # every rank's own wall time: the job's number is the slowest rank (MAX), min/max go to the JSON
+    mine = torch.tensor([dt], dtype=torch.float64, device=dev)
+    allt = torch.empty(world, dtype=torch.float64, device=dev)
+    comm.allgather(allt, mine)
+    per_rank_ms = [round(float(v) / args.steps * 1000, 3) for v in allt.cpu()]
+    dt = float(allt.max().item())
     lossv = float(loss.item())
     global_batch = cfg["batch"] * world
     ips = global_batch * args.steps / dt
+    # N > 1: a few untimed HIP-event-timed steps after the timed region answer "how much all-reduce
+    # was left exposed after the backward pass" in the same JSON line
+    if args.breakdown == 0 and world > 1 and not args.graph:
+        args.breakdown = 3
+    bd_max = None
     if args.breakdown > 0 and not args.graph:
         # untimed extra steps: per-phase GPU time from HIP events (no host sync inside a step)
         from deeplearning_mpi_amd.utils.profiler import StepTimer
@@ -214,9 +222,9 @@ def main():
         bd.setdefault("comm_exposed", 0.0)
         bdt = torch.tensor([bd["comm_exposed"], bd["step"]], dtype=torch.float64, device=dev)
         comm.allreduce(bdt, "max")
+        bd_max = {"comm_exposed": round(float(bdt[0]), 3), "step": round(float(bdt[1]), 3)}
         if comm.rank == 0:
-            print(json.dumps({"breakdown_ms_per_step": bd, "max_over_ranks": {"comm_exposed": float(bdt[0]),
-                                                                             "step": float(bdt[1])},
+            print(json.dumps({"breakdown_ms_per_step": bd, "max_over_ranks": bd_max,
                               "n_gpus": world, "config": args.config}), file=sys.stderr, flush=True)
     if args.mem and comm.rank == 0 and dev.type == "cuda":
         ms = torch.cuda.memory_stats(dev)
@@ -226,6 +234,17 @@ def main():
                                   "ooms": ms.get("num_ooms", 0),
                                   "device_total_gb": round(torch.cuda.get_device_properties(dev).total_memory / 2 ** 30, 1)}}),
               file=sys.stderr, flush=True)
+    # distributed facts of this run: the world size RCCL itself reports, its CU (channel) budget,
+    # the gradient bucket layout, per-rank step times and the exposed all-reduce (max over ranks)
+    native_comm = getattr(getattr(comm, "inner", comm), "c", None)
+    dist_info = {
+        "rccl_world_size": int(native_comm.size()) if native_comm is not None else None,
+        "rccl_channels": os.environ.get("NCCL_MAX_NCHANNELS") if native_comm is not None else None,
+        "bucket_mb": [round(b, 2) for b in ddp.bucket_sizes_mb()],
+        "reducer": ddp.reducer is not None,
+        "per_rank_ms_per_step": {"min": min(per_rank_ms), "max": max(per_rank_ms)},
+        "comm_exposed_ms": bd_max["comm_exposed"] if bd_max else None,
+    }
     if comm.rank == 0:
         headline = args.config == "resnet50" and cfg == PRESETS["resnet50"]
         print(json.dumps({
@@ -247,6 +266,7 @@ def main():
                        "parallelism": f"dp{world}", "backend": comm.backend, "device": dev.type,
                        "optimizer": optname, "hipgraph": bool(args.graph),
                        "final_loss": round(lossv, 4)},
+            "dist": dist_info,
         }), flush=True)
     dl.destroy_distributed()
 

@@ -71,17 +71,19 @@ def build_argparser(variant: str = "main") -> argparse.ArgumentParser:
     return p
 
 
-def use_graph(args, device, pixels=None) -> bool:
+def use_graph(args, device, pixels=None, comm_backend="single") -> bool:
     """--graph auto: capture the step when it is launch-bound -- native bf16 kernels on a GPU and a
     step smaller than the auxiliary-stream threshold (N*H*W < DLMPI_AUX_MIN_PIXELS, default 1M:
     the reference's ResNet-18 on CIFAR, 46k -> 85k img/s).  Larger steps run their weight-gradient
     and residual-branch streams concurrently, which a replayed graph loses (measured: ResNet-50
-    bs 256 -7 %, ResNet-152 -13 %, UNet 512 -2 %, profiles/r2_graph_ab)."""
+    bs 256 -7 %, ResNet-152 -13 %, UNet 512 -2 %, profiles/r2_graph_ab).  Auto mode also requires a
+    capturable data plane: RCCL (device collectives on the comm stream) or a single rank -- gloo's
+    host-staged collectives (the DLMPI_GLOO_DEVICE=cuda rehearsal) cannot live inside a hipGraph."""
     if args.graph in (True, "1"):
         return device.type == "cuda"
     if args.graph in (False, "0"):
         return False
-    if device.type != "cuda":
+    if device.type != "cuda" or comm_backend not in ("rccl", "single"):
         return False
     if pixels is None:
         side = args.image_size if getattr(args, "synthetic", False) else 32
@@ -122,7 +124,7 @@ def run(args) -> dict:
     model.precision = args.precision
     ddp = parallel.DistributedDataParallel(model, bucket_cap_mb=args.bucket_mb)
     model_filepath = os.path.join(args.model_dir, args.model_filename)
-    args.graph = use_graph(args, device)
+    args.graph = use_graph(args, device, comm_backend=getattr(comm, "backend", "single"))
 
     # the training step reads its batch from fixed tensors so that it can be captured (--graph)
     x_static = torch.empty((args.batch_size, 3, args.image_size, args.image_size) if args.synthetic else
@@ -141,7 +143,9 @@ def run(args) -> dict:
         test_set = DeviceImageDataset.cifar10(args.data_root, False, device, augment=False)
     else:
         # download=False semantics: the data must already be under data_root (see download.py)
-        train_set = CIFAR10(args.data_root, train=True, transform=CifarTransform(True), seed=args.random_seed + rank)
+        # augmentation = f(seed, epoch, index) (data/datasets.py SampleRng): rank-, worker- and
+        # resume-independent
+        train_set = CIFAR10(args.data_root, train=True, transform=CifarTransform(True), seed=args.random_seed)
         test_set = CIFAR10(args.data_root, train=False, transform=CifarTransform(False))
     sampler = DistributedSampler(train_set, seed=0)
     if on_device and not args.synthetic:
@@ -150,10 +154,13 @@ def run(args) -> dict:
         test_loader = DeviceBatches(test_set, test_bs)
     else:
         pin = device.type == "cuda"
+        # workers are re-created every epoch (reference default) so they see the dataset's epoch
         train_loader = DataLoader(train_set, batch_size=args.batch_size, sampler=sampler, num_workers=args.workers,
-                                  pin_memory=pin, persistent_workers=args.workers > 0)
+                                  pin_memory=pin)
+        # a private generator: rank-0-only evaluation must not advance the global host RNG (its
+        # state is the resume state every rank restores)
         test_loader = DataLoader(test_set, batch_size=test_bs, shuffle=False, num_workers=args.workers,
-                                 pin_memory=pin)
+                                 pin_memory=pin, generator=torch.Generator().manual_seed(args.random_seed))
     criterion = CrossEntropyLoss()
     optimizer = SGD(model.parameters(), lr=args.learning_rate, momentum=0.9, weight_decay=1e-5)
     start_epoch = 0
@@ -172,7 +179,8 @@ def run(args) -> dict:
 
     captured = None
     if args.graph and device.type == "cuda":
-        captured = CapturedStep(lambda: train_step(x_static, y_static), warmup=2, inputs=(x_static, y_static))
+        captured = CapturedStep(lambda: train_step(x_static, y_static), warmup=2, inputs=(x_static, y_static),
+                                comm=comm)
 
     if args.benchmark_steps:
         return benchmark(args, train_step, captured, x_static, y_static, comm, device)
@@ -180,8 +188,9 @@ def run(args) -> dict:
     history = {"loss": [], "accuracy": [], "images_per_sec": []}
 
     def eval_and_save(epoch, next_epoch):
+        state = resume_state(next_epoch)   # RNG states of the epoch boundary, taken before evaluating
         accuracy = evaluate(model, device, test_loader)
-        save_checkpoint(ddp, model_filepath, optimizer=optimizer, extra=resume_state(next_epoch), rank=rank)
+        save_checkpoint(ddp, model_filepath, optimizer=optimizer, extra=state, rank=rank)
         print("-" * 75)
         print("Epoch: {}, Accuracy: {}".format(epoch, accuracy))
         print("-" * 75)
@@ -190,6 +199,8 @@ def run(args) -> dict:
     try:
         for epoch in range(start_epoch, args.num_epochs):
             sampler.set_epoch(epoch)
+            if hasattr(train_set, "set_epoch"):
+                train_set.set_epoch(epoch)
             if args.eval_before_train and epoch % args.eval_every == 0 and rank == 0:
                 eval_and_save(epoch, epoch)
             print("Local Rank: {}, Epoch: {}, Training ...".format(local_rank, epoch))

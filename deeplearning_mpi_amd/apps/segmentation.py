@@ -135,7 +135,11 @@ def build_data_loaders(args, device):
         return DeviceBatches(train_c, args.batch_size, sampler), DeviceBatches(test_c, args.batch_size), sampler
     kw = dict(batch_size=args.batch_size, num_workers=args.workers, pin_memory=device.type == "cuda")
     sampler = DistributedSampler(train_ds)
-    return (DataLoader(train_ds, sampler=sampler, **kw), DataLoader(test_ds, shuffle=False, **kw), sampler)
+    # evaluation runs on rank 0 only: its loader gets a private generator so it never advances the
+    # global host RNG that every rank restores on --resume
+    return (DataLoader(train_ds, sampler=sampler, **kw),
+            DataLoader(test_ds, shuffle=False, generator=torch.Generator().manual_seed(args.random_seed), **kw),
+            sampler)
 
 
 def _use_device_data(args, device, ds) -> bool:
@@ -202,7 +206,8 @@ def run(args) -> dict:
         meta = load_checkpoint(ddp, model_filepath, map_location=device, optimizer=optimizer)
         start_epoch = int(meta.get("next_epoch", 0))
         set_rng_state(meta.get("rng"))
-    args.graph = use_graph(args, device, pixels=args.batch_size * args.image_size * args.image_size)
+    args.graph = use_graph(args, device, pixels=args.batch_size * args.image_size * args.image_size,
+                           comm_backend=getattr(comm, "backend", "single"))
 
     def train_step(images, masks):
         pred = ddp(images).squeeze(1)
@@ -219,7 +224,8 @@ def run(args) -> dict:
     y_static = torch.zeros(args.batch_size, S, S, device=device)
     captured = None
     if args.graph and device.type == "cuda":
-        captured = CapturedStep(lambda: train_step(x_static, y_static), warmup=2, inputs=(x_static, y_static))
+        captured = CapturedStep(lambda: train_step(x_static, y_static), warmup=2, inputs=(x_static, y_static),
+                                comm=comm)
     if args.benchmark_steps:
         return benchmark(args, train_step, captured, x_static, y_static, comm, device)
     history = {"loss": [], "dice": []}
@@ -252,8 +258,9 @@ def run(args) -> dict:
             print(f"Epoch {epoch + 1} finished with loss: {avg_loss:.4f}")
             log(f"Epoch {epoch + 1} | Loss: {avg_loss:.4f} | Duration: {time.time() - t0:.2f}s")
             if (epoch + 1) % args.eval_every == 0 and rank == 0:
+                state = resume_state(epoch + 1)   # epoch-boundary RNG states, taken before evaluating
                 dice = evaluate_model(model, device, test_loader)
-                save_checkpoint(ddp, model_filepath, optimizer=optimizer, extra=resume_state(epoch + 1), rank=rank)
+                save_checkpoint(ddp, model_filepath, optimizer=optimizer, extra=state, rank=rank)
                 print("-" * 75)
                 print(f"Epoch {epoch + 1} Dice Score: {dice:.4f}")
                 print("-" * 75)
@@ -261,8 +268,9 @@ def run(args) -> dict:
                 history["dice"].append(dice)
         if rank == 0:
             print("\n" + "=" * 80 + "\nTRAINING COMPLETED - FINAL EVALUATION\n" + "=" * 80)
+            state = resume_state(args.num_epochs)
             final = evaluate_model(model, device, test_loader)
-            save_checkpoint(ddp, model_filepath, optimizer=optimizer, extra=resume_state(args.num_epochs), rank=rank)
+            save_checkpoint(ddp, model_filepath, optimizer=optimizer, extra=state, rank=rank)
             print(f"FINAL DICE COEFFICIENT: {final:.4f}\n" + "=" * 80 + "\n")
             log("=" * 80)
             log("FINAL TRAINING RESULTS")

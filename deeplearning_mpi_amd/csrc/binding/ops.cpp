@@ -912,6 +912,11 @@ void register_ops(pybind11::module& m) {
   m.def("set_aux_stream", [](int64_t h, int role) {
     check(dlmpi_set_aux_stream(reinterpret_cast<hipStream_t>(h), role), "set_aux_stream");
   });
+  // bounded spin kernel on the current stream (tests: delays a collective to expose missing fences)
+  m.def("delay_ms", [](double ms) { check(dlmpi_delay(ms, cur_stream()), "delay_ms"); });
+  // reads and resets HIP's per-thread sticky error (a failed hipGraph capture leaves
+  // hipErrorStreamCaptureInvalidated behind, which the next checked launch would report)
+  m.def("clear_hip_error", []() { return (int)hipGetLastError(); });
   m.def("reduce_blocks", &reduce_blocks);
   m.def("bn_stats", &bn_stats);
   m.def("bn_apply", &bn_apply);

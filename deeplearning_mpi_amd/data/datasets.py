@@ -84,13 +84,58 @@ class CifarTransform:
         return (t - self.mean) / self.std
 
 
+_M64 = (1 << 64) - 1
+
+
+class SampleRng:
+    """Counter-based random stream of ONE sample: splitmix64 over (seed, epoch, index).
+
+    The augmentation of sample ``i`` in epoch ``e`` is a pure function of (seed, e, i): it does not
+    depend on which DataLoader worker or rank loads the sample, on how many samples that worker
+    loaded before, or on whether the run was interrupted and resumed -- so ``--resume`` continues
+    with exactly the crops and flips an uninterrupted run would have drawn,
+    with no generator state to checkpoint.  Offers the two ``np.random.Generator`` calls the
+    transforms use."""
+
+    __slots__ = ("_s",)
+
+    def __init__(self, seed: int, epoch: int, index: int):
+        self._s = ((seed & 0xFFFFFFFF) * 0x9E3779B97F4A7C15 ^ (epoch & 0xFFFFFFFF) * 0xC2B2AE3D27D4EB4F
+                   ^ (index & 0xFFFFFFFFFFFF) * 0x165667B19E3779F9) & _M64
+
+    def _next(self) -> int:
+        self._s = (self._s + 0x9E3779B97F4A7C15) & _M64
+        z = self._s
+        z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & _M64
+        z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & _M64
+        return z ^ (z >> 31)
+
+    def integers(self, low, high, size=None):
+        span = int(high) - int(low)
+        if size is None:
+            return int(low) + self._next() % span
+        return np.array([int(low) + self._next() % span for _ in range(int(np.prod(size)))]).reshape(size)
+
+    def random(self) -> float:
+        return (self._next() >> 11) * (1.0 / (1 << 53))
+
+
 class CIFAR10(Dataset):
+    """CIFAR-10 from the official binary / python releases.  Augmentation randomness comes from
+    :class:`SampleRng` keyed by (``seed``, epoch, index); call :meth:`set_epoch` every epoch (the
+    apps do it next to ``DistributedSampler.set_epoch``; DataLoader workers must not be persistent,
+    so each epoch's workers start from the updated dataset object)."""
+
     def __init__(self, root, train=True, transform=None, seed=0):
         self.root = root
         self.train = train
         self.transform = transform
         self.data, self.targets = self._load(root, train)
-        self._rng = np.random.default_rng(seed)
+        self.seed = int(seed)
+        self.epoch = 0
+
+    def set_epoch(self, epoch: int):
+        self.epoch = int(epoch)
 
     @staticmethod
     def _load(root, train):
@@ -120,7 +165,7 @@ class CIFAR10(Dataset):
     def __getitem__(self, i):
         img = self.data[i]
         if self.transform is not None:
-            x = self.transform(img, self._rng)
+            x = self.transform(img, SampleRng(self.seed, self.epoch, i))
         else:
             x = torch.from_numpy(img).permute(2, 0, 1).float().div_(255.0)
         return x, int(self.targets[i])

@@ -358,6 +358,7 @@ def _init(backend: str, timeout_s: float) -> Communicator:
         return TorchCommunicator(info, device)
     # RCCL data plane: no torch process group at all, only the 128-byte unique id has to reach
     # every rank before ncclCommInitRank
+    rccl_channel_budget()
     from .._ext import native
 
     C = native()
@@ -373,6 +374,30 @@ def _init(backend: str, timeout_s: float) -> Communicator:
     return RcclCommunicator(info, device, nc, control_group=store)
 
 
+DEFAULT_RCCL_CHANNELS = 16
+
+
+def rccl_channel_budget() -> dict:
+    """How many CUs RCCL's kernels may take from the compute streams.
+
+    Each RCCL channel is one workgroup (one CU) for the duration of a collective.  The gradient
+    all-reduces run on the comm stream while the backward convolutions fill the other 240+ CUs, so
+    the channel count is a CU budget: ``DLMPI_RCCL_CHANNELS`` (default 16 = 1/16 of the 256 CUs;
+    0 = leave RCCL's own choice) is exported as ``NCCL_MAX_NCHANNELS`` before the communicator is
+    created (RCCL reads it at ``ncclCommInitRank``).  An explicit ``NCCL_MAX_NCHANNELS`` /
+    ``NCCL_MIN_NCHANNELS`` in the environment wins.  Sizing: ResNet-50's 102 MB of fp32 gradients
+    move 2*(7/8)*102 MB per rank; at 16 channels (>= ~10 GB/s each over the 7 xGMI links) that is
+    about 1 ms, far inside the ~14 ms backward pass it overlaps.  Returns the effective settings
+    (bench.py reports them)."""
+    want = int(os.environ.get("DLMPI_RCCL_CHANNELS", str(DEFAULT_RCCL_CHANNELS)) or 0)
+    if want > 0 and "NCCL_MAX_NCHANNELS" not in os.environ:
+        os.environ["NCCL_MAX_NCHANNELS"] = str(want)
+    return {k: os.environ.get(k) for k in ("NCCL_MAX_NCHANNELS", "NCCL_MIN_NCHANNELS")}
+
+
+_UID_ROUND = 0   # init_distributed -> destroy -> init_distributed in one process: a fresh key each time
+
+
 def uid_via_store(info, make_uid, timeout_s=1800.0):
     """torchrun / env:// launch: the RCCL unique id goes through the launcher's c10d TCPStore (the
     elastic agent's store when torchrun shares it), obtained with the same env:// rendezvous
@@ -381,7 +406,9 @@ def uid_via_store(info, make_uid, timeout_s=1800.0):
     store, _, _ = next(dist.rendezvous("env://", rank=info.rank, world_size=info.world_size,
                                        timeout=datetime.timedelta(seconds=timeout_s)))
     store.set_timeout(datetime.timedelta(seconds=timeout_s))
-    key = f"dlmpi/rccl_uid/{os.environ.get('TORCHELASTIC_RESTART_COUNT', '0')}"
+    global _UID_ROUND
+    _UID_ROUND += 1
+    key = f"dlmpi/rccl_uid/{os.environ.get('TORCHELASTIC_RESTART_COUNT', '0')}/{_UID_ROUND}"
     if info.rank == 0:
         uid = make_uid()
         store.set(key, uid)

@@ -218,7 +218,10 @@ class ParamArena:
         return self.compute[off:off + n]
 
     def _version(self):
-        return sum(p._version for p in self.params) + self.flat._version
+        # hipGraph replays update the masters without touching any host-side version counter
+        from . import graphs
+
+        return (sum(p._version for p in self.params) + self.flat._version, graphs.REPLAYS)
 
     def refresh(self, force=False):
         """Recast all compute copies if any master parameter changed (one kernel launch)."""

@@ -8,18 +8,29 @@ sidecar ``<path>.state`` so the main file layout never changes; the apps write i
 checkpoint and ``--resume`` continues from it exactly (tests/test_resume_cpu.py).  Only GLOBAL rank 0 writes (the reference gates on
 LOCAL_RANK, which collides across nodes on a shared filesystem).
 Loading uses ``torch.load(..., weights_only=True)`` and accepts either key style.
+
+Crash consistency: the sidecar records the SHA-256 of the weights file it belongs to and is put in
+place BEFORE the weights file, so a crash between the two renames leaves a sidecar whose hash does
+not match the weights on disk; ``load_checkpoint`` then ignores it (warning) instead of silently
+mixing new weights with an old optimizer state / epoch.
 """
 from __future__ import annotations
 
+import hashlib
 import os
 import random
+import warnings
 
 import numpy as np
 import torch
 
 
-def _target(model):
-    return model
+def _sha256(path) -> str:
+    h = hashlib.sha256()
+    with open(path, "rb") as f:
+        for chunk in iter(lambda: f.read(1 << 22), b""):
+            h.update(chunk)
+    return h.hexdigest()
 
 
 def save_checkpoint(model, path, optimizer=None, extra=None, rank=None):
@@ -35,13 +46,14 @@ def save_checkpoint(model, path, optimizer=None, extra=None, rank=None):
     sd = {k: v.detach().cpu() for k, v in model.state_dict().items()}
     tmp = path + ".tmp"
     torch.save(sd, tmp)
-    os.replace(tmp, path)
     if optimizer is not None or extra:
         state = dict(extra or {})
         if optimizer is not None:
             state["optimizer"] = optimizer.state_dict()
+        state["weights_sha256"] = _sha256(tmp)
         torch.save(state, path + ".state.tmp")
-        os.replace(path + ".state.tmp", path + ".state")
+        os.replace(path + ".state.tmp", path + ".state")   # sidecar first (see module docstring)
+    os.replace(tmp, path)
     return path
 
 
@@ -67,6 +79,11 @@ def load_checkpoint(model, path, map_location=None, optimizer=None, strict=True)
     meta = {}
     if os.path.exists(path + ".state"):
         meta = torch.load(path + ".state", map_location=map_location, weights_only=True)
+        want = meta.get("weights_sha256")
+        if want is not None and want != _sha256(path):
+            warnings.warn(f"{path}.state belongs to a different weights file (interrupted save?): "
+                          "ignoring the resume state, starting from epoch 0 with fresh optimizer state")
+            meta = {}
         if optimizer is not None and "optimizer" in meta:
             optimizer.load_state_dict(meta["optimizer"])
     from .arena import arena_of

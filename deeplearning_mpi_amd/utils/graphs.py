@@ -17,21 +17,43 @@ Contract of :class:`CapturedStep`:
   so they stay correct across replays);
 * the first ``warmup`` calls run eagerly on a side stream (allocator / autograd / kernel caches
   and weight-layout descriptors are set up outside the capture), the next call captures, later
-  calls replay.
+  calls replay;
+* a replay changes parameters behind the host's back (the optimizer kernel writes the flat
+  master buffer through raw pointers), so every replay bumps :data:`REPLAYS`; ``ParamArena``
+  folds that counter into its version, and the next EAGER use of the model (evaluation, a ragged
+  last batch) recasts its compute weights instead of reading copies from before the replays;
+* a failed capture never kills the run: the error is reported, the device synchronised, the
+  graph dropped, and the step runs eagerly from then on, in the same process (no re-exec).  With
+  a communicator (``comm``) the ranks agree first -- if ANY rank failed to capture, every rank
+  runs eagerly -- so the collectives stay matched across ranks.
 """
 from __future__ import annotations
 
+import sys
+
 import torch
+
+REPLAYS = 0   # replays (and failed captures) of any captured step in this process; ParamArena._version reads it
+
+
+def _note_replay():
+    """Host-side state no longer describes the device: a replay ran kernels the host did not issue,
+    or a failed capture recorded (and never ran) kernels the host believes it issued -- e.g. the
+    weight recast of ``ParamArena.refresh``.  Bumping the counter makes the next eager use recast."""
+    global REPLAYS
+    REPLAYS += 1
 
 
 class CapturedStep:
-    def __init__(self, step_fn, warmup: int = 2, inputs=(), enabled: bool = True):
+    def __init__(self, step_fn, warmup: int = 2, inputs=(), enabled: bool = True, comm=None):
         self.step_fn = step_fn
         self.warmup = warmup
         self.inputs = tuple(inputs)
         self.enabled = enabled and torch.cuda.is_available()
+        self.comm = comm
         self.graph = None
         self.out = None
+        self.capture_error = None   # the exception of a failed capture (then enabled is False)
         self._calls = 0
         self._pool = None
 
@@ -50,6 +72,7 @@ class CapturedStep:
             return self.step_fn()
         if self.graph is not None:
             self.graph.replay()
+            _note_replay()
             return self.out
         self._calls += 1
         if self._calls <= self.warmup:
@@ -59,14 +82,54 @@ class CapturedStep:
                 out = self.step_fn()
             torch.cuda.current_stream().wait_stream(s)
             return out
+        g, err = self._capture()
+        if not self._agree(err is None):
+            self._fall_back(err)
+            return self.step_fn()
+        self.graph = g
+        # the capture only recorded the step: run it once so this call has the step's effect
+        g.replay()
+        _note_replay()
+        return self.out
+
+    # ------------------------------------------------------------------ capture / fallback
+    def _capture(self):
         torch.cuda.synchronize()
         g = torch.cuda.CUDAGraph()
         if self._pool is None:
             self._pool = torch.cuda.graph_pool_handle()
-        # thread_local: the RCCL watchdog thread may poll events while this thread captures
-        with torch.cuda.graph(g, pool=self._pool, capture_error_mode="thread_local"):
-            self.out = self.step_fn()
-        self.graph = g
-        # the capture only recorded the step: run it once so this call has the step's effect
-        g.replay()
-        return self.out
+        try:
+            # thread_local: the RCCL watchdog thread may poll events while this thread captures
+            with torch.cuda.graph(g, pool=self._pool, capture_error_mode="thread_local"):
+                self.out = self.step_fn()
+        except Exception as e:   # noqa: BLE001 -- any capture failure degrades to eager
+            self.out = None
+            return None, e
+        return g, None
+
+    def _agree(self, ok: bool) -> bool:
+        """True iff every rank captured (MIN over ranks of the local success flag)."""
+        c = self.comm
+        if c is None or getattr(c, "world_size", 1) == 1:
+            return ok
+        t = torch.tensor([1.0 if ok else 0.0], device=c.device)
+        c.allreduce(t, "min")
+        return bool(t.item() > 0.5)
+
+    def _fall_back(self, err):
+        self.capture_error = err if err is not None else RuntimeError("hipGraph capture failed on another rank")
+        print(f"[dlmpi] hipGraph capture failed ({self.capture_error!r}); running the step eagerly from now on",
+              file=sys.stderr, flush=True)
+        try:
+            torch.cuda.synchronize()
+        except Exception:   # noqa: BLE001 -- the invalidated capture's error may surface here
+            pass
+        # HIP keeps the capture error as the thread's sticky last error: reset it, or the next
+        # checked kernel launch of the eager step reports it as its own failure
+        from .._ext import has_native, native
+
+        if has_native():
+            native().clear_hip_error()
+        self.graph = None
+        self.enabled = False
+        _note_replay()

@@ -42,6 +42,11 @@ def test_bench_self_launches_n_ranks(launcher):
     j = lines[0]
     assert j["n_gpus"] == 2 and j["config"]["parallelism"] == "dp2" and j["config"]["global_batch"] == 8
     assert j["steps"] == 2 and j["warmup"] == 1 and j["value"] > 0
+    # distributed facts: bucket layout, per-rank step times, exposed all-reduce
+    d = j["dist"]
+    assert d["reducer"] and len(d["bucket_mb"]) >= 1 and d["comm_exposed_ms"] is not None
+    assert 0 < d["per_rank_ms_per_step"]["min"] <= d["per_rank_ms_per_step"]["max"]
+    assert d["per_rank_ms_per_step"]["max"] == pytest.approx(j["ms_per_step"], rel=1e-3, abs=1e-3)
 
 
 def test_bench_single_rank_unchanged():

@@ -231,3 +231,64 @@ def test_rccl_uid_exchange_through_launcher_store(tmp_path):
     assert r.returncode == 0, r.stdout + r.stderr
     uids = {l.split()[3] for l in r.stdout.splitlines() if l.startswith("rank ")}
     assert len(uids) == 1 and r.stdout.count("len 128") == 3, r.stdout
+
+
+def _w_ddp8_r50(rank, world, port, out):
+    """8 ranks, ResNet-50, the PRODUCTION bucket caps (DDP defaults: 2 MB first, 32 MB, 4 MB tail)."""
+    import deeplearning_mpi_amd as dl
+    from deeplearning_mpi_amd.models import resnet50
+    from deeplearning_mpi_amd.ops import cross_entropy
+
+    c = _setup(rank, world, port)
+    torch.set_num_threads(1)
+    torch.manual_seed(rank)      # different init per rank: K4 must broadcast rank 0's weights
+    model = resnet50(num_classes=10).double()
+    ddp = dl.DistributedDataParallel(model)   # default caps = the 8-GPU bench layout
+    init = {k: v.clone() for k, v in model.state_dict().items()}
+    g = torch.Generator().manual_seed(500 + rank)
+    x, y = torch.randn(2, 3, 32, 32, generator=g).double(), torch.randint(10, (2,), generator=g)
+    model.arena.zero_grad()
+    cross_entropy(ddp(x), y).backward()
+    torch.save({"init": init if rank == 0 else None, "grad": model.arena.grad.clone(),
+                "bounds": list(ddp.bucket_bounds), "launched": ddp.reducer.launched(),
+                "nb": ddp.reducer.num_buckets()}, f"{out}/r{rank}.pt")
+    dl.destroy_distributed()
+
+
+def test_ddp_8_ranks_resnet50_production_buckets(tmp_path):
+    """the bucket layout the 8-GPU bench uses, rehearsed at world size 8 (gloo):
+    every bucket is launched (in index order, by the C++ reducer) and every rank ends with the mean
+    of the 8 per-rank gradients."""
+    from deeplearning_mpi_amd.models import resnet50
+    from deeplearning_mpi_amd.ops import cross_entropy
+    from deeplearning_mpi_amd.parallel.ddp import (DEFAULT_BUCKET_MB, DEFAULT_FIRST_BUCKET_MB,
+                                                   DEFAULT_LAST_BUCKET_MB)
+
+    world = 8
+    res = _spawn(_w_ddp8_r50, world, tmp_path)
+    # production layout: the fp32 model's buckets under the default caps, element-for-element
+    m = resnet50(num_classes=10)
+    m.engine_setup("cpu")
+    want = m.arena.buckets(int(DEFAULT_FIRST_BUCKET_MB * 2 ** 20), int(DEFAULT_BUCKET_MB * 2 ** 20),
+                           int(DEFAULT_LAST_BUCKET_MB * 2 ** 20))[0]
+    sizes = [(e - s) * 4 / 2 ** 20 for s, e in want]
+    # a bucket closes with the parameter that crosses its cap (largest ResNet-50 tensor: 9.4 MB)
+    assert len(want) >= 4 and sizes[0] <= 2 + 4.1 and sizes[-1] <= 4.0 and max(sizes) <= 32 + 9.5, sizes
+    for r in range(world):
+        assert [tuple(b) for b in res[r]["bounds"]] == [tuple(b) for b in want]
+        assert res[r]["launched"] == res[r]["nb"] == len(want)   # no bucket left behind / inverted
+    # oracle: mean of the per-rank local gradients from rank 0's weights, one process
+    local = torch.zeros_like(res[0]["grad"])
+    for r in range(world):
+        torch.manual_seed(0)
+        mr = resnet50(num_classes=10).double()
+        mr.load_state_dict(res[0]["init"])
+        mr.engine_setup("cpu")
+        mr.arena.zero_grad()
+        g = torch.Generator().manual_seed(500 + r)
+        x, y = torch.randn(2, 3, 32, 32, generator=g).double(), torch.randint(10, (2,), generator=g)
+        cross_entropy(mr(x), y).backward()
+        local += mr.arena.grad
+    local /= world
+    for r in range(world):
+        assert torch.allclose(res[r]["grad"], local, rtol=1e-9, atol=1e-13), r

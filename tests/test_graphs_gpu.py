@@ -70,3 +70,91 @@ def test_unet_adam_clip_step_graph_replay_matches_eager():
     _check(lambda: UNet(out_classes=1),
            lambda m: Adam(m.parameters(), lr=1e-3),
            lambda m, x, y: bce_with_logits(m(x).squeeze(1), y), batches)
+
+
+def _sgd(m):
+    return SGD(m.parameters(), lr=0.05, momentum=0.9, weight_decay=1e-5)
+
+
+def _cifar_batches(n, seed):
+    g = torch.Generator(device=DEV).manual_seed(seed)
+    return [(torch.randn(32, 3, 32, 32, device=DEV, generator=g),
+             torch.randint(10, (32,), device=DEV, generator=g)) for _ in range(n)]
+
+
+def test_eager_eval_after_replays_sees_updated_weights():
+    """replays update the fp32 masters through raw pointers; an eager forward after them
+    (evaluation, a ragged last batch) must recast the bf16 compute weights instead of reusing the
+    copy from before the replays.  Train (graph) -> eval -> train (graph) -> eval must equal the
+    all-eager run, evals included."""
+    batches = _cifar_batches(8, 21)
+    xe = torch.randn(16, 3, 32, 32, device=DEV, generator=torch.Generator(device=DEV).manual_seed(22))
+
+    def run(graph):
+        torch.manual_seed(0)
+        m = resnet18(num_classes=10).to(DEV)
+        opt = _sgd(m)
+        x, y = batches[0][0].clone(), batches[0][1].clone()
+
+        def step():
+            opt.zero_grad()
+            loss = cross_entropy(m(x), y)
+            loss.backward()
+            opt.step()
+            return loss
+
+        cs = CapturedStep(step, warmup=2, inputs=(x, y), enabled=graph)
+        evals = []
+        for k, (bx, by) in enumerate(batches):
+            cs.set_inputs(bx, by)
+            cs()
+            if k in (3, 5, 7):   # eager evaluation between replays
+                m.eval()
+                with torch.no_grad():
+                    evals.append(m(xe).float().clone())
+                m.train()
+        torch.cuda.synchronize()
+        return evals
+
+    ref, got = run(False), run(True)
+    for a, b in zip(ref, got):
+        assert torch.equal(a, b)
+
+
+def test_failed_capture_falls_back_to_eager():
+    """an error inside the capture (here a host synchronisation in the middle of
+    the step, which a capturing stream refuses -- like an uncapturable collective) must not kill the
+    run: CapturedStep reports it, drops the graph and runs every step eagerly, in the same process,
+    bit-identical to an all-eager run."""
+    batches = _cifar_batches(6, 23)
+
+    def run(inject):
+        torch.manual_seed(0)
+        m = resnet18(num_classes=10).to(DEV)
+        opt = _sgd(m)
+        x, y = batches[0][0].clone(), batches[0][1].clone()
+
+        def step():
+            opt.zero_grad()
+            loss = cross_entropy(m(x), y)
+            if inject and torch.cuda.is_current_stream_capturing():
+                float(loss)   # device -> host copy + sync: refused while capturing
+            loss.backward()
+            opt.step()
+            return loss
+
+        cs = CapturedStep(step, warmup=2, inputs=(x, y), enabled=inject)
+        losses = []
+        for bx, by in batches:
+            cs.set_inputs(bx, by)
+            losses.append(cs().clone())
+        torch.cuda.synchronize()
+        if inject:
+            assert cs.graph is None and not cs.enabled and cs.capture_error is not None
+        return torch.stack(losses), [p.detach().clone() for p in list(m.parameters()) + list(m.buffers())]
+
+    l1, p1 = run(False)
+    l2, p2 = run(True)
+    assert torch.equal(l1, l2), (l1, l2)
+    for a, b in zip(p1, p2):
+        assert torch.equal(a, b)
