@@ -63,9 +63,19 @@ static ncclRedOp_t to_op(const std::string& op) {
 }
 
 // ---------------------------------------------------------------------------------------------
+// The comm stream is a raw HIP stream owned here (not a torch pool stream): a capture failure can
+// leave it stuck in capture mode, and a stuck POOL stream would later be handed to unrelated code.
+static hipStream_t new_raw_stream() {
+  hipStream_t s = nullptr;
+  hip_check(hipStreamCreateWithFlags(&s, hipStreamNonBlocking), "hipStreamCreateWithFlags");
+  return s;
+}
+
 struct RcclComm::Impl {
   ncclComm_t comm = nullptr;
   c10::hip::HIPStream stream;
+  hipStream_t raw = nullptr;                 // owned; `stream` wraps it
+  std::vector<hipStream_t> retired;          // streams abandoned in capture mode (never reused)
   int rank = 0, size = 1, device = 0;
   std::vector<hipEvent_t> events;   // ring of pre-created events for stream fences
   size_t next_event = 0;
@@ -179,6 +189,7 @@ struct RcclComm::Impl {
   ~Impl() {
     stop_watchdog();
     for (auto& e : events) hipEventDestroy(e);
+    if (raw) hipStreamDestroy(raw);
   }
 };
 
@@ -196,7 +207,16 @@ RcclComm::RcclComm(const std::string& uid, int rank, int size, int device) {
   // captured DDP step.  DLMPI_COMM_HIPRI=1 opts back in.
   const char* hp = std::getenv("DLMPI_COMM_HIPRI");
   const bool hipri = hp != nullptr && std::atoi(hp) != 0;
-  impl_ = std::make_unique<Impl>(c10::hip::getStreamFromPool(hipri, (c10::DeviceIndex)device));
+  hipStream_t raw = nullptr;
+  if (hipri) {
+    int lo = 0, hi = 0;
+    hip_check(hipDeviceGetStreamPriorityRange(&lo, &hi), "hipDeviceGetStreamPriorityRange");
+    hip_check(hipStreamCreateWithPriority(&raw, hipStreamNonBlocking, hi), "hipStreamCreateWithPriority");
+  } else {
+    raw = new_raw_stream();
+  }
+  impl_ = std::make_unique<Impl>(c10::hip::getStreamFromExternal(raw, (c10::DeviceIndex)device));
+  impl_->raw = raw;
   impl_->rank = rank;
   impl_->size = size;
   impl_->device = device;
@@ -341,6 +361,18 @@ void RcclComm::recv(at::Tensor t, int peer) {
 
 void RcclComm::wait() { fence_out(); }
 
+bool RcclComm::reset_stream_if_capturing() {
+  hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(impl_->raw, &st) != hipSuccess) st = hipStreamCaptureStatusActive;
+  (void)hipGetLastError();
+  if (st == hipStreamCaptureStatusNone) return false;
+  impl_->retired.push_back(impl_->raw);   // leaked on purpose: a stream stuck in capture mode
+  hip_check(hipSetDevice(impl_->device), "hipSetDevice");
+  impl_->raw = new_raw_stream();
+  impl_->stream = c10::hip::getStreamFromExternal(impl_->raw, (c10::DeviceIndex)impl_->device);
+  return true;
+}
+
 void RcclComm::synchronize() { hip_check(hipStreamSynchronize(impl_->stream.stream()), "hipStreamSynchronize"); }
 
 void RcclComm::barrier() {
@@ -420,6 +452,7 @@ void register_comm(pybind11::module& m) {
       .def("wait", &RcclComm::wait)
       .def("synchronize", &RcclComm::synchronize)
       .def("barrier", &RcclComm::barrier)
+      .def("reset_stream_if_capturing", &RcclComm::reset_stream_if_capturing)
       .def("destroy", &RcclComm::destroy);
 
   py::class_<CommBase, PyCommBase, std::shared_ptr<CommBase>>(m, "CommBase")

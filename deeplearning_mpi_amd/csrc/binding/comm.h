@@ -30,6 +30,10 @@ class RcclComm {
   void synchronize();
   void barrier();
   void destroy();
+  // After a failed hipGraph capture that had forked the comm stream: if the stream is still in
+  // capture mode (HIP leaves an invalidated capture open), switch to a fresh stream.  Returns true
+  // if the stream was replaced.
+  bool reset_stream_if_capturing();
 
  private:
   void record(const at::Tensor& t);

@@ -549,17 +549,18 @@ void conv2d_wgrad_pro(const at::Tensor& dy, int lddy, int dyoff, int Ko, const a
   a.fdS = make_fastdiv((uint32_t)S);
   const int64_t wsz = (int64_t)Ko * a.TC;
   const int G = splits > 1 ? dlmpi_wgrad_reduce_groups(splits, wsz) : 0;
-  // In-launch split reduction for few splits (DLMPI_WGRAD_INLAUNCH = max splits, default 8; 0 = off):
-  // the tile's last arriver reads all S slabs itself, a serial tail of S x 32-64 KB.  Most ResNet /
-  // UNet weight gradients split the pixel axis 15-500 ways (tiny Ko x R*S*C output, huge pixel
-  // reduction), where that tail costs far more than the two reduction launches it saves (all
-  // splits in-launch: ResNet-50 11,770 -> 7,630 img/s, profiles/r2_wgrad_inlaunch); those keep the
-  // slab workspace + two parallel reduction kernels.
+  // In-launch split reduction (DLMPI_WGRAD_INLAUNCH = max splits; default 0 = off): the tile's last
+  // arriver reads all S slabs itself (a serial tail of S x 32-64 KB) and adds its tile into the fp32
+  // gradient from the accumulator fragments (a strided read-modify-write).  Measured slower than the
+  // slab workspace + two parallel reduction kernels at EVERY split count, S = 1 included (same box,
+  // profiles/r3_wgrad_inlaunch_off: ResNet-18 CIFAR hipGraph 76.4k img/s with <= 8 splits in-launch,
+  // 83.6k with only S = 1 in-launch, 89.5k with none; ResNet-50 11,830 -> 11,970; all splits
+  // in-launch: ResNet-50 7,630, profiles/r2_wgrad_inlaunch).
   static const int inlaunch_max = [] {
     const char* e = getenv("DLMPI_WGRAD_INLAUNCH");
-    return e ? atoi(e) : 8;
+    return e ? atoi(e) : 0;
   }();
-  if (splits <= inlaunch_max && !a.f32) {
+  if (inlaunch_max > 0 && splits <= inlaunch_max && !a.f32) {
     hipStream_t st = cur_stream();
     const int tiles_n = a.mtiles * a.ntiles;
     float* slab = splits > 1 ? dlmpi_splitk_slab(st, (size_t)tiles_n * splits * bm * bn) : nullptr;
@@ -917,6 +918,19 @@ void register_ops(pybind11::module& m) {
   // reads and resets HIP's per-thread sticky error (a failed hipGraph capture leaves
   // hipErrorStreamCaptureInvalidated behind, which the next checked launch would report)
   m.def("clear_hip_error", []() { return (int)hipGetLastError(); });
+  // raw HIP streams (not torch pool streams: one that a failed capture leaves in capture mode is
+  // simply abandoned, never handed out again)
+  m.def("create_stream", []() {
+    hipStream_t s = nullptr;
+    check(hipStreamCreateWithFlags(&s, hipStreamNonBlocking), "hipStreamCreateWithFlags");
+    return reinterpret_cast<int64_t>(s);
+  });
+  m.def("stream_capturing", [](int64_t h) {
+    hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+    const hipError_t e = hipStreamIsCapturing(reinterpret_cast<hipStream_t>(h), &st);
+    (void)hipGetLastError();
+    return e != hipSuccess || st != hipStreamCaptureStatusNone;
+  });
   m.def("reduce_blocks", &reduce_blocks);
   m.def("bn_stats", &bn_stats);
   m.def("bn_apply", &bn_apply);

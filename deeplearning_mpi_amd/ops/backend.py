@@ -12,6 +12,7 @@ Both expose the same methods; the engine (models/*) is written once against this
 from __future__ import annotations
 
 import os
+import weakref
 import struct
 
 import torch
@@ -22,6 +23,16 @@ from .act import Act, Deferred
 
 # --------------------------------------------------------------------------------------------
 _AUX_STREAMS = {}
+_BACKENDS = weakref.WeakSet()   # NativeBackend instances (their aux stream references)
+
+
+def _new_aux_stream(idx, C, role):
+    with torch.cuda.device(idx):
+        # a raw HIP stream, not a torch pool stream: if a failed hipGraph capture leaves it stuck in
+        # capture mode it is abandoned (replace_poisoned_aux_streams), never handed out again
+        st = torch.cuda.ExternalStream(C.create_stream(), device=torch.device("cuda", idx))
+        C.set_aux_stream(st.cuda_stream, role)
+    return st
 
 
 def _aux_stream(device, C, role):
@@ -31,10 +42,31 @@ def _aux_stream(device, C, role):
     idx = device.index if device.index is not None else torch.cuda.current_device()
     st = _AUX_STREAMS.get((idx, role))
     if st is None:
-        st = _AUX_STREAMS[(idx, role)] = torch.cuda.Stream(device=idx)
-        with torch.cuda.device(idx):
-            C.set_aux_stream(st.cuda_stream, role)
+        st = _AUX_STREAMS[(idx, role)] = _new_aux_stream(idx, C, role)
     return st
+
+
+def replace_poisoned_aux_streams() -> int:
+    """After a failed hipGraph capture (utils/graphs.py): every auxiliary stream that the capture
+    had forked and that HIP left in capture mode is replaced by a fresh one, in the registry, in the
+    kernels' role table and in every live backend.  Returns the number replaced."""
+    if not _AUX_STREAMS:
+        return 0
+    from .._ext import native
+
+    C = native()
+    n = 0
+    for (idx, role), st in list(_AUX_STREAMS.items()):
+        if not C.stream_capturing(st.cuda_stream):
+            continue
+        fresh = _AUX_STREAMS[(idx, role)] = _new_aux_stream(idx, C, role)
+        for be in list(_BACKENDS):
+            if be._side is st:
+                be._side = fresh
+            if be._branch is st:
+                be._branch = fresh
+        n += 1
+    return n
 
 
 class NativeBackend:
@@ -71,6 +103,7 @@ class NativeBackend:
         # UNet bs 16 at 512^2, off for CIFAR).
         self.aux_min_pixels = int(os.environ.get("DLMPI_AUX_MIN_PIXELS", str(1 << 20)))
         self.aux_on = True
+        _BACKENDS.add(self)
 
     @property
     def side_stream(self):

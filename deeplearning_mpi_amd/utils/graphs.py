@@ -22,14 +22,25 @@ Contract of :class:`CapturedStep`:
   master buffer through raw pointers), so every replay bumps :data:`REPLAYS`; ``ParamArena``
   folds that counter into its version, and the next EAGER use of the model (evaluation, a ragged
   last batch) recasts its compute weights instead of reading copies from before the replays;
-* a failed capture never kills the run: the error is reported, the device synchronised, the
-  graph dropped, and the step runs eagerly from then on, in the same process (no re-exec).  With
-  a communicator (``comm``) the ranks agree first -- if ANY rank failed to capture, every rank
-  runs eagerly -- so the collectives stay matched across ranks.
+* a failed capture never kills the run: the error is reported, the graph dropped, and the step
+  runs eagerly from then on, in the same process (no re-exec).  With a communicator (``comm``)
+  the ranks agree first -- if ANY rank failed to capture, every rank runs eagerly -- so the
+  collectives stay matched across ranks.
+
+Why the capture runs on a helper thread, on a stream of its own: HIP (ROCm 7.2) does not close an
+invalidated capture -- ``hipStreamEndCapture`` fails and the stream, every stream forked into the
+capture and the capturing thread's legacy default stream all stay in capture mode, refusing every
+later launch (scripts/diag/capture_fail.py).  So the capture begins and ends on a short-lived
+thread (its thread-local capture state dies with it), on a raw HIP stream that is abandoned if the
+capture fails, and the auxiliary streams / RCCL comm stream that the capture had forked are
+replaced by fresh raw streams (``ops.backend.replace_poisoned_aux_streams``,
+``RcclComm.reset_stream_if_capturing``).  None of them is a torch pool stream, so a stuck stream
+is never handed out again.
 """
 from __future__ import annotations
 
 import sys
+import threading
 
 import torch
 
@@ -56,6 +67,7 @@ class CapturedStep:
         self.capture_error = None   # the exception of a failed capture (then enabled is False)
         self._calls = 0
         self._pool = None
+        self._stream = None   # the capture stream (ours, so a failed capture can be ended on it)
 
     def set_inputs(self, *tensors):
         """Copy a new batch into the captured input tensors (same shapes / dtypes)."""
@@ -98,13 +110,29 @@ class CapturedStep:
         g = torch.cuda.CUDAGraph()
         if self._pool is None:
             self._pool = torch.cuda.graph_pool_handle()
-        try:
-            # thread_local: the RCCL watchdog thread may poll events while this thread captures
-            with torch.cuda.graph(g, pool=self._pool, capture_error_mode="thread_local"):
-                self.out = self.step_fn()
-        except Exception as e:   # noqa: BLE001 -- any capture failure degrades to eager
+        if self._stream is None:
+            from .._ext import native
+
+            self._stream = torch.cuda.ExternalStream(native().create_stream())
+        dev = torch.cuda.current_device()
+        res = {}
+
+        def body():
+            try:
+                torch.cuda.set_device(dev)
+                # thread_local: the RCCL watchdog thread may poll events while this thread captures
+                with torch.cuda.graph(g, pool=self._pool, stream=self._stream, capture_error_mode="thread_local"):
+                    res["out"] = self.step_fn()
+            except BaseException as e:   # noqa: BLE001 -- any capture failure degrades to eager
+                res["err"] = e
+
+        t = threading.Thread(target=body, name="dlmpi-graph-capture")
+        t.start()
+        t.join()
+        if "err" in res:
             self.out = None
-            return None, e
+            return None, res["err"]
+        self.out = res["out"]
         return g, None
 
     def _agree(self, ok: bool) -> bool:
@@ -120,16 +148,19 @@ class CapturedStep:
         self.capture_error = err if err is not None else RuntimeError("hipGraph capture failed on another rank")
         print(f"[dlmpi] hipGraph capture failed ({self.capture_error!r}); running the step eagerly from now on",
               file=sys.stderr, flush=True)
-        try:
-            torch.cuda.synchronize()
-        except Exception:   # noqa: BLE001 -- the invalidated capture's error may surface here
-            pass
-        # HIP keeps the capture error as the thread's sticky last error: reset it, or the next
-        # checked kernel launch of the eager step reports it as its own failure
+        # streams the failed capture had forked stay in capture mode: replace them (module docstring)
+        from ..ops.backend import replace_poisoned_aux_streams
+
+        replace_poisoned_aux_streams()
+        nc = getattr(getattr(self.comm, "inner", self.comm), "c", None)
+        if nc is not None and hasattr(nc, "reset_stream_if_capturing"):
+            nc.reset_stream_if_capturing()
+        self._stream = None   # abandoned (possibly still in capture mode)
         from .._ext import has_native, native
 
         if has_native():
             native().clear_hip_error()
+        torch.cuda.synchronize()
         self.graph = None
         self.enabled = False
         _note_replay()

@@ -124,13 +124,15 @@ def test_eager_eval_after_replays_sees_updated_weights():
 def test_failed_capture_falls_back_to_eager():
     """an error inside the capture (here a host synchronisation in the middle of
     the step, which a capturing stream refuses -- like an uncapturable collective) must not kill the
-    run: CapturedStep reports it, drops the graph and runs every step eagerly, in the same process,
-    bit-identical to an all-eager run."""
+    run: CapturedStep reports it, drops the graph, replaces the streams the capture left stuck and
+    runs every step eagerly, in the same process, bit-identical to an all-eager run."""
     batches = _cifar_batches(6, 23)
 
     def run(inject):
         torch.manual_seed(0)
         m = resnet18(num_classes=10).to(DEV)
+        m.engine_setup(DEV)
+        m._be.aux_min_pixels = 0   # branch + side streams on: the capture forks them before failing
         opt = _sgd(m)
         x, y = batches[0][0].clone(), batches[0][1].clone()
 
