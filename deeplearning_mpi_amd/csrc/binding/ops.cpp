@@ -15,6 +15,7 @@ namespace dlmpi_ext {
 
 using dlmpi::ConvArgs;
 using dlmpi::ConvPhase;
+using dlmpi::FinArgs;
 using dlmpi::make_fastdiv;
 using dlmpi::WgradArgs;
 
@@ -214,13 +215,98 @@ static void set_prologue(ConvArgs& a, int pro, const c10::optional<at::Tensor>& 
   }
 }
 
+static at::Tensor colsum_ws(const at::Tensor& like, int T, int C);
+
+// In-launch BN finalize (bnfin.h) of a launch producing T stats rows over Kout channels: groups of
+// ~sqrt(T) rows.  DLMPI_FIN_IN_LAUNCH = largest T that finalizes in-launch (0 = off: the finalize
+// runs as its own launch).
+// Default 0: measured slower on ResNet-50 (profiles/r3_fin_in_launch_rejected: 11,941 img/s with every
+// finalize in-launch, 12,009 with T <= 512 only, 12,030 off) -- every conv block pays a drain of its
+// output stores + a returning ticket atomic before it can retire, which costs more than the
+// finalize launch it removes.
+static int g_fin_override = -1;   // dlmpi_ext set_fin_in_launch (tests)
+static int fin_in_launch_max() {
+  static const int v = [] {
+    const char* e = getenv("DLMPI_FIN_IN_LAUNCH");
+    return e ? atoi(e) : 0;
+  }();
+  return g_fin_override >= 0 ? g_fin_override : v;
+}
+
+static bool setup_fin(ConvArgs& a, int T, const FinArgs& f, int k2) {
+  if (T <= 0 || T > fin_in_launch_max()) return false;
+  int G = 8;
+  while (G * G < T && G < 256) G *= 2;
+  const int NG = ceil_div(T, G);
+  double* gsum = nullptr;
+  int* tk = nullptr;
+  if (!dlmpi_fin_scratch(cur_stream(), (size_t)NG * 2 * a.Kout, a.ntiles * (NG + 1), &gsum, &tk)) return false;
+  a.fin_on = 1;
+  a.fin_group = G;
+  a.fin_ngroups = NG;
+  a.fin_T = T;
+  a.fin_k2 = k2;
+  a.fin_gsum = gsum;
+  a.fin_tk = tk;
+  a.fin = f;
+  return true;
+}
+
 // y[n, p, q, yoff + k] = epilogue( sum_{r,s,c} x[n, p*stride - pad + r, q*stride - pad + s, xoff + c] * w[k][r][s][c] )
+// fin (with stats): also finalize the BatchNorm over these statistics -- inside the launch when the
+// in-launch finalize is available, else by the standalone finalize right after it.
+static int conv2d_fwd_impl(const at::Tensor& x, int N, int H, int W, int C, int ldx, int xoff, const at::Tensor& w, int K, int R,
+               int S, int stride, int pad, at::Tensor y, int ldy, int yoff, const c10::optional<at::Tensor>& bias,
+               const c10::optional<at::Tensor>& res, int ldres, int resoff, const c10::optional<at::Tensor>& scale,
+               const c10::optional<at::Tensor>& shift, bool relu, const c10::optional<at::Tensor>& stats, int bm_req,
+               int kvalid, int bn_req, int pro, const c10::optional<at::Tensor>& pk0,
+               const c10::optional<at::Tensor>& pk1, const c10::optional<at::Tensor>& pz, int ldpz, int pzoff,
+               const FinArgs* fin);
+
 int conv2d_fwd_pro(const at::Tensor& x, int N, int H, int W, int C, int ldx, int xoff, const at::Tensor& w, int K, int R,
                int S, int stride, int pad, at::Tensor y, int ldy, int yoff, const c10::optional<at::Tensor>& bias,
                const c10::optional<at::Tensor>& res, int ldres, int resoff, const c10::optional<at::Tensor>& scale,
                const c10::optional<at::Tensor>& shift, bool relu, const c10::optional<at::Tensor>& stats, int bm_req,
                int kvalid, int bn_req, int pro, const c10::optional<at::Tensor>& pk0,
                const c10::optional<at::Tensor>& pk1, const c10::optional<at::Tensor>& pz, int ldpz, int pzoff) {
+  return conv2d_fwd_impl(x, N, H, W, C, ldx, xoff, w, K, R, S, stride, pad, y, ldy, yoff, bias, res, ldres, resoff,
+                         scale, shift, relu, stats, bm_req, kvalid, bn_req, pro, pk0, pk1, pz, ldpz, pzoff, nullptr);
+}
+
+// conv2d_fwd_pro + the training BatchNorm finalize of its statistics (scale / shift / saved mean and
+// invstd / running statistics), as one launch when possible.
+int conv2d_fwd_bn(const at::Tensor& x, int N, int H, int W, int C, int ldx, int xoff, const at::Tensor& w, int K, int R,
+                  int S, int stride, int pad, at::Tensor y, int ldy, int yoff, const c10::optional<at::Tensor>& bias,
+                  const at::Tensor& stats, int pro, const c10::optional<at::Tensor>& pk0,
+                  const c10::optional<at::Tensor>& pk1, const c10::optional<at::Tensor>& pz, int ldpz, int pzoff,
+                  double count, const c10::optional<at::Tensor>& gamma, const c10::optional<at::Tensor>& beta,
+                  const c10::optional<at::Tensor>& running_mean, const c10::optional<at::Tensor>& running_var,
+                  double momentum, double eps, at::Tensor bnscale, at::Tensor bnshift,
+                  const c10::optional<at::Tensor>& save_mean, const c10::optional<at::Tensor>& save_invstd) {
+  FinArgs f{};
+  f.mode = 0;
+  f.count = count;
+  f.gamma = optr<float>(gamma);
+  f.beta = optr<float>(beta);
+  f.running_mean = optr<float>(running_mean);
+  f.running_var = optr<float>(running_var);
+  f.momentum = (float)momentum;
+  f.eps = (float)eps;
+  f.scale = ptr<float>(bnscale);
+  f.shift = ptr<float>(bnshift);
+  f.save_mean = optr<float>(save_mean);
+  f.save_invstd = optr<float>(save_invstd);
+  return conv2d_fwd_impl(x, N, H, W, C, ldx, xoff, w, K, R, S, stride, pad, y, ldy, yoff, bias, c10::nullopt, 0, 0,
+                         c10::nullopt, c10::nullopt, false, stats, 0, 0, 0, pro, pk0, pk1, pz, ldpz, pzoff, &f);
+}
+
+static int conv2d_fwd_impl(const at::Tensor& x, int N, int H, int W, int C, int ldx, int xoff, const at::Tensor& w, int K, int R,
+               int S, int stride, int pad, at::Tensor y, int ldy, int yoff, const c10::optional<at::Tensor>& bias,
+               const c10::optional<at::Tensor>& res, int ldres, int resoff, const c10::optional<at::Tensor>& scale,
+               const c10::optional<at::Tensor>& shift, bool relu, const c10::optional<at::Tensor>& stats, int bm_req,
+               int kvalid, int bn_req, int pro, const c10::optional<at::Tensor>& pk0,
+               const c10::optional<at::Tensor>& pk1, const c10::optional<at::Tensor>& pz, int ldpz, int pzoff,
+               const FinArgs* fin) {
   require_gpu(x, "x");
   const int P = (H + 2 * pad - R) / stride + 1, Q = (W + 2 * pad - S) / stride + 1;
   ConvArgs a{};
@@ -253,7 +339,18 @@ int conv2d_fwd_pro(const at::Tensor& x, int N, int H, int W, int C, int ldx, int
   p.wr0 = 0; p.wrs = 1; p.ws0 = 0; p.wss = 1;
   p.oh0 = 0; p.ow0 = 0;
   finish_phase(p, N, C, bm, a.f32);
+  if (fin != nullptr) {
+    if (!a.stats || stats->size(0) < p.mtiles) throw std::runtime_error("conv2d_fwd_bn: stats [mtiles][2][K] required");
+    setup_fin(a, p.mtiles, *fin, 1);
+  }
   check(dlmpi_conv_igemm(&a, bm, bn, cur_stream()), "conv2d_fwd");
+  if (fin != nullptr && !a.fin_on) {   // no scratch (e.g. first use inside a capture): separate finalize
+    at::Tensor ws = colsum_ws(*stats, p.mtiles, K);
+    check(dlmpi_bn_finalize(a.stats, p.mtiles, K, fin->count, fin->gamma, fin->beta, fin->running_mean,
+                            fin->running_var, fin->momentum, fin->eps, fin->scale, fin->shift, fin->save_mean,
+                            fin->save_invstd, ptr<double>(ws), cur_stream()),
+          "bn_finalize");
+  }
   return p.mtiles;   // rows of the stats partial buffer
 }
 
@@ -901,6 +998,8 @@ void register_ops(pybind11::module& m) {
   namespace py = pybind11;
   m.def("conv2d_fwd", &conv2d_fwd);
   m.def("conv2d_fwd_pro", &conv2d_fwd_pro);
+  m.def("conv2d_fwd_bn", &conv2d_fwd_bn);
+  m.def("set_fin_in_launch", [](int max_t) { g_fin_override = max_t; });
   m.def("conv2d_fwd_mtiles", &conv2d_fwd_mtiles);
   m.def("conv2d_fwd_mtiles_pro", &conv2d_fwd_mtiles_pro);
   m.def("conv2d_fwd_bnbwd", &conv2d_fwd_bnbwd);

@@ -14,6 +14,7 @@
 #include <cstdlib>
 
 #include "common.h"
+#include "bnfin.h"
 
 namespace dlmpi {
 
@@ -263,63 +264,6 @@ static inline int colsum_slices(int T) {
   }();
   int S = (T + tps - 1) / tps;
   return S < 1 ? 1 : (S > smax ? smax : S);
-}
-
-// Per-channel finalize bodies, shared by the two-kernel path and the fused last-arriver path.
-struct FinArgs {
-  int mode;   // 0: forward statistics -> scale/shift (+ running stats); 1: backward coefficients
-  double count;
-  const float* gamma;
-  const float* beta;
-  float* running_mean;
-  float* running_var;
-  float momentum, eps;
-  float* scale;
-  float* shift;
-  float* save_mean;
-  float* save_invstd;
-  const float* mean;     // backward
-  const float* invstd;
-  float* dgamma;
-  float* dbeta;
-  float* coef;
-  int raw_z;
-};
-
-__device__ __forceinline__ void fin_fwd(const FinArgs& f, int c, double s1, double s2) {
-  const double mean = s1 / f.count;
-  double var = s2 / f.count - mean * mean;
-  if (var < 0.0) var = 0.0;
-  const float invstd = (float)(1.0 / sqrt(var + (double)f.eps));
-  const float g = f.gamma ? f.gamma[c] : 1.f;
-  const float b = f.beta ? f.beta[c] : 0.f;
-  const float sc = g * invstd;
-  f.scale[c] = sc;
-  f.shift[c] = b - (float)mean * sc;
-  if (f.save_mean) f.save_mean[c] = (float)mean;
-  if (f.save_invstd) f.save_invstd[c] = invstd;
-  if (f.running_mean) {
-    const double unbiased = f.count > 1.0 ? var * f.count / (f.count - 1.0) : var;
-    f.running_mean[c] = (1.f - f.momentum) * f.running_mean[c] + f.momentum * (float)mean;
-    f.running_var[c] = (1.f - f.momentum) * f.running_var[c] + f.momentum * (float)unbiased;
-  }
-}
-
-// coef[0..2][C] = (k1, k2, k3) with dx = k1*dyr + k2*x + k3; dgamma/dbeta accumulate.
-__device__ __forceinline__ void fin_bwd(const FinArgs& f, int c, double s1, double s2, int C) {
-  // raw_z: the second sum is sum dyr*z (BN input), not sum dyr*xhat
-  if (f.raw_z) s2 = (double)f.invstd[c] * (s2 - (double)f.mean[c] * s1);
-  if (f.dbeta) f.dbeta[c] += (float)s1;
-  if (f.dgamma) f.dgamma[c] += (float)s2;
-  if (f.coef) {
-    const double is = f.invstd[c];
-    const double k1 = (f.gamma ? (double)f.gamma[c] : 1.0) * is;
-    const double k2 = -k1 * is * s2 / f.count;
-    const double k3 = -k1 * s1 / f.count - k2 * (double)f.mean[c];
-    f.coef[c] = (float)k1;
-    f.coef[C + c] = (float)k2;
-    f.coef[2 * C + c] = (float)k3;
-  }
 }
 
 __global__ __launch_bounds__(256) void finalize_kernel(const double* __restrict__ dpart, int S, int C, FinArgs f) {
@@ -771,6 +715,41 @@ extern "C" int* dlmpi_splitk_tickets(hipStream_t s, int n) {
     g_sk_tk[dev][r] = p;
   }
   return g_sk_tk[dev][r];
+}
+
+// Scratch of the conv epilogue's in-launch BN finalize (bnfin.h), per device and stream role: fp64
+// group sums (grown on demand outside captures, never freed -- a captured graph may reference it)
+// and self-resetting tickets (zeroed once, ordered before the first kernel that uses them).
+static double* g_fin_gsum[64][kTicketRoles] = {};
+static size_t g_fin_gsum_n[64][kTicketRoles] = {};
+static int* g_fin_tk[64][kTicketRoles] = {};
+constexpr int kFinTickets = 1 << 16;
+
+extern "C" int dlmpi_fin_scratch(hipStream_t s, size_t gsum_doubles, int tickets, double** gsum, int** tk) {
+  int dev = 0;
+  if (tickets > kFinTickets || hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 0;
+  const int r = role_of(s, dev);
+  const bool need = g_fin_gsum_n[dev][r] < gsum_doubles || !g_fin_tk[dev][r];
+  if (need) {
+    hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(s, &st) != hipSuccess || st != hipStreamCaptureStatusNone) return 0;
+  }
+  if (g_fin_gsum_n[dev][r] < gsum_doubles) {
+    const size_t n = gsum_doubles + gsum_doubles / 2 + 4096;
+    double* p = nullptr;
+    if (hipMalloc(&p, n * sizeof(double)) != hipSuccess) return 0;
+    g_fin_gsum[dev][r] = p;
+    g_fin_gsum_n[dev][r] = n;
+  }
+  if (!g_fin_tk[dev][r]) {
+    int* p = nullptr;
+    if (hipMalloc(&p, kFinTickets * sizeof(int)) != hipSuccess) return 0;
+    if (hipMemsetAsync(p, 0, kFinTickets * sizeof(int), s) != hipSuccess) return 0;
+    g_fin_tk[dev][r] = p;
+  }
+  *gsum = g_fin_gsum[dev][r];
+  *tk = g_fin_tk[dev][r];
+  return 1;
 }
 
 static bool fused_finalize() {

@@ -29,6 +29,7 @@
 #endif
 
 #include "common.h"
+#include "bnfin.h"
 
 namespace dlmpi {
 
@@ -576,6 +577,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(STAGES 
       red[(rg * 3 + 2) * BN + cg * 8 + e] = s3[e];
     }
     __syncthreads();
+    const bool fin = !SKM && a.fin_on;
     if (tid < BN && n0 + tid < a.Kout) {
       float t1 = 0.f, t2 = 0.f, t3 = 0.f;
       for (int g = 0; g < RG; ++g) {
@@ -584,9 +586,21 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(STAGES 
         t3 += red[(g * 3 + 2) * BN + tid];
       }
       float* st = a.stats + (int64_t)(ph.tile_base + mt) * ns * a.Kout + n0 + tid;
-      st[0] = t1;
-      st[a.Kout] = t2;
-      if (ns > 2) st[2 * a.Kout] = t3;
+      if (fin) {   // published write-through for the in-launch finalize (bnfin.h)
+        st_sc1(st, t1);
+        st_sc1(st + a.Kout, t2);
+        if (ns > 2) st_sc1(st + 2 * a.Kout, t3);
+      } else {
+        st[0] = t1;
+        st[a.Kout] = t2;
+        if (ns > 2) st[2 * a.Kout] = t3;
+      }
+    }
+    if (fin) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every storing wave drains its row stores
+      __syncthreads();                                   // (also: red is free again)
+      fin_in_launch<NT, BN>(a, a.stats, ns, ph.tile_base + mt, nt, n0, reinterpret_cast<double*>(smem),
+                            reinterpret_cast<int*>(smem + 2 * NT * sizeof(double)));
     }
   }
   if constexpr (!SKM) break;
@@ -741,7 +755,7 @@ extern "C" hipError_t dlmpi_conv_igemm(const ConvArgs* a_in, int bm, int bn, hip
     kzero |= a_in->ph[i].ksteps == 0;
     iters += a_in->ph[i].mtiles * a_in->ntiles * a_in->ph[i].ksteps;
   }
-  if (skm && ab.splitk == 1 && sk_tile && a->pro == 0 && a->C >= 64 && stages_choice() == 1 && !kzero &&
+  if (skm && !a->fin_on && ab.splitk == 1 && sk_tile && a->pro == 0 && a->C >= 64 && stages_choice() == 1 && !kzero &&
       tiles <= 4096 && iters > 0) {
     int occ = 2;
     if (bm == 128 && bn == 128) occ = sk_occupancy<128, 128>();

@@ -33,6 +33,28 @@ inline FastDiv make_fastdiv(uint32_t d) {
 // A forward conv is one phase (sa = stride, dh0 = -pad); a strided data-gradient or a
 // transposed conv is stride^2 phases (sub-pixel decomposition), selected by blockIdx.z.
 // ---------------------------------------------------------------------------------------------
+// Per-channel BatchNorm finalize arguments (bn.hip colsum kernels and the in-launch finalize of
+// the conv epilogue, bnfin.h).
+struct FinArgs {
+  int mode;   // 0: forward statistics -> scale/shift (+ running stats); 1: backward coefficients
+  double count;
+  const float* gamma;
+  const float* beta;
+  float* running_mean;
+  float* running_var;
+  float momentum, eps;
+  float* scale;
+  float* shift;
+  float* save_mean;
+  float* save_invstd;
+  const float* mean;     // backward
+  const float* invstd;
+  float* dgamma;
+  float* dbeta;
+  float* coef;
+  int raw_z;
+};
+
 struct ConvPhase {
   int P, Q;
   int Tr, Ts;
@@ -103,6 +125,15 @@ struct ConvArgs {
   const float* pcoef;
   const void* pz;
   int ldpz, pzoff;
+  // In-launch BatchNorm finalize of the statistics this launch produces (bnfin.h): every block
+  // publishes its stats row write-through; the last arriver of each group of fin_group stats tiles
+  // sums the group, the last group of each N-tile sums the group sums and finalizes that N-tile's
+  // channels (fin).  Saves the separate finalize launch on the BN critical path.
+  int fin_on;
+  int fin_group, fin_ngroups, fin_T, fin_k2;
+  double* fin_gsum;                // [ngroups][2][Kout]
+  int* fin_tk;                     // [ntiles][ngroups] group tickets, then [ntiles] N-tile tickets
+  FinArgs fin;
   ConvPhase ph[4];
 };
 
@@ -280,6 +311,7 @@ hipError_t dlmpi_image_batch(const uint8_t* data, const int64_t* labels, const i
 
 // fault injection: keep stream s busy for `ms` milliseconds (bounded; tests of the watchdog)
 hipError_t dlmpi_delay(double ms, hipStream_t s);
+int dlmpi_fin_scratch(hipStream_t s, size_t gsum_doubles, int tickets, double** gsum, int** tk);
 
 // utilities (util.hip): fp32 fill, int64 add, indexed gather dst[i] (+)= src[idx[i]] (idx < 0: zero;
 // esize 2 | 4 bytes, accumulate: fp32 only)

@@ -353,26 +353,28 @@ class ConvUnit:
                         self.Kp)
             else:
                 z = Act.empty(N, P, Q, self.Kp, be.act_dtype, dev)
+            vec = torch.empty(4, self.Kp, dtype=be.dt, device=dev)
+            scale, shift, mean, invstd = vec[0], vec[1], vec[2], vec[3]
+            mom = bn.momentum
+            if mom is None:   # cumulative moving average
+                mom = 1.0 / float(bn.num_batches_tracked.item())
+            fin = (N * P * Q, bn.weight.data if bn.affine else None, bn.bias.data if bn.affine else None,
+                   bn.running_mean if bn.track_running_stats else None,
+                   bn.running_var if bn.track_running_stats else None, mom, bn.eps, scale, shift, mean, invstd)
             if chunked:
                 stats, mt = self._conv_chunked(be, x, wf, z)
                 x = x.y
+                self.arena.wait_buffers()   # DDP's asynchronous buffer broadcast must land first
+                be.bn_finalize(stats, mt, self.Kp, *fin)
             else:
                 mt = be.conv_mtiles(N, x.H, x.W, x.C, self.Kp, self.R, self.S, self.stride, self.pad,
                                     pro=isinstance(x, Deferred))
                 stats = torch.empty(mt, 2, self.Kp, dtype=be.dt, device=dev)
-                be.conv_fwd(x, wf, self.Kp, self.R, self.S, self.stride, self.pad, z, bias=self._bias_vec(),
-                            stats=stats)
-            vec = torch.empty(4, self.Kp, dtype=be.dt, device=dev)
-            scale, shift, mean, invstd = vec[0], vec[1], vec[2], vec[3]
-            self.arena.wait_buffers()   # DDP's asynchronous buffer broadcast must land first
-            mom = bn.momentum
-            if mom is None:   # cumulative moving average
-                mom = 1.0 / float(bn.num_batches_tracked.item())
-            be.bn_finalize(stats, mt, self.Kp, N * P * Q, bn.weight.data if bn.affine else None,
-                           bn.bias.data if bn.affine else None,
-                           bn.running_mean if bn.track_running_stats else None,
-                           bn.running_var if bn.track_running_stats else None, mom, bn.eps, scale, shift, mean,
-                           invstd)
+                # the finalize (in the conv launch itself when possible) reads / updates the running
+                # statistics: DDP's asynchronous buffer broadcast must land before the conv
+                self.arena.wait_buffers()
+                be.conv_fwd_bn(x, wf, self.Kp, self.R, self.S, self.stride, self.pad, z, self._bias_vec(), stats,
+                               *fin)
             if defer_apply and save and res is None:
                 ctx = (x, z, None, mean, invstd, scale, shift, False, None)
                 if defer_apply == "act":

@@ -157,6 +157,16 @@ class NativeBackend:
                               res.off if res is not None else 0, scale, shift, bool(relu), stats, 0, int(kvalid), 0,
                               pm, k0, k1, zb, zld, zoff)
 
+    def conv_fwd_bn(self, x, w, K, R, S, stride, pad, z: Act, bias, stats, count, gamma, beta, rm, rv, momentum,
+                    eps, scale, shift, save_mean, save_invstd):
+        """conv_fwd into z with the BN-statistics epilogue AND the training-BN finalize of those
+        statistics (scale / shift / mean / invstd / running stats) -- in the same launch when the
+        in-launch finalize applies (csrc/kernels/bnfin.h), else followed by the finalize launch."""
+        x, pm, k0, k1, zb, zld, zoff = self._pro(x)
+        self.C.conv2d_fwd_bn(x.buf, x.N, x.H, x.W, x.C, x.ld, x.off, w, K, R, S, stride, pad, z.buf, z.ld, z.off,
+                             bias, stats, pm, k0, k1, zb, zld, zoff, float(count), gamma, beta, rm, rv,
+                             float(momentum), float(eps), scale, shift, save_mean, save_invstd)
+
     def conv_fwd_bnbwd(self, x: Act, w, K, R, S, stride, pad, y: Act, fuse):
         """Forward conv producing the gradient of relu(BN(z)) (fuse = BwdFuse(None, z, None, scale,
         shift)): masked in the epilogue, BN-backward partials [tiles][2][K] returned."""
@@ -458,6 +468,12 @@ class RefBackend:
         if relu:
             out = F.relu(out)
         self._store(y, out)
+
+    def conv_fwd_bn(self, x, w, K, R, S, stride, pad, z: Act, bias, stats, count, gamma, beta, rm, rv, momentum,
+                    eps, scale, shift, save_mean, save_invstd):
+        self.conv_fwd(x, w, K, R, S, stride, pad, z, bias=bias, stats=stats)
+        self.bn_finalize(stats, stats.shape[0], K, count, gamma, beta, rm, rv, momentum, eps, scale, shift,
+                         save_mean, save_invstd)
 
     def dual_weights(self, wT, C, K, coef):
         w = wT.reshape(C, K).to(self.dt)

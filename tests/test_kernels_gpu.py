@@ -763,3 +763,53 @@ def test_deferred_bn_passes_bit_identical_training(model):
     assert torch.equal(res[0][0], res[1][0])
     for a, b in zip(res[0][1] + res[0][2], res[1][1] + res[1][2]):
         assert torch.equal(a, b)
+
+
+# ------------------------------------------------------------------ in-launch BN finalize
+FIN_SHAPES = [
+    # N, H, W, Cin, Cout, R, stride, pad
+    (2, 14, 14, 64, 64, 3, 1, 1),        # 4 stats tiles: one group
+    (16, 28, 28, 64, 256, 1, 1, 0),      # 98 tiles x 2 N-tiles: several groups
+    (32, 56, 56, 64, 64, 1, 1, 0),       # 256-row / 64-wide tiles, many groups
+    (8, 14, 14, 256, 1024, 1, 1, 0),     # 8 N-tiles
+    (4, 16, 16, 512, 512, 3, 1, 1),      # 3x3, split-K grid
+    (2, 32, 32, 3, 64, 7, 2, 3),         # stem (small channels)
+    (64, 14, 14, 256, 256, 3, 1, 1),     # 8-wave 256-row tiles
+]
+
+
+@pytest.mark.parametrize("shape", FIN_SHAPES)
+def test_conv_fwd_bn_in_launch_finalize(shape, monkeypatch):
+    """conv + BN statistics + the training-BN finalize in ONE launch (csrc/kernels/bnfin.h: two-level
+    last-arriver tree over write-through stats rows; off by default, measured slower) against the
+    conv followed by the standalone finalize kernel: same z, same partials, scale / shift / mean / invstd / running stats within fp64-
+    summation-order noise; repeated launches (self-resetting tickets) give identical results."""
+    N, H, W, Cin, Cout, R, s, p = shape
+    nb = NativeBackend(DEV)
+    Cp = pad8(Cin)
+    x, _ = _act(N, H, W, Cp)
+    w = (torch.randn(Cout, R, R, Cp, device=DEV) * 0.1).to(torch.bfloat16)
+    P, Q = (H + 2 * p - R) // s + 1, (W + 2 * p - R) // s + 1
+    mt = nb.conv_mtiles(N, H, W, Cp, Cout, R, R, s, p)
+    gamma, beta = torch.rand(Cout, device=DEV) + 0.5, torch.randn(Cout, device=DEV)
+    res = []
+    for mode in ("fused", "fused", "separate"):
+        nb.C.set_fin_in_launch(1 << 30 if mode == "fused" else 0)
+        z = _empty(N, P, Q, Cout)
+        stats = torch.empty(mt, 2, Cout, device=DEV)
+        rm, rv = torch.zeros(Cout, device=DEV), torch.ones(Cout, device=DEV)
+        v = torch.empty(4, Cout, device=DEV)
+        if mode == "fused":
+            nb.conv_fwd_bn(x, w, Cout, R, R, s, p, z, None, stats, N * P * Q, gamma, beta, rm, rv, 0.1, 1e-5,
+                           v[0], v[1], v[2], v[3])
+        else:
+            nb.conv_fwd(x, w, Cout, R, R, s, p, z, stats=stats)
+            nb.bn_finalize(stats, mt, Cout, N * P * Q, gamma, beta, rm, rv, 0.1, 1e-5, v[0], v[1], v[2], v[3])
+        torch.cuda.synchronize()
+        res.append((z.buf.clone(), stats.clone(), v.clone(), rm.clone(), rv.clone()))
+    nb.C.set_fin_in_launch(-1)
+    for a, b in zip(res[0], res[1]):
+        assert torch.equal(a, b)   # deterministic across launches
+    assert torch.equal(res[0][0], res[2][0]) and torch.equal(res[0][1], res[2][1])
+    for a, b in zip(res[0][2:], res[2][2:]):
+        assert _rel(a, b) < 1e-6, shape
