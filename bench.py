@@ -111,6 +111,12 @@ def main():
                                                       "(gloo + DLMPI_GLOO_DEVICE=cuda rehearses several ranks on one GPU)")
     ap.add_argument("--launcher", default="torchrun", choices=("torchrun", "mpirun"),
                     help="how --gpus N > 1 starts its ranks when not already under a launcher")
+    ap.add_argument("--rccl1", type=int, default=0,
+                    help="1 (single GPU only): run the step through a world-size-1 RCCL communicator with the "
+                         "bucketed reducer forced on (every all-reduce / the K5 broadcast go through RCCL)")
+    ap.add_argument("--host_time", type=int, default=0,
+                    help="N > 0: after the timed steps, N more steps timing the HOST issue time of each step "
+                         "(call to return, GPU running behind) against the GPU step time; printed to stderr")
     args = ap.parse_args()
     if args.gpus > 1 and not _under_launcher():
         sys.exit(launch_ranks(args.gpus, args.launcher, sys.argv[1:]))
@@ -154,7 +160,19 @@ def main():
         crit = BCEWithLogitsLoss()
         x, y = device_batch("segmentation", cfg["batch"], dev, shape, seed=1234 + comm.rank)
         optname = "Adam(lr=1e-4) + clip_grad_norm(1.0)"
-    ddp = dl.DistributedDataParallel(model, bucket_cap_mb=args.bucket_mb)
+    if args.rccl1:
+        if world != 1:
+            print("[bench] --rccl1 is a single-GPU option", file=sys.stderr, flush=True)
+            sys.exit(2)
+        from deeplearning_mpi_amd._ext import native
+        from deeplearning_mpi_amd.parallel.comm import RcclCommunicator, rccl_channel_budget
+
+        rccl_channel_budget()
+        nc = native().RcclComm(native().RcclComm.unique_id(), 0, 1, dev.index or 0)
+        rc = RcclCommunicator(comm.info, dev, nc)
+        ddp = dl.DistributedDataParallel(model, bucket_cap_mb=args.bucket_mb, comm=rc, _force_reducer=True)
+    else:
+        ddp = dl.DistributedDataParallel(model, bucket_cap_mb=args.bucket_mb)
 
     def step():
         opt.zero_grad()
@@ -226,6 +244,29 @@ def main():
         if comm.rank == 0:
             print(json.dumps({"breakdown_ms_per_step": bd, "max_over_ranks": bd_max,
                               "n_gpus": world, "config": args.config}), file=sys.stderr, flush=True)
+    host_info = None
+    if args.host_time > 0 and dev.type == "cuda":
+        # host issue time of one step: the CPU time from calling step() to its return while the GPU
+        # runs behind (no sync inside a step), vs the GPU time per step measured above -- if the
+        # host needs less than the GPU, an eager step stays GPU-bound
+        sync()
+        issue = []
+        t0 = time.perf_counter()
+        for _ in range(args.host_time):
+            a = time.perf_counter()
+            step()
+            issue.append(time.perf_counter() - a)
+        sync()
+        wall = time.perf_counter() - t0
+        issue.sort()
+        host_info = {"host_issue_ms_per_step_median": round(issue[len(issue) // 2] * 1e3, 3),
+                     "host_issue_ms_per_step_max": round(issue[-1] * 1e3, 3),
+                     "gpu_ms_per_step": round(dt / args.steps * 1e3, 3),
+                     "wall_ms_per_step_during_probe": round(wall / args.host_time * 1e3, 3),
+                     "host_over_gpu": round(issue[len(issue) // 2] / (dt / args.steps), 3)}
+        if comm.rank == 0:
+            print(json.dumps({"host_time": host_info, "config": args.config, "graph": bool(args.graph),
+                              "rccl1": bool(args.rccl1)}), file=sys.stderr, flush=True)
     if args.mem and comm.rank == 0 and dev.type == "cuda":
         ms = torch.cuda.memory_stats(dev)
         print(json.dumps({"mem": {"peak_allocated_gb": round(ms.get("allocated_bytes.all.peak", 0) / 2 ** 30, 2),
@@ -236,7 +277,7 @@ def main():
               file=sys.stderr, flush=True)
     # distributed facts of this run: the world size RCCL itself reports, its CU (channel) budget,
     # the gradient bucket layout, per-rank step times and the exposed all-reduce (max over ranks)
-    native_comm = getattr(getattr(comm, "inner", comm), "c", None)
+    native_comm = getattr(getattr(ddp.comm, "inner", ddp.comm), "c", None)
     dist_info = {
         "rccl_world_size": int(native_comm.size()) if native_comm is not None else None,
         "rccl_channels": os.environ.get("NCCL_MAX_NCHANNELS") if native_comm is not None else None,
@@ -245,6 +286,8 @@ def main():
         "per_rank_ms_per_step": {"min": min(per_rank_ms), "max": max(per_rank_ms)},
         "comm_exposed_ms": bd_max["comm_exposed"] if bd_max else None,
     }
+    if host_info is not None:
+        dist_info["host_time"] = host_info
     if comm.rank == 0:
         headline = args.config == "resnet50" and cfg == PRESETS["resnet50"]
         print(json.dumps({

@@ -1063,6 +1063,7 @@ void register_ops(pybind11::module& m) {
   m.def("scale_", &scale_);
   m.def("fill_", &fill_);
   m.def("set_conv_sk", [](int mode) { dlmpi_set_conv_sk(mode); });
+  m.def("set_conv_repi", [](int mode) { dlmpi_set_conv_repi(mode); });
   m.def("conv_sk_last", []() { return dlmpi_conv_sk_last(); });
   m.def("add_i64_", &add_i64_);
   m.def("gather_", &gather_);

@@ -55,7 +55,7 @@ __device__ __forceinline__ void glds16(const void* g, char* lds_wave_base) {
 // (phase, tile, K-step) iterations; tiles split between blocks are summed by their last-arriving
 // contributor in a fixed block order (deterministic), exactly like the split-K combine.
 template <int BM, int BN, bool SMALLC, int STAGES, int NW, int WGM, int PRO = 0, typename ET = uint16_t,
-          bool SKM = false>
+          bool SKM = false, bool REPI = false>
 __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(STAGES == 1 && BM * BN <= 16384 ? (BM * BN == 16384 ? DLMPI_W128 : 3) : 2, 8))) void conv_igemm_kernel(const ConvArgs a) {
   constexpr int NT = 64 * NW;                 // threads
   constexpr int WGN = NW / WGM;               // wave grid WGM x WGN
@@ -78,8 +78,11 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(STAGES 
   static_assert(WM % (16 * NP) == 0 || NP == 1, "epilogue pass must split every wave's rows evenly");
   constexpr int EPI_BYTES = (BM / NP) * CS_LD * 4;
   constexpr int RED_BYTES = (NT / (BN / 8)) * 3 * BN * 4;    // stats combine
-  constexpr int SMEM0 = STAGE_BYTES > EPI_BYTES ? STAGE_BYTES : EPI_BYTES;
-  constexpr int SMEM = SMEM0 > RED_BYTES ? SMEM0 : RED_BYTES;
+  // REPI: no fp32 tile staging; [WGM][3][BN] floats of statistics, or the in-launch finalize's
+  // 2 x NT doubles + flag
+  constexpr int REPI_BYTES = (WGM * 3 * BN * 4 > 2 * NT * 8 + 16) ? WGM * 3 * BN * 4 : 2 * NT * 8 + 16;
+  constexpr int EPI_NEED = REPI ? REPI_BYTES : (EPI_BYTES > RED_BYTES ? EPI_BYTES : RED_BYTES);
+  constexpr int SMEM = STAGE_BYTES > EPI_NEED ? STAGE_BYTES : EPI_NEED;
   __shared__ __attribute__((aligned(16))) char smem[SMEM];
 
   const int tid = threadIdx.x, lane = tid & 63;
@@ -350,7 +353,13 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(STAGES 
 #pragma unroll
         for (int ni = 0; ni < TN; ++ni) {
           if constexpr (sizeof(T) == 2) {
-            acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[mi], bfr[ni], acc[mi][ni], 0, 0, 0);
+            // REPI: D^T (rows = output channels, columns = pixels) -- the 16x16x32 operand layouts of
+            // A and B are symmetric, so swapping them transposes the tile: every lane then holds 4
+            // consecutive CHANNELS of one pixel, i.e. a contiguous 8-byte piece of an NHWC row
+            if constexpr (REPI)
+              acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[ni], af[mi], acc[mi][ni], 0, 0, 0);
+            else
+              acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[mi], bfr[ni], acc[mi][ni], 0, 0, 0);
           } else {
             // the lane's 16-byte chunk holds reduction elements 4 fg + j (j < 4) of this half-step:
             // MFMA j reduces element j of every lane group -- a fixed permutation of the K order,
@@ -442,6 +451,150 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(STAGES 
     __syncthreads();   // flag (LDS) is reused by the epilogue staging
   }
 
+  // ---- register-direct epilogue (REPI) --------------------------------------------------------
+  // No LDS staging of the fp32 tile: lane (fr, fg) holds, for pixel tile mi and channel tile ni,
+  // output[pixel wm*WM + 16 mi + fr][channels wn*WN + 16 ni + 4 fg + 0..3] (D^T fragments), so the
+  // epilogue math runs in registers and every lane stores / loads 8-byte channel quads directly.
+  // BatchNorm partial sums: per lane over its pixels, then over the 16 lanes of a DPP row
+  // (row_shr prefix chain, fixed order), then over the wave rows through a small LDS array.
+  if constexpr (REPI) {
+    static_assert(sizeof(T) == 2 && PRO == 0, "register epilogue: bf16, no operand prologue");
+    const int fr = lane & 15, fg = lane >> 4;
+    const bool bwd = a.mask != nullptr || a.mscale != nullptr || a.mbits != nullptr;
+    const int ns = a.nstat;
+    float s1[TN][4], s2[TN][4], s3[TN][4];
+#pragma unroll
+    for (int ni = 0; ni < TN; ++ni)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) { s1[ni][r] = 0.f; s2[ni][r] = 0.f; s3[ni][r] = 0.f; }
+    auto ld4 = [](const void* base, int64_t off) -> f32x4 {
+      const u32x2 q = *reinterpret_cast<const u32x2*>(static_cast<const uint16_t*>(base) + off);
+      return f32x4{__uint_as_float(q[0] << 16), __uint_as_float(q[0] & 0xffff0000u), __uint_as_float(q[1] << 16),
+                   __uint_as_float(q[1] & 0xffff0000u)};
+    };
+#pragma unroll
+    for (int mi = 0; mi < TM; ++mi) {
+      const int m = m0 + wm * WM + mi * 16 + fr;
+      if (m >= M) continue;
+      const uint32_t n_img = fdiv((uint32_t)m, ph.fdPQ);
+      const uint32_t rem = (uint32_t)m - n_img * PQ;
+      const uint32_t p = fdiv(rem, ph.fdQ);
+      const uint32_t q = rem - p * ph.Q;
+      const int64_t pix = ((int64_t)n_img * a.OH + (int)p * a.so + ph.oh0) * a.OW + (int)q * a.so + ph.ow0;
+#pragma unroll
+      for (int ni = 0; ni < TN; ++ni) {
+        const int c = n0 + wn * WN + ni * 16 + 4 * fg;
+        if (c >= a.Kout) continue;   // Kout % 8 == 0: a quad is all in or all out
+        f32x4 v = acc[mi][ni];
+        if (a.bias) v += *reinterpret_cast<const f32x4*>(a.bias + c);
+        if (a.stats && !bwd) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float rv = stored<T>(v[r]);
+            s1[ni][r] += rv;
+            s2[ni][r] += rv * rv;
+          }
+        }
+        if (a.scale) v = v * *reinterpret_cast<const f32x4*>(a.scale + c) + *reinterpret_cast<const f32x4*>(a.shift + c);
+        if (a.res) v += ld4(a.res, pix * a.ldres + a.resoff + c);
+        if (a.relu) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[r] = fmaxf(v[r], 0.f);
+        }
+        if (bwd) {
+          f32x4 zz = f32x4{0.f, 0.f, 0.f, 0.f};
+          if (a.z) zz = ld4(a.z, pix * a.ldz + a.zoff + c);
+          if (a.mbits) {
+            const uint32_t b = a.mbits[pix * (a.Kout >> 3) + (c >> 3)] >> (c & 7);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) v[r] = (b >> r) & 1u ? v[r] : 0.f;
+          } else if (a.mask) {
+            const f32x4 yy = ld4(a.mask, pix * a.ldmask + a.maskoff + c);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) v[r] = yy[r] > 0.f ? v[r] : 0.f;
+          } else {   // same fma as the forward BN-apply -> same sign as y
+            const f32x4 ms = *reinterpret_cast<const f32x4*>(a.mscale + c);
+            const f32x4 mh = *reinterpret_cast<const f32x4*>(a.mshift + c);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) v[r] = zz[r] * ms[r] + mh[r] > 0.f ? v[r] : 0.f;
+          }
+          if (a.stats) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const float rv = stored<T>(v[r]);
+              s1[ni][r] += rv;
+              s2[ni][r] += rv * zz[r];
+            }
+            if (a.z2) {
+              const f32x4 z2 = ld4(a.z2, pix * a.ldz2 + a.z2off + c);
+#pragma unroll
+              for (int r = 0; r < 4; ++r) s3[ni][r] += stored<T>(v[r]) * z2[r];
+            }
+          }
+        }
+        if (a.out_f32) {
+          *reinterpret_cast<f32x4*>(reinterpret_cast<float*>(a.y) + pix * a.ldy + a.yoff + c) = v;
+        } else {
+          const u32x2 pk = u32x2{pack2bf(v[0], v[1]), pack2bf(v[2], v[3])};
+          u32x2* yp = reinterpret_cast<u32x2*>(reinterpret_cast<uint16_t*>(a.y) + pix * a.ldy + a.yoff + c);
+          if (a.nt_store) __builtin_nontemporal_store(pk, yp);
+          else *yp = pk;
+        }
+      }
+    }
+    if (a.stats) {
+      // sum over the 16 pixel lanes of each DPP row: lane 15 of the row ends with the full sum
+      auto row_sum = [](float v) {
+        v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x111, 0xf, 0xf, true));
+        v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x112, 0xf, 0xf, true));
+        v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x114, 0xf, 0xf, true));
+        v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x118, 0xf, 0xf, true));
+        return v;
+      };
+      float* red = reinterpret_cast<float*>(smem);   // [WGM][3][BN]
+      __syncthreads();   // the K loop's last LDS reads are done
+#pragma unroll
+      for (int ni = 0; ni < TN; ++ni)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float t1 = row_sum(s1[ni][r]), t2 = row_sum(s2[ni][r]);
+          const float t3 = ns > 2 ? row_sum(s3[ni][r]) : 0.f;
+          if (fr == 15) {
+            const int cl = wn * WN + ni * 16 + 4 * fg + r;
+            red[(wm * 3 + 0) * BN + cl] = t1;
+            red[(wm * 3 + 1) * BN + cl] = t2;
+            red[(wm * 3 + 2) * BN + cl] = t3;
+          }
+        }
+      __syncthreads();
+      const bool fin = !SKM && a.fin_on;
+      if (tid < BN && n0 + tid < a.Kout) {
+        float t1 = 0.f, t2 = 0.f, t3 = 0.f;
+#pragma unroll
+        for (int g = 0; g < WGM; ++g) {
+          t1 += red[(g * 3 + 0) * BN + tid];
+          t2 += red[(g * 3 + 1) * BN + tid];
+          t3 += red[(g * 3 + 2) * BN + tid];
+        }
+        float* st = a.stats + (int64_t)(ph.tile_base + mt) * ns * a.Kout + n0 + tid;
+        if (fin) {
+          st_sc1(st, t1);
+          st_sc1(st + a.Kout, t2);
+          if (ns > 2) st_sc1(st + 2 * a.Kout, t3);
+        } else {
+          st[0] = t1;
+          st[a.Kout] = t2;
+          if (ns > 2) st[2 * a.Kout] = t3;
+        }
+      }
+      if (fin) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        fin_in_launch<NT, BN>(a, a.stats, ns, ph.tile_base + mt, nt, n0, reinterpret_cast<double*>(smem),
+                              reinterpret_cast<int*>(smem + 2 * NT * sizeof(double)));
+      }
+    }
+  } else {
   // ---- epilogue ------------------------------------------------------------------------------
   float* Cs = reinterpret_cast<float*>(smem);
 
@@ -603,6 +756,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(STAGES 
                             reinterpret_cast<int*>(smem + 2 * NT * sizeof(double)));
     }
   }
+  }   // LDS epilogue
   if constexpr (!SKM) break;
   __syncthreads();   // LDS (epilogue staging / stats) is reused by the next segment's staging
   }   // segment loop
@@ -620,9 +774,31 @@ static int stages_choice() {
   return v;
 }
 
+// DLMPI_CONV_REPI: 1 = register-direct epilogue (D^T fragments, no LDS staging of the output tile)
+// for bf16 launches without operand prologue and with full-width vector stores; 0 (default) = the
+// LDS-staged epilogue.  Measured slower (profiles/r3_repi_rejected): per-network forward 4.86 vs
+// 4.70 ms, the memory-bound expand 1x1s +9..15 % (8-byte lane pieces make each store instruction
+// cover 16 rows x 32 B instead of 4 rows x 256 B), ResNet-50 step 10.8k vs 12.0k img/s (the masked
+// data-gradient epilogues' 8-byte z / mask loads).
+static int g_repi_override = -1;
+static bool repi_on(const ConvArgs* a) {
+  static const int v = [] {
+    const char* e = getenv("DLMPI_CONV_REPI");
+    return e ? atoi(e) : 0;
+  }();
+  const int m = g_repi_override >= 0 ? g_repi_override : v;
+  return m != 0 && !a->f32 && a->pro == 0 && a->vec_store && a->kvalid == a->Kout && a->Kout % 8 == 0;
+}
+extern "C" void dlmpi_set_conv_repi(int mode) { g_repi_override = mode; }
+
 template <int BM, int BN>
 static void launch_tile(const ConvArgs* a, dim3 grid, hipStream_t s) {
   const bool one = stages_choice() == 1;
+  if (one && repi_on(a)) {
+    if (a->C < 64) hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, true, 1, 4, 2, 0, uint16_t, false, true>), grid, dim3(256), 0, s, *a);
+    else hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, false, 1, 4, 2, 0, uint16_t, false, true>), grid, dim3(256), 0, s, *a);
+    return;
+  }
   if (a->pro == 1) {
     hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, false, 1, 4, 2, 1>), grid, dim3(256), 0, s, *a);
     return;
@@ -805,9 +981,13 @@ extern "C" hipError_t dlmpi_conv_igemm(const ConvArgs* a_in, int bm, int bn, hip
   if (a->pro != 0 && (a->C < 64 || a->C % 64 != 0 || (bm == 256 && bn == 256))) return hipErrorInvalidValue;
   if (bm == 256 && bn == 256) {   // 8 waves, double-buffered; regular channel counts only
     if (a->C < 64) return hipErrorInvalidValue;
-    hipLaunchKernelGGL((conv_igemm_kernel<256, 256, false, 2, 8, 2>), grid, dim3(512), 0, s, *a);
+    if (repi_on(a)) hipLaunchKernelGGL((conv_igemm_kernel<256, 256, false, 2, 8, 2, 0, uint16_t, false, true>), grid, dim3(512), 0, s, *a);
+    else hipLaunchKernelGGL((conv_igemm_kernel<256, 256, false, 2, 8, 2>), grid, dim3(512), 0, s, *a);
   } else if (bm == 256 && bn == 64) {   // 64-channel layers: 4 x 1 waves of 64 x 64
-    if (a->pro == 1) hipLaunchKernelGGL((conv_igemm_kernel<256, 64, false, 1, 4, 4, 1>), grid, dim3(256), 0, s, *a);
+    if (a->pro == 0 && repi_on(a)) {
+      if (a->C < 64) hipLaunchKernelGGL((conv_igemm_kernel<256, 64, true, 1, 4, 4, 0, uint16_t, false, true>), grid, dim3(256), 0, s, *a);
+      else hipLaunchKernelGGL((conv_igemm_kernel<256, 64, false, 1, 4, 4, 0, uint16_t, false, true>), grid, dim3(256), 0, s, *a);
+    } else if (a->pro == 1) hipLaunchKernelGGL((conv_igemm_kernel<256, 64, false, 1, 4, 4, 1>), grid, dim3(256), 0, s, *a);
     else if (a->pro == 2) hipLaunchKernelGGL((conv_igemm_kernel<256, 64, false, 1, 4, 4, 2>), grid, dim3(256), 0, s, *a);
     else if (a->C < 64) hipLaunchKernelGGL((conv_igemm_kernel<256, 64, true, 1, 4, 4>), grid, dim3(256), 0, s, *a);
     else hipLaunchKernelGGL((conv_igemm_kernel<256, 64, false, 1, 4, 4>), grid, dim3(256), 0, s, *a);

@@ -311,6 +311,7 @@ hipError_t dlmpi_image_batch(const uint8_t* data, const int64_t* labels, const i
 
 // fault injection: keep stream s busy for `ms` milliseconds (bounded; tests of the watchdog)
 hipError_t dlmpi_delay(double ms, hipStream_t s);
+void dlmpi_set_conv_repi(int mode);
 int dlmpi_fin_scratch(hipStream_t s, size_t gsum_doubles, int tickets, double** gsum, int** tk);
 
 // utilities (util.hip): fp32 fill, int64 add, indexed gather dst[i] (+)= src[idx[i]] (idx < 0: zero;
