@@ -16,6 +16,7 @@ namespace dlmpi_ext {
 using dlmpi::ConvArgs;
 using dlmpi::ConvPhase;
 using dlmpi::FinArgs;
+using dlmpi::Stream1x1Args;
 using dlmpi::make_fastdiv;
 using dlmpi::WgradArgs;
 
@@ -217,6 +218,18 @@ static void set_prologue(ConvArgs& a, int pro, const c10::optional<at::Tensor>& 
 
 static at::Tensor colsum_ws(const at::Tensor& like, int T, int C);
 
+// The streaming 1x1 kernel (conv1x1_stream.hip) applies to this forward conv: its statistics have
+// one row per block of an N-tile (G rows) instead of one per M-tile.  Shape-only decision (the
+// stats buffer is sized from it before the launch); the launch checks the rest (alignment, sizes).
+static int g_stream_ran = 0;   // 1 if the last conv2d_fwd ran the streaming 1x1 kernel (tests)
+
+static bool stream1x1_shape(int64_t M, int C, int K, int R, int S, int stride, int pad, int pro, int f32, int& bm,
+                            int& bn, int& G) {
+  if (R != 1 || S != 1 || stride != 1 || pad != 0 || pro != 0 || f32) return false;
+  return dlmpi_stream1x1_plan(M, C, K, &bm, &bn, &G) != 0;
+}
+
+
 // In-launch BN finalize (bnfin.h) of a launch producing T stats rows over Kout channels: groups of
 // ~sqrt(T) rows.  DLMPI_FIN_IN_LAUNCH = largest T that finalizes in-launch (0 = off: the finalize
 // runs as its own launch).
@@ -331,6 +344,42 @@ static int conv2d_fwd_impl(const at::Tensor& x, int N, int H, int W, int C, int 
   if (a.f32) f32_tiles(bm, bn);
   if (bm_req > 0) bm = bm_req;   // tests / experiments: force a tile shape
   if (bn_req > 0) bn = bn_req;
+  g_stream_ran = 0;
+  {  // streaming 1x1 kernel (short reductions into wide, memory-bound outputs)
+    const int64_t M = (int64_t)N * P * Q;
+    int sbm, sbn, G;
+    if (bm_req <= 0 && bn_req <= 0 && stream1x1_shape(M, C, K, R, S, stride, pad, pro, a.f32, sbm, sbn, G)) {
+      const bool ok = !res.has_value() && !scale.has_value() && !relu && a.kvalid == K && a.vec_store &&
+                      ldx % 8 == 0 && xoff % 8 == 0 && M * ldx < (1ll << 31) && M * ldy * 2 < (1ll << 31) &&
+                      y.scalar_type() == at::kBFloat16;
+      if (a.stats && !ok)
+        throw std::runtime_error("conv2d_fwd: statistics were sized for the streaming 1x1 kernel, which cannot run");
+      if (ok) {
+        Stream1x1Args sa{};
+        sa.x = ptr<uint16_t>(x);
+        sa.ldx = ldx; sa.xoff = xoff;
+        sa.w = ptr<uint16_t>(w);
+        sa.y = reinterpret_cast<uint16_t*>(a.y);
+        sa.ldy = ldy; sa.yoff = yoff;
+        sa.y_bytes = (int)std::min<int64_t>(INT32_MAX, (int64_t)y.numel() * 2);
+        sa.M = (int)M; sa.C = C; sa.Kout = K;
+        sa.bias = a.bias;
+        sa.stats = a.stats;
+        sa.G = G; sa.ntiles = K / sbn; sa.mtiles = ceil_div(M, sbm);
+        if (a.stats && stats->size(0) < G) throw std::runtime_error("conv2d_fwd: stats buffer too small");
+        check(dlmpi_conv1x1_stream(&sa, sbm, sbn, cur_stream()), "conv2d_fwd (stream 1x1)");
+        g_stream_ran = 1;
+        if (fin != nullptr) {
+          at::Tensor ws = colsum_ws(*stats, G, K);
+          check(dlmpi_bn_finalize(a.stats, G, K, fin->count, fin->gamma, fin->beta, fin->running_mean,
+                                  fin->running_var, fin->momentum, fin->eps, fin->scale, fin->shift, fin->save_mean,
+                                  fin->save_invstd, ptr<double>(ws), cur_stream()),
+                "bn_finalize");
+        }
+        return G;
+      }
+    }
+  }
   a.ntiles = ceil_div(K, bn);
   a.nphase = 1;
   ConvPhase& p = a.ph[0];
@@ -419,6 +468,8 @@ int conv2d_fwd_mtiles_pro(int N, int H, int W, int C, int K, int R, int S, int s
                           int f32) {
   const int P = (H + 2 * pad - R) / stride + 1, Q = (W + 2 * pad - S) / stride + 1;
   int bm, bn;
+  int G;
+  if (bm_req <= 0 && stream1x1_shape((int64_t)N * P * Q, C, K, R, S, stride, pad, pro, f32, bm, bn, G)) return G;
   pick_tiles((int64_t)N * P * Q, K, (int64_t)R * S * C, C, bm, bn, pro != 0);
   if (f32) f32_tiles(bm, bn);
   if (bm_req > 0) bm = bm_req;
@@ -1064,6 +1115,8 @@ void register_ops(pybind11::module& m) {
   m.def("fill_", &fill_);
   m.def("set_conv_sk", [](int mode) { dlmpi_set_conv_sk(mode); });
   m.def("set_conv_repi", [](int mode) { dlmpi_set_conv_repi(mode); });
+  m.def("set_conv_stream", [](int mode) { dlmpi_set_conv_stream(mode); });
+  m.def("conv_stream_last", []() { return g_stream_ran; });
   m.def("conv_sk_last", []() { return dlmpi_conv_sk_last(); });
   m.def("add_i64_", &add_i64_);
   m.def("gather_", &gather_);

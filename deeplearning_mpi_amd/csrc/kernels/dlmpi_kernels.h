@@ -55,6 +55,22 @@ struct FinArgs {
   int raw_z;
 };
 
+// Streaming 1x1 / stride-1 forward (conv1x1_stream.hip): y[m][yoff + n] = sum_c x[m][xoff + c] w[n][c]
+// (+ bias[n]) for m < M, bf16; stats (or null): [G][2][Kout] partial sums of the stored values, one
+// row per block of an N-tile.
+struct Stream1x1Args {
+  const uint16_t* x;
+  int ldx, xoff;
+  const uint16_t* w;               // [Kout][C]
+  uint16_t* y;
+  int ldy, yoff;
+  int y_bytes;                     // buffer-descriptor range of y (rows past M are dropped)
+  int M, C, Kout;
+  const float* bias;
+  float* stats;
+  int G, ntiles, mtiles;
+};
+
 struct ConvPhase {
   int P, Q;
   int Tr, Ts;
@@ -312,6 +328,9 @@ hipError_t dlmpi_image_batch(const uint8_t* data, const int64_t* labels, const i
 // fault injection: keep stream s busy for `ms` milliseconds (bounded; tests of the watchdog)
 hipError_t dlmpi_delay(double ms, hipStream_t s);
 void dlmpi_set_conv_repi(int mode);
+void dlmpi_set_conv_stream(int mode);
+int dlmpi_stream1x1_plan(int64_t M, int C, int Kout, int* bm, int* bn, int* G);
+hipError_t dlmpi_conv1x1_stream(const dlmpi::Stream1x1Args* a, int bm, int bn, hipStream_t s);
 int dlmpi_fin_scratch(hipStream_t s, size_t gsum_doubles, int tickets, double** gsum, int** tk);
 
 // utilities (util.hip): fp32 fill, int64 add, indexed gather dst[i] (+)= src[idx[i]] (idx < 0: zero;

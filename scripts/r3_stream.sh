@@ -1,0 +1,12 @@
+#!/bin/bash
+# Streaming 1x1 forward: correctness, per-shape conv bench (stream on/off), bench A/B.
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+cd "$R" && export HSA_ENABLE_IPC_MODE_LEGACY=0
+O=gpurun_out/r3_stream; mkdir -p $O
+timeout -k 10 600 python -u -m pytest tests/test_kernels_gpu.py -k "stream1x1 or conv_fwd or in_launch" -x -q --timeout 120 --timeout-method thread > $O/tests.log 2>&1
+rc=$?; tail -2 $O/tests.log; [ $rc -ne 0 ] && { grep -E "FAILED|Error|assert" $O/tests.log | head -20; exit 1; }
+for v in 0 1; do
+  DLMPI_CONV_STREAM=$v timeout -k 10 400 python benchmarks/conv_bench.py --iters 10 --no_miopen --only fwd > $O/cb_stream$v.log 2>&1 || { echo "cb fail $v"; tail $O/cb_stream$v.log; exit 1; }
+  tail -1 $O/cb_stream$v.log
+done
+CONFIGS=resnet50 STEPS=20 REPS=2 VARIANTS='base st0=DLMPI_CONV_STREAM=0' bash scripts/env_ab3.sh

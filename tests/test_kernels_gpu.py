@@ -817,3 +817,55 @@ def test_conv_fwd_bn_in_launch_finalize(shape, monkeypatch):
     assert torch.equal(res[0][0], res[2][0]) and torch.equal(res[0][1], res[2][1])
     for a, b in zip(res[0][2:], res[2][2:]):
         assert _rel(a, b) < 1e-6, shape
+
+
+# ------------------------------------------------------------------ streaming 1x1 forward
+STREAM_SHAPES = [
+    # N, H, W, Cin, Cout: 1x1 / stride 1 (the ResNet expand convs, small)
+    (4, 14, 14, 64, 256),      # 784 rows: 6.1 tiles of 128, ragged last tile
+    (2, 7, 9, 64, 128),        # 126 rows: a single partial tile
+    (8, 28, 28, 128, 512),
+    (4, 14, 14, 256, 1024),
+    (3, 5, 7, 256, 64),        # 105 rows, one N-tile
+    (32, 56, 56, 64, 256),     # bench-layer scale (100k rows, every block walks many tiles)
+]
+
+
+@pytest.mark.parametrize("shape", STREAM_SHAPES)
+@pytest.mark.parametrize("ld_out", ["dense", "dual"])
+def test_stream1x1_matches_general_kernel(shape, ld_out):
+    """conv1x1_stream.hip (persistent blocks, resident weights, prefetch under the epilogue, one
+    statistics row per block) against the general implicit-GEMM kernel: identical outputs (same
+    MFMA dot products and rounding), statistics summed over rows equal to fp32 noise, BN finalize
+    over the block rows equal to the finalize over the tile rows; 'dual' writes into the right half
+    of a [rows][2K] buffer (the dual data-gradient layout) and must leave the left half untouched."""
+    N, H, W, Cin, K = shape
+    nb = NativeBackend(DEV)
+    x, _ = _act(N, H, W, Cin)
+    w = (torch.randn(K, 1, 1, Cin, device=DEV) / Cin ** 0.5).to(torch.bfloat16)
+    bias = torch.randn(K, device=DEV) * 0.1
+    gamma, beta = torch.rand(K, device=DEV) + 0.5, torch.randn(K, device=DEV)
+    out = {}
+    for mode in (1, 0):
+        nb.C.set_conv_stream(mode)
+        mt = nb.conv_mtiles(N, H, W, Cin, K, 1, 1, 1, 0)
+        if ld_out == "dual":
+            buf = torch.full((N * H * W, 2 * K), 7.0, device=DEV).to(torch.bfloat16)
+            y = Act(buf, N, H, W, K, K)
+        else:
+            y = _empty(N, H, W, K)
+        st = torch.empty(mt, 2, K, device=DEV)
+        v = torch.empty(4, K, device=DEV)
+        rm, rv = torch.zeros(K, device=DEV), torch.ones(K, device=DEV)
+        nb.conv_fwd_bn(x, w, K, 1, 1, 1, 0, y, bias, st, N * H * W, gamma, beta, rm, rv, 0.1, 1e-5,
+                       v[0], v[1], v[2], v[3])
+        torch.cuda.synchronize()
+        assert nb.C.conv_stream_last() == mode   # the streaming kernel ran (mode 1) / did not (mode 0)
+        out[mode] = (y.buf.clone(), st.sum(0), v.clone(), rm.clone(), rv.clone(), mt)
+    nb.C.set_conv_stream(-1)
+    assert torch.equal(out[1][0], out[0][0])
+    if ld_out == "dual":
+        assert bool((out[1][0][:, :K].float() == 7.0).all())
+    assert _rel(out[1][1], out[0][1]) < 1e-5
+    for a, b in zip(out[1][2:5], out[0][2:5]):
+        assert _rel(a, b) < 1e-5
