@@ -222,6 +222,16 @@ using namespace dlmpi;
 
 // Tile plan of the streaming kernel: (BM, BN, blocks per N-tile G) or false if it does not apply.
 static int g_stream_override = -1;   // dlmpi_ext set_conv_stream (tests)
+// DLMPI_CONV_STREAM_C512=1: C = 512 (layer-4 expand, 7^2 512->2048) through the streaming kernel
+// too.  Off by default: its 144 KB of LDS leave one block per CU and it measured slower than the
+// general kernel (58.3 vs 50.7 us, profiles/r3_stream1x1/c512_*).
+static bool stream_c512() {
+  static const bool v = [] {
+    const char* e = getenv("DLMPI_CONV_STREAM_C512");
+    return e && atoi(e) != 0;
+  }();
+  return v;
+}
 extern "C" void dlmpi_set_conv_stream(int mode) { g_stream_override = mode; }
 
 extern "C" int dlmpi_stream1x1_plan(int64_t M, int C, int Kout, int* bm, int* bn, int* G) {
@@ -234,11 +244,13 @@ extern "C" int dlmpi_stream1x1_plan(int64_t M, int C, int Kout, int* bm, int* bn
   if (C == 64 && Kout % 128 == 0) { *bm = 128; *bn = 128; }
   else if (C == 128 && Kout % 128 == 0) { *bm = 64; *bn = 128; }
   else if (C == 256 && Kout % 64 == 0) { *bm = 64; *bn = 64; }
+  else if (C == 512 && Kout % 64 == 0 && stream_c512()) { *bm = 64; *bn = 64; }
   else return 0;
   const int ntiles = Kout / *bn;
   const int64_t mtiles = (M + *bm - 1) / *bm;
-  // ~2 resident blocks per CU over the whole chip (LDS 65-73 KB per block)
-  int target = 512 / ntiles;
+  // ~2 resident blocks per CU over the whole chip (LDS 65-80 KB per block); C = 512 holds 144 KB
+  // (1 block per CU)
+  int target = (C == 512 ? 256 : 512) / ntiles;
   if (target < 8) target = 8;
   *G = (int)(mtiles < target ? mtiles : target);
   return 1;
@@ -254,6 +266,7 @@ extern "C" hipError_t dlmpi_conv1x1_stream(const Stream1x1Args* a, int bm, int b
   if (bm == 128 && bn == 128 && a->C == 64) DLMPI_S1(128, 128, 1);
   else if (bm == 64 && bn == 128 && a->C == 128) DLMPI_S1(64, 128, 2);
   else if (bm == 64 && bn == 64 && a->C == 256) DLMPI_S1(64, 64, 4);
+  else if (bm == 64 && bn == 64 && a->C == 512) DLMPI_S1(64, 64, 8);
   else return hipErrorInvalidValue;
 #undef DLMPI_S1
   return hipGetLastError();

@@ -863,9 +863,13 @@ def test_stream1x1_matches_general_kernel(shape, ld_out):
         assert nb.C.conv_stream_last() == mode   # the streaming kernel ran (mode 1) / did not (mode 0)
         out[mode] = (y.buf.clone(), st.sum(0), v.clone(), rm.clone(), rv.clone(), mt)
     nb.C.set_conv_stream(-1)
-    assert torch.equal(out[1][0], out[0][0])
+    if Cin <= 256:
+        assert torch.equal(out[1][0], out[0][0])
+    else:   # the general kernel may split the 8 K-steps (split-K): another fp32 summation order
+        assert _rel(out[1][0], out[0][0]) < 1e-2
     if ld_out == "dual":
         assert bool((out[1][0][:, :K].float() == 7.0).all())
-    assert _rel(out[1][1], out[0][1]) < 1e-5
+    tol = 1e-5 if Cin <= 256 else 2e-4   # (split-K outputs differ in the last bf16 bit)
+    assert _rel(out[1][1], out[0][1]) < tol
     for a, b in zip(out[1][2:5], out[0][2:5]):
-        assert _rel(a, b) < 1e-5
+        assert _rel(a, b) < tol
