@@ -907,7 +907,8 @@ extern "C" hipError_t dlmpi_conv_igemm(const ConvArgs* a_in, int bm, int bn, hip
   const ConvArgs* a = &ab;
   ab.splitk = 1;
   g_sk_last = 0;
-  const int S = splitk_plan(tiles, maxk);
+  int S = a_in->splitk_req > 0 ? a_in->splitk_req : splitk_plan(tiles, maxk);
+  if (S > maxk) S = maxk > 0 ? maxk : 1;
   if (S > 1) {
     const int ntile_ids = maxt * a_in->ntiles * a_in->nphase;   // kernel: z * gridDim.x + mt * ntiles + nt
     float* slab = dlmpi_splitk_slab(s, (size_t)ntile_ids * S * bm * bn);

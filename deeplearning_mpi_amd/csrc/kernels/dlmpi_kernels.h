@@ -119,6 +119,7 @@ struct ConvArgs {
   int ntiles;
   int nphase;
   int splitk;                      // > 1: K split over blockIdx.y, last-arriver combine (set by the launcher)
+  int splitk_req;                  // 0: the launcher plans the split; >= 1: use exactly this (autotuner)
   float* sk_slab;                  // [tile][slice][TM*TN][threads] f32x4 fragment slabs
   int* sk_tk;                      // [tile] self-resetting arrival tickets
   // stream-K (set by the launcher): gridDim.x persistent blocks, block lb (XCD-remapped) runs the

@@ -301,14 +301,14 @@ class ConvUnit:
         xp.apply_images(be, 0, h)
         if side is not None:
             side.wait_stream(main)
-        o = 0
+        o = 0   # rows written so far (conv_mtiles is an upper bound; the launch returns the count)
         for i, ((n0, n1), mt) in enumerate(zip(halves, mts)):
             with torch.cuda.stream(side) if (i == 1 and side is not None) else contextlib.nullcontext():
                 if i == 1:
                     xp.apply_images(be, n0, n1)
-                be.conv_fwd(img_rows(xp.y, n0, n1), wf, self.Kp, self.R, self.S, self.stride, self.pad,
-                            img_rows(z, n0, n1), bias=bias, stats=stats[o:o + mt])
-            o += mt
+                rows = be.conv_fwd(img_rows(xp.y, n0, n1), wf, self.Kp, self.R, self.S, self.stride, self.pad,
+                                   img_rows(z, n0, n1), bias=bias, stats=stats[o:o + mt])
+            o += mt if rows is None else rows
         if side is not None:
             main.wait_stream(side)
         xp.done = True

@@ -151,11 +151,12 @@ class NativeBackend:
 
     def conv_fwd(self, x, w, K, R, S, stride, pad, y: Act, bias=None, res: Act = None, scale=None,
                  shift=None, relu=False, stats=None, kvalid=0):
+        """Returns the number of BN-statistics rows written (stats given)."""
         x, pm, k0, k1, zb, zld, zoff = self._pro(x)
-        self.C.conv2d_fwd_pro(x.buf, x.N, x.H, x.W, x.C, x.ld, x.off, w, K, R, S, stride, pad, y.buf, y.ld, y.off,
-                              bias, res.buf if res is not None else None, res.ld if res is not None else 0,
-                              res.off if res is not None else 0, scale, shift, bool(relu), stats, 0, int(kvalid), 0,
-                              pm, k0, k1, zb, zld, zoff)
+        return self.C.conv2d_fwd_pro(x.buf, x.N, x.H, x.W, x.C, x.ld, x.off, w, K, R, S, stride, pad, y.buf, y.ld,
+                                     y.off, bias, res.buf if res is not None else None,
+                                     res.ld if res is not None else 0, res.off if res is not None else 0, scale, shift,
+                                     bool(relu), stats, 0, int(kvalid), 0, pm, k0, k1, zb, zld, zoff)
 
     def conv_fwd_bn(self, x, w, K, R, S, stride, pad, z: Act, bias, stats, count, gamma, beta, rm, rv, momentum,
                     eps, scale, shift, save_mean, save_invstd):

@@ -662,6 +662,15 @@ PRO_SHAPES = [
 ]
 
 
+def _static_kernels(on: bool):
+    """Pin the plain implicit-GEMM kernel with the static tile rules (the operand-prologue kernels
+    have no register epilogue, streaming or autotuned variant): for bit-identity comparisons."""
+    C = NativeBackend(DEV).C
+    C.set_conv_repi(0 if on else -1)
+    C.set_conv_stream(0 if on else -1)
+    C.set_conv_autotune(0 if on else -1)
+
+
 def _deferred_pair(N, H, W, C):
     """(affine Deferred, its materialized Act) and (bnbwd Deferred, materialized)."""
     from deeplearning_mpi_amd.ops.act import Deferred
@@ -683,6 +692,14 @@ def test_conv_prologues_bit_identical_to_materialized_operands(shape):
     operand, weight gradient with either or both: every result bit-identical to the same kernels
     on the materialized tensors (incl. zero padding taps, row tails, stride-2 phases, split-K)."""
     nb = NativeBackend(DEV)
+    _static_kernels(True)
+    try:
+        _prologue_case(nb, shape)
+    finally:
+        _static_kernels(False)
+
+
+def _prologue_case(nb, shape):
     N, H, W, Cin, K, R, s, p = shape
     Cp, Kp = pad8(Cin), pad8(K)
     P, Q = (H + 2 * p - R) // s + 1, (W + 2 * p - R) // s + 1
@@ -741,9 +758,10 @@ def test_deferred_bn_passes_bit_identical_training(model):
     m0 = make().to(DEV)
     res = []
     old = (E.DEFER_BN_FWD, E.DEFER_BN_BWD)
-    # the prologue kernels use the LDS-staged epilogue: compare against the same epilogue (the
-    # register-direct epilogue sums the BN statistics in another order)
-    NativeBackend(DEV).C.set_conv_repi(0)
+    # the prologue kernels use the LDS-staged epilogue and the static tiling: compare against the
+    # same (the register-direct epilogue, the streaming 1x1 kernel and autotuned split-K plans sum
+    # in other orders)
+    _static_kernels(True)
     try:
         for flag in (True, False):
             E.DEFER_BN_FWD = E.DEFER_BN_BWD = flag
@@ -763,7 +781,7 @@ def test_deferred_bn_passes_bit_identical_training(model):
                         [b.detach().clone() for b in m.buffers()]))
     finally:
         E.DEFER_BN_FWD, E.DEFER_BN_BWD = old
-        NativeBackend(DEV).C.set_conv_repi(-1)
+        _static_kernels(False)
     assert torch.equal(res[0][0], res[1][0])
     for a, b in zip(res[0][1] + res[0][2], res[1][1] + res[1][2]):
         assert torch.equal(a, b)
@@ -797,6 +815,7 @@ def test_conv_fwd_bn_in_launch_finalize(shape, monkeypatch):
     mt = nb.conv_mtiles(N, H, W, Cp, Cout, R, R, s, p)
     gamma, beta = torch.rand(Cout, device=DEV) + 0.5, torch.randn(Cout, device=DEV)
     res = []
+    nb.C.set_conv_autotune(0)   # the same (static) tiling on both paths
     for mode in ("fused", "fused", "separate"):
         nb.C.set_fin_in_launch(1 << 30 if mode == "fused" else 0)
         z = _empty(N, P, Q, Cout)
@@ -812,6 +831,7 @@ def test_conv_fwd_bn_in_launch_finalize(shape, monkeypatch):
         torch.cuda.synchronize()
         res.append((z.buf.clone(), stats.clone(), v.clone(), rm.clone(), rv.clone()))
     nb.C.set_fin_in_launch(-1)
+    nb.C.set_conv_autotune(-1)
     for a, b in zip(res[0], res[1]):
         assert torch.equal(a, b)   # deterministic across launches
     assert torch.equal(res[0][0], res[2][0]) and torch.equal(res[0][1], res[2][1])
