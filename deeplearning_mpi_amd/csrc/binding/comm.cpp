@@ -189,7 +189,9 @@ struct RcclComm::Impl {
   ~Impl() {
     stop_watchdog();
     for (auto& e : events) hipEventDestroy(e);
-    if (raw) hipStreamDestroy(raw);
+    // `raw` is NOT destroyed: a process that had used it for RCCL collectives segfaulted at exit
+    // whenever it was (even after ncclCommDestroy; GPU test test_watchdog_quiet_on_healthy_collective)
+    // -- one leaked stream per communicator, which lives for the whole job anyway
   }
 };
 

@@ -188,6 +188,20 @@ struct WgradArgs {
   const float* pshift;
 };
 
+// 3x3 / stride-1 / pad-1 weight gradient by 8 x 8 output-pixel tiles (conv_wgrad3.hip): split z
+// reduces pixel tiles [z * tiles_per_split, ...) of the N x tiles_h x tiles_w grid into
+// ws[z][Ko][9 * C] (tap-major columns, the general path's workspace layout)
+struct Wgrad3Args {
+  const void* dy;
+  int ldy, dyoff, Ko;
+  const void* x;
+  int ldx, xoff, C;
+  int H, W;                        // input = output grid (stride 1, pad 1)
+  int tiles_h, tiles_w, ntiles_pix, tiles_per_split;
+  int mtiles, ntiles, splits;      // Ko / KT, C / CT, pixel splits
+  float* ws;
+};
+
 }  // namespace dlmpi
 
 extern "C" {
@@ -202,6 +216,9 @@ hipError_t dlmpi_conv_wgrad(const dlmpi::WgradArgs* a, int bm, int bn, hipStream
 hipError_t dlmpi_wgrad_reduce(const float* ws, int splits, int Ko, int T, int Cpad, int Creal,
                               int Ko_real, float* out, float* ws2, int ws2_floats, hipStream_t s);
 int dlmpi_wgrad_reduce_groups(int splits, int64_t total);
+// 3x3 spatial-tile weight gradient: tile plan (KT x CT; 0 if the channel counts do not fit) + launch
+int dlmpi_wgrad3_plan(int Ko, int C, int* kt, int* ct);
+hipError_t dlmpi_wgrad3x3(const dlmpi::Wgrad3Args* a, int kt, int ct, hipStream_t s);
 
 // batch norm
 hipError_t dlmpi_bn_finalize(const float* partial, int ntiles, int C, double count, const float* gamma,

@@ -21,6 +21,8 @@ from ..ops.act import Act, Deferred
 # uint8 window slots vs torch flat indices) feed maxpool_bwd; cast_weights / conv_mtiles are layout
 # bookkeeping
 SKIP = frozenset({"maxpool_bwd", "cast_weights", "conv_mtiles", "materialize"})
+# positional index of the BN-partials buffer of ops that take it positionally
+STATS_ARG = {"conv_fwd_bn": 9}
 
 
 def to64(a):
@@ -81,6 +83,8 @@ class ShadowBackend:
             a64, k64 = to64(args), {k: to64(v) for k, v in kw.items()}
             if k64.get("stats") is not None:   # the reference fills row 0 of the partials only
                 k64["stats"].zero_()
+            if name in STATS_ARG and len(a64) > STATS_ARG[name] and isinstance(a64[STATS_ARG[name]], torch.Tensor):
+                a64[STATS_ARG[name]].zero_()
             out = f(*args, **kw)
             sync()
             ref = getattr(self.shadow, name)(*a64, **k64)

@@ -321,7 +321,8 @@ def test_training_step_every_op_matches_fp64(name):
     print({k: f"{v:.1e}" for k, v in sorted(sh.worst.items())})
     assert sh.calls > 40
     assert not sh.records, sh.records[:5]
-    for op in ("conv_fwd", "conv_dgrad", "conv_wgrad", "bn_finalize", "bn_bwd"):
+    # the training forward runs conv + BN statistics + finalize as conv_fwd_bn (ops.cpp)
+    for op in ("conv_fwd_bn", "conv_dgrad", "conv_wgrad", "bn_bwd"):
         assert op in sh.worst
 
 

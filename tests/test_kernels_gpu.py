@@ -288,6 +288,44 @@ def test_conv_wgrad(shape):
     assert _rel(g, gr) < 5e-3
 
 
+WGRAD3_SHAPES = [
+    # N, H, W, Cin (real), Ko, x channel stride / offset, dy channel stride / offset
+    (2, 16, 16, 64, 64, None, 0, None, 0),        # 64 x 64 tiles, 2 x 2 pixel blocks per image
+    (2, 13, 11, 128, 64, None, 0, None, 0),       # 64 x 128 tiles; ragged 8 x 8 blocks at both edges
+    (3, 9, 20, 64, 128, 192, 64, None, 0),        # 128 x 64 tiles; x a channel slice of a concat buffer
+    (2, 7, 7, 256, 256, None, 0, 512, 256),       # dy a channel slice; 7 x 7 = one ragged block
+    (1, 40, 24, 60, 128, None, 0, None, 0),       # Cin padded 60 -> 64: un-padded gradient columns
+    (64, 14, 14, 256, 128, None, 0, None, 0),     # many pixel splits
+]
+
+
+@pytest.mark.parametrize("shape", WGRAD3_SHAPES, ids=lambda s: "x".join(str(v) for v in s[:5]))
+def test_wgrad3x3_spatial_tiles(shape):
+    """3x3 / stride-1 / pad-1 weight gradient by 8 x 8 pixel blocks with a staged halo
+    (conv_wgrad3.hip) against the fp32 reference, and against the general gather kernel (same bf16
+    products, fp32 sums in another order); accumulates into a non-zero gradient slot like the arena."""
+    nb, rb = _be()
+    N, H, W, Cin, K, ldx, xoff, ldy, dyoff = shape
+    Cp = pad8(Cin)
+    x, xr = _act(N, H, W, Cp, ld=ldx, off=xoff)
+    dy, dyr = _act(N, H, W, K, ld=ldy, off=dyoff)
+    g0 = torch.randn(K * 9 * Cin, device=DEV)
+    out = {}
+    for mode in (1, 0):
+        nb.C.set_wgrad3(mode)
+        g = g0.clone()
+        nb.conv_wgrad(dy, x, 3, 3, 1, 1, g, Cin, K)
+        torch.cuda.synchronize()
+        assert nb.C.wgrad3_last() == mode
+        out[mode] = g
+    nb.C.set_wgrad3(-1)
+    gr = g0.clone()
+    rb.conv_wgrad(dyr, xr, 3, 3, 1, 1, gr, Cin, K)
+    torch.cuda.synchronize()
+    assert _rel(out[1], gr) < 5e-3
+    assert _rel(out[1], out[0]) < 1e-4
+
+
 def test_linear_heads():
     nb, rb = _be()
     for (N, Cin, K) in [(8, 2048, 1000), (16, 512, 10)]:
@@ -812,10 +850,10 @@ def test_conv_fwd_bn_in_launch_finalize(shape, monkeypatch):
     x, _ = _act(N, H, W, Cp)
     w = (torch.randn(Cout, R, R, Cp, device=DEV) * 0.1).to(torch.bfloat16)
     P, Q = (H + 2 * p - R) // s + 1, (W + 2 * p - R) // s + 1
+    nb.C.set_conv_autotune(0)   # the same (static) tiling on both paths, and stats rows sized for it
     mt = nb.conv_mtiles(N, H, W, Cp, Cout, R, R, s, p)
     gamma, beta = torch.rand(Cout, device=DEV) + 0.5, torch.randn(Cout, device=DEV)
     res = []
-    nb.C.set_conv_autotune(0)   # the same (static) tiling on both paths
     for mode in ("fused", "fused", "separate"):
         nb.C.set_fin_in_launch(1 << 30 if mode == "fused" else 0)
         z = _empty(N, P, Q, Cout)
@@ -874,7 +912,7 @@ def test_stream1x1_matches_general_kernel(shape, ld_out):
             y = Act(buf, N, H, W, K, K)
         else:
             y = _empty(N, H, W, K)
-        st = torch.empty(mt, 2, K, device=DEV)
+        st = torch.zeros(mt, 2, K, device=DEV)   # an autotuned tile may write fewer rows than mt
         v = torch.empty(4, K, device=DEV)
         rm, rv = torch.zeros(K, device=DEV), torch.ones(K, device=DEV)
         nb.conv_fwd_bn(x, w, K, 1, 1, 1, 0, y, bias, st, N * H * W, gamma, beta, rm, rv, 0.1, 1e-5,
