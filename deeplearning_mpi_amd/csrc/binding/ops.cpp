@@ -829,11 +829,17 @@ void conv2d_wgrad_pro(const at::Tensor& dy, int lddy, int dyoff, int Ko, const a
     b.ntiles_pix = N * b.tiles_h * b.tiles_w;
     b.mtiles = Ko / kt;
     b.ntiles = C / ct;
-    // one 512-thread block per CU (~200 VGPRs: 2 waves per SIMD); splits fill the chip once
-    static const int target = [] {
+    // one 512-thread block per CU (252 VGPRs: 2 waves per SIMD take a SIMD's whole register file,
+    // so nothing of the data-gradient chain on the main stream can share a CU with it).  Large
+    // gradients (UNet, >= 64 G MAC) fill the chip once; the ResNet-size ones (~30 G MAC) leave ~100
+    // CUs to the main stream (measured, profiles/r3_wgrad3: ResNet-50 12,233 img/s at 256 blocks vs
+    // 12,348 at 160; UNet-512 470 vs 466).  DLMPI_WGRAD3_BLOCKS overrides.
+    static const int target_env = [] {
       const char* e = getenv("DLMPI_WGRAD3_BLOCKS");
-      return e ? std::max(8, atoi(e)) : 256;
+      return e ? std::max(8, atoi(e)) : 0;
     }();
+    const double macs = (double)N * H * W * Ko * 9.0 * C;
+    const int target = target_env ? target_env : (macs >= 64e9 ? 256 : 160);
     const int kc = b.mtiles * b.ntiles;
     int splits = std::max(1, std::min(b.ntiles_pix, target / kc));
     b.tiles_per_split = ceil_div(b.ntiles_pix, splits);

@@ -25,6 +25,8 @@
 //
 // Reference semantics: nn.Conv2d(3x3, padding=1) weight gradient of every UNet DoubleConv and the
 // ResNet bottleneck conv2 (/root/reference/pytorch/unet/model.py:9-14, resnet main.py:40-41).
+#include <cstdlib>
+
 #include "common.h"
 
 namespace dlmpi {
@@ -220,9 +222,15 @@ void wgrad3x3_kernel(const Wgrad3Args a) {
 
 using namespace dlmpi;
 
+// DLMPI_WGRAD3_KT=64: 64-row Ko tiles also where 128 fit (156 instead of 252 VGPRs: leaves room on
+// every SIMD for a wave of the concurrently running data-gradient chain)
 extern "C" int dlmpi_wgrad3_plan(int Ko, int C, int* kt, int* ct) {
+  static const int kt_max = [] {
+    const char* e = getenv("DLMPI_WGRAD3_KT");
+    return e ? atoi(e) : 128;
+  }();
   if (Ko % 64 || C % 64) return 0;
-  *kt = Ko % 128 == 0 ? 128 : 64;
+  *kt = (Ko % 128 == 0 && kt_max >= 128) ? 128 : 64;
   *ct = (*kt == 64 && C % 128 == 0) ? 128 : 64;
   return 1;
 }
