@@ -329,8 +329,19 @@ static void fill_epilogue(ConvArgs& a, at::Tensor& y, int ldy, int yoff, const c
   a.nt_store = nt;
 }
 
+// Extras of a pro-3 launch (conv2d_fwd_bn_apply sets them around the shared forward path).
+struct Pro3Extra {
+  const float* rscale;
+  const float* rshift;
+  uint16_t* y;
+  int ldy, yoff;
+  uint8_t* mbits;
+};
+static thread_local const Pro3Extra* g_pro3 = nullptr;
+
 // Operand prologue of the gathered operand (ConvArgs::pro): pro 1 = (k0 scale, k1 shift) of a deferred
-// BN-apply + ReLU; pro 2 = (k0 coef [3][C], pz = Z) of a deferred BN-backward apply.
+// BN-apply + ReLU; pro 2 = (k0 coef [3][C], pz = Z) of a deferred BN-backward apply; pro 3 = (k0 scale,
+// k1 shift, pz = residual) of the producer block's BN-apply + residual + ReLU, stored by the prologue.
 static void set_prologue(ConvArgs& a, int pro, const c10::optional<at::Tensor>& k0, const c10::optional<at::Tensor>& k1,
                          const c10::optional<at::Tensor>& pz, int ldpz, int pzoff) {
   a.pro = pro;
@@ -348,8 +359,24 @@ static void set_prologue(ConvArgs& a, int pro, const c10::optional<at::Tensor>& 
     a.pzoff = pzoff;
     if (!a.pcoef || !a.pz || k0->numel() < 3 * a.C || (ldpz | pzoff) % 8)
       throw std::runtime_error("conv prologue 2: coef [3][C] and an 8-channel aligned Z required");
+  } else if (pro == 3) {
+    a.pscale = optr<float>(k0);
+    a.pshift = optr<float>(k1);
+    a.pz = optr<uint16_t>(pz);
+    a.ldpz = ldpz;
+    a.pzoff = pzoff;
+    const Pro3Extra* e = g_pro3;
+    if (!e || !a.pscale || !a.pshift || !a.pz || !e->y || !e->mbits || k0->numel() < a.C || k1->numel() < a.C ||
+        (ldpz | pzoff | e->ldy | e->yoff) % 8 || ((e->rscale != nullptr) != (e->rshift != nullptr)) || a.f32)
+      throw std::runtime_error("conv prologue 3: scale / shift, an aligned residual, y and mask bits required");
+    a.prscale = e->rscale;
+    a.prshift = e->rshift;
+    a.py = e->y;
+    a.ldpy = e->ldy;
+    a.pyoff = e->yoff;
+    a.pmbits = e->mbits;
   } else {
-    throw std::runtime_error("conv prologue: mode 1 or 2");
+    throw std::runtime_error("conv prologue: mode 1, 2 or 3");
   }
 }
 
@@ -450,6 +477,37 @@ int conv2d_fwd_bn(const at::Tensor& x, int N, int H, int W, int C, int ldx, int 
                          c10::nullopt, c10::nullopt, false, stats, 0, 0, 0, pro, pk0, pk1, pz, ldpz, pzoff, &f);
 }
 
+// conv2d_fwd_bn whose input is the PRODUCER's pending BN-apply: x = that BN's input z (scale, shift),
+// res = its residual (rscale / rshift: a BN-output residual applied on the fly); the conv's operand
+// prologue (pro 3) computes relu(z * scale + shift + res), consumes it AND stores it to yapp with
+// its ReLU mask bits -- the standalone BN-apply pass and the consumer's re-read of its output go.
+int conv2d_fwd_bn_apply(const at::Tensor& x, int N, int H, int W, int C, int ldx, int xoff, const at::Tensor& w, int K,
+                        at::Tensor z, int ldz, int zoff, const c10::optional<at::Tensor>& bias, const at::Tensor& stats,
+                        const at::Tensor& ascale, const at::Tensor& ashift, const at::Tensor& res, int ldres,
+                        int resoff, const c10::optional<at::Tensor>& rscale, const c10::optional<at::Tensor>& rshift,
+                        at::Tensor yapp, int ldyapp, int yappoff, at::Tensor mbits, double count,
+                        const c10::optional<at::Tensor>& gamma, const c10::optional<at::Tensor>& beta,
+                        const c10::optional<at::Tensor>& running_mean, const c10::optional<at::Tensor>& running_var,
+                        double momentum, double eps, at::Tensor bnscale, at::Tensor bnshift,
+                        const c10::optional<at::Tensor>& save_mean, const c10::optional<at::Tensor>& save_invstd) {
+  same_type(x, res, "conv2d_fwd_bn_apply res");
+  same_type(x, yapp, "conv2d_fwd_bn_apply y");
+  if (mbits.scalar_type() != at::kByte || mbits.numel() < (int64_t)N * H * W * (C / 8))
+    throw std::runtime_error("conv2d_fwd_bn_apply: mask bits [pixels][C/8] uint8 required");
+  Pro3Extra e{optr<float>(rscale), optr<float>(rshift), ptr<uint16_t>(yapp), ldyapp, yappoff, ptr<uint8_t>(mbits)};
+  g_pro3 = &e;
+  try {
+    const int r = conv2d_fwd_bn(x, N, H, W, C, ldx, xoff, w, K, 1, 1, 1, 0, z, ldz, zoff, bias, stats, 3, ascale,
+                                ashift, res, ldres, resoff, count, gamma, beta, running_mean, running_var, momentum,
+                                eps, bnscale, bnshift, save_mean, save_invstd);
+    g_pro3 = nullptr;
+    return r;
+  } catch (...) {
+    g_pro3 = nullptr;
+    throw;
+  }
+}
+
 static int conv2d_fwd_impl(const at::Tensor& x, int N, int H, int W, int C, int ldx, int xoff, const at::Tensor& w, int K, int R,
                int S, int stride, int pad, at::Tensor y, int ldy, int yoff, const c10::optional<at::Tensor>& bias,
                const c10::optional<at::Tensor>& res, int ldres, int resoff, const c10::optional<at::Tensor>& scale,
@@ -518,6 +576,8 @@ static int conv2d_fwd_impl(const at::Tensor& x, int N, int H, int W, int C, int 
     }
   }
   a.ntiles = ceil_div(K, bn);
+  if (pro == 3 && (a.ntiles != 1 || R != 1 || S != 1 || stride != 1 || pad != 0))
+    throw std::runtime_error("conv prologue 3: a 1x1 / stride-1 conv with one output tile column");
   a.nphase = 1;
   ConvPhase& p = a.ph[0];
   p.P = P; p.Q = Q; p.Tr = R; p.Ts = S;
@@ -1323,6 +1383,7 @@ void register_ops(pybind11::module& m) {
   m.def("conv_stream_last", []() { return g_stream_ran; });
   m.def("set_conv_autotune", [](int mode) { g_autotune_override = mode; });
   m.def("set_wgrad3", [](int mode) { g_wgrad3_override = mode; });
+  m.def("conv2d_fwd_bn_apply", &conv2d_fwd_bn_apply);
   m.def("wgrad3_last", []() { return g_wgrad3_ran; });
   m.def("clear_conv_plans", []() { g_conv_plans.clear(); });
   m.def("conv_sk_last", []() { return dlmpi_conv_sk_last(); });

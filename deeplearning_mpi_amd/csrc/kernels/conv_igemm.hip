@@ -70,7 +70,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(STAGES 
   constexpr int AL = BM / RP, BL = BN / RP;   // 16-byte pieces per thread per tile
   constexpr int A_BYTES = BM * 128, B_BYTES = BN * 128;
   static_assert(PRO == 0 || (!SMALLC && STAGES == 1), "operand prologue: regular channels, single stage");
-  constexpr int Z_BYTES = PRO == 2 ? A_BYTES : 0;   // the second prologue operand, staged like A
+  constexpr int Z_BYTES = PRO >= 2 ? A_BYTES : 0;   // the second prologue operand, staged like A
   constexpr int SB = A_BYTES + B_BYTES + Z_BYTES;   // bytes per stage: [A | B | Z]
   constexpr int STAGE_BYTES = STAGES * SB;
   constexpr int CS_LD = BN + 4;
@@ -159,7 +159,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(STAGES 
   // ---- staging ------------------------------------------------------------------------------
   // Regular path (C % 64 == 0): the tap t and channel base c are wave-uniform.
   uint32_t a_off[AL];                                 // element offset of the row's input pixel
-  uint32_t z_off[PRO == 2 ? AL : 1];                  // the same pixel in the prologue's Z
+  uint32_t z_off[PRO >= 2 ? AL : 1];                  // the same pixel in the prologue's Z
   uint32_t a_vm = 0;                                  // bit i: (row, tap) inside the image
   int t_cur = 0, c_cur = 0, wtC2 = 0;
   auto tap_setup = [&](int t) {
@@ -176,10 +176,10 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(STAGES 
       const bool ok = ((a_okm >> i) & 1) && (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W;
       if (ok) a_vm |= 1u << i;
       a_off[i] = (uint32_t)(a_pix[i] + doff) * (uint32_t)a.ldx;
-      if constexpr (PRO == 2) z_off[i] = (uint32_t)(a_pix[i] + doff) * (uint32_t)a.ldpz;
+      if constexpr (PRO >= 2) z_off[i] = (uint32_t)(a_pix[i] + doff) * (uint32_t)a.ldpz;
     }
   };
-  const char* zlane = PRO == 2 ? reinterpret_cast<const char*>(a.pz) + ES * ((int64_t)a.pzoff + CPC * jc) : nullptr;
+  const char* zlane = PRO >= 2 ? reinterpret_cast<const char*>(a.pz) + ES * ((int64_t)a.pzoff + CPC * jc) : nullptr;
 
   auto issue = [&](int buf, int ks) {
     char* As = smem + buf * SB;
@@ -190,7 +190,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(STAGES 
         const char* s = ((a_vm >> i) & 1) ? xlane + ES * ((uint64_t)a_off[i] + c_cur) : zp;
         glds16(s, As + (RP * i + 8 * wid) * 128);
       }
-      if constexpr (PRO == 2) {
+      if constexpr (PRO >= 2) {
         char* Zs = Bs + B_BYTES;
 #pragma unroll
         for (int i = 0; i < AL; ++i) {
@@ -238,12 +238,20 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(STAGES 
     if constexpr (PRO != 0) {
       char* As = smem + buf * SB;
       const int c = c_cur + 8 * jc;
-      f32x4 k0a, k0b, k1a, k1b, k2a, k2b;
-      if constexpr (PRO == 1) {
+      f32x4 k0a, k0b, k1a, k1b, k2a, k2b, kra, krb;
+      if constexpr (PRO == 1 || PRO == 3) {
         k0a = *reinterpret_cast<const f32x4*>(a.pscale + c);
         k0b = *reinterpret_cast<const f32x4*>(a.pscale + c + 4);
         k1a = *reinterpret_cast<const f32x4*>(a.pshift + c);
         k1b = *reinterpret_cast<const f32x4*>(a.pshift + c + 4);
+        if constexpr (PRO == 3) {
+          if (a.prscale) {
+            k2a = *reinterpret_cast<const f32x4*>(a.prscale + c);
+            k2b = *reinterpret_cast<const f32x4*>(a.prscale + c + 4);
+            kra = *reinterpret_cast<const f32x4*>(a.prshift + c);
+            krb = *reinterpret_cast<const f32x4*>(a.prshift + c + 4);
+          }
+        }
       } else {
         k0a = *reinterpret_cast<const f32x4*>(a.pcoef + c);
         k0b = *reinterpret_cast<const f32x4*>(a.pcoef + c + 4);
@@ -264,6 +272,37 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(STAGES 
             v[e] = fmaxf(__builtin_fmaf(v[e], k0a[e], k1a[e]), 0.f);
             v[e + 4] = fmaxf(__builtin_fmaf(v[e + 4], k0b[e], k1b[e]), 0.f);
           }
+        } else if constexpr (PRO == 3) {
+          // the producer block's BN-apply + residual + ReLU (bn_apply_kernel's arithmetic, same
+          // order), written back as the A operand AND stored: y and its ReLU mask bits
+          float r[8];
+          unpack8(*reinterpret_cast<const u32x4*>(As + A_BYTES + B_BYTES + RP * i * 128 + tid * 16), r);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            v[e] = __builtin_fmaf(v[e], k0a[e], k1a[e]);
+            v[e + 4] = __builtin_fmaf(v[e + 4], k0b[e], k1b[e]);
+          }
+          if (a.prscale) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              r[e] = __builtin_fmaf(r[e], k2a[e], kra[e]);
+              r[e + 4] = __builtin_fmaf(r[e + 4], k2b[e], krb[e]);
+            }
+          }
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e] + r[e], 0.f);
+          const u32x4 pk = pack8(v);
+          *pa = pk;
+          const int64_t px = a_pix[i];   // 1x1 / stride 1 (host-checked): input pixel = tile row
+          *reinterpret_cast<u32x4*>(a.py + px * a.ldpy + a.pyoff + c) = pk;
+          uint32_t b = 0;
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            b |= (uint32_t)((pk[k] & 0xffffu) != 0u && !(pk[k] & 0x8000u)) << (2 * k);
+            b |= (uint32_t)((pk[k] >> 16) != 0u && !(pk[k] & 0x80000000u)) << (2 * k + 1);
+          }
+          a.pmbits[px * (C >> 3) + (c >> 3)] = (uint8_t)b;
+          continue;
         } else {
           float zv[8];
           unpack8(*reinterpret_cast<const u32x4*>(As + A_BYTES + B_BYTES + RP * i * 128 + tid * 16), zv);
@@ -807,6 +846,10 @@ static void launch_tile(const ConvArgs* a, dim3 grid, hipStream_t s) {
     hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, false, 1, 4, 2, 2>), grid, dim3(256), 0, s, *a);
     return;
   }
+  if (a->pro == 3) {
+    hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, false, 1, 4, 2, 3>), grid, dim3(256), 0, s, *a);
+    return;
+  }
   if (a->C < 64) {
     if (one) hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, true, 1, 4, 2>), grid, dim3(256), 0, s, *a);
     else hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, true, 2, 4, 2>), grid, dim3(256), 0, s, *a);
@@ -990,6 +1033,7 @@ extern "C" hipError_t dlmpi_conv_igemm(const ConvArgs* a_in, int bm, int bn, hip
       else hipLaunchKernelGGL((conv_igemm_kernel<256, 64, false, 1, 4, 4, 0, uint16_t, false, true>), grid, dim3(256), 0, s, *a);
     } else if (a->pro == 1) hipLaunchKernelGGL((conv_igemm_kernel<256, 64, false, 1, 4, 4, 1>), grid, dim3(256), 0, s, *a);
     else if (a->pro == 2) hipLaunchKernelGGL((conv_igemm_kernel<256, 64, false, 1, 4, 4, 2>), grid, dim3(256), 0, s, *a);
+    else if (a->pro == 3) hipLaunchKernelGGL((conv_igemm_kernel<256, 64, false, 1, 4, 4, 3>), grid, dim3(256), 0, s, *a);
     else if (a->C < 64) hipLaunchKernelGGL((conv_igemm_kernel<256, 64, true, 1, 4, 4>), grid, dim3(256), 0, s, *a);
     else hipLaunchKernelGGL((conv_igemm_kernel<256, 64, false, 1, 4, 4>), grid, dim3(256), 0, s, *a);
   } else if (bm == 128 && bn == 256) {   // short reductions, wide outputs: 8 waves (2 x 4 of 64 x 64)

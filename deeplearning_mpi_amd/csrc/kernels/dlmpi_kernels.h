@@ -142,6 +142,15 @@ struct ConvArgs {
   const float* pcoef;
   const void* pz;
   int ldpz, pzoff;
+  //   pro 3 (1x1 / stride 1 consumers with ONE output tile column): A := bf16(relu(A * pscale[c] +
+  //          pshift[c] + R)), R = Z (the residual, staged like pro 2's Z) or Z * prscale[c] +
+  //          prshift[c] (a BN-output residual); the transformed tile is also stored to py and its
+  //          ReLU mask bits to pmbits [pixels][C/8] (the producer block's BN-apply, fused)
+  const float* prscale;
+  const float* prshift;
+  uint16_t* py;
+  int ldpy, pyoff;
+  uint8_t* pmbits;
   // In-launch BatchNorm finalize of the statistics this launch produces (bnfin.h): every block
   // publishes its stats row write-through; the last arriver of each group of fin_group stats tiles
   // sums the group, the last group of each N-tile sums the group sums and finalizes that N-tile's

@@ -132,6 +132,14 @@ DUAL_WGRAD_PRO = os.environ.get("DLMPI_DUAL_WGRAD_PRO", "1") != "0"
 # wait for the later side-stream half before the BN finalize (1.8 ms of main-stream gaps per step)
 CHUNK_FWD = os.environ.get("DLMPI_CHUNK_FWD", "0") != "0"
 
+# DLMPI_FUSE_APPLY=0: run every residual block's BN-apply (+ residual + ReLU) as its own pass.  By
+# default a block output whose first consumer is a 1x1 / stride-1 convolution with ONE output tile
+# column (the next bottleneck's conv1 for <= 128 output channels: ResNet-50 layer1 / layer2) is left
+# pending (PendingApply) and computed by that convolution's operand prologue, which also stores it
+# and its ReLU mask bits (backend conv_fwd_bn_apply): no element is transformed twice, and the
+# apply's output is written once and never re-read by the consumer.
+FUSE_APPLY = os.environ.get("DLMPI_FUSE_APPLY", "1") != "0"
+
 
 def img_rows(a, n0: int, n1: int):
     """Images [n0, n1) of an Act (a row range of its 2-D buffer, same ld / channel offset) or of a
@@ -326,7 +334,11 @@ class ConvUnit:
         output is never materialised.  lazy (training BN, not deferred): return a PendingApply instead
         of running the BN-apply -- for a consumer that runs it chunk-wise beside its own GEMM."""
         chunked = train and self._chunkable(be, x)
-        if isinstance(x, PendingApply) and not chunked:
+        fuse_apply = (FUSE_APPLY and train and save and not chunked and isinstance(x, PendingApply) and not x.done
+                      and self.bn is not None and self.R == 1 and self.S == 1 and self.stride == 1 and self.pad == 0
+                      and self.Kp <= 128 and x.relu and x.res is not None and x.mbits is not None
+                      and x.C == self.Cp and hasattr(be, "conv_fwd_bn_apply") and not getattr(be, "f32", False))
+        if isinstance(x, PendingApply) and not chunked and not fuse_apply:
             x = x.resolve(be)
         assert x.C == self.Cp, (x, self.Cp)
         P, Q = self.out_hw(x.H, x.W)
@@ -366,6 +378,13 @@ class ConvUnit:
                 x = x.y
                 self.arena.wait_buffers()   # DDP's asynchronous buffer broadcast must land first
                 be.bn_finalize(stats, mt, self.Kp, *fin)
+            elif fuse_apply:   # the producer's BN-apply runs (and is stored) inside this GEMM
+                mt = be.conv_mtiles(N, x.H, x.W, x.C, self.Kp, 1, 1, 1, 0, pro=True)
+                stats = torch.empty(mt, 2, self.Kp, dtype=be.dt, device=dev)
+                self.arena.wait_buffers()
+                be.conv_fwd_bn_apply(x, wf, self.Kp, z, self._bias_vec(), stats, *fin)
+                x.done = True
+                x = x.y
             else:
                 mt = be.conv_mtiles(N, x.H, x.W, x.C, self.Kp, self.R, self.S, self.stride, self.pad,
                                     pro=isinstance(x, Deferred))
@@ -390,7 +409,7 @@ class ConvUnit:
             if before_res is not None and res is not None:
                 before_res()
             ctx = (x, z, y, mean, invstd, scale, shift, res is not None, mbits) if save else None
-            if lazy and CHUNK_FWD and out is None:
+            if lazy and (CHUNK_FWD or FUSE_APPLY) and out is None:
                 return PendingApply(y, z, scale, shift, res, self.relu, mbits), ctx
             be.bn_apply(z, scale, shift, res, self.relu, y, mbits=mbits)
             return y, ctx

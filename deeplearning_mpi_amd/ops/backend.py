@@ -168,6 +168,22 @@ class NativeBackend:
                              bias, stats, pm, k0, k1, zb, zld, zoff, float(count), gamma, beta, rm, rv,
                              float(momentum), float(eps), scale, shift, save_mean, save_invstd)
 
+    def conv_fwd_bn_apply(self, xp, w, K, z: Act, bias, stats, count, gamma, beta, rm, rv, momentum, eps, scale,
+                          shift, save_mean, save_invstd):
+        """conv_fwd_bn (1x1, stride 1) whose input is a pending BN-apply (engine.PendingApply: y =
+        relu(z * scale + shift + res), res an Act or a Deferred.bn): the conv's operand prologue computes y,
+        uses it and stores it with its ReLU mask bits (pro 3) -- no separate apply pass."""
+        x, res = xp.z, xp.res
+        rs = rh = None
+        if isinstance(res, Deferred):
+            assert res.kind == "bn", res
+            res, rs, rh = res.src, res.k0, res.k1
+        y = xp.y
+        self.C.conv2d_fwd_bn_apply(x.buf, x.N, x.H, x.W, x.C, x.ld, x.off, w, K, z.buf, z.ld, z.off, bias, stats,
+                                   xp.scale, xp.shift, res.buf, res.ld, res.off, rs, rh, y.buf, y.ld, y.off, xp.mbits,
+                                   float(count), gamma, beta, rm, rv, float(momentum), float(eps), scale, shift,
+                                   save_mean, save_invstd)
+
     def conv_fwd_bnbwd(self, x: Act, w, K, R, S, stride, pad, y: Act, fuse):
         """Forward conv producing the gradient of relu(BN(z)) (fuse = BwdFuse(None, z, None, scale,
         shift)): masked in the epilogue, BN-backward partials [tiles][2][K] returned."""
@@ -511,6 +527,11 @@ class RefBackend:
         if z2 is not None:
             rows.append((v * z2.nhwc().to(self.dt)).sum((0, 1, 2)))
         return torch.stack(rows).unsqueeze(0)
+
+    def conv_fwd_bn_apply(self, xp, w, K, z: Act, bias, stats, *fin):
+        """Reference form of the fused consumer: the pending BN-apply as its own pass, then conv_fwd_bn."""
+        self.bn_apply(xp.z, xp.scale, xp.shift, xp.res, xp.relu, xp.y, mbits=xp.mbits)
+        self.conv_fwd_bn(xp.y, w, K, 1, 1, 1, 0, z, bias, stats, *fin)
 
     def conv_fwd_bnbwd(self, x: Act, w, K, R, S, stride, pad, y: Act, fuse):
         wk = w.view(K, R, S, x.C).permute(0, 3, 1, 2).to(self.dt)

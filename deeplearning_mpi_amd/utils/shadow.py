@@ -21,6 +21,9 @@ from ..ops.act import Act, Deferred
 # uint8 window slots vs torch flat indices) feed maxpool_bwd; cast_weights / conv_mtiles are layout
 # bookkeeping
 SKIP = frozenset({"maxpool_bwd", "cast_weights", "conv_mtiles", "materialize"})
+# fused ops whose inputs are engine objects the shadow cannot copy (engine.PendingApply): hidden, so
+# the engine takes the unfused path (the same values, op by op)
+HIDDEN = frozenset({"conv_fwd_bn_apply"})
 # positional index of the BN-partials buffer of ops that take it positionally
 STATS_ARG = {"conv_fwd_bn": 9}
 
@@ -73,6 +76,8 @@ class ShadowBackend:
         setattr(self.primary, k, v)
 
     def __getattr__(self, name):
+        if name in HIDDEN:
+            raise AttributeError(name)
         f = getattr(self.primary, name)
         if not callable(f) or name in SKIP or name.startswith("_") or not hasattr(self.shadow, name):
             return f

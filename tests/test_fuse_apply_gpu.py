@@ -1,0 +1,113 @@
+"""Producer BN-apply fused into the consumer GEMM (conv prologue mode 3, models/engine.py FUSE_APPLY):
+the next bottleneck's 1x1 conv1 computes relu(z * scale + shift + residual) in its operand prologue,
+consumes it and stores it (plus ReLU mask bits) instead of a separate BN-apply pass.
+
+* kernel level: y and its mask bits bit-identical to bn_apply's, the conv output bit-identical to the
+  conv over the stored y, BN statistics / finalize equal to fp32 summation-order noise -- with a
+  plain and with a BatchNorm-output (downsample) residual;
+* model level: a ResNet-50 training step with the fusion on vs off."""
+import copy
+
+import pytest
+import torch
+
+from deeplearning_mpi_amd.models import resnet50
+from deeplearning_mpi_amd.models.engine import PendingApply
+from deeplearning_mpi_amd.ops import cross_entropy
+from deeplearning_mpi_amd.ops.act import Act, Deferred
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _rel(a, b):
+    a, b = a.double(), b.double()
+    return ((a - b).abs().max() / b.abs().max().clamp_min(1e-30)).item()
+
+
+SHAPES = [
+    # N, H, W, C (apply channels = conv input), K (conv output), BN-output residual
+    (4, 14, 14, 256, 64, False),
+    (2, 28, 28, 512, 128, True),
+    (3, 7, 9, 256, 128, False),     # ragged last tile
+    (8, 56, 56, 256, 64, True),     # ResNet-50 layer-1 width
+]
+
+
+@pytest.mark.parametrize("shape", SHAPES, ids=lambda s: "x".join(str(v) for v in s))
+def test_conv_fwd_bn_apply_matches_unfused(shape):
+    from deeplearning_mpi_amd.ops.backend import NativeBackend
+
+    N, H, W, C, K, bnres = shape
+    be = NativeBackend(torch.device(DEV))
+    g = torch.Generator(device=DEV).manual_seed(C + K + H)
+    M = N * H * W
+    z3 = Act(torch.randn(M, C, device=DEV, generator=g).to(torch.bfloat16), N, H, W, C)
+    rbuf = Act(torch.randn(M, C, device=DEV, generator=g).to(torch.bfloat16), N, H, W, C)
+    sc3, sh3 = torch.rand(C, device=DEV, generator=g) + 0.5, torch.randn(C, device=DEV, generator=g) * 0.2
+    res = Deferred.bn(rbuf, torch.rand(C, device=DEV, generator=g) + 0.5,
+                      torch.randn(C, device=DEV, generator=g) * 0.2) if bnres else rbuf
+    w = (torch.randn(K, 1, 1, C, device=DEV, generator=g) / C ** 0.5).to(torch.bfloat16)
+    gamma, beta = torch.rand(K, device=DEV, generator=g) + 0.5, torch.randn(K, device=DEV, generator=g)
+    out = {}
+    for fused in (True, False):
+        y = Act.empty(N, H, W, C, torch.bfloat16, DEV)
+        y.buf.fill_(7.0)
+        mb = torch.zeros(M, C // 8, dtype=torch.uint8, device=DEV)
+        z = Act.empty(N, H, W, K, torch.bfloat16, DEV)
+        mt = be.conv_mtiles(N, H, W, C, K, 1, 1, 1, 0, pro=True)
+        st = torch.zeros(max(mt, be.conv_mtiles(N, H, W, C, K, 1, 1, 1, 0)), 2, K, device=DEV)
+        rm, rv = torch.zeros(K, device=DEV), torch.ones(K, device=DEV)
+        v = torch.empty(4, K, device=DEV)
+        fin = (M, gamma, beta, rm, rv, 0.1, 1e-5, v[0], v[1], v[2], v[3])
+        if fused:
+            be.conv_fwd_bn_apply(PendingApply(y, z3, sc3, sh3, res, True, mb), w, K, z, None, st, *fin)
+        else:
+            be.bn_apply(z3, sc3, sh3, res, True, y, mbits=mb)
+            be.conv_fwd_bn(y, w, K, 1, 1, 1, 0, z, None, st, *fin)
+        torch.cuda.synchronize()
+        out[fused] = (y.buf.clone(), mb.clone(), z.buf.clone(), st.double().sum(0), v.clone(), rm.clone(), rv.clone())
+    a, b = out[True], out[False]
+    assert torch.equal(a[0], b[0])          # the stored apply output
+    assert torch.equal(a[1], b[1])          # its ReLU mask bits
+    assert torch.equal(a[2], b[2])          # the conv output (same bf16 operands, same dot products)
+    assert _rel(a[3], b[3]) < 1e-5          # statistics: another tiling's summation order
+    for x, r in zip(a[4:], b[4:]):
+        assert _rel(x, r) < 1e-5
+
+
+def test_resnet50_step_fused_apply_vs_unfused(monkeypatch):
+    from deeplearning_mpi_amd.models import engine
+
+    torch.manual_seed(0)
+    m1 = resnet50(num_classes=10).to(DEV)
+    m2 = copy.deepcopy(m1)
+    g = torch.Generator(device=DEV).manual_seed(11)
+    x = torch.randn(16, 3, 96, 96, device=DEV, generator=g)
+    y = torch.randint(10, (16,), device=DEV, generator=g)
+    losses, calls = [], {}
+    for m, on in ((m1, True), (m2, False)):
+        monkeypatch.setattr(engine, "FUSE_APPLY", on)
+        be = m._be if getattr(m, "_be", None) is not None else None
+        n = [0]
+        if on:
+            from deeplearning_mpi_amd.ops.backend import NativeBackend
+
+            orig = NativeBackend.conv_fwd_bn_apply
+
+            def counting(self, *a, **k):
+                n[0] += 1
+                return orig(self, *a, **k)
+
+            monkeypatch.setattr(NativeBackend, "conv_fwd_bn_apply", counting)
+        m.arena.zero_grad()
+        loss = cross_entropy(m(x), y)
+        loss.backward()
+        losses.append(loss.detach())
+        calls[on] = n[0]
+        del be
+    torch.cuda.synchronize()
+    assert calls[True] == 5   # layer1.1, layer1.2, layer2.1..3 (conv1 of <= 128 channels, identity blocks)
+    assert _rel(losses[0], losses[1]) < 2e-3
+    g1, g2 = m1.arena.grad, m2.arena.grad
+    assert ((g1 - g2).norm() / g2.norm()).item() < 3e-2
