@@ -246,9 +246,11 @@ def main():
                               "n_gpus": world, "config": args.config}), file=sys.stderr, flush=True)
     host_info = None
     if args.host_time > 0 and dev.type == "cuda":
-        # host issue time of one step: the CPU time from calling step() to its return while the GPU
-        # runs behind (no sync inside a step), vs the GPU time per step measured above -- if the
-        # host needs less than the GPU, an eager step stays GPU-bound
+        # host issue time of one step: the CPU time from calling step() to its return, each step
+        # issued onto an idle GPU with empty queues (synchronised before and after, so a full launch
+        # queue cannot block the host and inflate the number), vs the GPU time per step measured
+        # above -- if the host needs less than the GPU, an eager pipelined step stays GPU-bound
+        # 
         sync()
         issue = []
         t0 = time.perf_counter()
@@ -256,13 +258,13 @@ def main():
             a = time.perf_counter()
             step()
             issue.append(time.perf_counter() - a)
-        sync()
+            sync()
         wall = time.perf_counter() - t0
         issue.sort()
         host_info = {"host_issue_ms_per_step_median": round(issue[len(issue) // 2] * 1e3, 3),
                      "host_issue_ms_per_step_max": round(issue[-1] * 1e3, 3),
                      "gpu_ms_per_step": round(dt / args.steps * 1e3, 3),
-                     "wall_ms_per_step_during_probe": round(wall / args.host_time * 1e3, 3),
+                     "wall_ms_per_step_during_probe_unpipelined": round(wall / args.host_time * 1e3, 3),
                      "host_over_gpu": round(issue[len(issue) // 2] / (dt / args.steps), 3)}
         if comm.rank == 0:
             print(json.dumps({"host_time": host_info, "config": args.config, "graph": bool(args.graph),

@@ -156,6 +156,64 @@ static void pick_tiles(int64_t M, int Kout, int64_t red, int cin, int& bm, int& 
   else if (tiles < 512) bm = 64;
 }
 
+// ---- 2-D halo tiles for 3x3 / stride-1 / pad-1 convolutions (conv_igemm.hip HALO) ----------------
+// DLMPI_CONV_HALO=0: these convolutions through the im2col gather path too.
+static int g_halo_override = -1;   // dlmpi_ext set_conv_halo (tests)
+static bool halo_on() {
+  static const int v = [] {
+    const char* e = getenv("DLMPI_CONV_HALO");
+    return e ? atoi(e) : 1;
+  }();
+  return (g_halo_override >= 0 ? g_halo_override : v) != 0;
+}
+// Tile th x tw (th * tw <= 128, (th + 2) * (tw + 2) <= 192) covering a P x Q grid with the fewest
+// 128-row tiles (ties: the wider tile).
+static void halo_geom(int P, int Q, int& th, int& tw, int& tiles_h, int& tiles_w) {
+  int best = INT32_MAX;
+  for (int w = 16; w >= 4; --w) {
+    const int h = std::min(128 / w, 192 / (w + 2) - 2);
+    if (h < 1) continue;
+    const int t = ceil_div(P, h) * ceil_div(Q, w);
+    if (t < best) {
+      best = t;
+      th = h;
+      tw = w;
+    }
+  }
+  tiles_h = ceil_div(P, th);
+  tiles_w = ceil_div(Q, tw);
+}
+// Measured per shape (profiles/r3_halo): halo tiles win 1-6 % on grids >= 28 x 28 against the
+// 128-row gather tiles, tie with the 8-wave 256 x 256 tiles, and lose on 14^2 / 7^2 grids (a
+// 7 x 7 image fills a 126-pixel tile to 39 %) -- so only there, and not instead of 256 x 256 tiles.
+static bool halo_eligible(int f32, int pro, int C, int R, int S, int stride, int pad, int P, int Q, int bm, int bn) {
+  if (!halo_on() || f32 || pro != 0 || C % 64 != 0 || R != 3 || S != 3 || stride != 1 || pad != 1) return false;
+  return g_halo_override == 2 || (P >= 28 && Q >= 28 && !(bm == 256 && bn == 256));   // 2: any grid (tests)
+}
+static int g_halo_ran = 0;   // 1 if the last conv2d_fwd / conv2d_dgrad ran halo tiles (tests)
+// Switch a fully set-up single-phase launch (bm 128) to halo tiles: its M-tiles (and stats rows)
+// become N x tiles_h x tiles_w.
+static void apply_halo(ConvArgs& a, int N) {
+  ConvPhase& p = a.ph[0];
+  int th = 8, tw = 16, tiles_h = 1, tiles_w = 1;
+  halo_geom(p.P, p.Q, th, tw, tiles_h, tiles_w);
+  a.halo = 1;
+  a.th = th;
+  a.tw = tw;
+  a.tiles_h = tiles_h;
+  a.tiles_w = tiles_w;
+  a.fd_tw = make_fastdiv((uint32_t)tw);
+  a.fd_tilesw = make_fastdiv((uint32_t)tiles_w);
+  a.fd_thw = make_fastdiv((uint32_t)(tiles_h * tiles_w));
+  p.mtiles = N * tiles_h * tiles_w;
+  p.tile_base = 0;
+}
+static int halo_mtiles(int N, int P, int Q) {
+  int th = 8, tw = 16, tiles_h = 1, tiles_w = 1;
+  halo_geom(P, Q, th, tw, tiles_h, tiles_w);
+  return N * tiles_h * tiles_w;
+}
+
 // ---- conv tile autotuner ("benchmark mode", the reference's cudnn.benchmark = True,
 // /root/reference/pytorch/resnet/main.py:29) --------------------------------------------------------
 // At batch 256 most ResNet-50 layers quantize badly on 256 CUs (784 tiles of a 14^2 layer on 768
@@ -212,7 +270,7 @@ static int apply_tiles(ConvArgs& a, int bm, int bn) {
 // Plan for a fully set-up (default-tiled) launch: the cached one, or tune now.  Returns false if
 // autotuning does not apply (the caller keeps its static plan).
 static bool conv_plan(ConvArgs& a, int pass, int& bm, int& bn) {
-  if (!conv_autotune_on() || a.f32 || a.pro != 0 || a.fin_on) return false;
+  if (!conv_autotune_on() || a.f32 || a.pro != 0 || a.fin_on || a.halo) return false;
   // trials re-run the launch: an output that is also one of its inputs (in-place residual / mask /
   // z) would be transformed once per trial -- keep the static plan there
   const void* y = a.y;
@@ -537,6 +595,11 @@ static int conv2d_fwd_impl(const at::Tensor& x, int N, int H, int W, int C, int 
   int bm, bn;
   pick_tiles((int64_t)N * P * Q, K, (int64_t)R * S * C, C, bm, bn, pro != 0);
   if (a.f32) f32_tiles(bm, bn);
+  const bool halo = bm_req <= 0 && bn_req <= 0 && halo_eligible(a.f32, pro, C, R, S, stride, pad, P, Q, bm, bn);
+  if (halo) {
+    bm = 128;
+    bn = std::min(bn, 128);
+  }
   if (bm_req > 0) bm = bm_req;   // tests / experiments: force a tile shape
   if (bn_req > 0) bn = bn_req;
   g_stream_ran = 0;
@@ -585,6 +648,8 @@ static int conv2d_fwd_impl(const at::Tensor& x, int N, int H, int W, int C, int 
   p.wr0 = 0; p.wrs = 1; p.ws0 = 0; p.wss = 1;
   p.oh0 = 0; p.ow0 = 0;
   finish_phase(p, N, C, bm, a.f32);
+  if (halo) apply_halo(a, N);
+  g_halo_ran = halo ? 1 : 0;
   // autotuned tiling: BN-stats launches only through conv2d_fwd_bn (its buffer is sized for the
   // largest row count, conv2d_fwd_mtiles_pro, and its finalize uses the actual one)
   if ((fin != nullptr || !a.stats) && bm_req <= 0 && bn_req <= 0) conv_plan(a, 0, bm, bn);
@@ -670,6 +735,12 @@ int conv2d_fwd_mtiles_pro(int N, int H, int W, int C, int K, int R, int S, int s
   int bm, bn;
   int G;
   if (bm_req <= 0 && stream1x1_shape((int64_t)N * P * Q, C, K, R, S, stride, pad, pro, f32, bm, bn, G)) return G;
+  if (bm_req <= 0) {
+    int hbm, hbn;
+    pick_tiles((int64_t)N * P * Q, K, (int64_t)R * S * C, C, hbm, hbn, pro != 0);
+    if (f32) f32_tiles(hbm, hbn);
+    if (halo_eligible(f32, pro, C, R, S, stride, pad, P, Q, hbm, hbn)) return halo_mtiles(N, P, Q);
+  }
   // autotuned launches may pick any M tile: size for the smallest (64 rows)
   if (bm_req <= 0 && conv_autotune_on() && !f32 && pro == 0) return ceil_div((int64_t)N * P * Q, 64);
   pick_tiles((int64_t)N * P * Q, K, (int64_t)R * S * C, C, bm, bn, pro != 0);
@@ -743,6 +814,11 @@ c10::optional<at::Tensor> conv2d_dgrad_pro(const at::Tensor& dy, int N, int P, i
   int bm, bn;
   pick_tiles((int64_t)N * H * W / (stride * stride), C, (int64_t)R * S * K / (stride * stride), K, bm, bn, pro != 0);
   if (a.f32) f32_tiles(bm, bn);
+  const bool halo = halo_eligible(a.f32, pro, K, R, S, stride, pad, H, W, bm, bn) && P == H && Q == W;
+  if (halo) {
+    bm = 128;
+    bn = std::min(bn, 128);
+  }
   a.ntiles = ceil_div(C, bn);
   a.nphase = stride * stride;
   int tiles = 0;
@@ -763,6 +839,11 @@ c10::optional<at::Tensor> conv2d_dgrad_pro(const at::Tensor& dy, int N, int P, i
       tiles += p.mtiles;
     }
   }
+  if (halo) {
+    apply_halo(a, N);
+    tiles = a.ph[0].mtiles;
+  }
+  g_halo_ran = halo ? 1 : 0;
   {  // autotuned tiling (statistics: a placeholder until the tile count is known -- the trials
      // write to scratch)
     const bool want_stats = a.z || colsum;
@@ -1383,6 +1464,8 @@ void register_ops(pybind11::module& m) {
   m.def("conv_stream_last", []() { return g_stream_ran; });
   m.def("set_conv_autotune", [](int mode) { g_autotune_override = mode; });
   m.def("set_wgrad3", [](int mode) { g_wgrad3_override = mode; });
+  m.def("set_conv_halo", [](int mode) { g_halo_override = mode; });
+  m.def("conv_halo_last", []() { return g_halo_ran; });
   m.def("conv2d_fwd_bn_apply", &conv2d_fwd_bn_apply);
   m.def("wgrad3_last", []() { return g_wgrad3_ran; });
   m.def("clear_conv_plans", []() { g_conv_plans.clear(); });

@@ -54,8 +54,13 @@ __device__ __forceinline__ void glds16(const void* g, char* lds_wave_base) {
 // SKM: stream-K work decomposition (ConvArgs::sk_*): a persistent grid walks the flattened
 // (phase, tile, K-step) iterations; tiles split between blocks are summed by their last-arriving
 // contributor in a fixed block order (deterministic), exactly like the split-K combine.
+// HALO: 3x3 / stride-1 / pad-1 convolutions (forward and stride-1 data gradient) by 2-D output tiles
+// of th x tw pixels (th * tw <= 128 = BM) of one image: the (th + 2) x (tw + 2) input halo of a
+// 64-channel chunk is staged ONCE and the 9 taps are 9 K-steps over it (only the weight tile is
+// staged per tap) -- the K order is chunk-major, tap-minor.  An out-of-image halo pixel is staged as
+// zeros, which is the zero padding of every tap; no per-tap im2col decode exists.
 template <int BM, int BN, bool SMALLC, int STAGES, int NW, int WGM, int PRO = 0, typename ET = uint16_t,
-          bool SKM = false, bool REPI = false>
+          bool SKM = false, bool REPI = false, bool HALO = false>
 __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(STAGES == 1 && BM * BN <= 16384 ? (BM * BN == 16384 ? DLMPI_W128 : 3) : 2, 8))) void conv_igemm_kernel(const ConvArgs a) {
   constexpr int NT = 64 * NW;                 // threads
   constexpr int WGN = NW / WGM;               // wave grid WGM x WGN
@@ -68,7 +73,11 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(STAGES 
   constexpr int TM = WM / 16, TN = WN / 16;
   constexpr int RP = NT / 8;                  // tile rows staged per pass (8 lanes per 128-B row)
   constexpr int AL = BM / RP, BL = BN / RP;   // 16-byte pieces per thread per tile
-  constexpr int A_BYTES = BM * 128, B_BYTES = BN * 128;
+  constexpr int HALO_ROWS = 192;              // (th + 2) * (tw + 2) <= 192 (host-checked)
+  static_assert(!HALO || (BM == 128 && NW == 4 && !SMALLC && STAGES == 1 && PRO == 0 && !SKM && !REPI &&
+                          sizeof(ET) == 2), "halo mode: 128-pixel bf16 single-stage tiles");
+  constexpr int HL = HALO ? HALO_ROWS * 128 / (16 * 64 * NW) : 1;   // halo pieces per thread
+  constexpr int A_BYTES = (HALO ? HALO_ROWS : BM) * 128, B_BYTES = BN * 128;
   static_assert(PRO == 0 || (!SMALLC && STAGES == 1), "operand prologue: regular channels, single stage");
   constexpr int Z_BYTES = PRO >= 2 ? A_BYTES : 0;   // the second prologue operand, staged like A
   constexpr int SB = A_BYTES + B_BYTES + Z_BYTES;   // bytes per stage: [A | B | Z]
@@ -123,6 +132,14 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(STAGES 
   const ConvPhase ph = a.ph[zph];
   const int mt = bid / a.ntiles, nt = bid - mt * a.ntiles;
   const int m0 = mt * BM, n0 = nt * BN;
+  int hn = 0, hh0 = 0, hw0 = 0;                       // HALO: image and tile origin of this M-tile
+  if constexpr (HALO) {
+    hn = (int)fdiv((uint32_t)mt, a.fd_thw);
+    const int rem = mt - hn * a.tiles_h * a.tiles_w;
+    const int ti = (int)fdiv((uint32_t)rem, a.fd_tilesw);
+    hh0 = ti * a.th;
+    hw0 = (rem - ti * a.tiles_w) * a.tw;
+  }
   const int PQ = ph.P * ph.Q;
   const int M = a.Nimg * PQ;
 
@@ -181,10 +198,54 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(STAGES 
   };
   const char* zlane = PRO >= 2 ? reinterpret_cast<const char*>(a.pz) + ES * ((int64_t)a.pzoff + CPC * jc) : nullptr;
 
+  // HALO staging: piece i of this lane = halo row lrow + RP i (chunk jc), i.e. halo pixel (line,
+  // col) relative to the tile origin; rows past the halo read the zero page
+  const int hwd = HALO ? a.tw + 2 : 1;                 // halo row length (pixels)
+  int hl_dh[HL], hl_dw[HL];
+  uint32_t hl_ok = 0;
+  if constexpr (HALO) {
+    const int nrows = (a.th + 2) * hwd;
+#pragma unroll
+    for (int i = 0; i < HL; ++i) {
+      const int hr = lrow + RP * i;
+      const int line = hr / hwd;
+      hl_dh[i] = line - 1;
+      hl_dw[i] = hr - line * hwd - 1;
+      if (hr < nrows) hl_ok |= 1u << i;
+    }
+  }
+  int toff = 0;                                        // HALO: halo-row offset of the current tap
+  bool need_halo = true;
+  auto tap_setup_halo = [&](int t) {
+    const int tr = (int)fdiv((uint32_t)t, ph.fdTs);
+    const int ts = t - tr * ph.Ts;
+    const int dh = ph.dh0 + tr * ph.dhs, dw = ph.dw0 + ts * ph.dws;
+    const int wt = (ph.wr0 + tr * ph.wrs) * a.S + (ph.ws0 + ts * ph.wss);
+    wtC2 = wt * C * ES;
+    toff = (dh + 1) * hwd + (dw + 1);
+  };
+
   auto issue = [&](int buf, int ks) {
     char* As = smem + buf * SB;
     char* Bs = As + A_BYTES;
-    if constexpr (!SMALLC) {
+    if constexpr (HALO) {
+      if (need_halo) {
+        const char* xb = reinterpret_cast<const char*>(a.x) + ES * ((int64_t)a.xoff + c_cur + CPC * jc);
+#pragma unroll
+        for (int i = 0; i < HL; ++i) {
+          const int ih = hh0 + hl_dh[i], iw = hw0 + hl_dw[i];
+          const bool ok = ((hl_ok >> i) & 1) && (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W;
+          const char* src = ok ? xb + (int64_t)ES * (((int64_t)hn * a.H + ih) * a.W + iw) * a.ldx : zp;
+          glds16(src, As + (RP * i + 8 * wid) * 128);
+        }
+        need_halo = false;
+      }
+#pragma unroll
+      for (int i = 0; i < BL; ++i) {
+        const char* s = ((b_okm >> i) & 1) ? b_base + i * b_step + wtC2 + ES * c_cur : zp;
+        glds16(s, Bs + (RP * i + 8 * wid) * 128);
+      }
+    } else if constexpr (!SMALLC) {
 #pragma unroll
       for (int i = 0; i < AL; ++i) {
         const char* s = ((a_vm >> i) & 1) ? xlane + ES * ((uint64_t)a_off[i] + c_cur) : zp;
@@ -325,8 +386,26 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(STAGES 
     for (int ni = 0; ni < TN; ++ni) acc[mi][ni] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int fr = lane & 15, fg = lane >> 4;
+  // HALO: halo row of this lane's fragment pixel (tile pixel r = (r / tw, r % tw)) at tap offset 0;
+  // pixels past th * tw (unused tile rows) read halo row 0 -- computed, never stored
+  int hb[HALO ? TM : 1];
+  if constexpr (HALO) {
+#pragma unroll
+    for (int mi = 0; mi < TM; ++mi) {
+      const int r = wm * WM + mi * 16 + fr;
+      const int pr = (int)fdiv((uint32_t)r, a.fd_tw), pc = r - pr * a.tw;
+      hb[mi] = r < a.th * a.tw ? pr * hwd + pc : 0;
+    }
+  }
   auto advance = [&]() {
-    if constexpr (!SMALLC) {
+    if constexpr (HALO) {   // chunk-major, tap-minor
+      if (++t_cur == NTAP) {
+        t_cur = 0;
+        c_cur += BK;
+        need_halo = true;
+      }
+      tap_setup_halo(t_cur);
+    } else if constexpr (!SMALLC) {
       c_cur += BK;
       if (c_cur >= C) {
         c_cur = 0;
@@ -346,7 +425,11 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(STAGES 
     kend = min(nk, kbeg + per);
   }
   if (kend > kbeg) {
-    if constexpr (!SMALLC) {
+    if constexpr (HALO) {
+      c_cur = (kbeg / NTAP) * BK;
+      t_cur = kbeg - (kbeg / NTAP) * NTAP;
+      tap_setup_halo(t_cur);
+    } else if constexpr (!SMALLC) {
       const int cps = C / BK;   // K-steps per tap
       t_cur = kbeg / cps;
       c_cur = (kbeg - t_cur * cps) * BK;
@@ -379,7 +462,9 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(STAGES 
       const int ch = kk * 4 + fg;
 #pragma unroll
       for (int mi = 0; mi < TM; ++mi) {
-        const int r = wm * WM + mi * 16 + fr;
+        int r;
+        if constexpr (HALO) r = hb[mi] + toff;
+        else r = wm * WM + mi * 16 + fr;
         af[mi] = *reinterpret_cast<const frag_t*>(As + r * 128 + ((ch ^ ((r >> 1) & 7)) << 4));
       }
 #pragma unroll
@@ -674,7 +759,15 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(STAGES 
   for (int rr = rg; rr < BM / NP; rr += RG) {
     const int r = (rr / HM) * WM + h * HM + (rr % HM);
     const int m = m0 + r;
-    if (m >= M || !cvalid) continue;
+    int64_t pix;
+    if constexpr (HALO) {
+      const int pr = (int)fdiv((uint32_t)r, a.fd_tw), pc = r - pr * a.tw;
+      const int oh = hh0 + pr, ow = hw0 + pc;
+      if (r >= a.th * a.tw || oh >= ph.P || ow >= ph.Q || !cvalid) continue;
+      pix = ((int64_t)hn * a.OH + oh * a.so + ph.oh0) * a.OW + ow * a.so + ph.ow0;
+    } else {
+      if (m >= M || !cvalid) continue;
+    }
     float v[8];
     const f32x4 v0 = *reinterpret_cast<const f32x4*>(Cs + rr * CS_LD + cg * 8);
     const f32x4 v1 = *reinterpret_cast<const f32x4*>(Cs + rr * CS_LD + cg * 8 + 4);
@@ -692,11 +785,13 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(STAGES 
 #pragma unroll
       for (int e = 0; e < 8; ++e) v[e] = v[e] * a.scale[c0 + e] + a.shift[c0 + e];
     }
-    const uint32_t n_img = fdiv((uint32_t)m, ph.fdPQ);
-    const uint32_t rem = (uint32_t)m - n_img * PQ;
-    const uint32_t p = fdiv(rem, ph.fdQ);
-    const uint32_t q = rem - p * ph.Q;
-    const int64_t pix = ((int64_t)n_img * a.OH + (int)p * a.so + ph.oh0) * a.OW + (int)q * a.so + ph.ow0;
+    if constexpr (!HALO) {
+      const uint32_t n_img = fdiv((uint32_t)m, ph.fdPQ);
+      const uint32_t rem = (uint32_t)m - n_img * PQ;
+      const uint32_t p = fdiv(rem, ph.fdQ);
+      const uint32_t q = rem - p * ph.Q;
+      pix = ((int64_t)n_img * a.OH + (int)p * a.so + ph.oh0) * a.OW + (int)q * a.so + ph.ow0;
+    }
     if (a.res) {
       float rr[8];
       load8(static_cast<const T*>(a.res) + pix * a.ldres + a.resoff + c0, rr);
@@ -1021,6 +1116,13 @@ extern "C" hipError_t dlmpi_conv_igemm(const ConvArgs* a_in, int bm, int bn, hip
         }
       }
     }
+  }
+  if (a->halo) {   // 3x3 / stride 1 / pad 1 by 2-D tiles with a staged halo (host-planned)
+    if (a->pro != 0 || bm != 128 || a->C % 64 != 0 || a->sk_mode) return hipErrorInvalidValue;
+    if (bn == 128) hipLaunchKernelGGL((conv_igemm_kernel<128, 128, false, 1, 4, 2, 0, uint16_t, false, false, true>), grid, dim3(256), 0, s, *a);
+    else if (bn == 64) hipLaunchKernelGGL((conv_igemm_kernel<128, 64, false, 1, 4, 2, 0, uint16_t, false, false, true>), grid, dim3(256), 0, s, *a);
+    else return hipErrorInvalidValue;
+    return hipGetLastError();
   }
   if (a->pro != 0 && (a->C < 64 || a->C % 64 != 0 || (bm == 256 && bn == 256))) return hipErrorInvalidValue;
   if (bm == 256 && bn == 256) {   // 8 waves, double-buffered; regular channel counts only

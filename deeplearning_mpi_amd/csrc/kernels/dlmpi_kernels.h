@@ -160,6 +160,11 @@ struct ConvArgs {
   double* fin_gsum;                // [ngroups][2][Kout]
   int* fin_tk;                     // [ntiles][ngroups] group tickets, then [ntiles] N-tile tickets
   FinArgs fin;
+  // 2-D halo tiles (conv_igemm.hip HALO; 3x3 / stride 1 / pad 1, one phase): M-tile mt = (n, ti, tj)
+  // of the N x tiles_h x tiles_w grid covers output pixels [ti th, +th) x [tj tw, +tw)
+  int halo;
+  int th, tw, tiles_h, tiles_w;
+  FastDiv fd_tw, fd_tilesw, fd_thw;
   ConvPhase ph[4];
 };
 

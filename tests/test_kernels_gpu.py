@@ -288,6 +288,59 @@ def test_conv_wgrad(shape):
     assert _rel(g, gr) < 5e-3
 
 
+HALO_SHAPES = [
+    # N, H, W, Cin, Cout, x channel stride / offset (a concat slice)
+    (2, 16, 16, 64, 64, None, 0),        # 8 x 16 tiles
+    (2, 14, 14, 256, 256, None, 0),      # 9 x 14 tiles (ResNet layer 3)
+    (3, 7, 7, 512, 512, None, 0),        # 18 x 7 tiles, ragged rows (ResNet layer 4)
+    (1, 28, 30, 128, 128, None, 0),
+    (2, 9, 37, 64, 192, 192, 64),        # 192 outputs: a 64-wide last tile column; x a channel slice
+    (4, 56, 56, 64, 64, None, 0),        # ResNet layer 1
+    (2, 4, 4, 512, 512, None, 0),        # tiny grid: split-K over chunk-major K-steps
+]
+
+
+@pytest.mark.parametrize("shape", HALO_SHAPES, ids=lambda s: "x".join(str(v) for v in s[:5]))
+def test_conv3x3_halo_tiles(shape):
+    """3x3 / stride-1 / pad-1 forward (with BN statistics) and data gradient (with the fused
+    BN-backward epilogue, mask from z) by 2-D halo tiles vs the im2col gather path and the fp32
+    reference: same bf16 products, fp32 sums in another order (chunk-major K)."""
+    nb, rb = _be()
+    N, H, W, Cin, K, ldx, xoff = shape
+    x, xr = _act(N, H, W, Cin, ld=ldx, off=xoff)
+    w = (torch.randn(K, 3, 3, Cin, device=DEV) / (9 * Cin) ** 0.5).to(torch.bfloat16)
+    wT = w.permute(3, 1, 2, 0).contiguous()
+    dy, dyr = _act(N, H, W, K)
+    z, _ = _act(N, H, W, Cin)
+    sc, sh = torch.rand(Cin, device=DEV) + 0.5, torch.randn(Cin, device=DEV) * 0.5
+    out = {}
+    for mode in (2, 0):   # 2: halo tiles on any grid (the default keeps them to >= 28 x 28)
+        nb.C.set_conv_halo(mode)
+        y = _empty(N, H, W, K)
+        mt = nb.conv_mtiles(N, H, W, Cin, K, 3, 3, 1, 1)
+        st = torch.zeros(mt, 2, K, device=DEV)
+        rows = nb.conv_fwd(x, w, K, 3, 3, 1, 1, y, stats=st)
+        assert rows == mt and nb.C.conv_halo_last() == (mode == 2)
+        dx = _empty(N, H, W, Cin)
+        part = nb.conv_dgrad(dy, wT, Cin, 3, 3, 1, 1, dx, fuse=BwdFuse(None, z, None, sc, sh))
+        assert nb.C.conv_halo_last() == (mode == 2)
+        torch.cuda.synchronize()
+        out[mode] = (y.buf.clone(), st.double().sum(0), dx.buf.clone(), part.double().sum(0), mt)
+    nb.C.set_conv_halo(-1)
+    yr = _empty(N, H, W, K, torch.float32)
+    rb.conv_fwd(xr, w.float(), K, 3, 3, 1, 1, yr)
+    dxr = _empty(N, H, W, Cin, torch.float32)
+    rb.conv_dgrad(dyr, wT.float(), Cin, 3, 3, 1, 1, dxr)
+    torch.cuda.synchronize()
+    h, g = out[2], out[0]
+    assert _rel(h[0], yr.buf) < 1e-2 and _rel(h[0], g[0]) < 1e-2
+    assert _rel(h[1], g[1]) < 5e-4   # sums of bf16 outputs that may round the other way
+    keep = (z.buf.float() * sc + sh) > 0
+    assert _rel(h[2], torch.where(keep, dxr.buf, torch.zeros_like(dxr.buf))) < 1e-2
+    assert _rel(h[2], g[2]) < 1e-2
+    assert _rel(h[3], g[3]) < 1e-3
+
+
 WGRAD3_SHAPES = [
     # N, H, W, Cin (real), Ko, x channel stride / offset, dy channel stride / offset
     (2, 16, 16, 64, 64, None, 0, None, 0),        # 64 x 64 tiles, 2 x 2 pixel blocks per image
@@ -707,6 +760,8 @@ def _static_kernels(on: bool):
     C.set_conv_repi(0 if on else -1)
     C.set_conv_stream(0 if on else -1)
     C.set_conv_autotune(0 if on else -1)
+    C.set_conv_halo(0 if on else -1)    # 3x3 halo tiles sum chunk-major (no prologue variant)
+    C.set_wgrad3(0 if on else -1)       # 3x3 spatial-tile weight gradient (no prologue variant)
 
 
 def _deferred_pair(N, H, W, C):
