@@ -21,6 +21,7 @@ using dlmpi::ConvArgs;
 using dlmpi::ConvPhase;
 using dlmpi::FinArgs;
 using dlmpi::Stream1x1Args;
+using dlmpi::DgradStreamArgs;
 using dlmpi::make_fastdiv;
 using dlmpi::WgradArgs;
 
@@ -444,6 +445,7 @@ static at::Tensor colsum_ws(const at::Tensor& like, int T, int C);
 // one row per block of an N-tile (G rows) instead of one per M-tile.  Shape-only decision (the
 // stats buffer is sized from it before the launch); the launch checks the rest (alignment, sizes).
 static int g_stream_ran = 0;   // 1 if the last conv2d_fwd ran the streaming 1x1 kernel (tests)
+static int g_dgrad_stream_ran = 0;   // 1 if the last conv2d_dgrad ran the streaming 1x1 kernel (tests)
 
 static bool stream1x1_shape(int64_t M, int C, int K, int R, int S, int stride, int pad, int pro, int f32, int& bm,
                             int& bn, int& G) {
@@ -809,6 +811,43 @@ c10::optional<at::Tensor> conv2d_dgrad_pro(const at::Tensor& dy, int N, int P, i
   if (a.mscale && (!a.z || !a.mshift)) throw std::runtime_error("conv2d_dgrad: mask from z needs z, scale, shift");
   if ((a.mask || a.mscale || a.mbits) && ((ldmask | maskoff | ldz | zoff | ldz2 | z2off) % 8 != 0 || !a.vec_store))
     throw std::runtime_error("conv2d_dgrad: fused BN tensors must be 8-channel aligned");
+  g_dgrad_stream_ran = 0;
+  {  // streaming 1x1 data gradient (conv1x1_dgrad_stream.hip): memory-bound GEMMs with a heavy epilogue
+    const int64_t M = (int64_t)N * H * W;
+    const int mode = a.mbits ? 1 : (a.mscale ? 2 : 0);
+    int sbm, G;
+    const auto fits = [](int64_t rows, int64_t ld) { return rows * ld < (1ll << 31); };
+    if (R == 1 && S == 1 && stride == 1 && pad == 0 && !a.f32 && pro == 0 && !colsum && !a.mask && !a.z2 &&
+        (a.z != nullptr) == (mode != 0) && a.vec_store && a.kvalid == C && (lddy | dyoff) % 8 == 0 &&
+        (!a.res || (ldres | resoff) % 8 == 0) && fits(M, lddy) && fits(M, lddx) && (!a.res || fits(M, ldres)) &&
+        (!a.z || fits(M, ldz)) && dx.scalar_type() == at::kBFloat16 &&
+        dlmpi_dgrad_stream_plan(M, K, C, mode, &sbm, &G)) {
+      DgradStreamArgs sa{};
+      sa.x = ptr<uint16_t>(dy);
+      sa.ldx = lddy; sa.xoff = dyoff;
+      sa.w = ptr<uint16_t>(wT);
+      sa.y = reinterpret_cast<uint16_t*>(a.y);
+      sa.ldy = lddx; sa.yoff = dxoff;
+      sa.y_bytes = (int)std::min<int64_t>(INT32_MAX, (int64_t)dx.numel() * 2);
+      sa.M = (int)M; sa.K = K; sa.Kout = C;
+      sa.bias = a.bias;
+      sa.res = static_cast<const uint16_t*>(a.res);
+      sa.ldres = ldres; sa.resoff = resoff;
+      sa.z = static_cast<const uint16_t*>(a.z);
+      sa.ldz = ldz; sa.zoff = zoff;
+      sa.mbits = a.mbits;
+      sa.mscale = a.mscale; sa.mshift = a.mshift;
+      sa.G = G; sa.ntiles = C / 128; sa.mtiles = (int)ceil_div(M, sbm);
+      c10::optional<at::Tensor> st;
+      if (a.z) {
+        st = at::empty({(int64_t)G, 2, (int64_t)C}, dy.options().dtype(at::kFloat));
+        sa.stats = ptr<float>(*st);
+      }
+      check(dlmpi_conv1x1_dgrad_stream(&sa, sbm, mode, cur_stream()), "conv2d_dgrad (stream 1x1)");
+      g_dgrad_stream_ran = 1;
+      return st;
+    }
+  }
   set_kstep(a, K);
   set_prologue(a, pro, pk0, pk1, pz, ldpz, pzoff);
   int bm, bn;
@@ -1462,6 +1501,8 @@ void register_ops(pybind11::module& m) {
   m.def("set_conv_repi", [](int mode) { dlmpi_set_conv_repi(mode); });
   m.def("set_conv_stream", [](int mode) { dlmpi_set_conv_stream(mode); });
   m.def("conv_stream_last", []() { return g_stream_ran; });
+  m.def("set_dgrad_stream", [](int mode) { dlmpi_set_dgrad_stream(mode); });
+  m.def("dgrad_stream_last", []() { return g_dgrad_stream_ran; });
   m.def("set_conv_autotune", [](int mode) { g_autotune_override = mode; });
   m.def("set_wgrad3", [](int mode) { g_wgrad3_override = mode; });
   m.def("set_conv_halo", [](int mode) { g_halo_override = mode; });

@@ -71,6 +71,27 @@ struct Stream1x1Args {
   int G, ntiles, mtiles;
 };
 
+// Streaming 1x1 / stride-1 data gradient with the fused BN-backward epilogue (conv1x1_dgrad_stream.hip)
+struct DgradStreamArgs {
+  const uint16_t* x;               // GEMM A operand [M][ldx] (K channels at xoff): dy, or [dy | z]
+  int ldx, xoff;
+  const uint16_t* w;               // [Kout][K]
+  uint16_t* y;                     // dx [M][ldy] (Kout channels at yoff)
+  int ldy, yoff;
+  int y_bytes;
+  int M, K, Kout;
+  const float* bias;               // fp32 [Kout] or null (dual: W . k3)
+  const uint16_t* res;             // residual gradient added before the mask, or null
+  int ldres, resoff;
+  const uint16_t* z;               // BN input of the consumer (statistics, z-mask), or null
+  int ldz, zoff;
+  const uint8_t* mbits;            // [M][Kout / 8] ReLU mask bits (mask mode 1)
+  const float* mscale;             // mask mode 2: keep where z * mscale + mshift > 0
+  const float* mshift;
+  float* stats;                    // [G][2][Kout] {sum dx, sum dx * z} per block, or null
+  int G, ntiles, mtiles;
+};
+
 struct ConvPhase {
   int P, Q;
   int Tr, Ts;
@@ -361,8 +382,11 @@ hipError_t dlmpi_image_batch(const uint8_t* data, const int64_t* labels, const i
 hipError_t dlmpi_delay(double ms, hipStream_t s);
 void dlmpi_set_conv_repi(int mode);
 void dlmpi_set_conv_stream(int mode);
+void dlmpi_set_dgrad_stream(int mode);
 int dlmpi_stream1x1_plan(int64_t M, int C, int Kout, int* bm, int* bn, int* G);
 hipError_t dlmpi_conv1x1_stream(const dlmpi::Stream1x1Args* a, int bm, int bn, hipStream_t s);
+int dlmpi_dgrad_stream_plan(int64_t M, int K, int Kout, int mask_mode, int* bm, int* G);
+hipError_t dlmpi_conv1x1_dgrad_stream(const dlmpi::DgradStreamArgs* a, int bm, int mask_mode, hipStream_t s);
 int dlmpi_fin_scratch(hipStream_t s, size_t gsum_doubles, int tickets, double** gsum, int** tk);
 
 // utilities (util.hip): fp32 fill, int64 add, indexed gather dst[i] (+)= src[idx[i]] (idx < 0: zero;
