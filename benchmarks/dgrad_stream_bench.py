@@ -14,10 +14,12 @@ import torch  # noqa: E402
 CASES = [
     # name, N, H, W, K (A channels), C (dx channels), residual, mask mode, bias
     ("layer1 conv1 dual (2x64 -> 256)", 256, 56, 56, 128, 256, True, "bits", True),
+    ("layer1.1 conv1 dual + z2 (2x64 -> 256)", 256, 56, 56, 128, 256, True, "bits_z2", True),
     ("layer2.0 conv1 dual (2x128 -> 256)", 256, 56, 56, 256, 256, True, "bits", True),
     ("layer2 conv1 dual (2x128 -> 512)", 256, 28, 28, 256, 512, True, "bits", True),
     ("layer3 conv1 (256 -> 1024)", 256, 14, 14, 256, 1024, True, "bits", False),
     ("layer1 conv1 no-res (2x64 -> 256), z-mask", 256, 56, 56, 128, 256, False, "z", True),
+    ("layer1 conv3 dual (2x256 -> 64), z-mask", 256, 56, 56, 512, 64, False, "z", True),
 ]
 
 
@@ -38,10 +40,11 @@ def main():
         res = Act(torch.randn(rows, C, device=dev).to(torch.bfloat16), N, H, W, C) if has_res else None
         z = Act(torch.randn(rows, C, device=dev).to(torch.bfloat16), N, H, W, C)
         bias = torch.randn(C, device=dev) if has_bias else None
-        if mm == "bits":
+        if mm.startswith("bits"):
             mb = torch.randint(0, 256, (rows, C // 8), device=dev, dtype=torch.uint8)
-            fuse = BwdFuse(None, z, None, mbits=mb)
-            mbytes = mb.numel()
+            z2 = Act(torch.randn(rows, C, device=dev).to(torch.bfloat16), N, H, W, C) if mm == "bits_z2" else None
+            fuse = BwdFuse(None, z, z2, mbits=mb)
+            mbytes = mb.numel() + (rows * C * 2 if z2 is not None else 0)
         else:
             fuse = BwdFuse(None, z, None, torch.rand(C, device=dev) + 0.5, torch.randn(C, device=dev))
             mbytes = 0

@@ -815,13 +815,13 @@ c10::optional<at::Tensor> conv2d_dgrad_pro(const at::Tensor& dy, int N, int P, i
   {  // streaming 1x1 data gradient (conv1x1_dgrad_stream.hip): memory-bound GEMMs with a heavy epilogue
     const int64_t M = (int64_t)N * H * W;
     const int mode = a.mbits ? 1 : (a.mscale ? 2 : 0);
-    int sbm, G;
+    int sbm, sbn, G;
     const auto fits = [](int64_t rows, int64_t ld) { return rows * ld < (1ll << 31); };
-    if (R == 1 && S == 1 && stride == 1 && pad == 0 && !a.f32 && pro == 0 && !colsum && !a.mask && !a.z2 &&
+    if (R == 1 && S == 1 && stride == 1 && pad == 0 && !a.f32 && pro == 0 && !colsum && !a.mask &&
         (a.z != nullptr) == (mode != 0) && a.vec_store && a.kvalid == C && (lddy | dyoff) % 8 == 0 &&
         (!a.res || (ldres | resoff) % 8 == 0) && fits(M, lddy) && fits(M, lddx) && (!a.res || fits(M, ldres)) &&
-        (!a.z || fits(M, ldz)) && dx.scalar_type() == at::kBFloat16 &&
-        dlmpi_dgrad_stream_plan(M, K, C, mode, &sbm, &G)) {
+        (!a.z || fits(M, ldz)) && (!a.z2 || fits(M, ldz2)) && dx.scalar_type() == at::kBFloat16 &&
+        dlmpi_dgrad_stream_plan(M, K, C, mode, a.z2 ? 1 : 0, a.res ? 1 : 0, &sbm, &sbn, &G)) {
       DgradStreamArgs sa{};
       sa.x = ptr<uint16_t>(dy);
       sa.ldx = lddy; sa.xoff = dyoff;
@@ -835,15 +835,17 @@ c10::optional<at::Tensor> conv2d_dgrad_pro(const at::Tensor& dy, int N, int P, i
       sa.ldres = ldres; sa.resoff = resoff;
       sa.z = static_cast<const uint16_t*>(a.z);
       sa.ldz = ldz; sa.zoff = zoff;
+      sa.z2 = static_cast<const uint16_t*>(a.z2);
+      sa.ldz2 = ldz2; sa.z2off = z2off;
       sa.mbits = a.mbits;
       sa.mscale = a.mscale; sa.mshift = a.mshift;
-      sa.G = G; sa.ntiles = C / 128; sa.mtiles = (int)ceil_div(M, sbm);
+      sa.G = G; sa.ntiles = C / sbn; sa.mtiles = (int)ceil_div(M, sbm);
       c10::optional<at::Tensor> st;
       if (a.z) {
-        st = at::empty({(int64_t)G, 2, (int64_t)C}, dy.options().dtype(at::kFloat));
+        st = at::empty({(int64_t)G, (int64_t)a.nstat, (int64_t)C}, dy.options().dtype(at::kFloat));
         sa.stats = ptr<float>(*st);
       }
-      check(dlmpi_conv1x1_dgrad_stream(&sa, sbm, mode, cur_stream()), "conv2d_dgrad (stream 1x1)");
+      check(dlmpi_conv1x1_dgrad_stream(&sa, sbm, sbn, mode, cur_stream()), "conv2d_dgrad (stream 1x1)");
       g_dgrad_stream_ran = 1;
       return st;
     }

@@ -46,43 +46,60 @@ __device__ __forceinline__ void dgs_glds(const void* g, char* lds) {
   __builtin_amdgcn_global_load_lds(g, (dgs_lds_void*)lds, 16, 0, 0);
 }
 
-// Epilogue-operand tile of BM rows x 128 channels (256-byte rows): 16-byte chunk j of row r sits at
-// chunk position j ^ (r & 15), so that the 16 rows read by one D^T fragment column hit 16 different
-// chunk positions (all 64 banks once per lane pair)
+// Epilogue-operand tiles of BM rows x BN channels (2 BN-byte rows): 16-byte chunk j of row r sits at
+// chunk position j ^ sw(r) -- for 256-B rows sw = r & 15, for 128-B rows (two rows per 256-B bank
+// line) sw = (r >> 1) & 7 -- so the 16 rows read by one D^T fragment column hit 16 different
+// 16-byte bank slots.
+template <int BN>
+__device__ __forceinline__ int dgs_sw(int r) { return BN == 128 ? (r & 15) : ((r >> 1) & 7); }
+template <int BN>
 __device__ __forceinline__ int dgs_eoff(int r, int col) {   // byte offset of channel col (multiple of 4)
-  return r * 256 + ((((col >> 3) ^ (r & 15))) << 4) + ((col & 4) << 1);
+  return r * (2 * BN) + ((((col >> 3) ^ dgs_sw<BN>(r))) << 4) + ((col & 4) << 1);
 }
 
-// MASK: 1 = forward mask bits, 2 = z * mscale + mshift > 0, 0 = no mask and no statistics
-template <int BM, int KS, int NW, int MASK>
+// MASK: 1 = forward mask bits, 2 = z * mscale + mshift > 0, 0 = no mask and no statistics;
+// Z2: a second BN input (third partial row sum dx * z2);
+// ADB: A double-buffered, the next tile's A issued at the top of the current tile (long reductions:
+// the A tile is most of a tile's bytes), else single-buffered and issued after the MFMAs.
+template <int BM, int BN, int KS, int NW, int MASK, bool Z2, bool ADB>
 __global__ __launch_bounds__(64 * NW) void conv1x1_dgrad_stream_kernel(const DgradStreamArgs a) {
-  constexpr int BN = 128;
   constexpr bool Z = MASK != 0;
+  static_assert(!Z2 || Z, "z2 needs the fused statistics");
+  static_assert(MASK != 1 || BN == 128, "mask bits: 128-channel tiles (one 16-byte piece per row)");
+  static_assert(BN == 64 || BN == 128, "tile width");
+  constexpr bool RES = BN == 128;               // residual-gradient operand (64-wide tiles: none)
+  constexpr int NS = Z2 ? 3 : 2;
   constexpr int NT = 64 * NW;
   constexpr int WGM = 2, WGN = NW / 2;          // wave grid
   constexpr int WM = BM / WGM, WN = BN / WGN;
   constexpr int TM = WM / 16, TN = WN / 16;
   constexpr int RP = NT / 8;                    // 128-B rows staged per pass (A / W tiles)
   constexpr int AL = BM / RP, BL = BN / RP;
-  constexpr int EP = NT / 16;                   // 256-B rows staged per pass (epilogue operand tiles)
+  constexpr int ERB = 2 * BN, ECH = BN / 8;     // epilogue tiles: bytes / 16-B chunks per row
+  constexpr int EP = NT / ECH;                  // epilogue-tile rows staged per pass
   constexpr int EL = BM / EP;
   constexpr int NSTORE = BM / EP;               // 16-byte output row stores per thread per tile
   constexpr int MB_ROWS = BM > 64 ? BM : 64;    // mask-bit tile: one wave instruction (16 B / row)
-  constexpr int E_BYTES = BM * 256;
-  static_assert(AL >= 1 && BM % RP == 0 && BN % RP == 0 && BM % EP == 0 && TM >= 1 && TN >= 1, "tile shape");
+  constexpr int E_BYTES = BM * ERB;
+  static_assert(AL >= 1 && BL >= 1 && BM % RP == 0 && BN % RP == 0 && BM % EP == 0 && EL >= 1 && TM >= 1 &&
+                TN >= 1, "tile shape");
   constexpr int W_BYTES = KS * BN * 128, A_BYTES = KS * BM * 128;
   // distinct LDS objects per buffer (the compiler's LDS-DMA alias tracking then sees that the
   // epilogue's reads of one buffer do not depend on the prefetch in flight into the other; the
   // double-buffer index is static: the tile loop is unrolled by two)
   __shared__ __attribute__((aligned(16))) char Ws[W_BYTES];
-  __shared__ __attribute__((aligned(16))) char As[A_BYTES];
-  // epilogue-operand double buffer: [residual | z | mask bits] per buffer (one LDS object each: the
-  // compiler tracks a handful of LDS-DMA targets, more objects make it wait for all of them)
-  constexpr int EZ_OFF = E_BYTES, EM_OFF = E_BYTES + (Z ? E_BYTES : 0);
-  constexpr int EB_BYTES = EM_OFF + (MASK == 1 ? MB_ROWS * 16 : 0);
+  __shared__ __attribute__((aligned(16))) char A0[A_BYTES];
+  __shared__ __attribute__((aligned(16))) char A1[ADB ? A_BYTES : 16];
+  // epilogue-operand double buffer: [residual | z | z2 | mask bits] per buffer (one LDS object each:
+  // the compiler tracks a handful of LDS-DMA targets, more objects make it wait for all of them).
+  // With statistics the output tile is staged in place of the consumed z tile (each lane writes
+  // exactly the positions it has read); without, in a tile of its own.
+  constexpr int EZ_OFF = RES ? E_BYTES : 0, EZ2_OFF = EZ_OFF + (Z ? E_BYTES : 0), EM_OFF = EZ2_OFF + (Z2 ? E_BYTES : 0);
+  constexpr int EB_BYTES0 = EM_OFF + (MASK == 1 ? MB_ROWS * 16 : 0);
+  constexpr int EB_BYTES = EB_BYTES0 > 16 ? EB_BYTES0 : 16;
   __shared__ __attribute__((aligned(16))) char E0[EB_BYTES];
   __shared__ __attribute__((aligned(16))) char E1[EB_BYTES];
-  __shared__ __attribute__((aligned(16))) char Os[E_BYTES];
+  __shared__ __attribute__((aligned(16))) char Os[Z ? 16 : E_BYTES];
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -90,13 +107,13 @@ __global__ __launch_bounds__(64 * NW) void conv1x1_dgrad_stream_kernel(const Dgr
   const int fr = lane & 15, fg = lane >> 4;
   const int lrow = tid >> 3;                                 // A / W staging row (+ RP i)
   const int jc = (tid & 7) ^ ((tid >> 4) & 7);               // swizzled 16-B chunk this lane fetches
-  const int erow = tid >> 4;                                 // epilogue-tile staging row (+ EP i)
+  const int erow = tid / ECH, ej = tid % ECH;                // epilogue-tile staging row (+ EP i), chunk
   const char* zp = reinterpret_cast<const char*>(g_zero_page);
 
   const uint32_t lb = xcd_remap(blockIdx.x, gridDim.x);
   const int nt = lb % a.ntiles, g = lb / a.ntiles;
   const int n0 = nt * BN;
-  const bool has_res = a.res != nullptr;
+  const bool has_res = RES && a.res != nullptr;
 
   // ---- weights: staged once --------------------------------------------------------------------
 #pragma unroll
@@ -109,27 +126,28 @@ __global__ __launch_bounds__(64 * NW) void conv1x1_dgrad_stream_kernel(const Dgr
     }
   // rows past M re-read row M - 1 (outputs dropped, statistics masked): unconditional loads keep the
   // compiler's vmcnt scoreboard exact (32-bit offsets: host-checked)
-  auto issue_a = [&](int mt) {
+  auto issue_a = [&](int mt, char* Ab) {
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks)
 #pragma unroll
       for (int i = 0; i < AL; ++i) {
         const int m = min(mt * BM + lrow + RP * i, a.M - 1);
-        dgs_glds(a.x + (uint32_t)(m * a.ldx + a.xoff + ks * 64 + 8 * jc), As + ks * BM * 128 + (RP * i + 8 * wid) * 128);
+        dgs_glds(a.x + (uint32_t)(m * a.ldx + a.xoff + ks * 64 + 8 * jc), Ab + ks * BM * 128 + (RP * i + 8 * wid) * 128);
       }
   };
   auto issue_e = [&](int mt, char* Rb, char* Zb, char* Mb) {
-    const int ej = (tid & 15);
 #pragma unroll
     for (int i = 0; i < EL; ++i) {
       const int r = erow + EP * i;
       const int m = min(mt * BM + r, a.M - 1);
-      const int gj = ej ^ (r & 15);                           // global chunk stored at LDS chunk ej
+      const int gj = ej ^ dgs_sw<BN>(r);                      // global chunk stored at LDS chunk ej
       // LDS destination: lane-linear 1 KB per wave instruction = rows erow (+ EP i), chunk ej
       if (has_res)
-        dgs_glds(a.res + (uint32_t)(m * a.ldres + a.resoff + n0 + gj * 8), Rb + i * EP * 256 + wid * 1024);
+        dgs_glds(a.res + (uint32_t)(m * a.ldres + a.resoff + n0 + gj * 8), Rb + i * EP * ERB + wid * 1024);
       if constexpr (Z)
-        dgs_glds(a.z + (uint32_t)(m * a.ldz + a.zoff + n0 + gj * 8), Zb + i * EP * 256 + wid * 1024);
+        dgs_glds(a.z + (uint32_t)(m * a.ldz + a.zoff + n0 + gj * 8), Zb + i * EP * ERB + wid * 1024);
+      if constexpr (Z2)
+        dgs_glds(a.z2 + (uint32_t)(m * a.ldz2 + a.z2off + n0 + gj * 8), Zb + (EZ2_OFF - EZ_OFF) + i * EP * ERB + wid * 1024);
     }
     if constexpr (MASK == 1) {
       if (wid == 0) {   // one 16-B piece (128 mask bits) per row
@@ -150,21 +168,23 @@ __global__ __launch_bounds__(64 * NW) void conv1x1_dgrad_stream_kernel(const Dgr
       mh[ni] = *reinterpret_cast<const f32x4*>(a.mshift + c);
     }
   }
-  float s1[TN][4], s2[TN][4];
+  float s1[TN][4], s2[TN][4], s3[TN][4];
 #pragma unroll
   for (int ni = 0; ni < TN; ++ni)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) { s1[ni][j] = 0.f; s2[ni][j] = 0.f; }
+    for (int j = 0; j < 4; ++j) { s1[ni][j] = 0.f; s2[ni][j] = 0.f; s3[ni][j] = 0.f; }
 
-  const int cg = tid & 15, rg = tid >> 4;   // row-store phase: 16 threads per 256-B row
+  const int cg = tid % ECH, rg = tid / ECH;   // row-store phase: ECH threads per row
 
-  // one tile; Rc/Zc/Mc: this tile's epilogue operands, Rn/Zn/Mn: the next tile's (prefetched here)
-  auto tile = [&](int mt, int it, const char* Rc, const char* Zc, const char* Mc, char* Rn, char* Zn, char* Mn) {
-    (void)it;
+  // one tile; Ac / Rc / Zc / Mc: this tile's operands, An / Rn / Zn / Mn: the next tile's (prefetched)
+  auto tile = [&](int mt, const char* Ac, char* An, const char* Rc, char* Zc, const char* Mc, char* Rn, char* Zn,
+                  char* Mn) {
+    char* Ot = Z ? Zc : Os;   // output staging tile
     // this tile's A / epilogue operands: the only younger vector-memory operations of this wave are
     // the previous tile's NSTORE stores, which stay in flight (before the first tile: none)
     __builtin_amdgcn_s_waitcnt(dgs_vmcnt(NSTORE));
     dgs_barrier();   // this tile's A / epilogue operands landed in every wave; last tile's reads done
+    if constexpr (ADB) issue_a(mt + a.G, An);
 
     f32x4 acc[TM][TN];
 #pragma unroll
@@ -173,7 +193,7 @@ __global__ __launch_bounds__(64 * NW) void conv1x1_dgrad_stream_kernel(const Dgr
       for (int ni = 0; ni < TN; ++ni) acc[mi][ni] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) {
-      const char* A = As + ks * BM * 128;
+      const char* A = Ac + ks * BM * 128;
       const char* B = Ws + ks * BN * 128;
 #pragma unroll
       for (int kk = 0; kk < 2; ++kk) {
@@ -198,7 +218,7 @@ __global__ __launch_bounds__(64 * NW) void conv1x1_dgrad_stream_kernel(const Dgr
     }
     dgs_barrier();       // every wave is done reading this tile's A
     issue_e(mt + a.G, Rn, Zn, Mn);
-    issue_a(mt + a.G);   // the next tile's A streams in under this epilogue
+    if constexpr (!ADB) issue_a(mt + a.G, An);   // the next tile's A streams in under this epilogue
 
     // epilogue on the D^T fragments: lane (fr, fg) holds row wm*WM + 16 mi + fr, channels
     // wn*WN + 16 ni + 4 fg + [0, 4)
@@ -209,7 +229,7 @@ __global__ __launch_bounds__(64 * NW) void conv1x1_dgrad_stream_kernel(const Dgr
 #pragma unroll
       for (int ni = 0; ni < TN; ++ni) {
         const int col = wn * WN + ni * 16 + 4 * fg;
-        const int eo = dgs_eoff(row, col);
+        const int eo = dgs_eoff<BN>(row, col);
         f32x4 v = acc[mi][ni] + bq[ni];
         if (has_res) {
           const u32x2 q = *reinterpret_cast<const u32x2*>(Rc + eo);
@@ -234,61 +254,72 @@ __global__ __launch_bounds__(64 * NW) void conv1x1_dgrad_stream_kernel(const Dgr
             s1[ni][j] += rv;
             s2[ni][j] += rv * zz[j];
           }
+          if constexpr (Z2) {
+            const u32x2 q2 = *reinterpret_cast<const u32x2*>(Zc + (EZ2_OFF - EZ_OFF) + eo);
+            const f32x4 z2{__uint_as_float(q2[0] << 16), __uint_as_float(q2[0] & 0xffff0000u),
+                           __uint_as_float(q2[1] << 16), __uint_as_float(q2[1] & 0xffff0000u)};
+#pragma unroll
+            for (int j = 0; j < 4; ++j) s3[ni][j] += bf2f(f2bf(v[j])) * keep * z2[j];
+          }
         }
-        *reinterpret_cast<u32x2*>(Os + eo) = u32x2{pack2bf(v[0], v[1]), pack2bf(v[2], v[3])};
+        *reinterpret_cast<u32x2*>(Ot + eo) = u32x2{pack2bf(v[0], v[1]), pack2bf(v[2], v[3])};
       }
     }
     dgs_barrier();
 #pragma unroll
     for (int i = 0; i < NSTORE; ++i) {
       const int row = rg + EP * i;
-      const u32x4 q = *reinterpret_cast<const u32x4*>(Os + row * 256 + ((cg ^ (row & 15)) << 4));
+      const u32x4 q = *reinterpret_cast<const u32x4*>(Ot + row * ERB + ((cg ^ dgs_sw<BN>(row)) << 4));
       const int m = mt * BM + row;
       const uint32_t off0 = (uint32_t)(m * a.ldy + a.yoff + n0 + cg * 8) * 2u;   // 32-bit: host-checked
       __builtin_amdgcn_raw_buffer_store_b128(q, yr, m < a.M ? off0 : 0x80000000u, 0, 0);
     }
   };
 
+  char* const A1p = ADB ? A1 : A0;
   int mt = g;
   if (mt < a.mtiles) {
-    issue_a(mt);
+    issue_a(mt, A0);
     issue_e(mt, E0, E0 + EZ_OFF, E0 + EM_OFF);
   }
   __builtin_amdgcn_s_waitcnt(dgs_vmcnt(0));
-  for (int it = 0; mt < a.mtiles;) {
-    tile(mt, it, E0, E0 + EZ_OFF, E0 + EM_OFF, E1, E1 + EZ_OFF, E1 + EM_OFF);
+  for (; mt < a.mtiles;) {
+    tile(mt, A0, A1p, E0, E0 + EZ_OFF, E0 + EM_OFF, E1, E1 + EZ_OFF, E1 + EM_OFF);
     mt += a.G;
-    ++it;
     if (mt >= a.mtiles) break;
-    tile(mt, it, E1, E1 + EZ_OFF, E1 + EM_OFF, E0, E0 + EZ_OFF, E0 + EM_OFF);
+    tile(mt, A1p, A0, E1, E1 + EZ_OFF, E1 + EM_OFF, E0, E0 + EZ_OFF, E0 + EM_OFF);
     mt += a.G;
-    ++it;
   }
   __builtin_amdgcn_s_waitcnt(dgs_vmcnt(0));   // no LDS-DMA in flight when the block retires
 
   if constexpr (Z) {
     __syncthreads();
-    // per-lane sums -> [2][WGM * 16][BN] (the weight tile is free now) -> one row per block
-    float* red = reinterpret_cast<float*>(Ws);
-    static_assert(2 * WGM * 16 * BN * 4 <= W_BYTES, "statistics combine fits the weight tile");
+    // per-lane sums -> [NS][WGM * 16][BN] (the weight / operand tiles are free now) -> one row per block
+    constexpr int RED_BYTES = NS * WGM * 16 * BN * 4;
+    float* red = reinterpret_cast<float*>(RED_BYTES <= W_BYTES ? Ws : E0);
+    static_assert(RED_BYTES <= W_BYTES || RED_BYTES <= EB_BYTES, "statistics combine fits a free tile");
+    constexpr int RR = WGM * 16;
 #pragma unroll
     for (int ni = 0; ni < TN; ++ni)
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int col = wn * WN + ni * 16 + 4 * fg + j;
         red[(wm * 16 + fr) * BN + col] = s1[ni][j];
-        red[(WGM * 16 + wm * 16 + fr) * BN + col] = s2[ni][j];
+        red[(RR + wm * 16 + fr) * BN + col] = s2[ni][j];
+        if constexpr (Z2) red[(2 * RR + wm * 16 + fr) * BN + col] = s3[ni][j];
       }
     __syncthreads();
     if (tid < BN && n0 + tid < a.Kout) {
-      float t1 = 0.f, t2 = 0.f;
-      for (int q = 0; q < WGM * 16; ++q) {
+      float t1 = 0.f, t2 = 0.f, t3 = 0.f;
+      for (int q = 0; q < RR; ++q) {
         t1 += red[q * BN + tid];
-        t2 += red[(WGM * 16 + q) * BN + tid];
+        t2 += red[(RR + q) * BN + tid];
+        if constexpr (Z2) t3 += red[(2 * RR + q) * BN + tid];
       }
-      float* st = a.stats + (int64_t)g * 2 * a.Kout + n0 + tid;
+      float* st = a.stats + (int64_t)g * NS * a.Kout + n0 + tid;
       st[0] = t1;
       st[a.Kout] = t2;
+      if constexpr (Z2) st[2 * a.Kout] = t3;
     }
   }
 }
@@ -303,34 +334,53 @@ extern "C" void dlmpi_set_dgrad_stream(int mode) { g_dgs_override = mode; }
 
 // Tile plan: BM rows per tile and G blocks per 128-channel column (one block per CU over the chip),
 // or 0 if the kernel does not apply to this shape.
-extern "C" int dlmpi_dgrad_stream_plan(int64_t M, int K, int Kout, int mask_mode, int* bm, int* G) {
+// DLMPI_DGS_BLOCKS: grid size target (default 256 = one block per CU; more blocks = less work per
+// block, so a block that starts late behind another stream's kernel extends the tail less).
+extern "C" int dlmpi_dgrad_stream_plan(int64_t M, int K, int Kout, int mask_mode, int z2, int has_res, int* bm, int* bn,
+                                       int* G) {
   static const int env = [] {
     const char* e = getenv("DLMPI_DGRAD_STREAM");
     return e ? atoi(e) : 1;
   }();
+  static const int blocks = [] {
+    const char* e = getenv("DLMPI_DGS_BLOCKS");
+    return e ? atoi(e) : 256;
+  }();
   const int on = g_dgs_override >= 0 ? g_dgs_override : env;
-  if (!on || M <= 0 || Kout % 128 != 0 || mask_mode < 0 || mask_mode > 2) return 0;
-  if (K == 128) *bm = 64;
-  else if (K == 256) *bm = 32;
+  if (!on || M <= 0 || mask_mode < 0 || mask_mode > 2 || (z2 && mask_mode == 0)) return 0;
+  if (K == 512 && (has_res || z2 || mask_mode == 1)) return 0;   // 64-wide tiles: z (and z-mask) only
+  // LDS per block (one block per CU): weights KS x BN x 128 B resident + A + 2 x epilogue operands
+  if (K == 128 && Kout % 128 == 0) { *bm = 64; *bn = 128; }          // 98-146 KB
+  else if (K == 256 && Kout % 128 == 0) { *bm = 32; *bn = 128; }     // 106-133 KB
+  else if (K == 512 && Kout % 64 == 0) { *bm = 64; *bn = 64; }      // 8 waves: 136-144 KB
   else return 0;
-  const int ntiles = Kout / 128;
+  const int ntiles = Kout / *bn;
   const int64_t mtiles = (M + *bm - 1) / *bm;
-  int target = 256 / ntiles;
+  int target = blocks / ntiles;
   if (target < 8) target = 8;
   *G = (int)(mtiles < target ? mtiles : target);
   return 1;
 }
 
-extern "C" hipError_t dlmpi_conv1x1_dgrad_stream(const DgradStreamArgs* a, int bm, int mask_mode, hipStream_t s) {
+extern "C" hipError_t dlmpi_conv1x1_dgrad_stream(const DgradStreamArgs* a, int bm, int bn, int mask_mode, hipStream_t s) {
   const dim3 grid((unsigned)(a->ntiles * a->G));
-#define DLMPI_DGS(BM_, KS_, NW_)                                                                                    \
-  do {                                                                                                             \
-    if (mask_mode == 1) hipLaunchKernelGGL((conv1x1_dgrad_stream_kernel<BM_, KS_, NW_, 1>), grid, dim3(64 * NW_), 0, s, *a); \
-    else if (mask_mode == 2) hipLaunchKernelGGL((conv1x1_dgrad_stream_kernel<BM_, KS_, NW_, 2>), grid, dim3(64 * NW_), 0, s, *a); \
-    else hipLaunchKernelGGL((conv1x1_dgrad_stream_kernel<BM_, KS_, NW_, 0>), grid, dim3(64 * NW_), 0, s, *a);       \
+#define DLMPI_DGS(BM_, BN_, KS_, NW_, ADB_)                                                                   \
+  do {                                                                                                       \
+    const dim3 blk(64 * NW_);                                                                                \
+    if (a->z2) {                                                                                             \
+      if (mask_mode == 1) hipLaunchKernelGGL((conv1x1_dgrad_stream_kernel<BM_, BN_, KS_, NW_, 1, true, ADB_>), grid, blk, 0, s, *a); \
+      else hipLaunchKernelGGL((conv1x1_dgrad_stream_kernel<BM_, BN_, KS_, NW_, 2, true, ADB_>), grid, blk, 0, s, *a); \
+    } else if (mask_mode == 1) hipLaunchKernelGGL((conv1x1_dgrad_stream_kernel<BM_, BN_, KS_, NW_, 1, false, ADB_>), grid, blk, 0, s, *a); \
+    else if (mask_mode == 2) hipLaunchKernelGGL((conv1x1_dgrad_stream_kernel<BM_, BN_, KS_, NW_, 2, false, ADB_>), grid, blk, 0, s, *a); \
+    else hipLaunchKernelGGL((conv1x1_dgrad_stream_kernel<BM_, BN_, KS_, NW_, 0, false, ADB_>), grid, blk, 0, s, *a); \
   } while (0)
-  if (bm == 64 && a->K == 128) DLMPI_DGS(64, 2, 8);
-  else if (bm == 32 && a->K == 256) DLMPI_DGS(32, 4, 4);
+  if (bm == 64 && bn == 128 && a->K == 128) DLMPI_DGS(64, 128, 2, 8, false);
+  else if (bm == 32 && bn == 128 && a->K == 256) DLMPI_DGS(32, 128, 4, 4, false);
+  else if (bm == 64 && bn == 64 && a->K == 512 && !a->z2 && !a->res) {   // z-mask / plain only
+    if (mask_mode == 2) hipLaunchKernelGGL((conv1x1_dgrad_stream_kernel<64, 64, 8, 8, 2, false, false>), grid, dim3(512), 0, s, *a);
+    else if (mask_mode == 0) hipLaunchKernelGGL((conv1x1_dgrad_stream_kernel<64, 64, 8, 8, 0, false, false>), grid, dim3(512), 0, s, *a);
+    else return hipErrorInvalidValue;
+  }
   else return hipErrorInvalidValue;
 #undef DLMPI_DGS
   return hipGetLastError();

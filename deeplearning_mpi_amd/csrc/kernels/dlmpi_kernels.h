@@ -85,10 +85,12 @@ struct DgradStreamArgs {
   int ldres, resoff;
   const uint16_t* z;               // BN input of the consumer (statistics, z-mask), or null
   int ldz, zoff;
+  const uint16_t* z2;              // a second BN input consuming the same gradient (ResNet downsample)
+  int ldz2, z2off;
   const uint8_t* mbits;            // [M][Kout / 8] ReLU mask bits (mask mode 1)
   const float* mscale;             // mask mode 2: keep where z * mscale + mshift > 0
   const float* mshift;
-  float* stats;                    // [G][2][Kout] {sum dx, sum dx * z} per block, or null
+  float* stats;                    // [G][2|3][Kout] {sum dx, sum dx * z [, sum dx * z2]} per block
   int G, ntiles, mtiles;
 };
 
@@ -385,8 +387,8 @@ void dlmpi_set_conv_stream(int mode);
 void dlmpi_set_dgrad_stream(int mode);
 int dlmpi_stream1x1_plan(int64_t M, int C, int Kout, int* bm, int* bn, int* G);
 hipError_t dlmpi_conv1x1_stream(const dlmpi::Stream1x1Args* a, int bm, int bn, hipStream_t s);
-int dlmpi_dgrad_stream_plan(int64_t M, int K, int Kout, int mask_mode, int* bm, int* G);
-hipError_t dlmpi_conv1x1_dgrad_stream(const dlmpi::DgradStreamArgs* a, int bm, int mask_mode, hipStream_t s);
+int dlmpi_dgrad_stream_plan(int64_t M, int K, int Kout, int mask_mode, int z2, int has_res, int* bm, int* bn, int* G);
+hipError_t dlmpi_conv1x1_dgrad_stream(const dlmpi::DgradStreamArgs* a, int bm, int bn, int mask_mode, hipStream_t s);
 int dlmpi_fin_scratch(hipStream_t s, size_t gsum_doubles, int tickets, double** gsum, int** tk);
 
 // utilities (util.hip): fp32 fill, int64 add, indexed gather dst[i] (+)= src[idx[i]] (idx < 0: zero;

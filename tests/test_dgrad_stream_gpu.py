@@ -22,6 +22,8 @@ SHAPES = [
     (3, 5, 7, 128, 128),       # 105 rows, one 128-channel column
     (8, 28, 28, 256, 512),
     (32, 56, 56, 128, 256),    # layer-1 scale (100k rows, every block walks many tiles)
+    (4, 14, 14, 512, 64),      # long reduction into 64-channel tiles (z-mask / plain only)
+    (2, 28, 28, 512, 128),
 ]
 
 
@@ -46,7 +48,7 @@ def _run(nb, mode_on, dy, wT, C, res, fuse, out_layout, bias):
 
 
 @pytest.mark.parametrize("shape", SHAPES)
-@pytest.mark.parametrize("mode", ["bits", "from_z", "res_only", "plain"])
+@pytest.mark.parametrize("mode", ["bits", "bits_z2", "from_z", "from_z2", "res_only", "plain"])
 def test_dgrad_stream_matches_general_kernel(shape, mode):
     N, H, W, K, C = shape
     nb = NativeBackend(DEV)
@@ -54,29 +56,35 @@ def test_dgrad_stream_matches_general_kernel(shape, mode):
     rows = N * H * W
     dy = Act(torch.randn(rows, K, device=DEV, generator=g).to(torch.bfloat16), N, H, W, K)
     wT = (torch.randn(C, 1, 1, K, device=DEV, generator=g) / K ** 0.5).to(torch.bfloat16)
-    bias = torch.randn(C, device=DEV, generator=g) * 0.1 if mode in ("bits", "res_only") else None
+    bias = torch.randn(C, device=DEV, generator=g) * 0.1 if mode in ("bits", "bits_z2", "res_only") else None
     res = None
-    if mode in ("bits", "res_only"):
+    if mode in ("bits", "bits_z2", "res_only"):
         res = Act(torch.randn(rows, C, device=DEV, generator=g).to(torch.bfloat16), N, H, W, C)
     fuse = None
-    z = None
-    if mode == "bits":
+    z = z2 = None
+    if mode.endswith("z2"):
+        z2 = Act(torch.randn(rows, C, device=DEV, generator=g).to(torch.bfloat16), N, H, W, C)
+    if mode.startswith("bits"):
         z = Act(torch.randn(rows, C, device=DEV, generator=g).to(torch.bfloat16), N, H, W, C)
         y = torch.randn(rows, C, device=DEV, generator=g)
         pos = (y > 0).view(-1, C // 8, 8).to(torch.uint8)
         mb = (pos * (2 ** torch.arange(8, device=DEV, dtype=torch.uint8))).sum(-1).to(torch.uint8).contiguous()
-        fuse = BwdFuse(None, z, None, mbits=mb)
+        fuse = BwdFuse(None, z, z2, mbits=mb)
         keep = y > 0
-    elif mode == "from_z":
+    elif mode.startswith("from_z"):
         z = Act(torch.randn(rows, C, device=DEV, generator=g).to(torch.bfloat16), N, H, W, C)
         sc, sh = torch.rand(C, device=DEV, generator=g) + 0.5, torch.randn(C, device=DEV, generator=g) * 0.5
-        fuse = BwdFuse(None, z, None, sc, sh)
+        fuse = BwdFuse(None, z, z2, sc, sh)
         keep = torch.addcmul(sh, z.buf.float(), sc) > 0
     for layout in ("dense", "dual"):
         dx1, p1, ran1 = _run(nb, 1, dy, wT, C, res, fuse, layout, bias)
         dx0, p0, ran0 = _run(nb, 0, dy, wT, C, res, fuse, layout, bias)
-        assert ran1 == 1 and ran0 == 0
-        assert torch.equal(dx1.buf, dx0.buf), (layout, _rel(dx1.buf, dx0.buf))
+        supported = K != 512 or mode in ("from_z", "plain")
+        assert ran1 == int(supported) and ran0 == 0
+        if K <= 256:
+            assert torch.equal(dx1.buf, dx0.buf), (layout, _rel(dx1.buf, dx0.buf))
+        else:   # the general kernel may split the 8 K-steps of a small grid (split-K): another fp32 order
+            assert _rel(dx1.buf, dx0.buf) < 1e-2, (layout, _rel(dx1.buf, dx0.buf))
         if layout == "dual":
             assert bool((dx1.buf[:, C:].float() == 7.0).all())
         d = dx1.buf[:, :C]
@@ -84,9 +92,10 @@ def test_dgrad_stream_matches_general_kernel(shape, mode):
             assert p1 is None and p0 is None
             continue
         assert (d[~keep] == 0).all()
-        assert p1.shape[1:] == p0.shape[1:] == (2, C)
+        ns = 3 if z2 is not None else 2
+        assert p1.shape[1:] == p0.shape[1:] == (ns, C)
         v = d.double()
-        ref = [v.sum(0), (v * z.buf.double()).sum(0)]
+        ref = [v.sum(0), (v * z.buf.double()).sum(0)] + ([(v * z2.buf.double()).sum(0)] if z2 is not None else [])
         s1, s0 = p1.double().sum(0), p0.double().sum(0)
         for k, r in enumerate(ref):
             scale = r.abs().max().clamp_min(1e-3)
