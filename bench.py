@@ -114,6 +114,9 @@ def main():
     ap.add_argument("--rccl1", type=int, default=0,
                     help="1 (single GPU only): run the step through a world-size-1 RCCL communicator with the "
                          "bucketed reducer forced on (every all-reduce / the K5 broadcast go through RCCL)")
+    ap.add_argument("--pyprof", type=int, default=0,
+                    help="N > 0: after the timed steps, run N more steps under cProfile and print the top host "
+                         "functions (self time) to stderr -- where the eager step's issue time goes")
     ap.add_argument("--host_time", type=int, default=0,
                     help="N > 0: after the timed steps, N more steps timing the HOST issue time of each step "
                          "(call to return, GPU running behind) against the GPU step time; printed to stderr")
@@ -244,6 +247,21 @@ def main():
         if comm.rank == 0:
             print(json.dumps({"breakdown_ms_per_step": bd, "max_over_ranks": bd_max,
                               "n_gpus": world, "config": args.config}), file=sys.stderr, flush=True)
+    if args.pyprof > 0 and comm.rank == 0:
+        import cProfile
+        import io
+        import pstats
+
+        sync()
+        pr = cProfile.Profile()
+        pr.enable()
+        for _ in range(args.pyprof):
+            step()
+        pr.disable()
+        sync()
+        buf = io.StringIO()
+        pstats.Stats(pr, stream=buf).sort_stats("tottime").print_stats(45)
+        print(f"[pyprof] {args.pyprof} steps, self time per function\n" + buf.getvalue(), file=sys.stderr, flush=True)
     host_info = None
     if args.host_time > 0 and dev.type == "cuda":
         # host issue time of one step: the CPU time from calling step() to its return, each step

@@ -61,7 +61,8 @@ __device__ __forceinline__ int dgs_eoff(int r, int col) {   // byte offset of ch
 // Z2: a second BN input (third partial row sum dx * z2);
 // ADB: A double-buffered, the next tile's A issued at the top of the current tile (long reductions:
 // the A tile is most of a tile's bytes), else single-buffered and issued after the MFMAs.
-template <int BM, int BN, int KS, int NW, int MASK, bool Z2, bool ADB>
+// WGM: wave-grid rows (WGM x NW / WGM waves; 48-row tiles: 3 x 2).
+template <int BM, int BN, int KS, int NW, int WGM, int MASK, bool Z2, bool ADB>
 __global__ __launch_bounds__(64 * NW) void conv1x1_dgrad_stream_kernel(const DgradStreamArgs a) {
   constexpr bool Z = MASK != 0;
   static_assert(!Z2 || Z, "z2 needs the fused statistics");
@@ -70,20 +71,21 @@ __global__ __launch_bounds__(64 * NW) void conv1x1_dgrad_stream_kernel(const Dgr
   constexpr bool RES = BN == 128;               // residual-gradient operand (64-wide tiles: none)
   constexpr int NS = Z2 ? 3 : 2;
   constexpr int NT = 64 * NW;
-  constexpr int WGM = 2, WGN = NW / 2;          // wave grid
+  constexpr int WGN = NW / WGM;                 // wave grid
   constexpr int WM = BM / WGM, WN = BN / WGN;
   constexpr int TM = WM / 16, TN = WN / 16;
   constexpr int RP = NT / 8;                    // 128-B rows staged per pass (A / W tiles)
-  constexpr int AL = BM / RP, BL = BN / RP;
+  constexpr int AL = BM / RP;
+  constexpr int BL = (BN + RP - 1) / RP, WROWS = BL * RP;   // weight rows staged (>= BN: padding rows)
   constexpr int ERB = 2 * BN, ECH = BN / 8;     // epilogue tiles: bytes / 16-B chunks per row
   constexpr int EP = NT / ECH;                  // epilogue-tile rows staged per pass
   constexpr int EL = BM / EP;
   constexpr int NSTORE = BM / EP;               // 16-byte output row stores per thread per tile
   constexpr int MB_ROWS = BM > 64 ? BM : 64;    // mask-bit tile: one wave instruction (16 B / row)
   constexpr int E_BYTES = BM * ERB;
-  static_assert(AL >= 1 && BL >= 1 && BM % RP == 0 && BN % RP == 0 && BM % EP == 0 && EL >= 1 && TM >= 1 &&
-                TN >= 1, "tile shape");
-  constexpr int W_BYTES = KS * BN * 128, A_BYTES = KS * BM * 128;
+  static_assert(AL >= 1 && BM % RP == 0 && BM % EP == 0 && EL >= 1 && TM >= 1 && TN >= 1 && WM % 16 == 0 &&
+                WN % 16 == 0, "tile shape");
+  constexpr int W_BYTES = KS * WROWS * 128, A_BYTES = KS * BM * 128;
   // distinct LDS objects per buffer (the compiler's LDS-DMA alias tracking then sees that the
   // epilogue's reads of one buffer do not depend on the prefetch in flight into the other; the
   // double-buffer index is static: the tile loop is unrolled by two)
@@ -121,8 +123,9 @@ __global__ __launch_bounds__(64 * NW) void conv1x1_dgrad_stream_kernel(const Dgr
 #pragma unroll
     for (int i = 0; i < BL; ++i) {
       const int n = n0 + lrow + RP * i;
-      const char* src = n < a.Kout ? reinterpret_cast<const char*>(a.w + (int64_t)n * a.K + ks * 64 + 8 * jc) : zp;
-      dgs_glds(src, Ws + ks * BN * 128 + (RP * i + 8 * wid) * 128);
+      const char* src = (lrow + RP * i < BN && n < a.Kout)
+                            ? reinterpret_cast<const char*>(a.w + (int64_t)n * a.K + ks * 64 + 8 * jc) : zp;
+      dgs_glds(src, Ws + ks * WROWS * 128 + (RP * i + 8 * wid) * 128);
     }
   // rows past M re-read row M - 1 (outputs dropped, statistics masked): unconditional loads keep the
   // compiler's vmcnt scoreboard exact (32-bit offsets: host-checked)
@@ -194,7 +197,7 @@ __global__ __launch_bounds__(64 * NW) void conv1x1_dgrad_stream_kernel(const Dgr
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) {
       const char* A = Ac + ks * BM * 128;
-      const char* B = Ws + ks * BN * 128;
+      const char* B = Ws + ks * WROWS * 128;
 #pragma unroll
       for (int kk = 0; kk < 2; ++kk) {
         const int ch = kk * 4 + fg;
@@ -293,33 +296,26 @@ __global__ __launch_bounds__(64 * NW) void conv1x1_dgrad_stream_kernel(const Dgr
   __builtin_amdgcn_s_waitcnt(dgs_vmcnt(0));   // no LDS-DMA in flight when the block retires
 
   if constexpr (Z) {
-    __syncthreads();
-    // per-lane sums -> [NS][WGM * 16][BN] (the weight / operand tiles are free now) -> one row per block
-    constexpr int RED_BYTES = NS * WGM * 16 * BN * 4;
-    float* red = reinterpret_cast<float*>(RED_BYTES <= W_BYTES ? Ws : E0);
-    static_assert(RED_BYTES <= W_BYTES || RED_BYTES <= EB_BYTES, "statistics combine fits a free tile");
+    // per-lane sums -> [WGM * 16][BN] (one statistic at a time, in the now free weight tile) -> one
+    // row per block, summed in a fixed order
     constexpr int RR = WGM * 16;
+    static_assert(RR * BN * 4 <= W_BYTES, "statistics combine fits the weight tile");
+    float* red = reinterpret_cast<float*>(Ws);
+    float* st = a.stats + (int64_t)g * NS * a.Kout + n0 + tid;
 #pragma unroll
-    for (int ni = 0; ni < TN; ++ni)
+    for (int k = 0; k < NS; ++k) {
+      __syncthreads();
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int col = wn * WN + ni * 16 + 4 * fg + j;
-        red[(wm * 16 + fr) * BN + col] = s1[ni][j];
-        red[(RR + wm * 16 + fr) * BN + col] = s2[ni][j];
-        if constexpr (Z2) red[(2 * RR + wm * 16 + fr) * BN + col] = s3[ni][j];
+      for (int ni = 0; ni < TN; ++ni)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          red[(wm * 16 + fr) * BN + wn * WN + ni * 16 + 4 * fg + j] = k == 0 ? s1[ni][j] : (k == 1 ? s2[ni][j] : s3[ni][j]);
+      __syncthreads();
+      if (tid < BN && n0 + tid < a.Kout) {
+        float t = 0.f;
+        for (int q = 0; q < RR; ++q) t += red[q * BN + tid];
+        st[k * a.Kout] = t;
       }
-    __syncthreads();
-    if (tid < BN && n0 + tid < a.Kout) {
-      float t1 = 0.f, t2 = 0.f, t3 = 0.f;
-      for (int q = 0; q < RR; ++q) {
-        t1 += red[q * BN + tid];
-        t2 += red[(RR + q) * BN + tid];
-        if constexpr (Z2) t3 += red[(2 * RR + q) * BN + tid];
-      }
-      float* st = a.stats + (int64_t)g * NS * a.Kout + n0 + tid;
-      st[0] = t1;
-      st[a.Kout] = t2;
-      if constexpr (Z2) st[2 * a.Kout] = t3;
     }
   }
 }
@@ -351,7 +347,14 @@ extern "C" int dlmpi_dgrad_stream_plan(int64_t M, int K, int Kout, int mask_mode
   if (K == 512 && (has_res || z2 || mask_mode == 1)) return 0;   // 64-wide tiles: z (and z-mask) only
   // LDS per block (one block per CU): weights KS x BN x 128 B resident + A + 2 x epilogue operands
   if (K == 128 && Kout % 128 == 0) { *bm = 64; *bn = 128; }          // 98-146 KB
-  else if (K == 256 && Kout % 128 == 0) { *bm = 32; *bn = 128; }     // 106-133 KB
+  else if (K == 256 && Kout % 128 == 0) {   // 48 rows: 6 waves (3 x 2), 135-149 KB (DLMPI_DGS_K256_ROWS=32: 4 waves)
+    static const int rows = [] {
+      const char* e = getenv("DLMPI_DGS_K256_ROWS");
+      return e ? atoi(e) : 48;
+    }();
+    *bm = (z2 || rows == 32) ? 32 : 48;
+    *bn = 128;
+  }
   else if (K == 512 && Kout % 64 == 0) { *bm = 64; *bn = 64; }      // 8 waves: 136-144 KB
   else return 0;
   const int ntiles = Kout / *bn;
@@ -364,21 +367,32 @@ extern "C" int dlmpi_dgrad_stream_plan(int64_t M, int K, int Kout, int mask_mode
 
 extern "C" hipError_t dlmpi_conv1x1_dgrad_stream(const DgradStreamArgs* a, int bm, int bn, int mask_mode, hipStream_t s) {
   const dim3 grid((unsigned)(a->ntiles * a->G));
-#define DLMPI_DGS(BM_, BN_, KS_, NW_, ADB_)                                                                   \
+#define DLMPI_DGS(BM_, BN_, KS_, NW_, WGM_, ADB_)                                                                   \
   do {                                                                                                       \
     const dim3 blk(64 * NW_);                                                                                \
     if (a->z2) {                                                                                             \
-      if (mask_mode == 1) hipLaunchKernelGGL((conv1x1_dgrad_stream_kernel<BM_, BN_, KS_, NW_, 1, true, ADB_>), grid, blk, 0, s, *a); \
-      else hipLaunchKernelGGL((conv1x1_dgrad_stream_kernel<BM_, BN_, KS_, NW_, 2, true, ADB_>), grid, blk, 0, s, *a); \
-    } else if (mask_mode == 1) hipLaunchKernelGGL((conv1x1_dgrad_stream_kernel<BM_, BN_, KS_, NW_, 1, false, ADB_>), grid, blk, 0, s, *a); \
-    else if (mask_mode == 2) hipLaunchKernelGGL((conv1x1_dgrad_stream_kernel<BM_, BN_, KS_, NW_, 2, false, ADB_>), grid, blk, 0, s, *a); \
-    else hipLaunchKernelGGL((conv1x1_dgrad_stream_kernel<BM_, BN_, KS_, NW_, 0, false, ADB_>), grid, blk, 0, s, *a); \
+      if (mask_mode == 1) hipLaunchKernelGGL((conv1x1_dgrad_stream_kernel<BM_, BN_, KS_, NW_, WGM_, 1, true, ADB_>), grid, blk, 0, s, *a); \
+      else hipLaunchKernelGGL((conv1x1_dgrad_stream_kernel<BM_, BN_, KS_, NW_, WGM_, 2, true, ADB_>), grid, blk, 0, s, *a); \
+    } else if (mask_mode == 1) hipLaunchKernelGGL((conv1x1_dgrad_stream_kernel<BM_, BN_, KS_, NW_, WGM_, 1, false, ADB_>), grid, blk, 0, s, *a); \
+    else if (mask_mode == 2) hipLaunchKernelGGL((conv1x1_dgrad_stream_kernel<BM_, BN_, KS_, NW_, WGM_, 2, false, ADB_>), grid, blk, 0, s, *a); \
+    else hipLaunchKernelGGL((conv1x1_dgrad_stream_kernel<BM_, BN_, KS_, NW_, WGM_, 0, false, ADB_>), grid, blk, 0, s, *a); \
   } while (0)
-  if (bm == 64 && bn == 128 && a->K == 128) DLMPI_DGS(64, 128, 2, 8, false);
-  else if (bm == 32 && bn == 128 && a->K == 256) DLMPI_DGS(32, 128, 4, 4, false);
+  if (bm == 64 && bn == 128 && a->K == 128) DLMPI_DGS(64, 128, 2, 8, 2, false);
+  else if (bm == 48 && bn == 128 && a->K == 256 && !a->z2) {
+    if (mask_mode == 1) hipLaunchKernelGGL((conv1x1_dgrad_stream_kernel<48, 128, 4, 6, 3, 1, false, false>), grid, dim3(384), 0, s, *a);
+    else if (mask_mode == 2) hipLaunchKernelGGL((conv1x1_dgrad_stream_kernel<48, 128, 4, 6, 3, 2, false, false>), grid, dim3(384), 0, s, *a);
+    else hipLaunchKernelGGL((conv1x1_dgrad_stream_kernel<48, 128, 4, 6, 3, 0, false, false>), grid, dim3(384), 0, s, *a);
+  } else if (bm == 32 && bn == 128 && a->K == 256) {   // z2 (174 KB at 48 rows), or the 4-wave A/B variant
+    if (a->z2) {
+      if (mask_mode == 1) hipLaunchKernelGGL((conv1x1_dgrad_stream_kernel<32, 128, 4, 4, 2, 1, true, false>), grid, dim3(256), 0, s, *a);
+      else hipLaunchKernelGGL((conv1x1_dgrad_stream_kernel<32, 128, 4, 4, 2, 2, true, false>), grid, dim3(256), 0, s, *a);
+    } else if (mask_mode == 1) hipLaunchKernelGGL((conv1x1_dgrad_stream_kernel<32, 128, 4, 4, 2, 1, false, false>), grid, dim3(256), 0, s, *a);
+    else if (mask_mode == 2) hipLaunchKernelGGL((conv1x1_dgrad_stream_kernel<32, 128, 4, 4, 2, 2, false, false>), grid, dim3(256), 0, s, *a);
+    else hipLaunchKernelGGL((conv1x1_dgrad_stream_kernel<32, 128, 4, 4, 2, 0, false, false>), grid, dim3(256), 0, s, *a);
+  }
   else if (bm == 64 && bn == 64 && a->K == 512 && !a->z2 && !a->res) {   // z-mask / plain only
-    if (mask_mode == 2) hipLaunchKernelGGL((conv1x1_dgrad_stream_kernel<64, 64, 8, 8, 2, false, false>), grid, dim3(512), 0, s, *a);
-    else if (mask_mode == 0) hipLaunchKernelGGL((conv1x1_dgrad_stream_kernel<64, 64, 8, 8, 0, false, false>), grid, dim3(512), 0, s, *a);
+    if (mask_mode == 2) hipLaunchKernelGGL((conv1x1_dgrad_stream_kernel<64, 64, 8, 8, 2, 2, false, false>), grid, dim3(512), 0, s, *a);
+    else if (mask_mode == 0) hipLaunchKernelGGL((conv1x1_dgrad_stream_kernel<64, 64, 8, 8, 2, 0, false, false>), grid, dim3(512), 0, s, *a);
     else return hipErrorInvalidValue;
   }
   else return hipErrorInvalidValue;

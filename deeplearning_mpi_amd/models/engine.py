@@ -140,6 +140,11 @@ CHUNK_FWD = os.environ.get("DLMPI_CHUNK_FWD", "0") != "0"
 # apply's output is written once and never re-read by the consumer.
 FUSE_APPLY = os.environ.get("DLMPI_FUSE_APPLY", "1") != "0"
 
+# The step's last weight gradient (a unit with ``wgrad_main``: the ResNet stem, whose input needs no
+# gradient) runs on the main stream -- idle by then -- instead of queueing behind the side stream's
+# last weight gradients (profiles/r3_tail).  DLMPI_WGRAD_TAIL_MAIN=0: on the side stream like the rest.
+WGRAD_TAIL_MAIN = os.environ.get("DLMPI_WGRAD_TAIL_MAIN", "1") != "0"
+
 
 def img_rows(a, n0: int, n1: int):
     """Images [n0, n1) of an Act (a row range of its 2-D buffer, same ld / channel offset) or of a
@@ -220,6 +225,8 @@ class BwdFuse(NamedTuple):
 
 class ConvUnit:
     """conv2d / linear (+ training or folded-eval BatchNorm) (+ residual) (+ ReLU)."""
+
+    wgrad_main = False   # see WGRAD_TAIL_MAIN
 
     def __init__(self, arena: ParamArena, conv, bn=None, relu=True, cin_pad=None, need_dgrad=True):
         self.arena, self.conv, self.bn, self.relu = arena, conv, bn, relu
@@ -491,14 +498,26 @@ class ConvUnit:
             else:
                 dz = Act.empty(z.N, z.H, z.W, z.C, be.act_dtype, z.device)
                 be.bn_bwd(dy, mask, z, mean, invstd, gam, dgam, dbet, dz, dyr_out, pre=pre, k2=k2)
-            with grad_side(be, *bufs(dz, x)):
-                if bn.affine:
-                    ar.ready(bn.weight, bn.bias)
-                if self.bias is not None:
-                    # d(bias) of a conv followed by training-mode BN is exactly zero (BN removes the mean)
-                    ar.ready(self.bias)
+            if self.wgrad_main and WGRAD_TAIL_MAIN and not need_dx:
+                # the last weight gradient of the step (the stem): on the main stream, which has
+                # nothing left to do, beside the side stream's last weight gradients; the DDP
+                # announcements still go through the side stream (ordered after both)
                 self._wgrad(be, dz, x)
-                ar.ready(self.conv.weight)
+                with grad_side(be, *bufs(dz, x)):
+                    if bn.affine:
+                        ar.ready(bn.weight, bn.bias)
+                    if self.bias is not None:
+                        ar.ready(self.bias)
+                    ar.ready(self.conv.weight)
+            else:
+                with grad_side(be, *bufs(dz, x)):
+                    if bn.affine:
+                        ar.ready(bn.weight, bn.bias)
+                    if self.bias is not None:
+                        # d(bias) of a conv followed by training-mode BN is exactly zero (BN removes the mean)
+                        ar.ready(self.bias)
+                    self._wgrad(be, dz, x)
+                    ar.ready(self.conv.weight)
         else:
             x, y = ctx
             assert not self.relu, "ReLU without BN is not used by the engine models"

@@ -285,6 +285,7 @@ class ResNet(EngineModule):
             self.u_stem = S2DConvUnit(ar, self.conv1, self.bn1, relu=True)
         else:
             self.u_stem = ConvUnit(ar, self.conv1, self.bn1, relu=True, cin_pad=self.cin_pad, need_dgrad=False)
+        self.u_stem.wgrad_main = True   # the step's last weight gradient (engine.WGRAD_TAIL_MAIN)
         self.blocks = []
         for layer in (self.layer1, self.layer2, self.layer3, self.layer4):
             for b in layer:
