@@ -329,6 +329,15 @@ class ConvUnit:
         xp.done = True
         return stats, o
 
+    def can_fuse_apply(self, be, x, train: bool, save=True) -> bool:
+        """True if ``fwd`` computes the pending BN-apply ``x`` inside its GEMM's operand prologue
+        (FUSE_APPLY): a 1x1 / stride-1 conv with one output tile column behind a residual BN + ReLU."""
+        return (FUSE_APPLY and train and save and isinstance(x, PendingApply) and not x.done
+                and self.bn is not None and self.R == 1 and self.S == 1 and self.stride == 1 and self.pad == 0
+                and self.Kp <= 128 and x.relu and x.res is not None and x.mbits is not None
+                and x.C == self.Cp and hasattr(be, "conv_fwd_bn_apply") and not getattr(be, "f32", False)
+                and not self._chunkable(be, x))
+
     def fwd(self, be, x, train: bool, res: Act = None, out: Act = None, save=True, defer_apply=False,
             before_res=None, lazy=False):
         """Returns (output, saved context).  x: an Act or a Deferred operand (rebuilt by the GEMM's
@@ -341,10 +350,7 @@ class ConvUnit:
         output is never materialised.  lazy (training BN, not deferred): return a PendingApply instead
         of running the BN-apply -- for a consumer that runs it chunk-wise beside its own GEMM."""
         chunked = train and self._chunkable(be, x)
-        fuse_apply = (FUSE_APPLY and train and save and not chunked and isinstance(x, PendingApply) and not x.done
-                      and self.bn is not None and self.R == 1 and self.S == 1 and self.stride == 1 and self.pad == 0
-                      and self.Kp <= 128 and x.relu and x.res is not None and x.mbits is not None
-                      and x.C == self.Cp and hasattr(be, "conv_fwd_bn_apply") and not getattr(be, "f32", False))
+        fuse_apply = not chunked and self.can_fuse_apply(be, x, train, save)
         if isinstance(x, PendingApply) and not chunked and not fuse_apply:
             x = x.resolve(be)
         assert x.C == self.Cp, (x, self.Cp)

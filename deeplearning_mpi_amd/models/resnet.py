@@ -95,6 +95,14 @@ _LATE_JOIN = os.environ.get("DLMPI_LATE_JOIN", "1") != "0"
 # it inside the block's last BN-apply (A/B knob; backends without the fused residual ignore it)
 _DS_FUSE = os.environ.get("DLMPI_DS_FUSE", "1") != "0"
 
+# DLMPI_DS_AFTER_CONV1=1: a downsample block whose input is a pending residual BN-apply that conv1
+# can fuse (engine.FUSE_APPLY: ResNet-50 layer2.0) lets conv1 compute and store the input and starts
+# the branch (1x1 stride-2 conv + BN) after it, beside conv2, instead of a standalone apply pass
+# before both.  Off by default: measured slower (profiles/r3_ds_after_conv1_rejected: ResNet-50
+# 12,812 / 12,961 vs 12,941 / 13,045 img/s -- the branch no longer overlaps conv1, and the fused
+# 256 -> 128 conv1 at 56^2 costs about what the apply pass did).
+_DS_AFTER_CONV1 = os.environ.get("DLMPI_DS_AFTER_CONV1", "0") != "0"
+
 
 class _BlockExec:
     """Forward/backward schedule of one residual block (basic or bottleneck)."""
@@ -109,22 +117,38 @@ class _BlockExec:
         convolution rebuilds them in its operand prologue (ops.act.Deferred)."""
         ctxs = []
         lazy = train and save and not defer   # BN-applies run chunk-wise inside their consumer (PendingApply)
-        if self.ud is not None:   # the branch reads the whole block input
+        # the block input is still a pending BN-apply that conv1 can compute in its operand prologue
+        # (engine.FUSE_APPLY): with a downsample branch, the branch starts after conv1 has stored it
+        # instead of a standalone apply pass before both (_DS_AFTER_CONV1)
+        ds_late = (self.ud is not None and _DS_AFTER_CONV1 and self.u[0].can_fuse_apply(be, x, train, save))
+        if self.ud is not None and not ds_late:   # the branch reads the whole block input
             x = resolve(be, x)
         # the downsample BN output is read once, as the residual of the last unit's BN-apply: applied
         # there on the fly (Deferred.bn), which removes its own apply pass (read z_ds + write idn)
         ds_defer = "bn" if (_DS_FUSE and train and save) else False
         br = getattr(be, "branch_stream", None) if self.ud is not None else None
-        if br is not None:
-            main = torch.cuda.current_stream()
-            br.wait_stream(main)
-            with torch.cuda.stream(br):
-                idn, cd = self.ud.fwd(be, x, train, save=save, defer_apply=ds_defer)
-            record_on(br, x)
+        main = torch.cuda.current_stream() if br is not None else None
+        xin = x
+
+        def branch_fwd(xb):
+            if br is not None:
+                br.wait_stream(main)
+                with torch.cuda.stream(br):
+                    out = self.ud.fwd(be, xb, train, save=save, defer_apply=ds_defer)
+                record_on(br, xb)
+                return out
+            return self.ud.fwd(be, xb, train, save=save, defer_apply=ds_defer)
+
+        if br is not None and not ds_late:
+            idn, cd = branch_fwd(x)
         h = x
         for k, u in enumerate(self.u[:-1]):
             h, c = u.fwd(be, h, train, save=save, defer_apply="act" if defer else False, lazy=lazy)
             ctxs.append(c)
+            if k == 0 and ds_late:
+                xin = resolve(be, x)   # computed and stored by conv1's prologue
+                if br is not None:
+                    idn, cd = branch_fwd(xin)
         join = None
         if br is not None:
             def join():   # the residual is first read by the last unit's BN-apply, after its GEMM
@@ -134,7 +158,7 @@ class _BlockExec:
                 join()
                 join = None
         elif self.ud is not None:
-            idn, cd = self.ud.fwd(be, x, train, save=save, defer_apply=ds_defer)
+            idn, cd = self.ud.fwd(be, xin if ds_late else x, train, save=save, defer_apply=ds_defer)
         else:   # identity: the block input, complete once conv1 has consumed it
             idn, cd = resolve(be, x), None
         y, c = self.u[-1].fwd(be, h, train, res=idn, save=save, before_res=join, lazy=lazy)

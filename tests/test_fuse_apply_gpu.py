@@ -5,7 +5,8 @@ consumes it and stores it (plus ReLU mask bits) instead of a separate BN-apply p
 * kernel level: y and its mask bits bit-identical to bn_apply's, the conv output bit-identical to the
   conv over the stored y, BN statistics / finalize equal to fp32 summation-order noise -- with a
   plain and with a BatchNorm-output (downsample) residual;
-* model level: a ResNet-50 training step with the fusion on vs off."""
+* model level: the number of fused calls in a ResNet-50 step, the loss vs the unfused step, and the
+  fused step against the fp64 oracle."""
 import copy
 
 import pytest
@@ -107,7 +108,19 @@ def test_resnet50_step_fused_apply_vs_unfused(monkeypatch):
         calls[on] = n[0]
         del be
     torch.cuda.synchronize()
-    assert calls[True] == 5   # layer1.1, layer1.2, layer2.1..3 (conv1 of <= 128 channels, identity blocks)
-    assert _rel(losses[0], losses[1]) < 2e-3
-    g1, g2 = m1.arena.grad, m2.arena.grad
-    assert ((g1 - g2).norm() / g2.norm()).item() < 3e-2
+    # layer1.1, layer1.2, layer2.1..3 (conv1 of <= 128 channels, identity blocks); + layer2.0 with
+    # resnet._DS_AFTER_CONV1 (its downsample branch then starts after conv1 has stored the input)
+    from deeplearning_mpi_amd.models import resnet as rn
+
+    assert calls[True] == (6 if rn._DS_AFTER_CONV1 else 5)
+    # a fused conv1 may pick another M tile than the unfused conv (operand-prologue tile rules; e.g.
+    # layer2.0's with _DS_AFTER_CONV1), i.e. another fp32 order of its BN statistics.  A random-init bf16
+    # ResNet-50 is chaotic under such perturbations: switching ONLY the statistics summation order
+    # (streaming vs general 1x1 forward kernel, all fusions off) moves the loss by 0.7 % and the
+    # gradient by 95 % (scripts/diag/chaos_check.py), so the fused step is judged against the fp64
+    # oracle like any engine step (tests/test_models_gpu.py), not against the unfused bf16 step.
+    assert _rel(losses[0], losses[1]) < 1e-2
+    from test_models_gpu import _compare
+
+    monkeypatch.setattr(engine, "FUSE_APPLY", True)
+    _compare(lambda: resnet50(num_classes=10), x, y, cross_entropy, torch.nn.functional.cross_entropy)
