@@ -18,6 +18,8 @@ CASES = [
     ("layer2.0 conv1 dual (2x128 -> 256)", 256, 56, 56, 256, 256, True, "bits", True),
     ("layer2 conv1 dual (2x128 -> 512)", 256, 28, 28, 256, 512, True, "bits", True),
     ("layer3 conv1 (256 -> 1024)", 256, 14, 14, 256, 1024, True, "bits", False),
+    ("layer3.0 conv1 dual (2x256 -> 512)", 256, 28, 28, 512, 512, True, "bits", True),
+    ("layer4 conv1 (512 -> 2048)", 256, 7, 7, 512, 2048, True, "bits", False),
     ("layer1 conv1 no-res (2x64 -> 256), z-mask", 256, 56, 56, 128, 256, False, "z", True),
     ("layer1 conv3 dual (2x256 -> 64), z-mask", 256, 56, 56, 512, 64, False, "z", True),
 ]

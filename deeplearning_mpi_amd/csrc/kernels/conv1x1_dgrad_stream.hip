@@ -66,9 +66,8 @@ template <int BM, int BN, int KS, int NW, int WGM, int MASK, bool Z2, bool ADB>
 __global__ __launch_bounds__(64 * NW) void conv1x1_dgrad_stream_kernel(const DgradStreamArgs a) {
   constexpr bool Z = MASK != 0;
   static_assert(!Z2 || Z, "z2 needs the fused statistics");
-  static_assert(MASK != 1 || BN == 128, "mask bits: 128-channel tiles (one 16-byte piece per row)");
   static_assert(BN == 64 || BN == 128, "tile width");
-  constexpr bool RES = BN == 128;               // residual-gradient operand (64-wide tiles: none)
+  constexpr bool RES = !(BN == 64 && BM == 64);  // residual-gradient operand (64 x 64 tiles: none, LDS)
   constexpr int NS = Z2 ? 3 : 2;
   constexpr int NT = 64 * NW;
   constexpr int WGN = NW / WGM;                 // wave grid
@@ -81,7 +80,11 @@ __global__ __launch_bounds__(64 * NW) void conv1x1_dgrad_stream_kernel(const Dgr
   constexpr int EP = NT / ECH;                  // epilogue-tile rows staged per pass
   constexpr int EL = BM / EP;
   constexpr int NSTORE = BM / EP;               // 16-byte output row stores per thread per tile
-  constexpr int MB_ROWS = BM > 64 ? BM : 64;    // mask-bit tile: one wave instruction (16 B / row)
+  // mask-bit tile: BN / 8 bytes per row, staged with 16-byte (BN 128) or 4-byte (BN 64) pieces, in
+  // whole wave instructions (64 rows / 32 rows each)
+  constexpr int MBR = BN / 8, MB_PIECE = BN == 128 ? 16 : 4, MB_WROWS = 64 * MB_PIECE / MBR;
+  constexpr int MB_INSTR = (BM + MB_WROWS - 1) / MB_WROWS, MB_ROWS = MB_INSTR * MB_WROWS;
+  static_assert(MB_INSTR <= NW, "mask-bit staging: one instruction per wave");
   constexpr int E_BYTES = BM * ERB;
   static_assert(AL >= 1 && BM % RP == 0 && BM % EP == 0 && EL >= 1 && TM >= 1 && TN >= 1 && WM % 16 == 0 &&
                 WN % 16 == 0, "tile shape");
@@ -97,7 +100,7 @@ __global__ __launch_bounds__(64 * NW) void conv1x1_dgrad_stream_kernel(const Dgr
   // With statistics the output tile is staged in place of the consumed z tile (each lane writes
   // exactly the positions it has read); without, in a tile of its own.
   constexpr int EZ_OFF = RES ? E_BYTES : 0, EZ2_OFF = EZ_OFF + (Z ? E_BYTES : 0), EM_OFF = EZ2_OFF + (Z2 ? E_BYTES : 0);
-  constexpr int EB_BYTES0 = EM_OFF + (MASK == 1 ? MB_ROWS * 16 : 0);
+  constexpr int EB_BYTES0 = EM_OFF + (MASK == 1 ? MB_ROWS * MBR : 0);
   constexpr int EB_BYTES = EB_BYTES0 > 16 ? EB_BYTES0 : 16;
   __shared__ __attribute__((aligned(16))) char E0[EB_BYTES];
   __shared__ __attribute__((aligned(16))) char E1[EB_BYTES];
@@ -153,9 +156,13 @@ __global__ __launch_bounds__(64 * NW) void conv1x1_dgrad_stream_kernel(const Dgr
         dgs_glds(a.z2 + (uint32_t)(m * a.ldz2 + a.z2off + n0 + gj * 8), Zb + (EZ2_OFF - EZ_OFF) + i * EP * ERB + wid * 1024);
     }
     if constexpr (MASK == 1) {
-      if (wid == 0) {   // one 16-B piece (128 mask bits) per row
-        const int m = min(mt * BM + lane, a.M - 1);
-        dgs_glds(a.mbits + (uint32_t)(m * (a.Kout >> 3) + (n0 >> 3)), Mb);
+      if (wid < MB_INSTR) {   // wave w: rows [w MB_WROWS, (w + 1) MB_WROWS) of the mask-bit tile
+        const int piece = wid * 64 + lane;                     // MB_PIECE-byte piece of the tile
+        const int r = piece * MB_PIECE / MBR;
+        const int m = min(mt * BM + r, a.M - 1);
+        const uint8_t* src = a.mbits + (uint32_t)(m * (a.Kout >> 3) + (n0 >> 3) + (piece * MB_PIECE) % MBR);
+        if constexpr (MB_PIECE == 16) __builtin_amdgcn_global_load_lds(src, (dgs_lds_void*)(Mb + wid * 1024), 16, 0, 0);
+        else __builtin_amdgcn_global_load_lds(src, (dgs_lds_void*)(Mb + wid * 256), 4, 0, 0);
       }
     }
   };
@@ -244,7 +251,7 @@ __global__ __launch_bounds__(64 * NW) void conv1x1_dgrad_stream_kernel(const Dgr
           const f32x4 zz{__uint_as_float(q[0] << 16), __uint_as_float(q[0] & 0xffff0000u), __uint_as_float(q[1] << 16),
                          __uint_as_float(q[1] & 0xffff0000u)};
           if constexpr (MASK == 1) {
-            const uint32_t b = (uint32_t)(uint8_t)Mc[row * 16 + (col >> 3)] >> (col & 4);
+            const uint32_t b = (uint32_t)(uint8_t)Mc[row * MBR + (col >> 3)] >> (col & 4);
 #pragma unroll
             for (int j = 0; j < 4; ++j) v[j] = (b >> j) & 1u ? v[j] : 0.f;
           } else {   // same fma as the forward BN-apply -> same sign as its output
@@ -324,7 +331,8 @@ __global__ __launch_bounds__(64 * NW) void conv1x1_dgrad_stream_kernel(const Dgr
 
 using namespace dlmpi;
 
-// DLMPI_DGRAD_STREAM=0 disables the kernel (A/B); set_dgrad_stream(0|1) overrides (tests)
+// DLMPI_DGRAD_STREAM=0 disables the kernel (A/B); set_dgrad_stream(0|1) overrides (tests; 2: also the
+// opt-in tile variants)
 static int g_dgs_override = -1;
 extern "C" void dlmpi_set_dgrad_stream(int mode) { g_dgs_override = mode; }
 
@@ -344,7 +352,6 @@ extern "C" int dlmpi_dgrad_stream_plan(int64_t M, int K, int Kout, int mask_mode
   }();
   const int on = g_dgs_override >= 0 ? g_dgs_override : env;
   if (!on || M <= 0 || mask_mode < 0 || mask_mode > 2 || (z2 && mask_mode == 0)) return 0;
-  if (K == 512 && (has_res || z2 || mask_mode == 1)) return 0;   // 64-wide tiles: z (and z-mask) only
   // LDS per block (one block per CU): weights KS x BN x 128 B resident + A + 2 x epilogue operands
   if (K == 128 && Kout % 128 == 0) { *bm = 64; *bn = 128; }          // 98-146 KB
   else if (K == 256 && Kout % 128 == 0) {   // 48 rows: 6 waves (3 x 2), 135-149 KB (DLMPI_DGS_K256_ROWS=32: 4 waves)
@@ -355,7 +362,20 @@ extern "C" int dlmpi_dgrad_stream_plan(int64_t M, int K, int Kout, int mask_mode
     *bm = (z2 || rows == 32) ? 32 : 48;
     *bn = 128;
   }
-  else if (K == 512 && Kout % 64 == 0) { *bm = 64; *bn = 64; }      // 8 waves: 136-144 KB
+  else if (K == 512 && Kout % 64 == 0) {
+    // 64 x 64 tiles, 8 waves (136-144 KB) for the z-mask-only dual conv3 gradient; with a residual /
+    // mask bits / z2: 32 x 64, 4 waves (113-121 KB)
+    *bn = 64;
+    *bm = (has_res || z2 || mask_mode == 1) ? 32 : 64;
+    // 32 x 64 tiles measured slower than the general kernel (layer3.0 conv1 dual 2x256 -> 512: 359 vs
+    // 289 us; layer4 conv1 77 vs 69 us -- eight 64-wide columns re-read A, 4 waves per CU; ResNet-50
+    // 12,802 / 12,803 vs 12,837 / 12,968 img/s, profiles/r3_dgrad_stream/v4): opt-in DLMPI_DGS_K512=1
+    static const bool k512 = [] {
+      const char* e = getenv("DLMPI_DGS_K512");
+      return e && atoi(e) != 0;
+    }();
+    if (!k512 && g_dgs_override != 2 && *bm == 32) return 0;
+  }
   else return 0;
   const int ntiles = Kout / *bn;
   const int64_t mtiles = (M + *bm - 1) / *bm;
@@ -390,6 +410,7 @@ extern "C" hipError_t dlmpi_conv1x1_dgrad_stream(const DgradStreamArgs* a, int b
     else if (mask_mode == 2) hipLaunchKernelGGL((conv1x1_dgrad_stream_kernel<32, 128, 4, 4, 2, 2, false, false>), grid, dim3(256), 0, s, *a);
     else hipLaunchKernelGGL((conv1x1_dgrad_stream_kernel<32, 128, 4, 4, 2, 0, false, false>), grid, dim3(256), 0, s, *a);
   }
+  else if (bm == 32 && bn == 64 && a->K == 512) DLMPI_DGS(32, 64, 8, 4, 2, false);
   else if (bm == 64 && bn == 64 && a->K == 512 && !a->z2 && !a->res) {   // z-mask / plain only
     if (mask_mode == 2) hipLaunchKernelGGL((conv1x1_dgrad_stream_kernel<64, 64, 8, 8, 2, 2, false, false>), grid, dim3(512), 0, s, *a);
     else if (mask_mode == 0) hipLaunchKernelGGL((conv1x1_dgrad_stream_kernel<64, 64, 8, 8, 2, 0, false, false>), grid, dim3(512), 0, s, *a);

@@ -22,8 +22,9 @@ SHAPES = [
     (3, 5, 7, 128, 128),       # 105 rows, one 128-channel column
     (8, 28, 28, 256, 512),
     (32, 56, 56, 128, 256),    # layer-1 scale (100k rows, every block walks many tiles)
-    (4, 14, 14, 512, 64),      # long reduction into 64-channel tiles (z-mask / plain only)
+    (4, 14, 14, 512, 64),      # long reduction into 64-channel tiles
     (2, 28, 28, 512, 128),
+    (2, 14, 14, 512, 512),     # layer-3.0 conv1 dual / layer-4 conv1 widths
 ]
 
 
@@ -77,10 +78,10 @@ def test_dgrad_stream_matches_general_kernel(shape, mode):
         fuse = BwdFuse(None, z, z2, sc, sh)
         keep = torch.addcmul(sh, z.buf.float(), sc) > 0
     for layout in ("dense", "dual"):
-        dx1, p1, ran1 = _run(nb, 1, dy, wT, C, res, fuse, layout, bias)
+        # mode 2: also the opt-in variants (K = 512 with a residual / mask bits / z2 on 32 x 64 tiles)
+        dx1, p1, ran1 = _run(nb, 2, dy, wT, C, res, fuse, layout, bias)
         dx0, p0, ran0 = _run(nb, 0, dy, wT, C, res, fuse, layout, bias)
-        supported = K != 512 or mode in ("from_z", "plain")
-        assert ran1 == int(supported) and ran0 == 0
+        assert ran1 == 1 and ran0 == 0
         if K <= 256:
             assert torch.equal(dx1.buf, dx0.buf), (layout, _rel(dx1.buf, dx0.buf))
         else:   # the general kernel may split the 8 K-steps of a small grid (split-K): another fp32 order
@@ -97,10 +98,12 @@ def test_dgrad_stream_matches_general_kernel(shape, mode):
         v = d.double()
         ref = [v.sum(0), (v * z.buf.double()).sum(0)] + ([(v * z2.buf.double()).sum(0)] if z2 is not None else [])
         s1, s0 = p1.double().sum(0), p0.double().sum(0)
-        for k, r in enumerate(ref):
+        v0 = dx0.buf[:, :C].double()   # K > 256: the general kernel's own dx (another fp32 order)
+        ref0 = [v0.sum(0), (v0 * z.buf.double()).sum(0)] + ([(v0 * z2.buf.double()).sum(0)] if z2 is not None else [])
+        for k, (r, r0) in enumerate(zip(ref, ref0)):
             scale = r.abs().max().clamp_min(1e-3)
             assert ((s1[k] - r).abs().max() / scale).item() < 1e-4, (k, layout)
-            assert ((s1[k] - s0[k]).abs().max() / scale).item() < 1e-4, (k, layout)
+            assert ((s0[k] - r0).abs().max() / scale).item() < 1e-4, (k, layout)
 
 
 def test_dgrad_stream_dual_bottleneck_bit_identical():

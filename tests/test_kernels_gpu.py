@@ -762,6 +762,7 @@ def _static_kernels(on: bool):
     C.set_conv_autotune(0 if on else -1)
     C.set_conv_halo(0 if on else -1)    # 3x3 halo tiles sum chunk-major (no prologue variant)
     C.set_wgrad3(0 if on else -1)       # 3x3 spatial-tile weight gradient (no prologue variant)
+    C.set_dgrad_stream(0 if on else -1)  # streaming 1x1 data gradient (no prologue variant)
 
 
 def _deferred_pair(N, H, W, C):
