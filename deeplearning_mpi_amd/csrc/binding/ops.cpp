@@ -641,8 +641,8 @@ static int conv2d_fwd_impl(const at::Tensor& x, int N, int H, int W, int C, int 
     }
   }
   a.ntiles = ceil_div(K, bn);
-  if (pro == 3 && (a.ntiles != 1 || R != 1 || S != 1 || stride != 1 || pad != 0))
-    throw std::runtime_error("conv prologue 3: a 1x1 / stride-1 conv with one output tile column");
+  if (pro == 3 && (R != 1 || S != 1 || stride != 1 || pad != 0))
+    throw std::runtime_error("conv prologue 3: a 1x1 / stride-1 conv");
   a.nphase = 1;
   ConvPhase& p = a.ph[0];
   p.P = P; p.Q = Q; p.Tr = R; p.Ts = S;

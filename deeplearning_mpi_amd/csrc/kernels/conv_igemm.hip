@@ -354,15 +354,17 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(STAGES 
           for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e] + r[e], 0.f);
           const u32x4 pk = pack8(v);
           *pa = pk;
-          const int64_t px = a_pix[i];   // 1x1 / stride 1 (host-checked): input pixel = tile row
-          *reinterpret_cast<u32x4*>(a.py + px * a.ldpy + a.pyoff + c) = pk;
-          uint32_t b = 0;
+          if (nt == 0) {   // with several output tile columns every column's blocks rebuild y; one stores it
+            const int64_t px = a_pix[i];   // 1x1 / stride 1 (host-checked): input pixel = tile row
+            *reinterpret_cast<u32x4*>(a.py + px * a.ldpy + a.pyoff + c) = pk;
+            uint32_t b = 0;
 #pragma unroll
-          for (int k = 0; k < 4; ++k) {
-            b |= (uint32_t)((pk[k] & 0xffffu) != 0u && !(pk[k] & 0x8000u)) << (2 * k);
-            b |= (uint32_t)((pk[k] >> 16) != 0u && !(pk[k] & 0x80000000u)) << (2 * k + 1);
+            for (int k = 0; k < 4; ++k) {
+              b |= (uint32_t)((pk[k] & 0xffffu) != 0u && !(pk[k] & 0x8000u)) << (2 * k);
+              b |= (uint32_t)((pk[k] >> 16) != 0u && !(pk[k] & 0x80000000u)) << (2 * k + 1);
+            }
+            a.pmbits[px * (C >> 3) + (c >> 3)] = (uint8_t)b;
           }
-          a.pmbits[px * (C >> 3) + (c >> 3)] = (uint8_t)b;
           continue;
         } else {
           float zv[8];

@@ -133,12 +133,18 @@ DUAL_WGRAD_PRO = os.environ.get("DLMPI_DUAL_WGRAD_PRO", "1") != "0"
 CHUNK_FWD = os.environ.get("DLMPI_CHUNK_FWD", "0") != "0"
 
 # DLMPI_FUSE_APPLY=0: run every residual block's BN-apply (+ residual + ReLU) as its own pass.  By
-# default a block output whose first consumer is a 1x1 / stride-1 convolution with ONE output tile
-# column (the next bottleneck's conv1 for <= 128 output channels: ResNet-50 layer1 / layer2) is left
+# default a block output whose first consumer is a 1x1 / stride-1 convolution (the next bottleneck's
+# conv1, up to FUSE_APPLY_MAX_K output channels: ResNet-50 layer1 / layer2) is left
 # pending (PendingApply) and computed by that convolution's operand prologue, which also stores it
 # and its ReLU mask bits (backend conv_fwd_bn_apply): no element is transformed twice, and the
 # apply's output is written once and never re-read by the consumer.
 FUSE_APPLY = os.environ.get("DLMPI_FUSE_APPLY", "1") != "0"
+# ... for consumers of up to this many output channels.  With several output tile columns the blocks
+# of every column rebuild y in their prologue (only the first column's store it): correct, but
+# measured slower at 256 (layer-3 conv1: ResNet-50 12,730-12,746 vs 12,889-12,916 img/s, ResNet-152
+# 4,539-4,541 vs 4,657-4,663; profiles/r3_fuse_apply_2col_rejected) -- the per-K-step prologue of a
+# 16-K-step GEMM, repeated per column, costs more than the apply pass it removes.
+FUSE_APPLY_MAX_K = int(os.environ.get("DLMPI_FUSE_APPLY_MAXK", "128"))
 
 # The step's last weight gradient (a unit with ``wgrad_main``: the ResNet stem, whose input needs no
 # gradient) runs on the main stream -- idle by then -- instead of queueing behind the side stream's
@@ -331,10 +337,10 @@ class ConvUnit:
 
     def can_fuse_apply(self, be, x, train: bool, save=True) -> bool:
         """True if ``fwd`` computes the pending BN-apply ``x`` inside its GEMM's operand prologue
-        (FUSE_APPLY): a 1x1 / stride-1 conv with one output tile column behind a residual BN + ReLU."""
+        (FUSE_APPLY): a 1x1 / stride-1 conv of <= FUSE_APPLY_MAX_K outputs behind a residual BN + ReLU."""
         return (FUSE_APPLY and train and save and isinstance(x, PendingApply) and not x.done
                 and self.bn is not None and self.R == 1 and self.S == 1 and self.stride == 1 and self.pad == 0
-                and self.Kp <= 128 and x.relu and x.res is not None and x.mbits is not None
+                and self.Kp <= FUSE_APPLY_MAX_K and x.relu and x.res is not None and x.mbits is not None
                 and x.C == self.Cp and hasattr(be, "conv_fwd_bn_apply") and not getattr(be, "f32", False)
                 and not self._chunkable(be, x))
 
