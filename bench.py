@@ -252,16 +252,22 @@ def main():
         import io
         import pstats
 
+        from deeplearning_mpi_amd.models import engine as _eng
+
         sync()
-        pr = cProfile.Profile()
+        pr, prb = cProfile.Profile(), cProfile.Profile()
+        _eng.BWD_PROFILER = prb   # the engine backward runs on autograd's worker thread
         pr.enable()
         for _ in range(args.pyprof):
             step()
         pr.disable()
+        _eng.BWD_PROFILER = None
         sync()
-        buf = io.StringIO()
-        pstats.Stats(pr, stream=buf).sort_stats("tottime").print_stats(45)
-        print(f"[pyprof] {args.pyprof} steps, self time per function\n" + buf.getvalue(), file=sys.stderr, flush=True)
+        for name, p_ in (("step (calling thread)", pr), ("engine backward (autograd thread)", prb)):
+            buf = io.StringIO()
+            pstats.Stats(p_, stream=buf).sort_stats("tottime").print_stats(40)
+            print(f"[pyprof] {args.pyprof} steps, {name}, self time per function\n" + buf.getvalue(),
+                  file=sys.stderr, flush=True)
     host_info = None
     if args.host_time > 0 and dev.type == "cuda":
         # host issue time of one step: the CPU time from calling step() to its return, each step

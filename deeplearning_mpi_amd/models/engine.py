@@ -55,9 +55,16 @@ def grad_side(be, *tensors):
     if side is None:
         yield
         return
-    side.wait_stream(torch.cuda.current_stream())
-    with torch.cuda.stream(side):
+    # set_stream instead of the torch.cuda.stream() context manager: this runs ~300 times per
+    # ResNet-152 backward, and the context manager's device bookkeeping cost ~18 us of host time each
+    # (bench.py --pyprof, profiles/r3_host)
+    cur = torch.cuda.current_stream()
+    side.wait_stream(cur)
+    torch.cuda.set_stream(side)
+    try:
         yield
+    finally:
+        torch.cuda.set_stream(cur)
     if _STREAM_HOLD:
         be.held.extend(t for t in tensors if t is not None)
         return
@@ -732,7 +739,12 @@ class _EngineFn(torch.autograd.Function):
         if ctx.aux_on is not None:
             mod._be.aux_on = ctx.aux_on
         with trace_range(f"dlmpi.backward[{type(mod).__name__}]"):
+            prof = BWD_PROFILER   # bench.py --pyprof: the backward runs on autograd's worker thread
+            if prof is not None:
+                prof.enable()
             mod._engine_backward(state, gout)
+            if prof is not None:
+                prof.disable()
             side = getattr(mod._be, "side_stream", None)
             if side is not None:   # every parameter gradient is final before the optimizer runs
                 torch.cuda.current_stream().wait_stream(side)
@@ -742,6 +754,10 @@ class _EngineFn(torch.autograd.Function):
         with trace_range("dlmpi.ddp_finalize"):
             mod._arena.end_backward()
         return None, None, None
+
+
+# a cProfile.Profile enabled around every engine backward (bench.py --pyprof), else None
+BWD_PROFILER = None
 
 
 class EngineModule(nn.Module):

@@ -149,10 +149,17 @@ class ParamArena:
         i = self.index.get(id(p))
         if i is None:
             return False
-        return p.data.data_ptr() == self.flat.data_ptr() + self.flat.element_size() * self.offsets[i]
+        return p.data_ptr() == self.flat.data_ptr() + self.flat.element_size() * self.offsets[i]
 
     def valid(self) -> bool:
-        return all(self.owns(p) for p in self.params)
+        """Every parameter still views its arena slot (called every step by the engine and the
+        optimizers: one data_ptr comparison per parameter against addresses computed once)."""
+        base = self.flat.data_ptr()
+        exp = getattr(self, "_expect", None)
+        if exp is None or exp[0] != base:
+            es = self.flat.element_size()
+            exp = self._expect = (base, [base + es * o for o in self.offsets])
+        return all(p.data_ptr() == e for p, e in zip(self.params, exp[1]))
 
     def param_flat(self, p) -> torch.Tensor:
         i = self.index[id(p)]
