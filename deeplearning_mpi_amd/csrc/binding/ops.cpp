@@ -449,8 +449,17 @@ static int g_dgrad_stream_ran = 0;   // 1 if the last conv2d_dgrad ran the strea
 
 static bool stream1x1_shape(int64_t M, int C, int K, int R, int S, int stride, int pad, int pro, int f32, int& bm,
                             int& bn, int& G) {
-  if (R != 1 || S != 1 || stride != 1 || pad != 0 || pro != 0 || f32) return false;
-  return dlmpi_stream1x1_plan(M, C, K, &bm, &bn, &G) != 0;
+  if (R != 1 || S != 1 || stride != 1 || pad != 0 || pro > 1 || f32) return false;
+  if (!dlmpi_stream1x1_plan(M, C, K, &bm, &bn, &G)) return false;
+  // pro 1 (a deferred BN-apply + ReLU operand): plans with few output columns only
+  return pro == 0 || dlmpi_stream1x1_pro_ok(K / bn);
+}
+
+// The streaming kernel would run this 1x1 conv with a deferred BN-apply operand (engine: whether the
+// producer may skip its apply pass)
+bool conv_stream_pro_ok(int64_t M, int C, int K) {
+  int bm, bn, G;
+  return stream1x1_shape(M, C, K, 1, 1, 1, 0, 1, 0, bm, bn, G);
 }
 
 
@@ -626,6 +635,10 @@ static int conv2d_fwd_impl(const at::Tensor& x, int N, int H, int W, int C, int 
         sa.bias = a.bias;
         sa.stats = a.stats;
         sa.G = G; sa.ntiles = K / sbn; sa.mtiles = ceil_div(M, sbm);
+        if (pro == 1) {
+          sa.pscale = a.pscale;
+          sa.pshift = a.pshift;
+        }
         if (a.stats && stats->size(0) < G) throw std::runtime_error("conv2d_fwd: stats buffer too small");
         check(dlmpi_conv1x1_stream(&sa, sbm, sbn, cur_stream()), "conv2d_fwd (stream 1x1)");
         g_stream_ran = 1;
@@ -1503,6 +1516,7 @@ void register_ops(pybind11::module& m) {
   m.def("set_conv_repi", [](int mode) { dlmpi_set_conv_repi(mode); });
   m.def("set_conv_stream", [](int mode) { dlmpi_set_conv_stream(mode); });
   m.def("conv_stream_last", []() { return g_stream_ran; });
+  m.def("conv_stream_pro_ok", &conv_stream_pro_ok);
   m.def("set_dgrad_stream", [](int mode) { dlmpi_set_dgrad_stream(mode); });
   m.def("dgrad_stream_last", []() { return g_dgrad_stream_ran; });
   m.def("set_conv_autotune", [](int mode) { g_autotune_override = mode; });

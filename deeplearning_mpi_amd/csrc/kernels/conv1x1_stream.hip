@@ -42,7 +42,10 @@ constexpr int vmcnt_imm(int n) { return (n & 15) | 0x70 | 0xF00 | ((n >> 4) << 1
 
 __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
-template <int BM, int BN, int KS, bool STATS>
+// PRO: the activations are a deferred BN-apply + ReLU (the producer's output never stored): every
+// thread rewrites the pieces it fetched, in LDS, as relu(x * pscale[c] + pshift[c]) (the fma order
+// of bn_apply_kernel: bit-identical to the stored schedule) once they have landed, before the MFMAs.
+template <int BM, int BN, int KS, bool STATS, bool PRO = false>
 __global__ __launch_bounds__(256) void conv1x1_stream_kernel(const Stream1x1Args a) {
   constexpr int NT = 256;
   constexpr int WM = BM / 2, WN = BN / 2;       // 2 x 2 waves
@@ -113,17 +116,47 @@ __global__ __launch_bounds__(256) void conv1x1_stream_kernel(const Stream1x1Args
   float s1[8], s2[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) { s1[e] = 0.f; s2[e] = 0.f; }
+  // prologue coefficients of the 8 channels of each K-step this lane fetches
+  f32x4 pk[PRO ? KS : 1][4];
+  if constexpr (PRO) {
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      const int c = ks * 64 + 8 * jc;
+      pk[ks][0] = *reinterpret_cast<const f32x4*>(a.pscale + c);
+      pk[ks][1] = *reinterpret_cast<const f32x4*>(a.pscale + c + 4);
+      pk[ks][2] = *reinterpret_cast<const f32x4*>(a.pshift + c);
+      pk[ks][3] = *reinterpret_cast<const f32x4*>(a.pshift + c + 4);
+    }
+  }
 
   int mt = g;
   if (mt < a.mtiles) issue_a(mt);
+  __builtin_amdgcn_s_waitcnt(vmcnt_imm(0));   // weights + the first tile (one wait in the loop below)
   for (int it = 0; mt < a.mtiles; ++it, mt += a.G) {
     // the tile's activations have landed: the only younger vector-memory operations of this wave
     // are the previous tile's NSTORE stores, which stay in flight
     // (the builtin, not inline asm: the compiler's waitcnt pass folds it into its scoreboard and then
     // adds no conservative vmcnt(0) of its own before the activation reads)
-    if (it == 0) __builtin_amdgcn_s_waitcnt(vmcnt_imm(0));
-    else __builtin_amdgcn_s_waitcnt(vmcnt_imm(NSTORE));
+    __builtin_amdgcn_s_waitcnt(vmcnt_imm(NSTORE));
     lds_barrier();   // every wave's pieces are in LDS; the previous tile's staging reads are done
+    if constexpr (PRO) {   // rewrite this lane's own pieces in place (after the barrier: otherwise the
+                           // compiler drains the in-flight stores before these reads)
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+        for (int i = 0; i < AL; ++i) {
+          u32x4* pa = reinterpret_cast<u32x4*>(As + ks * BM * 128 + RP * i * 128 + tid * 16);
+          float v[8];
+          unpack8(*pa, v);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            v[e] = fmaxf(__builtin_fmaf(v[e], pk[ks][0][e], pk[ks][2][e]), 0.f);
+            v[e + 4] = fmaxf(__builtin_fmaf(v[e + 4], pk[ks][1][e], pk[ks][3][e]), 0.f);
+          }
+          *pa = pack8(v);
+        }
+      lds_barrier();
+    }
 
     f32x4 acc[TM][TN];
 #pragma unroll
@@ -234,6 +267,17 @@ static bool stream_c512() {
 }
 extern "C" void dlmpi_set_conv_stream(int mode) { g_stream_override = mode; }
 
+// Operand prologue (a deferred BN-apply + ReLU) on the streaming kernel: every N-tile column's blocks
+// rewrite the same activation rows, so only plans with few columns take it (DLMPI_STREAM_PRO: max
+// columns, default 4 -- the ResNet-50 layer-1 / layer-2 expand convs; 0 = never).
+extern "C" int dlmpi_stream1x1_pro_ok(int ntiles) {
+  static const int v = [] {
+    const char* e = getenv("DLMPI_STREAM_PRO");
+    return e ? atoi(e) : 4;
+  }();
+  return ntiles <= v ? 1 : 0;
+}
+
 extern "C" int dlmpi_stream1x1_plan(int64_t M, int C, int Kout, int* bm, int* bn, int* G) {
   static const int env = [] {
     const char* e = getenv("DLMPI_CONV_STREAM");
@@ -260,7 +304,10 @@ extern "C" hipError_t dlmpi_conv1x1_stream(const Stream1x1Args* a, int bm, int b
   const dim3 grid((unsigned)(a->ntiles * a->G)), block(256);
 #define DLMPI_S1(BM_, BN_, KS_)                                                                              \
   do {                                                                                                      \
-    if (a->stats) hipLaunchKernelGGL((conv1x1_stream_kernel<BM_, BN_, KS_, true>), grid, block, 0, s, *a);  \
+    if (a->pscale) {                                                                                        \
+      if (a->stats) hipLaunchKernelGGL((conv1x1_stream_kernel<BM_, BN_, KS_, true, true>), grid, block, 0, s, *a); \
+      else hipLaunchKernelGGL((conv1x1_stream_kernel<BM_, BN_, KS_, false, true>), grid, block, 0, s, *a);  \
+    } else if (a->stats) hipLaunchKernelGGL((conv1x1_stream_kernel<BM_, BN_, KS_, true>), grid, block, 0, s, *a); \
     else hipLaunchKernelGGL((conv1x1_stream_kernel<BM_, BN_, KS_, false>), grid, block, 0, s, *a);          \
   } while (0)
   if (bm == 128 && bn == 128 && a->C == 64) DLMPI_S1(128, 128, 1);

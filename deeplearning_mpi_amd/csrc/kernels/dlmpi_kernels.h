@@ -69,6 +69,8 @@ struct Stream1x1Args {
   const float* bias;
   float* stats;
   int G, ntiles, mtiles;
+  const float* pscale;             // operand prologue: x := relu(x * pscale[c] + pshift[c]) (or null)
+  const float* pshift;
 };
 
 // Streaming 1x1 / stride-1 data gradient with the fused BN-backward epilogue (conv1x1_dgrad_stream.hip)
@@ -387,6 +389,7 @@ void dlmpi_set_conv_stream(int mode);
 void dlmpi_set_dgrad_stream(int mode);
 int dlmpi_stream1x1_plan(int64_t M, int C, int Kout, int* bm, int* bn, int* G);
 hipError_t dlmpi_conv1x1_stream(const dlmpi::Stream1x1Args* a, int bm, int bn, hipStream_t s);
+int dlmpi_stream1x1_pro_ok(int ntiles);
 int dlmpi_dgrad_stream_plan(int64_t M, int K, int Kout, int mask_mode, int z2, int has_res, int* bm, int* bn, int* G);
 hipError_t dlmpi_conv1x1_dgrad_stream(const dlmpi::DgradStreamArgs* a, int bm, int bn, int mask_mode, hipStream_t s);
 int dlmpi_fin_scratch(hipStream_t s, size_t gsum_doubles, int tickets, double** gsum, int** tk);

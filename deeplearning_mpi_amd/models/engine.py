@@ -153,6 +153,15 @@ FUSE_APPLY = os.environ.get("DLMPI_FUSE_APPLY", "1") != "0"
 # 16-K-step GEMM, repeated per column, costs more than the apply pass it removes.
 FUSE_APPLY_MAX_K = int(os.environ.get("DLMPI_FUSE_APPLY_MAXK", "128"))
 
+# DLMPI_STREAM_PRO_FWD=1: where the bottleneck's conv3 runs on the streaming 1x1 kernel with few output
+# columns (ResNet-50 layer1 / layer2), its input -- the second BN-apply + ReLU (bn2) -- is rebuilt in
+# that kernel's operand prologue and never stored; conv3's weight gradient rebuilds it too (wgrad
+# prologue B), the BN backward recomputes its ReLU mask from z.  Bit-identical to the stored schedule
+# (tests/test_stream_pro_gpu.py) but neutral end to end (ResNet-50 13,039 / 13,066 vs 13,019 / 13,091
+# img/s, profiles/r3_stream_pro: the apply passes go, the prologue and its extra barrier cost the
+# streaming kernel about as much), so off by default.
+STREAM_PRO = os.environ.get("DLMPI_STREAM_PRO_FWD", "0") != "0"
+
 # The step's last weight gradient (a unit with ``wgrad_main``: the ResNet stem, whose input needs no
 # gradient) runs on the main stream -- idle by then -- instead of queueing behind the side stream's
 # last weight gradients (profiles/r3_tail).  DLMPI_WGRAD_TAIL_MAIN=0: on the side stream like the rest.
@@ -342,6 +351,13 @@ class ConvUnit:
         xp.done = True
         return stats, o
 
+    def takes_deferred_stream(self, be, N, H, W) -> bool:
+        """This 1x1 / stride-1 conv (the bottleneck conv3) runs on the streaming kernel with its input
+        a deferred BN-apply + ReLU rebuilt in the kernel's operand prologue (STREAM_PRO): the producer
+        skips its apply pass and never stores its output."""
+        return (STREAM_PRO and self.R == 1 and self.S == 1 and self.stride == 1 and self.pad == 0
+                and hasattr(be, "stream_pro_ok") and be.stream_pro_ok(N * H * W, self.Cp, self.Kp))
+
     def can_fuse_apply(self, be, x, train: bool, save=True) -> bool:
         """True if ``fwd`` computes the pending BN-apply ``x`` inside its GEMM's operand prologue
         (FUSE_APPLY): a 1x1 / stride-1 conv of <= FUSE_APPLY_MAX_K outputs behind a residual BN + ReLU."""
@@ -405,7 +421,7 @@ class ConvUnit:
                 self.arena.wait_buffers()   # DDP's asynchronous buffer broadcast must land first
                 be.bn_finalize(stats, mt, self.Kp, *fin)
             elif fuse_apply:   # the producer's BN-apply runs (and is stored) inside this GEMM
-                mt = be.conv_mtiles(N, x.H, x.W, x.C, self.Kp, 1, 1, 1, 0, pro=True)
+                mt = be.conv_mtiles(N, x.H, x.W, x.C, self.Kp, 1, 1, 1, 0, pro=3)
                 stats = torch.empty(mt, 2, self.Kp, dtype=be.dt, device=dev)
                 self.arena.wait_buffers()
                 be.conv_fwd_bn_apply(x, wf, self.Kp, z, self._bias_vec(), stats, *fin)
@@ -413,7 +429,7 @@ class ConvUnit:
                 x = x.y
             else:
                 mt = be.conv_mtiles(N, x.H, x.W, x.C, self.Kp, self.R, self.S, self.stride, self.pad,
-                                    pro=isinstance(x, Deferred))
+                                    pro=(1 if x.kind == "affine" else 2) if isinstance(x, Deferred) else 0)
                 stats = torch.empty(mt, 2, self.Kp, dtype=be.dt, device=dev)
                 # the finalize (in the conv launch itself when possible) reads / updates the running
                 # statistics: DDP's asynchronous buffer broadcast must land before the conv

@@ -143,7 +143,10 @@ class _BlockExec:
             idn, cd = branch_fwd(x)
         h = x
         for k, u in enumerate(self.u[:-1]):
-            h, c = u.fwd(be, h, train, save=save, defer_apply="act" if defer else False, lazy=lazy)
+            # the unit before a streaming conv3 that rebuilds its BN-apply (engine.STREAM_PRO)
+            d = defer or (train and save and k == len(self.u) - 2 and len(self.u) == 3
+                          and self.u[-1].takes_deferred_stream(be, h.N, *u.out_hw(h.H, h.W)))
+            h, c = u.fwd(be, h, train, save=save, defer_apply="act" if d else False, lazy=lazy)
             ctxs.append(c)
             if k == 0 and ds_late:
                 xin = resolve(be, x)   # computed and stored by conv1's prologue

@@ -146,8 +146,16 @@ class NativeBackend:
                                 d.k0, out.buf, None)
         return out
 
-    def conv_mtiles(self, N, H, W, C, K, R, S, stride, pad, pro=False):
-        return self.C.conv2d_fwd_mtiles_pro(N, H, W, C, K, R, S, stride, pad, 0, int(bool(pro)), int(self.f32))
+    def conv_mtiles(self, N, H, W, C, K, R, S, stride, pad, pro=0):
+        """BN-statistics rows the forward conv will write; pro: the operand prologue mode (0 none,
+        1 deferred BN-apply, 2 deferred BN-backward apply, 3 the producer's pending residual apply;
+        True = 1) -- the streaming 1x1 kernel takes modes 0 and 1 only."""
+        return self.C.conv2d_fwd_mtiles_pro(N, H, W, C, K, R, S, stride, pad, 0, int(pro), int(self.f32))
+
+    def stream_pro_ok(self, M, C, K) -> bool:
+        """The streaming 1x1 forward kernel takes a deferred BN-apply + ReLU operand of this shape
+        (conv1x1_stream.hip PRO: few output columns)."""
+        return (not self.f32) and bool(self.C.conv_stream_pro_ok(int(M), int(C), int(K)))
 
     def conv_fwd(self, x, w, K, R, S, stride, pad, y: Act, bias=None, res: Act = None, scale=None,
                  shift=None, relu=False, stats=None, kvalid=0):

@@ -58,7 +58,7 @@ def test_conv_fwd_bn_apply_matches_unfused(shape):
         y.buf.fill_(7.0)
         mb = torch.zeros(M, C // 8, dtype=torch.uint8, device=DEV)
         z = Act.empty(N, H, W, K, torch.bfloat16, DEV)
-        mt = be.conv_mtiles(N, H, W, C, K, 1, 1, 1, 0, pro=True)
+        mt = be.conv_mtiles(N, H, W, C, K, 1, 1, 1, 0, pro=3)
         st = torch.zeros(max(mt, be.conv_mtiles(N, H, W, C, K, 1, 1, 1, 0)), 2, K, device=DEV)
         rm, rv = torch.zeros(K, device=DEV), torch.ones(K, device=DEV)
         v = torch.empty(4, K, device=DEV)
