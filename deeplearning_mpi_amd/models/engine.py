@@ -126,7 +126,11 @@ DEFER_BN_WGRAD = os.environ.get("DLMPI_DEFER_BN_WGRAD", "1") != "0"
 # DLMPI_DUAL_DGRAD=0: off; DLMPI_DUAL_MIN_ROWS: only layers with at least this many output pixels
 # (N*P*Q; memory-bound 1x1 GEMMs -- the doubled reduction costs MFMA time on the small deep layers).
 DUAL_DGRAD = os.environ.get("DLMPI_DUAL_DGRAD", "1") != "0"
-DUAL_MIN_ROWS = int(os.environ.get("DLMPI_DUAL_MIN_ROWS", str(256 * 28 * 28)))
+# Since the streaming 1x1 data gradient (conv1x1_dgrad_stream.hip) the layer-2 shapes (200,704 rows
+# at bs 256) gain nothing from the doubled reduction: 401,408 keeps it for ResNet-50 layer 1 and the
+# ResNet-152 (bs 128) layer 1 (ResNet-50 12,948-12,968 vs 12,882-12,901 img/s with layer 2 included,
+# profiles/r3_cifar_ab2).
+DUAL_MIN_ROWS = int(os.environ.get("DLMPI_DUAL_MIN_ROWS", str(2 * 256 * 28 * 28)))
 # The dual path's weight gradient rebuilds dz in its operand prologue (PA 2) from the same [dy | z]
 # buffer; DLMPI_DUAL_WGRAD_PRO=0: an apply pass materialises dz on the side stream first (measured
 # slower: that pass competes with the main stream for HBM, profiles/r2_dual_dgrad)
