@@ -307,6 +307,7 @@ def main():
     dist_info = {
         "rccl_world_size": int(native_comm.size()) if native_comm is not None else None,
         "rccl_channels": os.environ.get("NCCL_MAX_NCHANNELS") if native_comm is not None else None,
+        "dgrad_stream_blocks": int(os.environ.get("DLMPI_DGS_BLOCKS", "256")),
         "bucket_mb": [round(b, 2) for b in ddp.bucket_sizes_mb()],
         "reducer": ddp.reducer is not None,
         "per_rank_ms_per_step": {"min": min(per_rank_ms), "max": max(per_rank_ms)},

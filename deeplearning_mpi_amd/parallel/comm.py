@@ -392,7 +392,14 @@ def rccl_channel_budget() -> dict:
     want = int(os.environ.get("DLMPI_RCCL_CHANNELS", str(DEFAULT_RCCL_CHANNELS)) or 0)
     if want > 0 and "NCCL_MAX_NCHANNELS" not in os.environ:
         os.environ["NCCL_MAX_NCHANNELS"] = str(want)
-    return {k: os.environ.get(k) for k in ("NCCL_MAX_NCHANNELS", "NCCL_MIN_NCHANNELS")}
+    # The persistent streaming data-gradient kernel (conv1x1_dgrad_stream.hip) splits its work
+    # statically over one block per CU of 100-160 KB of LDS: a block that cannot start because an
+    # RCCL workgroup holds LDS on its CU would hold the whole kernel -- and the backward -- until the
+    # collective ends.  With a communicator, size its grid to the CUs the channels leave free.
+    ch = int(os.environ.get("NCCL_MAX_NCHANNELS") or DEFAULT_RCCL_CHANNELS)
+    if "DLMPI_DGS_BLOCKS" not in os.environ:
+        os.environ["DLMPI_DGS_BLOCKS"] = str(max(64, 256 - ch))
+    return {k: os.environ.get(k) for k in ("NCCL_MAX_NCHANNELS", "NCCL_MIN_NCHANNELS", "DLMPI_DGS_BLOCKS")}
 
 
 _UID_ROUND = 0   # init_distributed -> destroy -> init_distributed in one process: a fresh key each time
