@@ -266,6 +266,16 @@ static bool stream_c512() {
   return v;
 }
 extern "C" void dlmpi_set_conv_stream(int mode) { g_stream_override = mode; }
+// DLMPI_STREAM_C256_BN=128: C = 256 (layer-3 expand, 14^2 256 -> 1024) on 64 x 128 tiles (one block per
+// CU, 8 output columns re-reading each activation tile from L2) instead of 64 x 64 (2 blocks per CU,
+// 16 columns): A/B (profiles/r3_c256)
+static int c256_bn() {
+  static const int v = [] {
+    const char* e = getenv("DLMPI_STREAM_C256_BN");
+    return e ? atoi(e) : 64;
+  }();
+  return v;
+}
 
 // Operand prologue (a deferred BN-apply + ReLU) on the streaming kernel: every N-tile column's blocks
 // rewrite the same activation rows, so only plans with few columns take it (DLMPI_STREAM_PRO: max
@@ -287,6 +297,7 @@ extern "C" int dlmpi_stream1x1_plan(int64_t M, int C, int Kout, int* bm, int* bn
   if (!on || M <= 0) return 0;
   if (C == 64 && Kout % 128 == 0) { *bm = 128; *bn = 128; }
   else if (C == 128 && Kout % 128 == 0) { *bm = 64; *bn = 128; }
+  else if (C == 256 && Kout % 128 == 0 && c256_bn() == 128) { *bm = 64; *bn = 128; }   // 113 KB: 1 block / CU
   else if (C == 256 && Kout % 64 == 0) { *bm = 64; *bn = 64; }
   else if (C == 512 && Kout % 64 == 0 && stream_c512()) { *bm = 64; *bn = 64; }
   else return 0;
@@ -294,7 +305,7 @@ extern "C" int dlmpi_stream1x1_plan(int64_t M, int C, int Kout, int* bm, int* bn
   const int64_t mtiles = (M + *bm - 1) / *bm;
   // ~2 resident blocks per CU over the whole chip (LDS 65-80 KB per block); C = 512 holds 144 KB
   // (1 block per CU)
-  int target = (C == 512 ? 256 : 512) / ntiles;
+  int target = (C == 512 || (C == 256 && *bn == 128) ? 256 : 512) / ntiles;
   if (target < 8) target = 8;
   *G = (int)(mtiles < target ? mtiles : target);
   return 1;
@@ -313,6 +324,7 @@ extern "C" hipError_t dlmpi_conv1x1_stream(const Stream1x1Args* a, int bm, int b
   if (bm == 128 && bn == 128 && a->C == 64) DLMPI_S1(128, 128, 1);
   else if (bm == 64 && bn == 128 && a->C == 128) DLMPI_S1(64, 128, 2);
   else if (bm == 64 && bn == 64 && a->C == 256) DLMPI_S1(64, 64, 4);
+  else if (bm == 64 && bn == 128 && a->C == 256) DLMPI_S1(64, 128, 4);
   else if (bm == 64 && bn == 64 && a->C == 512) DLMPI_S1(64, 64, 8);
   else return hipErrorInvalidValue;
 #undef DLMPI_S1
