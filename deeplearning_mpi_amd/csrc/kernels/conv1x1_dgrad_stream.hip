@@ -3,9 +3,13 @@
 //
 //   dx[m, c] = sum_k A[m, k] W[c, k] (+ bias[c]) (+ res[m, c]),  then the consumer's ReLU mask
 //   (mask bits of the forward BN-apply, or z * mscale + mshift > 0) and its BN-backward partials
-//   {sum dx, sum dx * z} of the stored (bf16) gradient.
+//   {sum dx, sum dx * z [, sum dx * z2]} of the stored (bf16) gradient (z2: a second BN input
+//   consuming the same gradient, the ResNet downsample branch).
 //
-// A is dy, or [dy | z] of the dual data gradient (engine.ConvUnit.dual, K = 2 x 64 / 2 x 128).
+// A is dy, or [dy | z] of the dual data gradient (engine.ConvUnit.dual, K = 2 x 64 / 2 x 256).
+// Tiles by reduction length (dlmpi_dgrad_stream_plan): K 128 -> 64 x 128 (8 waves), K 256 -> 48 x 128
+// (6 waves; 32 x 128 with z2), K 512 -> 64 x 64 (8 waves, z-mask only; 32 x 64 with a residual / mask
+// bits / z2 is opt-in, measured slower).  One block per CU; 98-160 KB of LDS.
 // Example (profiles/r3_s3_base/resnet50_step.txt): layer-1 conv1 of a bottleneck, 802,816 rows, K 128,
 // 256 output channels, plus a residual gradient, the previous block's z and mask bits: 1.46 GB of
 // traffic that the general implicit-GEMM kernel moved in 645 us (2.3 TB/s) -- every block stages
@@ -13,8 +17,8 @@
 // epilogue rows, so loads and stores never overlap inside a block.
 //
 // Here (same idea as conv1x1_stream.hip, extended to the epilogue operands):
-//   * persistent blocks (one per CU), each walking a column of 128-channel output tiles;
-//     the weight tile [128][K] is staged into LDS once and stays resident;
+//   * persistent blocks (one per CU), each walking a column of 128- (or 64-) channel output tiles;
+//     the weight tile [BN][K] is staged into LDS once and stays resident;
 //   * the NEXT tile's epilogue operands (residual, z, mask bits) and A are fetched global -> LDS
 //     (global_load_lds; the operands into the other half of a double buffer) right after the
 //     current tile's MFMAs, so they stream in under the current tile's epilogue math and stores
@@ -22,14 +26,17 @@
 //     the A / W fragment reads and waits for it there);
 //   * the epilogue runs on the D^T accumulator fragments (operands swapped: each lane holds 4
 //     consecutive channels of one pixel) reading its residual / z / mask pieces from LDS
-//     (XOR-swizzled rows: conflict-free 8-byte reads), writes bf16 quads into a staging tile and
+//     (XOR-swizzled rows: conflict-free 8-byte reads), writes bf16 quads in place of the consumed
+//     z tile (a staging tile of its own without statistics) and
 //     the tile leaves as 16-byte row stores that are never waited for (the only wait is
 //     vmcnt(NSTORE) at the top of the next tile: vmcnt retires in issue order and the stores were
 //     issued last);
 //   * BN partial sums accumulate per lane over ALL of the block's tiles: one partial row per block.
 // The per-element arithmetic is the conv_igemm epilogue's (fp32: (acc + bias) + res, mask, round
-// once to bf16), so dx is bit-identical to the general kernel; the partial sums differ only in
-// fp32 summation order.
+// once to bf16), so dx is bit-identical to the general kernel (K <= 256; at K = 512 the general
+// kernel may split K); the partial sums differ only in fp32 summation order.
+// With an RCCL communicator the grid is 256 - (RCCL channels) blocks (parallel/comm.py): a block
+// that cannot start because a collective's workgroup holds LDS on its CU would hold the kernel.
 //
 // Reference semantics: the autograd of nn.Conv2d(k=1) + BatchNorm2d + ReLU (+ residual add) in
 // torchvision's Bottleneck (/root/reference/pytorch/resnet/main.py:40-41, loss.backward() at :128).
