@@ -94,6 +94,18 @@ static int bm256_min_tiles() {
   return v;
 }
 
+// DLMPI_CONV_BM256_MIN_RED_1X1: shortest 1x1 reduction (red == cin) that takes the 256-row tile
+// (default 1024: the 14^2 1024->256 forward and 256<-1024 data gradient, 128x128 -> 256x128 tiles
+// halve the B-operand re-reads, -14 % each; ResNet-50 +0.8 %, profiles/r3_bm256red); other
+// reductions from 2304 as before
+static int bm256_min_red_1x1() {
+  static int v = [] {
+    const char* e = getenv("DLMPI_CONV_BM256_MIN_RED_1X1");
+    return e ? atoi(e) : 1024;
+  }();
+  return v;
+}
+
 static int bm_override() {   // experiments: force the M tile (64 | 128 | 256)
   static int v = [] {
     const char* e = getenv("DLMPI_CONV_BM");
@@ -111,7 +123,8 @@ static int sq256_min_tiles() {
 }
 
 // cin: channel count of the GEMM's gathered operand (the 8-wave 256x256 kernel needs cin % 64 == 0)
-static void pick_tiles(int64_t M, int Kout, int64_t red, int cin, int& bm, int& bn, bool pro = false) {
+static void pick_tiles(int64_t M, int Kout, int64_t red, int cin, int& bm, int& bn, bool pro = false,
+                       bool wide1x1 = true) {
   bn = Kout <= 64 ? 64 : 128;
   // 64 (mod 128) channels above 128 (the UNet's 192-channel top concat gradient): 64-wide tiles
   // cover them exactly instead of a half-empty last 128-wide tile (a third more MFMA work)
@@ -153,7 +166,7 @@ static void pick_tiles(int64_t M, int Kout, int64_t red, int cin, int& bm, int& 
   // the small-channel stems (-13 % ResNet 7x7, -10 % UNet first conv) and the 4M-row UNet level-1
   // 3x3s (-4 %), loses 3-8 % on the 0.8M-row ResNet layer1 GEMMs -> only there.
   if (bn == 64 && n64 && (M + 255) / 256 >= 512 && (cin < 64 || (M >= (2 << 20) && red >= 576))) bm = 256;
-  else if (Kout >= 256 && red >= 2304 && ((M + 255) / 256) * nt >= bm256_min_tiles()) bm = 256;
+  else if (Kout >= 256 && (red >= 2304 || (wide1x1 && red == cin && red >= bm256_min_red_1x1())) && ((M + 255) / 256) * nt >= bm256_min_tiles()) bm = 256;
   else if (tiles < 512) bm = 64;
 }
 
@@ -953,7 +966,7 @@ void convT2x2_fwd(const at::Tensor& x, int N, int H, int W, int Cin, int ldx, in
   a.vec_store = ((ldy % 8) == 0 && (yoff % 8) == 0) ? 1 : 0;
   set_kstep(a, Cin);
   int bm, bn;
-  pick_tiles((int64_t)N * H * W, Cout, Cin, Cin, bm, bn);
+  pick_tiles((int64_t)N * H * W, Cout, Cin, Cin, bm, bn, false, false);   // 4-phase convT: unmeasured at 256 rows
   if (a.f32) f32_tiles(bm, bn);
   a.ntiles = ceil_div(Cout, bn);
   a.nphase = 4;
