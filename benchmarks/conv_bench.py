@@ -86,15 +86,8 @@ def main():
     ap.add_argument("--only", default=None)
     ap.add_argument("--no_miopen", action="store_true")
     ap.add_argument("--net", default="resnet50", choices=["resnet50", "unet512"])
-    ap.add_argument("--stages", type=int, default=None, help="DLMPI_CONV_STAGES for our kernels")
     ap.add_argument("--bm256_min_tiles", type=int, default=None, help="DLMPI_CONV_BM256_MIN_TILES")
-    ap.add_argument("--repi", type=int, default=None, help="DLMPI_CONV_REPI (register-direct conv epilogue)")
     args = ap.parse_args()
-    if args.repi is not None:
-        os.environ["DLMPI_CONV_REPI"] = str(args.repi)
-    if args.stages:
-        os.environ["DLMPI_CONV_STAGES"] = str(args.stages)
-        os.environ["DLMPI_WGRAD_STAGES"] = str(args.stages)
     if args.bm256_min_tiles is not None:
         os.environ["DLMPI_CONV_BM256_MIN_TILES"] = str(args.bm256_min_tiles)
     if args.net == "unet512" and args.batch == 256:

@@ -170,6 +170,23 @@ static void pick_tiles(int64_t M, int Kout, int64_t red, int cin, int& bm, int& 
   else if (tiles < 512) bm = 64;
 }
 
+// ---- pipelined 8-wave tiles (conv_igemm.hip conv_pipe_kernel) -----------------------------------
+// Long reductions over >= 64-channel operands into wide outputs: one 8-wave block per CU with an
+// LDS ring instead of 2-3 single-stage 4-wave blocks.  Returns the kernel variant + 1 (0: keep the
+// single-stage tile bm x bn) and sets the pipelined tile.  g_pipe_override (tests): -1 the rule,
+// 0 never, 1 wherever the kernel applies.
+static int g_pipe_override = -1;
+static int pipe_select(int f32, int pro, int cin, int64_t M, int Kout, int64_t red, int& bm, int& bn) {
+  if (f32 || pro != 0 || cin % 64 != 0 || g_pipe_override == 0) return 0;
+  if (g_pipe_override == 1) {
+    bm = Kout >= 256 ? 256 : (Kout > 64 ? 256 : 512);
+    bn = Kout >= 256 ? 256 : (Kout > 64 ? 128 : 64);
+    return 1;
+  }
+  (void)M; (void)red;
+  return 0;
+}
+
 // ---- 2-D halo tiles for 3x3 / stride-1 / pad-1 convolutions (conv_igemm.hip HALO) ----------------
 // DLMPI_CONV_HALO=0: these convolutions through the im2col gather path too.
 static int g_halo_override = -1;   // dlmpi_ext set_conv_halo (tests)
@@ -284,7 +301,7 @@ static int apply_tiles(ConvArgs& a, int bm, int bn) {
 // Plan for a fully set-up (default-tiled) launch: the cached one, or tune now.  Returns false if
 // autotuning does not apply (the caller keeps its static plan).
 static bool conv_plan(ConvArgs& a, int pass, int& bm, int& bn) {
-  if (!conv_autotune_on() || a.f32 || a.pro != 0 || a.fin_on || a.halo) return false;
+  if (!conv_autotune_on() || a.f32 || a.pro != 0 || a.halo) return false;
   // trials re-run the launch: an output that is also one of its inputs (in-place residual / mask /
   // z) would be transformed once per trial -- keep the static plan there
   const void* y = a.y;
@@ -476,41 +493,6 @@ bool conv_stream_pro_ok(int64_t M, int C, int K) {
 }
 
 
-// In-launch BN finalize (bnfin.h) of a launch producing T stats rows over Kout channels: groups of
-// ~sqrt(T) rows.  DLMPI_FIN_IN_LAUNCH = largest T that finalizes in-launch (0 = off: the finalize
-// runs as its own launch).
-// Default 0: measured slower on ResNet-50 (profiles/r3_fin_in_launch_rejected: 11,941 img/s with every
-// finalize in-launch, 12,009 with T <= 512 only, 12,030 off) -- every conv block pays a drain of its
-// output stores + a returning ticket atomic before it can retire, which costs more than the
-// finalize launch it removes.
-static int g_fin_override = -1;   // dlmpi_ext set_fin_in_launch (tests)
-static int fin_in_launch_max() {
-  static const int v = [] {
-    const char* e = getenv("DLMPI_FIN_IN_LAUNCH");
-    return e ? atoi(e) : 0;
-  }();
-  return g_fin_override >= 0 ? g_fin_override : v;
-}
-
-static bool setup_fin(ConvArgs& a, int T, const FinArgs& f, int k2) {
-  if (T <= 0 || T > fin_in_launch_max()) return false;
-  int G = 8;
-  while (G * G < T && G < 256) G *= 2;
-  const int NG = ceil_div(T, G);
-  double* gsum = nullptr;
-  int* tk = nullptr;
-  if (!dlmpi_fin_scratch(cur_stream(), (size_t)NG * 2 * a.Kout, a.ntiles * (NG + 1), &gsum, &tk)) return false;
-  a.fin_on = 1;
-  a.fin_group = G;
-  a.fin_ngroups = NG;
-  a.fin_T = T;
-  a.fin_k2 = k2;
-  a.fin_gsum = gsum;
-  a.fin_tk = tk;
-  a.fin = f;
-  return true;
-}
-
 // y[n, p, q, yoff + k] = epilogue( sum_{r,s,c} x[n, p*stride - pad + r, q*stride - pad + s, xoff + c] * w[k][r][s][c] )
 // fin (with stats): also finalize the BatchNorm over these statistics -- inside the launch when the
 // in-launch finalize is available, else by the standalone finalize right after it.
@@ -619,7 +601,8 @@ static int conv2d_fwd_impl(const at::Tensor& x, int N, int H, int W, int C, int 
   int bm, bn;
   pick_tiles((int64_t)N * P * Q, K, (int64_t)R * S * C, C, bm, bn, pro != 0);
   if (a.f32) f32_tiles(bm, bn);
-  const bool halo = bm_req <= 0 && bn_req <= 0 && halo_eligible(a.f32, pro, C, R, S, stride, pad, P, Q, bm, bn);
+  int pipe = bm_req <= 0 && bn_req <= 0 ? pipe_select(a.f32, pro, C, (int64_t)N * P * Q, K, (int64_t)R * S * C, bm, bn) : 0;
+  const bool halo = !pipe && bm_req <= 0 && bn_req <= 0 && halo_eligible(a.f32, pro, C, R, S, stride, pad, P, Q, bm, bn);
   if (halo) {
     bm = 128;
     bn = std::min(bn, 128);
@@ -680,13 +663,11 @@ static int conv2d_fwd_impl(const at::Tensor& x, int N, int H, int W, int C, int 
   g_halo_ran = halo ? 1 : 0;
   // autotuned tiling: BN-stats launches only through conv2d_fwd_bn (its buffer is sized for the
   // largest row count, conv2d_fwd_mtiles_pro, and its finalize uses the actual one)
-  if ((fin != nullptr || !a.stats) && bm_req <= 0 && bn_req <= 0) conv_plan(a, 0, bm, bn);
-  if (fin != nullptr) {
-    if (!a.stats || stats->size(0) < p.mtiles) throw std::runtime_error("conv2d_fwd_bn: stats [mtiles][2][K] required");
-    setup_fin(a, p.mtiles, *fin, 1);
-  }
-  check(dlmpi_conv_igemm(&a, bm, bn, cur_stream()), "conv2d_fwd");
-  if (fin != nullptr && !a.fin_on) {   // no scratch (e.g. first use inside a capture): separate finalize
+  if (!pipe && (fin != nullptr || !a.stats) && bm_req <= 0 && bn_req <= 0) conv_plan(a, 0, bm, bn);
+  if (fin != nullptr && (!a.stats || stats->size(0) < p.mtiles))
+    throw std::runtime_error("conv2d_fwd_bn: stats [mtiles][2][K] required");
+  check(dlmpi_conv_igemm_ex(&a, bm, bn, pipe, cur_stream()), "conv2d_fwd");
+  if (fin != nullptr) {   // the BN finalize of these statistics
     at::Tensor ws = colsum_ws(*stats, p.mtiles, K);
     check(dlmpi_bn_finalize(a.stats, p.mtiles, K, fin->count, fin->gamma, fin->beta, fin->running_mean,
                             fin->running_var, fin->momentum, fin->eps, fin->scale, fin->shift, fin->save_mean,
@@ -742,6 +723,7 @@ at::Tensor conv2d_fwd_bnbwd(const at::Tensor& x, int N, int H, int W, int C, int
   int bm, bn;
   pick_tiles((int64_t)N * P * Q, K, (int64_t)R * S * C, C, bm, bn);
   if (a.f32) f32_tiles(bm, bn);
+  const int pipe = pipe_select(a.f32, 0, C, (int64_t)N * P * Q, K, (int64_t)R * S * C, bm, bn);
   a.ntiles = ceil_div(K, bn);
   a.nphase = 1;
   ConvPhase& p = a.ph[0];
@@ -752,7 +734,7 @@ at::Tensor conv2d_fwd_bnbwd(const at::Tensor& x, int N, int H, int W, int C, int
   finish_phase(p, N, C, bm, a.f32);
   at::Tensor stats = at::empty({(int64_t)p.mtiles, 2, (int64_t)K}, x.options().dtype(at::kFloat));
   a.stats = ptr<float>(stats);
-  check(dlmpi_conv_igemm(&a, bm, bn, cur_stream()), "conv2d_fwd_bnbwd");
+  check(dlmpi_conv_igemm_ex(&a, bm, bn, pipe, cur_stream()), "conv2d_fwd_bnbwd");
   return stats;
 }
 
@@ -767,6 +749,8 @@ int conv2d_fwd_mtiles_pro(int N, int H, int W, int C, int K, int R, int S, int s
     int hbm, hbn;
     pick_tiles((int64_t)N * P * Q, K, (int64_t)R * S * C, C, hbm, hbn, pro != 0);
     if (f32) f32_tiles(hbm, hbn);
+    if (pipe_select(f32, pro, C, (int64_t)N * P * Q, K, (int64_t)R * S * C, hbm, hbn))
+      return ceil_div((int64_t)N * P * Q, hbm);
     if (halo_eligible(f32, pro, C, R, S, stride, pad, P, Q, hbm, hbn)) return halo_mtiles(N, P, Q);
   }
   // autotuned launches may pick any M tile: size for the smallest (64 rows)
@@ -881,7 +865,9 @@ c10::optional<at::Tensor> conv2d_dgrad_pro(const at::Tensor& dy, int N, int P, i
   int bm, bn;
   pick_tiles((int64_t)N * H * W / (stride * stride), C, (int64_t)R * S * K / (stride * stride), K, bm, bn, pro != 0);
   if (a.f32) f32_tiles(bm, bn);
-  const bool halo = halo_eligible(a.f32, pro, K, R, S, stride, pad, H, W, bm, bn) && P == H && Q == W;
+  const int pipe = pipe_select(a.f32, pro, K, (int64_t)N * H * W / (stride * stride), C,
+                               (int64_t)R * S * K / (stride * stride), bm, bn);
+  const bool halo = !pipe && halo_eligible(a.f32, pro, K, R, S, stride, pad, H, W, bm, bn) && P == H && Q == W;
   if (halo) {
     bm = 128;
     bn = std::min(bn, 128);
@@ -915,7 +901,7 @@ c10::optional<at::Tensor> conv2d_dgrad_pro(const at::Tensor& dy, int N, int P, i
      // write to scratch)
     const bool want_stats = a.z || colsum;
     a.stats = want_stats ? reinterpret_cast<float*>(static_cast<uintptr_t>(256)) : nullptr;
-    if (conv_plan(a, 1, bm, bn)) {
+    if (!pipe && conv_plan(a, 1, bm, bn)) {
       tiles = 0;
       for (int i = 0; i < a.nphase; ++i) tiles += a.ph[i].mtiles;
     }
@@ -928,7 +914,7 @@ c10::optional<at::Tensor> conv2d_dgrad_pro(const at::Tensor& dy, int N, int P, i
     stats = at::empty({(int64_t)tiles, (int64_t)a.nstat, (int64_t)C}, dy.options().dtype(at::kFloat));
     a.stats = ptr<float>(*stats);
   }
-  check(dlmpi_conv_igemm(&a, bm, bn, cur_stream()), "conv2d_dgrad");
+  check(dlmpi_conv_igemm_ex(&a, bm, bn, pipe, cur_stream()), "conv2d_dgrad");
   return stats;
 }
 
@@ -1462,7 +1448,6 @@ void register_ops(pybind11::module& m) {
   m.def("conv2d_fwd", &conv2d_fwd);
   m.def("conv2d_fwd_pro", &conv2d_fwd_pro);
   m.def("conv2d_fwd_bn", &conv2d_fwd_bn);
-  m.def("set_fin_in_launch", [](int max_t) { g_fin_override = max_t; });
   m.def("conv2d_fwd_mtiles", &conv2d_fwd_mtiles);
   m.def("conv2d_fwd_mtiles_pro", &conv2d_fwd_mtiles_pro);
   m.def("conv2d_fwd_bnbwd", &conv2d_fwd_bnbwd);
@@ -1525,8 +1510,6 @@ void register_ops(pybind11::module& m) {
   m.def("grad_norm", &grad_norm);
   m.def("scale_", &scale_);
   m.def("fill_", &fill_);
-  m.def("set_conv_sk", [](int mode) { dlmpi_set_conv_sk(mode); });
-  m.def("set_conv_repi", [](int mode) { dlmpi_set_conv_repi(mode); });
   m.def("set_conv_stream", [](int mode) { dlmpi_set_conv_stream(mode); });
   m.def("conv_stream_last", []() { return g_stream_ran; });
   m.def("conv_stream_pro_ok", &conv_stream_pro_ok);
@@ -1535,11 +1518,11 @@ void register_ops(pybind11::module& m) {
   m.def("set_conv_autotune", [](int mode) { g_autotune_override = mode; });
   m.def("set_wgrad3", [](int mode) { g_wgrad3_override = mode; });
   m.def("set_conv_halo", [](int mode) { g_halo_override = mode; });
+  m.def("set_conv_pipe", [](int mode) { g_pipe_override = mode; });
   m.def("conv_halo_last", []() { return g_halo_ran; });
   m.def("conv2d_fwd_bn_apply", &conv2d_fwd_bn_apply);
   m.def("wgrad3_last", []() { return g_wgrad3_ran; });
   m.def("clear_conv_plans", []() { g_conv_plans.clear(); });
-  m.def("conv_sk_last", []() { return dlmpi_conv_sk_last(); });
   m.def("add_i64_", &add_i64_);
   m.def("gather_", &gather_);
   m.attr("CAST_ENTRY_BYTES") = (int)sizeof(CastEntry);

@@ -717,41 +717,6 @@ extern "C" int* dlmpi_splitk_tickets(hipStream_t s, int n) {
   return g_sk_tk[dev][r];
 }
 
-// Scratch of the conv epilogue's in-launch BN finalize (bnfin.h), per device and stream role: fp64
-// group sums (grown on demand outside captures, never freed -- a captured graph may reference it)
-// and self-resetting tickets (zeroed once, ordered before the first kernel that uses them).
-static double* g_fin_gsum[64][kTicketRoles] = {};
-static size_t g_fin_gsum_n[64][kTicketRoles] = {};
-static int* g_fin_tk[64][kTicketRoles] = {};
-constexpr int kFinTickets = 1 << 16;
-
-extern "C" int dlmpi_fin_scratch(hipStream_t s, size_t gsum_doubles, int tickets, double** gsum, int** tk) {
-  int dev = 0;
-  if (tickets > kFinTickets || hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 0;
-  const int r = role_of(s, dev);
-  const bool need = g_fin_gsum_n[dev][r] < gsum_doubles || !g_fin_tk[dev][r];
-  if (need) {
-    hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
-    if (hipStreamIsCapturing(s, &st) != hipSuccess || st != hipStreamCaptureStatusNone) return 0;
-  }
-  if (g_fin_gsum_n[dev][r] < gsum_doubles) {
-    const size_t n = gsum_doubles + gsum_doubles / 2 + 4096;
-    double* p = nullptr;
-    if (hipMalloc(&p, n * sizeof(double)) != hipSuccess) return 0;
-    g_fin_gsum[dev][r] = p;
-    g_fin_gsum_n[dev][r] = n;
-  }
-  if (!g_fin_tk[dev][r]) {
-    int* p = nullptr;
-    if (hipMalloc(&p, kFinTickets * sizeof(int)) != hipSuccess) return 0;
-    if (hipMemsetAsync(p, 0, kFinTickets * sizeof(int), s) != hipSuccess) return 0;
-    g_fin_tk[dev][r] = p;
-  }
-  *gsum = g_fin_gsum[dev][r];
-  *tk = g_fin_tk[dev][r];
-  return 1;
-}
-
 static bool fused_finalize() {
   static const bool v = [] {
     const char* e = getenv("DLMPI_BN_FUSED_FINALIZE");

@@ -1,6 +1,6 @@
 // Implicit-GEMM convolution on CDNA4 MFMA (v_mfma_f32_16x16x32_bf16), NHWC bf16, fp32 accumulate.
 //
-// One kernel serves every "gather-A" GEMM of the framework:
+// One GEMM formulation serves every "gather-A" GEMM of the framework:
 //   * Conv2d forward (any R x S, stride, pad; ResNet stem 7x7/s2, 3x3, 1x1, UNet 3x3),
 //   * Conv2d data-gradient (stride^2 sub-pixel phases, each a dense conv with its own tap list,
 //     so a stride-2 3x3 dgrad does no zero MACs),
@@ -9,27 +9,35 @@
 // Replaces what the reference gets implicitly from cuDNN conv fwd/dgrad and cuBLAS
 // (call sites /root/reference/pytorch/unet/model.py:9-14, resnet main.py:40-41).
 //
-// Tile: BM (pixels) x BN (channels) x 64 (reduction), 256 threads = 4 waves in 2x2, each wave
-// (BM/2) x (BN/2) as (BM/32) x (BN/32) MFMA 16x16 tiles.
-// Staging: global -> LDS directly with global_load_lds_dwordx4 (no VGPR round trip, no ds_write):
-// each wave instruction fills 8 LDS rows of 128 B lane-linearly; the XOR swizzle that makes the
-// ds_read_b128 fragment reads bank-conflict-free is applied on the per-lane SOURCE address
-// (cdna_hip_programming.md §5.4 rule 21).  Out-of-image im2col pieces read a zero page.  The
-// next K-tile's loads are issued before the current tile's MFMAs into the other LDS buffer
-// (one barrier per K-step).  Channel counts >= 64: the tap (r, s) and channel base are
-// wave-uniform scalars and the per-row source pointers are rebuilt only when the tap changes.
+// Two kernels share the staging scheme and the epilogue:
+//
+// conv_igemm_kernel -- 4 waves, single LDS stage, two barriers per K-step, 3-4 blocks per CU
+//   (latency hidden across blocks).  Every operand class: small channel counts (stem, UNet input),
+//   operand prologues (deferred BN-apply), 2-D halo tiles, split-K for small grids, fp32 storage.
+//   Best on the short / memory-bound GEMMs, where a block's whole life is a few K-steps.
+//
+// conv_pipe_kernel -- 8 waves, one block per CU, an LDS ring of STAGES K-steps with STAGES - 1 in
+//   flight and ONE barrier per K-step: the LDS-DMA of step k + STAGES - 1 is issued right after the
+//   barrier of step k and retired by a counted `s_waitcnt vmcnt` just before the barrier of the step
+//   that reads it, so the loads stay in flight across barriers while the MFMAs of the intermediate
+//   steps run (cdna_hip_programming.md §5 "Pipelining across barriers").  Per-wave 128 x 64 / 64 x 64
+//   output tiles (LDS read traffic per MFMA 25-50 % below the 4-wave 64 x 64 kernel).  For the
+//   compute-bound long reductions (3x3 convs from 64 channels, 1x1 from 1024).
+//
+// Staging (both): global -> LDS directly with global_load_lds_dwordx4 (no VGPR round trip, no
+// ds_write): each wave instruction fills 8 LDS rows of 128 B lane-linearly; the XOR swizzle that
+// makes the ds_read_b128 fragment reads bank-conflict-free is applied on the per-lane SOURCE address
+// (cdna_hip_programming.md §5.4 rule 21).  Out-of-image im2col pieces read a zero page.  Channel
+// counts >= 64: the tap (r, s) and channel base are wave-uniform scalars and the per-row source
+// pointers are rebuilt only when the tap changes.  All LDS is ONE __shared__ array: with a second
+// LDS object hipcc tracks the DMA targets and waits for every in-flight DMA before each fragment read.
 // Epilogue: the fp32 tile is staged through LDS for 16-byte stores with fused bias / residual
 // add / folded-BN affine / ReLU and the per-channel BatchNorm partial sums of the stored
 // (bf16-rounded) values.
 #include <cstdlib>
 #include <type_traits>
 
-#ifndef DLMPI_W128   // waves/SIMD target of the 128x128 / 256x64 tiles (A/B builds)
-#define DLMPI_W128 3
-#endif
-
 #include "common.h"
-#include "bnfin.h"
 
 namespace dlmpi {
 
@@ -39,29 +47,254 @@ __device__ __forceinline__ void glds16(const void* g, char* lds_wave_base) {
   __builtin_amdgcn_global_load_lds(g, (lds_void*)lds_wave_base, 16, 0, 0);
 }
 
-// STAGES = 2: double-buffered K loop (one barrier per K-step, 2 blocks/CU at 128x128);
-// STAGES = 1: single buffer, two barriers per K-step, 34 KB of LDS -> 4 blocks/CU (latency hidden
-// across blocks instead of inside one).  The epilogue stages the fp32 tile through LDS in two
-// row halves so it never needs more LDS than one stage.
-// NW = 8 (512 threads, waves 2 x 4, per-wave 128 x 64 at 256 x 256): 25 % less LDS traffic per
-// MFMA than 64 x 64 per wave, double-buffered (128 KB LDS, one block per CU) so that a whole
-// K-step of MFMA work (2048 SIMD cycles) covers the next step's loads.
-// WGM = wave rows (WGM x NW/WGM wave grid): 4 x 1 for the 256 x 64 tile of 64-channel layers
-// (per-wave 64 x 64 instead of 64 x 32: a third less LDS traffic per MFMA).
+// LDS bytes the epilogue needs: fp32 tile staging in NP passes of <= 64 rows, or the statistics combine
+template <int BM, int BN, int NT, int WM>
+struct EpiSmem {
+  static constexpr int NP0 = BM < 128 ? 1 : (BM / 64 < WM / 16 ? BM / 64 : WM / 16);
+  // a pass must take the same number of fragment rows from every wave (7-fragment waves: 7 passes)
+  static constexpr int NP = (WM / 16) % NP0 == 0 ? NP0 : WM / 16;
+  static constexpr int CS_LD = BN + 4;
+  static constexpr int EPI = (BM / NP) * CS_LD * 4;
+  static constexpr int RED = (NT / (BN / 8)) * 3 * BN * 4;
+  static constexpr int bytes = EPI > RED ? EPI : RED;
+};
+
+// ---- split-K combine (cdna_hip_programming.md "In-launch split-K reduction") ---------------------
+// Every slice stores its fp32 accumulators (fragment layout) to its slab, publishes with an
+// agent-scope release + ticket; the tile's last arriver acquires and sums ALL slices' slabs in
+// slice order (deterministic whichever block arrives last), then runs the normal epilogue.
+// Returns false in the blocks that are not the last arriver (they exit).
+template <int NT, int NF>
+__device__ __forceinline__ bool splitk_combine(const ConvArgs& a, f32x4* acc, char* smem, int tid, int mt, int nt) {
+  const int S = a.splitk;
+  // unique over phases (blockIdx.z): ConvTranspose phases all have tile_base 0
+  const int64_t tile = (int64_t)blockIdx.z * gridDim.x + (int64_t)mt * a.ntiles + nt;
+  f32x4* slab = reinterpret_cast<f32x4*>(a.sk_slab) + (tile * S + blockIdx.y) * NF * NT + tid;
+#pragma unroll
+  for (int i = 0; i < NF; ++i) slab[(int64_t)i * NT] = acc[i];
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  int* flag = reinterpret_cast<int*>(smem);   // the one LDS array (no second __shared__ object)
+  if (tid == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    flag[0] = __hip_atomic_fetch_add(a.sk_tk + tile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == S - 1;
+  }
+  __syncthreads();
+  if (!flag[0]) return false;
+  if (tid == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __hip_atomic_store(a.sk_tk + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+  const f32x4* base = reinterpret_cast<const f32x4*>(a.sk_slab) + tile * S * NF * NT + tid;
+#pragma unroll
+  for (int i = 0; i < NF; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int sp = 0; sp < S; ++sp)
+#pragma unroll
+    for (int i = 0; i < NF; ++i) acc[i] += base[((int64_t)sp * NF + i) * NT];
+  __syncthreads();   // flag (LDS) is reused by the epilogue staging
+  return true;
+}
+
+// ---- epilogue ------------------------------------------------------------------------------------
+// acc: this wave's (BM/WGM) x (BN/WGN) output fragments (wave (wm, wn) of a WGM x WGN grid).  The
+// tile is dumped to LDS in NP passes of BM/NP rows; every thread then owns 8 channels of a row:
+// bias -> BN statistics (forward) -> folded-BN affine -> residual -> ReLU -> backward mask and
+// BN-backward statistics -> 16-byte store.  Per-channel partial sums are combined over the row
+// groups in LDS and written as one stats row per M-tile.
+template <int BM, int BN, int NT, int WGM, int WGN, typename T, bool HALO>
+__device__ __forceinline__ void conv_epilogue(const ConvArgs& a, const ConvPhase& ph,
+                                              f32x4 (&acc)[BM / WGM / 16][BN / WGN / 16], char* smem, int tid,
+                                              int m0, int n0, int mt, int hn, int hh0, int hw0) {
+  constexpr int WM = BM / WGM, WN = BN / WGN;
+  constexpr int TM = WM / 16, TN = WN / 16;
+  constexpr int NP = EpiSmem<BM, BN, NT, WM>::NP;
+  constexpr int CS_LD = EpiSmem<BM, BN, NT, WM>::CS_LD;
+  static_assert(WM % (16 * NP) == 0 || NP == 1, "epilogue pass must split every wave's rows evenly");
+  const int lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wid / WGN, wn = wid % WGN;
+  const int fr = lane & 15, fg = lane >> 4;
+  const int PQ = ph.P * ph.Q;
+  const int M = a.Nimg * PQ;
+  float* Cs = reinterpret_cast<float*>(smem);
+
+  constexpr int CG = BN / 8;       // channel groups of 8
+  constexpr int RG = NT / CG;      // row groups
+  const int cg = tid % CG, rg = tid / CG;
+  const int c0 = n0 + cg * 8;
+  const bool cvalid = c0 < a.Kout;
+  float bias[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) bias[e] = 0.f;
+  if (cvalid && a.bias) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) bias[e] = a.bias[c0 + e];
+  }
+  float s1[8], s2[8], s3[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) { s1[e] = 0.f; s2[e] = 0.f; s3[e] = 0.f; }
+  // gradient of a BN+ReLU output: mask, then {sum dy, sum dy*z}
+  const bool bwd = a.mask != nullptr || a.mscale != nullptr || a.mbits != nullptr;
+
+  // NP passes over row slices: in pass h every wave dumps its fragments mi in
+  // [h*TM/NP, (h+1)*TM/NP), i.e. tile rows wm*WM + h*HM + [0, HM), into a BM/NP-row buffer.
+  constexpr int HM = WM / NP, HT = TM / NP;
+#pragma unroll
+  for (int h = 0; h < NP; ++h) {
+  if (h) __syncthreads();         // every thread is done with pass h - 1
+#pragma unroll
+  for (int mi = 0; mi < HT; ++mi)
+#pragma unroll
+    for (int ni = 0; ni < TN; ++ni)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        Cs[(wm * HM + mi * 16 + fg * 4 + r) * CS_LD + wn * WN + ni * 16 + fr] = acc[h * HT + mi][ni][r];
+  __syncthreads();
+  constexpr int EPI_UNROLL = BM >= 256 ? 1 : 2;   // two rows' loads in flight (memory-bound epilogues)
+#pragma unroll EPI_UNROLL
+  for (int rr = rg; rr < BM / NP; rr += RG) {
+    const int r = (rr / HM) * WM + h * HM + (rr % HM);
+    const int m = m0 + r;
+    int64_t pix;
+    if constexpr (HALO) {
+      const int pr = (int)fdiv((uint32_t)r, a.fd_tw), pc = r - pr * a.tw;
+      const int oh = hh0 + pr, ow = hw0 + pc;
+      if (r >= a.th * a.tw || oh >= ph.P || ow >= ph.Q || !cvalid) continue;
+      pix = ((int64_t)hn * a.OH + oh * a.so + ph.oh0) * a.OW + ow * a.so + ph.ow0;
+    } else {
+      if (m >= M || !cvalid) continue;
+    }
+    float v[8];
+    const f32x4 v0 = *reinterpret_cast<const f32x4*>(Cs + rr * CS_LD + cg * 8);
+    const f32x4 v1 = *reinterpret_cast<const f32x4*>(Cs + rr * CS_LD + cg * 8 + 4);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) { v[e] = v0[e] + bias[e]; v[e + 4] = v1[e] + bias[e + 4]; }
+    if (a.stats && !bwd) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float rv = stored<T>(v[e]);
+        s1[e] += rv;
+        s2[e] += rv * rv;
+      }
+    }
+    if (a.scale) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = v[e] * a.scale[c0 + e] + a.shift[c0 + e];
+    }
+    if constexpr (!HALO) {
+      const uint32_t n_img = fdiv((uint32_t)m, ph.fdPQ);
+      const uint32_t rem = (uint32_t)m - n_img * PQ;
+      const uint32_t p = fdiv(rem, ph.fdQ);
+      const uint32_t q = rem - p * ph.Q;
+      pix = ((int64_t)n_img * a.OH + (int)p * a.so + ph.oh0) * a.OW + (int)q * a.so + ph.ow0;
+    }
+    if (a.res) {
+      float rr8[8];
+      load8(static_cast<const T*>(a.res) + pix * a.ldres + a.resoff + c0, rr8);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] += rr8[e];
+    }
+    if (a.relu) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.f);
+    }
+    if (bwd) {
+      float zz[8];
+      if (a.z) load8(static_cast<const T*>(a.z) + pix * a.ldz + a.zoff + c0, zz);
+      if (a.mbits) {
+        const uint32_t b = a.mbits[pix * (a.Kout >> 3) + (c0 >> 3)];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = (b >> e) & 1u ? v[e] : 0.f;
+      } else if (a.mask) {
+        float yy[8];
+        load8(static_cast<const T*>(a.mask) + pix * a.ldmask + a.maskoff + c0, yy);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = yy[e] > 0.f ? v[e] : 0.f;
+      } else {   // same fma as the forward BN-apply -> same sign as y
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = zz[e] * a.mscale[c0 + e] + a.mshift[c0 + e] > 0.f ? v[e] : 0.f;
+      }
+      if (a.stats) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float rv = stored<T>(v[e]);   // statistics of the stored gradient
+          s1[e] += rv;
+          s2[e] += rv * zz[e];
+        }
+        if (a.z2) {
+          load8(static_cast<const T*>(a.z2) + pix * a.ldz2 + a.z2off + c0, zz);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) s3[e] += stored<T>(v[e]) * zz[e];
+        }
+      }
+    }
+    if (a.vec_store) {
+      if (a.out_f32) {
+        float* yp = reinterpret_cast<float*>(a.y) + pix * a.ldy + a.yoff + c0;
+        *reinterpret_cast<f32x4*>(yp) = f32x4{v[0], v[1], v[2], v[3]};
+        *reinterpret_cast<f32x4*>(yp + 4) = f32x4{v[4], v[5], v[6], v[7]};
+      } else {
+        uint16_t* yp = reinterpret_cast<uint16_t*>(a.y) + pix * a.ldy + a.yoff + c0;
+        if (a.nt_store) __builtin_nontemporal_store(pack8(v), reinterpret_cast<u32x4*>(yp));
+        else *reinterpret_cast<u32x4*>(yp) = pack8(v);
+      }
+    } else {   // narrow / unaligned output (e.g. the 1-channel UNet head written as fp32 [N,1,H,W])
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        if (c0 + e >= a.kvalid) break;
+        if (a.out_f32) reinterpret_cast<float*>(a.y)[pix * a.ldy + a.yoff + c0 + e] = v[e];
+        else reinterpret_cast<uint16_t*>(a.y)[pix * a.ldy + a.yoff + c0 + e] = f2bf(v[e]);
+      }
+    }
+  }
+  }
+
+  if (a.stats) {
+    __syncthreads();
+    float* red = reinterpret_cast<float*>(smem);
+    const int ns = a.nstat;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      red[(rg * 3 + 0) * BN + cg * 8 + e] = s1[e];
+      red[(rg * 3 + 1) * BN + cg * 8 + e] = s2[e];
+      red[(rg * 3 + 2) * BN + cg * 8 + e] = s3[e];
+    }
+    __syncthreads();
+    if (tid < BN && n0 + tid < a.Kout) {
+      float t1 = 0.f, t2 = 0.f, t3 = 0.f;
+      for (int g = 0; g < RG; ++g) {
+        t1 += red[(g * 3 + 0) * BN + tid];
+        t2 += red[(g * 3 + 1) * BN + tid];
+        t3 += red[(g * 3 + 2) * BN + tid];
+      }
+      float* st = a.stats + (int64_t)(ph.tile_base + mt) * ns * a.Kout + n0 + tid;
+      st[0] = t1;
+      st[a.Kout] = t2;
+      if (ns > 2) st[2 * a.Kout] = t3;
+    }
+  }
+}
+
+// ---- the single-stage 4-wave kernel --------------------------------------------------------------
+// Tile: BM (pixels) x BN (channels) x BK (reduction), 256 threads = 4 waves in WGM x (4 / WGM), each
+// wave (BM/WGM) x (BN/WGN) as 16x16 MFMA tiles.  The stage is issued, drained (vmcnt(0) +
+// barrier), read, and released by a second barrier: occupancy (3-4 blocks per CU) hides latency.
+// WGM = 4: the 256 x 64 tile of 64-channel layers (per-wave 64 x 64 instead of 64 x 32: a third
+// less LDS traffic per MFMA).
 // T: storage type of activations and weights -- uint16_t (bf16, v_mfma_f32_16x16x32_bf16) or float
 // (the fp32 precision path: v_mfma_f32_16x16x4_f32, four per 16-byte fragment; the LDS tile keeps
 // its 128-byte rows, i.e. 32 fp32 reduction elements per K-step instead of 64 bf16).
-// SKM: stream-K work decomposition (ConvArgs::sk_*): a persistent grid walks the flattened
-// (phase, tile, K-step) iterations; tiles split between blocks are summed by their last-arriving
-// contributor in a fixed block order (deterministic), exactly like the split-K combine.
 // HALO: 3x3 / stride-1 / pad-1 convolutions (forward and stride-1 data gradient) by 2-D output tiles
 // of th x tw pixels (th * tw <= 128 = BM) of one image: the (th + 2) x (tw + 2) input halo of a
 // 64-channel chunk is staged ONCE and the 9 taps are 9 K-steps over it (only the weight tile is
 // staged per tap) -- the K order is chunk-major, tap-minor.  An out-of-image halo pixel is staged as
 // zeros, which is the zero padding of every tap; no per-tap im2col decode exists.
-template <int BM, int BN, bool SMALLC, int STAGES, int NW, int WGM, int PRO = 0, typename ET = uint16_t,
-          bool SKM = false, bool REPI = false, bool HALO = false>
-__global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(STAGES == 1 && BM * BN <= 16384 ? (BM * BN == 16384 ? DLMPI_W128 : 3) : 2, 8))) void conv_igemm_kernel(const ConvArgs a) {
+template <int BM, int BN, bool SMALLC, int WGM, int PRO = 0, typename ET = uint16_t, bool HALO = false>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BM * BN <= 16384 ? 3 : 2, 8))) void conv_igemm_kernel(const ConvArgs a) {
+  constexpr int NW = 4;
   constexpr int NT = 64 * NW;                 // threads
   constexpr int WGN = NW / WGM;               // wave grid WGM x WGN
   using T = ET;                               // element (storage) type
@@ -74,24 +307,14 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(STAGES 
   constexpr int RP = NT / 8;                  // tile rows staged per pass (8 lanes per 128-B row)
   constexpr int AL = BM / RP, BL = BN / RP;   // 16-byte pieces per thread per tile
   constexpr int HALO_ROWS = 192;              // (th + 2) * (tw + 2) <= 192 (host-checked)
-  static_assert(!HALO || (BM == 128 && NW == 4 && !SMALLC && STAGES == 1 && PRO == 0 && !SKM && !REPI &&
-                          sizeof(ET) == 2), "halo mode: 128-pixel bf16 single-stage tiles");
+  static_assert(!HALO || (BM == 128 && !SMALLC && PRO == 0 && sizeof(ET) == 2), "halo mode: 128-pixel bf16 tiles");
   constexpr int HL = HALO ? HALO_ROWS * 128 / (16 * 64 * NW) : 1;   // halo pieces per thread
   constexpr int A_BYTES = (HALO ? HALO_ROWS : BM) * 128, B_BYTES = BN * 128;
-  static_assert(PRO == 0 || (!SMALLC && STAGES == 1), "operand prologue: regular channels, single stage");
+  static_assert(PRO == 0 || !SMALLC, "operand prologue: regular channels");
   constexpr int Z_BYTES = PRO >= 2 ? A_BYTES : 0;   // the second prologue operand, staged like A
-  constexpr int SB = A_BYTES + B_BYTES + Z_BYTES;   // bytes per stage: [A | B | Z]
-  constexpr int STAGE_BYTES = STAGES * SB;
-  constexpr int CS_LD = BN + 4;
-  constexpr int NP = BM >= 128 ? BM / 64 : 1;            // epilogue passes of <= 64 tile rows
-  static_assert(WM % (16 * NP) == 0 || NP == 1, "epilogue pass must split every wave's rows evenly");
-  constexpr int EPI_BYTES = (BM / NP) * CS_LD * 4;
-  constexpr int RED_BYTES = (NT / (BN / 8)) * 3 * BN * 4;    // stats combine
-  // REPI: no fp32 tile staging; [WGM][3][BN] floats of statistics, or the in-launch finalize's
-  // 2 x NT doubles + flag
-  constexpr int REPI_BYTES = (WGM * 3 * BN * 4 > 2 * NT * 8 + 16) ? WGM * 3 * BN * 4 : 2 * NT * 8 + 16;
-  constexpr int EPI_NEED = REPI ? REPI_BYTES : (EPI_BYTES > RED_BYTES ? EPI_BYTES : RED_BYTES);
-  constexpr int SMEM = STAGE_BYTES > EPI_NEED ? STAGE_BYTES : EPI_NEED;
+  constexpr int SB = A_BYTES + B_BYTES + Z_BYTES;   // bytes of the stage: [A | B | Z]
+  constexpr int EPI_NEED = EpiSmem<BM, BN, NT, WM>::bytes;
+  constexpr int SMEM = SB > EPI_NEED ? SB : EPI_NEED;
   __shared__ __attribute__((aligned(16))) char smem[SMEM];
 
   const int tid = threadIdx.x, lane = tid & 63;
@@ -101,34 +324,10 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(STAGES 
   const int jc = (tid & 7) ^ ((tid >> 4) & 7);        // swizzled 16-B chunk this lane fetches
   const char* zp = reinterpret_cast<const char*>(g_zero_page);
 
-  // stream-K: this block's iteration range (XCD-remapped so one XCD walks a contiguous range)
-  int sk_lb = 0, sk_it = 0, sk_end = 0;
-  if constexpr (SKM) {
-    sk_lb = (int)xcd_remap(blockIdx.x, gridDim.x);
-    sk_it = sk_lb * a.sk_per;
-    sk_end = min(a.sk_total, sk_it + a.sk_per);
-  }
-  for (;;) {   // SKM: one pass per tile segment of the range; otherwise exactly one pass
-  int zph, seg_k0 = 0, seg_k1 = 0, seg_start = 0;
-  uint32_t bid;
-  if constexpr (SKM) {
-    if (sk_it >= sk_end) break;
-    zph = 0;
-    while (zph + 1 < a.nphase && sk_it >= a.sk_base[zph + 1]) ++zph;
-    const int nkz = a.ph[zph].ksteps;
-    const int loc = sk_it - a.sk_base[zph];
-    const int tl = loc / nkz;
-    seg_k0 = loc - tl * nkz;
-    seg_k1 = min(nkz, seg_k0 + (sk_end - sk_it));
-    seg_start = sk_it;
-    sk_it += seg_k1 - seg_k0;
-    bid = (uint32_t)tl;
-  } else {
-    zph = blockIdx.z;
-    const uint32_t nwg0 = (uint32_t)a.ph[zph].mtiles * (uint32_t)a.ntiles;
-    if (blockIdx.x >= nwg0) return;
-    bid = xcd_remap(blockIdx.x, nwg0);
-  }
+  const int zph = blockIdx.z;
+  const uint32_t nwg0 = (uint32_t)a.ph[zph].mtiles * (uint32_t)a.ntiles;
+  if (blockIdx.x >= nwg0) return;
+  const uint32_t bid = xcd_remap(blockIdx.x, nwg0);
   const ConvPhase ph = a.ph[zph];
   const int mt = bid / a.ntiles, nt = bid - mt * a.ntiles;
   const int m0 = mt * BM, n0 = nt * BN;
@@ -143,7 +342,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(STAGES 
   const int PQ = ph.P * ph.Q;
   const int M = a.Nimg * PQ;
 
-  // ---- per-thread row state (kept compact: the 256-row tile has 8 rows per thread) ----------
+  // ---- per-thread row state (kept compact: the 256-row tile has 4 rows per thread) ----------
   int a_hw[AL], a_pix[AL];                            // (h << 16) | w of the row's input origin
   uint32_t a_okm = 0;                                 // bit i: GEMM row valid
 #pragma unroll
@@ -225,8 +424,8 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(STAGES 
     toff = (dh + 1) * hwd + (dw + 1);
   };
 
-  auto issue = [&](int buf, int ks) {
-    char* As = smem + buf * SB;
+  auto issue = [&](int ks) {
+    char* As = smem;
     char* Bs = As + A_BYTES;
     if constexpr (HALO) {
       if (need_halo) {
@@ -295,9 +494,9 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(STAGES 
   // out-of-image taps / rows past M hold zeros and are left alone.  Same fma order and bf16
   // rounding as the standalone kernels it replaces (bn_apply_kernel / bn_bwd_apply_kernel), so the
   // fused and the unfused schedules are bit-identical.
-  auto prologue = [&](int buf) {
+  auto prologue = [&]() {
     if constexpr (PRO != 0) {
-      char* As = smem + buf * SB;
+      char* As = smem;
       const int c = c_cur + 8 * jc;
       f32x4 k0a, k0b, k1a, k1b, k2a, k2b, kra, krb;
       if constexpr (PRO == 1 || PRO == 3) {
@@ -418,10 +617,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(STAGES 
   };
   // split-K (small grids): block y of a.splitk reduces K-steps [kbeg, kend)
   int kbeg = 0, kend = nk;
-  if constexpr (SKM) {
-    kbeg = seg_k0;
-    kend = seg_k1;
-  } else if (a.splitk > 1) {
+  if (a.splitk > 1) {
     const int per = (nk + a.splitk - 1) / a.splitk;
     kbeg = min(nk, (int)blockIdx.y * per);
     kend = min(nk, kbeg + per);
@@ -437,25 +633,18 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(STAGES 
       c_cur = (kbeg - t_cur * cps) * BK;
       tap_setup(t_cur);
     }
-    issue(0, kbeg);
+    issue(kbeg);
     __syncthreads();
-    prologue(0);
+    prologue();
   }
   for (int ks = kbeg; ks < kend; ++ks) {
-    int cur = 0;
-    if constexpr (STAGES == 2) {
-      cur = (ks - kbeg) & 1;
-      if (ks + 1 < kend) {
-        advance();
-        issue(cur ^ 1, ks + 1);
-      }
-    } else if (ks > kbeg) {
+    if (ks > kbeg) {
       advance();
-      issue(0, ks);
+      issue(ks);
       __syncthreads();   // this stage landed (vmcnt(0) + barrier)
-      prologue(0);
+      prologue();
     }
-    const char* As = smem + cur * SB;
+    const char* As = smem;
     const char* Bs = As + A_BYTES;
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
@@ -479,13 +668,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(STAGES 
 #pragma unroll
         for (int ni = 0; ni < TN; ++ni) {
           if constexpr (sizeof(T) == 2) {
-            // REPI: D^T (rows = output channels, columns = pixels) -- the 16x16x32 operand layouts of
-            // A and B are symmetric, so swapping them transposes the tile: every lane then holds 4
-            // consecutive CHANNELS of one pixel, i.e. a contiguous 8-byte piece of an NHWC row
-            if constexpr (REPI)
-              acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[ni], af[mi], acc[mi][ni], 0, 0, 0);
-            else
-              acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[mi], bfr[ni], acc[mi][ni], 0, 0, 0);
+            acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[mi], bfr[ni], acc[mi][ni], 0, 0, 0);
           } else {
             // the lane's 16-byte chunk holds reduction elements 4 fg + j (j < 4) of this half-step:
             // MFMA j reduces element j of every lane group -- a fixed permutation of the K order,
@@ -496,464 +679,219 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(STAGES 
           }
         }
     }
-    // STAGES 2: waits for this wave's glds of tile ks+1, then all waves -> buffers swap;
-    // STAGES 1: every wave is done reading the stage before it is overwritten
-    __syncthreads();
+    __syncthreads();   // every wave is done reading the stage before it is overwritten
   }
 
-  // ---- split-K combine (cdna_hip_programming.md "In-launch split-K reduction") --------------
-  // Every slice stores its fp32 accumulators (fragment layout) to its slab, publishes with an
-  // agent-scope release + ticket; the tile's last arriver acquires and sums ALL slices' slabs in
-  // slice order (deterministic whichever block arrives last), then runs the normal epilogue.
-  if constexpr (SKM) {
-    if (kbeg != 0 || kend != nk) {
-      // partial tile: store this block's accumulators write-through (sc1) into its slab slot
-      // (0: the range's first segment, 1: its last), take a ticket; the last contributor sums the
-      // slots of every contributing block in block order (deterministic) and runs the epilogue
-      constexpr int NF = TM * TN;
-      const int slot = seg_start == sk_lb * a.sk_per ? 0 : 1;
-      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-          a.sk_slab + (int64_t)(sk_lb * 2 + slot) * NF * NT * 4, (short)0, NF * NT * 16, 0x00020000);
+  if (a.splitk > 1 && !splitk_combine<NT, TM * TN>(a, &acc[0][0], smem, tid, mt, nt)) return;
+  conv_epilogue<BM, BN, NT, WGM, WGN, T, HALO>(a, ph, acc, smem, tid, m0, n0, mt, hn, hh0, hw0);
+}
+
+// ---- the pipelined 8-wave kernel -----------------------------------------------------------------
+// BM x BN x 64 tiles, 512 threads = 8 waves in WGM x WGN, one block per CU, bf16, C % 64 == 0, one
+// phase per blockIdx.z (forward convs, dgrad sub-pixel phases), no operand prologue, no split-K.
+// K loop (STAGES LDS slots of one K-step each, slot of step k = k mod STAGES):
+//     wait  until this wave's DMA of step k has landed (counted vmcnt: the STAGES - 2 younger steps'
+//           DMAs stay in flight) and its fragment reads of step k - 1 have returned (lgkmcnt(0))
+//     barrier  -> every wave's step-k DMA has landed: slot k is readable (RAW); every wave is done
+//              reading slot k - 1 = slot (k + STAGES - 1) mod STAGES: it may be refilled (WAR)
+//     issue the DMA of step k + STAGES - 1 into that slot
+//     MFMAs of step k from slot k
+// The raw s_barrier (not __syncthreads, whose workgroup fence drains vmcnt to 0 and with it the
+// prefetch) is bracketed by "memory"-clobbering asm statements, so neither the fragment reads nor the
+// DMA issue can be moved across it.
+// VAR (issue placement / priority; A/B in benchmarks/conv_lab): 0 = all DMAs of the next step right
+// after the barrier; 1 = the upper half of the waves issues after its first K-half of MFMAs (the two
+// waves of a SIMD then issue at different times); 2 = A pieces before the first K-half, B pieces
+// before the second; 3 = s_setprio(1) around the MFMA clusters.
+// BM need not be a multiple of the staging pass (224 = 2 x 7 fragments): rows past BM stage zeros.
+template <int BM, int BN, int WGM, int WGN, int STAGES, int VAR = 0>
+__global__ __launch_bounds__(64 * WGM * WGN) __attribute__((amdgpu_waves_per_eu(2, 2))) void conv_pipe_kernel(const ConvArgs a) {
+  constexpr int NW = WGM * WGN;
+  constexpr int NT = 64 * NW;
+  constexpr int WM = BM / WGM, WN = BN / WGN;
+  constexpr int TM = WM / 16, TN = WN / 16;
+  static_assert(WM % 16 == 0 && WN % 16 == 0, "whole fragments");
+  constexpr int RP = NT / 8;                  // tile rows staged per pass (8 lanes per 128-B row)
+  static_assert(BN % RP == 0, "staging: whole passes");
+  constexpr int AL = (BM + RP - 1) / RP, BL = BN / RP;   // 16-byte pieces per thread per K-step
+  constexpr int NLD = AL + BL;                // DMA instructions per thread per K-step
+  static_assert(STAGES == 2 || STAGES == 3, "2 or 3 slots");
+  constexpr int A_BYTES = AL * RP * 128, B_BYTES = BN * 128;
+  constexpr int SB = A_BYTES + B_BYTES;
+  constexpr int EPI_NEED = EpiSmem<BM, BN, NT, WM>::bytes;
+  constexpr int SMEM = STAGES * SB > EPI_NEED ? STAGES * SB : EPI_NEED;
+  static_assert(SMEM <= 160 * 1024, "LDS");
+  __shared__ __attribute__((aligned(16))) char smem[SMEM];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wid / WGN, wn = wid % WGN;
+  const int lrow = tid >> 3;
+  const int jc = (tid & 7) ^ ((tid >> 4) & 7);
+  const char* zp = reinterpret_cast<const char*>(g_zero_page);
+
+  const int zph = blockIdx.z;
+  const uint32_t nwg0 = (uint32_t)a.ph[zph].mtiles * (uint32_t)a.ntiles;
+  if (blockIdx.x >= nwg0) return;
+  const uint32_t bid = xcd_remap(blockIdx.x, nwg0);
+  const ConvPhase ph = a.ph[zph];
+  const int mt = bid / a.ntiles, nt = bid - mt * a.ntiles;
+  const int m0 = mt * BM, n0 = nt * BN;
+  const int PQ = ph.P * ph.Q;
+  const int M = a.Nimg * PQ;
+
+  int a_hw[AL], a_pix[AL];
+  uint32_t a_okm = 0;
 #pragma unroll
-      for (int i = 0; i < NF; ++i)
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[i / TN][i % TN]), rs,
-                                               (i * NT + tid) * 16, 0, 16 /* sc1 */);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-      const int s_it = a.sk_base[zph] + (int)bid * nk;       // the tile's iteration range [s_it, s_it + nk)
-      const int b_lo = s_it / a.sk_per, b_hi = (s_it + nk - 1) / a.sk_per;
-      const int gt = a.sk_tbase[zph] + (int)bid;
-      int* flag = reinterpret_cast<int*>(smem);
-      if (tid == 0)
-        flag[0] = __hip_atomic_fetch_add(a.sk_tk + gt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == b_hi - b_lo;
-      __syncthreads();
-      if (!flag[0]) continue;
-      if (tid == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __hip_atomic_store(a.sk_tk + gt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-      __syncthreads();
-#pragma unroll
-      for (int i = 0; i < NF; ++i) acc[i / TN][i % TN] = f32x4{0.f, 0.f, 0.f, 0.f};
-      for (int b = b_lo; b <= b_hi; ++b) {
-        const int sl = b * a.sk_per >= s_it ? 0 : 1;
-        const f32x4* src = reinterpret_cast<const f32x4*>(a.sk_slab) + (int64_t)(b * 2 + sl) * NF * NT + tid;
-#pragma unroll
-        for (int i = 0; i < NF; ++i) acc[i / TN][i % TN] += src[(int64_t)i * NT];
-      }
-      __syncthreads();   // flag (LDS) is reused by the epilogue staging
-    }
-  } else if (a.splitk > 1) {
-    constexpr int NF = TM * TN;
-    const int S = a.splitk;
-    // unique over phases (blockIdx.z): ConvTranspose phases all have tile_base 0
-    const int64_t tile = (int64_t)blockIdx.z * gridDim.x + (int64_t)mt * a.ntiles + nt;
-    f32x4* slab = reinterpret_cast<f32x4*>(a.sk_slab) + (tile * S + blockIdx.y) * NF * NT + tid;
-#pragma unroll
-    for (int i = 0; i < NF; ++i) slab[(int64_t)i * NT] = acc[i / TN][i % TN];
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    int* flag = reinterpret_cast<int*>(smem);   // the one LDS array (no second __shared__ object)
-    if (tid == 0) {
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      flag[0] = __hip_atomic_fetch_add(a.sk_tk + tile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == S - 1;
-    }
-    __syncthreads();
-    if (!flag[0]) return;
-    if (tid == 0) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __hip_atomic_store(a.sk_tk + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    __syncthreads();
-    const f32x4* base = reinterpret_cast<const f32x4*>(a.sk_slab) + tile * S * NF * NT + tid;
-#pragma unroll
-    for (int i = 0; i < NF; ++i) acc[i / TN][i % TN] = f32x4{0.f, 0.f, 0.f, 0.f};
-    for (int sp = 0; sp < S; ++sp)
-#pragma unroll
-      for (int i = 0; i < NF; ++i) acc[i / TN][i % TN] += base[((int64_t)sp * NF + i) * NT];
-    __syncthreads();   // flag (LDS) is reused by the epilogue staging
+  for (int i = 0; i < AL; ++i) {
+    const int m = m0 + lrow + RP * i;
+    if (m < M && lrow + RP * i < BM) a_okm |= 1u << i;
+    const uint32_t mm = m < M ? (uint32_t)m : 0u;
+    const uint32_t n_img = fdiv(mm, ph.fdPQ);
+    const uint32_t rem = mm - n_img * PQ;
+    const uint32_t p = fdiv(rem, ph.fdQ);
+    const uint32_t q = rem - p * ph.Q;
+    const int h = (int)p * a.sa, w = (int)q * a.sa;
+    a_hw[i] = (h << 16) | w;
+    a_pix[i] = ((int)n_img * a.H + h) * a.W + w;
   }
+  const char* xlane = reinterpret_cast<const char*>(a.x) + 2 * ((int64_t)a.xoff + 8 * jc);
+  const char* b_base = reinterpret_cast<const char*>(a.w) + 2 * ((int64_t)(n0 + lrow) * a.ldw + 8 * jc);
+  const int64_t b_step = (int64_t)2 * RP * a.ldw;
+  uint32_t b_okm = 0;
+#pragma unroll
+  for (int i = 0; i < BL; ++i)
+    if (n0 + lrow + RP * i < a.Kout) b_okm |= 1u << i;
 
-  // ---- register-direct epilogue (REPI) --------------------------------------------------------
-  // No LDS staging of the fp32 tile: lane (fr, fg) holds, for pixel tile mi and channel tile ni,
-  // output[pixel wm*WM + 16 mi + fr][channels wn*WN + 16 ni + 4 fg + 0..3] (D^T fragments), so the
-  // epilogue math runs in registers and every lane stores / loads 8-byte channel quads directly.
-  // BatchNorm partial sums: per lane over its pixels, then over the 16 lanes of a DPP row
-  // (row_shr prefix chain, fixed order), then over the wave rows through a small LDS array.
-  if constexpr (REPI) {
-    static_assert(sizeof(T) == 2 && PRO == 0, "register epilogue: bf16, no operand prologue");
-    const int fr = lane & 15, fg = lane >> 4;
-    const bool bwd = a.mask != nullptr || a.mscale != nullptr || a.mbits != nullptr;
-    const int ns = a.nstat;
-    float s1[TN][4], s2[TN][4], s3[TN][4];
+  const int C = a.C;
+  const int nk = ph.ksteps;
+  uint32_t a_off[AL];
+  uint32_t a_vm = 0;
+  int t_cur = 0, c_cur = 0, wtC2 = 0;
+  auto tap_setup = [&](int t) {
+    const int tr = (int)fdiv((uint32_t)t, ph.fdTs);
+    const int ts = t - tr * ph.Ts;
+    const int dh = ph.dh0 + tr * ph.dhs, dw = ph.dw0 + ts * ph.dws;
+    const int wt = (ph.wr0 + tr * ph.wrs) * a.S + (ph.ws0 + ts * ph.wss);
+    wtC2 = wt * C * 2;
+    const int doff = dh * a.W + dw;
+    a_vm = 0;
 #pragma unroll
-    for (int ni = 0; ni < TN; ++ni)
+    for (int i = 0; i < AL; ++i) {
+      const int ih = (a_hw[i] >> 16) + dh, iw = (a_hw[i] & 0xffff) + dw;
+      const bool ok = ((a_okm >> i) & 1) && (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W;
+      if (ok) a_vm |= 1u << i;
+      a_off[i] = (uint32_t)(a_pix[i] + doff) * (uint32_t)a.ldx;
+    }
+  };
+  auto advance = [&]() {
+    c_cur += 64;
+    if (c_cur >= C) {
+      c_cur = 0;
+      ++t_cur;
+      tap_setup(t_cur);
+    }
+  };
+  auto issue_a = [&](int slot) {
+    char* As = smem + slot * SB;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) { s1[ni][r] = 0.f; s2[ni][r] = 0.f; s3[ni][r] = 0.f; }
-    auto ld4 = [](const void* base, int64_t off) -> f32x4 {
-      const u32x2 q = *reinterpret_cast<const u32x2*>(static_cast<const uint16_t*>(base) + off);
-      return f32x4{__uint_as_float(q[0] << 16), __uint_as_float(q[0] & 0xffff0000u), __uint_as_float(q[1] << 16),
-                   __uint_as_float(q[1] & 0xffff0000u)};
-    };
+    for (int i = 0; i < AL; ++i) {
+      const char* s = ((a_vm >> i) & 1) ? xlane + 2 * ((uint64_t)a_off[i] + c_cur) : zp;
+      glds16(s, As + (RP * i + 8 * wid) * 128);
+    }
+  };
+  auto issue_b = [&](int slot) {
+    char* Bs = smem + slot * SB + A_BYTES;
 #pragma unroll
-    for (int mi = 0; mi < TM; ++mi) {
-      const int m = m0 + wm * WM + mi * 16 + fr;
-      if (m >= M) continue;
-      const uint32_t n_img = fdiv((uint32_t)m, ph.fdPQ);
-      const uint32_t rem = (uint32_t)m - n_img * PQ;
-      const uint32_t p = fdiv(rem, ph.fdQ);
-      const uint32_t q = rem - p * ph.Q;
-      const int64_t pix = ((int64_t)n_img * a.OH + (int)p * a.so + ph.oh0) * a.OW + (int)q * a.so + ph.ow0;
+    for (int i = 0; i < BL; ++i) {
+      const char* s = ((b_okm >> i) & 1) ? b_base + i * b_step + wtC2 + 2 * c_cur : zp;
+      glds16(s, Bs + (RP * i + 8 * wid) * 128);
+    }
+  };
+  auto issue = [&](int slot) {
+    issue_a(slot);
+    issue_b(slot);
+  };
+
+  f32x4 acc[TM][TN];
 #pragma unroll
-      for (int ni = 0; ni < TN; ++ni) {
-        const int c = n0 + wn * WN + ni * 16 + 4 * fg;
-        if (c >= a.Kout) continue;   // Kout % 8 == 0: a quad is all in or all out
-        f32x4 v = acc[mi][ni];
-        if (a.bias) v += *reinterpret_cast<const f32x4*>(a.bias + c);
-        if (a.stats && !bwd) {
+  for (int mi = 0; mi < TM; ++mi)
 #pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const float rv = stored<T>(v[r]);
-            s1[ni][r] += rv;
-            s2[ni][r] += rv * rv;
-          }
-        }
-        if (a.scale) v = v * *reinterpret_cast<const f32x4*>(a.scale + c) + *reinterpret_cast<const f32x4*>(a.shift + c);
-        if (a.res) v += ld4(a.res, pix * a.ldres + a.resoff + c);
-        if (a.relu) {
-#pragma unroll
-          for (int r = 0; r < 4; ++r) v[r] = fmaxf(v[r], 0.f);
-        }
-        if (bwd) {
-          f32x4 zz = f32x4{0.f, 0.f, 0.f, 0.f};
-          if (a.z) zz = ld4(a.z, pix * a.ldz + a.zoff + c);
-          if (a.mbits) {
-            const uint32_t b = a.mbits[pix * (a.Kout >> 3) + (c >> 3)] >> (c & 7);
-#pragma unroll
-            for (int r = 0; r < 4; ++r) v[r] = (b >> r) & 1u ? v[r] : 0.f;
-          } else if (a.mask) {
-            const f32x4 yy = ld4(a.mask, pix * a.ldmask + a.maskoff + c);
-#pragma unroll
-            for (int r = 0; r < 4; ++r) v[r] = yy[r] > 0.f ? v[r] : 0.f;
-          } else {   // same fma as the forward BN-apply -> same sign as y
-            const f32x4 ms = *reinterpret_cast<const f32x4*>(a.mscale + c);
-            const f32x4 mh = *reinterpret_cast<const f32x4*>(a.mshift + c);
-#pragma unroll
-            for (int r = 0; r < 4; ++r) v[r] = zz[r] * ms[r] + mh[r] > 0.f ? v[r] : 0.f;
-          }
-          if (a.stats) {
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              const float rv = stored<T>(v[r]);
-              s1[ni][r] += rv;
-              s2[ni][r] += rv * zz[r];
-            }
-            if (a.z2) {
-              const f32x4 z2 = ld4(a.z2, pix * a.ldz2 + a.z2off + c);
-#pragma unroll
-              for (int r = 0; r < 4; ++r) s3[ni][r] += stored<T>(v[r]) * z2[r];
-            }
-          }
-        }
-        if (a.out_f32) {
-          *reinterpret_cast<f32x4*>(reinterpret_cast<float*>(a.y) + pix * a.ldy + a.yoff + c) = v;
-        } else {
-          const u32x2 pk = u32x2{pack2bf(v[0], v[1]), pack2bf(v[2], v[3])};
-          u32x2* yp = reinterpret_cast<u32x2*>(reinterpret_cast<uint16_t*>(a.y) + pix * a.ldy + a.yoff + c);
-          if (a.nt_store) __builtin_nontemporal_store(pk, yp);
-          else *yp = pk;
-        }
+    for (int ni = 0; ni < TN; ++ni) acc[mi][ni] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int fr = lane & 15, fg = lane >> 4;
+  // per-lane fragment row byte offsets (A rows wm*WM + 16 mi + fr, B rows wn*WN + 16 ni + fr) and
+  // the swizzle term of each: ((r >> 1) & 7) is the same for every mi (16 | row step)
+  const int sw = (fr >> 1) & 7;
+  const int a_row0 = (wm * WM + fr) * 128, b_row0 = A_BYTES + (wn * WN + fr) * 128;
+
+  if (nk > 0) {
+    tap_setup(0);
+    issue(0);
+    if constexpr (STAGES == 3) {
+      if (nk > 1) {
+        advance();
+        issue(1);
       }
     }
-    if (a.stats) {
-      // sum over the 16 pixel lanes of each DPP row: lane 15 of the row ends with the full sum
-      auto row_sum = [](float v) {
-        v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x111, 0xf, 0xf, true));
-        v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x112, 0xf, 0xf, true));
-        v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x114, 0xf, 0xf, true));
-        v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x118, 0xf, 0xf, true));
-        return v;
-      };
-      float* red = reinterpret_cast<float*>(smem);   // [WGM][3][BN]
-      __syncthreads();   // the K loop's last LDS reads are done
-#pragma unroll
-      for (int ni = 0; ni < TN; ++ni)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float t1 = row_sum(s1[ni][r]), t2 = row_sum(s2[ni][r]);
-          const float t3 = ns > 2 ? row_sum(s3[ni][r]) : 0.f;
-          if (fr == 15) {
-            const int cl = wn * WN + ni * 16 + 4 * fg + r;
-            red[(wm * 3 + 0) * BN + cl] = t1;
-            red[(wm * 3 + 1) * BN + cl] = t2;
-            red[(wm * 3 + 2) * BN + cl] = t3;
-          }
-        }
-      __syncthreads();
-      const bool fin = !SKM && a.fin_on;
-      if (tid < BN && n0 + tid < a.Kout) {
-        float t1 = 0.f, t2 = 0.f, t3 = 0.f;
-#pragma unroll
-        for (int g = 0; g < WGM; ++g) {
-          t1 += red[(g * 3 + 0) * BN + tid];
-          t2 += red[(g * 3 + 1) * BN + tid];
-          t3 += red[(g * 3 + 2) * BN + tid];
-        }
-        float* st = a.stats + (int64_t)(ph.tile_base + mt) * ns * a.Kout + n0 + tid;
-        if (fin) {
-          st_sc1(st, t1);
-          st_sc1(st + a.Kout, t2);
-          if (ns > 2) st_sc1(st + 2 * a.Kout, t3);
-        } else {
-          st[0] = t1;
-          st[a.Kout] = t2;
-          if (ns > 2) st[2 * a.Kout] = t3;
-        }
-      }
-      if (fin) {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        fin_in_launch<NT, BN>(a, a.stats, ns, ph.tile_base + mt, nt, n0, reinterpret_cast<double*>(smem),
-                              reinterpret_cast<int*>(smem + 2 * NT * sizeof(double)));
-      }
-    }
-  } else {
-  // ---- epilogue ------------------------------------------------------------------------------
-  float* Cs = reinterpret_cast<float*>(smem);
-
-  constexpr int CG = BN / 8;       // channel groups of 8
-  constexpr int RG = NT / CG;      // row groups
-  const int cg = tid % CG, rg = tid / CG;
-  const int c0 = n0 + cg * 8;
-  const bool cvalid = c0 < a.Kout;
-  float bias[8];
-#pragma unroll
-  for (int e = 0; e < 8; ++e) bias[e] = 0.f;
-  if (cvalid && a.bias) {
-#pragma unroll
-    for (int e = 0; e < 8; ++e) bias[e] = a.bias[c0 + e];
   }
-  float s1[8], s2[8], s3[8];
-#pragma unroll
-  for (int e = 0; e < 8; ++e) { s1[e] = 0.f; s2[e] = 0.f; s3[e] = 0.f; }
-  // gradient of a BN+ReLU output: mask, then {sum dy, sum dy*z}
-  const bool bwd = a.mask != nullptr || a.mscale != nullptr || a.mbits != nullptr;
-
-  // NP passes over row slices: in pass h every wave dumps its fragments mi in
-  // [h*TM/NP, (h+1)*TM/NP), i.e. tile rows wm*WM + h*HM + [0, HM), into a BM/NP-row buffer.
-  constexpr int HM = WM / NP, HT = TM / NP;
-#pragma unroll
-  for (int h = 0; h < NP; ++h) {
-  if (h) __syncthreads();         // every thread is done with pass 0
-#pragma unroll
-  for (int mi = 0; mi < HT; ++mi)
-#pragma unroll
-    for (int ni = 0; ni < TN; ++ni)
-#pragma unroll
-      for (int r = 0; r < 4; ++r)
-        Cs[(wm * HM + mi * 16 + fg * 4 + r) * CS_LD + wn * WN + ni * 16 + fr] = acc[h * HT + mi][ni][r];
-  __syncthreads();
-  constexpr int EPI_UNROLL = BM >= 256 ? 1 : 2;   // two rows' loads in flight (memory-bound epilogues)
-#pragma unroll EPI_UNROLL
-  for (int rr = rg; rr < BM / NP; rr += RG) {
-    const int r = (rr / HM) * WM + h * HM + (rr % HM);
-    const int m = m0 + r;
-    int64_t pix;
-    if constexpr (HALO) {
-      const int pr = (int)fdiv((uint32_t)r, a.fd_tw), pc = r - pr * a.tw;
-      const int oh = hh0 + pr, ow = hw0 + pc;
-      if (r >= a.th * a.tw || oh >= ph.P || ow >= ph.Q || !cvalid) continue;
-      pix = ((int64_t)hn * a.OH + oh * a.so + ph.oh0) * a.OW + ow * a.so + ph.ow0;
+  int rd = 0;   // slot of step ks
+  for (int ks = 0; ks < nk; ++ks) {
+    if constexpr (STAGES == 3) {
+      if (ks + 1 < nk) asm volatile("s_waitcnt vmcnt(%0)\n\ts_waitcnt lgkmcnt(0)" :: "n"(NLD) : "memory");
+      else asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)" ::: "memory");
     } else {
-      if (m >= M || !cvalid) continue;
+      asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)" ::: "memory");
     }
-    float v[8];
-    const f32x4 v0 = *reinterpret_cast<const f32x4*>(Cs + rr * CS_LD + cg * 8);
-    const f32x4 v1 = *reinterpret_cast<const f32x4*>(Cs + rr * CS_LD + cg * 8 + 4);
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    const bool more = ks + STAGES - 1 < nk;
+    int wr = rd + STAGES - 1;
+    if (wr >= STAGES) wr -= STAGES;
+    if (more) advance();
+    const bool late = VAR == 1 && wid >= NW / 2;   // wave-uniform
+    if (more && !late) {
+      if constexpr (VAR == 2) issue_a(wr);
+      else issue(wr);
+    }
+    const char* As = smem + rd * SB;
 #pragma unroll
-    for (int e = 0; e < 4; ++e) { v[e] = v0[e] + bias[e]; v[e + 4] = v1[e] + bias[e + 4]; }
-    if (a.stats && !bwd) {
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const float rv = stored<T>(v[e]);
-        s1[e] += rv;
-        s2[e] += rv * rv;
+    for (int kk = 0; kk < 2; ++kk) {
+      if (kk == 1 && more) {
+        if constexpr (VAR == 2) issue_b(wr);
+        else if (late) issue(wr);
+        asm volatile("" ::: "memory");
       }
+      bf16x8 af[TM], bfr[TN];
+      const int cb = ((kk * 4 + fg) ^ sw) << 4;
+#pragma unroll
+      for (int mi = 0; mi < TM; ++mi) af[mi] = *reinterpret_cast<const bf16x8*>(As + a_row0 + mi * 16 * 128 + cb);
+#pragma unroll
+      for (int ni = 0; ni < TN; ++ni) bfr[ni] = *reinterpret_cast<const bf16x8*>(As + b_row0 + ni * 16 * 128 + cb);
+      if constexpr (VAR == 3) __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int mi = 0; mi < TM; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < TN; ++ni)
+          acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[mi], bfr[ni], acc[mi][ni], 0, 0, 0);
+      if constexpr (VAR == 3) __builtin_amdgcn_s_setprio(0);
     }
-    if (a.scale) {
-#pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] = v[e] * a.scale[c0 + e] + a.shift[c0 + e];
-    }
-    if constexpr (!HALO) {
-      const uint32_t n_img = fdiv((uint32_t)m, ph.fdPQ);
-      const uint32_t rem = (uint32_t)m - n_img * PQ;
-      const uint32_t p = fdiv(rem, ph.fdQ);
-      const uint32_t q = rem - p * ph.Q;
-      pix = ((int64_t)n_img * a.OH + (int)p * a.so + ph.oh0) * a.OW + (int)q * a.so + ph.ow0;
-    }
-    if (a.res) {
-      float rr[8];
-      load8(static_cast<const T*>(a.res) + pix * a.ldres + a.resoff + c0, rr);
-#pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] += rr[e];
-    }
-    if (a.relu) {
-#pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.f);
-    }
-    if (bwd) {
-      float zz[8];
-      if (a.z) load8(static_cast<const T*>(a.z) + pix * a.ldz + a.zoff + c0, zz);
-      if (a.mbits) {
-        const uint32_t b = a.mbits[pix * (a.Kout >> 3) + (c0 >> 3)];
-#pragma unroll
-        for (int e = 0; e < 8; ++e) v[e] = (b >> e) & 1u ? v[e] : 0.f;
-      } else if (a.mask) {
-        float yy[8];
-        load8(static_cast<const T*>(a.mask) + pix * a.ldmask + a.maskoff + c0, yy);
-#pragma unroll
-        for (int e = 0; e < 8; ++e) v[e] = yy[e] > 0.f ? v[e] : 0.f;
-      } else {   // same fma as the forward BN-apply -> same sign as y
-#pragma unroll
-        for (int e = 0; e < 8; ++e) v[e] = zz[e] * a.mscale[c0 + e] + a.mshift[c0 + e] > 0.f ? v[e] : 0.f;
-      }
-      if (a.stats) {
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          const float rv = stored<T>(v[e]);   // statistics of the stored gradient
-          s1[e] += rv;
-          s2[e] += rv * zz[e];
-        }
-        if (a.z2) {
-          load8(static_cast<const T*>(a.z2) + pix * a.ldz2 + a.z2off + c0, zz);
-#pragma unroll
-          for (int e = 0; e < 8; ++e) s3[e] += stored<T>(v[e]) * zz[e];
-        }
-      }
-    }
-    if (a.vec_store) {
-      if (a.out_f32) {
-        float* yp = reinterpret_cast<float*>(a.y) + pix * a.ldy + a.yoff + c0;
-        *reinterpret_cast<f32x4*>(yp) = f32x4{v[0], v[1], v[2], v[3]};
-        *reinterpret_cast<f32x4*>(yp + 4) = f32x4{v[4], v[5], v[6], v[7]};
-      } else {
-        uint16_t* yp = reinterpret_cast<uint16_t*>(a.y) + pix * a.ldy + a.yoff + c0;
-        if (a.nt_store) __builtin_nontemporal_store(pack8(v), reinterpret_cast<u32x4*>(yp));
-        else *reinterpret_cast<u32x4*>(yp) = pack8(v);
-      }
-    } else {   // narrow / unaligned output (e.g. the 1-channel UNet head written as fp32 [N,1,H,W])
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        if (c0 + e >= a.kvalid) break;
-        if (a.out_f32) reinterpret_cast<float*>(a.y)[pix * a.ldy + a.yoff + c0 + e] = v[e];
-        else reinterpret_cast<uint16_t*>(a.y)[pix * a.ldy + a.yoff + c0 + e] = f2bf(v[e]);
-      }
-    }
+    rd = rd + 1 == STAGES ? 0 : rd + 1;
   }
-  }
-
-  if (a.stats) {
-    __syncthreads();
-    float* red = reinterpret_cast<float*>(smem);
-    const int ns = a.nstat;
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      red[(rg * 3 + 0) * BN + cg * 8 + e] = s1[e];
-      red[(rg * 3 + 1) * BN + cg * 8 + e] = s2[e];
-      red[(rg * 3 + 2) * BN + cg * 8 + e] = s3[e];
-    }
-    __syncthreads();
-    const bool fin = !SKM && a.fin_on;
-    if (tid < BN && n0 + tid < a.Kout) {
-      float t1 = 0.f, t2 = 0.f, t3 = 0.f;
-      for (int g = 0; g < RG; ++g) {
-        t1 += red[(g * 3 + 0) * BN + tid];
-        t2 += red[(g * 3 + 1) * BN + tid];
-        t3 += red[(g * 3 + 2) * BN + tid];
-      }
-      float* st = a.stats + (int64_t)(ph.tile_base + mt) * ns * a.Kout + n0 + tid;
-      if (fin) {   // published write-through for the in-launch finalize (bnfin.h)
-        st_sc1(st, t1);
-        st_sc1(st + a.Kout, t2);
-        if (ns > 2) st_sc1(st + 2 * a.Kout, t3);
-      } else {
-        st[0] = t1;
-        st[a.Kout] = t2;
-        if (ns > 2) st[2 * a.Kout] = t3;
-      }
-    }
-    if (fin) {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every storing wave drains its row stores
-      __syncthreads();                                   // (also: red is free again)
-      fin_in_launch<NT, BN>(a, a.stats, ns, ph.tile_base + mt, nt, n0, reinterpret_cast<double*>(smem),
-                            reinterpret_cast<int*>(smem + 2 * NT * sizeof(double)));
-    }
-  }
-  }   // LDS epilogue
-  if constexpr (!SKM) break;
-  __syncthreads();   // LDS (epilogue staging / stats) is reused by the next segment's staging
-  }   // segment loop
+  __syncthreads();   // the last fragment reads are done before the epilogue reuses the LDS
+  conv_epilogue<BM, BN, NT, WGM, WGN, uint16_t, false>(a, ph, acc, smem, tid, m0, n0, mt, 0, 0, 0);
 }
 
 }  // namespace dlmpi
 
 using namespace dlmpi;
 
-static int stages_choice() {
-  static int v = [] {
-    const char* e = getenv("DLMPI_CONV_STAGES");
-    return e ? atoi(e) : 1;
-  }();
-  return v;
-}
-
-// DLMPI_CONV_REPI: 1 = register-direct epilogue (D^T fragments, no LDS staging of the output tile)
-// for bf16 launches without operand prologue and with full-width vector stores; 0 (default) = the
-// LDS-staged epilogue.  Measured slower (profiles/r3_repi_rejected): per-network forward 4.86 vs
-// 4.70 ms, the memory-bound expand 1x1s +9..15 % (8-byte lane pieces make each store instruction
-// cover 16 rows x 32 B instead of 4 rows x 256 B), ResNet-50 step 10.8k vs 12.0k img/s (the masked
-// data-gradient epilogues' 8-byte z / mask loads).
-static int g_repi_override = -1;
-static bool repi_on(const ConvArgs* a) {
-  static const int v = [] {
-    const char* e = getenv("DLMPI_CONV_REPI");
-    return e ? atoi(e) : 0;
-  }();
-  const int m = g_repi_override >= 0 ? g_repi_override : v;
-  return m != 0 && !a->f32 && a->pro == 0 && a->vec_store && a->kvalid == a->Kout && a->Kout % 8 == 0;
-}
-extern "C" void dlmpi_set_conv_repi(int mode) { g_repi_override = mode; }
-
 template <int BM, int BN>
 static void launch_tile(const ConvArgs* a, dim3 grid, hipStream_t s) {
-  const bool one = stages_choice() == 1;
-  if (one && repi_on(a)) {
-    if (a->C < 64) hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, true, 1, 4, 2, 0, uint16_t, false, true>), grid, dim3(256), 0, s, *a);
-    else hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, false, 1, 4, 2, 0, uint16_t, false, true>), grid, dim3(256), 0, s, *a);
-    return;
-  }
-  if (a->pro == 1) {
-    hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, false, 1, 4, 2, 1>), grid, dim3(256), 0, s, *a);
-    return;
-  }
-  if (a->pro == 2) {
-    hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, false, 1, 4, 2, 2>), grid, dim3(256), 0, s, *a);
-    return;
-  }
-  if (a->pro == 3) {
-    hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, false, 1, 4, 2, 3>), grid, dim3(256), 0, s, *a);
-    return;
-  }
-  if (a->C < 64) {
-    if (one) hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, true, 1, 4, 2>), grid, dim3(256), 0, s, *a);
-    else hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, true, 2, 4, 2>), grid, dim3(256), 0, s, *a);
-  } else {
-    if (one) hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, false, 1, 4, 2>), grid, dim3(256), 0, s, *a);
-    else hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, false, 2, 4, 2>), grid, dim3(256), 0, s, *a);
-  }
+  if (a->pro == 1) hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, false, 2, 1>), grid, dim3(256), 0, s, *a);
+  else if (a->pro == 2) hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, false, 2, 2>), grid, dim3(256), 0, s, *a);
+  else if (a->pro == 3) hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, false, 2, 3>), grid, dim3(256), 0, s, *a);
+  else if (a->C < 64) hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, true, 2>), grid, dim3(256), 0, s, *a);
+  else hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, false, 2>), grid, dim3(256), 0, s, *a);
 }
 
 // Split-K plan for small grids (ResNet-18 on 32x32 CIFAR: layer4 is 1x1 pixels, 8 tiles x 72
@@ -972,60 +910,16 @@ static int splitk_plan(int tiles, int nk) {
   return S < 2 ? 1 : S;
 }
 
-// ---- stream-K planning --------------------------------------------------------------------------
-// A launch of T tiles on a chip holding `slots` resident blocks takes ceil(T / slots) tile-times; at
-// ResNet-50 bs 256 many layers sit just above a multiple (784 tiles of 14^2 x 256 channels on 768
-// slots: 2 tile-times for 1.02 tiles of work each, measured +48 % vs 248 images).  Stream-K runs
-// exactly `slots` persistent blocks over the flattened (tile, K-step) iterations instead; a tile cut
-// between two blocks costs one slab round trip + a ticket (sk_time below: + 0.15 tile-times).
-static int cu_count() {
-  static const int n = [] {
-    int d = 0, v = 0;
-    if (hipGetDevice(&d) != hipSuccess || hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, d) != hipSuccess)
-      v = 256;
-    return v > 0 ? v : 256;
-  }();
-  return n;
-}
-
-template <int BM, int BN>
-static int sk_occupancy() {   // resident blocks per CU of the stream-K instance
-  static const int occ = [] {
-    int n = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, conv_igemm_kernel<BM, BN, false, 1, 4, 2, 0, uint16_t, true>,
-                                                     256, 0) != hipSuccess || n < 1)
-      n = 2;
-    return n;
-  }();
-  return occ;
-}
-
-static int g_sk_override = -1;   // dlmpi_set_conv_sk (tests); -1: the environment decides
-static int g_sk_last = 0;        // 1 if the last conv launch ran stream-K (tests)
-// DLMPI_CONV_SK: 0 off (default), 1 auto, 2 whenever applicable (tests).  Measured slower on every
-// targeted ResNet-50 shape (profiles/r2_streamk_rejected): with ~1 iteration range per tile almost
-// every tile is cut, and the 64 KB fp32 partials per cut tile cost more than the wave tail saved.
-static int sk_mode_env() {
-  static const int v = [] {
-    const char* e = getenv("DLMPI_CONV_SK");
-    return e ? atoi(e) : 0;
-  }();
-  return g_sk_override >= 0 ? g_sk_override : v;
-}
-
-extern "C" void dlmpi_set_conv_sk(int mode) { g_sk_override = mode; }
-extern "C" int dlmpi_conv_sk_last() { return g_sk_last; }
-
 // fp32 precision path: single-stage 4-wave tiles up to 128 x 128 (the f32 MFMA is 1/16 of the
 // bf16 rate, so the wider bf16 tiles buy nothing here)
 static hipError_t launch_f32(const ConvArgs* a, int bm, int bn, dim3 grid, hipStream_t s) {
   if (a->pro != 0) return hipErrorInvalidValue;
   // the regular staging walks whole 32-channel K-steps per tap; anything else stages per 16-B piece
   const bool small = a->C < 32 || a->C % 32 != 0;
-#define DLMPI_F32(BM_, BN_)                                                                                        \
-  do {                                                                                                            \
-    if (small) hipLaunchKernelGGL((conv_igemm_kernel<BM_, BN_, true, 1, 4, 2, 0, float>), grid, dim3(256), 0, s, *a); \
-    else hipLaunchKernelGGL((conv_igemm_kernel<BM_, BN_, false, 1, 4, 2, 0, float>), grid, dim3(256), 0, s, *a);     \
+#define DLMPI_F32(BM_, BN_)                                                                                   \
+  do {                                                                                                       \
+    if (small) hipLaunchKernelGGL((conv_igemm_kernel<BM_, BN_, true, 2, 0, float>), grid, dim3(256), 0, s, *a); \
+    else hipLaunchKernelGGL((conv_igemm_kernel<BM_, BN_, false, 2, 0, float>), grid, dim3(256), 0, s, *a);     \
   } while (0)
   if (bm == 128 && bn == 128) DLMPI_F32(128, 128);
   else if (bm == 128 && bn == 64) DLMPI_F32(128, 64);
@@ -1036,7 +930,29 @@ static hipError_t launch_f32(const ConvArgs* a, int bm, int bn, dim3 grid, hipSt
   return hipGetLastError();
 }
 
-extern "C" hipError_t dlmpi_conv_igemm(const ConvArgs* a_in, int bm, int bn, hipStream_t s) {
+// Pipelined 8-wave tiles (conv_pipe_kernel): (bm, bn) -> instance.  Returns hipErrorInvalidValue
+// when the launch does not fit the kernel (channels, prologue, split, fp32).
+static hipError_t launch_pipe(const ConvArgs* a, int bm, int bn, int var, dim3 grid, hipStream_t s) {
+  if (a->f32 || a->pro != 0 || a->C % 64 != 0 || a->halo || grid.y != 1) return hipErrorInvalidValue;
+#define DLMPI_PIPE(BM_, BN_, WGM_, WGN_, ST_)                                                                        \
+  do {                                                                                                              \
+    if (var == 1) hipLaunchKernelGGL((conv_pipe_kernel<BM_, BN_, WGM_, WGN_, ST_, 1>), grid, dim3(512), 0, s, *a);  \
+    else if (var == 2) hipLaunchKernelGGL((conv_pipe_kernel<BM_, BN_, WGM_, WGN_, ST_, 2>), grid, dim3(512), 0, s, *a); \
+    else if (var == 3) hipLaunchKernelGGL((conv_pipe_kernel<BM_, BN_, WGM_, WGN_, ST_, 3>), grid, dim3(512), 0, s, *a); \
+    else hipLaunchKernelGGL((conv_pipe_kernel<BM_, BN_, WGM_, WGN_, ST_, 0>), grid, dim3(512), 0, s, *a);           \
+  } while (0)
+  if (bm == 256 && bn == 256) DLMPI_PIPE(256, 256, 2, 4, 2);
+  else if (bm == 224 && bn == 256) DLMPI_PIPE(224, 256, 2, 4, 2);
+  else if (bm == 256 && bn == 128) DLMPI_PIPE(256, 128, 4, 2, 3);
+  else if (bm == 128 && bn == 256) DLMPI_PIPE(128, 256, 2, 4, 3);
+  else if (bm == 512 && bn == 64) DLMPI_PIPE(512, 64, 8, 1, 2);
+  else return hipErrorInvalidValue;
+#undef DLMPI_PIPE
+  return hipGetLastError();
+}
+
+// pipe != 0: the launch runs the pipelined kernel (tile bm x bn must be one of launch_pipe's)
+extern "C" hipError_t dlmpi_conv_igemm_ex(const ConvArgs* a_in, int bm, int bn, int pipe, hipStream_t s) {
   int maxt = 0, tiles = 0, maxk = 0;
   for (int i = 0; i < a_in->nphase; ++i) {
     maxt = a_in->ph[i].mtiles > maxt ? a_in->ph[i].mtiles : maxt;
@@ -1046,7 +962,11 @@ extern "C" hipError_t dlmpi_conv_igemm(const ConvArgs* a_in, int bm, int bn, hip
   ConvArgs ab = *a_in;
   const ConvArgs* a = &ab;
   ab.splitk = 1;
-  g_sk_last = 0;
+  if (pipe) {
+    const dim3 grid((unsigned)(maxt * a->ntiles), 1, (unsigned)a->nphase);
+    if (grid.x == 0) return hipSuccess;
+    return launch_pipe(a, bm, bn, pipe - 1, grid, s);
+  }
   int S = a_in->splitk_req > 0 ? a_in->splitk_req : splitk_plan(tiles, maxk);
   if (S > maxk) S = maxk > 0 ? maxk : 1;
   if (S > 1) {
@@ -1062,87 +982,20 @@ extern "C" hipError_t dlmpi_conv_igemm(const ConvArgs* a_in, int bm, int bn, hip
   dim3 grid((unsigned)(maxt * a->ntiles), (unsigned)ab.splitk, (unsigned)a->nphase);
   if (grid.x == 0) return hipSuccess;
   if (a->f32) return launch_f32(a, bm, bn, grid, s);
-  // stream-K: regular channel counts, no prologue, the single-stage 4-wave tiles
-  const int skm = sk_mode_env();
-  const bool sk_tile = (bm == 128 && (bn == 128 || bn == 64)) || (bm == 64 && (bn == 128 || bn == 64)) ||
-                       (bm == 256 && bn == 128);
-  bool kzero = false;
-  int iters = 0;
-  for (int i = 0; i < a_in->nphase; ++i) {
-    kzero |= a_in->ph[i].ksteps == 0;
-    iters += a_in->ph[i].mtiles * a_in->ntiles * a_in->ph[i].ksteps;
-  }
-  if (skm && !a->fin_on && ab.splitk == 1 && sk_tile && a->pro == 0 && a->C >= 64 && stages_choice() == 1 && !kzero &&
-      tiles <= 4096 && iters > 0) {
-    int occ = 2;
-    if (bm == 128 && bn == 128) occ = sk_occupancy<128, 128>();
-    else if (bm == 128) occ = sk_occupancy<128, 64>();
-    else if (bm == 64 && bn == 128) occ = sk_occupancy<64, 128>();
-    else if (bm == 64) occ = sk_occupancy<64, 64>();
-    else occ = sk_occupancy<256, 128>();
-    const int slots = cu_count() * occ;
-    const int G = tiles < slots ? (tiles * 2 < slots ? 0 : slots) : slots;   // < half a wave: leave it
-    if (G > 0) {
-      const int per = (iters + G - 1) / G;
-      const double now = (double)((tiles + slots - 1) / slots);
-      const double sk = (double)per * tiles / iters + 0.15;
-      if (skm == 2 || sk < 0.85 * now) {
-        const int Ge = (iters + per - 1) / per;
-        float* slab = dlmpi_splitk_slab(s, (size_t)Ge * 2 * bm * bn);
-        int* tk = dlmpi_splitk_tickets(s, tiles);
-        if (slab && tk) {
-          ab.sk_mode = 1;
-          ab.sk_per = per;
-          ab.sk_total = iters;
-          ab.sk_slab = slab;
-          ab.sk_tk = tk;
-          int it = 0, tb = 0;
-          for (int i = 0; i < a_in->nphase; ++i) {
-            ab.sk_base[i] = it;
-            ab.sk_tbase[i] = tb;
-            it += a_in->ph[i].mtiles * a_in->ntiles * a_in->ph[i].ksteps;
-            tb += a_in->ph[i].mtiles * a_in->ntiles;
-          }
-          ab.sk_base[a_in->nphase] = it;
-          const dim3 g((unsigned)Ge, 1, 1);
-#define DLMPI_SK(BM_, BN_) \
-  hipLaunchKernelGGL((conv_igemm_kernel<BM_, BN_, false, 1, 4, 2, 0, uint16_t, true>), g, dim3(256), 0, s, *a)
-          if (bm == 128 && bn == 128) DLMPI_SK(128, 128);
-          else if (bm == 128) DLMPI_SK(128, 64);
-          else if (bm == 64 && bn == 128) DLMPI_SK(64, 128);
-          else if (bm == 64) DLMPI_SK(64, 64);
-          else DLMPI_SK(256, 128);
-#undef DLMPI_SK
-          g_sk_last = 1;
-          return hipGetLastError();
-        }
-      }
-    }
-  }
   if (a->halo) {   // 3x3 / stride 1 / pad 1 by 2-D tiles with a staged halo (host-planned)
-    if (a->pro != 0 || bm != 128 || a->C % 64 != 0 || a->sk_mode) return hipErrorInvalidValue;
-    if (bn == 128) hipLaunchKernelGGL((conv_igemm_kernel<128, 128, false, 1, 4, 2, 0, uint16_t, false, false, true>), grid, dim3(256), 0, s, *a);
-    else if (bn == 64) hipLaunchKernelGGL((conv_igemm_kernel<128, 64, false, 1, 4, 2, 0, uint16_t, false, false, true>), grid, dim3(256), 0, s, *a);
+    if (a->pro != 0 || bm != 128 || a->C % 64 != 0) return hipErrorInvalidValue;
+    if (bn == 128) hipLaunchKernelGGL((conv_igemm_kernel<128, 128, false, 2, 0, uint16_t, true>), grid, dim3(256), 0, s, *a);
+    else if (bn == 64) hipLaunchKernelGGL((conv_igemm_kernel<128, 64, false, 2, 0, uint16_t, true>), grid, dim3(256), 0, s, *a);
     else return hipErrorInvalidValue;
     return hipGetLastError();
   }
-  if (a->pro != 0 && (a->C < 64 || a->C % 64 != 0 || (bm == 256 && bn == 256))) return hipErrorInvalidValue;
-  if (bm == 256 && bn == 256) {   // 8 waves, double-buffered; regular channel counts only
-    if (a->C < 64) return hipErrorInvalidValue;
-    if (repi_on(a)) hipLaunchKernelGGL((conv_igemm_kernel<256, 256, false, 2, 8, 2, 0, uint16_t, false, true>), grid, dim3(512), 0, s, *a);
-    else hipLaunchKernelGGL((conv_igemm_kernel<256, 256, false, 2, 8, 2>), grid, dim3(512), 0, s, *a);
-  } else if (bm == 256 && bn == 64) {   // 64-channel layers: 4 x 1 waves of 64 x 64
-    if (a->pro == 0 && repi_on(a)) {
-      if (a->C < 64) hipLaunchKernelGGL((conv_igemm_kernel<256, 64, true, 1, 4, 4, 0, uint16_t, false, true>), grid, dim3(256), 0, s, *a);
-      else hipLaunchKernelGGL((conv_igemm_kernel<256, 64, false, 1, 4, 4, 0, uint16_t, false, true>), grid, dim3(256), 0, s, *a);
-    } else if (a->pro == 1) hipLaunchKernelGGL((conv_igemm_kernel<256, 64, false, 1, 4, 4, 1>), grid, dim3(256), 0, s, *a);
-    else if (a->pro == 2) hipLaunchKernelGGL((conv_igemm_kernel<256, 64, false, 1, 4, 4, 2>), grid, dim3(256), 0, s, *a);
-    else if (a->pro == 3) hipLaunchKernelGGL((conv_igemm_kernel<256, 64, false, 1, 4, 4, 3>), grid, dim3(256), 0, s, *a);
-    else if (a->C < 64) hipLaunchKernelGGL((conv_igemm_kernel<256, 64, true, 1, 4, 4>), grid, dim3(256), 0, s, *a);
-    else hipLaunchKernelGGL((conv_igemm_kernel<256, 64, false, 1, 4, 4>), grid, dim3(256), 0, s, *a);
-  } else if (bm == 128 && bn == 256) {   // short reductions, wide outputs: 8 waves (2 x 4 of 64 x 64)
-    if (a->C < 64 || a->pro != 0) return hipErrorInvalidValue;
-    hipLaunchKernelGGL((conv_igemm_kernel<128, 256, false, 1, 8, 2>), grid, dim3(512), 0, s, *a);
+  if (a->pro != 0 && (a->C < 64 || a->C % 64 != 0)) return hipErrorInvalidValue;
+  if (bm == 256 && bn == 64) {   // 64-channel layers: 4 x 1 waves of 64 x 64
+    if (a->pro == 1) hipLaunchKernelGGL((conv_igemm_kernel<256, 64, false, 4, 1>), grid, dim3(256), 0, s, *a);
+    else if (a->pro == 2) hipLaunchKernelGGL((conv_igemm_kernel<256, 64, false, 4, 2>), grid, dim3(256), 0, s, *a);
+    else if (a->pro == 3) hipLaunchKernelGGL((conv_igemm_kernel<256, 64, false, 4, 3>), grid, dim3(256), 0, s, *a);
+    else if (a->C < 64) hipLaunchKernelGGL((conv_igemm_kernel<256, 64, true, 4>), grid, dim3(256), 0, s, *a);
+    else hipLaunchKernelGGL((conv_igemm_kernel<256, 64, false, 4>), grid, dim3(256), 0, s, *a);
   } else if (bm == 256 && bn == 128) launch_tile<256, 128>(a, grid, s);
   else if (bm == 128 && bn == 128) launch_tile<128, 128>(a, grid, s);
   else if (bm == 128 && bn == 64) launch_tile<128, 64>(a, grid, s);
@@ -1150,4 +1003,8 @@ extern "C" hipError_t dlmpi_conv_igemm(const ConvArgs* a_in, int bm, int bn, hip
   else if (bm == 64 && bn == 64) launch_tile<64, 64>(a, grid, s);
   else return hipErrorInvalidValue;
   return hipGetLastError();
+}
+
+extern "C" hipError_t dlmpi_conv_igemm(const ConvArgs* a, int bm, int bn, hipStream_t s) {
+  return dlmpi_conv_igemm_ex(a, bm, bn, 0, s);
 }

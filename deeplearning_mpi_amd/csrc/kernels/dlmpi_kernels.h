@@ -147,13 +147,6 @@ struct ConvArgs {
   int splitk_req;                  // 0: the launcher plans the split; >= 1: use exactly this (autotuner)
   float* sk_slab;                  // [tile][slice][TM*TN][threads] f32x4 fragment slabs
   int* sk_tk;                      // [tile] self-resetting arrival tickets
-  // stream-K (set by the launcher): gridDim.x persistent blocks, block lb (XCD-remapped) runs the
-  // flattened (phase, tile, K-step) iterations [lb * sk_per, min(sk_total, (lb + 1) * sk_per)); a tile
-  // split between blocks is combined by its last-arriving contributor from per-block slab slots
-  int sk_mode;                     // 0: one tile (or split) per block, 1: stream-K
-  int sk_per, sk_total;
-  int sk_base[5];                  // first iteration of each phase (sk_base[nphase] = total)
-  int sk_tbase[4];                 // first global tile index of each phase (tickets)
   int cstep, tstep;                // K-iteration: c += cstep, t += tstep per 64-wide step
   // Operand prologue (regular channel counts, single-stage kernels): every staged A piece of an
   // in-image tap is rewritten in LDS before the MFMAs (out-of-image taps stay zero):
@@ -176,15 +169,6 @@ struct ConvArgs {
   uint16_t* py;
   int ldpy, pyoff;
   uint8_t* pmbits;
-  // In-launch BatchNorm finalize of the statistics this launch produces (bnfin.h): every block
-  // publishes its stats row write-through; the last arriver of each group of fin_group stats tiles
-  // sums the group, the last group of each N-tile sums the group sums and finalizes that N-tile's
-  // channels (fin).  Saves the separate finalize launch on the BN critical path.
-  int fin_on;
-  int fin_group, fin_ngroups, fin_T, fin_k2;
-  double* fin_gsum;                // [ngroups][2][Kout]
-  int* fin_tk;                     // [ntiles][ngroups] group tickets, then [ntiles] N-tile tickets
-  FinArgs fin;
   // 2-D halo tiles (conv_igemm.hip HALO; 3x3 / stride 1 / pad 1, one phase): M-tile mt = (n, ti, tj)
   // of the N x tiles_h x tiles_w grid covers output pixels [ti th, +th) x [tj tw, +tw)
   int halo;
@@ -246,10 +230,9 @@ struct Wgrad3Args {
 extern "C" {
 // conv / gemm
 hipError_t dlmpi_conv_igemm(const dlmpi::ConvArgs* a, int bm, int bn, hipStream_t s);
-// stream-K mode override (-1: DLMPI_CONV_SK decides; 0 off, 1 auto, 2 whenever applicable) and
-// whether the last conv launch used it
-void dlmpi_set_conv_sk(int mode);
-int dlmpi_conv_sk_last();
+// pipe = 1: the pipelined 8-wave kernel (tiles 256x256, 256x128, 128x256, 256x64, 512x64; bf16,
+// C % 64 == 0, no prologue / halo / split); pipe = 0: dlmpi_conv_igemm
+hipError_t dlmpi_conv_igemm_ex(const dlmpi::ConvArgs* a, int bm, int bn, int pipe, hipStream_t s);
 hipError_t dlmpi_conv_wgrad(const dlmpi::WgradArgs* a, int bm, int bn, hipStream_t s);   // bn: 128 | 256
 // sum of split partials -> grad (accumulated), with channel un-padding and row limit
 hipError_t dlmpi_wgrad_reduce(const float* ws, int splits, int Ko, int T, int Cpad, int Creal,
@@ -384,7 +367,6 @@ hipError_t dlmpi_image_batch(const uint8_t* data, const int64_t* labels, const i
 
 // fault injection: keep stream s busy for `ms` milliseconds (bounded; tests of the watchdog)
 hipError_t dlmpi_delay(double ms, hipStream_t s);
-void dlmpi_set_conv_repi(int mode);
 void dlmpi_set_conv_stream(int mode);
 void dlmpi_set_dgrad_stream(int mode);
 int dlmpi_stream1x1_plan(int64_t M, int C, int Kout, int* bm, int* bn, int* G);
@@ -392,7 +374,6 @@ hipError_t dlmpi_conv1x1_stream(const dlmpi::Stream1x1Args* a, int bm, int bn, h
 int dlmpi_stream1x1_pro_ok(int ntiles);
 int dlmpi_dgrad_stream_plan(int64_t M, int K, int Kout, int mask_mode, int z2, int has_res, int* bm, int* bn, int* G);
 hipError_t dlmpi_conv1x1_dgrad_stream(const dlmpi::DgradStreamArgs* a, int bm, int bn, int mask_mode, hipStream_t s);
-int dlmpi_fin_scratch(hipStream_t s, size_t gsum_doubles, int tickets, double** gsum, int** tk);
 
 // utilities (util.hip): fp32 fill, int64 add, indexed gather dst[i] (+)= src[idx[i]] (idx < 0: zero;
 // esize 2 | 4 bytes, accumulate: fp32 only)

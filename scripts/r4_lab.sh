@@ -1,0 +1,19 @@
+#!/bin/bash
+# Round 4: conv main-loop lab (benchmarks/conv_lab) on the compute-bound ResNet-50 / UNet shapes, then
+# one PMC pass per kernel of interest.  Output: gpurun_out/r4_lab/
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+O=$R/gpurun_out/r4_lab${TAG:+_$TAG}; mkdir -p $O
+cd $R
+timeout -k 10 400 ./benchmarks/conv_lab 5 ${SHAPES} > $O/lab.log 2>&1 || { echo lab failed; tail -5 $O/lab.log; exit 1; }
+grep -c OK $O/lab.log; grep -c BAD $O/lab.log
+[ -n "$NOPMC" ] && exit 0
+cd /tmp && export TMPDIR=/tmp
+CTR="SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CU_CYCLES SQ_WAVE_CYCLES SQ_WAIT_INST_LDS SQ_WAIT_ANY SQ_INSTS_MFMA SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS"
+i=0
+for spec in "pipe256x256 256,14,14,256,256,3,1,1" "old256x128 256,14,14,256,256,3,1,1" "pipe256x256 16,32,32,1024,1024,3,1,1" "old256x128 16,32,32,1024,1024,3,1,1" "oldhalo128 16,256,256,128,128,3,1,1" ${PMC_EXTRA}; do
+  set -- $spec
+  i=$((i+1))
+  timeout -s KILL 60 rocprofv3 --pmc $CTR --kernel-trace -d $O/pmc$i -o c --output-format csv -- $R/benchmarks/conv_lab --only=$1 2 $2 > $O/pmc$i.log 2>&1
+  rc=$?; echo "pmc$i $1 $2 rc=$rc"; [ $rc -ne 0 ] && exit $rc
+done
+exit 0

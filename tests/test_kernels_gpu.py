@@ -176,16 +176,17 @@ def test_wide_tile_bit_identical_to_128x128():
     assert torch.allclose(sts[0].double().sum(0), sts[1].double().sum(0), rtol=1e-5, atol=1e-2)
 
 
-SK_SHAPES = [(256, 14, 14, 1024, 256, 1, 1, 0), (256, 14, 14, 256, 256, 3, 1, 1), (256, 28, 28, 512, 128, 1, 1, 0),
-             (256, 7, 7, 512, 2048, 1, 1, 0), (128, 14, 14, 256, 256, 3, 2, 1), (256, 28, 28, 256, 512, 1, 2, 0)]
+PIPE_SHAPES = [(2, 14, 14, 256, 256, 3, 1, 1), (3, 7, 7, 512, 512, 3, 1, 1), (2, 16, 16, 128, 256, 3, 2, 1),
+               (4, 14, 14, 1024, 256, 1, 1, 0), (2, 28, 28, 128, 128, 3, 1, 1), (1, 32, 32, 64, 64, 3, 1, 1),
+               (2, 9, 11, 192, 320, 3, 1, 1), (2, 14, 14, 512, 1024, 1, 2, 0)]
 
 
-@pytest.mark.parametrize("shape", SK_SHAPES, ids=lambda s: "x".join(map(str, s)))
-def test_stream_k_conv_matches_tile_per_block(shape):
-    """Stream-K (persistent blocks over the flattened (phase, tile, K-step) iterations, tiles cut
-    between blocks combined by the last contributor) forced on: forward with BN partials and the
-    data gradient (incl. stride-2 sub-pixel phases) against the one-tile-per-block launch, and
-    bit-reproducible from run to run."""
+@pytest.mark.parametrize("shape", PIPE_SHAPES, ids=lambda s: "x".join(map(str, s)))
+def test_pipelined_conv_bit_identical_to_single_stage(shape):
+    """The pipelined 8-wave kernel (LDS ring, counted vmcnt, one barrier per K-step) forced on against
+    the single-stage gather kernel: forward with BN partials and the data gradient (incl. stride-2
+    sub-pixel phases, ragged M / Kout tails) -- same K order, so bit-identical outputs; statistics
+    column sums equal to fp32 rounding; bit-reproducible from run to run."""
     nb, _ = _be()
     N, H, W, Cin, K, R, s, p = shape
     Cp, Kp = pad8(Cin), pad8(K)
@@ -196,26 +197,29 @@ def test_stream_k_conv_matches_tile_per_block(shape):
     dy, _ = _act(N, P, Q, Kp)
     wT = w.permute(3, 1, 2, 0).contiguous()
     out = {}
+    C = nb.C
     try:
-        for mode in (0, 2, 2):
-            nb.C.set_conv_sk(mode)
+        C.set_conv_halo(0)
+        C.set_conv_stream(0)
+        C.set_dgrad_stream(0)
+        C.set_conv_autotune(0)
+        for mode in (0, 1, 1):
+            C.set_conv_pipe(mode)
             y = _empty(N, P, Q, Kp)
             st = torch.zeros(nb.conv_mtiles(N, H, W, Cp, Kp, R, R, s, p), 2, Kp, device=DEV)
             nb.conv_fwd(x, w, Kp, R, R, s, p, y, stats=st)
-            used_fwd = nb.C.conv_sk_last()
             dx = _empty(N, H, W, Cp)
             nb.conv_dgrad(dy, wT, Cp, R, R, s, p, dx)
-            used_dg = nb.C.conv_sk_last()
             torch.cuda.synchronize()
-            out.setdefault(mode, []).append((y.buf.clone(), st.double().sum(0), dx.buf.clone(), used_fwd, used_dg))
+            out.setdefault(mode, []).append((y.buf.clone(), st.double().sum(0), dx.buf.clone()))
     finally:
-        nb.C.set_conv_sk(-1)
-    base, sk1, sk2 = out[0][0], out[2][0], out[2][1]
-    assert base[3] == 0 and base[4] == 0
-    assert sk1[3] == 1 or sk1[4] == 1, "stream-K did not engage"
-    assert torch.equal(sk1[0], sk2[0]) and torch.equal(sk1[2], sk2[2]) and torch.equal(sk1[1], sk2[1])
-    assert _rel(sk1[0], base[0]) < 1e-2 and _rel(sk1[2], base[2]) < 1e-2
-    assert _rel(sk1[1], base[1]) < 1e-4
+        for f in (C.set_conv_pipe, C.set_conv_halo, C.set_conv_stream, C.set_dgrad_stream, C.set_conv_autotune):
+            f(-1)
+    base, p1, p2 = out[0][0], out[1][0], out[1][1]
+    assert torch.equal(p1[0], p2[0]) and torch.equal(p1[1], p2[1]) and torch.equal(p1[2], p2[2])
+    assert torch.equal(p1[0], base[0]), "forward differs from the single-stage kernel"
+    assert torch.equal(p1[2], base[2]), "data gradient differs from the single-stage kernel"
+    assert _rel(p1[1], base[1]) < 1e-5
 
 
 @pytest.mark.parametrize("shape", [CONV_SHAPES[1], CONV_SHAPES[2], CONV_SHAPES[3], CONV_SHAPES[5]])
@@ -757,7 +761,6 @@ def _static_kernels(on: bool):
     """Pin the plain implicit-GEMM kernel with the static tile rules (the operand-prologue kernels
     have no register epilogue, streaming or autotuned variant): for bit-identity comparisons."""
     C = NativeBackend(DEV).C
-    C.set_conv_repi(0 if on else -1)
     C.set_conv_stream(0 if on else -1)
     C.set_conv_autotune(0 if on else -1)
     C.set_conv_halo(0 if on else -1)    # 3x3 halo tiles sum chunk-major (no prologue variant)
@@ -879,58 +882,6 @@ def test_deferred_bn_passes_bit_identical_training(model):
     assert torch.equal(res[0][0], res[1][0])
     for a, b in zip(res[0][1] + res[0][2], res[1][1] + res[1][2]):
         assert torch.equal(a, b)
-
-
-# ------------------------------------------------------------------ in-launch BN finalize
-FIN_SHAPES = [
-    # N, H, W, Cin, Cout, R, stride, pad
-    (2, 14, 14, 64, 64, 3, 1, 1),        # 4 stats tiles: one group
-    (16, 28, 28, 64, 256, 1, 1, 0),      # 98 tiles x 2 N-tiles: several groups
-    (32, 56, 56, 64, 64, 1, 1, 0),       # 256-row / 64-wide tiles, many groups
-    (8, 14, 14, 256, 1024, 1, 1, 0),     # 8 N-tiles
-    (4, 16, 16, 512, 512, 3, 1, 1),      # 3x3, split-K grid
-    (2, 32, 32, 3, 64, 7, 2, 3),         # stem (small channels)
-    (64, 14, 14, 256, 256, 3, 1, 1),     # 8-wave 256-row tiles
-]
-
-
-@pytest.mark.parametrize("shape", FIN_SHAPES)
-def test_conv_fwd_bn_in_launch_finalize(shape, monkeypatch):
-    """conv + BN statistics + the training-BN finalize in ONE launch (csrc/kernels/bnfin.h: two-level
-    last-arriver tree over write-through stats rows; off by default, measured slower) against the
-    conv followed by the standalone finalize kernel: same z, same partials, scale / shift / mean / invstd / running stats within fp64-
-    summation-order noise; repeated launches (self-resetting tickets) give identical results."""
-    N, H, W, Cin, Cout, R, s, p = shape
-    nb = NativeBackend(DEV)
-    Cp = pad8(Cin)
-    x, _ = _act(N, H, W, Cp)
-    w = (torch.randn(Cout, R, R, Cp, device=DEV) * 0.1).to(torch.bfloat16)
-    P, Q = (H + 2 * p - R) // s + 1, (W + 2 * p - R) // s + 1
-    nb.C.set_conv_autotune(0)   # the same (static) tiling on both paths, and stats rows sized for it
-    mt = nb.conv_mtiles(N, H, W, Cp, Cout, R, R, s, p)
-    gamma, beta = torch.rand(Cout, device=DEV) + 0.5, torch.randn(Cout, device=DEV)
-    res = []
-    for mode in ("fused", "fused", "separate"):
-        nb.C.set_fin_in_launch(1 << 30 if mode == "fused" else 0)
-        z = _empty(N, P, Q, Cout)
-        stats = torch.empty(mt, 2, Cout, device=DEV)
-        rm, rv = torch.zeros(Cout, device=DEV), torch.ones(Cout, device=DEV)
-        v = torch.empty(4, Cout, device=DEV)
-        if mode == "fused":
-            nb.conv_fwd_bn(x, w, Cout, R, R, s, p, z, None, stats, N * P * Q, gamma, beta, rm, rv, 0.1, 1e-5,
-                           v[0], v[1], v[2], v[3])
-        else:
-            nb.conv_fwd(x, w, Cout, R, R, s, p, z, stats=stats)
-            nb.bn_finalize(stats, mt, Cout, N * P * Q, gamma, beta, rm, rv, 0.1, 1e-5, v[0], v[1], v[2], v[3])
-        torch.cuda.synchronize()
-        res.append((z.buf.clone(), stats.clone(), v.clone(), rm.clone(), rv.clone()))
-    nb.C.set_fin_in_launch(-1)
-    nb.C.set_conv_autotune(-1)
-    for a, b in zip(res[0], res[1]):
-        assert torch.equal(a, b)   # deterministic across launches
-    assert torch.equal(res[0][0], res[2][0]) and torch.equal(res[0][1], res[2][1])
-    for a, b in zip(res[0][2:], res[2][2:]):
-        assert _rel(a, b) < 1e-6, shape
 
 
 # ------------------------------------------------------------------ streaming 1x1 forward
