@@ -101,7 +101,10 @@ def main():
     ap.add_argument("--image", type=int, default=None)
     ap.add_argument("--classes", type=int, default=None)
     ap.add_argument("--bucket_mb", type=float, default=None)
-    ap.add_argument("--graph", type=int, default=0, help="1: replay the whole step from a captured hipGraph")
+    ap.add_argument("--graph", default="auto", choices=["auto", "0", "1"],
+                    help="1: replay the whole step from a captured hipGraph; auto (default): the training app's "
+                         "decision (apps/classification.py use_graph: on for launch-bound steps, e.g. the "
+                         "reference's ResNet-18 on CIFAR; off where concurrent streams win)")
     ap.add_argument("--breakdown", type=int, default=0,
                     help="N > 0: after the timed steps, N more steps with HIP-event phase timing (forward / "
                          "backward / exposed all-reduce wait / optimizer), printed to stderr")
@@ -114,6 +117,16 @@ def main():
     ap.add_argument("--rccl1", type=int, default=0,
                     help="1 (single GPU only): run the step through a world-size-1 RCCL communicator with the "
                          "bucketed reducer forced on (every all-reduce / the K5 broadcast go through RCCL)")
+    ap.add_argument("--rehearse", type=int, default=0,
+                    help="C > 0 (single GPU): comm-load rehearsal of a --rehearse_world-rank all-reduce -- the "
+                         "--rccl1 path plus, after every bucket all-reduce, C workgroups on the comm stream that "
+                         "move the ring all-reduce's traffic and hold their CUs for the modeled collective time "
+                         "(RCCL channels = C; parallel/comm.py rccl_channel_budget)")
+    ap.add_argument("--rehearse_world", type=int, default=8)
+    ap.add_argument("--rehearse_gbps_ch", type=float, default=25.0, help="modeled bus bandwidth per channel (GB/s)")
+    ap.add_argument("--rehearse_gbps_max", type=float, default=400.0, help="modeled bus bandwidth cap (GB/s)")
+    ap.add_argument("--rehearse_lds", type=int, default=32768, help="LDS bytes per modeled channel workgroup")
+    ap.add_argument("--rehearse_lat_us", type=float, default=20.0, help="modeled latency per all-reduce (us)")
     ap.add_argument("--pyprof", type=int, default=0,
                     help="N > 0: after the timed steps, run N more steps under cProfile and print the top host "
                          "functions (self time) to stderr -- where the eager step's issue time goes")
@@ -121,6 +134,10 @@ def main():
                     help="N > 0: after the timed steps, N more steps timing the HOST issue time of each step "
                          "(call to return, GPU running behind) against the GPU step time; printed to stderr")
     args = ap.parse_args()
+    if args.rehearse > 0:
+        args.rccl1 = 1
+        os.environ["DLMPI_RCCL_CHANNELS"] = str(args.rehearse)
+        os.environ.pop("NCCL_MAX_NCHANNELS", None)
     if args.gpus > 1 and not _under_launcher():
         sys.exit(launch_ranks(args.gpus, args.launcher, sys.argv[1:]))
     cfg = dict(PRESETS[args.config])
@@ -170,9 +187,19 @@ def main():
         from deeplearning_mpi_amd._ext import native
         from deeplearning_mpi_amd.parallel.comm import RcclCommunicator, rccl_channel_budget
 
-        rccl_channel_budget()
+        budget = rccl_channel_budget()
         nc = native().RcclComm(native().RcclComm.unique_id(), 0, 1, dev.index or 0)
-        rc = RcclCommunicator(comm.info, dev, nc)
+        if args.rehearse > 0:
+            class _Rehearsal(RcclCommunicator):
+                def bucket_comm(self):
+                    self.rbc = native().RehearsalBucketComm(self.c, args.rehearse_world, args.rehearse,
+                                                            args.rehearse_lds, args.rehearse_gbps_ch,
+                                                            args.rehearse_gbps_max, args.rehearse_lat_us)
+                    return self.rbc
+
+            rc = _Rehearsal(comm.info, dev, nc, budget=budget)
+        else:
+            rc = RcclCommunicator(comm.info, dev, nc, budget=budget)
         ddp = dl.DistributedDataParallel(model, bucket_cap_mb=args.bucket_mb, comm=rc, _force_reducer=True)
     else:
         ddp = dl.DistributedDataParallel(model, bucket_cap_mb=args.bucket_mb)
@@ -190,6 +217,13 @@ def main():
         opt.step()
         return loss
 
+    if args.graph == "auto":
+        from deeplearning_mpi_amd.apps.classification import use_graph
+
+        args.graph = "1" if (not args.pyprof and not args.rehearse and not args.rccl1 and
+                             use_graph(args, dev, pixels=cfg["batch"] * cfg["image"] * cfg["image"],
+                                       comm_backend=getattr(comm, "backend", "single"))) else "0"
+    args.graph = int(args.graph)
     if args.graph:
         from deeplearning_mpi_amd.utils.graphs import CapturedStep
 
@@ -217,7 +251,7 @@ def main():
     ips = global_batch * args.steps / dt
     # N > 1: a few untimed HIP-event-timed steps after the timed region answer "how much all-reduce
     # was left exposed after the backward pass" in the same JSON line
-    if args.breakdown == 0 and world > 1 and not args.graph:
+    if args.breakdown == 0 and (world > 1 or args.rehearse) and not args.graph:
         args.breakdown = 3
     bd_max = None
     if args.breakdown > 0 and not args.graph:
@@ -304,10 +338,12 @@ def main():
     # distributed facts of this run: the world size RCCL itself reports, its CU (channel) budget,
     # the gradient bucket layout, per-rank step times and the exposed all-reduce (max over ranks)
     native_comm = getattr(getattr(ddp.comm, "inner", ddp.comm), "c", None)
+    from deeplearning_mpi_amd._ext import native as _native
+
     dist_info = {
         "rccl_world_size": int(native_comm.size()) if native_comm is not None else None,
         "rccl_channels": os.environ.get("NCCL_MAX_NCHANNELS") if native_comm is not None else None,
-        "dgrad_stream_blocks": int(os.environ.get("DLMPI_DGS_BLOCKS", "256")),
+        "dgrad_stream_blocks": int(_native().dgs_blocks()),
         "bucket_mb": [round(b, 2) for b in ddp.bucket_sizes_mb()],
         "reducer": ddp.reducer is not None,
         "per_rank_ms_per_step": {"min": min(per_rank_ms), "max": max(per_rank_ms)},
@@ -315,6 +351,16 @@ def main():
     }
     if host_info is not None:
         dist_info["host_time"] = host_info
+    if args.rehearse > 0:
+        rbc = ddp.comm.rbc
+        dist_info["rehearsal"] = {
+            "channels": args.rehearse, "world_modeled": args.rehearse_world, "lds_bytes": args.rehearse_lds,
+            "gbps_per_channel": args.rehearse_gbps_ch, "gbps_max": args.rehearse_gbps_max,
+            "latency_us": args.rehearse_lat_us,
+            "modeled_allreduce_us_per_step": round(rbc.modeled_us_total() / max(1, rbc.buckets())
+                                                   * len(ddp.bucket_sizes_mb()), 1),
+            "buckets_launched": int(rbc.buckets()),
+        }
     if comm.rank == 0:
         headline = args.config == "resnet50" and cfg == PRESETS["resnet50"]
         print(json.dumps({

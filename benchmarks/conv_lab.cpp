@@ -127,9 +127,10 @@ int main(int argc, char** argv) {
       {"old128x128", 128, 128, 0, 0}, {"old256x128", 256, 128, 0, 0}, {"old256x64", 256, 64, 0, 0},
       {"oldhalo128", 128, 128, 0, 1}, {"oldhalo64", 128, 64, 0, 1},
       {"pipe256x256", 256, 256, 1, 0}, {"pipe256x256v1", 256, 256, 2, 0}, {"pipe256x256v2", 256, 256, 3, 0},
-      {"pipe256x256v3", 256, 256, 4, 0}, {"pipe224x256", 224, 256, 1, 0}, {"pipe224x256v1", 224, 256, 2, 0},
+      {"pipe256x256v3", 256, 256, 4, 0}, {"pipe256x256v4", 256, 256, 5, 0}, {"pipe224x256", 224, 256, 1, 0},
+      {"pipe224x256v1", 224, 256, 2, 0}, {"pipe224x256v2", 224, 256, 3, 0}, {"pipe224x256v4", 224, 256, 5, 0},
       {"pipe256x128", 256, 128, 1, 0}, {"pipe256x128v1", 256, 128, 2, 0}, {"pipe128x256", 128, 256, 1, 0},
-      {"pipe128x256v1", 128, 256, 2, 0}, {"pipe512x64", 512, 64, 1, 0}, {"pipe512x64v1", 512, 64, 2, 0},
+      {"pipe128x256v1", 128, 256, 2, 0}, {"pipe128x256v4", 128, 256, 5, 0}, {"pipe512x64v1", 512, 64, 2, 0},
   };
   const int NV = sizeof(vars) / sizeof(vars[0]);
   hipStream_t st;

@@ -466,6 +466,11 @@ void register_comm(pybind11::module& m) {
   py::class_<RcclBucketComm, CommBase, std::shared_ptr<RcclBucketComm>>(m, "RcclBucketComm")
       .def(py::init<std::shared_ptr<RcclComm>>());
 
+  py::class_<RehearsalBucketComm, CommBase, std::shared_ptr<RehearsalBucketComm>>(m, "RehearsalBucketComm")
+      .def(py::init<std::shared_ptr<RcclComm>, int, int, int, double, double, double>())
+      .def("modeled_us_total", &RehearsalBucketComm::modeled_us_total)
+      .def("buckets", &RehearsalBucketComm::buckets);
+
   py::class_<Reducer, std::shared_ptr<Reducer>>(m, "Reducer")
       .def(py::init<std::vector<at::Tensor>, std::vector<int64_t>, std::shared_ptr<CommBase>, bool>())
       .def("prepare_for_backward", &Reducer::prepare_for_backward)
@@ -481,5 +486,34 @@ void register_comm(pybind11::module& m) {
 void RcclBucketComm::begin_bucket() { comm_->fence_in(); }
 void RcclBucketComm::allreduce_bucket(at::Tensor t, bool average) { comm_->allreduce_async(t, average ? "avg" : "sum"); }
 void RcclBucketComm::end_backward() { comm_->fence_out(); }
+
+RehearsalBucketComm::RehearsalBucketComm(std::shared_ptr<RcclComm> c, int world, int channels, int lds_bytes,
+                                         double gbps_per_channel, double gbps_max, double latency_us)
+    : comm_(std::move(c)), world_(world), channels_(channels), lds_(lds_bytes), gbps_ch_(gbps_per_channel),
+      gbps_max_(gbps_max), lat_us_(latency_us) {
+  if (world_ < 2 || channels_ < 1 || gbps_ch_ <= 0 || gbps_max_ <= 0)
+    throw std::runtime_error("RehearsalBucketComm: world >= 2, channels >= 1, positive bandwidths");
+}
+void RehearsalBucketComm::begin_bucket() { comm_->fence_in(); }
+void RehearsalBucketComm::allreduce_bucket(at::Tensor t, bool average) {
+  comm_->allreduce_async(t, average ? "avg" : "sum");   // world size 1: the real RCCL launch path, identity data
+  const int64_t bytes = t.numel() * t.element_size();
+  if (!scratch_.defined() || scratch_.numel() < bytes) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    hipStream_t st = reinterpret_cast<hipStream_t>(comm_->stream_handle());
+    if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone)
+      throw std::runtime_error("RehearsalBucketComm: first use inside a capture");
+    scratch_ = at::empty({bytes + 16}, t.options().dtype(at::kByte));
+  }
+  const double frac = 2.0 * (world_ - 1) / world_;
+  const double bw = std::min(gbps_max_, channels_ * gbps_ch_) * 1e9;
+  const double us = frac * (double)bytes / bw * 1e6 + lat_us_;
+  modeled_us_ += us;
+  ++nbuckets_;
+  hip_check(dlmpi_comm_load(t.data_ptr(), bytes, scratch_.data_ptr(), (int64_t)(frac * bytes), channels_, lds_, us,
+                            reinterpret_cast<hipStream_t>(comm_->stream_handle())),
+            "comm_load");
+}
+void RehearsalBucketComm::end_backward() { comm_->fence_out(); }
 
 }  // namespace dlmpi_ext

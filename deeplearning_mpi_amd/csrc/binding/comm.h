@@ -72,6 +72,30 @@ class RcclBucketComm : public CommBase {
   std::shared_ptr<RcclComm> comm_;
 };
 
+// One-GPU rehearsal of an N-rank all-reduce's cost to the compute streams (comm.cpp): the real
+// (world-size-1) RCCL all-reduce, followed on the comm stream by a load kernel that occupies
+// `channels` workgroups with `lds_bytes` of LDS each, moves the ring all-reduce's per-rank traffic
+// 2 (W-1)/W * bytes, and holds the CUs for the modeled collective time
+// 2 (W-1)/W * bytes / min(gbps_max, channels * gbps_per_channel) + latency_us.
+class RehearsalBucketComm : public CommBase {
+ public:
+  RehearsalBucketComm(std::shared_ptr<RcclComm> c, int world, int channels, int lds_bytes, double gbps_per_channel,
+                      double gbps_max, double latency_us);
+  void begin_bucket() override;
+  void allreduce_bucket(at::Tensor t, bool average) override;
+  void end_backward() override;
+  double modeled_us_total() const { return modeled_us_; }   // sum over buckets since construction
+  int64_t buckets() const { return nbuckets_; }
+
+ private:
+  std::shared_ptr<RcclComm> comm_;
+  int world_, channels_, lds_;
+  double gbps_ch_, gbps_max_, lat_us_;
+  at::Tensor scratch_;
+  double modeled_us_ = 0.0;
+  int64_t nbuckets_ = 0;
+};
+
 // Gradient-bucket reducer (see comm.cpp).
 class Reducer {
  public:

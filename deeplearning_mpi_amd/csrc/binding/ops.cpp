@@ -114,17 +114,10 @@ static int bm_override() {   // experiments: force the M tile (64 | 128 | 256)
   return v;
 }
 
-static int sq256_min_tiles() {
-  static int v = [] {
-    const char* e = getenv("DLMPI_CONV_256SQ_MIN_TILES");
-    return e ? atoi(e) : 256;
-  }();
-  return v;
-}
-
-// cin: channel count of the GEMM's gathered operand (the 8-wave 256x256 kernel needs cin % 64 == 0)
+// cin: channel count of the GEMM's gathered operand
 static void pick_tiles(int64_t M, int Kout, int64_t red, int cin, int& bm, int& bn, bool pro = false,
                        bool wide1x1 = true) {
+  (void)pro;
   bn = Kout <= 64 ? 64 : 128;
   // 64 (mod 128) channels above 128 (the UNet's 192-channel top concat gradient): 64-wide tiles
   // cover them exactly instead of a half-empty last 128-wide tile (a third more MFMA work)
@@ -133,27 +126,6 @@ static void pick_tiles(int64_t M, int Kout, int64_t red, int cin, int& bm, int& 
   if (bm_override()) {
     bm = bm_override();
     if (bm == 256 && bn != 128) bm = 128;
-    return;
-  }
-  // long reductions into >= 256 output channels: 8-wave 256x256 tiles while the grid still gives
-  // every CU a block (UNet levels 3-5, the wide 3x3 layers)
-  // (the operand prologue exists for the single-stage kernels only)
-  if (!pro && Kout >= 256 && red >= 2304 && cin % 64 == 0 &&
-      ((M + 255) / 256) * ((Kout + 255) / 256) >= sq256_min_tiles()) {
-    bm = bn = 256;
-    return;
-  }
-  // DLMPI_CONV_WIDE=<max reduction>: 128 x 256 tiles of 8 waves for short reductions into
-  // 256-multiple outputs (each input row read once, every output row written whole by one block).
-  // Off by default: measured 15-25 % SLOWER than 128 x 128 on the ResNet-50 expand / reduce 1x1
-  // shapes and -6 % on the bench (profiles/r2_wide_rejected).
-  static const int wide = [] {
-    const char* e = getenv("DLMPI_CONV_WIDE");
-    return e ? atoi(e) : 0;
-  }();
-  if (!pro && wide > 0 && Kout % 256 == 0 && red <= wide && cin % 64 == 0 && (M + 127) / 128 >= 256) {
-    bm = 128;
-    bn = 256;
     return;
   }
   const int64_t nt = (Kout + bn - 1) / bn;
@@ -183,7 +155,12 @@ static int pipe_select(int f32, int pro, int cin, int64_t M, int Kout, int64_t r
     bn = Kout >= 256 ? 256 : (Kout > 64 ? 128 : 64);
     return 1;
   }
-  (void)M; (void)red;
+  // long reductions into >= 256 output channels while 256 x 256 tiles still give every CU one
+  // (UNet levels 3-5: the 8-wave tiles the single-stage kernel had, now pipelined)
+  if (Kout >= 256 && red >= 2304 && ((M + 255) / 256) * ((Kout + 255) / 256) >= 256) {
+    bm = bn = 256;
+    return 1;
+  }
   return 0;
 }
 
@@ -428,45 +405,29 @@ struct Pro3Extra {
 };
 static thread_local const Pro3Extra* g_pro3 = nullptr;
 
-// Operand prologue of the gathered operand (ConvArgs::pro): pro 1 = (k0 scale, k1 shift) of a deferred
-// BN-apply + ReLU; pro 2 = (k0 coef [3][C], pz = Z) of a deferred BN-backward apply; pro 3 = (k0 scale,
-// k1 shift, pz = residual) of the producer block's BN-apply + residual + ReLU, stored by the prologue.
+// Operand prologue of the gathered operand (ConvArgs::pro 3): (k0 scale, k1 shift, pz = residual) of
+// the producer block's BN-apply + residual + ReLU, computed and stored by the consumer's prologue.
 static void set_prologue(ConvArgs& a, int pro, const c10::optional<at::Tensor>& k0, const c10::optional<at::Tensor>& k1,
                          const c10::optional<at::Tensor>& pz, int ldpz, int pzoff) {
   a.pro = pro;
   if (pro == 0) return;
+  if (pro != 3) throw std::runtime_error("conv prologue: mode 3 (the producer's pending BN-apply) or none");
   if (a.C < 64 || a.C % 64) throw std::runtime_error("conv prologue: channel count must be a multiple of 64");
-  if (pro == 1) {
-    a.pscale = optr<float>(k0);
-    a.pshift = optr<float>(k1);
-    if (!a.pscale || !a.pshift || k0->numel() < a.C || k1->numel() < a.C)
-      throw std::runtime_error("conv prologue 1: scale / shift of C channels required");
-  } else if (pro == 2) {
-    a.pcoef = optr<float>(k0);
-    a.pz = optr<uint16_t>(pz);
-    a.ldpz = ldpz;
-    a.pzoff = pzoff;
-    if (!a.pcoef || !a.pz || k0->numel() < 3 * a.C || (ldpz | pzoff) % 8)
-      throw std::runtime_error("conv prologue 2: coef [3][C] and an 8-channel aligned Z required");
-  } else if (pro == 3) {
-    a.pscale = optr<float>(k0);
-    a.pshift = optr<float>(k1);
-    a.pz = optr<uint16_t>(pz);
-    a.ldpz = ldpz;
-    a.pzoff = pzoff;
-    const Pro3Extra* e = g_pro3;
-    if (!e || !a.pscale || !a.pshift || !a.pz || !e->y || !e->mbits || k0->numel() < a.C || k1->numel() < a.C ||
-        (ldpz | pzoff | e->ldy | e->yoff) % 8 || ((e->rscale != nullptr) != (e->rshift != nullptr)) || a.f32)
-      throw std::runtime_error("conv prologue 3: scale / shift, an aligned residual, y and mask bits required");
-    a.prscale = e->rscale;
-    a.prshift = e->rshift;
-    a.py = e->y;
-    a.ldpy = e->ldy;
-    a.pyoff = e->yoff;
-    a.pmbits = e->mbits;
-  } else {
-    throw std::runtime_error("conv prologue: mode 1, 2 or 3");
-  }
+  a.pscale = optr<float>(k0);
+  a.pshift = optr<float>(k1);
+  a.pz = optr<uint16_t>(pz);
+  a.ldpz = ldpz;
+  a.pzoff = pzoff;
+  const Pro3Extra* e = g_pro3;
+  if (!e || !a.pscale || !a.pshift || !a.pz || !e->y || !e->mbits || k0->numel() < a.C || k1->numel() < a.C ||
+      (ldpz | pzoff | e->ldy | e->yoff) % 8 || ((e->rscale != nullptr) != (e->rshift != nullptr)) || a.f32)
+    throw std::runtime_error("conv prologue 3: scale / shift, an aligned residual, y and mask bits required");
+  a.prscale = e->rscale;
+  a.prshift = e->rshift;
+  a.py = e->y;
+  a.ldpy = e->ldy;
+  a.pyoff = e->yoff;
+  a.pmbits = e->mbits;
 }
 
 static at::Tensor colsum_ws(const at::Tensor& like, int T, int C);
@@ -479,18 +440,10 @@ static int g_dgrad_stream_ran = 0;   // 1 if the last conv2d_dgrad ran the strea
 
 static bool stream1x1_shape(int64_t M, int C, int K, int R, int S, int stride, int pad, int pro, int f32, int& bm,
                             int& bn, int& G) {
-  if (R != 1 || S != 1 || stride != 1 || pad != 0 || pro > 1 || f32) return false;
-  if (!dlmpi_stream1x1_plan(M, C, K, &bm, &bn, &G)) return false;
-  // pro 1 (a deferred BN-apply + ReLU operand): plans with few output columns only
-  return pro == 0 || dlmpi_stream1x1_pro_ok(K / bn);
+  if (R != 1 || S != 1 || stride != 1 || pad != 0 || pro != 0 || f32) return false;
+  return dlmpi_stream1x1_plan(M, C, K, &bm, &bn, &G) != 0;
 }
 
-// The streaming kernel would run this 1x1 conv with a deferred BN-apply operand (engine: whether the
-// producer may skip its apply pass)
-bool conv_stream_pro_ok(int64_t M, int C, int K) {
-  int bm, bn, G;
-  return stream1x1_shape(M, C, K, 1, 1, 1, 0, 1, 0, bm, bn, G);
-}
 
 
 // y[n, p, q, yoff + k] = epilogue( sum_{r,s,c} x[n, p*stride - pad + r, q*stride - pad + s, xoff + c] * w[k][r][s][c] )
@@ -631,10 +584,6 @@ static int conv2d_fwd_impl(const at::Tensor& x, int N, int H, int W, int C, int 
         sa.bias = a.bias;
         sa.stats = a.stats;
         sa.G = G; sa.ntiles = K / sbn; sa.mtiles = ceil_div(M, sbm);
-        if (pro == 1) {
-          sa.pscale = a.pscale;
-          sa.pshift = a.pshift;
-        }
         if (a.stats && stats->size(0) < G) throw std::runtime_error("conv2d_fwd: stats buffer too small");
         check(dlmpi_conv1x1_stream(&sa, sbm, sbn, cur_stream()), "conv2d_fwd (stream 1x1)");
         g_stream_ran = 1;
@@ -1095,35 +1044,6 @@ void conv2d_wgrad_pro(const at::Tensor& dy, int lddy, int dyoff, int Ko, const a
   a.fdS = make_fastdiv((uint32_t)S);
   const int64_t wsz = (int64_t)Ko * a.TC;
   const int G = splits > 1 ? dlmpi_wgrad_reduce_groups(splits, wsz) : 0;
-  // In-launch split reduction (DLMPI_WGRAD_INLAUNCH = max splits; default 0 = off): the tile's last
-  // arriver reads all S slabs itself (a serial tail of S x 32-64 KB) and adds its tile into the fp32
-  // gradient from the accumulator fragments (a strided read-modify-write).  Measured slower than the
-  // slab workspace + two parallel reduction kernels at EVERY split count, S = 1 included (same box,
-  // profiles/r3_wgrad_inlaunch_off: ResNet-18 CIFAR hipGraph 76.4k img/s with <= 8 splits in-launch,
-  // 83.6k with only S = 1 in-launch, 89.5k with none; ResNet-50 11,830 -> 11,970; all splits
-  // in-launch: ResNet-50 7,630, profiles/r2_wgrad_inlaunch).
-  static const int inlaunch_max = [] {
-    const char* e = getenv("DLMPI_WGRAD_INLAUNCH");
-    return e ? atoi(e) : 0;
-  }();
-  if (inlaunch_max > 0 && splits <= inlaunch_max && !a.f32) {
-    hipStream_t st = cur_stream();
-    const int tiles_n = a.mtiles * a.ntiles;
-    float* slab = splits > 1 ? dlmpi_splitk_slab(st, (size_t)tiles_n * splits * bm * bn) : nullptr;
-    int* tk = splits > 1 ? dlmpi_splitk_tickets(st, tiles_n) : nullptr;
-    if (splits == 1 || (slab && tk)) {
-      a.ws = nullptr;
-      a.slab = slab;
-      a.tk = tk;
-      a.out = ptr<float>(grad);
-      a.T = R * S;
-      a.Creal = Creal;
-      a.Ko_real = Ko_real;
-      a.groups = std::max(1, G);
-      check(dlmpi_conv_wgrad(&a, bm, bn, st), "conv2d_wgrad");
-      return;
-    }
-  }
   at::Tensor ws = at::empty({(int64_t)(splits + G) * wsz}, dy.options().dtype(at::kFloat));
   a.ws = ptr<float>(ws);
   check(dlmpi_conv_wgrad(&a, bm, bn, cur_stream()), "conv2d_wgrad");
@@ -1512,13 +1432,14 @@ void register_ops(pybind11::module& m) {
   m.def("fill_", &fill_);
   m.def("set_conv_stream", [](int mode) { dlmpi_set_conv_stream(mode); });
   m.def("conv_stream_last", []() { return g_stream_ran; });
-  m.def("conv_stream_pro_ok", &conv_stream_pro_ok);
   m.def("set_dgrad_stream", [](int mode) { dlmpi_set_dgrad_stream(mode); });
   m.def("dgrad_stream_last", []() { return g_dgrad_stream_ran; });
   m.def("set_conv_autotune", [](int mode) { g_autotune_override = mode; });
   m.def("set_wgrad3", [](int mode) { g_wgrad3_override = mode; });
   m.def("set_conv_halo", [](int mode) { g_halo_override = mode; });
   m.def("set_conv_pipe", [](int mode) { g_pipe_override = mode; });
+  m.def("set_dgs_blocks", [](int n) { dlmpi_set_dgs_blocks(n); });
+  m.def("dgs_blocks", []() { return dlmpi_dgs_blocks(); });
   m.def("conv_halo_last", []() { return g_halo_ran; });
   m.def("conv2d_fwd_bn_apply", &conv2d_fwd_bn_apply);
   m.def("wgrad3_last", []() { return g_wgrad3_ran; });

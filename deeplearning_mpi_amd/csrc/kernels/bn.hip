@@ -618,7 +618,7 @@ extern "C" int dlmpi_reduce_blocks(int64_t M, int C) {
 
 // Storage-type dispatch of the templated kernels: f32 = 1 -> float activations (fp32 precision
 // path), 0 -> bf16.  TA(p) casts a `const void*` / `void*` launcher argument to the chosen type.
-#define DLMPI_TLAUNCH(KER, GRID, ...)                                               \
+#define LAUNCH_TLAUNCH(KER, GRID, ...)                                               \
   do {                                                                             \
     if (f32) {                                                                     \
       typedef float T;                                                             \
@@ -634,7 +634,7 @@ extern "C" int dlmpi_reduce_blocks(int64_t M, int C) {
 extern "C" hipError_t dlmpi_bn_stats(const void* x, int64_t M, int C, int ldx, int xoff, float* partial, int nblk,
                                      int f32, hipStream_t s) {
   if (C % 8 || C > 2048) return hipErrorInvalidValue;
-  DLMPI_TLAUNCH(bn_stats_kernel, dim3(nblk), CT(x), M, C, ldx, xoff, partial);
+  LAUNCH_TLAUNCH(bn_stats_kernel, dim3(nblk), CT(x), M, C, ldx, xoff, partial);
   return hipGetLastError();
 }
 
@@ -765,7 +765,7 @@ extern "C" hipError_t dlmpi_outer_dgrad_bn(const void* dy, int lddy, int64_t M, 
                                          const void* z, const float* mscale, const float* mshift, void* dx,
                                          float* partial, int nblk, int f32, hipStream_t s) {
   if (C % 8 || C > 2048 || M <= 0) return hipErrorInvalidValue;
-  DLMPI_TLAUNCH(outer_dgrad_bn_kernel, dim3(nblk), CT(dy), lddy, M, C, CT(w), ldw, CT(z), mscale, mshift, MT(dx),
+  LAUNCH_TLAUNCH(outer_dgrad_bn_kernel, dim3(nblk), CT(dy), lddy, M, C, CT(w), ldw, CT(z), mscale, mshift, MT(dx),
                 partial);
   return hipGetLastError();
 }
@@ -806,7 +806,7 @@ extern "C" hipError_t dlmpi_bn_apply2(const void* x, int ldx, int xoff, int64_t 
                                       int f32, hipStream_t s) {
   if (C % 8 || ((rscale != nullptr) != (rshift != nullptr)) || (rscale && !res)) return hipErrorInvalidValue;
   const int64_t total = M * (C / 8);
-  DLMPI_TLAUNCH(bn_apply_kernel, dim3(ew_blocks(total)), CT(x), ldx, xoff, M, C, make_fastdiv(C / 8), scale, shift,
+  LAUNCH_TLAUNCH(bn_apply_kernel, dim3(ew_blocks(total)), CT(x), ldx, xoff, M, C, make_fastdiv(C / 8), scale, shift,
                 CT(res), ldres, resoff, relu, MT(y), ldy, yoff, mbits, rscale, rshift);
   return hipGetLastError();
 }
@@ -823,7 +823,7 @@ extern "C" hipError_t dlmpi_bn_bwd_reduce(const void* dy, int lddy, int dyoff, c
                                           const float* mean, const float* invstd, float* partial, int nblk,
                                           int f32, hipStream_t s) {
   if (C % 8 || C > 2048) return hipErrorInvalidValue;
-  DLMPI_TLAUNCH(bn_bwd_reduce_kernel, dim3(nblk), CT(dy), lddy, dyoff, CT(ymask), ldym, ymoff, CT(x), ldx, xoff, M, C,
+  LAUNCH_TLAUNCH(bn_bwd_reduce_kernel, dim3(nblk), CT(dy), lddy, dyoff, CT(ymask), ldym, ymoff, CT(x), ldx, xoff, M, C,
                 mean, invstd, partial);
   return hipGetLastError();
 }
@@ -857,7 +857,7 @@ extern "C" hipError_t dlmpi_bn_bwd_apply(const void* dy, int lddy, int dyoff, co
                                          const float* coef, void* dx, void* dyr_out, int f32, hipStream_t s) {
   if (C % 8) return hipErrorInvalidValue;
   const int64_t total = M * (C / 8);
-  DLMPI_TLAUNCH(bn_bwd_apply_kernel, dim3(ew_blocks(total)), CT(dy), lddy, dyoff, CT(ymask), ldym, ymoff, CT(x), ldx,
+  LAUNCH_TLAUNCH(bn_bwd_apply_kernel, dim3(ew_blocks(total)), CT(dy), lddy, dyoff, CT(ymask), ldym, ymoff, CT(x), ldx,
                 xoff, M, C, make_fastdiv(C / 8), coef, MT(dx), MT(dyr_out));
   return hipGetLastError();
 }
@@ -866,7 +866,7 @@ extern "C" hipError_t dlmpi_bn_bwd_apply(const void* dy, int lddy, int dyoff, co
 extern "C" hipError_t dlmpi_dual_dgrad_weights(const void* w, int C, int K, const float* coef, void* w2, float* b,
                                                int f32, hipStream_t s) {
   if (C <= 0 || K <= 0) return hipErrorInvalidValue;
-  DLMPI_TLAUNCH(dual_dgrad_weights_kernel, dim3(C), CT(w), K, coef, MT(w2), b);
+  LAUNCH_TLAUNCH(dual_dgrad_weights_kernel, dim3(C), CT(w), K, coef, MT(w2), b);
   return hipGetLastError();
 }
 
@@ -889,24 +889,24 @@ extern "C" hipError_t dlmpi_maxpool_bwd_bn(const void* dy, const uint8_t* idx, i
     const char* e = getenv("DLMPI_POOL_BWD_GENERIC");
     return e && atoi(e) != 0;
   }();
-#define DLMPI_MPB1(NW, T)                                                                                          \
+#define LAUNCH_MPB1(NW, T)                                                                                          \
   hipLaunchKernelGGL((maxpool_bwd_bn_kernel<NW, T>), dim3(nblk), dim3(256), 0, s, CT(dy), idx, N, H, W, C, k, stride, \
                      pad, OH, OW, make_fastdiv(W), make_fastdiv(H), CT(z), mscale, mshift, CT(add), ldadd, addoff,   \
                      MT(dx), partial)
-#define DLMPI_MPB(NW)          \
+#define LAUNCH_MPB(NW)          \
   do {                         \
     if (f32) {                 \
       typedef float T;         \
-      DLMPI_MPB1(NW, T);       \
+      LAUNCH_MPB1(NW, T);       \
     } else {                   \
       typedef uint16_t T;      \
-      DLMPI_MPB1(NW, T);       \
+      LAUNCH_MPB1(NW, T);       \
     }                          \
   } while (0)
-  if (!generic && nw == 1) DLMPI_MPB(1);
-  else if (!generic && nw == 2) DLMPI_MPB(2);
-  else DLMPI_MPB(0);
-#undef DLMPI_MPB
-#undef DLMPI_MPB1
+  if (!generic && nw == 1) LAUNCH_MPB(1);
+  else if (!generic && nw == 2) LAUNCH_MPB(2);
+  else LAUNCH_MPB(0);
+#undef LAUNCH_MPB
+#undef LAUNCH_MPB1
   return hipGetLastError();
 }

@@ -342,21 +342,29 @@ using namespace dlmpi;
 // opt-in tile variants)
 static int g_dgs_override = -1;
 extern "C" void dlmpi_set_dgrad_stream(int mode) { g_dgs_override = mode; }
+// grid-size budget (blocks) set by the communicator that owns the CUs RCCL takes (parallel/comm.py
+// rccl_channel_budget); <= 0: DLMPI_DGS_BLOCKS or one block per CU
+static int g_dgs_blocks = 0;
+extern "C" void dlmpi_set_dgs_blocks(int n) { g_dgs_blocks = n; }
+extern "C" int dlmpi_dgs_blocks() {
+  static const int env = [] {
+    const char* e = getenv("DLMPI_DGS_BLOCKS");
+    return e ? atoi(e) : 256;
+  }();
+  return g_dgs_blocks > 0 ? g_dgs_blocks : env;
+}
 
 // Tile plan: BM rows per tile and G blocks per 128-channel column (one block per CU over the chip),
 // or 0 if the kernel does not apply to this shape.
-// DLMPI_DGS_BLOCKS: grid size target (default 256 = one block per CU; more blocks = less work per
-// block, so a block that starts late behind another stream's kernel extends the tail less).
+// Grid size target: dlmpi_dgs_blocks() (default 256 = one block per CU; fewer with an RCCL
+// communicator whose channels hold CUs).
 extern "C" int dlmpi_dgrad_stream_plan(int64_t M, int K, int Kout, int mask_mode, int z2, int has_res, int* bm, int* bn,
                                        int* G) {
   static const int env = [] {
     const char* e = getenv("DLMPI_DGRAD_STREAM");
     return e ? atoi(e) : 1;
   }();
-  static const int blocks = [] {
-    const char* e = getenv("DLMPI_DGS_BLOCKS");
-    return e ? atoi(e) : 256;
-  }();
+  const int blocks = dlmpi_dgs_blocks();
   const int on = g_dgs_override >= 0 ? g_dgs_override : env;
   if (!on || M <= 0 || mask_mode < 0 || mask_mode > 2 || (z2 && mask_mode == 0)) return 0;
   // LDS per block (one block per CU): weights KS x BN x 128 B resident + A + 2 x epilogue operands
@@ -394,7 +402,7 @@ extern "C" int dlmpi_dgrad_stream_plan(int64_t M, int K, int Kout, int mask_mode
 
 extern "C" hipError_t dlmpi_conv1x1_dgrad_stream(const DgradStreamArgs* a, int bm, int bn, int mask_mode, hipStream_t s) {
   const dim3 grid((unsigned)(a->ntiles * a->G));
-#define DLMPI_DGS(BM_, BN_, KS_, NW_, WGM_, ADB_)                                                                   \
+#define LAUNCH_DGS(BM_, BN_, KS_, NW_, WGM_, ADB_)                                                                   \
   do {                                                                                                       \
     const dim3 blk(64 * NW_);                                                                                \
     if (a->z2) {                                                                                             \
@@ -404,7 +412,7 @@ extern "C" hipError_t dlmpi_conv1x1_dgrad_stream(const DgradStreamArgs* a, int b
     else if (mask_mode == 2) hipLaunchKernelGGL((conv1x1_dgrad_stream_kernel<BM_, BN_, KS_, NW_, WGM_, 2, false, ADB_>), grid, blk, 0, s, *a); \
     else hipLaunchKernelGGL((conv1x1_dgrad_stream_kernel<BM_, BN_, KS_, NW_, WGM_, 0, false, ADB_>), grid, blk, 0, s, *a); \
   } while (0)
-  if (bm == 64 && bn == 128 && a->K == 128) DLMPI_DGS(64, 128, 2, 8, 2, false);
+  if (bm == 64 && bn == 128 && a->K == 128) LAUNCH_DGS(64, 128, 2, 8, 2, false);
   else if (bm == 48 && bn == 128 && a->K == 256 && !a->z2) {
     if (mask_mode == 1) hipLaunchKernelGGL((conv1x1_dgrad_stream_kernel<48, 128, 4, 6, 3, 1, false, false>), grid, dim3(384), 0, s, *a);
     else if (mask_mode == 2) hipLaunchKernelGGL((conv1x1_dgrad_stream_kernel<48, 128, 4, 6, 3, 2, false, false>), grid, dim3(384), 0, s, *a);
@@ -417,13 +425,13 @@ extern "C" hipError_t dlmpi_conv1x1_dgrad_stream(const DgradStreamArgs* a, int b
     else if (mask_mode == 2) hipLaunchKernelGGL((conv1x1_dgrad_stream_kernel<32, 128, 4, 4, 2, 2, false, false>), grid, dim3(256), 0, s, *a);
     else hipLaunchKernelGGL((conv1x1_dgrad_stream_kernel<32, 128, 4, 4, 2, 0, false, false>), grid, dim3(256), 0, s, *a);
   }
-  else if (bm == 32 && bn == 64 && a->K == 512) DLMPI_DGS(32, 64, 8, 4, 2, false);
+  else if (bm == 32 && bn == 64 && a->K == 512) LAUNCH_DGS(32, 64, 8, 4, 2, false);
   else if (bm == 64 && bn == 64 && a->K == 512 && !a->z2 && !a->res) {   // z-mask / plain only
     if (mask_mode == 2) hipLaunchKernelGGL((conv1x1_dgrad_stream_kernel<64, 64, 8, 8, 2, 2, false, false>), grid, dim3(512), 0, s, *a);
     else if (mask_mode == 0) hipLaunchKernelGGL((conv1x1_dgrad_stream_kernel<64, 64, 8, 8, 2, 0, false, false>), grid, dim3(512), 0, s, *a);
     else return hipErrorInvalidValue;
   }
   else return hipErrorInvalidValue;
-#undef DLMPI_DGS
+#undef LAUNCH_DGS
   return hipGetLastError();
 }

@@ -42,10 +42,7 @@ constexpr int vmcnt_imm(int n) { return (n & 15) | 0x70 | 0xF00 | ((n >> 4) << 1
 
 __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
-// PRO: the activations are a deferred BN-apply + ReLU (the producer's output never stored): every
-// thread rewrites the pieces it fetched, in LDS, as relu(x * pscale[c] + pshift[c]) (the fma order
-// of bn_apply_kernel: bit-identical to the stored schedule) once they have landed, before the MFMAs.
-template <int BM, int BN, int KS, bool STATS, bool PRO = false>
+template <int BM, int BN, int KS, bool STATS>
 __global__ __launch_bounds__(256) void conv1x1_stream_kernel(const Stream1x1Args a) {
   constexpr int NT = 256;
   constexpr int WM = BM / 2, WN = BN / 2;       // 2 x 2 waves
@@ -116,18 +113,6 @@ __global__ __launch_bounds__(256) void conv1x1_stream_kernel(const Stream1x1Args
   float s1[8], s2[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) { s1[e] = 0.f; s2[e] = 0.f; }
-  // prologue coefficients of the 8 channels of each K-step this lane fetches
-  f32x4 pk[PRO ? KS : 1][4];
-  if constexpr (PRO) {
-#pragma unroll
-    for (int ks = 0; ks < KS; ++ks) {
-      const int c = ks * 64 + 8 * jc;
-      pk[ks][0] = *reinterpret_cast<const f32x4*>(a.pscale + c);
-      pk[ks][1] = *reinterpret_cast<const f32x4*>(a.pscale + c + 4);
-      pk[ks][2] = *reinterpret_cast<const f32x4*>(a.pshift + c);
-      pk[ks][3] = *reinterpret_cast<const f32x4*>(a.pshift + c + 4);
-    }
-  }
 
   int mt = g;
   if (mt < a.mtiles) issue_a(mt);
@@ -139,24 +124,6 @@ __global__ __launch_bounds__(256) void conv1x1_stream_kernel(const Stream1x1Args
     // adds no conservative vmcnt(0) of its own before the activation reads)
     __builtin_amdgcn_s_waitcnt(vmcnt_imm(NSTORE));
     lds_barrier();   // every wave's pieces are in LDS; the previous tile's staging reads are done
-    if constexpr (PRO) {   // rewrite this lane's own pieces in place (after the barrier: otherwise the
-                           // compiler drains the in-flight stores before these reads)
-#pragma unroll
-      for (int ks = 0; ks < KS; ++ks)
-#pragma unroll
-        for (int i = 0; i < AL; ++i) {
-          u32x4* pa = reinterpret_cast<u32x4*>(As + ks * BM * 128 + RP * i * 128 + tid * 16);
-          float v[8];
-          unpack8(*pa, v);
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            v[e] = fmaxf(__builtin_fmaf(v[e], pk[ks][0][e], pk[ks][2][e]), 0.f);
-            v[e + 4] = fmaxf(__builtin_fmaf(v[e + 4], pk[ks][1][e], pk[ks][3][e]), 0.f);
-          }
-          *pa = pack8(v);
-        }
-      lds_barrier();
-    }
 
     f32x4 acc[TM][TN];
 #pragma unroll
@@ -254,58 +221,23 @@ __global__ __launch_bounds__(256) void conv1x1_stream_kernel(const Stream1x1Args
 using namespace dlmpi;
 
 // Tile plan of the streaming kernel: (BM, BN, blocks per N-tile G) or false if it does not apply.
+// (C = 512, the layer-4 expand, measured slower than the general kernel: 144 KB of LDS leave one block
+// per CU, 58.3 vs 50.7 us, profiles/r3_stream1x1; C = 256 on 64 x 128 tiles was neutral,
+// profiles/r3_c256.)
 static int g_stream_override = -1;   // dlmpi_ext set_conv_stream (tests)
-// DLMPI_CONV_STREAM_C512=1: C = 512 (layer-4 expand, 7^2 512->2048) through the streaming kernel
-// too.  Off by default: its 144 KB of LDS leave one block per CU and it measured slower than the
-// general kernel (58.3 vs 50.7 us, profiles/r3_stream1x1/c512_*).
-static bool stream_c512() {
-  static const bool v = [] {
-    const char* e = getenv("DLMPI_CONV_STREAM_C512");
-    return e && atoi(e) != 0;
-  }();
-  return v;
-}
 extern "C" void dlmpi_set_conv_stream(int mode) { g_stream_override = mode; }
-// DLMPI_STREAM_C256_BN=128: C = 256 (layer-3 expand, 14^2 256 -> 1024) on 64 x 128 tiles (one block per
-// CU, 8 output columns re-reading each activation tile from L2) instead of 64 x 64 (2 blocks per CU,
-// 16 columns): A/B (profiles/r3_c256)
-static int c256_bn() {
-  static const int v = [] {
-    const char* e = getenv("DLMPI_STREAM_C256_BN");
-    return e ? atoi(e) : 64;
-  }();
-  return v;
-}
-
-// Operand prologue (a deferred BN-apply + ReLU) on the streaming kernel: every N-tile column's blocks
-// rewrite the same activation rows, so only plans with few columns take it (DLMPI_STREAM_PRO: max
-// columns, default 4 -- the ResNet-50 layer-1 / layer-2 expand convs; 0 = never).
-extern "C" int dlmpi_stream1x1_pro_ok(int ntiles) {
-  static const int v = [] {
-    const char* e = getenv("DLMPI_STREAM_PRO");
-    return e ? atoi(e) : 4;
-  }();
-  return ntiles <= v ? 1 : 0;
-}
 
 extern "C" int dlmpi_stream1x1_plan(int64_t M, int C, int Kout, int* bm, int* bn, int* G) {
-  static const int env = [] {
-    const char* e = getenv("DLMPI_CONV_STREAM");
-    return e ? atoi(e) : 1;
-  }();
-  const int on = g_stream_override >= 0 ? g_stream_override : env;
+  const int on = g_stream_override >= 0 ? g_stream_override : 1;
   if (!on || M <= 0) return 0;
   if (C == 64 && Kout % 128 == 0) { *bm = 128; *bn = 128; }
   else if (C == 128 && Kout % 128 == 0) { *bm = 64; *bn = 128; }
-  else if (C == 256 && Kout % 128 == 0 && c256_bn() == 128) { *bm = 64; *bn = 128; }   // 113 KB: 1 block / CU
   else if (C == 256 && Kout % 64 == 0) { *bm = 64; *bn = 64; }
-  else if (C == 512 && Kout % 64 == 0 && stream_c512()) { *bm = 64; *bn = 64; }
   else return 0;
   const int ntiles = Kout / *bn;
   const int64_t mtiles = (M + *bm - 1) / *bm;
-  // ~2 resident blocks per CU over the whole chip (LDS 65-80 KB per block); C = 512 holds 144 KB
-  // (1 block per CU)
-  int target = (C == 512 || (C == 256 && *bn == 128) ? 256 : 512) / ntiles;
+  // ~2 resident blocks per CU over the whole chip (LDS 65-80 KB per block)
+  int target = 512 / ntiles;
   if (target < 8) target = 8;
   *G = (int)(mtiles < target ? mtiles : target);
   return 1;
@@ -313,20 +245,15 @@ extern "C" int dlmpi_stream1x1_plan(int64_t M, int C, int Kout, int* bm, int* bn
 
 extern "C" hipError_t dlmpi_conv1x1_stream(const Stream1x1Args* a, int bm, int bn, hipStream_t s) {
   const dim3 grid((unsigned)(a->ntiles * a->G)), block(256);
-#define DLMPI_S1(BM_, BN_, KS_)                                                                              \
+#define LAUNCH_S1(BM_, BN_, KS_)                                                                              \
   do {                                                                                                      \
-    if (a->pscale) {                                                                                        \
-      if (a->stats) hipLaunchKernelGGL((conv1x1_stream_kernel<BM_, BN_, KS_, true, true>), grid, block, 0, s, *a); \
-      else hipLaunchKernelGGL((conv1x1_stream_kernel<BM_, BN_, KS_, false, true>), grid, block, 0, s, *a);  \
-    } else if (a->stats) hipLaunchKernelGGL((conv1x1_stream_kernel<BM_, BN_, KS_, true>), grid, block, 0, s, *a); \
+    if (a->stats) hipLaunchKernelGGL((conv1x1_stream_kernel<BM_, BN_, KS_, true>), grid, block, 0, s, *a);     \
     else hipLaunchKernelGGL((conv1x1_stream_kernel<BM_, BN_, KS_, false>), grid, block, 0, s, *a);          \
   } while (0)
-  if (bm == 128 && bn == 128 && a->C == 64) DLMPI_S1(128, 128, 1);
-  else if (bm == 64 && bn == 128 && a->C == 128) DLMPI_S1(64, 128, 2);
-  else if (bm == 64 && bn == 64 && a->C == 256) DLMPI_S1(64, 64, 4);
-  else if (bm == 64 && bn == 128 && a->C == 256) DLMPI_S1(64, 128, 4);
-  else if (bm == 64 && bn == 64 && a->C == 512) DLMPI_S1(64, 64, 8);
+  if (bm == 128 && bn == 128 && a->C == 64) LAUNCH_S1(128, 128, 1);
+  else if (bm == 64 && bn == 128 && a->C == 128) LAUNCH_S1(64, 128, 2);
+  else if (bm == 64 && bn == 64 && a->C == 256) LAUNCH_S1(64, 64, 4);
   else return hipErrorInvalidValue;
-#undef DLMPI_S1
+#undef LAUNCH_S1
   return hipGetLastError();
 }

@@ -27,7 +27,11 @@
 // Staging (both): global -> LDS directly with global_load_lds_dwordx4 (no VGPR round trip, no
 // ds_write): each wave instruction fills 8 LDS rows of 128 B lane-linearly; the XOR swizzle that
 // makes the ds_read_b128 fragment reads bank-conflict-free is applied on the per-lane SOURCE address
-// (cdna_hip_programming.md §5.4 rule 21).  Out-of-image im2col pieces read a zero page.  Channel
+// (cdna_hip_programming.md §5.4 rule 21): chunk ch of row r sits at slot ch ^ (r & 7).  That is
+// conflict-free for 16 consecutive rows starting at ANY row (benchmarks/lds_banks.py), which the
+// halo tiles need -- their fragment rows start at a tap-dependent halo offset; the former
+// ch ^ ((r >> 1) & 7) was 2-way conflicted at 3 of every 4 offsets (halo: SQ_LDS_BANK_CONFLICT 92 % of
+// the LDS-active cycles, profiles/r4_lab).  Out-of-image im2col pieces read a zero page.  Channel
 // counts >= 64: the tap (r, s) and channel base are wave-uniform scalars and the per-row source
 // pointers are rebuilt only when the tap changes.  All LDS is ONE __shared__ array: with a second
 // LDS object hipcc tracks the DMA targets and waits for every in-flight DMA before each fragment read.
@@ -301,7 +305,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BM * BN <= 
   constexpr int ES = sizeof(T);               // bytes per element
   constexpr int BK = 128 / ES;                // reduction elements per K-step (one 128-B LDS row)
   constexpr int CPC = 16 / ES;                // channels per 16-byte chunk
-  static_assert(PRO == 0 || ES == 2, "operand prologues: bf16 only");
+  static_assert(PRO == 0 || (PRO == 3 && ES == 2), "operand prologue: mode 3, bf16");
   constexpr int WM = BM / WGM, WN = BN / WGN;
   constexpr int TM = WM / 16, TN = WN / 16;
   constexpr int RP = NT / 8;                  // tile rows staged per pass (8 lanes per 128-B row)
@@ -311,7 +315,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BM * BN <= 
   constexpr int HL = HALO ? HALO_ROWS * 128 / (16 * 64 * NW) : 1;   // halo pieces per thread
   constexpr int A_BYTES = (HALO ? HALO_ROWS : BM) * 128, B_BYTES = BN * 128;
   static_assert(PRO == 0 || !SMALLC, "operand prologue: regular channels");
-  constexpr int Z_BYTES = PRO >= 2 ? A_BYTES : 0;   // the second prologue operand, staged like A
+  constexpr int Z_BYTES = PRO == 3 ? A_BYTES : 0;   // the prologue's residual operand, staged like A
   constexpr int SB = A_BYTES + B_BYTES + Z_BYTES;   // bytes of the stage: [A | B | Z]
   constexpr int EPI_NEED = EpiSmem<BM, BN, NT, WM>::bytes;
   constexpr int SMEM = SB > EPI_NEED ? SB : EPI_NEED;
@@ -321,7 +325,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BM * BN <= 
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wid / WGN, wn = wid % WGN;
   const int lrow = tid >> 3;                          // staging row (+RP i)
-  const int jc = (tid & 7) ^ ((tid >> 4) & 7);        // swizzled 16-B chunk this lane fetches
+  const int jc = (tid & 7) ^ ((tid >> 3) & 7);        // swizzled 16-B chunk this lane fetches (row & 7)
   const char* zp = reinterpret_cast<const char*>(g_zero_page);
 
   const int zph = blockIdx.z;
@@ -375,7 +379,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BM * BN <= 
   // ---- staging ------------------------------------------------------------------------------
   // Regular path (C % 64 == 0): the tap t and channel base c are wave-uniform.
   uint32_t a_off[AL];                                 // element offset of the row's input pixel
-  uint32_t z_off[PRO >= 2 ? AL : 1];                  // the same pixel in the prologue's Z
+  uint32_t z_off[PRO == 3 ? AL : 1];                  // the same pixel in the prologue's Z
   uint32_t a_vm = 0;                                  // bit i: (row, tap) inside the image
   int t_cur = 0, c_cur = 0, wtC2 = 0;
   auto tap_setup = [&](int t) {
@@ -392,10 +396,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BM * BN <= 
       const bool ok = ((a_okm >> i) & 1) && (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W;
       if (ok) a_vm |= 1u << i;
       a_off[i] = (uint32_t)(a_pix[i] + doff) * (uint32_t)a.ldx;
-      if constexpr (PRO >= 2) z_off[i] = (uint32_t)(a_pix[i] + doff) * (uint32_t)a.ldpz;
+      if constexpr (PRO == 3) z_off[i] = (uint32_t)(a_pix[i] + doff) * (uint32_t)a.ldpz;
     }
   };
-  const char* zlane = PRO >= 2 ? reinterpret_cast<const char*>(a.pz) + ES * ((int64_t)a.pzoff + CPC * jc) : nullptr;
+  const char* zlane = PRO == 3 ? reinterpret_cast<const char*>(a.pz) + ES * ((int64_t)a.pzoff + CPC * jc) : nullptr;
 
   // HALO staging: piece i of this lane = halo row lrow + RP i (chunk jc), i.e. halo pixel (line,
   // col) relative to the tile origin; rows past the halo read the zero page
@@ -450,7 +454,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BM * BN <= 
         const char* s = ((a_vm >> i) & 1) ? xlane + ES * ((uint64_t)a_off[i] + c_cur) : zp;
         glds16(s, As + (RP * i + 8 * wid) * 128);
       }
-      if constexpr (PRO >= 2) {
+      if constexpr (PRO == 3) {
         char* Zs = Bs + B_BYTES;
 #pragma unroll
         for (int i = 0; i < AL; ++i) {
@@ -489,92 +493,61 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BM * BN <= 
     }
   };
 
-  // Operand prologue: this lane's own staged A pieces (row lrow + RP i, chunk jc = channels
-  // c_cur + 8 jc of the current tap) are rewritten in place once the stage has landed; pieces of
-  // out-of-image taps / rows past M hold zeros and are left alone.  Same fma order and bf16
-  // rounding as the standalone kernels it replaces (bn_apply_kernel / bn_bwd_apply_kernel), so the
-  // fused and the unfused schedules are bit-identical.
+  // Operand prologue (PRO 3, 1x1 / stride-1 consumers): this lane's own staged A pieces (row
+  // lrow + RP i, chunk jc = channels c_cur + 8 jc) are the producer block's BN input z; once the stage
+  // has landed they are rewritten in place as y = relu(z * scale + shift + r) -- r the staged
+  // residual Z, or Z * rscale + rshift for a BN-output residual -- with bn_apply_kernel's arithmetic
+  // in the same order (bit-identical to the unfused schedule); the blocks of output tile column 0 also
+  // store y and its ReLU mask bits.  Pieces of rows past M hold zeros and are left alone.
   auto prologue = [&]() {
-    if constexpr (PRO != 0) {
+    if constexpr (PRO == 3) {
       char* As = smem;
       const int c = c_cur + 8 * jc;
-      f32x4 k0a, k0b, k1a, k1b, k2a, k2b, kra, krb;
-      if constexpr (PRO == 1 || PRO == 3) {
-        k0a = *reinterpret_cast<const f32x4*>(a.pscale + c);
-        k0b = *reinterpret_cast<const f32x4*>(a.pscale + c + 4);
-        k1a = *reinterpret_cast<const f32x4*>(a.pshift + c);
-        k1b = *reinterpret_cast<const f32x4*>(a.pshift + c + 4);
-        if constexpr (PRO == 3) {
-          if (a.prscale) {
-            k2a = *reinterpret_cast<const f32x4*>(a.prscale + c);
-            k2b = *reinterpret_cast<const f32x4*>(a.prscale + c + 4);
-            kra = *reinterpret_cast<const f32x4*>(a.prshift + c);
-            krb = *reinterpret_cast<const f32x4*>(a.prshift + c + 4);
-          }
-        }
-      } else {
-        k0a = *reinterpret_cast<const f32x4*>(a.pcoef + c);
-        k0b = *reinterpret_cast<const f32x4*>(a.pcoef + c + 4);
-        k1a = *reinterpret_cast<const f32x4*>(a.pcoef + C + c);
-        k1b = *reinterpret_cast<const f32x4*>(a.pcoef + C + c + 4);
-        k2a = *reinterpret_cast<const f32x4*>(a.pcoef + 2 * C + c);
-        k2b = *reinterpret_cast<const f32x4*>(a.pcoef + 2 * C + c + 4);
+      const f32x4 k0a = *reinterpret_cast<const f32x4*>(a.pscale + c);
+      const f32x4 k0b = *reinterpret_cast<const f32x4*>(a.pscale + c + 4);
+      const f32x4 k1a = *reinterpret_cast<const f32x4*>(a.pshift + c);
+      const f32x4 k1b = *reinterpret_cast<const f32x4*>(a.pshift + c + 4);
+      f32x4 k2a, k2b, kra, krb;
+      if (a.prscale) {
+        k2a = *reinterpret_cast<const f32x4*>(a.prscale + c);
+        k2b = *reinterpret_cast<const f32x4*>(a.prscale + c + 4);
+        kra = *reinterpret_cast<const f32x4*>(a.prshift + c);
+        krb = *reinterpret_cast<const f32x4*>(a.prshift + c + 4);
       }
 #pragma unroll
       for (int i = 0; i < AL; ++i) {
         if (!((a_vm >> i) & 1)) continue;
         u32x4* pa = reinterpret_cast<u32x4*>(As + RP * i * 128 + tid * 16);
-        float v[8];
+        float v[8], r[8];
         unpack8(*pa, v);
-        if constexpr (PRO == 1) {
+        unpack8(*reinterpret_cast<const u32x4*>(As + A_BYTES + B_BYTES + RP * i * 128 + tid * 16), r);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          v[e] = __builtin_fmaf(v[e], k0a[e], k1a[e]);
+          v[e + 4] = __builtin_fmaf(v[e + 4], k0b[e], k1b[e]);
+        }
+        if (a.prscale) {
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
-            v[e] = fmaxf(__builtin_fmaf(v[e], k0a[e], k1a[e]), 0.f);
-            v[e + 4] = fmaxf(__builtin_fmaf(v[e + 4], k0b[e], k1b[e]), 0.f);
-          }
-        } else if constexpr (PRO == 3) {
-          // the producer block's BN-apply + residual + ReLU (bn_apply_kernel's arithmetic, same
-          // order), written back as the A operand AND stored: y and its ReLU mask bits
-          float r[8];
-          unpack8(*reinterpret_cast<const u32x4*>(As + A_BYTES + B_BYTES + RP * i * 128 + tid * 16), r);
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            v[e] = __builtin_fmaf(v[e], k0a[e], k1a[e]);
-            v[e + 4] = __builtin_fmaf(v[e + 4], k0b[e], k1b[e]);
-          }
-          if (a.prscale) {
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              r[e] = __builtin_fmaf(r[e], k2a[e], kra[e]);
-              r[e + 4] = __builtin_fmaf(r[e + 4], k2b[e], krb[e]);
-            }
-          }
-#pragma unroll
-          for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e] + r[e], 0.f);
-          const u32x4 pk = pack8(v);
-          *pa = pk;
-          if (nt == 0) {   // with several output tile columns every column's blocks rebuild y; one stores it
-            const int64_t px = a_pix[i];   // 1x1 / stride 1 (host-checked): input pixel = tile row
-            *reinterpret_cast<u32x4*>(a.py + px * a.ldpy + a.pyoff + c) = pk;
-            uint32_t b = 0;
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-              b |= (uint32_t)((pk[k] & 0xffffu) != 0u && !(pk[k] & 0x8000u)) << (2 * k);
-              b |= (uint32_t)((pk[k] >> 16) != 0u && !(pk[k] & 0x80000000u)) << (2 * k + 1);
-            }
-            a.pmbits[px * (C >> 3) + (c >> 3)] = (uint8_t)b;
-          }
-          continue;
-        } else {
-          float zv[8];
-          unpack8(*reinterpret_cast<const u32x4*>(As + A_BYTES + B_BYTES + RP * i * 128 + tid * 16), zv);
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            v[e] = __builtin_fmaf(k0a[e], v[e], __builtin_fmaf(k1a[e], zv[e], k2a[e]));
-            v[e + 4] = __builtin_fmaf(k0b[e], v[e + 4], __builtin_fmaf(k1b[e], zv[e + 4], k2b[e]));
+            r[e] = __builtin_fmaf(r[e], k2a[e], kra[e]);
+            r[e + 4] = __builtin_fmaf(r[e + 4], k2b[e], krb[e]);
           }
         }
-        *pa = pack8(v);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e] + r[e], 0.f);
+        const u32x4 pk = pack8(v);
+        *pa = pk;
+        if (nt == 0) {   // with several output tile columns every column's blocks rebuild y; one stores it
+          const int64_t px = a_pix[i];   // 1x1 / stride 1 (host-checked): input pixel = tile row
+          *reinterpret_cast<u32x4*>(a.py + px * a.ldpy + a.pyoff + c) = pk;
+          uint32_t b = 0;
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            b |= (uint32_t)((pk[k] & 0xffffu) != 0u && !(pk[k] & 0x8000u)) << (2 * k);
+            b |= (uint32_t)((pk[k] >> 16) != 0u && !(pk[k] & 0x80000000u)) << (2 * k + 1);
+          }
+          a.pmbits[px * (C >> 3) + (c >> 3)] = (uint8_t)b;
+        }
       }
       __syncthreads();   // every wave's pieces are rewritten before any fragment read
     }
@@ -656,12 +629,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BM * BN <= 
         int r;
         if constexpr (HALO) r = hb[mi] + toff;
         else r = wm * WM + mi * 16 + fr;
-        af[mi] = *reinterpret_cast<const frag_t*>(As + r * 128 + ((ch ^ ((r >> 1) & 7)) << 4));
+        af[mi] = *reinterpret_cast<const frag_t*>(As + r * 128 + ((ch ^ (r & 7)) << 4));
       }
 #pragma unroll
       for (int ni = 0; ni < TN; ++ni) {
         const int r = wn * WN + ni * 16 + fr;
-        bfr[ni] = *reinterpret_cast<const frag_t*>(Bs + r * 128 + ((ch ^ ((r >> 1) & 7)) << 4));
+        bfr[ni] = *reinterpret_cast<const frag_t*>(Bs + r * 128 + ((ch ^ (r & 7)) << 4));
       }
 #pragma unroll
       for (int mi = 0; mi < TM; ++mi)
@@ -699,10 +672,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BM * BN <= 
 // The raw s_barrier (not __syncthreads, whose workgroup fence drains vmcnt to 0 and with it the
 // prefetch) is bracketed by "memory"-clobbering asm statements, so neither the fragment reads nor the
 // DMA issue can be moved across it.
-// VAR (issue placement / priority; A/B in benchmarks/conv_lab): 0 = all DMAs of the next step right
-// after the barrier; 1 = the upper half of the waves issues after its first K-half of MFMAs (the two
-// waves of a SIMD then issue at different times); 2 = A pieces before the first K-half, B pieces
-// before the second; 3 = s_setprio(1) around the MFMA clusters.
+// VAR (issue placement / priority; A/B in benchmarks/conv_lab).  A K-step runs in 4 phases (K-half
+// kk, half of the A fragments); the next step's DMA is issued at: 0 = phase 0 (all of it, right after
+// the barrier); 1 = phase 0 for the lower half of the waves, phase 2 for the upper half (the two waves
+// of a SIMD then issue at different times); 2 = A pieces at phase 0, B pieces at phase 2; 3 = as 0
+// with s_setprio(1) around the MFMA clusters; 4 = A at phase 0 / B at phase 2 for the lower waves,
+// A at 1 / B at 3 for the upper waves.
 // BM need not be a multiple of the staging pass (224 = 2 x 7 fragments): rows past BM stage zeros.
 template <int BM, int BN, int WGM, int WGN, int STAGES, int VAR = 0>
 __global__ __launch_bounds__(64 * WGM * WGN) __attribute__((amdgpu_waves_per_eu(2, 2))) void conv_pipe_kernel(const ConvArgs a) {
@@ -727,7 +702,7 @@ __global__ __launch_bounds__(64 * WGM * WGN) __attribute__((amdgpu_waves_per_eu(
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wid / WGN, wn = wid % WGN;
   const int lrow = tid >> 3;
-  const int jc = (tid & 7) ^ ((tid >> 4) & 7);
+  const int jc = (tid & 7) ^ ((tid >> 3) & 7);
   const char* zp = reinterpret_cast<const char*>(g_zero_page);
 
   const int zph = blockIdx.z;
@@ -820,8 +795,8 @@ __global__ __launch_bounds__(64 * WGM * WGN) __attribute__((amdgpu_waves_per_eu(
     for (int ni = 0; ni < TN; ++ni) acc[mi][ni] = f32x4{0.f, 0.f, 0.f, 0.f};
   const int fr = lane & 15, fg = lane >> 4;
   // per-lane fragment row byte offsets (A rows wm*WM + 16 mi + fr, B rows wn*WN + 16 ni + fr) and
-  // the swizzle term of each: ((r >> 1) & 7) is the same for every mi (16 | row step)
-  const int sw = (fr >> 1) & 7;
+  // the swizzle term of each: (r & 7) is the same for every mi (16 | row step)
+  const int sw = fr & 7;
   const int a_row0 = (wm * WM + fr) * 128, b_row0 = A_BYTES + (wn * WN + fr) * 128;
 
   if (nk > 0) {
@@ -848,32 +823,42 @@ __global__ __launch_bounds__(64 * WGM * WGN) __attribute__((amdgpu_waves_per_eu(
     int wr = rd + STAGES - 1;
     if (wr >= STAGES) wr -= STAGES;
     if (more) advance();
-    const bool late = VAR == 1 && wid >= NW / 2;   // wave-uniform
-    if (more && !late) {
-      if constexpr (VAR == 2) issue_a(wr);
-      else issue(wr);
-    }
     const char* As = smem + rd * SB;
+    const bool up = wid >= NW / 2;   // wave-uniform: waves w and w + NW/2 share a SIMD
+    constexpr int MH = (TM + 1) / 2;
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
-      if (kk == 1 && more) {
-        if constexpr (VAR == 2) issue_b(wr);
-        else if (late) issue(wr);
-        asm volatile("" ::: "memory");
-      }
-      bf16x8 af[TM], bfr[TN];
       const int cb = ((kk * 4 + fg) ^ sw) << 4;
-#pragma unroll
-      for (int mi = 0; mi < TM; ++mi) af[mi] = *reinterpret_cast<const bf16x8*>(As + a_row0 + mi * 16 * 128 + cb);
+      bf16x8 bfr[TN];
 #pragma unroll
       for (int ni = 0; ni < TN; ++ni) bfr[ni] = *reinterpret_cast<const bf16x8*>(As + b_row0 + ni * 16 * 128 + cb);
-      if constexpr (VAR == 3) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-      for (int mi = 0; mi < TM; ++mi)
+      for (int h = 0; h < 2; ++h) {
+        // DMA issue points: phase p = (kk, half of the A fragments)
+        const int p = kk * 2 + h;
+        bool doA, doB;
+        if constexpr (VAR == 1) doA = doB = p == (up ? 2 : 0);
+        else if constexpr (VAR == 2) { doA = p == 0; doB = p == 2; }
+        else if constexpr (VAR == 4) { doA = p == (up ? 1 : 0); doB = p == (up ? 3 : 2); }
+        else doA = doB = p == 0;
+        if (more && (doA || doB)) {
+          if (doA) issue_a(wr);
+          if (doB) issue_b(wr);
+          asm volatile("" ::: "memory");
+        }
+        bf16x8 af[MH];
 #pragma unroll
-        for (int ni = 0; ni < TN; ++ni)
-          acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[mi], bfr[ni], acc[mi][ni], 0, 0, 0);
-      if constexpr (VAR == 3) __builtin_amdgcn_s_setprio(0);
+        for (int q = 0; q < MH; ++q)
+          if (h * MH + q < TM) af[q] = *reinterpret_cast<const bf16x8*>(As + a_row0 + (h * MH + q) * 16 * 128 + cb);
+        if constexpr (VAR == 3) __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int q = 0; q < MH; ++q)
+#pragma unroll
+          for (int ni = 0; ni < TN; ++ni)
+            if (h * MH + q < TM)
+              acc[h * MH + q][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[q], bfr[ni], acc[h * MH + q][ni], 0, 0, 0);
+        if constexpr (VAR == 3) __builtin_amdgcn_s_setprio(0);
+      }
     }
     rd = rd + 1 == STAGES ? 0 : rd + 1;
   }
@@ -887,9 +872,7 @@ using namespace dlmpi;
 
 template <int BM, int BN>
 static void launch_tile(const ConvArgs* a, dim3 grid, hipStream_t s) {
-  if (a->pro == 1) hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, false, 2, 1>), grid, dim3(256), 0, s, *a);
-  else if (a->pro == 2) hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, false, 2, 2>), grid, dim3(256), 0, s, *a);
-  else if (a->pro == 3) hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, false, 2, 3>), grid, dim3(256), 0, s, *a);
+  if (a->pro == 3) hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, false, 2, 3>), grid, dim3(256), 0, s, *a);
   else if (a->C < 64) hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, true, 2>), grid, dim3(256), 0, s, *a);
   else hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, false, 2>), grid, dim3(256), 0, s, *a);
 }
@@ -916,17 +899,17 @@ static hipError_t launch_f32(const ConvArgs* a, int bm, int bn, dim3 grid, hipSt
   if (a->pro != 0) return hipErrorInvalidValue;
   // the regular staging walks whole 32-channel K-steps per tap; anything else stages per 16-B piece
   const bool small = a->C < 32 || a->C % 32 != 0;
-#define DLMPI_F32(BM_, BN_)                                                                                   \
+#define LAUNCH_F32(BM_, BN_)                                                                                   \
   do {                                                                                                       \
     if (small) hipLaunchKernelGGL((conv_igemm_kernel<BM_, BN_, true, 2, 0, float>), grid, dim3(256), 0, s, *a); \
     else hipLaunchKernelGGL((conv_igemm_kernel<BM_, BN_, false, 2, 0, float>), grid, dim3(256), 0, s, *a);     \
   } while (0)
-  if (bm == 128 && bn == 128) DLMPI_F32(128, 128);
-  else if (bm == 128 && bn == 64) DLMPI_F32(128, 64);
-  else if (bm == 64 && bn == 128) DLMPI_F32(64, 128);
-  else if (bm == 64 && bn == 64) DLMPI_F32(64, 64);
+  if (bm == 128 && bn == 128) LAUNCH_F32(128, 128);
+  else if (bm == 128 && bn == 64) LAUNCH_F32(128, 64);
+  else if (bm == 64 && bn == 128) LAUNCH_F32(64, 128);
+  else if (bm == 64 && bn == 64) LAUNCH_F32(64, 64);
   else return hipErrorInvalidValue;
-#undef DLMPI_F32
+#undef LAUNCH_F32
   return hipGetLastError();
 }
 
@@ -934,20 +917,21 @@ static hipError_t launch_f32(const ConvArgs* a, int bm, int bn, dim3 grid, hipSt
 // when the launch does not fit the kernel (channels, prologue, split, fp32).
 static hipError_t launch_pipe(const ConvArgs* a, int bm, int bn, int var, dim3 grid, hipStream_t s) {
   if (a->f32 || a->pro != 0 || a->C % 64 != 0 || a->halo || grid.y != 1) return hipErrorInvalidValue;
-#define DLMPI_PIPE(BM_, BN_, WGM_, WGN_, ST_)                                                                        \
+#define LAUNCH_PIPE(BM_, BN_, WGM_, WGN_, ST_)                                                                        \
   do {                                                                                                              \
     if (var == 1) hipLaunchKernelGGL((conv_pipe_kernel<BM_, BN_, WGM_, WGN_, ST_, 1>), grid, dim3(512), 0, s, *a);  \
     else if (var == 2) hipLaunchKernelGGL((conv_pipe_kernel<BM_, BN_, WGM_, WGN_, ST_, 2>), grid, dim3(512), 0, s, *a); \
     else if (var == 3) hipLaunchKernelGGL((conv_pipe_kernel<BM_, BN_, WGM_, WGN_, ST_, 3>), grid, dim3(512), 0, s, *a); \
+    else if (var == 4) hipLaunchKernelGGL((conv_pipe_kernel<BM_, BN_, WGM_, WGN_, ST_, 4>), grid, dim3(512), 0, s, *a); \
     else hipLaunchKernelGGL((conv_pipe_kernel<BM_, BN_, WGM_, WGN_, ST_, 0>), grid, dim3(512), 0, s, *a);           \
   } while (0)
-  if (bm == 256 && bn == 256) DLMPI_PIPE(256, 256, 2, 4, 2);
-  else if (bm == 224 && bn == 256) DLMPI_PIPE(224, 256, 2, 4, 2);
-  else if (bm == 256 && bn == 128) DLMPI_PIPE(256, 128, 4, 2, 3);
-  else if (bm == 128 && bn == 256) DLMPI_PIPE(128, 256, 2, 4, 3);
-  else if (bm == 512 && bn == 64) DLMPI_PIPE(512, 64, 8, 1, 2);
+  if (bm == 256 && bn == 256) LAUNCH_PIPE(256, 256, 2, 4, 2);
+  else if (bm == 224 && bn == 256) LAUNCH_PIPE(224, 256, 2, 4, 2);
+  else if (bm == 256 && bn == 128) LAUNCH_PIPE(256, 128, 4, 2, 3);
+  else if (bm == 128 && bn == 256) LAUNCH_PIPE(128, 256, 2, 4, 3);
+  else if (bm == 512 && bn == 64) LAUNCH_PIPE(512, 64, 8, 1, 2);
   else return hipErrorInvalidValue;
-#undef DLMPI_PIPE
+#undef LAUNCH_PIPE
   return hipGetLastError();
 }
 
@@ -989,11 +973,9 @@ extern "C" hipError_t dlmpi_conv_igemm_ex(const ConvArgs* a_in, int bm, int bn, 
     else return hipErrorInvalidValue;
     return hipGetLastError();
   }
-  if (a->pro != 0 && (a->C < 64 || a->C % 64 != 0)) return hipErrorInvalidValue;
+  if (a->pro != 0 && (a->pro != 3 || a->C < 64 || a->C % 64 != 0)) return hipErrorInvalidValue;
   if (bm == 256 && bn == 64) {   // 64-channel layers: 4 x 1 waves of 64 x 64
-    if (a->pro == 1) hipLaunchKernelGGL((conv_igemm_kernel<256, 64, false, 4, 1>), grid, dim3(256), 0, s, *a);
-    else if (a->pro == 2) hipLaunchKernelGGL((conv_igemm_kernel<256, 64, false, 4, 2>), grid, dim3(256), 0, s, *a);
-    else if (a->pro == 3) hipLaunchKernelGGL((conv_igemm_kernel<256, 64, false, 4, 3>), grid, dim3(256), 0, s, *a);
+    if (a->pro == 3) hipLaunchKernelGGL((conv_igemm_kernel<256, 64, false, 4, 3>), grid, dim3(256), 0, s, *a);
     else if (a->C < 64) hipLaunchKernelGGL((conv_igemm_kernel<256, 64, true, 4>), grid, dim3(256), 0, s, *a);
     else hipLaunchKernelGGL((conv_igemm_kernel<256, 64, false, 4>), grid, dim3(256), 0, s, *a);
   } else if (bm == 256 && bn == 128) launch_tile<256, 128>(a, grid, s);

@@ -5,10 +5,10 @@
 // staged row-major [64 pixels][cols] into LDS and fed to v_mfma_f32_16x16x32_bf16 through the
 // gfx950 hardware-transposing read ds_read_b64_tr_b16 (cdna_hip_programming.md T10), with the
 // XOR swizzle that makes those reads conflict-free.  The pixel axis is split across workgroups
-// (split-K); every split writes an fp32 slab and the tile's last-arriving split sums the slabs in a
-// fixed order (bit-reproducible, no float atomics) straight into the flat fp32 gradient buffer,
-// undoing the compute-layout channel padding on the way.  (Fallback, e.g. a slab too small inside
-// a hipGraph capture: a [splits][Ko][TC] workspace and two reduction kernels.)
+// (split-K); every split writes its fp32 slice of a [splits][Ko][TC] workspace, and two reduction
+// kernels sum the slices in a fixed order (bit-reproducible, no float atomics) into the flat fp32
+// gradient buffer, undoing the compute-layout channel padding on the way.  (A last-arriver
+// reduction inside this kernel measured slower at every split count, profiles/r3_wgrad_inlaunch_off.)
 //
 // Also used for ConvTranspose2d(k2,s2) weight-grad (roles of X and dY swapped, stride 2) and for
 // Linear weight-grad (1x1 "conv" on a 1x1 image).
@@ -299,72 +299,6 @@ void conv_wgrad_kernel(const WgradArgs a) {
 
   // D[row = ko][col = tc]: lane holds col (lane&15), rows 4*(lane>>4) + r.
   const int fr = lane & 15, fg = lane >> 4;
-  if (a.ws == nullptr) {
-    // ---- in-launch split reduction (cdna_hip_programming.md "In-launch split-K reduction") ----
-    // Every split stores its accumulators (fragment layout) to its slab, publishes with an
-    // agent-scope release + ticket; the tile's last arriver acquires and sums ALL slabs in split
-    // order -- bit-identical whichever block arrives last, and to the two-kernel path.
-    constexpr int NF = TM * TN;
-    const int S = a.splits;
-    if (S > 1) {
-      // slabs are stored WRITE-THROUGH (sc1) so that no agent-scope release is needed: a release
-      // writes back the whole XCD L2's dirty lines, i.e. also the activations the concurrently
-      // running data-gradient chain just wrote (measured: ResNet-50 step 1.6x slower that way)
-      const float* tbase = a.slab + (int64_t)tile * S * NF * 256 * 4;
-      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-          const_cast<float*>(tbase), (short)0, S * NF * 256 * 16, 0x00020000);
-#pragma unroll
-      for (int i = 0; i < NF; ++i)
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[i / TN][i % TN]), rs,
-                                               ((z * NF + i) * 256 + tid) * 16, 0, 16 /* sc1 */);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every storing wave drains its stores
-      __syncthreads();
-      int* flag = reinterpret_cast<int*>(smem);   // the one LDS array (no second __shared__ object)
-      if (tid == 0)
-        flag[0] = __hip_atomic_fetch_add(a.tk + tile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == S - 1;
-      __syncthreads();
-      if (!flag[0]) return;
-      if (tid == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __hip_atomic_store(a.tk + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-      __syncthreads();
-      // every slab (this block's own included) is loaded: no per-element register/load select
-      const f32x4* base = reinterpret_cast<const f32x4*>(a.slab) + (int64_t)tile * S * NF * 256 + tid;
-      const int per = (S + a.groups - 1) / a.groups;
-#pragma unroll
-      for (int i = 0; i < NF; ++i) acc[i / TN][i % TN] = f32x4{0.f, 0.f, 0.f, 0.f};
-      for (int z0 = 0; z0 < S; z0 += per) {
-        const int z1 = min(S, z0 + per);
-        f32x4 sg[NF];
-#pragma unroll
-        for (int i = 0; i < NF; ++i) sg[i] = f32x4{0.f, 0.f, 0.f, 0.f};
-        for (int zz = z0; zz < z1; ++zz) {
-#pragma unroll
-          for (int i = 0; i < NF; ++i) sg[i] += base[((int64_t)zz * NF + i) * 256];
-        }
-#pragma unroll
-        for (int i = 0; i < NF; ++i) acc[i / TN][i % TN] += sg[i];
-      }
-    }
-#pragma unroll
-    for (int mi = 0; mi < TM; ++mi)
-#pragma unroll
-      for (int ni = 0; ni < TN; ++ni) {
-        const int cc = n0 + wn * WN + ni * 16 + fr;
-        if (cc >= a.TC) continue;
-        const int t = (int)fdiv((uint32_t)cc, a.fdC);
-        const int c = cc - t * a.C;
-        if (c >= a.Creal) continue;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int ko = m0 + wm * WM + mi * 16 + fg * 4 + r;
-          if (ko < a.Ko_real) a.out[((int64_t)ko * a.T + t) * a.Creal + c] += 0.f + acc[mi][ni][r];
-        }
-      }
-    return;
-  }
   float* wsz = a.ws + (int64_t)z * a.Ko * a.TC;
 #pragma unroll
   for (int mi = 0; mi < TM; ++mi)
@@ -545,35 +479,35 @@ extern "C" hipError_t dlmpi_conv_wgrad(const WgradArgs* a, int bm, int bn, hipSt
   if (a->pro_a != 0 || a->pro_b != 0) {
     if ((a->pro_a != 0 && a->pro_a != 2) || (a->pro_b != 0 && a->pro_b != 1)) return hipErrorInvalidValue;
     const int m = (a->pro_a ? 2 : 0) | (a->pro_b ? 1 : 0);
-#define DLMPI_WGP(BM_, D_)                                                                             \
+#define LAUNCH_WGP(BM_, D_)                                                                             \
   do {                                                                                                \
     if (m == 2) hipLaunchKernelGGL((conv_wgrad_kernel<BM_, 128, 1, D_, 2, 0>), g, b, 0, s, *a);      \
     else if (m == 1) hipLaunchKernelGGL((conv_wgrad_kernel<BM_, 128, 1, D_, 0, 1>), g, b, 0, s, *a); \
     else hipLaunchKernelGGL((conv_wgrad_kernel<BM_, 128, 1, D_, 2, 1>), g, b, 0, s, *a);             \
   } while (0)
     if (bm == 128) {
-      if (d) DLMPI_WGP(128, true);
-      else DLMPI_WGP(128, false);
+      if (d) LAUNCH_WGP(128, true);
+      else LAUNCH_WGP(128, false);
     } else {
-      if (d) DLMPI_WGP(64, true);
-      else DLMPI_WGP(64, false);
+      if (d) LAUNCH_WGP(64, true);
+      else LAUNCH_WGP(64, false);
     }
-#undef DLMPI_WGP
+#undef LAUNCH_WGP
     return hipGetLastError();
   }
-#define DLMPI_WG(BM_, ST_)                                                                  \
+#define LAUNCH_WG(BM_, ST_)                                                                  \
   do {                                                                                     \
     if (d) hipLaunchKernelGGL((conv_wgrad_kernel<BM_, 128, ST_, true>), g, b, 0, s, *a);   \
     else hipLaunchKernelGGL((conv_wgrad_kernel<BM_, 128, ST_, false>), g, b, 0, s, *a);    \
   } while (0)
   if (bm == 128) {
-    if (stages == 1) DLMPI_WG(128, 1);
-    else DLMPI_WG(128, 2);
+    if (stages == 1) LAUNCH_WG(128, 1);
+    else LAUNCH_WG(128, 2);
   } else {
-    if (stages == 1) DLMPI_WG(64, 1);
-    else DLMPI_WG(64, 2);
+    if (stages == 1) LAUNCH_WG(64, 1);
+    else LAUNCH_WG(64, 2);
   }
-#undef DLMPI_WG
+#undef LAUNCH_WG
   return hipGetLastError();
 }
 

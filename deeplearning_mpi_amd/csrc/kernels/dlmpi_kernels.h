@@ -69,8 +69,6 @@ struct Stream1x1Args {
   const float* bias;
   float* stats;
   int G, ntiles, mtiles;
-  const float* pscale;             // operand prologue: x := relu(x * pscale[c] + pshift[c]) (or null)
-  const float* pshift;
 };
 
 // Streaming 1x1 / stride-1 data gradient with the fused BN-backward epilogue (conv1x1_dgrad_stream.hip)
@@ -148,22 +146,17 @@ struct ConvArgs {
   float* sk_slab;                  // [tile][slice][TM*TN][threads] f32x4 fragment slabs
   int* sk_tk;                      // [tile] self-resetting arrival tickets
   int cstep, tstep;                // K-iteration: c += cstep, t += tstep per 64-wide step
-  // Operand prologue (regular channel counts, single-stage kernels): every staged A piece of an
-  // in-image tap is rewritten in LDS before the MFMAs (out-of-image taps stay zero):
-  //   pro 1: A := bf16(relu(A * pscale[c] + pshift[c]))   (a deferred forward BN-apply + ReLU)
-  //   pro 2: A := bf16(pcoef[c] * A + pcoef[C + c] * Z + pcoef[2C + c])   (a deferred BN-backward
-  //          apply: A = the masked output gradient dy, Z = the BN input, same pixel grid / C)
+  // Operand prologue (single-stage kernel, regular channel counts), pro 3 (1x1 / stride 1
+  // consumers): every staged A piece is rewritten in LDS before the MFMAs as A := bf16(relu(A *
+  // pscale[c] + pshift[c] + R)), R = Z (the residual, staged like A) or Z * prscale[c] + prshift[c]
+  // (a BN-output residual); output tile column 0 also stores it to py and its ReLU mask bits to
+  // pmbits [pixels][C/8] (the producer block's BN-apply, fused); pro 0: none
   int pro;
   int f32;                         // 1: activations / weights are fp32 (the fp32 precision path)
   const float* pscale;
   const float* pshift;
-  const float* pcoef;
   const void* pz;
   int ldpz, pzoff;
-  //   pro 3 (1x1 / stride 1 consumers with ONE output tile column): A := bf16(relu(A * pscale[c] +
-  //          pshift[c] + R)), R = Z (the residual, staged like pro 2's Z) or Z * prscale[c] +
-  //          prshift[c] (a BN-output residual); the transformed tile is also stored to py and its
-  //          ReLU mask bits to pmbits [pixels][C/8] (the producer block's BN-apply, fused)
   const float* prscale;
   const float* prshift;
   uint16_t* py;
@@ -191,14 +184,7 @@ struct WgradArgs {
   int mtiles, ntiles, splits;
   int direct;                      // 1: 1x1 / stride 1 / pad 0 on the same grid (no gather decode)
   FastDiv fdPQ, fdQ, fdC, fdS;
-  float* ws;                       // [splits][Ko][TC] fp32 partials (two-kernel path)
-  // in-launch reduction (ws == nullptr): per (tile, split) fp32 fragment slabs + per-tile tickets;
-  // the tile's last-arriving split sums the slabs in split order (in `groups` consecutive groups,
-  // the association of the two-kernel path) and accumulates out[ko][t][c] (c < Creal, ko < Ko_real)
-  float* slab;
-  int* tk;
-  float* out;
-  int T, Creal, Ko_real, groups;
+  float* ws;                       // [splits][Ko][TC] fp32 partials (reduced by dlmpi_wgrad_reduce)
   // Operand prologues (conv_igemm's pro modes, applied in LDS to in-range pieces only):
   //   dy side (A): pro_a 2 -> dz = pcoef[k] * dy + pcoef[Ko + k] * Z + pcoef[2 Ko + k]
   //   x side  (B): pro_b 1 -> x := relu(x * pscale[c] + pshift[c])
@@ -367,12 +353,17 @@ hipError_t dlmpi_image_batch(const uint8_t* data, const int64_t* labels, const i
 
 // fault injection: keep stream s busy for `ms` milliseconds (bounded; tests of the watchdog)
 hipError_t dlmpi_delay(double ms, hipStream_t s);
+// comm-load rehearsal: `channels` workgroups (lds_bytes of LDS each) copy copy_bytes of the bucket
+// into scratch and hold their CUs for `us` microseconds (fault.hip)
+hipError_t dlmpi_comm_load(const void* bucket, int64_t bytes, void* scratch, int64_t copy_bytes, int channels,
+                           int lds_bytes, double us, hipStream_t s);
 void dlmpi_set_conv_stream(int mode);
 void dlmpi_set_dgrad_stream(int mode);
 int dlmpi_stream1x1_plan(int64_t M, int C, int Kout, int* bm, int* bn, int* G);
 hipError_t dlmpi_conv1x1_stream(const dlmpi::Stream1x1Args* a, int bm, int bn, hipStream_t s);
-int dlmpi_stream1x1_pro_ok(int ntiles);
 int dlmpi_dgrad_stream_plan(int64_t M, int K, int Kout, int mask_mode, int z2, int has_res, int* bm, int* bn, int* G);
+void dlmpi_set_dgs_blocks(int n);
+int dlmpi_dgs_blocks();
 hipError_t dlmpi_conv1x1_dgrad_stream(const dlmpi::DgradStreamArgs* a, int bm, int bn, int mask_mode, hipStream_t s);
 
 // utilities (util.hip): fp32 fill, int64 add, indexed gather dst[i] (+)= src[idx[i]] (idx < 0: zero;

@@ -98,78 +98,53 @@ def record_on(stream, *objs):
             record_on(stream, *o)
 
 
-# DLMPI_STREAM_HOLD=0: cross-stream buffer lifetimes through record_stream instead (A/B; grad_side)
-_STREAM_HOLD = os.environ.get("DLMPI_STREAM_HOLD", "1") != "0"
+# Cross-stream buffer lifetimes are held by the issuing step (grad_side) rather than record_stream.
+_STREAM_HOLD = True
 
-# DLMPI_OUTER_DGRAD=0: one-output-channel 1x1 data gradients through the GEMM kernel (A/B)
-_OUTER_DGRAD = os.environ.get("DLMPI_OUTER_DGRAD", "1") != "0"
+# One-output-channel 1x1 data gradients as a streaming outer product (bn.hip outer_dgrad_bn_kernel).
+_OUTER_DGRAD = True
 
-# Deferred BatchNorm elementwise passes (ops.act.Deferred), off by default:
-# DLMPI_DEFER_BN_FWD=1: never store a BN-apply + ReLU output without residual; the consumer
-#                       convolution rebuilds it in its operand prologue (forward GEMM and weight
-#                       gradient);
-# DLMPI_DEFER_BN_BWD=1: never store dz = BN-backward(dy); the unit's own weight-gradient and
-#                       data-gradient GEMMs rebuild it in their operand prologues.
-# Bit-identical results either way, but measured slower (ResNet-50 bs 256 9,924 vs 11,655 img/s,
-# UNet 512 266 vs 421, profiles/r2_defer_bn_rejected): a consumer re-transforms every element once
-# per tap and per output tile, with an extra LDS round trip and barrier in every K-step, which
-# costs more than the single elementwise pass it removes.
-DEFER_BN_FWD = os.environ.get("DLMPI_DEFER_BN_FWD", "0") != "0"
-DEFER_BN_BWD = os.environ.get("DLMPI_DEFER_BN_BWD", "0") != "0"
-DEFER_BN_WGRAD = os.environ.get("DLMPI_DEFER_BN_WGRAD", "1") != "0"
+# BN-backward apply of a unit whose input needs no gradient (the ResNet stem, UNet's first conv) is
+# rebuilt in its weight-gradient GEMM's operand prologue instead of stored (ops.act.Deferred).
+# (Deferring the other BatchNorm elementwise passes -- forward BN-apply rebuilt by every consumer
+# conv, every BN-backward apply rebuilt by its data gradient -- was bit-identical but measured
+# slower, ResNet-50 9,924 vs 11,655 img/s, profiles/r2_defer_bn_rejected, and was removed.)
+DEFER_BN_WGRAD = True
 
 # Dual data gradient of 1x1 stride-1 convolutions behind a training BN (ConvUnit.dual): the forward
 # stores the BN input z in the right half of a [rows][2K] buffer whose left half later receives the
 # BN's output gradient dy, so the data gradient reduces over [dy | z] with weights {W*k1, W*k2} and
 # bias W.k3 -- dx = dz.W without dz -- and the BN-backward apply pass (dz = k1 dy + k2 z + k3, needed
 # only by the weight gradient now) moves to the side stream, off the data-gradient critical path.
-# DLMPI_DUAL_DGRAD=0: off; DLMPI_DUAL_MIN_ROWS: only layers with at least this many output pixels
-# (N*P*Q; memory-bound 1x1 GEMMs -- the doubled reduction costs MFMA time on the small deep layers).
-DUAL_DGRAD = os.environ.get("DLMPI_DUAL_DGRAD", "1") != "0"
-# Since the streaming 1x1 data gradient (conv1x1_dgrad_stream.hip) the layer-2 shapes (200,704 rows
-# at bs 256) gain nothing from the doubled reduction: 401,408 keeps it for ResNet-50 layer 1 and the
-# ResNet-152 (bs 128) layer 1 (ResNet-50 12,948-12,968 vs 12,882-12,901 img/s with layer 2 included,
-# profiles/r3_cifar_ab2).
-DUAL_MIN_ROWS = int(os.environ.get("DLMPI_DUAL_MIN_ROWS", str(2 * 256 * 28 * 28)))
+# Only for layers with at least DUAL_MIN_ROWS output pixels (N*P*Q): since the streaming 1x1 data
+# gradient (conv1x1_dgrad_stream.hip) the layer-2 shapes (200,704 rows at bs 256) gain nothing from
+# the doubled reduction: 401,408 keeps it for ResNet-50 layer 1 and the ResNet-152 (bs 128) layer 1
+# (ResNet-50 12,948-12,968 vs 12,882-12,901 img/s with layer 2 included, profiles/r3_cifar_ab2).
+DUAL_DGRAD = True
+DUAL_MIN_ROWS = 2 * 256 * 28 * 28
 # The dual path's weight gradient rebuilds dz in its operand prologue (PA 2) from the same [dy | z]
-# buffer; DLMPI_DUAL_WGRAD_PRO=0: an apply pass materialises dz on the side stream first (measured
-# slower: that pass competes with the main stream for HBM, profiles/r2_dual_dgrad)
-DUAL_WGRAD_PRO = os.environ.get("DLMPI_DUAL_WGRAD_PRO", "1") != "0"
+# buffer (an apply pass materialising dz on the side stream first measured slower: it competes with
+# the main stream for HBM, profiles/r2_dual_dgrad).
+DUAL_WGRAD_PRO = True
 
-# DLMPI_CHUNK_FWD=1: run each forward BN-apply in two image chunks interleaved with its consumer's
-# GEMM on the main + side streams (PendingApply).  Off by default: measured slower (ResNet-50 bs 256
-# 11,501 vs 11,894 img/s, ResNet-152 3,963 vs 4,390; profiles/r2_chunk_fwd_rejected) -- the bn_apply
-# time with nothing beside it drops 2.1 -> 1.5 ms, but every join costs the main stream a ~40 us
-# wait for the later side-stream half before the BN finalize (1.8 ms of main-stream gaps per step)
-CHUNK_FWD = os.environ.get("DLMPI_CHUNK_FWD", "0") != "0"
-
-# DLMPI_FUSE_APPLY=0: run every residual block's BN-apply (+ residual + ReLU) as its own pass.  By
-# default a block output whose first consumer is a 1x1 / stride-1 convolution (the next bottleneck's
-# conv1, up to FUSE_APPLY_MAX_K output channels: ResNet-50 layer1 / layer2) is left
-# pending (PendingApply) and computed by that convolution's operand prologue, which also stores it
-# and its ReLU mask bits (backend conv_fwd_bn_apply): no element is transformed twice, and the
-# apply's output is written once and never re-read by the consumer.
-FUSE_APPLY = os.environ.get("DLMPI_FUSE_APPLY", "1") != "0"
-# ... for consumers of up to this many output channels.  With several output tile columns the blocks
-# of every column rebuild y in their prologue (only the first column's store it): correct, but
-# measured slower at 256 (layer-3 conv1: ResNet-50 12,730-12,746 vs 12,889-12,916 img/s, ResNet-152
-# 4,539-4,541 vs 4,657-4,663; profiles/r3_fuse_apply_2col_rejected) -- the per-K-step prologue of a
-# 16-K-step GEMM, repeated per column, costs more than the apply pass it removes.
-FUSE_APPLY_MAX_K = int(os.environ.get("DLMPI_FUSE_APPLY_MAXK", "128"))
-
-# DLMPI_STREAM_PRO_FWD=1: where the bottleneck's conv3 runs on the streaming 1x1 kernel with few output
-# columns (ResNet-50 layer1 / layer2), its input -- the second BN-apply + ReLU (bn2) -- is rebuilt in
-# that kernel's operand prologue and never stored; conv3's weight gradient rebuilds it too (wgrad
-# prologue B), the BN backward recomputes its ReLU mask from z.  Bit-identical to the stored schedule
-# (tests/test_stream_pro_gpu.py) but neutral end to end (ResNet-50 13,039 / 13,066 vs 13,019 / 13,091
-# img/s, profiles/r3_stream_pro: the apply passes go, the prologue and its extra barrier cost the
-# streaming kernel about as much), so off by default.
-STREAM_PRO = os.environ.get("DLMPI_STREAM_PRO_FWD", "0") != "0"
+# A residual block's BN-apply (+ residual + ReLU) whose first consumer is a 1x1 / stride-1
+# convolution of up to FUSE_APPLY_MAX_K output channels (the next bottleneck's conv1 in ResNet-50
+# layer1 / layer2) is left pending (PendingApply) and computed by that convolution's operand
+# prologue, which also stores it and its ReLU mask bits (backend conv_fwd_bn_apply): no element is
+# transformed twice, and the apply's output is written once and never re-read by the consumer.
+# With several output tile columns the blocks of every column rebuild y in their prologue: correct
+# but measured slower at 256 (ResNet-50 12,730-12,746 vs 12,889-12,916 img/s, profiles/
+# r3_fuse_apply_2col_rejected).  (Running the apply in two image chunks beside the consumer's GEMM on
+# two streams measured slower too -- a cross-stream join before every BN finalize,
+# profiles/r2_chunk_fwd_rejected -- and was removed, as was rebuilding bn2 in the streaming conv3's
+# prologue: bit-identical but neutral, profiles/r3_stream_pro.)
+FUSE_APPLY = True
+FUSE_APPLY_MAX_K = 128
 
 # The step's last weight gradient (a unit with ``wgrad_main``: the ResNet stem, whose input needs no
 # gradient) runs on the main stream -- idle by then -- instead of queueing behind the side stream's
-# last weight gradients (profiles/r3_tail).  DLMPI_WGRAD_TAIL_MAIN=0: on the side stream like the rest.
-WGRAD_TAIL_MAIN = os.environ.get("DLMPI_WGRAD_TAIL_MAIN", "1") != "0"
+# last weight gradients (profiles/r3_tail).
+WGRAD_TAIL_MAIN = True
 
 
 def img_rows(a, n0: int, n1: int):
@@ -185,12 +160,8 @@ def img_rows(a, n0: int, n1: int):
 
 class PendingApply:
     """A training BN-apply (+ residual) (+ ReLU) (+ mask bits) whose output ``y`` is allocated but
-    not yet computed.  The consuming convolution (``ConvUnit.fwd``) runs it image-chunk by
-    image-chunk interleaved with its own GEMM on two streams -- chunk 0's apply and GEMM on the
-    main stream, chunk 1's apply and GEMM on the side stream, which starts after chunk 0's apply --
-    so the memory-bound apply of one half runs beside the MFMA-bound GEMM of the other instead of
-    alone on the forward's critical path (profiles/r2_profile_v4: 2.1 ms of bn_apply with nothing
-    beside it per ResNet-50 step).  Any other consumer calls ``resolve`` (one whole apply)."""
+    not yet computed: a 1x1 consumer convolution computes (and stores) it in its operand prologue
+    (FUSE_APPLY, ``ConvUnit.fwd``); any other consumer calls ``resolve`` (one whole apply)."""
 
     __slots__ = ("y", "z", "scale", "shift", "res", "relu", "mbits", "done")
 
@@ -203,12 +174,6 @@ class PendingApply:
     W = property(lambda self: self.y.W)
     C = property(lambda self: self.y.C)
     device = property(lambda self: self.y.device)
-
-    def apply_images(self, be, n0, n1):
-        hw = self.y.H * self.y.W
-        mb = self.mbits[n0 * hw:n1 * hw] if self.mbits is not None else None
-        be.bn_apply(img_rows(self.z, n0, n1), self.scale, self.shift, img_rows(self.res, n0, n1), self.relu,
-                    img_rows(self.y, n0, n1), mbits=mb)
 
     def resolve(self, be) -> Act:
         if not self.done:
@@ -320,56 +285,13 @@ class ConvUnit:
         self.arena.backend.gather_(self._bias_pad, self.bias.data, self._bias_idx)   # one launch of ours
         return self._bias_pad
 
-    def _chunkable(self, be, x) -> bool:
-        """Can this unit consume a PendingApply input chunk-wise (ConvUnit._conv_chunked)?"""
-        return (CHUNK_FWD and isinstance(x, PendingApply) and self.bn is not None and x.N >= 2 and x.N % 2 == 0
-                and (getattr(be, "side_stream", None) is not None or getattr(be, "chunk_serial", False)))
-
-    def _conv_chunked(self, be, xp: PendingApply, wf, z: Act):
-        """The producer's BN-apply and this GEMM (with its BN-statistics epilogue) over two image
-        halves: apply(0) -> GEMM(0) on the current stream; the side stream starts after apply(0)
-        and runs apply(1) -> GEMM(1) beside GEMM(0); the current stream joins it before the
-        finalize.  Each half writes its own rows of the statistics partials, so the finalize sees
-        the same column sums as one whole GEMM (bit-identical outputs).  Returns (stats, rows)."""
-        N, h = xp.N, xp.N // 2
-        halves = ((0, h), (h, N))
-        mts = [be.conv_mtiles(n1 - n0, xp.H, xp.W, self.Cp, self.Kp, self.R, self.S, self.stride, self.pad)
-               for n0, n1 in halves]
-        stats = torch.empty(sum(mts), 2, self.Kp, dtype=be.dt, device=z.device)
-        bias = self._bias_vec()
-        side = getattr(be, "side_stream", None)
-        main = torch.cuda.current_stream() if side is not None else None
-        xp.apply_images(be, 0, h)
-        if side is not None:
-            side.wait_stream(main)
-        o = 0   # rows written so far (conv_mtiles is an upper bound; the launch returns the count)
-        for i, ((n0, n1), mt) in enumerate(zip(halves, mts)):
-            with torch.cuda.stream(side) if (i == 1 and side is not None) else contextlib.nullcontext():
-                if i == 1:
-                    xp.apply_images(be, n0, n1)
-                rows = be.conv_fwd(img_rows(xp.y, n0, n1), wf, self.Kp, self.R, self.S, self.stride, self.pad,
-                                   img_rows(z, n0, n1), bias=bias, stats=stats[o:o + mt])
-            o += mt if rows is None else rows
-        if side is not None:
-            main.wait_stream(side)
-        xp.done = True
-        return stats, o
-
-    def takes_deferred_stream(self, be, N, H, W) -> bool:
-        """This 1x1 / stride-1 conv (the bottleneck conv3) runs on the streaming kernel with its input
-        a deferred BN-apply + ReLU rebuilt in the kernel's operand prologue (STREAM_PRO): the producer
-        skips its apply pass and never stores its output."""
-        return (STREAM_PRO and self.R == 1 and self.S == 1 and self.stride == 1 and self.pad == 0
-                and hasattr(be, "stream_pro_ok") and be.stream_pro_ok(N * H * W, self.Cp, self.Kp))
-
     def can_fuse_apply(self, be, x, train: bool, save=True) -> bool:
         """True if ``fwd`` computes the pending BN-apply ``x`` inside its GEMM's operand prologue
         (FUSE_APPLY): a 1x1 / stride-1 conv of <= FUSE_APPLY_MAX_K outputs behind a residual BN + ReLU."""
         return (FUSE_APPLY and train and save and isinstance(x, PendingApply) and not x.done
                 and self.bn is not None and self.R == 1 and self.S == 1 and self.stride == 1 and self.pad == 0
                 and self.Kp <= FUSE_APPLY_MAX_K and x.relu and x.res is not None and x.mbits is not None
-                and x.C == self.Cp and hasattr(be, "conv_fwd_bn_apply") and not getattr(be, "f32", False)
-                and not self._chunkable(be, x))
+                and x.C == self.Cp and hasattr(be, "conv_fwd_bn_apply") and not getattr(be, "f32", False))
 
     def fwd(self, be, x, train: bool, res: Act = None, out: Act = None, save=True, defer_apply=False,
             before_res=None, lazy=False):
@@ -381,10 +303,9 @@ class ConvUnit:
         convolution, "bn" (BN without ReLU) Deferred.bn(z, scale, shift) for a residual consumer
         (the ResNet downsample branch, applied inside the block's last BN-apply).  Either way the BN
         output is never materialised.  lazy (training BN, not deferred): return a PendingApply instead
-        of running the BN-apply -- for a consumer that runs it chunk-wise beside its own GEMM."""
-        chunked = train and self._chunkable(be, x)
-        fuse_apply = not chunked and self.can_fuse_apply(be, x, train, save)
-        if isinstance(x, PendingApply) and not chunked and not fuse_apply:
+        of running the BN-apply -- for a consumer that computes it in its operand prologue."""
+        fuse_apply = self.can_fuse_apply(be, x, train, save)
+        if isinstance(x, PendingApply) and not fuse_apply:
             x = x.resolve(be)
         assert x.C == self.Cp, (x, self.Cp)
         P, Q = self.out_hw(x.H, x.W)
@@ -419,12 +340,7 @@ class ConvUnit:
             fin = (N * P * Q, bn.weight.data if bn.affine else None, bn.bias.data if bn.affine else None,
                    bn.running_mean if bn.track_running_stats else None,
                    bn.running_var if bn.track_running_stats else None, mom, bn.eps, scale, shift, mean, invstd)
-            if chunked:
-                stats, mt = self._conv_chunked(be, x, wf, z)
-                x = x.y
-                self.arena.wait_buffers()   # DDP's asynchronous buffer broadcast must land first
-                be.bn_finalize(stats, mt, self.Kp, *fin)
-            elif fuse_apply:   # the producer's BN-apply runs (and is stored) inside this GEMM
+            if fuse_apply:   # the producer's BN-apply runs (and is stored) inside this GEMM
                 mt = be.conv_mtiles(N, x.H, x.W, x.C, self.Kp, 1, 1, 1, 0, pro=3)
                 stats = torch.empty(mt, 2, self.Kp, dtype=be.dt, device=dev)
                 self.arena.wait_buffers()
@@ -455,7 +371,7 @@ class ConvUnit:
             if before_res is not None and res is not None:
                 before_res()
             ctx = (x, z, y, mean, invstd, scale, shift, res is not None, mbits) if save else None
-            if lazy and (CHUNK_FWD or FUSE_APPLY) and out is None:
+            if lazy and FUSE_APPLY and out is None:
                 return PendingApply(y, z, scale, shift, res, self.relu, mbits), ctx
             be.bn_apply(z, scale, shift, res, self.relu, y, mbits=mbits)
             return y, ctx
@@ -527,10 +443,9 @@ class ConvUnit:
             gam = bn.weight.data if bn.affine else None
             dgam = ar.grad_flat(bn.weight) if bn.affine else None
             dbet = ar.grad_flat(bn.bias) if bn.affine else None
-            # deferred: always with DLMPI_DEFER_BN_BWD; by default also when the weight gradient is
-            # dz's only consumer (need_dx False: the ResNet stem, the UNet input conv) -- then the
+            # deferred when the weight gradient is dz's only consumer (need_dx False: the ResNet stem, the UNet input conv) -- then the
             # BN-backward apply pass (read dy, z; write dz) is replaced by the wgrad reading dy and z
-            defer = DEFER_BN_BWD or (not need_dx and DEFER_BN_WGRAD and getattr(be, "prologue", False))
+            defer = not need_dx and DEFER_BN_WGRAD and getattr(be, "prologue", False)
             if pre is not None and mask is None and dyr_out is None and defer:
                 # finalize only: dz = k1 dy + k2 z + k3 is rebuilt inside the wgrad / dgrad GEMMs
                 dz = be.bn_bwd_deferred(dy, z, mean, invstd, gam, dgam, dbet, pre=pre, k2=k2)
@@ -788,8 +703,8 @@ class EngineModule(nn.Module):
         self._arena = None
         self._be = None
         self._anchor = torch.zeros(0, requires_grad=True)
-        # BN-backward reductions fused into the producing dgrad epilogue (DLMPI_FUSE_BN_BWD=0: off)
-        self.fuse_bn_bwd = os.environ.get("DLMPI_FUSE_BN_BWD", "1") != "0"
+        # BN-backward reductions fused into the producing dgrad epilogue (False: separate passes)
+        self.fuse_bn_bwd = True
         self.precision = "bf16"    # "fp32": fp32 activations / weights in the same kernels (set before first use)
 
     def engine_setup(self, device=None):

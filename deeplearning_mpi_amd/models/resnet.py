@@ -12,14 +12,12 @@ path of the same parameters (stock PyTorch baseline and test oracle).
 """
 from __future__ import annotations
 
-import os
 
 import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
 from ..ops.act import Act, padc
-from . import engine as _engine
 from .engine import BwdFuse, ConvUnit, EngineModule, S2DConvUnit, record_on, resolve
 
 
@@ -88,20 +86,12 @@ class Bottleneck(nn.Module):
         return u, ud
 
 
-# DLMPI_LATE_JOIN=0: join the downsample branch stream before the last unit's GEMM (forward) /
-# before conv1's BN backward (backward) instead of right before the residual is read (A/B knob)
-_LATE_JOIN = os.environ.get("DLMPI_LATE_JOIN", "1") != "0"
-# DLMPI_DS_FUSE=0: store the downsample branch's BN output (a pass of its own) instead of applying
-# it inside the block's last BN-apply (A/B knob; backends without the fused residual ignore it)
-_DS_FUSE = os.environ.get("DLMPI_DS_FUSE", "1") != "0"
-
-# DLMPI_DS_AFTER_CONV1=1: a downsample block whose input is a pending residual BN-apply that conv1
-# can fuse (engine.FUSE_APPLY: ResNet-50 layer2.0) lets conv1 compute and store the input and starts
-# the branch (1x1 stride-2 conv + BN) after it, beside conv2, instead of a standalone apply pass
-# before both.  Off by default: measured slower (profiles/r3_ds_after_conv1_rejected: ResNet-50
-# 12,812 / 12,961 vs 12,941 / 13,045 img/s -- the branch no longer overlaps conv1, and the fused
-# 256 -> 128 conv1 at 56^2 costs about what the apply pass did).
-_DS_AFTER_CONV1 = os.environ.get("DLMPI_DS_AFTER_CONV1", "0") != "0"
+# The downsample branch stream is joined right before the residual is first read (the last unit's
+# BN-apply in the forward, conv1's data gradient in the backward), and its BN output is applied inside
+# the block's last BN-apply (Deferred.bn) instead of a pass of its own (profiles/r2_ds_fuse).
+# (Starting the branch after a fused conv1 instead measured slower: profiles/r3_ds_after_conv1_rejected.)
+_LATE_JOIN = True
+_DS_FUSE = True
 
 
 class _BlockExec:
@@ -110,25 +100,18 @@ class _BlockExec:
     def __init__(self, units, ds):
         self.u, self.ud = units, ds
 
-    def fwd(self, be, x: Act, train, save, defer=False):
+    def fwd(self, be, x: Act, train, save):
         """The downsample branch (1x1 conv + BN) depends only on the block input: with a branch
-        stream it runs beside conv1 -> conv2 and joins before the residual add of conv3's BN.
-        defer: the inner BN + ReLU outputs (bn1, bn2 of a bottleneck) are never stored -- the next
-        convolution rebuilds them in its operand prologue (ops.act.Deferred)."""
+        stream it runs beside conv1 -> conv2 and joins before the residual add of conv3's BN."""
         ctxs = []
-        lazy = train and save and not defer   # BN-applies run chunk-wise inside their consumer (PendingApply)
-        # the block input is still a pending BN-apply that conv1 can compute in its operand prologue
-        # (engine.FUSE_APPLY): with a downsample branch, the branch starts after conv1 has stored it
-        # instead of a standalone apply pass before both (_DS_AFTER_CONV1)
-        ds_late = (self.ud is not None and _DS_AFTER_CONV1 and self.u[0].can_fuse_apply(be, x, train, save))
-        if self.ud is not None and not ds_late:   # the branch reads the whole block input
+        lazy = train and save   # the block output's BN-apply may run inside its consumer (PendingApply)
+        if self.ud is not None:   # the branch reads the whole block input
             x = resolve(be, x)
         # the downsample BN output is read once, as the residual of the last unit's BN-apply: applied
         # there on the fly (Deferred.bn), which removes its own apply pass (read z_ds + write idn)
         ds_defer = "bn" if (_DS_FUSE and train and save) else False
         br = getattr(be, "branch_stream", None) if self.ud is not None else None
         main = torch.cuda.current_stream() if br is not None else None
-        xin = x
 
         def branch_fwd(xb):
             if br is not None:
@@ -139,19 +122,12 @@ class _BlockExec:
                 return out
             return self.ud.fwd(be, xb, train, save=save, defer_apply=ds_defer)
 
-        if br is not None and not ds_late:
+        if br is not None:
             idn, cd = branch_fwd(x)
         h = x
-        for k, u in enumerate(self.u[:-1]):
-            # the unit before a streaming conv3 that rebuilds its BN-apply (engine.STREAM_PRO)
-            d = defer or (train and save and k == len(self.u) - 2 and len(self.u) == 3
-                          and self.u[-1].takes_deferred_stream(be, h.N, *u.out_hw(h.H, h.W)))
-            h, c = u.fwd(be, h, train, save=save, defer_apply="act" if d else False, lazy=lazy)
+        for u in self.u[:-1]:
+            h, c = u.fwd(be, h, train, save=save, lazy=lazy)
             ctxs.append(c)
-            if k == 0 and ds_late:
-                xin = resolve(be, x)   # computed and stored by conv1's prologue
-                if br is not None:
-                    idn, cd = branch_fwd(xin)
         join = None
         if br is not None:
             def join():   # the residual is first read by the last unit's BN-apply, after its GEMM
@@ -161,7 +137,7 @@ class _BlockExec:
                 join()
                 join = None
         elif self.ud is not None:
-            idn, cd = self.ud.fwd(be, xin if ds_late else x, train, save=save, defer_apply=ds_defer)
+            idn, cd = self.ud.fwd(be, x, train, save=save, defer_apply=ds_defer)
         else:   # identity: the block input, complete once conv1 has consumed it
             idn, cd = resolve(be, x), None
         y, c = self.u[-1].fwd(be, h, train, res=idn, save=save, before_res=join, lazy=lazy)
@@ -307,7 +283,7 @@ class ResNet(EngineModule):
 
     def _build_units(self, ar):
         self.cin_pad = padc(self.in_channels)
-        if self.in_channels <= S2DConvUnit.CS and os.environ.get("DLMPI_STEM_S2D", "1") != "0":
+        if self.in_channels <= S2DConvUnit.CS:
             # 7x7/s2 stem as a 4x4/s1 conv over a 2x2 space-to-depth image (engine.py:S2DConvUnit)
             self.u_stem = S2DConvUnit(ar, self.conv1, self.bn1, relu=True)
         else:
@@ -332,9 +308,8 @@ class ResNet(EngineModule):
         idx = be.maxpool_fwd(h, 3, 2, 1, p, bn=(cs[5], cs[6]) if defer else None)
         st_blocks = []
         a = p
-        dfr = train and save and self.fuse_bn_bwd and _engine.DEFER_BN_FWD
         for blk in self.blocks:
-            a, st = blk.fwd(be, a, train, save, defer=dfr)
+            a, st = blk.fwd(be, a, train, save)
             st_blocks.append(st)
         a = resolve(be, a)
         pooled = Act.empty(N, 1, 1, a.C, be.act_dtype, x.device)

@@ -20,7 +20,6 @@ import torch
 import torch.nn as nn
 
 from ..ops.act import Act, padc
-from . import engine as _engine
 from .engine import ConvTUnit, ConvUnit, EngineModule
 
 
@@ -145,15 +144,13 @@ class UNet(EngineModule):
         dt, dev = be.act_dtype, x.device
         a = be.nchw_to_nhwc(x, self.cin_pad)
         cats, ctx_enc, idxs, skips = [], [], [], []
-        # the first BN + ReLU of every DoubleConv is rebuilt in the second conv's operand prologue
-        dfr = "act" if (train and save and self.fuse_bn_bwd and _engine.DEFER_BN_FWD) else False
         h, w = H, W
         for k in range(4):
             ccat = self.up_ch[k] + self.skip_ch[k]
             cat = Act.empty(N, h, w, ccat, dt, dev)
             cats.append(cat)
             ua, ub = self.enc[k]
-            t, ca = ua.fwd(be, a, train, save=save, defer_apply=dfr)
+            t, ca = ua.fwd(be, a, train, save=save)
             skip = cat.slice(self.up_ch[k], self.skip_ch[k])
             _, cb = ub.fwd(be, t, train, out=skip, save=save)
             down = Act.empty(N, h // 2, w // 2, self.skip_ch[k], dt, dev)
@@ -164,7 +161,7 @@ class UNet(EngineModule):
             a = down
             h, w = h // 2, w // 2
         ua, ub = self.bott
-        t, cba = ua.fwd(be, a, train, save=save, defer_apply=dfr)
+        t, cba = ua.fwd(be, a, train, save=save)
         a, cbb = ub.fwd(be, t, train, save=save)
         ctx_dec = [None] * 4
         for k in range(3, -1, -1):
@@ -176,7 +173,7 @@ class UNet(EngineModule):
                 be.upsample_fwd(a, up)
             below = a
             ua, ub = self.dec[k]
-            t, ca = ua.fwd(be, cat, train, save=save, defer_apply=dfr)
+            t, ca = ua.fwd(be, cat, train, save=save)
             a, cb = ub.fwd(be, t, train, save=save)
             ctx_dec[k] = (below, ca, cb)
         K = self.out_classes

@@ -122,7 +122,9 @@ class NativeBackend:
         self._branch = s
 
     # ---------------- conv family ----------------
-    prologue = True   # the GEMM kernels consume ops.act.Deferred operands directly (bf16)
+    # the weight-gradient GEMM consumes ops.act.Deferred operands directly in its operand prologues
+    # (bf16); the forward / data-gradient GEMMs take them materialized (one elementwise pass)
+    prologue = True
 
     @staticmethod
     def _pro(op):
@@ -147,33 +149,28 @@ class NativeBackend:
         return out
 
     def conv_mtiles(self, N, H, W, C, K, R, S, stride, pad, pro=0):
-        """BN-statistics rows the forward conv will write; pro: the operand prologue mode (0 none,
-        1 deferred BN-apply, 2 deferred BN-backward apply, 3 the producer's pending residual apply;
-        True = 1) -- the streaming 1x1 kernel takes modes 0 and 1 only."""
-        return self.C.conv2d_fwd_mtiles_pro(N, H, W, C, K, R, S, stride, pad, 0, int(pro), int(self.f32))
-
-    def stream_pro_ok(self, M, C, K) -> bool:
-        """The streaming 1x1 forward kernel takes a deferred BN-apply + ReLU operand of this shape
-        (conv1x1_stream.hip PRO: few output columns)."""
-        return (not self.f32) and bool(self.C.conv_stream_pro_ok(int(M), int(C), int(K)))
+        """BN-statistics rows the forward conv will write; pro: 3 = the consumer GEMM of a pending
+        residual BN-apply (conv_fwd_bn_apply), else 0."""
+        return self.C.conv2d_fwd_mtiles_pro(N, H, W, C, K, R, S, stride, pad, 0, 3 if pro == 3 else 0,
+                                            int(self.f32))
 
     def conv_fwd(self, x, w, K, R, S, stride, pad, y: Act, bias=None, res: Act = None, scale=None,
                  shift=None, relu=False, stats=None, kvalid=0):
         """Returns the number of BN-statistics rows written (stats given)."""
-        x, pm, k0, k1, zb, zld, zoff = self._pro(x)
-        return self.C.conv2d_fwd_pro(x.buf, x.N, x.H, x.W, x.C, x.ld, x.off, w, K, R, S, stride, pad, y.buf, y.ld,
-                                     y.off, bias, res.buf if res is not None else None,
-                                     res.ld if res is not None else 0, res.off if res is not None else 0, scale, shift,
-                                     bool(relu), stats, 0, int(kvalid), 0, pm, k0, k1, zb, zld, zoff)
+        x = self.materialize(x)
+        return self.C.conv2d_fwd(x.buf, x.N, x.H, x.W, x.C, x.ld, x.off, w, K, R, S, stride, pad, y.buf, y.ld,
+                                 y.off, bias, res.buf if res is not None else None,
+                                 res.ld if res is not None else 0, res.off if res is not None else 0, scale, shift,
+                                 bool(relu), stats, 0, int(kvalid), 0)
 
     def conv_fwd_bn(self, x, w, K, R, S, stride, pad, z: Act, bias, stats, count, gamma, beta, rm, rv, momentum,
                     eps, scale, shift, save_mean, save_invstd):
         """conv_fwd into z with the BN-statistics epilogue AND the training-BN finalize of those
-        statistics (scale / shift / mean / invstd / running stats) -- in the same launch when the
-        in-launch finalize applies (csrc/kernels/bnfin.h), else followed by the finalize launch."""
-        x, pm, k0, k1, zb, zld, zoff = self._pro(x)
+        statistics (scale / shift / mean / invstd / running stats): the conv, then the column-reduce +
+        finalize launch."""
+        x = self.materialize(x)
         self.C.conv2d_fwd_bn(x.buf, x.N, x.H, x.W, x.C, x.ld, x.off, w, K, R, S, stride, pad, z.buf, z.ld, z.off,
-                             bias, stats, pm, k0, k1, zb, zld, zoff, float(count), gamma, beta, rm, rv,
+                             bias, stats, 0, None, None, None, 0, 0, float(count), gamma, beta, rm, rv,
                              float(momentum), float(eps), scale, shift, save_mean, save_invstd)
 
     def conv_fwd_bn_apply(self, xp, w, K, z: Act, bias, stats, count, gamma, beta, rm, rv, momentum, eps, scale,
@@ -211,10 +208,10 @@ class NativeBackend:
         def t(a):
             return (a.buf, a.ld, a.off) if a is not None else (None, 0, 0)
 
-        dy, pm, k0, k1, zb, zld, zoff = self._pro(dy)
+        dy = self.materialize(dy)
         return self.C.conv2d_dgrad_pro(dy.buf, dy.N, dy.H, dy.W, dy.C, dy.ld, dy.off, wT, C, R, S, stride, pad, dx.H,
                                        dx.W, dx.buf, dx.ld, dx.off, *t(res), *t(m), *t(z), *t(z2), sc, sh, mb,
-                                       bool(colsum and fuse is None), pm, k0, k1, zb, zld, zoff, bias)
+                                       bool(colsum and fuse is None), 0, None, None, None, 0, 0, bias)
 
     def dual_weights(self, wT, C, K, coef):
         """[dy | z] weights of the dual 1x1 data gradient (engine.ConvUnit, dual path): w2 [C][2K] =

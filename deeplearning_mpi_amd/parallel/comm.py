@@ -106,10 +106,16 @@ class SingleCommunicator(Communicator):
 class RcclCommunicator(Communicator):
     backend = "rccl"
 
-    def __init__(self, info, device, native_comm, control_group=None):
+    def __init__(self, info, device, native_comm, control_group=None, budget=None):
         super().__init__(info, device)
         self.c = native_comm
         self.control = control_group
+        # the CUs this communicator's channels take are withheld from the persistent streaming
+        # data-gradient grid for as long as it exists (rccl_channel_budget)
+        self.budget = budget if budget is not None else rccl_channel_budget()
+        from .._ext import native
+
+        native().set_dgs_blocks(int(self.budget["dgrad_stream_blocks"]))
 
     def allreduce(self, t, op="sum"):
         self.c.allreduce(t, op, False)
@@ -155,6 +161,9 @@ class RcclCommunicator(Communicator):
     def destroy(self):
         self.c.destroy()
         self.control = None
+        from .._ext import native
+
+        native().set_dgs_blocks(0)
 
 
 def _make_torch_bucket_comm(group, world_size):
@@ -358,7 +367,7 @@ def _init(backend: str, timeout_s: float) -> Communicator:
         return TorchCommunicator(info, device)
     # RCCL data plane: no torch process group at all, only the 128-byte unique id has to reach
     # every rank before ncclCommInitRank
-    rccl_channel_budget()
+    budget = rccl_channel_budget()
     from .._ext import native
 
     C = native()
@@ -371,7 +380,7 @@ def _init(backend: str, timeout_s: float) -> Communicator:
     else:
         uid, store = uid_via_store(info, C.RcclComm.unique_id, timeout_s)
     nc = C.RcclComm(uid, info.rank, info.world_size, device.index)
-    return RcclCommunicator(info, device, nc, control_group=store)
+    return RcclCommunicator(info, device, nc, control_group=store, budget=budget)
 
 
 DEFAULT_RCCL_CHANNELS = 16
@@ -381,25 +390,30 @@ def rccl_channel_budget() -> dict:
     """How many CUs RCCL's kernels may take from the compute streams.
 
     Each RCCL channel is one workgroup (one CU) for the duration of a collective.  The gradient
-    all-reduces run on the comm stream while the backward convolutions fill the other 240+ CUs, so
-    the channel count is a CU budget: ``DLMPI_RCCL_CHANNELS`` (default 16 = 1/16 of the 256 CUs;
-    0 = leave RCCL's own choice) is exported as ``NCCL_MAX_NCHANNELS`` before the communicator is
-    created (RCCL reads it at ``ncclCommInitRank``).  An explicit ``NCCL_MAX_NCHANNELS`` /
-    ``NCCL_MIN_NCHANNELS`` in the environment wins.  Sizing: ResNet-50's 102 MB of fp32 gradients
-    move 2*(7/8)*102 MB per rank; at 16 channels (>= ~10 GB/s each over the 7 xGMI links) that is
-    about 1 ms, far inside the ~14 ms backward pass it overlaps.  Returns the effective settings
-    (bench.py reports them)."""
+    all-reduces run on the comm stream while the backward convolutions fill the other CUs, so the
+    channel count is a CU budget: ``DLMPI_RCCL_CHANNELS`` (default 16 = 1/16 of the 256 CUs; 0 =
+    leave RCCL its own choice) is exported as ``NCCL_MAX_NCHANNELS`` before the communicator is
+    created (RCCL reads it at ``ncclCommInitRank``).  An explicit ``NCCL_MAX_NCHANNELS`` in the
+    environment wins.  The default is chosen by the one-GPU comm-load rehearsal
+    (``bench.py --rehearse``, profiles/r4_commload): the backward slowdown of a channel-sized
+    workgroup load per all-reduce, measured for 8/16/32 channels.
+
+    The persistent streaming data-gradient kernel (conv1x1_dgrad_stream.hip) splits its work
+    statically over one block per CU of 100-160 KB of LDS: a block that cannot start because an
+    RCCL workgroup holds LDS on its CU would hold the whole kernel -- and the backward -- until the
+    collective ends.  Its grid is therefore sized to the CUs the channels leave free
+    (``dgrad_stream_blocks``; with RCCL's own, unknown, channel count: 256 - 32, RCCL's per-peer
+    channel ceiling on this node size).  The communicator applies it natively for its lifetime
+    (``RcclCommunicator``), so a later communicator with another budget takes effect.  Returns the
+    effective settings (bench.py reports them)."""
     want = int(os.environ.get("DLMPI_RCCL_CHANNELS", str(DEFAULT_RCCL_CHANNELS)) or 0)
     if want > 0 and "NCCL_MAX_NCHANNELS" not in os.environ:
         os.environ["NCCL_MAX_NCHANNELS"] = str(want)
-    # The persistent streaming data-gradient kernel (conv1x1_dgrad_stream.hip) splits its work
-    # statically over one block per CU of 100-160 KB of LDS: a block that cannot start because an
-    # RCCL workgroup holds LDS on its CU would hold the whole kernel -- and the backward -- until the
-    # collective ends.  With a communicator, size its grid to the CUs the channels leave free.
-    ch = int(os.environ.get("NCCL_MAX_NCHANNELS") or DEFAULT_RCCL_CHANNELS)
-    if "DLMPI_DGS_BLOCKS" not in os.environ:
-        os.environ["DLMPI_DGS_BLOCKS"] = str(max(64, 256 - ch))
-    return {k: os.environ.get(k) for k in ("NCCL_MAX_NCHANNELS", "NCCL_MIN_NCHANNELS", "DLMPI_DGS_BLOCKS")}
+    env = os.environ.get("NCCL_MAX_NCHANNELS")
+    ch = int(env) if env else 32
+    blocks = int(os.environ.get("DLMPI_DGS_BLOCKS") or max(64, 256 - ch))
+    return {"NCCL_MAX_NCHANNELS": env, "NCCL_MIN_NCHANNELS": os.environ.get("NCCL_MIN_NCHANNELS"),
+            "dgrad_stream_blocks": blocks}
 
 
 _UID_ROUND = 0   # init_distributed -> destroy -> init_distributed in one process: a fresh key each time

@@ -9,10 +9,12 @@ checkpoint and ``--resume`` continues from it exactly (tests/test_resume_cpu.py)
 LOCAL_RANK, which collides across nodes on a shared filesystem).
 Loading uses ``torch.load(..., weights_only=True)`` and accepts either key style.
 
-Crash consistency: the sidecar records the SHA-256 of the weights file it belongs to and is put in
-place BEFORE the weights file, so a crash between the two renames leaves a sidecar whose hash does
-not match the weights on disk; ``load_checkpoint`` then ignores it (warning) instead of silently
-mixing new weights with an old optimizer state / epoch.
+Crash consistency: the sidecar records the SHA-256 of the weights file it belongs to.  A save keeps
+the previous sidecar as ``<path>.state.prev`` (it belongs to the weights still on disk), then puts
+the new sidecar and finally the new weights in place.  A crash anywhere in between leaves weights
+whose own sidecar is on disk under one of the two names, and ``load_checkpoint`` takes the one whose
+hash matches -- never new weights with an old optimizer state / epoch, and never an already trained
+checkpoint restarted from epoch 0.
 """
 from __future__ import annotations
 
@@ -52,7 +54,9 @@ def save_checkpoint(model, path, optimizer=None, extra=None, rank=None):
             state["optimizer"] = optimizer.state_dict()
         state["weights_sha256"] = _sha256(tmp)
         torch.save(state, path + ".state.tmp")
-        os.replace(path + ".state.tmp", path + ".state")   # sidecar first (see module docstring)
+        if os.path.exists(path + ".state"):   # the resume state of the weights still on disk
+            os.replace(path + ".state", path + ".state.prev")
+        os.replace(path + ".state.tmp", path + ".state")   # sidecar before weights (module docstring)
     os.replace(tmp, path)
     return path
 
@@ -77,13 +81,18 @@ def load_checkpoint(model, path, map_location=None, optimizer=None, strict=True)
     with torch.no_grad():
         model.load_state_dict(sd, strict=strict)
     meta = {}
-    if os.path.exists(path + ".state"):
-        meta = torch.load(path + ".state", map_location=map_location, weights_only=True)
-        want = meta.get("weights_sha256")
-        if want is not None and want != _sha256(path):
-            warnings.warn(f"{path}.state belongs to a different weights file (interrupted save?): "
-                          "ignoring the resume state, starting from epoch 0 with fresh optimizer state")
-            meta = {}
+    cands = [c for c in (path + ".state", path + ".state.prev") if os.path.exists(c)]
+    if cands:
+        digest = _sha256(path)
+        for c in cands:
+            m = torch.load(c, map_location=map_location, weights_only=True)
+            want = m.get("weights_sha256")
+            if want is None or want == digest:
+                meta = m
+                break
+        else:
+            warnings.warn(f"no resume state of {path} matches its weights (interrupted save?): "
+                          "starting from epoch 0 with fresh optimizer state")
         if optimizer is not None and "optimizer" in meta:
             optimizer.load_state_dict(meta["optimizer"])
     from .arena import arena_of

@@ -25,7 +25,8 @@ Contract of :class:`CapturedStep`:
 * a failed capture never kills the run: the error is reported, the graph dropped, and the step
   runs eagerly from then on, in the same process (no re-exec).  With a communicator (``comm``)
   the ranks agree first -- if ANY rank failed to capture, every rank runs eagerly -- so the
-  collectives stay matched across ranks.
+  collectives stay matched across ranks.  A rank whose capture failed replaces its stuck streams
+  (the communicator's included) BEFORE that agreement collective, which runs on the comm stream.
 
 Why the capture runs on a helper thread, on a stream of its own: HIP (ROCm 7.2) does not close an
 invalidated capture -- ``hipStreamEndCapture`` fails and the stream, every stream forked into the
@@ -95,6 +96,10 @@ class CapturedStep:
             torch.cuda.current_stream().wait_stream(s)
             return out
         g, err = self._capture()
+        if err is not None:
+            # before anything else touches a stream: the communicator's stream may be one the failed
+            # capture forked and left in capture mode, and the agreement below runs on it
+            self._reset_streams()
         if not self._agree(err is None):
             self._fall_back(err)
             return self.step_fn()
@@ -144,11 +149,9 @@ class CapturedStep:
         c.allreduce(t, "min")
         return bool(t.item() > 0.5)
 
-    def _fall_back(self, err):
-        self.capture_error = err if err is not None else RuntimeError("hipGraph capture failed on another rank")
-        print(f"[dlmpi] hipGraph capture failed ({self.capture_error!r}); running the step eagerly from now on",
-              file=sys.stderr, flush=True)
-        # streams the failed capture had forked stay in capture mode: replace them (module docstring)
+    def _reset_streams(self):
+        """Replace every stream a failed capture left in capture mode (module docstring): the engine's
+        auxiliary streams, the communicator's stream, our capture stream; clear the sticky HIP error."""
         from ..ops.backend import replace_poisoned_aux_streams
 
         replace_poisoned_aux_streams()
@@ -160,6 +163,13 @@ class CapturedStep:
 
         if has_native():
             native().clear_hip_error()
+
+    def _fall_back(self, err):
+        self.capture_error = err if err is not None else RuntimeError("hipGraph capture failed on another rank")
+        print(f"[dlmpi] hipGraph capture failed ({self.capture_error!r}); running the step eagerly from now on",
+              file=sys.stderr, flush=True)
+        if err is None:   # this rank captured fine (its graph is dropped): nothing is stuck here
+            self._stream = None
         torch.cuda.synchronize()
         self.graph = None
         self.enabled = False

@@ -178,60 +178,6 @@ def test_flat_gradient_layout_follows_backward_ready_order(name):
         assert bseq == sorted(bseq)
 
 
-@pytest.mark.parametrize("arch", ["resnet50", "resnet18", "unet", "unet_bilinear"])
-def test_deferred_bn_passes_match_torch(arch, monkeypatch):
-    """The schedules with deferred BatchNorm elementwise passes (ops.act.Deferred: forward BN-apply
-    rebuilt by the next conv, BN-backward apply rebuilt by the unit's wgrad / dgrad) are exact
-    against fp64 autograd too (the reference backend materializes the deferred operands)."""
-    import deeplearning_mpi_amd.models.engine as E
-
-    monkeypatch.setattr(E, "DEFER_BN_FWD", True)
-    monkeypatch.setattr(E, "DEFER_BN_BWD", True)
-    g = torch.Generator().manual_seed(4)
-    if arch.startswith("unet"):
-        mode = "bilinear" if "bilinear" in arch else "conv_transpose"
-        x = torch.randn(2, 3, 32, 32, generator=g)
-        y = (torch.rand(2, 32, 32, generator=g) > 0.5).float()
-        skip = lambda n: n.endswith("bias") and "double_conv.double_conv" in n  # noqa: E731 (grad == 0)
-        _run_pair(lambda: UNet(out_classes=1, up_sample_mode=mode), x, y,
-                  lambda o, t: bce_with_logits(o.squeeze(1), t),
-                  lambda o, t: F.binary_cross_entropy_with_logits(o.squeeze(1), t), skip=skip)
-    else:
-        x = torch.randn(8, 3, 64, 64, generator=g)
-        y = torch.randint(10, (8,), generator=g)
-        make = resnet50 if arch == "resnet50" else resnet18
-        _run_pair(lambda: make(num_classes=10), x, y, cross_entropy, F.cross_entropy)
-
-
-@pytest.mark.parametrize("arch", ["resnet18", "resnet50"])
-def test_chunked_forward_bn_apply_matches_torch(arch, monkeypatch):
-    """Forward BN-applies run in two image chunks inside their consumer convolution
-    (engine.PendingApply; serial here, main + side stream on the GPU): same fp64 results as
-    autograd, and the chunked path is really taken for every chained BN-apply."""
-    from deeplearning_mpi_amd.models import engine
-    from deeplearning_mpi_amd.models.resnet import resnet18 as r18
-    from deeplearning_mpi_amd.ops.backend import RefBackend
-
-    monkeypatch.setattr(RefBackend, "chunk_serial", True, raising=False)
-    monkeypatch.setattr(engine, "CHUNK_FWD", True)
-    calls = []
-    orig = engine.ConvUnit._conv_chunked
-
-    def counted(self, *a, **k):
-        calls.append(self)
-        return orig(self, *a, **k)
-
-    monkeypatch.setattr(engine.ConvUnit, "_conv_chunked", counted)
-    g = torch.Generator().manual_seed(3)
-    x = torch.randn(4, 3, 64, 64, generator=g)
-    y = torch.randint(10, (4,), generator=g)
-    make = (lambda: r18(num_classes=10)) if arch == "resnet18" else (lambda: resnet50(num_classes=10))
-    _run_pair(make, x, y, cross_entropy, F.cross_entropy)
-    # every conv whose input is a BN-apply output, except conv1 of blocks with a downsample branch
-    # (the branch reads the whole input): resnet18 2*8 - 3 - 1(stem pool input) = 12, resnet50 3*16 - 4
-    assert len(calls) == (12 if arch == "resnet18" else 44)
-
-
 @pytest.mark.parametrize("fused", [True, False])
 def test_dual_dgrad_matches_torch(monkeypatch, fused):
     """1x1 data gradients over [dy | z] with weights {W*k1, W*k2} and bias W.k3 (engine.DUAL_DGRAD,

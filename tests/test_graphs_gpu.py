@@ -160,3 +160,85 @@ def test_failed_capture_falls_back_to_eager():
     assert torch.equal(l1, l2), (l1, l2)
     for a, b in zip(p1, p2):
         assert torch.equal(a, b)
+
+
+def test_failed_capture_agreement_runs_on_reset_comm_stream():
+    """with world_size > 1 the rank agreement after a failed capture is a collective on the
+    communicator's stream -- a stream the failed capture had forked and left in capture mode.  The
+    fake communicator below reports world_size 2 and runs both a step-internal collective and the
+    agreement on such a stream; the fallback must replace that stream BEFORE the agreement, then run
+    every step eagerly, bit-identical to an all-eager run."""
+    from deeplearning_mpi_amd._ext import native
+
+    C = native()
+
+    class FakeRccl:   # the `c` of a communicator: its raw HIP stream + reset_stream_if_capturing
+        def __init__(self):
+            self.stream = torch.cuda.ExternalStream(C.create_stream())
+            self.was_capturing = None
+
+        def reset_stream_if_capturing(self):
+            self.was_capturing = bool(C.stream_capturing(self.stream.cuda_stream))
+            if self.was_capturing:
+                self.stream = torch.cuda.ExternalStream(C.create_stream())
+
+    class FakeComm:
+        world_size = 2
+
+        def __init__(self):
+            self.c = FakeRccl()
+            self.device = torch.device(DEV, torch.cuda.current_device())
+            self.agreements = 0
+
+        def _on_comm_stream(self, t):
+            s = self.c.stream
+            s.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(s):
+                t.mul_(1.0)
+            torch.cuda.current_stream().wait_stream(s)
+
+        def collective(self, t):   # a collective of the step (forked into the capture)
+            self._on_comm_stream(t)
+
+        def allreduce(self, t, op):   # the agreement: the simulated peer agrees with this rank
+            assert op == "min"
+            self.agreements += 1
+            self._on_comm_stream(t)
+
+    batches = _cifar_batches(5, 29)
+
+    def run(inject):
+        torch.manual_seed(0)
+        m = resnet18(num_classes=10).to(DEV)
+        m.engine_setup(DEV)
+        opt = _sgd(m)
+        comm = FakeComm()
+        x, y = batches[0][0].clone(), batches[0][1].clone()
+
+        def step():
+            opt.zero_grad()
+            loss = cross_entropy(m(x), y)
+            comm.collective(loss)
+            if inject and torch.cuda.is_current_stream_capturing():
+                float(loss)   # refused while capturing: the capture fails after the comm stream joined it
+            loss.backward()
+            opt.step()
+            return loss
+
+        cs = CapturedStep(step, warmup=2, inputs=(x, y), enabled=inject, comm=comm)
+        losses = []
+        for bx, by in batches:
+            cs.set_inputs(bx, by)
+            losses.append(cs().clone())
+        torch.cuda.synchronize()
+        if inject:
+            assert cs.graph is None and not cs.enabled and cs.capture_error is not None
+            assert comm.agreements == 1
+            assert comm.c.was_capturing, "the failed capture did not leave the comm stream capturing"
+        return torch.stack(losses), [p.detach().clone() for p in m.parameters()]
+
+    l1, p1 = run(False)
+    l2, p2 = run(True)
+    assert torch.equal(l1, l2), (l1, l2)
+    for a, b in zip(p1, p2):
+        assert torch.equal(a, b)

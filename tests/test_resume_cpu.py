@@ -101,3 +101,41 @@ def test_two_epochs_plus_resume_equals_three_epochs(tmp_path, case):
     assert oa and oa.keys() == ob.keys()
     for k in oa:
         assert torch.equal(oa[k], ob[k]), k
+
+
+def test_checkpoint_sidecar_survives_interrupted_save(tmp_path):
+    """a crash between the sidecar and the weights rename must leave a loadable resume
+    state for the weights still on disk (the previous sidecar, kept as <path>.state.prev), and the
+    finished save must load its own."""
+    import os
+
+    import torch
+
+    from deeplearning_mpi_amd.utils.checkpoint import load_checkpoint, save_checkpoint
+
+    m = torch.nn.Linear(4, 3)
+    p = str(tmp_path / "ck.pth")
+    save_checkpoint(m, p, extra={"next_epoch": 1}, rank=0)
+    with torch.no_grad():
+        m.weight.add_(1.0)
+    # an interrupted second save: sidecar of epoch 2 in place, weights of epoch 1 still on disk
+    orig = os.replace
+
+    def crash_on_weights(src, dst):
+        if dst == p:
+            raise KeyboardInterrupt("simulated crash")
+        return orig(src, dst)
+
+    os.replace = crash_on_weights
+    try:
+        save_checkpoint(m, p, extra={"next_epoch": 2}, rank=0)
+    except KeyboardInterrupt:
+        pass
+    finally:
+        os.replace = orig
+    m2 = torch.nn.Linear(4, 3)
+    meta = load_checkpoint(m2, p, map_location="cpu")
+    assert meta.get("next_epoch") == 1   # the weights on disk are epoch 1's, and so is the state
+    save_checkpoint(m, p, extra={"next_epoch": 2}, rank=0)
+    assert load_checkpoint(m2, p, map_location="cpu").get("next_epoch") == 2
+    assert torch.equal(m2.weight, m.weight)
