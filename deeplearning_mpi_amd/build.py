@@ -105,7 +105,7 @@ def build_kernels(jobs=8, force=False, verbose=False):
 
     def one(so):
         s, o = so
-        extra = os.environ.get("DLMPI_HIPCC_FLAGS", "").split()   # experiments, e.g. -DDLMPI_SETPRIO=1
+        extra = os.environ.get("DLMPI_HIPCC_FLAGS", "").split()   # experiments: extra hipcc flags
         _run([hipcc, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-munsafe-fp-atomics", *extra,
               "-c", s, "-o", o], verbose)
         return o

@@ -206,9 +206,8 @@ RcclComm::RcclComm(const std::string& uid, int rank, int size, int device) {
   hip_check(hipSetDevice(device), "hipSetDevice");
   // Default priority: a high-priority stream inside a hipGraph capture was seen to segfault in
   // capture_end on this ROCm build (profiles/r1_hipri_rejected), and the comm stream joins every
-  // captured DDP step.  DLMPI_COMM_HIPRI=1 opts back in.
-  const char* hp = std::getenv("DLMPI_COMM_HIPRI");
-  const bool hipri = hp != nullptr && std::atoi(hp) != 0;
+  // captured DDP step.
+  constexpr bool hipri = false;
   hipStream_t raw = nullptr;
   if (hipri) {
     int lo = 0, hi = 0;

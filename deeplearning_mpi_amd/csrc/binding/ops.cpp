@@ -87,30 +87,21 @@ static void set_kstep(ConvArgs& a, int C) {
 // benchmarks/conv_bench.py) and loses on the short / memory-bound ResNet GEMMs; 64-row tiles for
 // small grids.  `red` = GEMM reduction length (R*S*C).
 static int bm256_min_tiles() {
-  static int v = [] {
-    const char* e = getenv("DLMPI_CONV_BM256_MIN_TILES");
-    return e ? atoi(e) : 256;
-  }();
+  static int v = 256;
   return v;
 }
 
-// DLMPI_CONV_BM256_MIN_RED_1X1: shortest 1x1 reduction (red == cin) that takes the 256-row tile
+// Shortest 1x1 reduction (red == cin) that takes the 256-row tile
 // (default 1024: the 14^2 1024->256 forward and 256<-1024 data gradient, 128x128 -> 256x128 tiles
 // halve the B-operand re-reads, -14 % each; ResNet-50 +0.8 %, profiles/r3_bm256red); other
 // reductions from 2304 as before
 static int bm256_min_red_1x1() {
-  static int v = [] {
-    const char* e = getenv("DLMPI_CONV_BM256_MIN_RED_1X1");
-    return e ? atoi(e) : 1024;
-  }();
+  static int v = 1024;
   return v;
 }
 
 static int bm_override() {   // experiments: force the M tile (64 | 128 | 256)
-  static int v = [] {
-    const char* e = getenv("DLMPI_CONV_BM");
-    return e ? atoi(e) : 0;
-  }();
+  static int v = 0;
   return v;
 }
 
@@ -130,10 +121,7 @@ static void pick_tiles(int64_t M, int Kout, int64_t red, int cin, int& bm, int& 
   }
   const int64_t nt = (Kout + bn - 1) / bn;
   const int64_t tiles = ((M + 127) / 128) * nt;
-  static const int n64 = [] {
-    const char* e = getenv("DLMPI_CONV_BM256_N64");
-    return e ? atoi(e) : 1;
-  }();
+  static const int n64 = 1;
   // 64-channel outputs: 256 x 64 tiles (4 x 1 waves of 64 x 64).  Measured (conv_bench): wins for
   // the small-channel stems (-13 % ResNet 7x7, -10 % UNet first conv) and the 4M-row UNet level-1
   // 3x3s (-4 %), loses 3-8 % on the 0.8M-row ResNet layer1 GEMMs -> only there.
@@ -165,13 +153,10 @@ static int pipe_select(int f32, int pro, int cin, int64_t M, int Kout, int64_t r
 }
 
 // ---- 2-D halo tiles for 3x3 / stride-1 / pad-1 convolutions (conv_igemm.hip HALO) ----------------
-// DLMPI_CONV_HALO=0: these convolutions through the im2col gather path too.
+// set_conv_halo(0) (tests): these convolutions through the im2col gather path too.
 static int g_halo_override = -1;   // dlmpi_ext set_conv_halo (tests)
 static bool halo_on() {
-  static const int v = [] {
-    const char* e = getenv("DLMPI_CONV_HALO");
-    return e ? atoi(e) : 1;
-  }();
+  static const int v = 1;
   return (g_halo_override >= 0 ? g_halo_override : v) != 0;
 }
 // Tile th x tw (th * tw <= 128, (th + 2) * (tw + 2) <= 192) covering a P x Q grid with the fewest
@@ -242,7 +227,7 @@ static int g_autotune_override = -1;
 static bool conv_autotune_on() {
   static const int v = [] {
     const char* e = getenv("DLMPI_CONV_AUTOTUNE");
-    return e ? atoi(e) : 0;
+    return e ? atoi(e) : 0;   // 2: also log every plan to stderr
   }();
   return (g_autotune_override >= 0 ? g_autotune_override : v) != 0;
 }
@@ -343,7 +328,7 @@ static bool conv_plan(ConvArgs& a, int pass, int& bm, int& bn) {
     hipEventDestroy(e0);
     hipEventDestroy(e1);
     a.stats = real_stats;
-    if (getenv("DLMPI_CONV_AUTOTUNE_LOG"))
+    if (getenv("DLMPI_CONV_AUTOTUNE") && atoi(getenv("DLMPI_CONV_AUTOTUNE")) == 2)
       fprintf(stderr, "[dlmpi autotune] pass %d %s -> %dx%d split %d (%.1f us; static %dx%d)\n", pass, key.c_str(),
               best.bm, best.bn, best.splitk_req, best_ms / 3 * 1000, bm, bn);
     it = g_conv_plans.emplace(key, best).first;
@@ -388,10 +373,7 @@ static void fill_epilogue(ConvArgs& a, at::Tensor& y, int ldy, int yoff, const c
   a.relu = relu ? 1 : 0;
   a.stats = optr<float>(stats);
   a.nstat = 2;
-  static const int nt = [] {
-    const char* e = getenv("DLMPI_NT_STORE");
-    return e ? atoi(e) : 0;
-  }();
+  static const int nt = 0;
   a.nt_store = nt;
 }
 
@@ -921,7 +903,7 @@ void convT2x2_fwd(const at::Tensor& x, int N, int H, int W, int Cin, int ldx, in
 // dy is over the P x Q output grid of a conv (R x S, stride, pad) applied to x (H x W).
 // Operand prologues: pro_a 2 -> the dy operand is dz = pcoef[0] dy + pcoef[1] Z + pcoef[2] (a deferred
 // BN-backward apply, Z = the BN input); pro_b 1 -> the x operand is relu(x * pscale + pshift).
-static int g_wgrad3_override = -1;   // dlmpi_ext set_wgrad3 (tests); -1: DLMPI_WGRAD3 decides
+static int g_wgrad3_override = -1;   // dlmpi_ext set_wgrad3 (tests); -1: on
 static int g_wgrad3_ran = 0;         // 1 if the last weight gradient ran the 3x3 spatial-tile kernel
 
 void conv2d_wgrad_pro(const at::Tensor& dy, int lddy, int dyoff, int Ko, const at::Tensor& x, int N, int H, int W,
@@ -953,11 +935,7 @@ void conv2d_wgrad_pro(const at::Tensor& dy, int lddy, int dyoff, int Ko, const a
   }
   // 3x3 / stride 1 / pad 1 without operand prologues (UNet DoubleConv, ResNet conv2): the
   // spatial-tile kernel (conv_wgrad3.hip) -- X staged once per 8 x 8 pixel block for all 9 taps.
-  // DLMPI_WGRAD3=0: the general gather kernel for these too.
-  static const int w3 = [] {
-    const char* e = getenv("DLMPI_WGRAD3");
-    return e ? atoi(e) : 1;
-  }();
+  static const int w3 = 1;
   int kt = 0, ct = 0;
   if ((g_wgrad3_override >= 0 ? g_wgrad3_override : w3) && !a.f32 && pro_a == 0 && pro_b == 0 && R == 3 && S == 3 &&
       stride == 1 && pad == 1 && P == H && Q == W && dlmpi_wgrad3_plan(Ko, C, &kt, &ct)) {
@@ -976,13 +954,9 @@ void conv2d_wgrad_pro(const at::Tensor& dy, int lddy, int dyoff, int Ko, const a
     // so nothing of the data-gradient chain on the main stream can share a CU with it).  Large
     // gradients (UNet, >= 64 G MAC) fill the chip once; the ResNet-size ones (~30 G MAC) leave ~100
     // CUs to the main stream (measured, profiles/r3_wgrad3: ResNet-50 12,233 img/s at 256 blocks vs
-    // 12,348 at 160; UNet-512 470 vs 466).  DLMPI_WGRAD3_BLOCKS overrides.
-    static const int target_env = [] {
-      const char* e = getenv("DLMPI_WGRAD3_BLOCKS");
-      return e ? std::max(8, atoi(e)) : 0;
-    }();
+    // 12,348 at 160; UNet-512 470 vs 466).
     const double macs = (double)N * H * W * Ko * 9.0 * C;
-    const int target = target_env ? target_env : (macs >= 64e9 ? 256 : 160);
+    const int target = macs >= 64e9 ? 256 : 160;
     const int kc = b.mtiles * b.ntiles;
     int splits = std::max(1, std::min(b.ntiles_pix, target / kc));
     b.tiles_per_split = ceil_div(b.ntiles_pix, splits);
@@ -1014,23 +988,17 @@ void conv2d_wgrad_pro(const at::Tensor& dy, int lddy, int dyoff, int Ko, const a
   // Ko <= 64 gather-form (3x3 / strided / stem) weight gradients: 64 x 256 tiles (1 x 4 waves of
   // 64 x 64) -- each dy row staged once per 256 columns, fewer LDS reads per MFMA.  The tile holds
   // ~200 VGPRs (2 blocks per CU), so its split count is floored to fit the grid in one round
-  // (profiles/r2_wgrad_wide).  DLMPI_WGRAD_WIDE: 0 off, 1 gather-form only (default), 2 also 1x1.
-  static const int wide = [] {
-    const char* e = getenv("DLMPI_WGRAD_WIDE");
-    return e ? atoi(e) : 1;
-  }();
+  // (profiles/r2_wgrad_wide).  Gather-form only (1x1s measured no gain).
+  static const int wide = 1;
   const bool w256 = !a.f32 && Ko <= 64 && pro_b == 0 && a.TC >= 256 && (wide == 2 || (wide == 1 && !a.direct));
   const int bn = a.f32 ? 64 : (w256 ? 256 : 128);
   a.ntiles = ceil_div(a.TC, bn);
   const int tiles = a.mtiles * a.ntiles;
   // split the pixel reduction so the grid covers the chip ~2 blocks deep, but keep each split at
   // least 8 K-steps (512 pixels) so the fp32 slab traffic stays small next to the MFMA work.
-  // DLMPI_WGRAD_BLOCKS: target grid size (the weight gradients share the GPU with the data-gradient
+  // target grid size (the weight gradients share the GPU with the data-gradient
   // chain on another stream, so they need not fill it alone)
-  static const int target_blocks = [] {
-    const char* e = getenv("DLMPI_WGRAD_BLOCKS");
-    return e ? std::max(64, atoi(e)) : 512;
-  }();
+  constexpr int target_blocks = 512;
   const int maxsplit = std::max(1, ceil_div(a.npix, 512));
   int splits = std::max(1, std::min(maxsplit, w256 ? target_blocks / tiles : ceil_div(target_blocks, tiles)));
   int pps = ceil_div(a.npix, splits);

@@ -253,15 +253,8 @@ __device__ __forceinline__ void colsum2_final(const double* __restrict__ dpart, 
 }
 
 static inline int colsum_slices(int T) {
-  // tiles per slice / slice cap (DLMPI_COLSUM_TPS / DLMPI_COLSUM_SMAX: A/B knobs)
-  static const int tps = [] {
-    const char* e = getenv("DLMPI_COLSUM_TPS");
-    return e && atoi(e) > 0 ? atoi(e) : 32;
-  }();
-  static const int smax = [] {
-    const char* e = getenv("DLMPI_COLSUM_SMAX");
-    return e && atoi(e) > 0 ? atoi(e) : 64;
-  }();
+  // tiles per slice / slice cap (measured, profiles/r2_*)
+  constexpr int tps = 32, smax = 64;
   int S = (T + tps - 1) / tps;
   return S < 1 ? 1 : (S > smax ? smax : S);
 }
@@ -718,29 +711,16 @@ extern "C" int* dlmpi_splitk_tickets(hipStream_t s, int n) {
 }
 
 static bool fused_finalize() {
-  static const bool v = [] {
-    const char* e = getenv("DLMPI_BN_FUSED_FINALIZE");
-    return !(e && atoi(e) == 0);
-  }();
+  static const bool v = true;
   return v;
 }
 
-static bool fin_sc1() {   // DLMPI_FIN_SC1=0: the fenced hand-off (A/B)
-  static const bool v = [] {
-    const char* e = getenv("DLMPI_FIN_SC1");
-    return !(e && atoi(e) == 0);
-  }();
+static bool fin_sc1() {   // false: the fenced hand-off (A/B)
+  static const bool v = true;
   return v;
 }
 
-static int colsum_direct_max() {
-  static const int v = [] {
-    const char* e = getenv("DLMPI_COLSUM_DIRECT");
-    const int t = e ? atoi(e) : kDirectMaxT;
-    return t < kDirectMaxT ? t : kDirectMaxT;   // the kernel holds <= kDirectMaxT rows
-  }();
-  return v;
-}
+static int colsum_direct_max() { return kDirectMaxT; }   // the kernel holds <= kDirectMaxT rows
 
 static hipError_t colsum_finalize(const float* partial, int T, int C, int ns, int k2, double* ws, const FinArgs& f,
                                   hipStream_t s) {
@@ -885,10 +865,7 @@ extern "C" hipError_t dlmpi_maxpool_bwd_bn(const void* dy, const uint8_t* idx, i
                                            void* dx, float* partial, int nblk, int f32, hipStream_t s) {
   if (C % 8 || C > 2048 || (int64_t)N * H * W >= (1ll << 31)) return hipErrorInvalidValue;
   const int nw = (k + stride - 1) / stride;
-  static const bool generic = [] {   // DLMPI_POOL_BWD_GENERIC=1: the dependent window loop (A/B)
-    const char* e = getenv("DLMPI_POOL_BWD_GENERIC");
-    return e && atoi(e) != 0;
-  }();
+  constexpr bool generic = false;   // true: the dependent window loop (measured slower, kept generic)
 #define LAUNCH_MPB1(NW, T)                                                                                          \
   hipLaunchKernelGGL((maxpool_bwd_bn_kernel<NW, T>), dim3(nblk), dim3(256), 0, s, CT(dy), idx, N, H, W, C, k, stride, \
                      pad, OH, OW, make_fastdiv(W), make_fastdiv(H), CT(z), mscale, mshift, CT(add), ldadd, addoff,   \

@@ -338,7 +338,7 @@ __global__ __launch_bounds__(64 * NW) void conv1x1_dgrad_stream_kernel(const Dgr
 
 using namespace dlmpi;
 
-// DLMPI_DGRAD_STREAM=0 disables the kernel (A/B); set_dgrad_stream(0|1) overrides (tests; 2: also the
+// set_dgrad_stream(0|1) overrides the plan (tests; 2: also the
 // opt-in tile variants)
 static int g_dgs_override = -1;
 extern "C" void dlmpi_set_dgrad_stream(int mode) { g_dgs_override = mode; }
@@ -360,20 +360,14 @@ extern "C" int dlmpi_dgs_blocks() {
 // communicator whose channels hold CUs).
 extern "C" int dlmpi_dgrad_stream_plan(int64_t M, int K, int Kout, int mask_mode, int z2, int has_res, int* bm, int* bn,
                                        int* G) {
-  static const int env = [] {
-    const char* e = getenv("DLMPI_DGRAD_STREAM");
-    return e ? atoi(e) : 1;
-  }();
+  static const int env = 1;
   const int blocks = dlmpi_dgs_blocks();
   const int on = g_dgs_override >= 0 ? g_dgs_override : env;
   if (!on || M <= 0 || mask_mode < 0 || mask_mode > 2 || (z2 && mask_mode == 0)) return 0;
   // LDS per block (one block per CU): weights KS x BN x 128 B resident + A + 2 x epilogue operands
   if (K == 128 && Kout % 128 == 0) { *bm = 64; *bn = 128; }          // 98-146 KB
-  else if (K == 256 && Kout % 128 == 0) {   // 48 rows: 6 waves (3 x 2), 135-149 KB (DLMPI_DGS_K256_ROWS=32: 4 waves)
-    static const int rows = [] {
-      const char* e = getenv("DLMPI_DGS_K256_ROWS");
-      return e ? atoi(e) : 48;
-    }();
+  else if (K == 256 && Kout % 128 == 0) {   // 48 rows: 6 waves (3 x 2), 135-149 KB
+    static const int rows = 48;
     *bm = (z2 || rows == 32) ? 32 : 48;
     *bn = 128;
   }
@@ -384,11 +378,8 @@ extern "C" int dlmpi_dgrad_stream_plan(int64_t M, int K, int Kout, int mask_mode
     *bm = (has_res || z2 || mask_mode == 1) ? 32 : 64;
     // 32 x 64 tiles measured slower than the general kernel (layer3.0 conv1 dual 2x256 -> 512: 359 vs
     // 289 us; layer4 conv1 77 vs 69 us -- eight 64-wide columns re-read A, 4 waves per CU; ResNet-50
-    // 12,802 / 12,803 vs 12,837 / 12,968 img/s, profiles/r3_dgrad_stream/v4): opt-in DLMPI_DGS_K512=1
-    static const bool k512 = [] {
-      const char* e = getenv("DLMPI_DGS_K512");
-      return e && atoi(e) != 0;
-    }();
+    // 12,802 / 12,803 vs 12,837 / 12,968 img/s, profiles/r3_dgrad_stream/v4)
+    static const bool k512 = false;
     if (!k512 && g_dgs_override != 2 && *bm == 32) return 0;
   }
   else return 0;

@@ -879,13 +879,10 @@ static void launch_tile(const ConvArgs* a, dim3 grid, hipStream_t s) {
 
 // Split-K plan for small grids (ResNet-18 on 32x32 CIFAR: layer4 is 1x1 pixels, 8 tiles x 72
 // K-steps): slices so that tiles x slices reaches ~256 blocks, >= 4 K-steps per slice, <= 8 slices.
-// DLMPI_CONV_SPLITK=0 disables.  Slabs (fp32) and tickets come per stream role (bn.hip), so the
+// Slabs (fp32) and tickets come per stream role (bn.hip), so the
 // main and the branch stream can run split convolutions concurrently.
 static int splitk_plan(int tiles, int nk) {
-  static const int on = [] {
-    const char* e = getenv("DLMPI_CONV_SPLITK");
-    return e ? atoi(e) : 1;
-  }();
+  static const int on = 1;
   if (!on || tiles >= 256 || nk < 8) return 1;
   int S = (256 + tiles - 1) / tiles;
   S = S < nk / 4 ? S : nk / 4;

@@ -450,10 +450,7 @@ using namespace dlmpi;
 extern "C" hipError_t dlmpi_conv_wgrad(const WgradArgs* a, int bm, int bn, hipStream_t s) {
   const unsigned nwg = (unsigned)(a->mtiles * a->ntiles * a->splits);
   if (nwg == 0) return hipSuccess;
-  static const int stages = [] {
-    const char* e = getenv("DLMPI_WGRAD_STAGES");
-    return e ? atoi(e) : 1;
-  }();
+  static const int stages = 1;
   const dim3 g(nwg), b(256);
   if (a->f32) {
     if (bm != 64 || bn != 64 || a->ws == nullptr || a->pro_a || a->pro_b) return hipErrorInvalidValue;

@@ -44,7 +44,7 @@ def grad_side(be, *tensors):
     (kept alive for it in the caching allocator).  The engine backward joins the side stream
     before the optimizer (``_EngineFn.backward``).
 
-    Keeping them alive: by default (``DLMPI_STREAM_HOLD=1``) the buffers are held in ``be.held``
+    Keeping them alive: the buffers are held in ``be.held``
     until that join and then dropped, so their blocks go back to the main stream's pool already
     ordered after the side-stream work.  ``record_stream`` instead defers each block's reuse to an
     event the host polls only at the next allocation; the host runs a whole backward ahead of the
@@ -77,7 +77,7 @@ def record_on(stream, *objs):
     """Mark every tensor (or Act buffer) inside ``objs`` (nested tuples / lists allowed) as used on
     ``stream``, so the caching allocator does not recycle it before that stream's work is done.
 
-    With ``DLMPI_STREAM_HOLD=1`` (default) this is a no-op: its callers (the ResNet downsample
+    With ``_STREAM_HOLD`` (always) this is a no-op: its callers (the ResNet downsample
     branch, models/resnet.py:_BlockExec) keep the main-pool tensors they hand to the branch stream
     referenced until the main stream has waited for it, and the branch stream waits for the main
     stream every time it is entered, so a branch-pool block freed after a main-stream read is only

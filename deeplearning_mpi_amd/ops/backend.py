@@ -71,6 +71,8 @@ def replace_poisoned_aux_streams() -> int:
 
 class NativeBackend:
     name = "native"
+    use_side_stream = True     # False: weight gradients on the current stream (A/B)
+    use_branch_stream = True   # False: the ResNet downsample branch on the current stream (A/B)
     dt = torch.float32
 
     def __init__(self, device, act_dtype=torch.bfloat16):
@@ -88,13 +90,12 @@ class NativeBackend:
         self.held = []   # buffers read on the side stream, dropped at the backward's join (engine.grad_side)
         # parameter-gradient work (weight-gradient GEMMs + split reductions, DDP bucket launches)
         # runs on this side stream, off the data-gradient critical path (models/engine.py:grad_side);
-        # DLMPI_WGRAD_STREAM=0 keeps everything on the current stream
-        self._side = _aux_stream(self.device, self.C, 1) if os.environ.get("DLMPI_WGRAD_STREAM", "1") != "0" \
+        self._side = _aux_stream(self.device, self.C, 1) if self.use_side_stream \
             else None
         # independent residual branches (the ResNet downsample conv + BN) run on this stream beside
-        # the main branch, forward and backward (models/resnet.py:_BlockExec); DLMPI_BRANCH_STREAM=0: off
+        # the main branch, forward and backward (models/resnet.py:_BlockExec)
         self._branch = _aux_stream(self.device, self.C, 2) \
-            if os.environ.get("DLMPI_BRANCH_STREAM", "1") != "0" else None
+            if self.use_branch_stream else None
         # The auxiliary streams pay off when kernels are long enough to leave idle CUs beside each
         # other; a launch-bound step (ResNet-18 on 32x32 CIFAR: ~300 kernels of a few us) only pays
         # their per-launch event traffic (measured 31-36k vs 58-60k img/s eager).  The engine turns
