@@ -131,25 +131,39 @@ static void pick_tiles(int64_t M, int Kout, int64_t red, int cin, int& bm, int& 
 }
 
 // ---- pipelined 8-wave tiles (conv_igemm.hip conv_pipe_kernel) -----------------------------------
-// Long reductions over >= 64-channel operands into wide outputs: one 8-wave block per CU with an
-// LDS ring instead of 2-3 single-stage 4-wave blocks.  Returns the kernel variant + 1 (0: keep the
-// single-stage tile bm x bn) and sets the pipelined tile.  g_pipe_override (tests): -1 the rule,
-// 0 never, 1 wherever the kernel applies.
+// Long reductions over >= 64-channel operands into 256-multiple outputs: one 8-wave block per CU
+// with an LDS ring instead of 2-3 single-stage 4-wave blocks.  Of the pipelined tiles (256 x 256,
+// 224 x 256, 128 x 256) the one with the least modeled time: rounds of the 256-CU chip x tile area
+// x a per-area cost (128 x 256: per-wave 64 x 64 tiles, 1.25x the LDS traffic per MFMA of the
+// 128 x 64 per-wave tiles of the others; profiles/r4_lab).  At batch 256 the 14^2 ResNet layers are
+// 50,176 rows: 196 tiles of 256 rows leave 60 CUs idle, 224 tiles of 224 rows 32.  Returns the kernel
+// variant + 1 (0: keep the single-stage tile bm x bn).  g_pipe_override (tests): -1 the rule, 0 never,
+// 1 wherever the kernel applies.
 static int g_pipe_override = -1;
+// conv_igemm.hip VAR of the DMA issue: A pieces before the first K-half of MFMAs, B pieces before the
+// second (2) for the 256 / 224-row tiles; additionally staggered over the two waves of a SIMD (4) for
+// 128 x 256 (profiles/r4_lab: 3-8 % over issuing all at once, on every measured shape)
 static int pipe_select(int f32, int pro, int cin, int64_t M, int Kout, int64_t red, int& bm, int& bn) {
   if (f32 || pro != 0 || cin % 64 != 0 || g_pipe_override == 0) return 0;
   if (g_pipe_override == 1) {
     bm = Kout >= 256 ? 256 : (Kout > 64 ? 256 : 512);
     bn = Kout >= 256 ? 256 : (Kout > 64 ? 128 : 64);
-    return 1;
+    return 2 + 1;
   }
-  // long reductions into >= 256 output channels while 256 x 256 tiles still give every CU one
-  // (UNet levels 3-5: the 8-wave tiles the single-stage kernel had, now pipelined)
-  if (Kout >= 256 && red >= 2304 && ((M + 255) / 256) * ((Kout + 255) / 256) >= 256) {
-    bm = bn = 256;
-    return 1;
+  if (Kout < 256 || Kout % 256 != 0 || red < 1024) return 0;
+  struct Cand { int bm; double unit; };
+  const Cand cands[] = {{256, 1.0}, {224, 1.0}, {128, 1.25}};
+  double best = 1e300;
+  for (const Cand& c : cands) {
+    const int64_t tiles = ((M + c.bm - 1) / c.bm) * (Kout / 256);
+    const double t = (double)((tiles + 255) / 256) * c.bm * c.unit;
+    if (t < best - 1e-9) {
+      best = t;
+      bm = c.bm;
+    }
   }
-  return 0;
+  bn = 256;
+  return (bm == 128 ? 4 : 2) + 1;
 }
 
 // ---- 2-D halo tiles for 3x3 / stride-1 / pad-1 convolutions (conv_igemm.hip HALO) ----------------
@@ -161,10 +175,11 @@ static bool halo_on() {
 }
 // Tile th x tw (th * tw <= 128, (th + 2) * (tw + 2) <= 192) covering a P x Q grid with the fewest
 // 128-row tiles (ties: the wider tile).
-static void halo_geom(int P, int Q, int& th, int& tw, int& tiles_h, int& tiles_w) {
+static void halo_geom(int P, int Q, int bm, int& th, int& tw, int& tiles_h, int& tiles_w) {
   int best = INT32_MAX;
-  for (int w = 16; w >= 4; --w) {
-    const int h = std::min(128 / w, 192 / (w + 2) - 2);
+  const int rows = bm == 256 ? 352 : 192;   // conv_igemm.hip HALO_ROWS
+  for (int w = bm == 256 ? 32 : 16; w >= 4; --w) {
+    const int h = std::min(bm / w, rows / (w + 2) - 2);
     if (h < 1) continue;
     const int t = ceil_div(P, h) * ceil_div(Q, w);
     if (t < best) {
@@ -176,6 +191,13 @@ static void halo_geom(int P, int Q, int& th, int& tw, int& tiles_h, int& tiles_w
   tiles_h = ceil_div(P, th);
   tiles_w = ceil_div(Q, tw);
 }
+// Halo tile shape (profiles/r4_halo): 256-pixel tiles (16 x 16, 18 x 18 halo) for 64-channel
+// outputs (+9 % on 56^2 / 512^2 grids: half the B-fragment reads per MFMA) and for >= 256-channel
+// outputs (+2-4 %); 128-pixel tiles for 128-channel outputs, where the 256 x 128 tile loses 4-7 %.
+static void halo_tiles(int Kout, int& bm, int& bn) {
+  bn = std::min(bn, 128);
+  bm = (bn == 64 || Kout >= 256) ? 256 : 128;
+}
 // Measured per shape (profiles/r3_halo): halo tiles win 1-6 % on grids >= 28 x 28 against the
 // 128-row gather tiles, tie with the 8-wave 256 x 256 tiles, and lose on 14^2 / 7^2 grids (a
 // 7 x 7 image fills a 126-pixel tile to 39 %) -- so only there, and not instead of 256 x 256 tiles.
@@ -184,12 +206,12 @@ static bool halo_eligible(int f32, int pro, int C, int R, int S, int stride, int
   return g_halo_override == 2 || (P >= 28 && Q >= 28 && !(bm == 256 && bn == 256));   // 2: any grid (tests)
 }
 static int g_halo_ran = 0;   // 1 if the last conv2d_fwd / conv2d_dgrad ran halo tiles (tests)
-// Switch a fully set-up single-phase launch (bm 128) to halo tiles: its M-tiles (and stats rows)
+// Switch a fully set-up single-phase launch (bm 128 / 256) to halo tiles: its M-tiles (and stats rows)
 // become N x tiles_h x tiles_w.
-static void apply_halo(ConvArgs& a, int N) {
+static void apply_halo(ConvArgs& a, int N, int bm) {
   ConvPhase& p = a.ph[0];
   int th = 8, tw = 16, tiles_h = 1, tiles_w = 1;
-  halo_geom(p.P, p.Q, th, tw, tiles_h, tiles_w);
+  halo_geom(p.P, p.Q, bm, th, tw, tiles_h, tiles_w);
   a.halo = 1;
   a.th = th;
   a.tw = tw;
@@ -201,9 +223,10 @@ static void apply_halo(ConvArgs& a, int N) {
   p.mtiles = N * tiles_h * tiles_w;
   p.tile_base = 0;
 }
-static int halo_mtiles(int N, int P, int Q) {
-  int th = 8, tw = 16, tiles_h = 1, tiles_w = 1;
-  halo_geom(P, Q, th, tw, tiles_h, tiles_w);
+static int halo_mtiles(int N, int P, int Q, int Kout, int bn) {
+  int th = 8, tw = 16, tiles_h = 1, tiles_w = 1, bm = 128;
+  halo_tiles(Kout, bm, bn);
+  halo_geom(P, Q, bm, th, tw, tiles_h, tiles_w);
   return N * tiles_h * tiles_w;
 }
 
@@ -538,10 +561,7 @@ static int conv2d_fwd_impl(const at::Tensor& x, int N, int H, int W, int C, int 
   if (a.f32) f32_tiles(bm, bn);
   int pipe = bm_req <= 0 && bn_req <= 0 ? pipe_select(a.f32, pro, C, (int64_t)N * P * Q, K, (int64_t)R * S * C, bm, bn) : 0;
   const bool halo = !pipe && bm_req <= 0 && bn_req <= 0 && halo_eligible(a.f32, pro, C, R, S, stride, pad, P, Q, bm, bn);
-  if (halo) {
-    bm = 128;
-    bn = std::min(bn, 128);
-  }
+  if (halo) halo_tiles(K, bm, bn);
   if (bm_req > 0) bm = bm_req;   // tests / experiments: force a tile shape
   if (bn_req > 0) bn = bn_req;
   g_stream_ran = 0;
@@ -590,7 +610,7 @@ static int conv2d_fwd_impl(const at::Tensor& x, int N, int H, int W, int C, int 
   p.wr0 = 0; p.wrs = 1; p.ws0 = 0; p.wss = 1;
   p.oh0 = 0; p.ow0 = 0;
   finish_phase(p, N, C, bm, a.f32);
-  if (halo) apply_halo(a, N);
+  if (halo) apply_halo(a, N, bm);
   g_halo_ran = halo ? 1 : 0;
   // autotuned tiling: BN-stats launches only through conv2d_fwd_bn (its buffer is sized for the
   // largest row count, conv2d_fwd_mtiles_pro, and its finalize uses the actual one)
@@ -682,7 +702,7 @@ int conv2d_fwd_mtiles_pro(int N, int H, int W, int C, int K, int R, int S, int s
     if (f32) f32_tiles(hbm, hbn);
     if (pipe_select(f32, pro, C, (int64_t)N * P * Q, K, (int64_t)R * S * C, hbm, hbn))
       return ceil_div((int64_t)N * P * Q, hbm);
-    if (halo_eligible(f32, pro, C, R, S, stride, pad, P, Q, hbm, hbn)) return halo_mtiles(N, P, Q);
+    if (halo_eligible(f32, pro, C, R, S, stride, pad, P, Q, hbm, hbn)) return halo_mtiles(N, P, Q, K, hbn);
   }
   // autotuned launches may pick any M tile: size for the smallest (64 rows)
   if (bm_req <= 0 && conv_autotune_on() && !f32 && pro == 0) return ceil_div((int64_t)N * P * Q, 64);
@@ -799,10 +819,7 @@ c10::optional<at::Tensor> conv2d_dgrad_pro(const at::Tensor& dy, int N, int P, i
   const int pipe = pipe_select(a.f32, pro, K, (int64_t)N * H * W / (stride * stride), C,
                                (int64_t)R * S * K / (stride * stride), bm, bn);
   const bool halo = !pipe && halo_eligible(a.f32, pro, K, R, S, stride, pad, H, W, bm, bn) && P == H && Q == W;
-  if (halo) {
-    bm = 128;
-    bn = std::min(bn, 128);
-  }
+  if (halo) halo_tiles(C, bm, bn);
   a.ntiles = ceil_div(C, bn);
   a.nphase = stride * stride;
   int tiles = 0;
@@ -824,7 +841,7 @@ c10::optional<at::Tensor> conv2d_dgrad_pro(const at::Tensor& dy, int N, int P, i
     }
   }
   if (halo) {
-    apply_halo(a, N);
+    apply_halo(a, N, bm);
     tiles = a.ph[0].mtiles;
   }
   g_halo_ran = halo ? 1 : 0;

@@ -310,8 +310,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BM * BN <= 
   constexpr int TM = WM / 16, TN = WN / 16;
   constexpr int RP = NT / 8;                  // tile rows staged per pass (8 lanes per 128-B row)
   constexpr int AL = BM / RP, BL = BN / RP;   // 16-byte pieces per thread per tile
-  constexpr int HALO_ROWS = 192;              // (th + 2) * (tw + 2) <= 192 (host-checked)
-  static_assert(!HALO || (BM == 128 && !SMALLC && PRO == 0 && sizeof(ET) == 2), "halo mode: 128-pixel bf16 tiles");
+  // (th + 2) * (tw + 2) <= HALO_ROWS (host-checked): 128-pixel tiles (8 x 16 -> 10 x 18 = 180 rows),
+  // 256-pixel tiles (16 x 16 -> 18 x 18 = 324 rows)
+  constexpr int HALO_ROWS = BM == 256 ? 352 : 192;
+  static_assert(!HALO || ((BM == 128 || BM == 256) && !SMALLC && PRO == 0 && sizeof(ET) == 2),
+                "halo mode: 128- or 256-pixel bf16 tiles");
   constexpr int HL = HALO ? HALO_ROWS * 128 / (16 * 64 * NW) : 1;   // halo pieces per thread
   constexpr int A_BYTES = (HALO ? HALO_ROWS : BM) * 128, B_BYTES = BN * 128;
   static_assert(PRO == 0 || !SMALLC, "operand prologue: regular channels");
@@ -964,9 +967,12 @@ extern "C" hipError_t dlmpi_conv_igemm_ex(const ConvArgs* a_in, int bm, int bn, 
   if (grid.x == 0) return hipSuccess;
   if (a->f32) return launch_f32(a, bm, bn, grid, s);
   if (a->halo) {   // 3x3 / stride 1 / pad 1 by 2-D tiles with a staged halo (host-planned)
-    if (a->pro != 0 || bm != 128 || a->C % 64 != 0) return hipErrorInvalidValue;
-    if (bn == 128) hipLaunchKernelGGL((conv_igemm_kernel<128, 128, false, 2, 0, uint16_t, true>), grid, dim3(256), 0, s, *a);
-    else if (bn == 64) hipLaunchKernelGGL((conv_igemm_kernel<128, 64, false, 2, 0, uint16_t, true>), grid, dim3(256), 0, s, *a);
+    if (a->pro != 0 || a->C % 64 != 0) return hipErrorInvalidValue;
+    if (bm == 128 && bn == 128) hipLaunchKernelGGL((conv_igemm_kernel<128, 128, false, 2, 0, uint16_t, true>), grid, dim3(256), 0, s, *a);
+    else if (bm == 128 && bn == 64) hipLaunchKernelGGL((conv_igemm_kernel<128, 64, false, 2, 0, uint16_t, true>), grid, dim3(256), 0, s, *a);
+    // 256-pixel tiles: per-wave 64 x 64 (4 x 1 waves) / 128 x 64 (2 x 2): half the LDS reads per MFMA
+    else if (bm == 256 && bn == 64) hipLaunchKernelGGL((conv_igemm_kernel<256, 64, false, 4, 0, uint16_t, true>), grid, dim3(256), 0, s, *a);
+    else if (bm == 256 && bn == 128) hipLaunchKernelGGL((conv_igemm_kernel<256, 128, false, 2, 0, uint16_t, true>), grid, dim3(256), 0, s, *a);
     else return hipErrorInvalidValue;
     return hipGetLastError();
   }

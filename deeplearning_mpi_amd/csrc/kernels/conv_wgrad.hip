@@ -435,7 +435,11 @@ __global__ __launch_bounds__(256) void wgrad_reduce_stage2(const float* __restri
   }
 }
 
+// Stage-1 groups: 0 (no stage 1: stage 2 sums the splits itself) when the tensor alone gives stage 2
+// >= 1024 blocks of parallelism (>= 256k floats: every ResNet-50 layer-3/4 weight) -- one launch and
+// one slab round trip less; else enough groups for >= 1024 stage-1 blocks.
 static inline int reduce_groups(int splits, int64_t total) {
+  if (total >= (int64_t)1024 * 256) return 0;
   const int64_t xb = (total / 4 + 255) / 256;
   int64_t G = (1024 + xb - 1) / xb;   // aim at >= 1024 blocks in stage 1
   if (G > splits) G = splits;
@@ -518,7 +522,7 @@ extern "C" hipError_t dlmpi_wgrad_reduce(const float* ws, int splits, int Ko, in
   const int G = reduce_groups(splits, total);
   const float* src = ws;
   int Gs = splits;
-  if (splits > 1) {
+  if (splits > 1 && G > 0) {
     if ((int64_t)G * total > (int64_t)ws2_floats) return hipErrorInvalidValue;
     hipLaunchKernelGGL(wgrad_reduce_stage1, dim3((unsigned)((total / 4 + 255) / 256), G), dim3(256), 0, s, ws, splits,
                        total, ws2);
