@@ -230,8 +230,13 @@ def main():
         step = CapturedStep(step, warmup=2, inputs=(x, y))
         args.warmup = max(args.warmup, 3)   # 2 eager warmup calls + the capturing call stay untimed
 
-    for _ in range(args.warmup):
+    from deeplearning_mpi_amd._ext import native as _native
+
+    red0 = _native().wgrad_reduce_launches()
+    for i in range(args.warmup):
         step()
+        if i == 0:   # one eager step: weight-gradient reduction launches (graph replays issue none)
+            red_per_step = _native().wgrad_reduce_launches() - red0
     comm.barrier()
     sync()
     t0 = time.perf_counter()
@@ -338,12 +343,11 @@ def main():
     # distributed facts of this run: the world size RCCL itself reports, its CU (channel) budget,
     # the gradient bucket layout, per-rank step times and the exposed all-reduce (max over ranks)
     native_comm = getattr(getattr(ddp.comm, "inner", ddp.comm), "c", None)
-    from deeplearning_mpi_amd._ext import native as _native
-
     dist_info = {
         "rccl_world_size": int(native_comm.size()) if native_comm is not None else None,
         "rccl_channels": os.environ.get("NCCL_MAX_NCHANNELS") if native_comm is not None else None,
         "dgrad_stream_blocks": int(_native().dgs_blocks()),
+        "wgrad_reduce_launches_per_step": int(red_per_step) if args.warmup > 0 else None,
         "bucket_mb": [round(b, 2) for b in ddp.bucket_sizes_mb()],
         "reducer": ddp.reducer is not None,
         "per_rank_ms_per_step": {"min": min(per_rank_ms), "max": max(per_rank_ms)},

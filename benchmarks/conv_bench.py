@@ -86,10 +86,7 @@ def main():
     ap.add_argument("--only", default=None)
     ap.add_argument("--no_miopen", action="store_true")
     ap.add_argument("--net", default="resnet50", choices=["resnet50", "unet512"])
-    ap.add_argument("--bm256_min_tiles", type=int, default=None, help="DLMPI_CONV_BM256_MIN_TILES")
     args = ap.parse_args()
-    if args.bm256_min_tiles is not None:
-        os.environ["DLMPI_CONV_BM256_MIN_TILES"] = str(args.bm256_min_tiles)
     if args.net == "unet512" and args.batch == 256:
         args.batch = 16
     from deeplearning_mpi_amd.ops.act import Act, padc

@@ -13,6 +13,7 @@
 // Buckets launch strictly in index order (identical collective order on every rank); a bucket
 // goes out as soon as it and all earlier buckets are complete.
 #include "comm.h"
+#include "ops.h"
 
 #include "../kernels/dlmpi_kernels.h"
 
@@ -408,6 +409,7 @@ void Reducer::launch_ready() {
   bool fenced = false;
   while (next_ < (int64_t)buckets_.size() && pending_[next_] == 0) {
     if (!fenced) {   // comm stream waits for the compute stream once per group of ready buckets
+      wgrad_flush();   // the queued weight-gradient reductions of these buckets, on the compute stream
       comm_->begin_bucket();
       fenced = true;
     }

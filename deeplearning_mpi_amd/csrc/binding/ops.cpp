@@ -4,6 +4,7 @@
 // step can be captured into a hipGraph.
 #include "ops.h"
 
+#include <c10/hip/HIPCachingAllocator.h>
 #include <c10/hip/HIPStream.h>
 
 #include <algorithm>
@@ -173,8 +174,8 @@ static bool halo_on() {
   static const int v = 1;
   return (g_halo_override >= 0 ? g_halo_override : v) != 0;
 }
-// Tile th x tw (th * tw <= 128, (th + 2) * (tw + 2) <= 192) covering a P x Q grid with the fewest
-// 128-row tiles (ties: the wider tile).
+// Tile th x tw (th * tw <= bm, (th + 2) * (tw + 2) <= 192 / 352 rows for bm 128 / 256) covering a
+// P x Q grid with the fewest tiles (ties: the wider tile).
 static void halo_geom(int P, int Q, int bm, int& th, int& tw, int& tiles_h, int& tiles_w) {
   int best = INT32_MAX;
   const int rows = bm == 256 ? 352 : 192;   // conv_igemm.hip HALO_ROWS
@@ -201,10 +202,14 @@ static void halo_tiles(int Kout, int& bm, int& bn) {
 // Measured per shape (profiles/r3_halo): halo tiles win 1-6 % on grids >= 28 x 28 against the
 // 128-row gather tiles, tie with the 8-wave 256 x 256 tiles, and lose on 14^2 / 7^2 grids (a
 // 7 x 7 image fills a 126-pixel tile to 39 %) -- so only there, and not instead of 256 x 256 tiles.
-static bool halo_eligible(int f32, int pro, int C, int R, int S, int stride, int pad, int P, int Q, int bm, int bn) {
+static bool halo_eligible(int f32, int pro, int C, int R, int S, int stride, int pad, int P, int Q) {
   if (!halo_on() || f32 || pro != 0 || C % 64 != 0 || R != 3 || S != 3 || stride != 1 || pad != 1) return false;
-  return g_halo_override == 2 || (P >= 28 && Q >= 28 && !(bm == 256 && bn == 256));   // 2: any grid (tests)
+  return g_halo_override == 2 || (P >= 28 && Q >= 28);   // 2: any grid (tests)
 }
+// Halo tiles before the pipelined kernel for >= 256 output channels (profiles/r4_halo: the 256 x 128
+// halo tile beat the best pipe tile on every UNet 3x3 of >= 32^2 grid, 2-5 %; 32^2 1024 -> 1024: 231.6
+// vs 243.2 us); the pipe kernel keeps the 14^2 / 7^2 grids, where halo tiles are not eligible.
+static bool halo_first(bool halo_ok, int Kout) { return halo_ok && Kout >= 256; }
 static int g_halo_ran = 0;   // 1 if the last conv2d_fwd / conv2d_dgrad ran halo tiles (tests)
 // Switch a fully set-up single-phase launch (bm 128 / 256) to halo tiles: its M-tiles (and stats rows)
 // become N x tiles_h x tiles_w.
@@ -445,8 +450,8 @@ static int g_dgrad_stream_ran = 0;   // 1 if the last conv2d_dgrad ran the strea
 
 static bool stream1x1_shape(int64_t M, int C, int K, int R, int S, int stride, int pad, int pro, int f32, int& bm,
                             int& bn, int& G) {
-  if (R != 1 || S != 1 || stride != 1 || pad != 0 || pro != 0 || f32) return false;
-  return dlmpi_stream1x1_plan(M, C, K, &bm, &bn, &G) != 0;
+  if (R != 1 || S != 1 || (stride != 1 && stride != 2) || pad != 0 || pro != 0 || f32) return false;
+  return dlmpi_stream1x1_plan(M, C, K, stride, &bm, &bn, &G) != 0;
 }
 
 
@@ -559,8 +564,10 @@ static int conv2d_fwd_impl(const at::Tensor& x, int N, int H, int W, int C, int 
   int bm, bn;
   pick_tiles((int64_t)N * P * Q, K, (int64_t)R * S * C, C, bm, bn, pro != 0);
   if (a.f32) f32_tiles(bm, bn);
-  int pipe = bm_req <= 0 && bn_req <= 0 ? pipe_select(a.f32, pro, C, (int64_t)N * P * Q, K, (int64_t)R * S * C, bm, bn) : 0;
-  const bool halo = !pipe && bm_req <= 0 && bn_req <= 0 && halo_eligible(a.f32, pro, C, R, S, stride, pad, P, Q, bm, bn);
+  const bool halo_ok = bm_req <= 0 && bn_req <= 0 && halo_eligible(a.f32, pro, C, R, S, stride, pad, P, Q);
+  const int pipe = bm_req <= 0 && bn_req <= 0 && !halo_first(halo_ok, K)
+                       ? pipe_select(a.f32, pro, C, (int64_t)N * P * Q, K, (int64_t)R * S * C, bm, bn) : 0;
+  const bool halo = !pipe && halo_ok;
   if (halo) halo_tiles(K, bm, bn);
   if (bm_req > 0) bm = bm_req;   // tests / experiments: force a tile shape
   if (bn_req > 0) bn = bn_req;
@@ -570,8 +577,8 @@ static int conv2d_fwd_impl(const at::Tensor& x, int N, int H, int W, int C, int 
     int sbm, sbn, G;
     if (bm_req <= 0 && bn_req <= 0 && stream1x1_shape(M, C, K, R, S, stride, pad, pro, a.f32, sbm, sbn, G)) {
       const bool ok = !res.has_value() && !scale.has_value() && !relu && a.kvalid == K && a.vec_store &&
-                      ldx % 8 == 0 && xoff % 8 == 0 && M * ldx < (1ll << 31) && M * ldy * 2 < (1ll << 31) &&
-                      y.scalar_type() == at::kBFloat16;
+                      ldx % 8 == 0 && xoff % 8 == 0 && (int64_t)N * H * W * ldx < (1ll << 31) &&
+                      M * ldy * 2 < (1ll << 31) && y.scalar_type() == at::kBFloat16;
       if (a.stats && !ok)
         throw std::runtime_error("conv2d_fwd: statistics were sized for the streaming 1x1 kernel, which cannot run");
       if (ok) {
@@ -586,6 +593,10 @@ static int conv2d_fwd_impl(const at::Tensor& x, int N, int H, int W, int C, int 
         sa.bias = a.bias;
         sa.stats = a.stats;
         sa.G = G; sa.ntiles = K / sbn; sa.mtiles = ceil_div(M, sbm);
+        sa.s2 = stride == 2 ? 1 : 0;
+        sa.H = H; sa.W = W;
+        sa.fdPQ = make_fastdiv((uint32_t)(P * Q));
+        sa.fdQ = make_fastdiv((uint32_t)Q);
         if (a.stats && stats->size(0) < G) throw std::runtime_error("conv2d_fwd: stats buffer too small");
         check(dlmpi_conv1x1_stream(&sa, sbm, sbn, cur_stream()), "conv2d_fwd (stream 1x1)");
         g_stream_ran = 1;
@@ -700,9 +711,10 @@ int conv2d_fwd_mtiles_pro(int N, int H, int W, int C, int K, int R, int S, int s
     int hbm, hbn;
     pick_tiles((int64_t)N * P * Q, K, (int64_t)R * S * C, C, hbm, hbn, pro != 0);
     if (f32) f32_tiles(hbm, hbn);
-    if (pipe_select(f32, pro, C, (int64_t)N * P * Q, K, (int64_t)R * S * C, hbm, hbn))
+    const bool halo_ok = halo_eligible(f32, pro, C, R, S, stride, pad, P, Q);
+    if (!halo_first(halo_ok, K) && pipe_select(f32, pro, C, (int64_t)N * P * Q, K, (int64_t)R * S * C, hbm, hbn))
       return ceil_div((int64_t)N * P * Q, hbm);
-    if (halo_eligible(f32, pro, C, R, S, stride, pad, P, Q, hbm, hbn)) return halo_mtiles(N, P, Q, K, hbn);
+    if (halo_ok) return halo_mtiles(N, P, Q, K, hbn);
   }
   // autotuned launches may pick any M tile: size for the smallest (64 rows)
   if (bm_req <= 0 && conv_autotune_on() && !f32 && pro == 0) return ceil_div((int64_t)N * P * Q, 64);
@@ -816,9 +828,10 @@ c10::optional<at::Tensor> conv2d_dgrad_pro(const at::Tensor& dy, int N, int P, i
   int bm, bn;
   pick_tiles((int64_t)N * H * W / (stride * stride), C, (int64_t)R * S * K / (stride * stride), K, bm, bn, pro != 0);
   if (a.f32) f32_tiles(bm, bn);
-  const int pipe = pipe_select(a.f32, pro, K, (int64_t)N * H * W / (stride * stride), C,
-                               (int64_t)R * S * K / (stride * stride), bm, bn);
-  const bool halo = !pipe && halo_eligible(a.f32, pro, K, R, S, stride, pad, H, W, bm, bn) && P == H && Q == W;
+  const bool halo_ok = halo_eligible(a.f32, pro, K, R, S, stride, pad, H, W) && P == H && Q == W;
+  const int pipe = halo_first(halo_ok, C) ? 0 : pipe_select(a.f32, pro, K, (int64_t)N * H * W / (stride * stride), C,
+                                                          (int64_t)R * S * K / (stride * stride), bm, bn);
+  const bool halo = !pipe && halo_ok;
   if (halo) halo_tiles(C, bm, bn);
   a.ntiles = ceil_div(C, bn);
   a.nphase = stride * stride;
@@ -920,6 +933,81 @@ void convT2x2_fwd(const at::Tensor& x, int N, int H, int W, int Cin, int ldx, in
 // dy is over the P x Q output grid of a conv (R x S, stride, pad) applied to x (H x W).
 // Operand prologues: pro_a 2 -> the dy operand is dz = pcoef[0] dy + pcoef[1] Z + pcoef[2] (a deferred
 // BN-backward apply, Z = the BN input); pro_b 1 -> the x operand is relu(x * pscale + pshift).
+// ---- deferred weight-gradient split reductions --------------------------------------------------
+// With set_wgrad_defer(1) (the engine backward) a weight gradient's split reduction is queued instead
+// of launched; wgrad_flush() -- the DDP reducer before each bucket launch, the engine at the end of its
+// backward, and a full queue (kWgradBatch entries) -- launches the queue as ONE batched kernel
+// (conv_wgrad.hip wgrad_reduce_batched: the same sums in the same order as dlmpi_wgrad_reduce's two
+// launches) on the current stream.  Queued entries keep their slab tensors alive; an entry queued on
+// another stream is ordered before the flush by an event, and its slab's reuse by recordStream.
+struct PendingReduce {
+  at::Tensor ws;
+  hipStream_t s;
+  dlmpi::WgradReduceEntry e;
+};
+static std::vector<PendingReduce> g_pending;
+static bool g_wgrad_defer = false;
+static int64_t g_reduce_launches = 0;   // reduction launches (either form), for tests / bench
+
+void wgrad_flush() {
+  if (g_pending.empty()) return;
+  const hipStream_t cur = cur_stream();
+  std::vector<hipStream_t> waited;
+  for (auto& p : g_pending) {
+    if (p.s == cur) continue;
+    if (std::find(waited.begin(), waited.end(), p.s) == waited.end()) {
+      hipEvent_t ev;
+      check(hipEventCreateWithFlags(&ev, hipEventDisableTiming), "wgrad_flush event");
+      check(hipEventRecord(ev, p.s), "wgrad_flush record");
+      check(hipStreamWaitEvent(cur, ev, 0), "wgrad_flush wait");
+      check(hipEventDestroy(ev), "wgrad_flush event");
+      waited.push_back(p.s);
+    }
+    c10::hip::HIPCachingAllocator::recordStream(p.ws.storage().data_ptr(), c10::hip::getCurrentHIPStream());
+  }
+  dlmpi::WgradReduceBatch b{};
+  for (size_t i = 0; i < g_pending.size(); ++i) {
+    b.e[b.n++] = g_pending[i].e;
+    if (b.n == dlmpi::kWgradBatch || i + 1 == g_pending.size()) {
+      check(dlmpi_wgrad_reduce_batch(&b, cur), "wgrad_reduce_batch");
+      ++g_reduce_launches;
+      b.n = 0;
+    }
+  }
+  g_pending.clear();
+}
+
+// the split reduction of a weight gradient: ws = [splits + G][wsz] (G = dlmpi_wgrad_reduce_groups)
+static void wgrad_reduce_or_defer(const at::Tensor& ws, int splits, int G, int64_t wsz, int Ko, int T, int Cpad,
+                                  int Creal, int Ko_real, at::Tensor& grad) {
+  float* out = ptr<float>(grad);
+  if (!g_wgrad_defer) {
+    check(dlmpi_wgrad_reduce(ptr<float>(ws), splits, Ko, T, Cpad, Creal, Ko_real, out, ptr<float>(ws) + (int64_t)splits * wsz,
+                             (int)std::min<int64_t>(INT32_MAX, (int64_t)G * wsz), cur_stream()),
+          "wgrad_reduce");
+    g_reduce_launches += splits > 1 && G > 0 ? 2 : 1;
+    return;
+  }
+  if (Ko_real == 0 || wsz == 0) return;
+  for (const auto& p : g_pending)   // a gradient accumulated twice: its first sum goes out first
+    if (p.e.out == out) {
+      wgrad_flush();
+      break;
+    }
+  PendingReduce p{ws, cur_stream(), {}};
+  p.e.ws = ptr<float>(ws);
+  p.e.ws2 = G > 0 ? ptr<float>(ws) + (int64_t)splits * wsz : nullptr;
+  p.e.out = out;
+  p.e.total = (int64_t)Ko * T * Cpad;
+  p.e.splits = splits;
+  p.e.Ko_real = Ko_real;
+  p.e.T = T;
+  p.e.Cpad = Cpad;
+  p.e.Creal = Creal;
+  g_pending.push_back(std::move(p));
+  if ((int)g_pending.size() >= dlmpi::kWgradBatch) wgrad_flush();
+}
+
 static int g_wgrad3_override = -1;   // dlmpi_ext set_wgrad3 (tests); -1: on
 static int g_wgrad3_ran = 0;         // 1 if the last weight gradient ran the 3x3 spatial-tile kernel
 
@@ -985,9 +1073,7 @@ void conv2d_wgrad_pro(const at::Tensor& dy, int lddy, int dyoff, int Ko, const a
     b.ws = ptr<float>(ws);
     g_wgrad3_ran = 1;
     check(dlmpi_wgrad3x3(&b, kt, ct, cur_stream()), "conv2d_wgrad (3x3 tiles)");
-    check(dlmpi_wgrad_reduce(b.ws, splits, Ko, 9, C, Creal, Ko_real, ptr<float>(grad), b.ws + (int64_t)splits * wsz,
-                             (int)std::min<int64_t>(INT32_MAX, (int64_t)G * wsz), cur_stream()),
-          "wgrad_reduce");
+    wgrad_reduce_or_defer(ws, splits, G, wsz, Ko, 9, C, Creal, Ko_real, grad);
     return;
   }
   g_wgrad3_ran = 0;
@@ -1032,9 +1118,7 @@ void conv2d_wgrad_pro(const at::Tensor& dy, int lddy, int dyoff, int Ko, const a
   at::Tensor ws = at::empty({(int64_t)(splits + G) * wsz}, dy.options().dtype(at::kFloat));
   a.ws = ptr<float>(ws);
   check(dlmpi_conv_wgrad(&a, bm, bn, cur_stream()), "conv2d_wgrad");
-  check(dlmpi_wgrad_reduce(a.ws, splits, Ko, R * S, C, Creal, Ko_real, ptr<float>(grad), a.ws + (int64_t)splits * wsz,
-                           (int)std::min<int64_t>(INT32_MAX, (int64_t)G * wsz), cur_stream()),
-        "wgrad_reduce");
+  wgrad_reduce_or_defer(ws, splits, G, wsz, Ko, R * S, C, Creal, Ko_real, grad);
 }
 
 void conv2d_wgrad(const at::Tensor& dy, int lddy, int dyoff, int Ko, const at::Tensor& x, int N, int H, int W, int C,
@@ -1421,6 +1505,13 @@ void register_ops(pybind11::module& m) {
   m.def("dgrad_stream_last", []() { return g_dgrad_stream_ran; });
   m.def("set_conv_autotune", [](int mode) { g_autotune_override = mode; });
   m.def("set_wgrad3", [](int mode) { g_wgrad3_override = mode; });
+  m.def("set_wgrad_defer", [](bool on) {
+    if (!on) wgrad_flush();
+    g_wgrad_defer = on;
+  });
+  m.def("wgrad_flush", &wgrad_flush);
+  m.def("wgrad_pending", []() { return (int)g_pending.size(); });
+  m.def("wgrad_reduce_launches", []() { return g_reduce_launches; });
   m.def("set_conv_halo", [](int mode) { g_halo_override = mode; });
   m.def("set_conv_pipe", [](int mode) { g_pipe_override = mode; });
   m.def("set_dgs_blocks", [](int n) { dlmpi_set_dgs_blocks(n); });

@@ -118,7 +118,7 @@ __global__ __launch_bounds__(64 * NW) void conv1x1_dgrad_stream_kernel(const Dgr
   const int wm = wid / WGN, wn = wid % WGN;
   const int fr = lane & 15, fg = lane >> 4;
   const int lrow = tid >> 3;                                 // A / W staging row (+ RP i)
-  const int jc = (tid & 7) ^ ((tid >> 4) & 7);               // swizzled 16-B chunk this lane fetches
+  const int jc = (tid & 7) ^ ((tid >> 3) & 7);               // swizzled 16-B chunk this lane fetches
   const int erow = tid / ECH, ej = tid % ECH;                // epilogue-tile staging row (+ EP i), chunk
   const char* zp = reinterpret_cast<const char*>(g_zero_page);
 
@@ -219,12 +219,12 @@ __global__ __launch_bounds__(64 * NW) void conv1x1_dgrad_stream_kernel(const Dgr
 #pragma unroll
         for (int mi = 0; mi < TM; ++mi) {
           const int r = wm * WM + mi * 16 + fr;
-          af[mi] = *reinterpret_cast<const bf16x8*>(A + r * 128 + ((ch ^ ((r >> 1) & 7)) << 4));
+          af[mi] = *reinterpret_cast<const bf16x8*>(A + r * 128 + ((ch ^ (r & 7)) << 4));
         }
 #pragma unroll
         for (int ni = 0; ni < TN; ++ni) {
           const int r = wn * WN + ni * 16 + fr;
-          bfr[ni] = *reinterpret_cast<const bf16x8*>(B + r * 128 + ((ch ^ ((r >> 1) & 7)) << 4));
+          bfr[ni] = *reinterpret_cast<const bf16x8*>(B + r * 128 + ((ch ^ (r & 7)) << 4));
         }
 #pragma unroll
         for (int mi = 0; mi < TM; ++mi)

@@ -1,6 +1,7 @@
-// Streaming 1x1 / stride-1 convolution forward for short reductions (C = 64 / 128 / 256 input
-// channels): the memory-bound "expand" convolutions of the ResNet bottleneck (conv3 and the
-// layer-1 downsample, 56^2 64->256, 28^2 128->512, 14^2 256->1024), whose output write dominates.
+// Streaming 1x1 convolution forward for short reductions (C = 64 / 128 / 256 input channels): the
+// memory-bound "expand" convolutions of the ResNet bottleneck (conv3 and the layer-1 downsample,
+// 56^2 64->256, 28^2 128->512, 14^2 256->1024), whose output write dominates, the layer-1 block-1
+// conv1 (56^2 64->64), and the stride-2 layer-2 projection (56^2 256->512, S2: gathered rows).
 //
 // Why a kernel of its own (profiles/r3_stream1x1): the general implicit-GEMM kernel runs one tile
 // per block -- stage A and B, one or two K-steps of MFMA, then the epilogue's stores -- so while a
@@ -42,7 +43,7 @@ constexpr int vmcnt_imm(int n) { return (n & 15) | 0x70 | 0xF00 | ((n >> 4) << 1
 
 __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
-template <int BM, int BN, int KS, bool STATS>
+template <int BM, int BN, int KS, bool STATS, bool S2>
 __global__ __launch_bounds__(256) void conv1x1_stream_kernel(const Stream1x1Args a) {
   constexpr int NT = 256;
   constexpr int WM = BM / 2, WN = BN / 2;       // 2 x 2 waves
@@ -68,7 +69,7 @@ __global__ __launch_bounds__(256) void conv1x1_stream_kernel(const Stream1x1Args
   const int wm = wid >> 1, wn = wid & 1;
   const int fr = lane & 15, fg = lane >> 4;
   const int lrow = tid >> 3;                                // staging row (+ RP i)
-  const int jc = (tid & 7) ^ ((tid >> 4) & 7);              // swizzled 16-byte chunk this lane fetches
+  const int jc = (tid & 7) ^ ((tid >> 3) & 7);              // swizzled 16-byte chunk this lane fetches
   const char* zp = reinterpret_cast<const char*>(g_zero_page);   // weight rows past Kout
 
   // block -> (N-tile, position in the N-tile's block group); the ntiles blocks that walk the same
@@ -95,7 +96,13 @@ __global__ __launch_bounds__(256) void conv1x1_stream_kernel(const Stream1x1Args
         // no select / exec-masked region around the load, which keeps the compiler's vmcnt
         // scoreboard exact so that it adds no vmcnt(0) of its own (32-bit offsets: host-checked)
         const int m = min(mt * BM + lrow + RP * i, a.M - 1);
-        const char* src = reinterpret_cast<const char*>(a.x + (uint32_t)(m * a.ldx + a.xoff + ks * 64 + 8 * jc));
+        int row = m;
+        if constexpr (S2) {   // output pixel (n, p, q) reads input pixel (n, 2p, 2q)
+          const uint32_t n = fdiv((uint32_t)m, a.fdPQ), rem = (uint32_t)m - n * a.fdPQ.d;
+          const uint32_t p = fdiv(rem, a.fdQ), q = rem - p * a.fdQ.d;
+          row = (int)((n * a.H + 2 * p) * a.W + 2 * q);
+        }
+        const char* src = reinterpret_cast<const char*>(a.x + (uint32_t)(row * a.ldx + a.xoff + ks * 64 + 8 * jc));
         __builtin_amdgcn_global_load_lds(src, (s1x1_lds_void*)(As + ks * BM * 128 + (RP * i + 8 * wid) * 128), 16, 0,
                                          0);
       }
@@ -141,12 +148,12 @@ __global__ __launch_bounds__(256) void conv1x1_stream_kernel(const Stream1x1Args
 #pragma unroll
         for (int mi = 0; mi < TM; ++mi) {
           const int r = wm * WM + mi * 16 + fr;
-          af[mi] = *reinterpret_cast<const bf16x8*>(A + r * 128 + ((ch ^ ((r >> 1) & 7)) << 4));
+          af[mi] = *reinterpret_cast<const bf16x8*>(A + r * 128 + ((ch ^ (r & 7)) << 4));
         }
 #pragma unroll
         for (int ni = 0; ni < TN; ++ni) {
           const int r = wn * WN + ni * 16 + fr;
-          bfr[ni] = *reinterpret_cast<const bf16x8*>(B + r * 128 + ((ch ^ ((r >> 1) & 7)) << 4));
+          bfr[ni] = *reinterpret_cast<const bf16x8*>(B + r * 128 + ((ch ^ (r & 7)) << 4));
         }
 #pragma unroll
         for (int mi = 0; mi < TM; ++mi)
@@ -227,10 +234,12 @@ using namespace dlmpi;
 static int g_stream_override = -1;   // dlmpi_ext set_conv_stream (tests)
 extern "C" void dlmpi_set_conv_stream(int mode) { g_stream_override = mode; }
 
-extern "C" int dlmpi_stream1x1_plan(int64_t M, int C, int Kout, int* bm, int* bn, int* G) {
+extern "C" int dlmpi_stream1x1_plan(int64_t M, int C, int Kout, int stride, int* bm, int* bn, int* G) {
   const int on = g_stream_override >= 0 ? g_stream_override : 1;
   if (!on || M <= 0) return 0;
+  if (stride == 2 && !(C == 256 && Kout % 64 == 0)) return 0;
   if (C == 64 && Kout % 128 == 0) { *bm = 128; *bn = 128; }
+  else if (C == 64 && Kout == 64) { *bm = 128; *bn = 64; }   // layer-1 block-1 conv1 (56^2 64 -> 64)
   else if (C == 128 && Kout % 128 == 0) { *bm = 64; *bn = 128; }
   else if (C == 256 && Kout % 64 == 0) { *bm = 64; *bn = 64; }
   else return 0;
@@ -245,14 +254,18 @@ extern "C" int dlmpi_stream1x1_plan(int64_t M, int C, int Kout, int* bm, int* bn
 
 extern "C" hipError_t dlmpi_conv1x1_stream(const Stream1x1Args* a, int bm, int bn, hipStream_t s) {
   const dim3 grid((unsigned)(a->ntiles * a->G)), block(256);
-#define LAUNCH_S1(BM_, BN_, KS_)                                                                              \
-  do {                                                                                                      \
-    if (a->stats) hipLaunchKernelGGL((conv1x1_stream_kernel<BM_, BN_, KS_, true>), grid, block, 0, s, *a);     \
-    else hipLaunchKernelGGL((conv1x1_stream_kernel<BM_, BN_, KS_, false>), grid, block, 0, s, *a);          \
+#define LAUNCH_S1(BM_, BN_, KS_, S2_)                                                                              \
+  do {                                                                                                           \
+    if (a->stats) hipLaunchKernelGGL((conv1x1_stream_kernel<BM_, BN_, KS_, true, S2_>), grid, block, 0, s, *a);     \
+    else hipLaunchKernelGGL((conv1x1_stream_kernel<BM_, BN_, KS_, false, S2_>), grid, block, 0, s, *a);          \
   } while (0)
-  if (bm == 128 && bn == 128 && a->C == 64) LAUNCH_S1(128, 128, 1);
-  else if (bm == 64 && bn == 128 && a->C == 128) LAUNCH_S1(64, 128, 2);
-  else if (bm == 64 && bn == 64 && a->C == 256) LAUNCH_S1(64, 64, 4);
+  if (a->s2) {   // the stride-2 projection (layer-2 downsample, 56^2 256 -> 512)
+    if (bm == 64 && bn == 64 && a->C == 256) LAUNCH_S1(64, 64, 4, true);
+    else return hipErrorInvalidValue;
+  } else if (bm == 128 && bn == 128 && a->C == 64) LAUNCH_S1(128, 128, 1, false);
+  else if (bm == 128 && bn == 64 && a->C == 64) LAUNCH_S1(128, 64, 1, false);
+  else if (bm == 64 && bn == 128 && a->C == 128) LAUNCH_S1(64, 128, 2, false);
+  else if (bm == 64 && bn == 64 && a->C == 256) LAUNCH_S1(64, 64, 4, false);
   else return hipErrorInvalidValue;
 #undef LAUNCH_S1
   return hipGetLastError();

@@ -447,6 +447,74 @@ static inline int reduce_groups(int splits, int64_t total) {
   return (int)(G < 1 ? 1 : G);
 }
 
+// Batched split reduction (one launch for up to kWgradBatch weight gradients that became ready
+// together; ops.cpp defers and flushes them).  Entry with G == 0: a block per 1024-float chunk sums
+// all splits in order (stage 2 reading the slabs directly).  G > 0: a block per (chunk, group g)
+// writes its group sum to ws2[g] (stage 1); the chunk's last-arriving block (a self-resetting
+// completion ticket) sums the G group sums in order (stage 2).  Every output gets the sums of
+// dlmpi_wgrad_reduce's two launches in the same order: bit-identical.
+__device__ __forceinline__ void reduce_store4(const WgradReduceEntry& e, int64_t i4, f32x4 v) {
+  const int64_t TC = (int64_t)e.T * e.Cpad;
+  const int64_t ko = i4 / TC;
+  if (ko >= e.Ko_real) return;
+  const int64_t rem = i4 - ko * TC;
+  const int64_t tt = rem / e.Cpad;   // Cpad % 8 == 0: the 4 outputs share (ko, tt)
+  const int c = (int)(rem - tt * e.Cpad);
+  float* o = e.out + (ko * e.T + tt) * e.Creal;
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+    if (c + k < e.Creal) o[c + k] += v[k];
+}
+
+__global__ __launch_bounds__(256) void wgrad_reduce_batched(const WgradReduceBatch b, int* __restrict__ tickets) {
+  int k = 0;
+  while (k + 1 < b.n && (int)blockIdx.x >= b.e[k + 1].block0) ++k;
+  const WgradReduceEntry& e = b.e[k];
+  const int tid = threadIdx.x;
+  const int local = (int)blockIdx.x - e.block0;
+  if (e.G == 0) {
+    const int64_t i4 = ((int64_t)local * 256 + tid) * 4;
+    if (i4 >= e.total) return;
+    f32x4 s = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll 8
+    for (int z = 0; z < e.splits; ++z) s += *reinterpret_cast<const f32x4*>(e.ws + (int64_t)z * e.total + i4);
+    reduce_store4(e, i4, s);
+    return;
+  }
+  const int G = e.G, g = local % G, chunk = local / G;
+  const int per = (e.splits + G - 1) / G;
+  const int z0 = g * per, z1 = min(e.splits, z0 + per);
+  const int64_t i4 = ((int64_t)chunk * 256 + tid) * 4;
+  const bool in = i4 < e.total;
+  if (in) {
+    f32x4 s = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll 8
+    for (int z = z0; z < z1; ++z) s += *reinterpret_cast<const f32x4*>(e.ws + (int64_t)z * e.total + i4);
+    *reinterpret_cast<f32x4*>(e.ws2 + (int64_t)g * e.total + i4) = s;
+  }
+  __shared__ int last;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    last = __hip_atomic_fetch_add(tickets + e.tk0 + chunk, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == G - 1;
+  }
+  __syncthreads();
+  if (!last) return;
+  if (tid == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __hip_atomic_store(tickets + e.tk0 + chunk, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+  if (!in) return;
+  f32x4 s = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll 8
+  for (int gg = 0; gg < G; ++gg) s += *reinterpret_cast<const f32x4*>(e.ws2 + (int64_t)gg * e.total + i4);
+  reduce_store4(e, i4, s);
+}
+
 }  // namespace dlmpi
 
 using namespace dlmpi;
@@ -533,5 +601,29 @@ extern "C" hipError_t dlmpi_wgrad_reduce(const float* ws, int splits, int Ko, in
   if (blocks > 8192) blocks = 8192;
   hipLaunchKernelGGL(wgrad_reduce_stage2, dim3((unsigned)blocks), dim3(256), 0, s, src, Gs, Ko, T, Cpad, Creal, Ko_real,
                      out);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t dlmpi_wgrad_reduce_batch(WgradReduceBatch* b, hipStream_t s) {
+  if (b->n <= 0) return hipSuccess;
+  if (b->n > kWgradBatch) return hipErrorInvalidValue;
+  int64_t blocks = 0;
+  int tks = 0;
+  for (int i = 0; i < b->n; ++i) {
+    WgradReduceEntry& e = b->e[i];
+    if (e.total % 4 != 0 || e.Cpad % 8 != 0) return hipErrorInvalidValue;
+    e.G = e.splits > 1 ? reduce_groups(e.splits, e.total) : 0;
+    if (e.G > 0 && e.ws2 == nullptr) return hipErrorInvalidValue;
+    const int64_t chunks = (e.total + 1023) / 1024;
+    e.block0 = (int)blocks;
+    e.tk0 = tks;
+    blocks += chunks * (e.G > 0 ? e.G : 1);
+    if (e.G > 0) tks += (int)chunks;
+  }
+  if (blocks == 0) return hipSuccess;
+  if (blocks > INT32_MAX || tks > 4096) return hipErrorInvalidValue;
+  int* tk = dlmpi_splitk_tickets(s, tks > 0 ? tks : 1);
+  if (tk == nullptr) return hipErrorOutOfMemory;
+  hipLaunchKernelGGL(wgrad_reduce_batched, dim3((unsigned)blocks), dim3(256), 0, s, *b, tk);
   return hipGetLastError();
 }

@@ -55,9 +55,10 @@ struct FinArgs {
   int raw_z;
 };
 
-// Streaming 1x1 / stride-1 forward (conv1x1_stream.hip): y[m][yoff + n] = sum_c x[m][xoff + c] w[n][c]
+// Streaming 1x1 forward (conv1x1_stream.hip): y[m][yoff + n] = sum_c x[row(m)][xoff + c] w[n][c]
 // (+ bias[n]) for m < M, bf16; stats (or null): [G][2][Kout] partial sums of the stored values, one
-// row per block of an N-tile.
+// row per block of an N-tile.  row(m) = m (stride 1) or, with s2, the input pixel (n, 2p, 2q) of
+// output pixel m = (n, p, q) of a P x Q grid over an H x W input (the stride-2 projection).
 struct Stream1x1Args {
   const uint16_t* x;
   int ldx, xoff;
@@ -69,6 +70,8 @@ struct Stream1x1Args {
   const float* bias;
   float* stats;
   int G, ntiles, mtiles;
+  int s2, H, W;                    // stride-2 gather (s2 = 1): input grid
+  FastDiv fdPQ, fdQ;               // output grid P x Q
 };
 
 // Streaming 1x1 / stride-1 data gradient with the fused BN-backward epilogue (conv1x1_dgrad_stream.hip)
@@ -200,6 +203,23 @@ struct WgradArgs {
 // 3x3 / stride-1 / pad-1 weight gradient by 8 x 8 output-pixel tiles (conv_wgrad3.hip): split z
 // reduces pixel tiles [z * tiles_per_split, ...) of the N x tiles_h x tiles_w grid into
 // ws[z][Ko][9 * C] (tap-major columns, the general path's workspace layout)
+// One deferred split reduction of a weight gradient (dlmpi_wgrad_reduce_batch): the same sums in
+// the same order as dlmpi_wgrad_reduce(ws, splits, Ko, T, Cpad, Creal, Ko_real, out, ws2, ...).
+struct WgradReduceEntry {
+  const float* ws;                 // [splits][Ko][T][Cpad] partials
+  float* ws2;                      // [G][Ko][T][Cpad] group sums (G > 0)
+  float* out;                      // [Ko_real][T][Creal], accumulated
+  int64_t total;                   // Ko * T * Cpad
+  int splits, G, Ko_real, T, Cpad, Creal;
+  int block0;                      // first block of this entry in the batch grid
+  int tk0;                         // first completion ticket (G > 0: one per 1024-float chunk)
+};
+constexpr int kWgradBatch = 16;
+struct WgradReduceBatch {
+  int n;
+  WgradReduceEntry e[kWgradBatch];
+};
+
 struct Wgrad3Args {
   const void* dy;
   int ldy, dyoff, Ko;
@@ -224,6 +244,9 @@ hipError_t dlmpi_conv_wgrad(const dlmpi::WgradArgs* a, int bm, int bn, hipStream
 hipError_t dlmpi_wgrad_reduce(const float* ws, int splits, int Ko, int T, int Cpad, int Creal,
                               int Ko_real, float* out, float* ws2, int ws2_floats, hipStream_t s);
 int dlmpi_wgrad_reduce_groups(int splits, int64_t total);
+// up to kWgradBatch deferred reductions in one launch (block0 / tk0 filled in here); tickets: the
+// split-K completion tickets of stream s (self-resetting), at most 4096 used
+hipError_t dlmpi_wgrad_reduce_batch(dlmpi::WgradReduceBatch* b, hipStream_t s);
 // 3x3 spatial-tile weight gradient: tile plan (KT x CT; 0 if the channel counts do not fit) + launch
 int dlmpi_wgrad3_plan(int Ko, int C, int* kt, int* ct);
 hipError_t dlmpi_wgrad3x3(const dlmpi::Wgrad3Args* a, int kt, int ct, hipStream_t s);
@@ -359,7 +382,7 @@ hipError_t dlmpi_comm_load(const void* bucket, int64_t bytes, void* scratch, int
                            int lds_bytes, double us, hipStream_t s);
 void dlmpi_set_conv_stream(int mode);
 void dlmpi_set_dgrad_stream(int mode);
-int dlmpi_stream1x1_plan(int64_t M, int C, int Kout, int* bm, int* bn, int* G);
+int dlmpi_stream1x1_plan(int64_t M, int C, int Kout, int stride, int* bm, int* bn, int* G);
 hipError_t dlmpi_conv1x1_stream(const dlmpi::Stream1x1Args* a, int bm, int bn, hipStream_t s);
 int dlmpi_dgrad_stream_plan(int64_t M, int K, int Kout, int mask_mode, int z2, int has_res, int* bm, int* bn, int* G);
 void dlmpi_set_dgs_blocks(int n);

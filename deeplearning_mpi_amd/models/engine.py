@@ -592,6 +592,9 @@ class S2DConvUnit(ConvUnit):
         g2 = torch.empty(K * R * S * CT, dtype=be.dt, device=dz.device)
         be.fill_(g2, 0.0)
         be.conv_wgrad(dz, x, R, S, 1, 0, g2, CT, K)
+        flush = getattr(be, "wgrad_flush", None)   # g2 is read right below: its reduction must have run
+        if flush is not None:
+            flush()
         if self._gidx is None or self._gidx.device != dz.device:
             # grad[k][r][s][c] <- g2[k][r // 2][s // 2][((r % 2) * 2 + s % 2) * CS + c]
             k, r, s_, c = torch.meshgrid(torch.arange(K), torch.arange(self.R0), torch.arange(self.S0),
@@ -677,12 +680,22 @@ class _EngineFn(torch.autograd.Function):
             prof = BWD_PROFILER   # bench.py --pyprof: the backward runs on autograd's worker thread
             if prof is not None:
                 prof.enable()
-            mod._engine_backward(state, gout)
+            be = mod._be
+            # weight-gradient split reductions are queued and launched in batches (at DDP bucket
+            # launches, every kWgradBatch gradients, and below): a handful of launches per step
+            defer = getattr(be, "wgrad_defer", None)   # (the shadow backend checks every call: never)
+            if defer is not None:
+                defer(True)
+            try:
+                mod._engine_backward(state, gout)
+            finally:
+                side = getattr(be, "side_stream", None)
+                if side is not None:   # every parameter gradient is final before the optimizer runs
+                    torch.cuda.current_stream().wait_stream(side)
+                if defer is not None:
+                    defer(False)   # flushes the queue's tail on this stream
             if prof is not None:
                 prof.disable()
-            side = getattr(mod._be, "side_stream", None)
-            if side is not None:   # every parameter gradient is final before the optimizer runs
-                torch.cuda.current_stream().wait_stream(side)
             held = getattr(mod._be, "held", None)
             if held:   # buffers read on the side stream: freed now, ordered after it (grad_side)
                 held.clear()

@@ -225,6 +225,14 @@ class NativeBackend:
     def convT_fwd(self, x: Act, wf, Cout, y: Act, bias=None):
         self.C.convT2x2_fwd(x.buf, x.N, x.H, x.W, x.C, x.ld, x.off, wf, Cout, y.buf, y.ld, y.off, bias)
 
+    def wgrad_defer(self, on: bool):
+        """Queue weight-gradient split reductions (on) / flush the queue and launch them at once
+        again (off); ops.cpp wgrad_reduce_or_defer."""
+        self.C.set_wgrad_defer(bool(on))
+
+    def wgrad_flush(self):
+        self.C.wgrad_flush()
+
     def conv_wgrad(self, dy, x, R, S, stride, pad, grad, Creal, Ko_real):
         dy, pa, ca, _, zb, zld, zoff = self._pro(dy)
         x, pb, sb, hb, _, _, _ = self._pro(x)
@@ -553,6 +561,12 @@ class RefBackend:
         wk = wf.view(Cout, 2, 2, Cin).permute(3, 0, 1, 2).to(self.dt)
         out = F.conv_transpose2d(x.nchw().to(self.dt), wk, bias, stride=2)
         self._store(y, out)
+
+    def wgrad_defer(self, on: bool):
+        pass
+
+    def wgrad_flush(self):
+        pass
 
     def conv_wgrad(self, dy, x, R, S, stride, pad, grad, Creal, Ko_real):
         dy, x = self.materialize(dy), self.materialize(x)

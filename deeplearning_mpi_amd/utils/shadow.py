@@ -23,7 +23,8 @@ from ..ops.act import Act, Deferred
 SKIP = frozenset({"maxpool_bwd", "cast_weights", "conv_mtiles", "materialize"})
 # fused ops whose inputs are engine objects the shadow cannot copy (engine.PendingApply): hidden, so
 # the engine takes the unfused path (the same values, op by op)
-HIDDEN = frozenset({"conv_fwd_bn_apply"})
+# (wgrad_defer: the weight gradients are compared call by call, so their reductions must not queue)
+HIDDEN = frozenset({"conv_fwd_bn_apply", "wgrad_defer", "wgrad_flush"})
 # positional index of the BN-partials buffer of ops that take it positionally
 STATS_ARG = {"conv_fwd_bn": 9}
 

@@ -292,6 +292,49 @@ def test_conv_wgrad(shape):
     assert _rel(g, gr) < 5e-3
 
 
+def test_wgrad_reduce_batched_bit_identical():
+    """Deferred weight-gradient split reductions (set_wgrad_defer, the engine backward's mode): 19
+    gradients of mixed kinds (gather / 1x1 direct / 3x3 spatial-tile kernels; two-stage and
+    direct reductions; channel un-padding) queued and launched as batched kernels -- the queue
+    flushes at 16 entries, when a gradient is accumulated twice, and when deferral ends -- give
+    bit-identical gradients to the immediate two-launch reductions, in a handful of launches."""
+    nb, _ = _be()
+    C = nb.C
+    torch.manual_seed(3)
+    jobs = []
+    shapes = CONV_SHAPES + [(64, 14, 14, 256, 128, 3, 1, 1), (8, 28, 28, 64, 64, 1, 1, 0), (2, 56, 56, 64, 64, 1, 1, 0)]
+    for sh in shapes + shapes[:6]:
+        N, H, W, Cin, K, R, s, p = sh
+        Cp, Kp = pad8(Cin), pad8(K)
+        P, Q = (H + 2 * p - R) // s + 1, (W + 2 * p - R) // s + 1
+        jobs.append((_act(N, H, W, Cp)[0], _act(N, P, Q, Kp)[0], R, s, p, Cin, K))
+    jobs = jobs[:19]
+    g0 = [torch.randn(K * R * R * Cin, device=DEV) for (_, _, R, _, _, Cin, K) in jobs]
+
+    def run(defer):
+        gs = [g.clone() for g in g0]
+        n0 = C.wgrad_reduce_launches()
+        C.set_wgrad_defer(defer)
+        try:
+            for i, (x, dy, R, s, p, Cin, K) in enumerate(jobs):
+                nb.conv_wgrad(dy, x, R, R, s, p, gs[i], Cin, K)
+                if i == 17:   # the same gradient slot accumulated twice inside one queue
+                    nb.conv_wgrad(dy, x, R, R, s, p, gs[i], Cin, K)
+            if defer:
+                assert C.wgrad_pending() > 0
+        finally:
+            C.set_wgrad_defer(False)
+        assert C.wgrad_pending() == 0
+        torch.cuda.synchronize()
+        return gs, C.wgrad_reduce_launches() - n0
+
+    imm, n_imm = run(False)
+    dfr, n_dfr = run(True)
+    for i, (a, b) in enumerate(zip(imm, dfr)):
+        assert torch.equal(a, b), i
+    assert n_dfr <= 3 < n_imm, (n_dfr, n_imm)
+
+
 HALO_SHAPES = [
     # N, H, W, Cin, Cout, x channel stride / offset (a concat slice)
     (2, 16, 16, 64, 64, None, 0),        # 8 x 16 tiles
@@ -794,6 +837,9 @@ STREAM_SHAPES = [
     (4, 14, 14, 256, 1024),
     (3, 5, 7, 256, 64),        # 105 rows, one N-tile
     (32, 56, 56, 64, 256),     # bench-layer scale (100k rows, every block walks many tiles)
+    (4, 28, 28, 64, 64),       # 64 -> 64 (the layer-1 block-1 conv1): 128 x 64 tiles
+    (4, 28, 28, 256, 512, 2),  # stride-2 projection (gathered rows), even grid
+    (3, 15, 13, 256, 128, 2),  # stride 2 over an odd grid: 8 x 7 outputs
 ]
 
 
@@ -805,7 +851,9 @@ def test_stream1x1_matches_general_kernel(shape, ld_out):
     MFMA dot products and rounding), statistics summed over rows equal to fp32 noise, BN finalize
     over the block rows equal to the finalize over the tile rows; 'dual' writes into the right half
     of a [rows][2K] buffer (the dual data-gradient layout) and must leave the left half untouched."""
-    N, H, W, Cin, K = shape
+    N, H, W, Cin, K = shape[:5]
+    s = shape[5] if len(shape) > 5 else 1
+    P, Q = (H - 1) // s + 1, (W - 1) // s + 1
     nb = NativeBackend(DEV)
     x, _ = _act(N, H, W, Cin)
     w = (torch.randn(K, 1, 1, Cin, device=DEV) / Cin ** 0.5).to(torch.bfloat16)
@@ -814,16 +862,16 @@ def test_stream1x1_matches_general_kernel(shape, ld_out):
     out = {}
     for mode in (1, 0):
         nb.C.set_conv_stream(mode)
-        mt = nb.conv_mtiles(N, H, W, Cin, K, 1, 1, 1, 0)
+        mt = nb.conv_mtiles(N, H, W, Cin, K, 1, 1, s, 0)
         if ld_out == "dual":
-            buf = torch.full((N * H * W, 2 * K), 7.0, device=DEV).to(torch.bfloat16)
-            y = Act(buf, N, H, W, K, K)
+            buf = torch.full((N * P * Q, 2 * K), 7.0, device=DEV).to(torch.bfloat16)
+            y = Act(buf, N, P, Q, K, K)
         else:
-            y = _empty(N, H, W, K)
+            y = _empty(N, P, Q, K)
         st = torch.zeros(mt, 2, K, device=DEV)   # an autotuned tile may write fewer rows than mt
         v = torch.empty(4, K, device=DEV)
         rm, rv = torch.zeros(K, device=DEV), torch.ones(K, device=DEV)
-        nb.conv_fwd_bn(x, w, K, 1, 1, 1, 0, y, bias, st, N * H * W, gamma, beta, rm, rv, 0.1, 1e-5,
+        nb.conv_fwd_bn(x, w, K, 1, 1, s, 0, y, bias, st, N * P * Q, gamma, beta, rm, rv, 0.1, 1e-5,
                        v[0], v[1], v[2], v[3])
         torch.cuda.synchronize()
         assert nb.C.conv_stream_last() == mode   # the streaming kernel ran (mode 1) / did not (mode 0)
