@@ -133,6 +133,10 @@ def main():
     ap.add_argument("--host_time", type=int, default=0,
                     help="N > 0: after the timed steps, N more steps timing the HOST issue time of each step "
                          "(call to return, GPU running behind) against the GPU step time; printed to stderr")
+    ap.add_argument("--pin", default="",
+                    help="A/B only: kernel-choice pins NAME=V[,NAME=V] -- pipe / halo / stream / dgrad_stream / "
+                         "autotune / wgrad3 / splitk (the extension's test setters; -1 = production choice), "
+                         "defer=0 (weight-gradient reductions launched one by one)")
     args = ap.parse_args()
     if args.rehearse > 0:
         args.rccl1 = 1
@@ -166,6 +170,21 @@ def main():
     def sync():
         if dev.type == "cuda":
             torch.cuda.synchronize()
+    pins = dict(kv.split("=") for kv in args.pin.split(",") if kv)
+    if pins:
+        from deeplearning_mpi_amd._ext import native as _nat
+
+        setters = {"pipe": "set_conv_pipe", "halo": "set_conv_halo", "stream": "set_conv_stream",
+                   "dgrad_stream": "set_dgrad_stream", "autotune": "set_conv_autotune", "wgrad3": "set_wgrad3",
+                   "splitk": "set_conv_splitk", "pipe_dgrad": "set_conv_pipe_dgrad", "wgrad_batch": "set_wgrad_batch",
+                   "defer_direct": "set_defer_direct", "wgrad3_blocks": "set_wgrad3_blocks"}
+        for k, v in pins.items():
+            if k in setters:
+                getattr(_nat(), setters[k])(int(v))
+        if pins.get("defer") == "0":
+            from deeplearning_mpi_amd.ops.backend import NativeBackend
+
+            NativeBackend.wgrad_defer = lambda self, on: None
     torch.manual_seed(0)
     shape = (cfg["cin"], cfg["image"], cfg["image"])
     if cfg["task"] == "cls":

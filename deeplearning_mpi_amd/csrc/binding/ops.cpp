@@ -141,6 +141,7 @@ static void pick_tiles(int64_t M, int Kout, int64_t red, int cin, int& bm, int& 
 // variant + 1 (0: keep the single-stage tile bm x bn).  g_pipe_override (tests): -1 the rule, 0 never,
 // 1 wherever the kernel applies.
 static int g_pipe_override = -1;
+static int g_pipe_dgrad_override = -1;   // dlmpi_ext set_conv_pipe_dgrad (A/B): 0 keeps data gradients off it
 // conv_igemm.hip VAR of the DMA issue: A pieces before the first K-half of MFMAs, B pieces before the
 // second (2) for the 256 / 224-row tiles; additionally staggered over the two waves of a SIMD (4) for
 // 128 x 256 (profiles/r4_lab: 3-8 % over issuing all at once, on every measured shape)
@@ -155,14 +156,19 @@ static int pipe_select(int f32, int pro, int cin, int64_t M, int Kout, int64_t r
   struct Cand { int bm; double unit; };
   const Cand cands[] = {{256, 1.0}, {224, 1.0}, {128, 1.25}};
   double best = 1e300;
+  int pbm = 256;
   for (const Cand& c : cands) {
     const int64_t tiles = ((M + c.bm - 1) / c.bm) * (Kout / 256);
     const double t = (double)((tiles + 255) / 256) * c.bm * c.unit;
     if (t < best - 1e-9) {
       best = t;
-      bm = c.bm;
+      pbm = c.bm;
     }
   }
+  // one block per CU and no split-K: small grids (ResNet-18 on 32 x 32 CIFAR reaches 2 tiles) stay
+  // on the single-stage kernel, which splits their K over otherwise idle CUs
+  if (((M + pbm - 1) / pbm) * (Kout / 256) < 96) return 0;
+  bm = pbm;
   bn = 256;
   return (bm == 128 ? 4 : 2) + 1;
 }
@@ -170,6 +176,7 @@ static int pipe_select(int f32, int pro, int cin, int64_t M, int Kout, int64_t r
 // ---- 2-D halo tiles for 3x3 / stride-1 / pad-1 convolutions (conv_igemm.hip HALO) ----------------
 // set_conv_halo(0) (tests): these convolutions through the im2col gather path too.
 static int g_halo_override = -1;   // dlmpi_ext set_conv_halo (tests)
+static int g_splitk_override = 0;   // dlmpi_ext set_conv_splitk (tests): > 0 forces that many K slices
 static bool halo_on() {
   static const int v = 1;
   return (g_halo_override >= 0 ? g_halo_override : v) != 0;
@@ -565,12 +572,17 @@ static int conv2d_fwd_impl(const at::Tensor& x, int N, int H, int W, int C, int 
   pick_tiles((int64_t)N * P * Q, K, (int64_t)R * S * C, C, bm, bn, pro != 0);
   if (a.f32) f32_tiles(bm, bn);
   const bool halo_ok = bm_req <= 0 && bn_req <= 0 && halo_eligible(a.f32, pro, C, R, S, stride, pad, P, Q);
-  const int pipe = bm_req <= 0 && bn_req <= 0 && !halo_first(halo_ok, K)
-                       ? pipe_select(a.f32, pro, C, (int64_t)N * P * Q, K, (int64_t)R * S * C, bm, bn) : 0;
+  int pipe = bm_req <= 0 && bn_req <= 0 && !halo_first(halo_ok, K)
+                 ? pipe_select(a.f32, pro, C, (int64_t)N * P * Q, K, (int64_t)R * S * C, bm, bn) : 0;
   const bool halo = !pipe && halo_ok;
   if (halo) halo_tiles(K, bm, bn);
   if (bm_req > 0) bm = bm_req;   // tests / experiments: force a tile shape
   if (bn_req > 0) bn = bn_req;
+  if (bn_req == 256) {   // 256-column tiles (128 x 256, 256 x 256) exist only as the pipelined 8-wave kernel
+    if (a.f32 || pro != 0 || C % 64 != 0 || (bm != 128 && bm != 256))
+      throw std::runtime_error("conv2d_fwd: 256-column tiles need bf16, no prologue, C % 64 == 0, 128 / 256 rows");
+    pipe = (bm == 128 ? 4 : 2) + 1;
+  }
   g_stream_ran = 0;
   {  // streaming 1x1 kernel (short reductions into wide, memory-bound outputs)
     const int64_t M = (int64_t)N * P * Q;
@@ -628,6 +640,7 @@ static int conv2d_fwd_impl(const at::Tensor& x, int N, int H, int W, int C, int 
   if (!pipe && (fin != nullptr || !a.stats) && bm_req <= 0 && bn_req <= 0) conv_plan(a, 0, bm, bn);
   if (fin != nullptr && (!a.stats || stats->size(0) < p.mtiles))
     throw std::runtime_error("conv2d_fwd_bn: stats [mtiles][2][K] required");
+  if (g_splitk_override > 0) a.splitk_req = g_splitk_override;
   check(dlmpi_conv_igemm_ex(&a, bm, bn, pipe, cur_stream()), "conv2d_fwd");
   if (fin != nullptr) {   // the BN finalize of these statistics
     at::Tensor ws = colsum_ws(*stats, p.mtiles, K);
@@ -696,6 +709,7 @@ at::Tensor conv2d_fwd_bnbwd(const at::Tensor& x, int N, int H, int W, int C, int
   finish_phase(p, N, C, bm, a.f32);
   at::Tensor stats = at::empty({(int64_t)p.mtiles, 2, (int64_t)K}, x.options().dtype(at::kFloat));
   a.stats = ptr<float>(stats);
+  if (g_splitk_override > 0) a.splitk_req = g_splitk_override;
   check(dlmpi_conv_igemm_ex(&a, bm, bn, pipe, cur_stream()), "conv2d_fwd_bnbwd");
   return stats;
 }
@@ -829,8 +843,9 @@ c10::optional<at::Tensor> conv2d_dgrad_pro(const at::Tensor& dy, int N, int P, i
   pick_tiles((int64_t)N * H * W / (stride * stride), C, (int64_t)R * S * K / (stride * stride), K, bm, bn, pro != 0);
   if (a.f32) f32_tiles(bm, bn);
   const bool halo_ok = halo_eligible(a.f32, pro, K, R, S, stride, pad, H, W) && P == H && Q == W;
-  const int pipe = halo_first(halo_ok, C) ? 0 : pipe_select(a.f32, pro, K, (int64_t)N * H * W / (stride * stride), C,
-                                                          (int64_t)R * S * K / (stride * stride), bm, bn);
+  const int pipe = halo_first(halo_ok, C) || g_pipe_dgrad_override == 0
+                       ? 0 : pipe_select(a.f32, pro, K, (int64_t)N * H * W / (stride * stride), C,
+                                         (int64_t)R * S * K / (stride * stride), bm, bn);
   const bool halo = !pipe && halo_ok;
   if (halo) halo_tiles(C, bm, bn);
   a.ntiles = ceil_div(C, bn);
@@ -875,6 +890,7 @@ c10::optional<at::Tensor> conv2d_dgrad_pro(const at::Tensor& dy, int N, int P, i
     stats = at::empty({(int64_t)tiles, (int64_t)a.nstat, (int64_t)C}, dy.options().dtype(at::kFloat));
     a.stats = ptr<float>(*stats);
   }
+  if (g_splitk_override > 0) a.splitk_req = g_splitk_override;
   check(dlmpi_conv_igemm_ex(&a, bm, bn, pipe, cur_stream()), "conv2d_dgrad");
   return stats;
 }
@@ -936,9 +952,9 @@ void convT2x2_fwd(const at::Tensor& x, int N, int H, int W, int Cin, int ldx, in
 // ---- deferred weight-gradient split reductions --------------------------------------------------
 // With set_wgrad_defer(1) (the engine backward) a weight gradient's split reduction is queued instead
 // of launched; wgrad_flush() -- the DDP reducer before each bucket launch, the engine at the end of its
-// backward, and a full queue (kWgradBatch entries) -- launches the queue as ONE batched kernel
-// (conv_wgrad.hip wgrad_reduce_batched: the same sums in the same order as dlmpi_wgrad_reduce's two
-// launches) on the current stream.  Queued entries keep their slab tensors alive; an entry queued on
+// backward, and a full queue (kWgradBatch entries) -- launches the queue as two batched kernels
+// (conv_wgrad.hip wgrad_reduce_batch_s1/s2: the same sums in the same order as dlmpi_wgrad_reduce's
+// two launches per gradient) on the current stream.  Queued entries keep their slab tensors alive; an entry queued on
 // another stream is ordered before the flush by an event, and its slab's reuse by recordStream.
 struct PendingReduce {
   at::Tensor ws;
@@ -947,6 +963,9 @@ struct PendingReduce {
 };
 static std::vector<PendingReduce> g_pending;
 static bool g_wgrad_defer = false;
+static int g_wgrad_batch = dlmpi::kWgradBatch;   // queue length that triggers a flush (A/B: set_wgrad_batch)
+static bool g_defer_direct = true;               // also queue the one-launch (G == 0) reductions (A/B)
+static bool g_wgrad_bypass = false;              // reduce the next weight gradients immediately, queue kept
 static int64_t g_reduce_launches = 0;   // reduction launches (either form), for tests / bench
 
 void wgrad_flush() {
@@ -966,12 +985,16 @@ void wgrad_flush() {
     c10::hip::HIPCachingAllocator::recordStream(p.ws.storage().data_ptr(), c10::hip::getCurrentHIPStream());
   }
   dlmpi::WgradReduceBatch b{};
+  bool two = false;
   for (size_t i = 0; i < g_pending.size(); ++i) {
-    b.e[b.n++] = g_pending[i].e;
-    if (b.n == dlmpi::kWgradBatch || i + 1 == g_pending.size()) {
+    const dlmpi::WgradReduceEntry& e = g_pending[i].e;
+    two |= e.splits > 1 && dlmpi_wgrad_reduce_groups(e.splits, e.total) > 0;
+    b.e[b.n++] = e;
+    if (b.n == g_wgrad_batch || i + 1 == g_pending.size()) {
       check(dlmpi_wgrad_reduce_batch(&b, cur), "wgrad_reduce_batch");
-      ++g_reduce_launches;
+      g_reduce_launches += two ? 2 : 1;
       b.n = 0;
+      two = false;
     }
   }
   g_pending.clear();
@@ -981,7 +1004,12 @@ void wgrad_flush() {
 static void wgrad_reduce_or_defer(const at::Tensor& ws, int splits, int G, int64_t wsz, int Ko, int T, int Cpad,
                                   int Creal, int Ko_real, at::Tensor& grad) {
   float* out = ptr<float>(grad);
-  if (!g_wgrad_defer) {
+  for (const auto& p : g_pending)   // a gradient accumulated twice: its first sum goes out first
+    if (p.e.out == out) {
+      wgrad_flush();
+      break;
+    }
+  if (!g_wgrad_defer || g_wgrad_bypass || (!g_defer_direct && !(splits > 1 && G > 0))) {
     check(dlmpi_wgrad_reduce(ptr<float>(ws), splits, Ko, T, Cpad, Creal, Ko_real, out, ptr<float>(ws) + (int64_t)splits * wsz,
                              (int)std::min<int64_t>(INT32_MAX, (int64_t)G * wsz), cur_stream()),
           "wgrad_reduce");
@@ -989,11 +1017,6 @@ static void wgrad_reduce_or_defer(const at::Tensor& ws, int splits, int G, int64
     return;
   }
   if (Ko_real == 0 || wsz == 0) return;
-  for (const auto& p : g_pending)   // a gradient accumulated twice: its first sum goes out first
-    if (p.e.out == out) {
-      wgrad_flush();
-      break;
-    }
   PendingReduce p{ws, cur_stream(), {}};
   p.e.ws = ptr<float>(ws);
   p.e.ws2 = G > 0 ? ptr<float>(ws) + (int64_t)splits * wsz : nullptr;
@@ -1005,10 +1028,11 @@ static void wgrad_reduce_or_defer(const at::Tensor& ws, int splits, int G, int64
   p.e.Cpad = Cpad;
   p.e.Creal = Creal;
   g_pending.push_back(std::move(p));
-  if ((int)g_pending.size() >= dlmpi::kWgradBatch) wgrad_flush();
+  if ((int)g_pending.size() >= g_wgrad_batch) wgrad_flush();
 }
 
 static int g_wgrad3_override = -1;   // dlmpi_ext set_wgrad3 (tests); -1: on
+static int g_wgrad3_blocks = 0;      // dlmpi_ext set_wgrad3_blocks (A/B): > 0 overrides the grid target
 static int g_wgrad3_ran = 0;         // 1 if the last weight gradient ran the 3x3 spatial-tile kernel
 
 void conv2d_wgrad_pro(const at::Tensor& dy, int lddy, int dyoff, int Ko, const at::Tensor& x, int N, int H, int W,
@@ -1061,7 +1085,7 @@ void conv2d_wgrad_pro(const at::Tensor& dy, int lddy, int dyoff, int Ko, const a
     // CUs to the main stream (measured, profiles/r3_wgrad3: ResNet-50 12,233 img/s at 256 blocks vs
     // 12,348 at 160; UNet-512 470 vs 466).
     const double macs = (double)N * H * W * Ko * 9.0 * C;
-    const int target = macs >= 64e9 ? 256 : 160;
+    const int target = g_wgrad3_blocks > 0 ? g_wgrad3_blocks : (macs >= 64e9 ? 256 : 160);
     const int kc = b.mtiles * b.ntiles;
     int splits = std::max(1, std::min(b.ntiles_pix, target / kc));
     b.tiles_per_split = ceil_div(b.ntiles_pix, splits);
@@ -1505,14 +1529,20 @@ void register_ops(pybind11::module& m) {
   m.def("dgrad_stream_last", []() { return g_dgrad_stream_ran; });
   m.def("set_conv_autotune", [](int mode) { g_autotune_override = mode; });
   m.def("set_wgrad3", [](int mode) { g_wgrad3_override = mode; });
+  m.def("set_wgrad3_blocks", [](int n) { g_wgrad3_blocks = n; });
   m.def("set_wgrad_defer", [](bool on) {
     if (!on) wgrad_flush();
     g_wgrad_defer = on;
   });
   m.def("wgrad_flush", &wgrad_flush);
+  m.def("set_wgrad_batch", [](int n) { g_wgrad_batch = n > 0 && n <= dlmpi::kWgradBatch ? n : dlmpi::kWgradBatch; });
+  m.def("set_defer_direct", [](int on) { g_defer_direct = on != 0; });
+  m.def("set_wgrad_bypass", [](bool on) { g_wgrad_bypass = on; });
   m.def("wgrad_pending", []() { return (int)g_pending.size(); });
   m.def("wgrad_reduce_launches", []() { return g_reduce_launches; });
   m.def("set_conv_halo", [](int mode) { g_halo_override = mode; });
+  m.def("set_conv_splitk", [](int n) { g_splitk_override = n; });
+  m.def("set_conv_pipe_dgrad", [](int mode) { g_pipe_dgrad_override = mode; });
   m.def("set_conv_pipe", [](int mode) { g_pipe_override = mode; });
   m.def("set_dgs_blocks", [](int n) { dlmpi_set_dgs_blocks(n); });
   m.def("dgs_blocks", []() { return dlmpi_dgs_blocks(); });

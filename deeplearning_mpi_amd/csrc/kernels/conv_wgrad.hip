@@ -447,12 +447,14 @@ static inline int reduce_groups(int splits, int64_t total) {
   return (int)(G < 1 ? 1 : G);
 }
 
-// Batched split reduction (one launch for up to kWgradBatch weight gradients that became ready
-// together; ops.cpp defers and flushes them).  Entry with G == 0: a block per 1024-float chunk sums
-// all splits in order (stage 2 reading the slabs directly).  G > 0: a block per (chunk, group g)
-// writes its group sum to ws2[g] (stage 1); the chunk's last-arriving block (a self-resetting
-// completion ticket) sums the G group sums in order (stage 2).  Every output gets the sums of
-// dlmpi_wgrad_reduce's two launches in the same order: bit-identical.
+// Batched split reduction (up to kWgradBatch weight gradients that became ready together; ops.cpp
+// queues and flushes them): stage 1 -- a block per (entry with G > 0, 1024-float chunk, group g)
+// writes the group sum to ws2[g]; stage 2 -- a block per (entry, chunk) sums the G group sums (or,
+// G == 0, the splits themselves) in order and accumulates into the gradient.  The same sums in the
+// same order as dlmpi_wgrad_reduce's two launches per gradient: bit-identical.  (A single launch with
+// a last-arriver ticket per chunk was measured 5x slower: every block's agent-scope release / acquire
+// fence writes back / invalidates its XCD's L2 -- and the L2 of the data-gradient kernel running
+// beside it.)
 __device__ __forceinline__ void reduce_store4(const WgradReduceEntry& e, int64_t i4, f32x4 v) {
   const int64_t TC = (int64_t)e.T * e.Cpad;
   const int64_t ko = i4 / TC;
@@ -466,52 +468,33 @@ __device__ __forceinline__ void reduce_store4(const WgradReduceEntry& e, int64_t
     if (c + k < e.Creal) o[c + k] += v[k];
 }
 
-__global__ __launch_bounds__(256) void wgrad_reduce_batched(const WgradReduceBatch b, int* __restrict__ tickets) {
+__global__ __launch_bounds__(256) void wgrad_reduce_batch_s1(const WgradReduceBatch b) {
   int k = 0;
-  while (k + 1 < b.n && (int)blockIdx.x >= b.e[k + 1].block0) ++k;
+  while (k + 1 < b.n && (int)blockIdx.x >= b.e[k + 1].block1) ++k;
   const WgradReduceEntry& e = b.e[k];
-  const int tid = threadIdx.x;
-  const int local = (int)blockIdx.x - e.block0;
-  if (e.G == 0) {
-    const int64_t i4 = ((int64_t)local * 256 + tid) * 4;
-    if (i4 >= e.total) return;
-    f32x4 s = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll 8
-    for (int z = 0; z < e.splits; ++z) s += *reinterpret_cast<const f32x4*>(e.ws + (int64_t)z * e.total + i4);
-    reduce_store4(e, i4, s);
-    return;
-  }
+  const int local = (int)blockIdx.x - e.block1;
   const int G = e.G, g = local % G, chunk = local / G;
   const int per = (e.splits + G - 1) / G;
   const int z0 = g * per, z1 = min(e.splits, z0 + per);
-  const int64_t i4 = ((int64_t)chunk * 256 + tid) * 4;
-  const bool in = i4 < e.total;
-  if (in) {
-    f32x4 s = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll 8
-    for (int z = z0; z < z1; ++z) s += *reinterpret_cast<const f32x4*>(e.ws + (int64_t)z * e.total + i4);
-    *reinterpret_cast<f32x4*>(e.ws2 + (int64_t)g * e.total + i4) = s;
-  }
-  __shared__ int last;
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (tid == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    last = __hip_atomic_fetch_add(tickets + e.tk0 + chunk, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == G - 1;
-  }
-  __syncthreads();
-  if (!last) return;
-  if (tid == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __hip_atomic_store(tickets + e.tk0 + chunk, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-  __syncthreads();
-  if (!in) return;
+  const int64_t i4 = ((int64_t)chunk * 256 + threadIdx.x) * 4;
+  if (i4 >= e.total) return;
   f32x4 s = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll 8
-  for (int gg = 0; gg < G; ++gg) s += *reinterpret_cast<const f32x4*>(e.ws2 + (int64_t)gg * e.total + i4);
+  for (int z = z0; z < z1; ++z) s += *reinterpret_cast<const f32x4*>(e.ws + (int64_t)z * e.total + i4);
+  *reinterpret_cast<f32x4*>(e.ws2 + (int64_t)g * e.total + i4) = s;
+}
+
+__global__ __launch_bounds__(256) void wgrad_reduce_batch_s2(const WgradReduceBatch b) {
+  int k = 0;
+  while (k + 1 < b.n && (int)blockIdx.x >= b.e[k + 1].block2) ++k;
+  const WgradReduceEntry& e = b.e[k];
+  const int64_t i4 = ((int64_t)((int)blockIdx.x - e.block2) * 256 + threadIdx.x) * 4;
+  if (i4 >= e.total) return;
+  const float* src = e.G > 0 ? e.ws2 : e.ws;
+  const int n = e.G > 0 ? e.G : e.splits;
+  f32x4 s = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll 8
+  for (int z = 0; z < n; ++z) s += *reinterpret_cast<const f32x4*>(src + (int64_t)z * e.total + i4);
   reduce_store4(e, i4, s);
 }
 
@@ -607,23 +590,21 @@ extern "C" hipError_t dlmpi_wgrad_reduce(const float* ws, int splits, int Ko, in
 extern "C" hipError_t dlmpi_wgrad_reduce_batch(WgradReduceBatch* b, hipStream_t s) {
   if (b->n <= 0) return hipSuccess;
   if (b->n > kWgradBatch) return hipErrorInvalidValue;
-  int64_t blocks = 0;
-  int tks = 0;
+  int64_t blocks1 = 0, blocks2 = 0;
   for (int i = 0; i < b->n; ++i) {
     WgradReduceEntry& e = b->e[i];
     if (e.total % 4 != 0 || e.Cpad % 8 != 0) return hipErrorInvalidValue;
     e.G = e.splits > 1 ? reduce_groups(e.splits, e.total) : 0;
     if (e.G > 0 && e.ws2 == nullptr) return hipErrorInvalidValue;
     const int64_t chunks = (e.total + 1023) / 1024;
-    e.block0 = (int)blocks;
-    e.tk0 = tks;
-    blocks += chunks * (e.G > 0 ? e.G : 1);
-    if (e.G > 0) tks += (int)chunks;
+    e.block1 = (int)blocks1;
+    e.block2 = (int)blocks2;
+    if (e.G > 0) blocks1 += chunks * e.G;
+    blocks2 += chunks;
   }
-  if (blocks == 0) return hipSuccess;
-  if (blocks > INT32_MAX || tks > 4096) return hipErrorInvalidValue;
-  int* tk = dlmpi_splitk_tickets(s, tks > 0 ? tks : 1);
-  if (tk == nullptr) return hipErrorOutOfMemory;
-  hipLaunchKernelGGL(wgrad_reduce_batched, dim3((unsigned)blocks), dim3(256), 0, s, *b, tk);
+  if (blocks1 > INT32_MAX || blocks2 > INT32_MAX) return hipErrorInvalidValue;
+  // entries without a stage 1 get block1 = the next entry's start (the lookup skips them)
+  if (blocks1 > 0) hipLaunchKernelGGL(wgrad_reduce_batch_s1, dim3((unsigned)blocks1), dim3(256), 0, s, *b);
+  if (blocks2 > 0) hipLaunchKernelGGL(wgrad_reduce_batch_s2, dim3((unsigned)blocks2), dim3(256), 0, s, *b);
   return hipGetLastError();
 }

@@ -211,8 +211,8 @@ struct WgradReduceEntry {
   float* out;                      // [Ko_real][T][Creal], accumulated
   int64_t total;                   // Ko * T * Cpad
   int splits, G, Ko_real, T, Cpad, Creal;
-  int block0;                      // first block of this entry in the batch grid
-  int tk0;                         // first completion ticket (G > 0: one per 1024-float chunk)
+  int block1;                      // first block of this entry in the stage-1 grid (G > 0)
+  int block2;                      // first block of this entry in the stage-2 grid
 };
 constexpr int kWgradBatch = 16;
 struct WgradReduceBatch {
@@ -244,8 +244,8 @@ hipError_t dlmpi_conv_wgrad(const dlmpi::WgradArgs* a, int bm, int bn, hipStream
 hipError_t dlmpi_wgrad_reduce(const float* ws, int splits, int Ko, int T, int Cpad, int Creal,
                               int Ko_real, float* out, float* ws2, int ws2_floats, hipStream_t s);
 int dlmpi_wgrad_reduce_groups(int splits, int64_t total);
-// up to kWgradBatch deferred reductions in one launch (block0 / tk0 filled in here); tickets: the
-// split-K completion tickets of stream s (self-resetting), at most 4096 used
+// up to kWgradBatch deferred reductions in two launches (stage 1 only if an entry has G > 0; G and the
+// block offsets are filled in here)
 hipError_t dlmpi_wgrad_reduce_batch(dlmpi::WgradReduceBatch* b, hipStream_t s);
 // 3x3 spatial-tile weight gradient: tile plan (KT x CT; 0 if the channel counts do not fit) + launch
 int dlmpi_wgrad3_plan(int Ko, int C, int* kt, int* ct);

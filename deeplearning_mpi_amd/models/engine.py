@@ -591,10 +591,15 @@ class S2DConvUnit(ConvUnit):
         K, R, S, CT = self.K, self.R, self.S, 4 * self.CS
         g2 = torch.empty(K * R * S * CT, dtype=be.dt, device=dz.device)
         be.fill_(g2, 0.0)
-        be.conv_wgrad(dz, x, R, S, 1, 0, g2, CT, K)
-        flush = getattr(be, "wgrad_flush", None)   # g2 is read right below: its reduction must have run
-        if flush is not None:
-            flush()
+        # g2 is read right below: its reduction runs now, on this stream (the queued ones stay queued)
+        bypass = getattr(be, "wgrad_bypass", None)
+        if bypass is not None:
+            bypass(True)
+        try:
+            be.conv_wgrad(dz, x, R, S, 1, 0, g2, CT, K)
+        finally:
+            if bypass is not None:
+                bypass(False)
         if self._gidx is None or self._gidx.device != dz.device:
             # grad[k][r][s][c] <- g2[k][r // 2][s // 2][((r % 2) * 2 + s % 2) * CS + c]
             k, r, s_, c = torch.meshgrid(torch.arange(K), torch.arange(self.R0), torch.arange(self.S0),
@@ -690,10 +695,13 @@ class _EngineFn(torch.autograd.Function):
                 mod._engine_backward(state, gout)
             finally:
                 side = getattr(be, "side_stream", None)
-                if side is not None:   # every parameter gradient is final before the optimizer runs
-                    torch.cuda.current_stream().wait_stream(side)
+                if side is not None:
+                    if defer is not None:   # the queue's tail on the side stream, beside the main
+                        with torch.cuda.stream(side):   # stream's last work (the stem's weight gradient)
+                            be.wgrad_flush()
+                    torch.cuda.current_stream().wait_stream(side)   # every gradient final before the optimizer
                 if defer is not None:
-                    defer(False)   # flushes the queue's tail on this stream
+                    defer(False)   # (flushes what is still queued -- nothing with a side stream)
             if prof is not None:
                 prof.disable()
             held = getattr(mod._be, "held", None)

@@ -233,6 +233,10 @@ class NativeBackend:
     def wgrad_flush(self):
         self.C.wgrad_flush()
 
+    def wgrad_bypass(self, on: bool):
+        """Reduce the next weight gradients right away (their consumer reads them next), queue kept."""
+        self.C.set_wgrad_bypass(bool(on))
+
     def conv_wgrad(self, dy, x, R, S, stride, pad, grad, Creal, Ko_real):
         dy, pa, ca, _, zb, zld, zoff = self._pro(dy)
         x, pb, sb, hb, _, _, _ = self._pro(x)
@@ -566,6 +570,9 @@ class RefBackend:
         pass
 
     def wgrad_flush(self):
+        pass
+
+    def wgrad_bypass(self, on: bool):
         pass
 
     def conv_wgrad(self, dy, x, R, S, stride, pad, grad, Creal, Ko_real):

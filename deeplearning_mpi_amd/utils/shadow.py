@@ -24,7 +24,7 @@ SKIP = frozenset({"maxpool_bwd", "cast_weights", "conv_mtiles", "materialize"})
 # fused ops whose inputs are engine objects the shadow cannot copy (engine.PendingApply): hidden, so
 # the engine takes the unfused path (the same values, op by op)
 # (wgrad_defer: the weight gradients are compared call by call, so their reductions must not queue)
-HIDDEN = frozenset({"conv_fwd_bn_apply", "wgrad_defer", "wgrad_flush"})
+HIDDEN = frozenset({"conv_fwd_bn_apply", "wgrad_defer", "wgrad_flush", "wgrad_bypass"})
 # positional index of the BN-partials buffer of ops that take it positionally
 STATS_ARG = {"conv_fwd_bn": 9}
 

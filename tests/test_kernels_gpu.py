@@ -98,8 +98,8 @@ def test_conv_dgrad(shape):
                                    (2, 17, 19, 64, 64, 3, 1, 1), (2, 16, 16, 32, 64, 3, 1, 1)])
 @pytest.mark.parametrize("bn", [0, 64, 256])
 def test_conv_fwd_256_row_tile(shape, bn):
-    """The 256x128 tile and the 8-wave 256x256 tile (chosen automatically for large grids) forced
-    on small shapes, incl. BN statistics partials and row/column remainders."""
+    """The 256x128 single-stage tile and the 256x256 tile (the pipelined 8-wave kernel) forced on small
+    shapes, incl. BN statistics partials and row/column remainders."""
     nb, rb = _be()
     N, H, W, Cin, K, R, s, p = shape
     if (bn == 64) != (K == 64) or (bn == 256 and Cin < 64):
@@ -125,8 +125,8 @@ def test_conv_fwd_256_row_tile(shape, bn):
 @pytest.mark.parametrize("shape", [(2, 20, 20, 64, 256, 1, 1, 0), (3, 9, 11, 128, 512, 1, 1, 0),
                                    (2, 16, 16, 256, 256, 3, 2, 1), (2, 17, 19, 64, 768, 3, 1, 1)])
 def test_conv_fwd_128x256_wide_tile(shape):
-    """The 8-wave 128x256 tile (chosen for short reductions into 256-multiple outputs) forced on
-    small shapes: forward with BN partials, row remainders, 3x3 / strided taps."""
+    """The 128x256 tile (the pipelined 8-wave kernel, conv_pipe_kernel) forced on small shapes: forward
+    with BN partials, row remainders, 3x3 / strided taps, and the residual + affine + ReLU epilogue."""
     nb, rb = _be()
     N, H, W, Cin, K, R, s, p = shape
     Cp, Kp = pad8(Cin), pad8(K)
@@ -203,6 +203,7 @@ def test_pipelined_conv_bit_identical_to_single_stage(shape):
         C.set_conv_stream(0)
         C.set_dgrad_stream(0)
         C.set_conv_autotune(0)
+        C.set_conv_splitk(1)   # the single-stage kernel would split small grids' K (another order)
         for mode in (0, 1, 1):
             C.set_conv_pipe(mode)
             y = _empty(N, P, Q, Kp)
@@ -215,6 +216,7 @@ def test_pipelined_conv_bit_identical_to_single_stage(shape):
     finally:
         for f in (C.set_conv_pipe, C.set_conv_halo, C.set_conv_stream, C.set_dgrad_stream, C.set_conv_autotune):
             f(-1)
+        C.set_conv_splitk(0)
     base, p1, p2 = out[0][0], out[1][0], out[1][1]
     assert torch.equal(p1[0], p2[0]) and torch.equal(p1[1], p2[1]) and torch.equal(p1[2], p2[2])
     assert torch.equal(p1[0], base[0]), "forward differs from the single-stage kernel"
@@ -332,7 +334,7 @@ def test_wgrad_reduce_batched_bit_identical():
     dfr, n_dfr = run(True)
     for i, (a, b) in enumerate(zip(imm, dfr)):
         assert torch.equal(a, b), i
-    assert n_dfr <= 3 < n_imm, (n_dfr, n_imm)
+    assert n_dfr <= 6 < n_imm, (n_dfr, n_imm)   # 3 flushes of at most 2 launches
 
 
 HALO_SHAPES = [
