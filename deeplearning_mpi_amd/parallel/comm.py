@@ -383,6 +383,11 @@ def _init(backend: str, timeout_s: float) -> Communicator:
     return RcclCommunicator(info, device, nc, control_group=store, budget=budget)
 
 
+# Measured by the one-GPU comm-load rehearsal (bench.py --rehearse, profiles/r4_commload): with a
+# modeled 8-rank ring all-reduce after every gradient bucket, 8 channels cost the step 1.7 % (ResNet-50)
+# / 2.1 % (ResNet-152) against the world-1 RCCL step -- the collective holds its CUs twice as long --
+# while 16 and 32 channels cost 0.6 / 0.4 % and 1.1 / 0.3 %: within noise of each other, and 16 is the
+# smallest budget at which the modeled collective is bus-bandwidth-, not channel-bound.
 DEFAULT_RCCL_CHANNELS = 16
 
 
@@ -394,9 +399,8 @@ def rccl_channel_budget() -> dict:
     channel count is a CU budget: ``DLMPI_RCCL_CHANNELS`` (default 16 = 1/16 of the 256 CUs; 0 =
     leave RCCL its own choice) is exported as ``NCCL_MAX_NCHANNELS`` before the communicator is
     created (RCCL reads it at ``ncclCommInitRank``).  An explicit ``NCCL_MAX_NCHANNELS`` in the
-    environment wins.  The default is chosen by the one-GPU comm-load rehearsal
-    (``bench.py --rehearse``, profiles/r4_commload): the backward slowdown of a channel-sized
-    workgroup load per all-reduce, measured for 8/16/32 channels.
+    environment wins.  The default (16) is the measured choice of the one-GPU comm-load rehearsal
+    (``bench.py --rehearse``, profiles/r4_commload; see DEFAULT_RCCL_CHANNELS).
 
     The persistent streaming data-gradient kernel (conv1x1_dgrad_stream.hip) splits its work
     statically over one block per CU of 100-160 KB of LDS: a block that cannot start because an
