@@ -181,10 +181,6 @@ def main():
         for k, v in pins.items():
             if k in setters:
                 getattr(_nat(), setters[k])(int(v))
-        if pins.get("unet_wmain") == "0":
-            from deeplearning_mpi_amd.models import unet as _unet
-
-            _unet.FIRST_WGRAD_MAIN = False
         if pins.get("defer") == "0":
             from deeplearning_mpi_amd.ops.backend import NativeBackend
 

@@ -24,10 +24,6 @@ from .engine import ConvTUnit, ConvUnit, EngineModule
 
 
 
-# UNet's input conv computes its weight gradient on the main stream at the end of the backward
-FIRST_WGRAD_MAIN = True
-
-
 class DoubleConv(nn.Module):
     def __init__(self, in_channels, out_channels):
         super().__init__()
@@ -135,9 +131,6 @@ class UNet(EngineModule):
         ups = [self.up_conv1, self.up_conv2, self.up_conv3, self.up_conv4]   # level 1..4
         self.enc = [d.double_conv.units(ar, cin_pad=self.cin_pad if k == 0 else None, need_dgrad=k != 0)
                     for k, d in enumerate(downs)]
-        # the input conv's weight gradient is the step's last: on the main stream, idle by then, beside
-        # the side stream's last 3x3 weight gradient (engine.WGRAD_TAIL_MAIN; profiles/r4_unet)
-        self.enc[0][0].wgrad_main = FIRST_WGRAD_MAIN
         self.bott = self.double_conv.units(ar)
         self.skip_ch = [64, 128, 256, 512]
         self.up_ch = [128, 256, 512, 1024]   # channels arriving from below at levels 1..4
