@@ -1,10 +1,10 @@
 #!/bin/bash
 # Comm-load rehearsal sweep: world-1 RCCL reducer (--rccl1) vs the modeled 8-rank
 # all-reduce load with 8 / 16 / 32 channels, ResNet-50 and ResNet-152, same box.  Output:
-# gpurun_out/r4_commload/
+# gpurun_out/commload/
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 cd "$R" && export HSA_ENABLE_IPC_MODE_LEGACY=0
-O=$R/gpurun_out/r4_commload; mkdir -p $O
+O=$R/gpurun_out/commload; mkdir -p $O
 for c in ${CONFIGS:-resnet50 resnet152}; do
   for v in rccl1 8 16 32; do
     if [ $v = rccl1 ]; then args="--rccl1 1 --breakdown 3"; else args="--rehearse $v"; fi

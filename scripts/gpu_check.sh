@@ -3,7 +3,7 @@
 # benches.  Every GPU step has its own time limit; the script stops at the first failure.
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 cd "$R" && export HSA_ENABLE_IPC_MODE_LEGACY=0
-O=$R/gpurun_out/r4_check${TAG:+_$TAG}; mkdir -p $O
+O=$R/gpurun_out/gpu_check${TAG:+_$TAG}; mkdir -p $O
 if [ -z "$NOLAB" ]; then
   timeout -k 10 300 ./benchmarks/conv_lab 3 ${SHAPES} > $O/lab.log 2>&1 || { echo lab failed; tail -5 $O/lab.log; exit 1; }
   echo "lab OK=$(grep -c ' OK ' $O/lab.log) BAD=$(grep -c ' BAD ' $O/lab.log)"

@@ -2,7 +2,7 @@
 # Kernel-trace profiles of the training step (rocprofv3 --kernel-trace --stats; no counters): one
 # per CONFIG (extra bench arguments: ARGS, e.g. --graph 0).  Digest on the CPU side with scripts/prof_summary.py and scripts/step_analysis.py.
 R=${GRAFT_REPO_ROOT:-$(pwd)}
-O=$R/gpurun_out/r4_prof${TAG:+_$TAG}; mkdir -p $O
+O=$R/gpurun_out/prof${TAG:+_$TAG}; mkdir -p $O
 export HSA_ENABLE_IPC_MODE_LEGACY=0
 cd /tmp && export TMPDIR=/tmp
 for c in ${CONFIGS:-unet512 resnet50}; do
