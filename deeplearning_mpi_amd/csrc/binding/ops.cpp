@@ -129,6 +129,10 @@ static void pick_tiles(int64_t M, int Kout, int64_t red, int cin, int& bm, int& 
   if (bn == 64 && n64 && (M + 255) / 256 >= 512 && (cin < 64 || (M >= (2 << 20) && red >= 576))) bm = 256;
   else if (Kout >= 256 && (red >= 2304 || (wide1x1 && red == cin && red >= bm256_min_red_1x1())) && ((M + 255) / 256) * nt >= bm256_min_tiles()) bm = 256;
   else if (tiles < 512) bm = 64;
+  // grids that do not fill the chip even with 64-row tiles (ResNet-18 on 32 x 32 CIFAR: 8-128 tiles):
+  // 64-wide output tiles too -- twice the blocks before split-K (the autotuner's choice on every such
+  // layer, forward and data gradient: +5 % CIFAR img/s, profiles/r4_cifar)
+  if (bm == 64 && bn == 128 && ((M + 63) / 64) * nt < 256) bn = 64;
 }
 
 // ---- pipelined 8-wave tiles (conv_igemm.hip conv_pipe_kernel) -----------------------------------
