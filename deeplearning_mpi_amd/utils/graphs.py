@@ -56,6 +56,20 @@ def _note_replay():
     REPLAYS += 1
 
 
+
+def _release_generator():
+    """A capture that failed inside ``torch.cuda.graph`` leaves the device's default generator marked as
+    capturing (its capture epilogue never ran): every later torch RNG call on the device then raises
+    "Offset increment outside graph capture".  An empty capture on a fresh stream runs the prologue /
+    epilogue pair again and clears the mark (tests/test_graphs_gpu.py checks torch RNG afterwards)."""
+    try:
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=torch.cuda.Stream(), capture_error_mode="thread_local"):
+            pass
+        del g
+    except Exception:   # noqa: BLE001 -- best effort: the eager fallback does not depend on it
+        pass
+
 class CapturedStep:
     def __init__(self, step_fn, warmup: int = 2, inputs=(), enabled: bool = True, comm=None):
         self.step_fn = step_fn
@@ -171,6 +185,8 @@ class CapturedStep:
         if err is None:   # this rank captured fine (its graph is dropped): nothing is stuck here
             self._stream = None
         torch.cuda.synchronize()
+        if err is not None:
+            _release_generator()
         self.graph = None
         self.enabled = False
         _note_replay()

@@ -153,6 +153,7 @@ def test_failed_capture_falls_back_to_eager():
         torch.cuda.synchronize()
         if inject:
             assert cs.graph is None and not cs.enabled and cs.capture_error is not None
+            torch.randn(8, device=DEV)   # the device's torch RNG still works after the failed capture
         return torch.stack(losses), [p.detach().clone() for p in list(m.parameters()) + list(m.buffers())]
 
     l1, p1 = run(False)
