@@ -66,3 +66,12 @@ def test_bench_rejects_world_size_mismatch():
                        env=_env(), capture_output=True, text=True, timeout=600)
     assert r.returncode != 0
     assert "--gpus 4 but the launcher started 2 ranks" in r.stderr
+
+
+def test_bench_kernel_pins_parse():
+    """--pin (A/B only) sets the extension's kernel-choice switches by name and runs the step."""
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "1", "--pin", "pipe=0,halo=0,wgrad_batch=8,defer=0",
+                        *SMALL], cwd=ROOT, env=_env(), capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    (j,) = _json_lines(r.stdout)
+    assert j["n_gpus"] == 1

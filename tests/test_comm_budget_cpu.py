@@ -1,0 +1,38 @@
+"""RCCL channel (CU) budget (parallel/comm.py rccl_channel_budget): the measured 16-channel default
+(profiles/r4_commload) is exported as NCCL_MAX_NCHANNELS, an explicit NCCL_MAX_NCHANNELS wins, 0
+leaves RCCL its own choice, and the streaming data-gradient grid is sized to the CUs left (a
+conservative 32 channels when RCCL's count is unknown; DLMPI_DGS_BLOCKS overrides)."""
+from deeplearning_mpi_amd.parallel.comm import DEFAULT_RCCL_CHANNELS, rccl_channel_budget
+
+
+def _clean(monkeypatch):
+    for k in ("DLMPI_RCCL_CHANNELS", "NCCL_MAX_NCHANNELS", "NCCL_MIN_NCHANNELS", "DLMPI_DGS_BLOCKS"):
+        monkeypatch.delenv(k, raising=False)
+
+
+def test_default_budget(monkeypatch):
+    _clean(monkeypatch)
+    b = rccl_channel_budget()
+    assert DEFAULT_RCCL_CHANNELS == 16
+    assert b["NCCL_MAX_NCHANNELS"] == "16" and b["dgrad_stream_blocks"] == 256 - 16
+
+
+def test_explicit_nccl_env_wins(monkeypatch):
+    _clean(monkeypatch)
+    monkeypatch.setenv("NCCL_MAX_NCHANNELS", "8")
+    monkeypatch.setenv("DLMPI_RCCL_CHANNELS", "32")
+    b = rccl_channel_budget()
+    assert b["NCCL_MAX_NCHANNELS"] == "8" and b["dgrad_stream_blocks"] == 248
+
+
+def test_rccl_own_choice_sizes_the_grid_conservatively(monkeypatch):
+    _clean(monkeypatch)
+    monkeypatch.setenv("DLMPI_RCCL_CHANNELS", "0")
+    b = rccl_channel_budget()
+    assert b["NCCL_MAX_NCHANNELS"] is None and b["dgrad_stream_blocks"] == 256 - 32
+
+
+def test_grid_override(monkeypatch):
+    _clean(monkeypatch)
+    monkeypatch.setenv("DLMPI_DGS_BLOCKS", "200")
+    assert rccl_channel_budget()["dgrad_stream_blocks"] == 200
