@@ -1089,7 +1089,10 @@ void conv2d_wgrad_pro(const at::Tensor& dy, int lddy, int dyoff, int Ko, const a
     // CUs to the main stream (measured, profiles/r3_wgrad3: ResNet-50 12,233 img/s at 256 blocks vs
     // 12,348 at 160; UNet-512 470 vs 466).
     const double macs = (double)N * H * W * Ko * 9.0 * C;
-    const int target = g_wgrad3_blocks > 0 ? g_wgrad3_blocks : (macs >= 64e9 ? 256 : 160);
+    // (UNet-size gradients: 224 blocks leave 32 CUs to the data-gradient chain's small kernels, which
+    // otherwise wait for the whole kernel -- UNet-512 +0.65 %, UNet-1024 +0.4 % over 256, 5 same-box
+    // pairs, profiles/r4_unet)
+    const int target = g_wgrad3_blocks > 0 ? g_wgrad3_blocks : (macs >= 64e9 ? 224 : 160);
     const int kc = b.mtiles * b.ntiles;
     int splits = std::max(1, std::min(b.ntiles_pix, target / kc));
     b.tiles_per_split = ceil_div(b.ntiles_pix, splits);
