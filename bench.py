@@ -256,14 +256,24 @@ def main():
         step()
         if i == 0:   # one eager step: weight-gradient reduction launches (graph replays issue none)
             red_per_step = _native().wgrad_reduce_launches() - red0
+    from deeplearning_mpi_amd.utils.profiler import ClockStamps
+
+    clk = ClockStamps(dev)   # in-kernel shader clock over the timed steps (two 32-wave stamp launches)
     comm.barrier()
     sync()
     t0 = time.perf_counter()
+    clk.start()
     for _ in range(args.steps):
         loss = step()
+    clk.stop()
     comm.barrier()
     sync()
     dt = time.perf_counter() - t0
+    clock = clk.summary()
+    myclk = torch.tensor([clock["sclk_mhz"] if clock else -1.0], dtype=torch.float64, device=dev)
+    allclk = torch.empty(world, dtype=torch.float64, device=dev)
+    comm.allgather(allclk, myclk)
+    sclk_per_rank = [round(float(v), 1) if v > 0 else None for v in allclk.cpu()]
     # every rank's own wall time: the job's number is the slowest rank (MAX), min/max go to the JSON
     mine = torch.tensor([dt], dtype=torch.float64, device=dev)
     allt = torch.empty(world, dtype=torch.float64, device=dev)
@@ -371,6 +381,7 @@ def main():
         "reducer": ddp.reducer is not None,
         "per_rank_ms_per_step": {"min": min(per_rank_ms), "max": max(per_rank_ms)},
         "comm_exposed_ms": bd_max["comm_exposed"] if bd_max else None,
+        "sclk_mhz_per_rank": sclk_per_rank,
     }
     if host_info is not None:
         dist_info["host_time"] = host_info
@@ -405,6 +416,8 @@ def main():
                        "parallelism": f"dp{world}", "backend": comm.backend, "device": dev.type,
                        "optimizer": optname, "hipgraph": bool(args.graph),
                        "final_loss": round(lossv, 4)},
+            "sclk_mhz": clock["sclk_mhz"] if clock else None,
+            "clock": clock,
             "dist": dist_info,
         }), flush=True)
     dl.destroy_distributed()

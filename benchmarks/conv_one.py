@@ -16,12 +16,16 @@ def main():
     ap.add_argument("--shape", default="16,64,64,512,512,3,1,1")
     ap.add_argument("--pass", dest="ps", default="fwd")
     ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--set", default="", help="extension setters for A/B: name=value,name=value")
     a = ap.parse_args()
     from deeplearning_mpi_amd.ops.act import Act, padc
     from deeplearning_mpi_amd.ops.backend import NativeBackend
 
     N, H, W, Cin, K, R, s, p = map(int, a.shape.split(","))
     be = NativeBackend("cuda")
+    for kv in filter(None, a.set.split(",")):
+        k, v = kv.split("=")
+        getattr(be.C, k)(int(v))
     dev = "cuda"
     Cp, Kp = padc(Cin), padc(K)
     P = (H + 2 * p - R) // s + 1

@@ -101,38 +101,28 @@ static int bm256_min_red_1x1() {
   return v;
 }
 
-static int bm_override() {   // experiments: force the M tile (64 | 128 | 256)
-  static int v = 0;
-  return v;
-}
-
 // cin: channel count of the GEMM's gathered operand
 static void pick_tiles(int64_t M, int Kout, int64_t red, int cin, int& bm, int& bn, bool pro = false,
                        bool wide1x1 = true) {
-  (void)pro;
   bn = Kout <= 64 ? 64 : 128;
   // 64 (mod 128) channels above 128 (the UNet's 192-channel top concat gradient): 64-wide tiles
   // cover them exactly instead of a half-empty last 128-wide tile (a third more MFMA work)
   if (Kout > 128 && Kout % 128 == 64) bn = 64;
   bm = 128;
-  if (bm_override()) {
-    bm = bm_override();
-    if (bm == 256 && bn != 128) bm = 128;
-    return;
-  }
   const int64_t nt = (Kout + bn - 1) / bn;
   const int64_t tiles = ((M + 127) / 128) * nt;
-  static const int n64 = 1;
   // 64-channel outputs: 256 x 64 tiles (4 x 1 waves of 64 x 64).  Measured (conv_bench): wins for
   // the small-channel stems (-13 % ResNet 7x7, -10 % UNet first conv) and the 4M-row UNet level-1
   // 3x3s (-4 %), loses 3-8 % on the 0.8M-row ResNet layer1 GEMMs -> only there.
-  if (bn == 64 && n64 && (M + 255) / 256 >= 512 && (cin < 64 || (M >= (2 << 20) && red >= 576))) bm = 256;
+  if (bn == 64 && (M + 255) / 256 >= 512 && (cin < 64 || (M >= (2 << 20) && red >= 576))) bm = 256;
   else if (Kout >= 256 && (red >= 2304 || (wide1x1 && red == cin && red >= bm256_min_red_1x1())) && ((M + 255) / 256) * nt >= bm256_min_tiles()) bm = 256;
   else if (tiles < 512) bm = 64;
   // grids that do not fill the chip even with 64-row tiles (ResNet-18 on 32 x 32 CIFAR: 8-128 tiles):
   // 64-wide output tiles too -- twice the blocks before split-K (the autotuner's choice on every such
-  // layer, forward and data gradient: +5 % CIFAR img/s, profiles/r4_cifar)
-  if (bm == 64 && bn == 128 && ((M + 63) / 64) * nt < 256) bn = 64;
+  // layer, forward and data gradient: +5 % CIFAR img/s, profiles/r4_cifar).  Not for fused BN-apply
+  // consumers (pro): their one output column is what lets column 0 alone store the applied input;
+  // two columns would each recompute the prologue (profiles/r3_fuse_apply_2col_rejected).
+  if (!pro && bm == 64 && bn == 128 && ((M + 63) / 64) * nt < 256) bn = 64;
 }
 
 // ---- pipelined 8-wave tiles (conv_igemm.hip conv_pipe_kernel) -----------------------------------
@@ -972,11 +962,16 @@ static bool g_defer_direct = true;               // also queue the one-launch (G
 static bool g_wgrad_bypass = false;              // reduce the next weight gradients immediately, queue kept
 static int64_t g_reduce_launches = 0;   // reduction launches (either form), for tests / bench
 
+// Launches the queue.  The queue is moved out first: if a launch throws midway, the batches already
+// launched are not launched (and added into the gradients) a second time by a later flush, and the
+// rest are dropped with the step that failed.
 void wgrad_flush() {
   if (g_pending.empty()) return;
+  std::vector<PendingReduce> pending;
+  pending.swap(g_pending);
   const hipStream_t cur = cur_stream();
   std::vector<hipStream_t> waited;
-  for (auto& p : g_pending) {
+  for (auto& p : pending) {
     if (p.s == cur) continue;
     if (std::find(waited.begin(), waited.end(), p.s) == waited.end()) {
       hipEvent_t ev;
@@ -990,18 +985,26 @@ void wgrad_flush() {
   }
   dlmpi::WgradReduceBatch b{};
   bool two = false;
-  for (size_t i = 0; i < g_pending.size(); ++i) {
-    const dlmpi::WgradReduceEntry& e = g_pending[i].e;
+  for (size_t i = 0; i < pending.size(); ++i) {
+    const dlmpi::WgradReduceEntry& e = pending[i].e;
     two |= e.splits > 1 && dlmpi_wgrad_reduce_groups(e.splits, e.total) > 0;
     b.e[b.n++] = e;
-    if (b.n == g_wgrad_batch || i + 1 == g_pending.size()) {
+    if (b.n == g_wgrad_batch || i + 1 == pending.size()) {
       check(dlmpi_wgrad_reduce_batch(&b, cur), "wgrad_reduce_batch");
       g_reduce_launches += two ? 2 : 1;
       b.n = 0;
       two = false;
     }
   }
+}
+
+// Drops the queue without launching it and turns deferral off: the backward that queued it failed
+// (e.g. a hipGraph capture torn down mid-backward: its slabs were never computed and its streams are
+// abandoned).  The engine's error path and CapturedStep's stream reset call it.
+void wgrad_discard() {
   g_pending.clear();
+  g_wgrad_defer = false;
+  g_wgrad_bypass = false;
 }
 
 // the split reduction of a weight gradient: ws = [splits + G][wsz] (G = dlmpi_wgrad_reduce_groups)
@@ -1092,7 +1095,8 @@ void conv2d_wgrad_pro(const at::Tensor& dy, int lddy, int dyoff, int Ko, const a
     // (UNet-size gradients: 224 blocks leave 32 CUs to the data-gradient chain's small kernels, which
     // otherwise wait for the whole kernel -- UNet-512 +0.65 %, UNet-1024 +0.4 % over 256, 5 same-box
     // pairs, profiles/r4_unet)
-    const int target = g_wgrad3_blocks > 0 ? g_wgrad3_blocks : (macs >= 64e9 ? 224 : 160);
+    // (64 x 64 tiles are 4-wave blocks, two per CU: twice the blocks for the same CUs)
+    const int target = (g_wgrad3_blocks > 0 ? g_wgrad3_blocks : (macs >= 64e9 ? 224 : 160)) * (kt == 64 && ct == 64 ? 2 : 1);
     const int kc = b.mtiles * b.ntiles;
     int splits = std::max(1, std::min(b.ntiles_pix, target / kc));
     b.tiles_per_split = ceil_div(b.ntiles_pix, splits);
@@ -1431,6 +1435,13 @@ void fill_(at::Tensor t, double v) {
   if (t.scalar_type() != at::kFloat || !t.is_contiguous()) throw std::runtime_error("fill_: contiguous fp32 tensor");
   check(dlmpi_fill_f32(ptr<float>(t), t.numel(), (float)v, cur_stream()), "fill");
 }
+// t: int64 [blocks][3] on the device (bench.py clock stamps)
+void clock_stamp(at::Tensor t) {
+  if (t.scalar_type() != at::kLong || !t.is_contiguous() || t.dim() != 2 || t.size(1) != 3)
+    throw std::runtime_error("clock_stamp: contiguous int64 [blocks][3]");
+  check(dlmpi_clock_stamp(reinterpret_cast<unsigned long long*>(t.data_ptr<int64_t>()), (int)t.size(0), cur_stream()),
+        "clock_stamp");
+}
 void add_i64_(at::Tensor t, int64_t v) {
   if (t.scalar_type() != at::kLong || !t.is_contiguous()) throw std::runtime_error("add_i64_: contiguous int64 tensor");
   check(dlmpi_add_i64(ptr<int64_t>(t), t.numel(), v, cur_stream()), "add_i64");
@@ -1537,11 +1548,15 @@ void register_ops(pybind11::module& m) {
   m.def("set_conv_autotune", [](int mode) { g_autotune_override = mode; });
   m.def("set_wgrad3", [](int mode) { g_wgrad3_override = mode; });
   m.def("set_wgrad3_blocks", [](int n) { g_wgrad3_blocks = n; });
+  m.def("set_wgrad3_var", [](int v) { dlmpi_wgrad3_set_var(v); });
+  m.def("set_wgrad_stages", [](int v) { dlmpi_wgrad_set_stages(v); });
   m.def("set_wgrad_defer", [](bool on) {
     if (!on) wgrad_flush();
     g_wgrad_defer = on;
   });
   m.def("wgrad_flush", &wgrad_flush);
+  m.def("wgrad_discard", &wgrad_discard);
+  m.def("clock_stamp", &clock_stamp);
   m.def("set_wgrad_batch", [](int n) { g_wgrad_batch = n > 0 && n <= dlmpi::kWgradBatch ? n : dlmpi::kWgradBatch; });
   m.def("set_defer_direct", [](int on) { g_defer_direct = on != 0; });
   m.def("set_wgrad_bypass", [](bool on) { g_wgrad_bypass = on; });

@@ -117,6 +117,23 @@ __device__ __forceinline__ float warp_max(float v) {
   return v;
 }
 
+// 16-byte LDS-DMA piece (global_load_lds_dwordx4) issued from inline asm, so the compiler does not
+// know it is in flight.  With the builtin, hipcc puts `s_waitcnt vmcnt(0)` in front of every
+// ds_read_b64_tr_b16 that follows a DMA issue (the transposing read carries no memory operand the
+// waitcnt pass could disambiguate), which drains every prefetch before the first fragment read of
+// the K-step: the weight-gradient kernels' double buffer hid no DMA latency at all.  Callers own
+// the wait (`s_waitcnt vmcnt(N)` + barrier before the stage is read) and must not mix this with
+// the builtin in one kernel (M0 is set here and nowhere tracked).  `lds` is the wave's 1 KB
+// destination (wave-uniform); lane i writes lds + 16 i.
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm"   // m0 is reserved: the clobber documents, it does not save
+__device__ __forceinline__ void glds16_raw(const void* g, const char* lds) {
+  const uint32_t l = __builtin_amdgcn_readfirstlane(
+      (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)lds);
+  asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(g), "s"(l) : "memory", "m0");
+}
+#pragma clang diagnostic pop
+
 // 4 KiB of zeros: out-of-bounds im2col / tile pieces load from here instead of branching
 // around the load (keeps the staging loads unconditional).
 static __device__ u32x4 g_zero_page[16] = {};

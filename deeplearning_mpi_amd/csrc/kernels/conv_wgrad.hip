@@ -57,8 +57,12 @@ __device__ __forceinline__ bf16x8 tr_frag(const char* tile, int k0, int cb, int 
 
 typedef __attribute__((address_space(3))) void lds_void;
 
+// RAW: issue through glds16_raw (common.h), invisible to the compiler's waitcnt pass -- the
+// double-buffered kernel owns its waits; single-stage kernels keep the builtin and __syncthreads.
+template <bool RAW>
 __device__ __forceinline__ void glds16(const void* g, char* lds_wave_base) {
-  __builtin_amdgcn_global_load_lds(g, (lds_void*)lds_wave_base, 16, 0, 0);
+  if constexpr (RAW) glds16_raw(g, lds_wave_base);
+  else __builtin_amdgcn_global_load_lds(g, (lds_void*)lds_wave_base, 16, 0, 0);
 }
 
 // Inverse of tr_off within a row: the chunk that lives at 16-B slot `pos` of row `row`.
@@ -88,7 +92,7 @@ void conv_wgrad_kernel(const WgradArgs a) {
   constexpr int A_ROW = BM * 2, B_ROW = BN * 2;          // bytes per LDS row
   constexpr int AL = BK * A_ROW / 4096, BL = BK * B_ROW / 4096;   // 16-B pieces per thread
   constexpr int A_BYTES = BK * A_ROW, B_BYTES = BK * B_ROW;
-  static_assert((PA == 0 && PB == 0) || STAGES == 1, "operand prologues: single-stage kernels");
+  constexpr bool RAW = STAGES == 2;
   constexpr int Z_BYTES = PA == 2 ? A_BYTES : 0;
   constexpr int SB = A_BYTES + B_BYTES + Z_BYTES;        // per stage: [A | B | Z]
   __shared__ __attribute__((aligned(16))) char smem[STAGES * SB];
@@ -154,9 +158,9 @@ void conv_wgrad_kernel(const WgradArgs a) {
       int row, ch;
       piece(i, A_ROW, row, ch);
       const int pix = pix0 + row, col = m0 + 8 * ch;
-      glds16(pick(pix < pend && col < a.Ko, dyb + (int64_t)pix * a.ldy + col), As + 16 * (256 * i + 64 * wid));
+      glds16<RAW>(pick(pix < pend && col < a.Ko, dyb + (int64_t)pix * a.ldy + col), As + 16 * (256 * i + 64 * wid));
       if constexpr (PA == 2)
-        glds16(pick(pix < pend && col < a.Ko, zb + (int64_t)pix * a.ldpz + col),
+        glds16<RAW>(pick(pix < pend && col < a.Ko, zb + (int64_t)pix * a.ldpz + col),
                As + A_BYTES + B_BYTES + 16 * (256 * i + 64 * wid));
     }
 #pragma unroll
@@ -167,7 +171,7 @@ void conv_wgrad_kernel(const WgradArgs a) {
       const int bp = b_pack[i];
       const bool ok = pix < pend && bp >= 0;
       if constexpr (DIRECT) {   // 1x1, stride 1, no padding: the input pixel IS the output pixel
-        glds16(pick(ok, xb + (int64_t)pix * a.ldx + (bp & 0xffff)), Bs + 16 * (256 * i + 64 * wid));
+        glds16<RAW>(pick(ok, xb + (int64_t)pix * a.ldx + (bp & 0xffff)), Bs + 16 * (256 * i + 64 * wid));
       } else {
         const uint32_t pp = ok ? (uint32_t)pix : 0u;
         const uint32_t n_img = fdiv(pp, a.fdPQ);
@@ -178,7 +182,7 @@ void conv_wgrad_kernel(const WgradArgs a) {
         const int iw = (int)q * a.stride_w + ((bp >> 24) & 255) - 64;
         const bool in = ok && (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W;
         const int64_t off = (((int64_t)n_img * a.H + ih) * a.W + iw) * a.ldx + (bp & 0xffff);
-        glds16(pick(in, xb + off), Bs + 16 * (256 * i + 64 * wid));
+        glds16<RAW>(pick(in, xb + off), Bs + 16 * (256 * i + 64 * wid));
       }
     }
   };
@@ -254,7 +258,13 @@ void conv_wgrad_kernel(const WgradArgs a) {
           }
         }
       }
-      __syncthreads();
+      if constexpr (RAW) {   // the rewritten stage is visible to every wave (no vmcnt: the next DMA flies)
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+      } else {
+        __syncthreads();
+      }
     }
   };
 
@@ -266,14 +276,23 @@ void conv_wgrad_kernel(const WgradArgs a) {
 
   if (nk > 0) {
     issue(0, pbeg);
-    __syncthreads();
-    prologue(0, pbeg);
+    if constexpr (!RAW) {
+      __syncthreads();
+      prologue(0, pbeg);
+    }
   }
   for (int ks = 0; ks < nk; ++ks) {
     int cur = 0;
     if constexpr (STAGES == 2) {
+      // double buffer, one barrier per K-step (two with a prologue): stage cur landed (own DMA:
+      // vmcnt(0); everyone's: the barrier); every wave's reads of stage cur ^ 1 (step ks - 1) have
+      // returned -> refill it now, so the DMA flies under this step's MFMAs
       cur = ks & 1;
+      asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
       if (ks + 1 < nk) issue(cur ^ 1, pbeg + (ks + 1) * BK);
+      prologue(cur, pbeg + ks * BK);
     } else if (ks > 0) {
       issue(0, pbeg + ks * BK);
       __syncthreads();
@@ -294,7 +313,7 @@ void conv_wgrad_kernel(const WgradArgs a) {
         for (int ni = 0; ni < TN; ++ni)
           acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[mi], bfr[ni], acc[mi][ni], 0, 0, 0);
     }
-    __syncthreads();
+    if constexpr (!RAW) __syncthreads();
   }
 
   // D[row = ko][col = tc]: lane holds col (lane&15), rows 4*(lane>>4) + r.
@@ -502,10 +521,31 @@ __global__ __launch_bounds__(256) void wgrad_reduce_batch_s2(const WgradReduceBa
 
 using namespace dlmpi;
 
+static int g_wgrad_stages = 1;   // A/B (lab): 2 = double-buffered raw-DMA kernels
+extern "C" void dlmpi_wgrad_set_stages(int st) { g_wgrad_stages = st == 2 ? 2 : 1; }
+
+template <int BM, int BN, int ST, int WR>
+static void launch_wg(const WgradArgs* a, dim3 g, hipStream_t s) {
+  const bool d = a->direct != 0;
+  const int m = (a->pro_a ? 2 : 0) | (a->pro_b ? 1 : 0);
+#define WG(D_, PA_, PB_) hipLaunchKernelGGL((conv_wgrad_kernel<BM, BN, ST, D_, PA_, PB_, WR>), g, dim3(256), 0, s, *a)
+  if (d) {
+    if (m == 0) WG(true, 0, 0);
+    else if (m == 2) WG(true, 2, 0);
+    else if (m == 1) WG(true, 0, 1);
+    else WG(true, 2, 1);
+  } else {
+    if (m == 0) WG(false, 0, 0);
+    else if (m == 2) WG(false, 2, 0);
+    else if (m == 1) WG(false, 0, 1);
+    else WG(false, 2, 1);
+  }
+#undef WG
+}
+
 extern "C" hipError_t dlmpi_conv_wgrad(const WgradArgs* a, int bm, int bn, hipStream_t s) {
   const unsigned nwg = (unsigned)(a->mtiles * a->ntiles * a->splits);
   if (nwg == 0) return hipSuccess;
-  static const int stages = 1;
   const dim3 g(nwg), b(256);
   if (a->f32) {
     if (bm != 64 || bn != 64 || a->ws == nullptr || a->pro_a || a->pro_b) return hipErrorInvalidValue;
@@ -513,53 +553,24 @@ extern "C" hipError_t dlmpi_conv_wgrad(const WgradArgs* a, int bm, int bn, hipSt
     else hipLaunchKernelGGL(conv_wgrad_f32_kernel<false>, g, b, 0, s, *a);
     return hipGetLastError();
   }
-  const bool d = a->direct != 0;
-  // 64 x 256, 1 x 4 waves (Ko <= 64 layers); prologue a (deferred BN-backward apply) or none
+  if ((a->pro_a != 0 && a->pro_a != 2) || (a->pro_b != 0 && a->pro_b != 1)) return hipErrorInvalidValue;
+  const bool two = g_wgrad_stages == 2;
+  // 64 x 256, 1 x 4 waves (Ko <= 64 layers)
   if (bm == 64 && bn == 256) {
-    if (a->pro_b != 0 || (a->pro_a != 0 && a->pro_a != 2) || stages != 1) return hipErrorInvalidValue;
-    if (a->pro_a == 2) {
-      if (d) hipLaunchKernelGGL((conv_wgrad_kernel<64, 256, 1, true, 2, 0, 1>), g, b, 0, s, *a);
-      else hipLaunchKernelGGL((conv_wgrad_kernel<64, 256, 1, false, 2, 0, 1>), g, b, 0, s, *a);
-    } else {
-      if (d) hipLaunchKernelGGL((conv_wgrad_kernel<64, 256, 1, true, 0, 0, 1>), g, b, 0, s, *a);
-      else hipLaunchKernelGGL((conv_wgrad_kernel<64, 256, 1, false, 0, 0, 1>), g, b, 0, s, *a);
-    }
+    if (a->pro_b != 0) return hipErrorInvalidValue;
+    if (two) launch_wg<64, 256, 2, 1>(a, g, s);
+    else launch_wg<64, 256, 1, 1>(a, g, s);
     return hipGetLastError();
   }
   // (a 128 x 256 variant was measured 1.3-1.9x slower: 2 waves/SIMD and register spills)
   if (bn != 128 || (bm != 128 && bm != 64)) return hipErrorInvalidValue;
-  if (a->pro_a != 0 || a->pro_b != 0) {
-    if ((a->pro_a != 0 && a->pro_a != 2) || (a->pro_b != 0 && a->pro_b != 1)) return hipErrorInvalidValue;
-    const int m = (a->pro_a ? 2 : 0) | (a->pro_b ? 1 : 0);
-#define LAUNCH_WGP(BM_, D_)                                                                             \
-  do {                                                                                                \
-    if (m == 2) hipLaunchKernelGGL((conv_wgrad_kernel<BM_, 128, 1, D_, 2, 0>), g, b, 0, s, *a);      \
-    else if (m == 1) hipLaunchKernelGGL((conv_wgrad_kernel<BM_, 128, 1, D_, 0, 1>), g, b, 0, s, *a); \
-    else hipLaunchKernelGGL((conv_wgrad_kernel<BM_, 128, 1, D_, 2, 1>), g, b, 0, s, *a);             \
-  } while (0)
-    if (bm == 128) {
-      if (d) LAUNCH_WGP(128, true);
-      else LAUNCH_WGP(128, false);
-    } else {
-      if (d) LAUNCH_WGP(64, true);
-      else LAUNCH_WGP(64, false);
-    }
-#undef LAUNCH_WGP
-    return hipGetLastError();
-  }
-#define LAUNCH_WG(BM_, ST_)                                                                  \
-  do {                                                                                     \
-    if (d) hipLaunchKernelGGL((conv_wgrad_kernel<BM_, 128, ST_, true>), g, b, 0, s, *a);   \
-    else hipLaunchKernelGGL((conv_wgrad_kernel<BM_, 128, ST_, false>), g, b, 0, s, *a);    \
-  } while (0)
   if (bm == 128) {
-    if (stages == 1) LAUNCH_WG(128, 1);
-    else LAUNCH_WG(128, 2);
+    if (two) launch_wg<128, 128, 2, 2>(a, g, s);
+    else launch_wg<128, 128, 1, 2>(a, g, s);
   } else {
-    if (stages == 1) LAUNCH_WG(64, 1);
-    else LAUNCH_WG(64, 2);
+    if (two) launch_wg<64, 128, 2, 2>(a, g, s);
+    else launch_wg<64, 128, 1, 2>(a, g, s);
   }
-#undef LAUNCH_WG
   return hipGetLastError();
 }
 

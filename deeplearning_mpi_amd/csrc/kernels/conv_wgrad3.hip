@@ -51,11 +51,15 @@ __device__ __forceinline__ int w3_halo_swz(int line, int col) {
   else return ((((col >> 1) & 1) | ((line & 1) << 1)) << 1);
 }
 
-template <int KT, int CT, int WR>
-__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 8)))
+// KT x CT block tile over WR x WC waves; every wave owns 64 (ko) x 16 (c) x 9 taps (144 fp32
+// accumulators): 4 dY fragments shared by the 9 taps, 1 X fragment per tap -- (64 + 9 x 16) rows of
+// transposed reads per 9 x 64 x 16 MACs.  128 x 64 = 2 x 4 waves, 64 x 128 = 1 x 8, 64 x 64 = 1 x 4
+// (a 4-wave block, 2 per CU: the 2 x 2 grid of 32 x 16 wave tiles it replaced read 1.7x the LDS
+// bytes per MFMA).
+template <int KT, int CT, int WR, int WC, int RAW = 1>
+__global__ __launch_bounds__(64 * WR * WC) __attribute__((amdgpu_waves_per_eu(2, 8)))
 void wgrad3x3_kernel(const Wgrad3Args a) {
-  constexpr int NT = 512;
-  constexpr int WC = 8 / WR;                  // wave grid WR (ko) x WC (c)
+  constexpr int NT = 64 * WR * WC;
   constexpr int WM = KT / WR, WN = CT / WC;   // per-wave ko x c
   constexpr int TM = WM / 16, TN = WN / 16;
   constexpr int A_ROW = KT * 2, B_ROW = CT * 2;
@@ -78,50 +82,54 @@ void wgrad3x3_kernel(const Wgrad3Args a) {
   const int t_beg = z * a.tiles_per_split;
   const int t_end = min(a.ntiles_pix, t_beg + a.tiles_per_split);
   const char* zp = reinterpret_cast<const char*>(g_zero_page);
+  const int H = a.H, W = a.W;
 
   // ---- per-thread staging pieces (fixed slot -> (row, chunk) map) --------------------------
-  int a_pi[AL], a_pj[AL], a_col[AL];          // dY: pixel (pi, pj) of the block, channel offset
+  // A piece: pixel (pi, pj) of the 8 x 8 block; B piece: halo (line, col) (line 10+: unused slot).
+  // The byte offset of a piece from its tile origin (pixel (h0, w0) of image n) is fixed per thread;
+  // per K-step only the origin (a scalar) and the bounds test change.
+  int a_pi[AL], a_pj[AL], a_off[AL];
 #pragma unroll
   for (int i = 0; i < AL; ++i) {
     const int o = NT * i + tid;
     const int row = (o * 16) / A_ROW, pos = (o * 16 % A_ROW) / 16;
     a_pi[i] = row >> 3;
     a_pj[i] = row & 7;
-    a_col[i] = a.dyoff + ko0 + 8 * (pos ^ w3_dy_swz<A_ROW>(row));
+    a_off[i] = 2 * ((a_pi[i] * W + a_pj[i]) * a.ldy + a.dyoff + ko0 + 8 * (pos ^ w3_dy_swz<A_ROW>(row)));
   }
-  int b_li[BL], b_co[BL], b_col[BL];          // X halo: line, col (line = -1: padding slot)
+  int b_li[BL], b_co[BL], b_off[BL];
 #pragma unroll
   for (int i = 0; i < BL; ++i) {
     const int o = NT * i + tid;
     const int row = (o * 16) / B_ROW, pos = (o * 16 % B_ROW) / 16;
     const int line = row / 10, col = row - line * 10;
-    b_li[i] = row < 100 ? line : -1000;
-    b_co[i] = col;
-    b_col[i] = a.xoff + c0 + 8 * (pos ^ w3_halo_swz<B_ROW>(line, col));
+    b_li[i] = row < 100 ? line - 1 : -1000;   // halo line / col relative to the tile origin
+    b_co[i] = col - 1;
+    b_off[i] = row < 100 ? 2 * ((b_li[i] * W + b_co[i]) * a.ldx + a.xoff + c0 + 8 * (pos ^ w3_halo_swz<B_ROW>(line, col))) : 0;
   }
-  const uint16_t* dyb = static_cast<const uint16_t*>(a.dy);
-  const uint16_t* xb = static_cast<const uint16_t*>(a.x);
-  const int H = a.H, W = a.W;
+  const char* dyb = static_cast<const char*>(a.dy);
+  const char* xb = static_cast<const char*>(a.x);
 
   auto issue = [&](int buf, int n, int h0, int w0) {
     char* As = smem + buf * SB;
     char* Bs = As + A_BYTES;
-    const int64_t img = (int64_t)n * H;
+    const int64_t pix = ((int64_t)n * H + h0) * W + w0;   // wave-uniform tile origin
+    const char* da = dyb + 2 * pix * a.ldy;
+    const char* db = xb + 2 * pix * a.ldx;
+    const int hl = H - h0, wl = W - w0;
 #pragma unroll
     for (int i = 0; i < AL; ++i) {
-      const int h = h0 + a_pi[i], w = w0 + a_pj[i];
-      const bool ok = h < H && w < W;
-      const uintptr_t src = reinterpret_cast<uintptr_t>(dyb + ((img + h) * W + w) * a.ldy + a_col[i]);
-      __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(ok ? src : reinterpret_cast<uintptr_t>(zp)),
-                                       (w3_lds_void*)(As + 16 * (NT * i + 64 * wid)), 16, 0, 0);
+      const bool ok = a_pi[i] < hl && a_pj[i] < wl;
+      const char* src = ok ? da + a_off[i] : zp;
+      if constexpr (RAW) glds16_raw(src, As + 16 * (NT * i + 64 * wid));
+      else __builtin_amdgcn_global_load_lds(src, (w3_lds_void*)(As + 16 * (NT * i + 64 * wid)), 16, 0, 0);
     }
 #pragma unroll
     for (int i = 0; i < BL; ++i) {
-      const int h = h0 - 1 + b_li[i], w = w0 - 1 + b_co[i];
-      const bool ok = (unsigned)h < (unsigned)H && (unsigned)w < (unsigned)W;
-      const uintptr_t src = reinterpret_cast<uintptr_t>(xb + ((img + h) * W + w) * a.ldx + b_col[i]);
-      __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(ok ? src : reinterpret_cast<uintptr_t>(zp)),
-                                       (w3_lds_void*)(Bs + 16 * (NT * i + 64 * wid)), 16, 0, 0);
+      const bool ok = (unsigned)(h0 + b_li[i]) < (unsigned)H && (unsigned)(w0 + b_co[i]) < (unsigned)W;
+      const char* src = ok ? db + b_off[i] : zp;
+      if constexpr (RAW) glds16_raw(src, Bs + 16 * (NT * i + 64 * wid));
+      else __builtin_amdgcn_global_load_lds(src, (w3_lds_void*)(Bs + 16 * (NT * i + 64 * wid)), 16, 0, 0);
     }
   };
 
@@ -175,7 +183,17 @@ void wgrad3x3_kernel(const Wgrad3Args a) {
       tj = 0;
       if (++ti == a.tiles_h) { ti = 0; ++n; }
     }
-    __syncthreads();   // stage cur landed (every wave's vmcnt(0) + barrier); stage cur^1 is free
+    // stage cur landed (this wave's DMA: vmcnt(0); every wave's: the barrier); every wave's reads of
+    // stage cur^1 (step t - 1) have returned (lgkmcnt(0)) -> it may be refilled.  The DMA is issued
+    // through glds16_raw, so no compiler wait drains it before the fragment reads below: it has the
+    // whole K-step to land.
+    if constexpr (RAW) {
+      asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+    } else {
+      __syncthreads();
+    }
     if (t + 1 < t_end) issue(cur ^ 1, n, ti * 8, tj * 8);
     const char* As = smem + cur * SB;
     const char* Bs = As + A_BYTES;
@@ -232,13 +250,24 @@ extern "C" int dlmpi_wgrad3_plan(int Ko, int C, int* kt, int* ct) {
   return 1;
 }
 
+static int g_w3var = 1;
+extern "C" void dlmpi_wgrad3_set_var(int v) { g_w3var = v; }
 extern "C" hipError_t dlmpi_wgrad3x3(const Wgrad3Args* a, int kt, int ct, hipStream_t s) {
   const unsigned nwg = (unsigned)(a->mtiles * a->ntiles * a->splits);
   if (nwg == 0) return hipSuccess;
-  const dim3 g(nwg), b(512);
-  if (kt == 128 && ct == 64) hipLaunchKernelGGL((wgrad3x3_kernel<128, 64, 2>), g, b, 0, s, *a);
-  else if (kt == 64 && ct == 128) hipLaunchKernelGGL((wgrad3x3_kernel<64, 128, 1>), g, b, 0, s, *a);
-  else if (kt == 64 && ct == 64) hipLaunchKernelGGL((wgrad3x3_kernel<64, 64, 2>), g, b, 0, s, *a);
-  else return hipErrorInvalidValue;
+  const dim3 g(nwg);
+  if (g_w3var == 0) {
+    if (kt == 128 && ct == 64) hipLaunchKernelGGL((wgrad3x3_kernel<128, 64, 2, 4, 0>), g, dim3(512), 0, s, *a);
+    else if (kt == 64 && ct == 128) hipLaunchKernelGGL((wgrad3x3_kernel<64, 128, 1, 8, 0>), g, dim3(512), 0, s, *a);
+    else if (kt == 64 && ct == 64) hipLaunchKernelGGL((wgrad3x3_kernel<64, 64, 2, 4, 0>), g, dim3(512), 0, s, *a);
+    else return hipErrorInvalidValue;
+    return hipGetLastError();
+  }
+  if (kt == 128 && ct == 64) hipLaunchKernelGGL((wgrad3x3_kernel<128, 64, 2, 4>), g, dim3(512), 0, s, *a);
+  else if (kt == 64 && ct == 128) hipLaunchKernelGGL((wgrad3x3_kernel<64, 128, 1, 8>), g, dim3(512), 0, s, *a);
+  else if (kt == 64 && ct == 64) {
+    if (g_w3var == 2) hipLaunchKernelGGL((wgrad3x3_kernel<64, 64, 2, 4>), g, dim3(512), 0, s, *a);
+    else hipLaunchKernelGGL((wgrad3x3_kernel<64, 64, 1, 4>), g, dim3(256), 0, s, *a);
+  } else return hipErrorInvalidValue;
   return hipGetLastError();
 }

@@ -240,6 +240,7 @@ hipError_t dlmpi_conv_igemm(const dlmpi::ConvArgs* a, int bm, int bn, hipStream_
 // C % 64 == 0, no prologue / halo / split); pipe = 0: dlmpi_conv_igemm
 hipError_t dlmpi_conv_igemm_ex(const dlmpi::ConvArgs* a, int bm, int bn, int pipe, hipStream_t s);
 hipError_t dlmpi_conv_wgrad(const dlmpi::WgradArgs* a, int bm, int bn, hipStream_t s);   // bn: 128 | 256
+void dlmpi_wgrad_set_stages(int st);   // A/B (lab): 1 single-stage, 2 double-buffered raw DMA
 // sum of split partials -> grad (accumulated), with channel un-padding and row limit
 hipError_t dlmpi_wgrad_reduce(const float* ws, int splits, int Ko, int T, int Cpad, int Creal,
                               int Ko_real, float* out, float* ws2, int ws2_floats, hipStream_t s);
@@ -250,6 +251,7 @@ hipError_t dlmpi_wgrad_reduce_batch(dlmpi::WgradReduceBatch* b, hipStream_t s);
 // 3x3 spatial-tile weight gradient: tile plan (KT x CT; 0 if the channel counts do not fit) + launch
 int dlmpi_wgrad3_plan(int Ko, int C, int* kt, int* ct);
 hipError_t dlmpi_wgrad3x3(const dlmpi::Wgrad3Args* a, int kt, int ct, hipStream_t s);
+void dlmpi_wgrad3_set_var(int v);   // A/B (lab): 0 = builtin DMA + __syncthreads, 1 = raw DMA
 
 // batch norm
 hipError_t dlmpi_bn_finalize(const float* partial, int ntiles, int C, double count, const float* gamma,
@@ -392,6 +394,8 @@ hipError_t dlmpi_conv1x1_dgrad_stream(const dlmpi::DgradStreamArgs* a, int bm, i
 // utilities (util.hip): fp32 fill, int64 add, indexed gather dst[i] (+)= src[idx[i]] (idx < 0: zero;
 // esize 2 | 4 bytes, accumulate: fp32 only)
 hipError_t dlmpi_fill_f32(float* p, int64_t n, float v, hipStream_t s);
+// out [blocks][3] uint64: {XCC id, s_memtime, s_memrealtime} per one-wave block (bench clock stamps)
+hipError_t dlmpi_clock_stamp(unsigned long long* out, int blocks, hipStream_t s);
 hipError_t dlmpi_add_i64(int64_t* p, int64_t n, int64_t v, hipStream_t s);
 hipError_t dlmpi_gather(void* dst, const void* src, const int64_t* idx, int64_t n, int esize, int accumulate,
                         hipStream_t s);

@@ -73,3 +73,23 @@ extern "C" hipError_t dlmpi_gather(void* dst, const void* src, const int64_t* id
     return hipErrorInvalidValue;
   return hipGetLastError();
 }
+
+// Clock stamp (bench.py sclk): `blocks` one-wave blocks; block b writes {XCC id, shader-clock counter
+// (s_memtime), 100 MHz reference counter (s_memrealtime)} to out[3 b ..].  Two stamps bracketing a
+// region give its mean shader clock per XCD: d(memtime) / d(realtime) x 100 MHz (MI355X_MICROARCH.md
+// DVFS item 6).  Blocks are dispatched round-robin over the 8 XCDs, so 32 blocks sample each a few
+// times.  Lanes 0-2 store one value each (vector stores of per-lane data).
+__global__ __launch_bounds__(64) void clock_stamp_kernel(unsigned long long* out) {
+  const int l = threadIdx.x;
+  const unsigned xcc = __builtin_amdgcn_s_getreg(20 | (3 << 11)) & 15u;   // hwreg(HW_REG_XCC_ID, 0, 4)
+  const unsigned long long t = __builtin_amdgcn_s_memtime();
+  const unsigned long long r = __builtin_amdgcn_s_memrealtime();
+  const unsigned long long v = l == 0 ? (unsigned long long)xcc : (l == 1 ? t : r);
+  if (l < 3) out[3 * blockIdx.x + l] = v;
+}
+
+extern "C" hipError_t dlmpi_clock_stamp(unsigned long long* out, int blocks, hipStream_t s) {
+  if (blocks <= 0) return hipSuccess;
+  hipLaunchKernelGGL(clock_stamp_kernel, dim3(blocks), dim3(64), 0, s, out);
+  return hipGetLastError();
+}

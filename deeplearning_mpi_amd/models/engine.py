@@ -693,13 +693,20 @@ class _EngineFn(torch.autograd.Function):
                 defer(True)
             try:
                 mod._engine_backward(state, gout)
-            finally:
+            except BaseException:
+                # a failed backward (e.g. a capture torn down inside it): its queued reductions point at
+                # slabs that were never computed and at abandoned streams -- drop them, never launch them
+                if defer is not None:
+                    be.wgrad_discard()
+                raise
+            try:
                 side = getattr(be, "side_stream", None)
                 if side is not None:
                     if defer is not None:   # the queue's tail on the side stream, beside the main
                         with torch.cuda.stream(side):   # stream's last work (the stem's weight gradient)
                             be.wgrad_flush()
                     torch.cuda.current_stream().wait_stream(side)   # every gradient final before the optimizer
+            finally:
                 if defer is not None:
                     defer(False)   # (flushes what is still queued -- nothing with a side stream)
             if prof is not None:

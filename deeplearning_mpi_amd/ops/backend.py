@@ -233,6 +233,10 @@ class NativeBackend:
     def wgrad_flush(self):
         self.C.wgrad_flush()
 
+    def wgrad_discard(self):
+        """Drop the queued reductions of a failed backward and turn deferral off."""
+        self.C.wgrad_discard()
+
     def wgrad_bypass(self, on: bool):
         """Reduce the next weight gradients right away (their consumer reads them next), queue kept."""
         self.C.set_wgrad_bypass(bool(on))
@@ -570,6 +574,9 @@ class RefBackend:
         pass
 
     def wgrad_flush(self):
+        pass
+
+    def wgrad_discard(self):
         pass
 
     def wgrad_bypass(self, on: bool):

@@ -113,9 +113,8 @@ class RcclCommunicator(Communicator):
         # the CUs this communicator's channels take are withheld from the persistent streaming
         # data-gradient grid for as long as it exists (rccl_channel_budget)
         self.budget = budget if budget is not None else rccl_channel_budget()
-        from .._ext import native
-
-        native().set_dgs_blocks(int(self.budget["dgrad_stream_blocks"]))
+        _LIVE_RCCL.append(self)
+        _apply_dgs_budget()
 
     def allreduce(self, t, op="sum"):
         self.c.allreduce(t, op, False)
@@ -161,9 +160,23 @@ class RcclCommunicator(Communicator):
     def destroy(self):
         self.c.destroy()
         self.control = None
-        from .._ext import native
+        if self in _LIVE_RCCL:
+            _LIVE_RCCL.remove(self)
+        _apply_dgs_budget()
 
-        native().set_dgs_blocks(0)
+
+# RCCL communicators alive in this process (bench --rccl1 builds one beside init_distributed's).  The
+# streaming data-gradient grid leaves room for the channels of every one of them: the smallest grid of
+# the live budgets, the default (0) once none is left -- destroying one communicator must not hand the
+# other's channels' CUs back to the persistent grid.
+_LIVE_RCCL = []
+
+
+def _apply_dgs_budget():
+    from .._ext import native
+
+    blocks = [int(c.budget["dgrad_stream_blocks"]) for c in _LIVE_RCCL]
+    native().set_dgs_blocks(min(blocks) if blocks else 0)
 
 
 def _make_torch_bucket_comm(group, world_size):

@@ -10,8 +10,9 @@ LOCAL_RANK, which collides across nodes on a shared filesystem; SURVEY.md §5.2 
 Loading uses ``torch.load(..., weights_only=True)`` and accepts either key style.
 
 Crash consistency: the sidecar records the SHA-256 of the weights file it belongs to.  A save keeps
-the previous sidecar as ``<path>.state.prev`` (it belongs to the weights still on disk), then puts
-the new sidecar and finally the new weights in place.  A crash anywhere in between leaves weights
+the previous sidecar as ``<path>.state.prev`` when it belongs to the weights still on disk (after an
+interrupted save it may not: then the existing ``.state.prev`` is kept), then puts the new sidecar
+and finally the new weights in place.  A crash anywhere in between leaves weights
 whose own sidecar is on disk under one of the two names, and ``load_checkpoint`` takes the one whose
 hash matches -- never new weights with an old optimizer state / epoch, and never an already trained
 checkpoint restarted from epoch 0.
@@ -35,6 +36,18 @@ def _sha256(path) -> str:
     return h.hexdigest()
 
 
+def _sidecar_matches(state_path, weights_path) -> bool:
+    """True if the sidecar belongs to the weights file on disk (or there are no weights, or the
+    sidecar predates the hash)."""
+    if not os.path.exists(weights_path):
+        return True
+    try:
+        want = torch.load(state_path, map_location="cpu", weights_only=True).get("weights_sha256")
+    except Exception:   # unreadable (torn) sidecar: never rotate it over a good one
+        return False
+    return want is None or want == _sha256(weights_path)
+
+
 def save_checkpoint(model, path, optimizer=None, extra=None, rank=None):
     if rank is None:
         from ..parallel.comm import get_comm
@@ -54,7 +67,10 @@ def save_checkpoint(model, path, optimizer=None, extra=None, rank=None):
             state["optimizer"] = optimizer.state_dict()
         state["weights_sha256"] = _sha256(tmp)
         torch.save(state, path + ".state.tmp")
-        if os.path.exists(path + ".state"):   # the resume state of the weights still on disk
+        # keep the resume state of the weights still on disk as .state.prev -- but only if .state IS
+        # theirs: after an interrupted save .state may belong to weights that never landed, and then
+        # the existing .state.prev is the one to keep
+        if os.path.exists(path + ".state") and _sidecar_matches(path + ".state", path):
             os.replace(path + ".state", path + ".state.prev")
         os.replace(path + ".state.tmp", path + ".state")   # sidecar before weights (module docstring)
     os.replace(tmp, path)

@@ -176,6 +176,7 @@ class CapturedStep:
         from .._ext import has_native, native
 
         if has_native():
+            native().wgrad_discard()   # reductions queued by a backward the failed capture cut short
             native().clear_hip_error()
 
     def _fall_back(self, err):

@@ -88,3 +88,51 @@ class StepTimer:
 
 def throughput(images: int, seconds: float) -> float:
     return images / max(seconds, 1e-12)
+
+
+class ClockStamps:
+    """Mean shader clock of a GPU region, measured in-kernel: ``start()`` and
+    ``stop()`` each launch a stamp kernel (util.hip clock_stamp_kernel: 32 one-wave blocks writing
+    {XCC id, s_memtime, s_memrealtime}) on the current stream; after a synchronisation ``summary()``
+    pairs the two stamps per XCD: clock = d(memtime) / d(realtime) x 100 MHz.  Reports the mean over
+    the XCDs and their min / max, or None where the native library is absent."""
+
+    BLOCKS = 32
+
+    def __init__(self, device):
+        from .._ext import has_native, native
+
+        self.C = native() if has_native() and torch.device(device).type == "cuda" else None
+        if self.C is not None:
+            self.buf = torch.zeros(2, self.BLOCKS, 3, dtype=torch.int64, device=device)
+
+    def start(self):
+        if self.C is not None:
+            self.C.clock_stamp(self.buf[0])
+
+    def stop(self):
+        if self.C is not None:
+            self.C.clock_stamp(self.buf[1])
+
+    def summary(self):
+        if self.C is None:
+            return None
+        b = self.buf.cpu().tolist()
+        first = [{}, {}]
+        for k in (0, 1):
+            for xcc, mt, rt in b[k]:
+                # per XCD: the earliest start stamp, the latest stop stamp
+                cur = first[k].get(xcc)
+                if cur is None or (rt < cur[1] if k == 0 else rt > cur[1]):
+                    first[k][xcc] = (mt, rt)
+        mhz = {}
+        for xcc, (mt0, rt0) in first[0].items():
+            if xcc in first[1]:
+                mt1, rt1 = first[1][xcc]
+                if rt1 > rt0:
+                    mhz[int(xcc)] = (mt1 - mt0) / (rt1 - rt0) * 100.0
+        if not mhz:
+            return None
+        v = list(mhz.values())
+        return {"sclk_mhz": round(sum(v) / len(v), 1), "sclk_mhz_min": round(min(v), 1),
+                "sclk_mhz_max": round(max(v), 1), "xcds": len(v)}

@@ -36,3 +36,30 @@ def test_grid_override(monkeypatch):
     _clean(monkeypatch)
     monkeypatch.setenv("DLMPI_DGS_BLOCKS", "200")
     assert rccl_channel_budget()["dgrad_stream_blocks"] == 200
+
+
+def test_destroying_one_communicator_keeps_the_other_ones_budget(monkeypatch):
+    """with two RCCL communicators alive (bench --rccl1 builds one beside
+    init_distributed's), destroying one must leave the streaming data-gradient grid sized for the
+    other's channels; the default grid comes back only when none is left."""
+    _clean(monkeypatch)
+    from deeplearning_mpi_amd._ext import native
+    from deeplearning_mpi_amd.parallel.bootstrap import LaunchInfo
+    from deeplearning_mpi_amd.parallel.comm import RcclCommunicator
+
+    class FakeNative:   # the raw communicator: only destroy() is used here
+        def destroy(self):
+            pass
+
+    info = LaunchInfo("single", 0, 1, 0, 1)
+    C = native()
+    a = RcclCommunicator(info, "cpu", FakeNative(), budget={"dgrad_stream_blocks": 240})
+    assert C.dgs_blocks() == 240
+    b = RcclCommunicator(info, "cpu", FakeNative(), budget={"dgrad_stream_blocks": 224})
+    assert C.dgs_blocks() == 224   # room for the channels of both
+    b.destroy()
+    assert C.dgs_blocks() == 240   # a's channels still hold their CUs
+    b.destroy()                    # idempotent
+    assert C.dgs_blocks() == 240
+    a.destroy()
+    assert C.dgs_blocks() == 256   # none left: the default grid

@@ -163,6 +163,63 @@ def test_failed_capture_falls_back_to_eager():
         assert torch.equal(a, b)
 
 
+def test_failed_capture_inside_backward_drops_queued_reductions():
+    """a capture that fails INSIDE the engine backward (here a host sync after the 6th
+    weight gradient, with the side stream on) leaves weight-gradient split reductions queued whose
+    slabs were never computed.  They must be dropped -- not flushed into the gradients of the eager
+    fallback step -- and deferral turned off: every step bit-identical to an all-eager run."""
+    from deeplearning_mpi_amd._ext import native
+
+    C = native()
+    batches = _cifar_batches(5, 31)
+
+    def run(inject):
+        torch.manual_seed(0)
+        m = resnet18(num_classes=10).to(DEV)
+        m.engine_setup(DEV)
+        m._be.aux_min_pixels = 0   # side stream on: the reductions queue there
+        be = m._be
+        orig = be.conv_wgrad
+        calls, seen = [0], []
+
+        def conv_wgrad(*a, **k):
+            orig(*a, **k)
+            if inject and torch.cuda.is_current_stream_capturing():
+                calls[0] += 1
+            if calls[0] == 6 and torch.cuda.is_current_stream_capturing():
+                seen.append(C.wgrad_pending())   # reductions queued when the capture dies
+                float(torch.ones(1, device=DEV).sum())   # refused while capturing
+
+        be.conv_wgrad = conv_wgrad
+        opt = _sgd(m)
+        x, y = batches[0][0].clone(), batches[0][1].clone()
+
+        def step():
+            opt.zero_grad()
+            loss = cross_entropy(m(x), y)
+            loss.backward()
+            opt.step()
+            return loss
+
+        cs = CapturedStep(step, warmup=2, inputs=(x, y), enabled=inject)
+        losses = []
+        for bx, by in batches:
+            cs.set_inputs(bx, by)
+            losses.append(cs().clone())
+        torch.cuda.synchronize()
+        if inject:
+            assert cs.graph is None and not cs.enabled and cs.capture_error is not None
+            assert seen and seen[0] > 0, seen
+        assert C.wgrad_pending() == 0
+        return torch.stack(losses), [p.detach().clone() for p in list(m.parameters()) + list(m.buffers())]
+
+    l1, p1 = run(False)
+    l2, p2 = run(True)
+    assert torch.equal(l1, l2), (l1, l2)
+    for a, b in zip(p1, p2):
+        assert torch.equal(a, b)
+
+
 def test_failed_capture_agreement_runs_on_reset_comm_stream():
     """with world_size > 1 the rank agreement after a failed capture is a collective on the
     communicator's stream -- a stream the failed capture had forked and left in capture mode.  The

@@ -139,3 +139,43 @@ def test_checkpoint_sidecar_survives_interrupted_save(tmp_path):
     save_checkpoint(m, p, extra={"next_epoch": 2}, rank=0)
     assert load_checkpoint(m2, p, map_location="cpu").get("next_epoch") == 2
     assert torch.equal(m2.weight, m.weight)
+
+
+def test_checkpoint_sidecar_survives_two_interrupted_saves(tmp_path):
+    """two saves interrupted in the same window (after the sidecar, before the weights)
+    must not rotate the first interrupted save's stale sidecar over the only one matching the weights
+    on disk: the load still resumes epoch 1's state, not epoch 0 with a fresh optimizer."""
+    import os
+
+    import torch
+
+    from deeplearning_mpi_amd.utils.checkpoint import load_checkpoint, save_checkpoint
+
+    m = torch.nn.Linear(4, 3)
+    p = str(tmp_path / "ck.pth")
+    save_checkpoint(m, p, extra={"next_epoch": 1}, rank=0)
+    orig = os.replace
+
+    def crash_on_weights(src, dst):
+        if dst == p:
+            raise KeyboardInterrupt("simulated crash")
+        return orig(src, dst)
+
+    for ep in (2, 3):
+        with torch.no_grad():
+            m.weight.add_(1.0)
+        os.replace = crash_on_weights
+        try:
+            save_checkpoint(m, p, extra={"next_epoch": ep}, rank=0)
+        except KeyboardInterrupt:
+            pass
+        finally:
+            os.replace = orig
+    m2 = torch.nn.Linear(4, 3)
+    with __import__("warnings").catch_warnings():
+        __import__("warnings").simplefilter("error")   # "no resume state matches" would be a failure
+        meta = load_checkpoint(m2, p, map_location="cpu")
+    assert meta.get("next_epoch") == 1
+    save_checkpoint(m, p, extra={"next_epoch": 4}, rank=0)
+    assert load_checkpoint(m2, p, map_location="cpu").get("next_epoch") == 4
+    assert torch.equal(m2.weight, m.weight)
