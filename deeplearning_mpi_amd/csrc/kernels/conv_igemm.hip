@@ -675,14 +675,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BM * BN <= 
 // The raw s_barrier (not __syncthreads, whose workgroup fence drains vmcnt to 0 and with it the
 // prefetch) is bracketed by "memory"-clobbering asm statements, so neither the fragment reads nor the
 // DMA issue can be moved across it.
-// VAR (issue placement / priority; A/B in benchmarks/conv_lab).  A K-step runs in 4 phases (K-half
-// kk, half of the A fragments); the next step's DMA is issued at: 0 = phase 0 (all of it, right after
-// the barrier); 1 = phase 0 for the lower half of the waves, phase 2 for the upper half (the two waves
-// of a SIMD then issue at different times); 2 = A pieces at phase 0, B pieces at phase 2; 3 = as 0
-// with s_setprio(1) around the MFMA clusters; 4 = A at phase 0 / B at phase 2 for the lower waves,
-// A at 1 / B at 3 for the upper waves.
+// VAR (issue placement, measured in benchmarks/conv_lab, profiles/r4_lab).  A K-step runs in 4 phases
+// (K-half kk, half of the A fragments); the next step's DMA is issued at: 2 = A pieces at phase 0, B
+// pieces at phase 2; 4 = A at phase 0 / B at phase 2 for the lower waves, A at 1 / B at 3 for the
+// upper waves (the two waves of a SIMD then issue at different times).  Issuing everything at phase 0,
+// staggering only by wave, and s_setprio around the MFMA clusters were 3-8 % slower and are gone.
 // BM need not be a multiple of the staging pass (224 = 2 x 7 fragments): rows past BM stage zeros.
-template <int BM, int BN, int WGM, int WGN, int STAGES, int VAR = 0>
+template <int BM, int BN, int WGM, int WGN, int STAGES, int VAR>
 __global__ __launch_bounds__(64 * WGM * WGN) __attribute__((amdgpu_waves_per_eu(2, 2))) void conv_pipe_kernel(const ConvArgs a) {
   constexpr int NW = WGM * WGN;
   constexpr int NT = 64 * NW;
@@ -839,11 +838,10 @@ __global__ __launch_bounds__(64 * WGM * WGN) __attribute__((amdgpu_waves_per_eu(
       for (int h = 0; h < 2; ++h) {
         // DMA issue points: phase p = (kk, half of the A fragments)
         const int p = kk * 2 + h;
+        static_assert(VAR == 2 || VAR == 4, "issue placement");
         bool doA, doB;
-        if constexpr (VAR == 1) doA = doB = p == (up ? 2 : 0);
-        else if constexpr (VAR == 2) { doA = p == 0; doB = p == 2; }
-        else if constexpr (VAR == 4) { doA = p == (up ? 1 : 0); doB = p == (up ? 3 : 2); }
-        else doA = doB = p == 0;
+        if constexpr (VAR == 2) { doA = p == 0; doB = p == 2; }
+        else { doA = p == (up ? 1 : 0); doB = p == (up ? 3 : 2); }
         if (more && (doA || doB)) {
           if (doA) issue_a(wr);
           if (doB) issue_b(wr);
@@ -853,14 +851,12 @@ __global__ __launch_bounds__(64 * WGM * WGN) __attribute__((amdgpu_waves_per_eu(
 #pragma unroll
         for (int q = 0; q < MH; ++q)
           if (h * MH + q < TM) af[q] = *reinterpret_cast<const bf16x8*>(As + a_row0 + (h * MH + q) * 16 * 128 + cb);
-        if constexpr (VAR == 3) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
         for (int q = 0; q < MH; ++q)
 #pragma unroll
           for (int ni = 0; ni < TN; ++ni)
             if (h * MH + q < TM)
               acc[h * MH + q][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[q], bfr[ni], acc[h * MH + q][ni], 0, 0, 0);
-        if constexpr (VAR == 3) __builtin_amdgcn_s_setprio(0);
       }
     }
     rd = rd + 1 == STAGES ? 0 : rd + 1;
@@ -885,8 +881,7 @@ static void launch_tile(const ConvArgs* a, dim3 grid, hipStream_t s) {
 // Slabs (fp32) and tickets come per stream role (bn.hip), so the
 // main and the branch stream can run split convolutions concurrently.
 static int splitk_plan(int tiles, int nk) {
-  static const int on = 1;
-  if (!on || tiles >= 256 || nk < 8) return 1;
+  if (tiles >= 256 || nk < 8) return 1;
   int S = (256 + tiles - 1) / tiles;
   S = S < nk / 4 ? S : nk / 4;
   S = S < 8 ? S : 8;
@@ -917,21 +912,15 @@ static hipError_t launch_f32(const ConvArgs* a, int bm, int bn, dim3 grid, hipSt
 // when the launch does not fit the kernel (channels, prologue, split, fp32).
 static hipError_t launch_pipe(const ConvArgs* a, int bm, int bn, int var, dim3 grid, hipStream_t s) {
   if (a->f32 || a->pro != 0 || a->C % 64 != 0 || a->halo || grid.y != 1) return hipErrorInvalidValue;
-#define LAUNCH_PIPE(BM_, BN_, WGM_, WGN_, ST_)                                                                        \
-  do {                                                                                                              \
-    if (var == 1) hipLaunchKernelGGL((conv_pipe_kernel<BM_, BN_, WGM_, WGN_, ST_, 1>), grid, dim3(512), 0, s, *a);  \
-    else if (var == 2) hipLaunchKernelGGL((conv_pipe_kernel<BM_, BN_, WGM_, WGN_, ST_, 2>), grid, dim3(512), 0, s, *a); \
-    else if (var == 3) hipLaunchKernelGGL((conv_pipe_kernel<BM_, BN_, WGM_, WGN_, ST_, 3>), grid, dim3(512), 0, s, *a); \
-    else if (var == 4) hipLaunchKernelGGL((conv_pipe_kernel<BM_, BN_, WGM_, WGN_, ST_, 4>), grid, dim3(512), 0, s, *a); \
-    else hipLaunchKernelGGL((conv_pipe_kernel<BM_, BN_, WGM_, WGN_, ST_, 0>), grid, dim3(512), 0, s, *a);           \
-  } while (0)
-  if (bm == 256 && bn == 256) LAUNCH_PIPE(256, 256, 2, 4, 2);
-  else if (bm == 224 && bn == 256) LAUNCH_PIPE(224, 256, 2, 4, 2);
-  else if (bm == 256 && bn == 128) LAUNCH_PIPE(256, 128, 4, 2, 3);
-  else if (bm == 128 && bn == 256) LAUNCH_PIPE(128, 256, 2, 4, 3);
-  else if (bm == 512 && bn == 64) LAUNCH_PIPE(512, 64, 8, 1, 2);
+  // the measured issue placement of each tile (profiles/r4_lab): VAR 2 for the 256 / 224 / 512-row
+  // tiles, VAR 4 for 128 x 256; the other placements are gone (var must name the tile's own)
+  if (var != (bm == 128 ? 4 : 2)) return hipErrorInvalidValue;
+  if (bm == 256 && bn == 256) hipLaunchKernelGGL((conv_pipe_kernel<256, 256, 2, 4, 2, 2>), grid, dim3(512), 0, s, *a);
+  else if (bm == 224 && bn == 256) hipLaunchKernelGGL((conv_pipe_kernel<224, 256, 2, 4, 2, 2>), grid, dim3(512), 0, s, *a);
+  else if (bm == 256 && bn == 128) hipLaunchKernelGGL((conv_pipe_kernel<256, 128, 4, 2, 3, 2>), grid, dim3(512), 0, s, *a);
+  else if (bm == 128 && bn == 256) hipLaunchKernelGGL((conv_pipe_kernel<128, 256, 2, 4, 3, 4>), grid, dim3(512), 0, s, *a);
+  else if (bm == 512 && bn == 64) hipLaunchKernelGGL((conv_pipe_kernel<512, 64, 8, 1, 2, 2>), grid, dim3(512), 0, s, *a);
   else return hipErrorInvalidValue;
-#undef LAUNCH_PIPE
   return hipGetLastError();
 }
 

@@ -521,8 +521,13 @@ __global__ __launch_bounds__(256) void wgrad_reduce_batch_s2(const WgradReduceBa
 
 using namespace dlmpi;
 
-static int g_wgrad_stages = 1;   // A/B (lab): 2 = double-buffered raw-DMA kernels
-extern "C" void dlmpi_wgrad_set_stages(int st) { g_wgrad_stages = st == 2 ? 2 : 1; }
+// Stages: the double-buffered kernel (2) for 1x1 gradients and for gathers over >= 100k pixels;
+// the single-stage kernel (3 blocks per CU) for the short strided gathers of the 14^2 / 7^2 ResNet
+// layers, where its occupancy hides more than the second stage (benchmarks/wgrad_lab.py,
+// profiles/r5_wgrad: 1x1s -5..-13 %, 56^2 stride-2 -14 %, 28^2 / 14^2 stride-2 +19-20 % with 2).
+// g_wgrad_stages (A/B): 0 = this rule, 1 / 2 = forced.
+static int g_wgrad_stages = 0;
+extern "C" void dlmpi_wgrad_set_stages(int st) { g_wgrad_stages = st == 1 || st == 2 ? st : 0; }
 
 template <int BM, int BN, int ST, int WR>
 static void launch_wg(const WgradArgs* a, dim3 g, hipStream_t s) {
@@ -554,7 +559,7 @@ extern "C" hipError_t dlmpi_conv_wgrad(const WgradArgs* a, int bm, int bn, hipSt
     return hipGetLastError();
   }
   if ((a->pro_a != 0 && a->pro_a != 2) || (a->pro_b != 0 && a->pro_b != 1)) return hipErrorInvalidValue;
-  const bool two = g_wgrad_stages == 2;
+  const bool two = g_wgrad_stages ? g_wgrad_stages == 2 : (a->direct != 0 || a->npix >= 100000);
   // 64 x 256, 1 x 4 waves (Ko <= 64 layers)
   if (bm == 64 && bn == 256) {
     if (a->pro_b != 0) return hipErrorInvalidValue;

@@ -1,11 +1,11 @@
 #!/bin/bash
 # Weight-gradient lab on the GPU box (benchmarks/wgrad_lab.py), optional GPU tests first.
-#   ARMS="new:;old:set_wgrad3_var=0" LABARGS="--only3x3" TESTS="-k wgrad" TAG=x bash scripts/wlab.sh
+#   ARMS="new:;old:set_wgrad3_var=0" LABARGS="--only3x3" TESTK="wgrad" TAG=x bash scripts/wlab.sh
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 cd "$R" && export HSA_ENABLE_IPC_MODE_LEGACY=0
 O=$R/gpurun_out/wlab${TAG:+_$TAG}; mkdir -p $O
-if [ -n "$TESTS" ]; then
-  timeout -k 10 600 python -u -m pytest tests -m gpu -q -x --timeout 120 --timeout-method thread $TESTS > $O/tests.log 2>&1
+if [ -n "$TESTK" ]; then
+  timeout -k 10 600 python -u -m pytest tests -m gpu -q -x --timeout 120 --timeout-method thread -k "$TESTK" > $O/tests.log 2>&1
   rc=$?; tail -1 $O/tests.log
   if [ $rc -ne 0 ]; then grep -E "^FAILED|^ERROR|Error" $O/tests.log | head -20; exit 1; fi
 fi
