@@ -4,7 +4,7 @@ extension setter configurations, in interleaved rounds (box drift hits every arm
 checked against the first (bitwise or to --tol) and the first against the fp32 reference once.
 
 python benchmarks/wgrad_lab.py [--net resnet50|unet512|all] [--only3x3] [--rounds 3] [--iters 20]
-       [--arms "base:;old:set_wgrad3_var=0;full:set_wgrad3_blocks=256"]
+       [--arms "base:;gen:set_wgrad3=0;full:set_wgrad3_blocks=256"]
 Arm syntax: name:setter=value,setter=value (setters of deeplearning_mpi_amd._C; restored to -1/0 after).
 """
 import argparse
@@ -18,7 +18,7 @@ import torch  # noqa: E402
 
 from conv_bench import resnet50_shapes, unet_shapes  # noqa: E402
 
-RESET = {"set_wgrad3_var": 1, "set_wgrad3_blocks": 0, "set_wgrad3": -1, "set_wgrad_stages": 0}
+RESET = {"set_wgrad3_blocks": 0, "set_wgrad3": -1}
 
 
 def parse_arms(spec):

@@ -1548,8 +1548,6 @@ void register_ops(pybind11::module& m) {
   m.def("set_conv_autotune", [](int mode) { g_autotune_override = mode; });
   m.def("set_wgrad3", [](int mode) { g_wgrad3_override = mode; });
   m.def("set_wgrad3_blocks", [](int n) { g_wgrad3_blocks = n; });
-  m.def("set_wgrad3_var", [](int v) { dlmpi_wgrad3_set_var(v); });
-  m.def("set_wgrad_stages", [](int v) { dlmpi_wgrad_set_stages(v); });
   m.def("set_wgrad_defer", [](bool on) {
     if (!on) wgrad_flush();
     g_wgrad_defer = on;

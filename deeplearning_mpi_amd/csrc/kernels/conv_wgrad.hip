@@ -57,12 +57,8 @@ __device__ __forceinline__ bf16x8 tr_frag(const char* tile, int k0, int cb, int 
 
 typedef __attribute__((address_space(3))) void lds_void;
 
-// RAW: issue through glds16_raw (common.h), invisible to the compiler's waitcnt pass -- the
-// double-buffered kernel owns its waits; single-stage kernels keep the builtin and __syncthreads.
-template <bool RAW>
 __device__ __forceinline__ void glds16(const void* g, char* lds_wave_base) {
-  if constexpr (RAW) glds16_raw(g, lds_wave_base);
-  else __builtin_amdgcn_global_load_lds(g, (lds_void*)lds_wave_base, 16, 0, 0);
+  __builtin_amdgcn_global_load_lds(g, (lds_void*)lds_wave_base, 16, 0, 0);
 }
 
 // Inverse of tr_off within a row: the chunk that lives at 16-B slot `pos` of row `row`.
@@ -73,9 +69,11 @@ __device__ __forceinline__ int tr_chunk(int row, int pos) {
 
 // Operands are staged global -> LDS with global_load_lds (no VGPR round trip): piece i of thread
 // tid fills the 16-B LDS slot 16*(256 i + tid), i.e. each wave writes 1 KB contiguously, and the
-// lane fetches whichever (pixel row, 16-B chunk) the swizzled layout puts there.  STAGES = 1:
-// single stage, two barriers per K-step, 32 KB LDS at BM = 128 -> several blocks per CU hide
-// the load latency of one another.
+// lane fetches whichever (pixel row, 16-B chunk) the swizzled layout puts there.  Single stage,
+// two barriers per K-step, 32 KB LDS at BM = 128 -> several blocks per CU hide the load latency of
+// one another.  (A double-buffered form with the DMA issued through glds16_raw ran the 1x1 weight
+// gradients 5-13 % faster in isolation but cost ResNet-50 0.6-0.8 % in the step: 64 KB of LDS per
+// block keep the data-gradient chain's streaming blocks off the CU, profiles/r5_wgrad.)
 // PA = 2: the dy operand is a deferred BN-backward apply (dz = k1 dy + k2 Z + k3, Z staged beside
 // dy); PB = 1: the x operand is a deferred BN-apply + ReLU (relu(x * scale + shift)).  Both are
 // rewritten in LDS once a stage has landed, in-range pieces only (padding / tails stay zero), with
@@ -83,8 +81,8 @@ __device__ __forceinline__ int tr_chunk(int row, int pos) {
 // WR: wave-grid rows (WR x 4/WR waves).  64 x 256 (Ko <= 64 layers: the whole Ko by 256 columns)
 // runs 1 x 4 waves of 64 x 64: 16 transposed-read pairs per 16 MFMAs instead of the 64 x 128 tile's
 // 12 per 8, and every dy row is staged once per 256 instead of per 128 columns.
-template <int BM, int BN, int STAGES, bool DIRECT, int PA = 0, int PB = 0, int WR = 2>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(STAGES == 1 && BN == 128 ? 3 : 2, 8)))
+template <int BM, int BN, bool DIRECT, int PA = 0, int PB = 0, int WR = 2>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BN == 128 ? 3 : 2, 8)))
 void conv_wgrad_kernel(const WgradArgs a) {
   constexpr int BK = 64;
   constexpr int WC = 4 / WR;                               // wave-grid columns
@@ -92,10 +90,9 @@ void conv_wgrad_kernel(const WgradArgs a) {
   constexpr int A_ROW = BM * 2, B_ROW = BN * 2;          // bytes per LDS row
   constexpr int AL = BK * A_ROW / 4096, BL = BK * B_ROW / 4096;   // 16-B pieces per thread
   constexpr int A_BYTES = BK * A_ROW, B_BYTES = BK * B_ROW;
-  constexpr bool RAW = STAGES == 2;
   constexpr int Z_BYTES = PA == 2 ? A_BYTES : 0;
   constexpr int SB = A_BYTES + B_BYTES + Z_BYTES;        // per stage: [A | B | Z]
-  __shared__ __attribute__((aligned(16))) char smem[STAGES * SB];
+  __shared__ __attribute__((aligned(16))) char smem[SB];
 
   const uint32_t ntile = (uint32_t)a.mtiles * a.ntiles;
   const uint32_t nwg = ntile * a.splits;
@@ -158,9 +155,9 @@ void conv_wgrad_kernel(const WgradArgs a) {
       int row, ch;
       piece(i, A_ROW, row, ch);
       const int pix = pix0 + row, col = m0 + 8 * ch;
-      glds16<RAW>(pick(pix < pend && col < a.Ko, dyb + (int64_t)pix * a.ldy + col), As + 16 * (256 * i + 64 * wid));
+      glds16(pick(pix < pend && col < a.Ko, dyb + (int64_t)pix * a.ldy + col), As + 16 * (256 * i + 64 * wid));
       if constexpr (PA == 2)
-        glds16<RAW>(pick(pix < pend && col < a.Ko, zb + (int64_t)pix * a.ldpz + col),
+        glds16(pick(pix < pend && col < a.Ko, zb + (int64_t)pix * a.ldpz + col),
                As + A_BYTES + B_BYTES + 16 * (256 * i + 64 * wid));
     }
 #pragma unroll
@@ -171,7 +168,7 @@ void conv_wgrad_kernel(const WgradArgs a) {
       const int bp = b_pack[i];
       const bool ok = pix < pend && bp >= 0;
       if constexpr (DIRECT) {   // 1x1, stride 1, no padding: the input pixel IS the output pixel
-        glds16<RAW>(pick(ok, xb + (int64_t)pix * a.ldx + (bp & 0xffff)), Bs + 16 * (256 * i + 64 * wid));
+        glds16(pick(ok, xb + (int64_t)pix * a.ldx + (bp & 0xffff)), Bs + 16 * (256 * i + 64 * wid));
       } else {
         const uint32_t pp = ok ? (uint32_t)pix : 0u;
         const uint32_t n_img = fdiv(pp, a.fdPQ);
@@ -182,7 +179,7 @@ void conv_wgrad_kernel(const WgradArgs a) {
         const int iw = (int)q * a.stride_w + ((bp >> 24) & 255) - 64;
         const bool in = ok && (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W;
         const int64_t off = (((int64_t)n_img * a.H + ih) * a.W + iw) * a.ldx + (bp & 0xffff);
-        glds16<RAW>(pick(in, xb + off), Bs + 16 * (256 * i + 64 * wid));
+        glds16(pick(in, xb + off), Bs + 16 * (256 * i + 64 * wid));
       }
     }
   };
@@ -258,13 +255,7 @@ void conv_wgrad_kernel(const WgradArgs a) {
           }
         }
       }
-      if constexpr (RAW) {   // the rewritten stage is visible to every wave (no vmcnt: the next DMA flies)
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
-        asm volatile("" ::: "memory");
-      } else {
-        __syncthreads();
-      }
+      __syncthreads();
     }
   };
 
@@ -276,29 +267,16 @@ void conv_wgrad_kernel(const WgradArgs a) {
 
   if (nk > 0) {
     issue(0, pbeg);
-    if constexpr (!RAW) {
-      __syncthreads();
-      prologue(0, pbeg);
-    }
+    __syncthreads();
+    prologue(0, pbeg);
   }
   for (int ks = 0; ks < nk; ++ks) {
-    int cur = 0;
-    if constexpr (STAGES == 2) {
-      // double buffer, one barrier per K-step (two with a prologue): stage cur landed (own DMA:
-      // vmcnt(0); everyone's: the barrier); every wave's reads of stage cur ^ 1 (step ks - 1) have
-      // returned -> refill it now, so the DMA flies under this step's MFMAs
-      cur = ks & 1;
-      asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-      asm volatile("" ::: "memory");
-      if (ks + 1 < nk) issue(cur ^ 1, pbeg + (ks + 1) * BK);
-      prologue(cur, pbeg + ks * BK);
-    } else if (ks > 0) {
+    if (ks > 0) {
       issue(0, pbeg + ks * BK);
       __syncthreads();
       prologue(0, pbeg + ks * BK);
     }
-    const char* As = smem + cur * SB;
+    const char* As = smem;
     const char* Bs = As + A_BYTES;
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
@@ -313,7 +291,7 @@ void conv_wgrad_kernel(const WgradArgs a) {
         for (int ni = 0; ni < TN; ++ni)
           acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[mi], bfr[ni], acc[mi][ni], 0, 0, 0);
     }
-    if constexpr (!RAW) __syncthreads();
+    __syncthreads();
   }
 
   // D[row = ko][col = tc]: lane holds col (lane&15), rows 4*(lane>>4) + r.
@@ -521,19 +499,11 @@ __global__ __launch_bounds__(256) void wgrad_reduce_batch_s2(const WgradReduceBa
 
 using namespace dlmpi;
 
-// Stages: the double-buffered kernel (2) for 1x1 gradients and for gathers over >= 100k pixels;
-// the single-stage kernel (3 blocks per CU) for the short strided gathers of the 14^2 / 7^2 ResNet
-// layers, where its occupancy hides more than the second stage (benchmarks/wgrad_lab.py,
-// profiles/r5_wgrad: 1x1s -5..-13 %, 56^2 stride-2 -14 %, 28^2 / 14^2 stride-2 +19-20 % with 2).
-// g_wgrad_stages (A/B): 0 = this rule, 1 / 2 = forced.
-static int g_wgrad_stages = 0;
-extern "C" void dlmpi_wgrad_set_stages(int st) { g_wgrad_stages = st == 1 || st == 2 ? st : 0; }
-
-template <int BM, int BN, int ST, int WR>
+template <int BM, int BN, int WR>
 static void launch_wg(const WgradArgs* a, dim3 g, hipStream_t s) {
   const bool d = a->direct != 0;
   const int m = (a->pro_a ? 2 : 0) | (a->pro_b ? 1 : 0);
-#define WG(D_, PA_, PB_) hipLaunchKernelGGL((conv_wgrad_kernel<BM, BN, ST, D_, PA_, PB_, WR>), g, dim3(256), 0, s, *a)
+#define WG(D_, PA_, PB_) hipLaunchKernelGGL((conv_wgrad_kernel<BM, BN, D_, PA_, PB_, WR>), g, dim3(256), 0, s, *a)
   if (d) {
     if (m == 0) WG(true, 0, 0);
     else if (m == 2) WG(true, 2, 0);
@@ -559,23 +529,16 @@ extern "C" hipError_t dlmpi_conv_wgrad(const WgradArgs* a, int bm, int bn, hipSt
     return hipGetLastError();
   }
   if ((a->pro_a != 0 && a->pro_a != 2) || (a->pro_b != 0 && a->pro_b != 1)) return hipErrorInvalidValue;
-  const bool two = g_wgrad_stages ? g_wgrad_stages == 2 : (a->direct != 0 || a->npix >= 100000);
   // 64 x 256, 1 x 4 waves (Ko <= 64 layers)
   if (bm == 64 && bn == 256) {
     if (a->pro_b != 0) return hipErrorInvalidValue;
-    if (two) launch_wg<64, 256, 2, 1>(a, g, s);
-    else launch_wg<64, 256, 1, 1>(a, g, s);
+    launch_wg<64, 256, 1>(a, g, s);
     return hipGetLastError();
   }
   // (a 128 x 256 variant was measured 1.3-1.9x slower: 2 waves/SIMD and register spills)
   if (bn != 128 || (bm != 128 && bm != 64)) return hipErrorInvalidValue;
-  if (bm == 128) {
-    if (two) launch_wg<128, 128, 2, 2>(a, g, s);
-    else launch_wg<128, 128, 1, 2>(a, g, s);
-  } else {
-    if (two) launch_wg<64, 128, 2, 2>(a, g, s);
-    else launch_wg<64, 128, 1, 2>(a, g, s);
-  }
+  if (bm == 128) launch_wg<128, 128, 2>(a, g, s);
+  else launch_wg<64, 128, 2>(a, g, s);
   return hipGetLastError();
 }
 

@@ -6,7 +6,9 @@
 // K-step and gathers X once per (pixel, tap): every X element is fetched 9 times per Ko tile and
 // every K-step pays a per-lane im2col decode.  Here a K-step is an 8 x 8 block of output pixels of
 // one image: its dY rows [64][KT] and the 10 x 10 X halo around it [100][CT] are staged once
-// (global_load_lds, double-buffered), and all 9 taps are 9 GEMMs over the SAME staged tiles --
+// (LDS-DMA, double-buffered: the next block's DMA is issued right after the K-step's barrier through
+// glds16_raw, so the compiler adds no drain before the transposed reads -- with the builtin it did,
+// and no DMA latency was hidden: profiles/r5_wgrad), and all 9 taps are 9 GEMMs over the SAME staged tiles --
 // tap (r, s) reads the halo window shifted by (r, s).  Out-of-image halo pixels are staged as
 // zeros, which IS the zero padding for every tap, so no per-tap masking exists anywhere.  The
 // block owns dW for all 9 taps of a KT x CT (ko, c) tile: 9 x (KT x CT) fp32 accumulators over 8
@@ -32,7 +34,6 @@
 namespace dlmpi {
 
 typedef __attribute__((address_space(3))) i16x4 w3_lds_i16x4;
-typedef __attribute__((address_space(3))) void w3_lds_void;
 
 // 16-byte chunk XOR of a row holding 8 consecutive output pixels (dY tile: row = pixel k of the
 // 8 x 8 block, a half-wave reads rows k0 + q, k0 + 8 + q, q < 4)
@@ -56,7 +57,7 @@ __device__ __forceinline__ int w3_halo_swz(int line, int col) {
 // transposed reads per 9 x 64 x 16 MACs.  128 x 64 = 2 x 4 waves, 64 x 128 = 1 x 8, 64 x 64 = 1 x 4
 // (a 4-wave block, 2 per CU: the 2 x 2 grid of 32 x 16 wave tiles it replaced read 1.7x the LDS
 // bytes per MFMA).
-template <int KT, int CT, int WR, int WC, int RAW = 1>
+template <int KT, int CT, int WR, int WC>
 __global__ __launch_bounds__(64 * WR * WC) __attribute__((amdgpu_waves_per_eu(2, 8)))
 void wgrad3x3_kernel(const Wgrad3Args a) {
   constexpr int NT = 64 * WR * WC;
@@ -121,15 +122,13 @@ void wgrad3x3_kernel(const Wgrad3Args a) {
     for (int i = 0; i < AL; ++i) {
       const bool ok = a_pi[i] < hl && a_pj[i] < wl;
       const char* src = ok ? da + a_off[i] : zp;
-      if constexpr (RAW) glds16_raw(src, As + 16 * (NT * i + 64 * wid));
-      else __builtin_amdgcn_global_load_lds(src, (w3_lds_void*)(As + 16 * (NT * i + 64 * wid)), 16, 0, 0);
+      glds16_raw(src, As + 16 * (NT * i + 64 * wid));
     }
 #pragma unroll
     for (int i = 0; i < BL; ++i) {
       const bool ok = (unsigned)(h0 + b_li[i]) < (unsigned)H && (unsigned)(w0 + b_co[i]) < (unsigned)W;
       const char* src = ok ? db + b_off[i] : zp;
-      if constexpr (RAW) glds16_raw(src, Bs + 16 * (NT * i + 64 * wid));
-      else __builtin_amdgcn_global_load_lds(src, (w3_lds_void*)(Bs + 16 * (NT * i + 64 * wid)), 16, 0, 0);
+      glds16_raw(src, Bs + 16 * (NT * i + 64 * wid));
     }
   };
 
@@ -187,13 +186,9 @@ void wgrad3x3_kernel(const Wgrad3Args a) {
     // stage cur^1 (step t - 1) have returned (lgkmcnt(0)) -> it may be refilled.  The DMA is issued
     // through glds16_raw, so no compiler wait drains it before the fragment reads below: it has the
     // whole K-step to land.
-    if constexpr (RAW) {
-      asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-      asm volatile("" ::: "memory");
-    } else {
-      __syncthreads();
-    }
+    asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
     if (t + 1 < t_end) issue(cur ^ 1, n, ti * 8, tj * 8);
     const char* As = smem + cur * SB;
     const char* Bs = As + A_BYTES;
@@ -250,24 +245,13 @@ extern "C" int dlmpi_wgrad3_plan(int Ko, int C, int* kt, int* ct) {
   return 1;
 }
 
-static int g_w3var = 1;
-extern "C" void dlmpi_wgrad3_set_var(int v) { g_w3var = v; }
 extern "C" hipError_t dlmpi_wgrad3x3(const Wgrad3Args* a, int kt, int ct, hipStream_t s) {
   const unsigned nwg = (unsigned)(a->mtiles * a->ntiles * a->splits);
   if (nwg == 0) return hipSuccess;
   const dim3 g(nwg);
-  if (g_w3var == 0) {
-    if (kt == 128 && ct == 64) hipLaunchKernelGGL((wgrad3x3_kernel<128, 64, 2, 4, 0>), g, dim3(512), 0, s, *a);
-    else if (kt == 64 && ct == 128) hipLaunchKernelGGL((wgrad3x3_kernel<64, 128, 1, 8, 0>), g, dim3(512), 0, s, *a);
-    else if (kt == 64 && ct == 64) hipLaunchKernelGGL((wgrad3x3_kernel<64, 64, 2, 4, 0>), g, dim3(512), 0, s, *a);
-    else return hipErrorInvalidValue;
-    return hipGetLastError();
-  }
   if (kt == 128 && ct == 64) hipLaunchKernelGGL((wgrad3x3_kernel<128, 64, 2, 4>), g, dim3(512), 0, s, *a);
   else if (kt == 64 && ct == 128) hipLaunchKernelGGL((wgrad3x3_kernel<64, 128, 1, 8>), g, dim3(512), 0, s, *a);
-  else if (kt == 64 && ct == 64) {
-    if (g_w3var == 2) hipLaunchKernelGGL((wgrad3x3_kernel<64, 64, 2, 4>), g, dim3(512), 0, s, *a);
-    else hipLaunchKernelGGL((wgrad3x3_kernel<64, 64, 1, 4>), g, dim3(256), 0, s, *a);
-  } else return hipErrorInvalidValue;
+  else if (kt == 64 && ct == 64) hipLaunchKernelGGL((wgrad3x3_kernel<64, 64, 1, 4>), g, dim3(256), 0, s, *a);
+  else return hipErrorInvalidValue;
   return hipGetLastError();
 }

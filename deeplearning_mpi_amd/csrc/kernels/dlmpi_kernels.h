@@ -240,7 +240,6 @@ hipError_t dlmpi_conv_igemm(const dlmpi::ConvArgs* a, int bm, int bn, hipStream_
 // C % 64 == 0, no prologue / halo / split); pipe = 0: dlmpi_conv_igemm
 hipError_t dlmpi_conv_igemm_ex(const dlmpi::ConvArgs* a, int bm, int bn, int pipe, hipStream_t s);
 hipError_t dlmpi_conv_wgrad(const dlmpi::WgradArgs* a, int bm, int bn, hipStream_t s);   // bn: 128 | 256
-void dlmpi_wgrad_set_stages(int st);   // A/B (lab): 0 the size rule, 1 single-stage, 2 double-buffered
 // sum of split partials -> grad (accumulated), with channel un-padding and row limit
 hipError_t dlmpi_wgrad_reduce(const float* ws, int splits, int Ko, int T, int Cpad, int Creal,
                               int Ko_real, float* out, float* ws2, int ws2_floats, hipStream_t s);
@@ -251,7 +250,6 @@ hipError_t dlmpi_wgrad_reduce_batch(dlmpi::WgradReduceBatch* b, hipStream_t s);
 // 3x3 spatial-tile weight gradient: tile plan (KT x CT; 0 if the channel counts do not fit) + launch
 int dlmpi_wgrad3_plan(int Ko, int C, int* kt, int* ct);
 hipError_t dlmpi_wgrad3x3(const dlmpi::Wgrad3Args* a, int kt, int ct, hipStream_t s);
-void dlmpi_wgrad3_set_var(int v);   // A/B (lab): 0 = builtin DMA + __syncthreads, 1 = raw DMA
 
 // batch norm
 hipError_t dlmpi_bn_finalize(const float* partial, int ntiles, int C, double count, const float* gamma,
