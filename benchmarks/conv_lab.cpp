@@ -61,7 +61,7 @@ static void halo_geom(int P, int Q, int bm, int& th, int& tw, int& tiles_h, int&
 
 // forward-conv ConvArgs for tile bm x bn (halo: 2-D tiles, bm must be 128)
 static ConvArgs make_args(const Shape& s, const uint16_t* x, const uint16_t* w, uint16_t* y, float* stats, int bm,
-                          int bn, bool halo) {
+                          int bn, int halo) {
   const int P = (s.H + 2 * s.pad - s.R) / s.stride + 1, Q = (s.W + 2 * s.pad - s.R) / s.stride + 1;
   ConvArgs a{};
   a.x = x; a.H = s.H; a.W = s.W; a.C = s.C; a.ldx = s.C; a.xoff = 0;
@@ -86,7 +86,7 @@ static ConvArgs make_args(const Shape& s, const uint16_t* x, const uint16_t* w, 
   if (halo) {
     int th = 8, tw = 16, tiles_h = 1, tiles_w = 1;
     halo_geom(P, Q, bm, th, tw, tiles_h, tiles_w);
-    a.halo = 1; a.th = th; a.tw = tw; a.tiles_h = tiles_h; a.tiles_w = tiles_w;
+    a.halo = halo; a.th = th; a.tw = tw; a.tiles_h = tiles_h; a.tiles_w = tiles_w;
     a.fd_tw = make_fastdiv((uint32_t)tw);
     a.fd_tilesw = make_fastdiv((uint32_t)tiles_w);
     a.fd_thw = make_fastdiv((uint32_t)(tiles_h * tiles_w));
