@@ -177,7 +177,8 @@ def main():
         setters = {"pipe": "set_conv_pipe", "halo": "set_conv_halo", "stream": "set_conv_stream",
                    "dgrad_stream": "set_dgrad_stream", "autotune": "set_conv_autotune", "wgrad3": "set_wgrad3",
                    "splitk": "set_conv_splitk", "pipe_dgrad": "set_conv_pipe_dgrad", "wgrad_batch": "set_wgrad_batch",
-                   "defer_direct": "set_defer_direct", "wgrad3_blocks": "set_wgrad3_blocks"}
+                   "defer_direct": "set_defer_direct", "wgrad3_blocks": "set_wgrad3_blocks",
+                   "conv3_stream": "set_conv3_stream"}
         for k, v in pins.items():
             if k in setters:
                 getattr(_nat(), setters[k])(int(v))

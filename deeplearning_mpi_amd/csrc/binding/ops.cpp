@@ -455,6 +455,33 @@ static bool stream1x1_shape(int64_t M, int C, int K, int R, int S, int stride, i
   return dlmpi_stream1x1_plan(M, C, K, stride, &bm, &bn, &G) != 0;
 }
 
+// The streaming 3x3 kernel (conv3x3_stream.hip: 64 -> 64 channels, stride 1, pad 1) applies: shape-only
+// decision, as stream1x1_shape (its statistics have G rows, one per block).  Its grid shares the
+// RCCL-aware budget of the streaming data gradient (one block per CU).
+static int g_conv3_ran = 0;   // 1 if the last conv2d_fwd / conv2d_dgrad ran the streaming 3x3 kernel (tests)
+static bool stream3x3_shape(int N, int H, int W, int C, int K, int R, int S, int stride, int pad, int pro, int f32,
+                            int& th, int& tw, int& G) {
+  if (R != 3 || S != 3 || stride != 1 || pad != 1 || pro != 0 || f32) return false;
+  return dlmpi_conv3_stream_plan(N, H, W, C, K, dlmpi_dgs_blocks(), &th, &tw, &G) != 0;
+}
+static dlmpi::Conv3StreamArgs conv3_args(const at::Tensor& x, int N, int H, int W, int ldx, int xoff, const at::Tensor& w,
+                                         int flip, void* y, int ldy, int yoff, int th, int tw, int G) {
+  dlmpi::Conv3StreamArgs c{};
+  c.x = ptr<uint16_t>(x);
+  c.ldx = ldx; c.xoff = xoff;
+  c.w = ptr<uint16_t>(w);
+  c.ldw = 9 * 64; c.flip = flip;
+  c.y = reinterpret_cast<uint16_t*>(y);
+  c.ldy = ldy; c.yoff = yoff;
+  c.N = N; c.H = H; c.W = W;
+  c.th = th; c.tw = tw;
+  c.tiles_h = ceil_div(H, th);
+  c.tiles_w = ceil_div(W, tw);
+  c.ntiles = N * c.tiles_h * c.tiles_w;
+  c.G = G;
+  return c;
+}
+
 
 
 // y[n, p, q, yoff + k] = epilogue( sum_{r,s,c} x[n, p*stride - pad + r, q*stride - pad + s, xoff + c] * w[k][r][s][c] )
@@ -578,6 +605,33 @@ static int conv2d_fwd_impl(const at::Tensor& x, int N, int H, int W, int C, int 
     pipe = (bm == 128 ? 4 : 2) + 1;
   }
   g_stream_ran = 0;
+  g_conv3_ran = 0;
+  {  // streaming 3x3 kernel (64 -> 64: the full-resolution UNet layers, ResNet layer-1 conv2)
+    int th, tw, G;
+    if (bm_req <= 0 && bn_req <= 0 && stream3x3_shape(N, H, W, C, K, R, S, stride, pad, pro, a.f32, th, tw, G)) {
+      const bool ok = !res.has_value() && !scale.has_value() && !relu && a.kvalid == K && a.vec_store &&
+                      ldx % 8 == 0 && xoff % 8 == 0 && (int64_t)H * W * ldy * 2 < (1ll << 31) &&
+                      y.scalar_type() == at::kBFloat16 && w.scalar_type() == at::kBFloat16;
+      if (a.stats && !ok)
+        throw std::runtime_error("conv2d_fwd: statistics were sized for the streaming 3x3 kernel, which cannot run");
+      if (ok) {
+        if (a.stats && stats->size(0) < G) throw std::runtime_error("conv2d_fwd: stats buffer too small");
+        dlmpi::Conv3StreamArgs c = conv3_args(x, N, H, W, ldx, xoff, w, 0, a.y, ldy, yoff, th, tw, G);
+        c.bias = a.bias;
+        c.stats = a.stats;
+        check(dlmpi_conv3x3_stream(&c, a.stats ? 0 : 1, cur_stream()), "conv2d_fwd (stream 3x3)");
+        g_conv3_ran = 1;
+        if (fin != nullptr) {
+          at::Tensor ws = colsum_ws(*stats, G, K);
+          check(dlmpi_bn_finalize(a.stats, G, K, fin->count, fin->gamma, fin->beta, fin->running_mean,
+                                  fin->running_var, fin->momentum, fin->eps, fin->scale, fin->shift, fin->save_mean,
+                                  fin->save_invstd, ptr<double>(ws), cur_stream()),
+                "bn_finalize");
+        }
+        return G;
+      }
+    }
+  }
   {  // streaming 1x1 kernel (short reductions into wide, memory-bound outputs)
     const int64_t M = (int64_t)N * P * Q;
     int sbm, sbn, G;
@@ -715,6 +769,8 @@ int conv2d_fwd_mtiles_pro(int N, int H, int W, int C, int K, int R, int S, int s
   int bm, bn;
   int G;
   if (bm_req <= 0 && stream1x1_shape((int64_t)N * P * Q, C, K, R, S, stride, pad, pro, f32, bm, bn, G)) return G;
+  int th, tw;
+  if (bm_req <= 0 && stream3x3_shape(N, H, W, C, K, R, S, stride, pad, pro, f32, th, tw, G)) return G;
   if (bm_req <= 0) {
     int hbm, hbn;
     pick_tiles((int64_t)N * P * Q, K, (int64_t)R * S * C, C, hbm, hbn, pro != 0);
@@ -793,6 +849,28 @@ c10::optional<at::Tensor> conv2d_dgrad_pro(const at::Tensor& dy, int N, int P, i
   if ((a.mask || a.mscale || a.mbits) && ((ldmask | maskoff | ldz | zoff | ldz2 | z2off) % 8 != 0 || !a.vec_store))
     throw std::runtime_error("conv2d_dgrad: fused BN tensors must be 8-channel aligned");
   g_dgrad_stream_ran = 0;
+  g_conv3_ran = 0;
+  {  // streaming 3x3 data gradient (conv3x3_stream.hip, 64 -> 64): a forward conv of dy with wT, taps flipped
+    const int mode = a.mscale ? 2 : 0;
+    int th, tw, G;
+    if (stream3x3_shape(N, H, W, K, C, R, S, stride, pad, pro, a.f32, th, tw, G) && P == H && Q == W && !colsum &&
+        !a.mask && !a.mbits && !a.z2 && !a.res && !a.bias && (a.z != nullptr) == (mode == 2) && a.vec_store &&
+        a.kvalid == C && (lddy | dyoff) % 8 == 0 && (int64_t)H * W * lddx * 2 < (1ll << 31) &&
+        dx.scalar_type() == at::kBFloat16) {
+      dlmpi::Conv3StreamArgs c = conv3_args(dy, N, H, W, lddy, dyoff, wT, 1, a.y, lddx, dxoff, th, tw, G);
+      c.z = static_cast<const uint16_t*>(a.z);
+      c.ldz = ldz; c.zoff = zoff;
+      c.mscale = a.mscale; c.mshift = a.mshift;
+      c10::optional<at::Tensor> st;
+      if (a.z) {
+        st = at::empty({(int64_t)G, 2, (int64_t)C}, dy.options().dtype(at::kFloat));
+        c.stats = ptr<float>(*st);
+      }
+      check(dlmpi_conv3x3_stream(&c, mode == 2 ? 2 : 1, cur_stream()), "conv2d_dgrad (stream 3x3)");
+      g_conv3_ran = 1;
+      return st;
+    }
+  }
   {  // streaming 1x1 data gradient (conv1x1_dgrad_stream.hip): memory-bound GEMMs with a heavy epilogue
     const int64_t M = (int64_t)N * H * W;
     const int mode = a.mbits ? 1 : (a.mscale ? 2 : 0);
@@ -1564,6 +1642,9 @@ void register_ops(pybind11::module& m) {
   m.def("set_conv_splitk", [](int n) { g_splitk_override = n; });
   m.def("set_conv_pipe_dgrad", [](int mode) { g_pipe_dgrad_override = mode; });
   m.def("set_conv_pipe", [](int mode) { g_pipe_override = mode; });
+  m.def("set_conv3_stream", [](int mode) { dlmpi_set_conv3_stream(mode); });
+  m.def("set_conv3_waves", [](int nw) { dlmpi_set_conv3_waves(nw); });
+  m.def("conv3_stream_last", []() { return g_conv3_ran; });
   m.def("set_dgs_blocks", [](int n) { dlmpi_set_dgs_blocks(n); });
   m.def("dgs_blocks", []() { return dlmpi_dgs_blocks(); });
   m.def("conv_halo_last", []() { return g_halo_ran; });

@@ -200,6 +200,28 @@ struct WgradArgs {
   const float* pshift;
 };
 
+// Streaming 3x3 / stride-1 / pad-1 convolution, 64 -> 64 channels (conv3x3_stream.hip): persistent
+// blocks over th x tw output tiles with all 9 taps' weights resident.  Forward (w [64][3][3][64],
+// flip 0) or stride-1 data gradient (w = wT [C][3][3][K], flip 1); mode 0: + bias, statistics
+// {sum y, sum y^2}; 1: plain; 2: dgrad into a BN + ReLU output (mask z * mscale + mshift > 0,
+// statistics {sum dx, sum dx * z}); stats [G][2][64].
+struct Conv3StreamArgs {
+  const uint16_t* x;
+  int ldx, xoff;
+  const uint16_t* w;
+  int ldw, flip;
+  uint16_t* y;
+  int ldy, yoff;
+  int N, H, W;
+  int th, tw, tiles_h, tiles_w, ntiles, G;
+  const float* bias;
+  const uint16_t* z;
+  int ldz, zoff;
+  const float* mscale;
+  const float* mshift;
+  float* stats;
+};
+
 // 3x3 / stride-1 / pad-1 weight gradient by 8 x 8 output-pixel tiles (conv_wgrad3.hip): split z
 // reduces pixel tiles [z * tiles_per_split, ...) of the N x tiles_h x tiles_w grid into
 // ws[z][Ko][9 * C] (tap-major columns, the general path's workspace layout)
@@ -250,6 +272,11 @@ hipError_t dlmpi_wgrad_reduce_batch(dlmpi::WgradReduceBatch* b, hipStream_t s);
 // 3x3 spatial-tile weight gradient: tile plan (KT x CT; 0 if the channel counts do not fit) + launch
 int dlmpi_wgrad3_plan(int Ko, int C, int* kt, int* ct);
 hipError_t dlmpi_wgrad3x3(const dlmpi::Wgrad3Args* a, int kt, int ct, hipStream_t s);
+// streaming 64 -> 64 3x3 conv: plan (tile th x tw, G blocks; 0 if it does not apply) + launch
+int dlmpi_conv3_stream_plan(int N, int H, int W, int C, int K, int blocks, int* th, int* tw, int* G);
+hipError_t dlmpi_conv3x3_stream(const dlmpi::Conv3StreamArgs* a, int mode, hipStream_t s);
+void dlmpi_set_conv3_stream(int mode);
+void dlmpi_set_conv3_waves(int nw);
 
 // batch norm
 hipError_t dlmpi_bn_finalize(const float* partial, int ntiles, int C, double count, const float* gamma,

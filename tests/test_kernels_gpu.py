@@ -200,6 +200,7 @@ def test_pipelined_conv_bit_identical_to_single_stage(shape):
     C = nb.C
     try:
         C.set_conv_halo(0)
+        C.set_conv3_stream(0)
         C.set_conv_stream(0)
         C.set_dgrad_stream(0)
         C.set_conv_autotune(0)
@@ -214,7 +215,8 @@ def test_pipelined_conv_bit_identical_to_single_stage(shape):
             torch.cuda.synchronize()
             out.setdefault(mode, []).append((y.buf.clone(), st.double().sum(0), dx.buf.clone()))
     finally:
-        for f in (C.set_conv_pipe, C.set_conv_halo, C.set_conv_stream, C.set_dgrad_stream, C.set_conv_autotune):
+        for f in (C.set_conv_pipe, C.set_conv_halo, C.set_conv_stream, C.set_dgrad_stream, C.set_conv_autotune,
+                  C.set_conv3_stream):
             f(-1)
         C.set_conv_splitk(0)
     base, p1, p2 = out[0][0], out[1][0], out[1][1]
@@ -363,6 +365,7 @@ def test_conv3x3_halo_tiles(shape):
     z, _ = _act(N, H, W, Cin)
     sc, sh = torch.rand(Cin, device=DEV) + 0.5, torch.randn(Cin, device=DEV) * 0.5
     out = {}
+    nb.C.set_conv3_stream(0)   # 64 -> 64: the halo kernel itself, not the streaming 3x3 kernel
     for mode in (2, 0):   # 2: halo tiles on any grid (the default keeps them to >= 28 x 28)
         nb.C.set_conv_halo(mode)
         y = _empty(N, H, W, K)
@@ -376,6 +379,7 @@ def test_conv3x3_halo_tiles(shape):
         torch.cuda.synchronize()
         out[mode] = (y.buf.clone(), st.double().sum(0), dx.buf.clone(), part.double().sum(0), mt)
     nb.C.set_conv_halo(-1)
+    nb.C.set_conv3_stream(-1)
     yr = _empty(N, H, W, K, torch.float32)
     rb.conv_fwd(xr, w.float(), K, 3, 3, 1, 1, yr)
     dxr = _empty(N, H, W, Cin, torch.float32)
@@ -388,6 +392,66 @@ def test_conv3x3_halo_tiles(shape):
     assert _rel(h[2], torch.where(keep, dxr.buf, torch.zeros_like(dxr.buf))) < 1e-2
     assert _rel(h[2], g[2]) < 1e-2
     assert _rel(h[3], g[3]) < 1e-3
+
+
+CONV3_STREAM_SHAPES = [
+    # N, H, W, x channel stride / offset, y channel stride / offset
+    (2, 16, 16, None, 0, None, 0),      # one 8 x 16 tile per 8 rows
+    (3, 56, 56, None, 0, None, 0),      # ResNet layer 1 (14-wide tiles)
+    (2, 37, 23, 192, 64, 128, 64),      # ragged tiles; x and y channel slices (UNet concat buffers)
+    (1, 9, 5, None, 0, None, 0),        # fewer tiles than blocks
+]
+
+
+@pytest.mark.parametrize("shape", CONV3_STREAM_SHAPES, ids=lambda s: "x".join(str(v) for v in s[:3]))
+def test_conv3x3_stream_64(shape):
+    """Streaming 64 -> 64 3x3 kernel (conv3x3_stream.hip): forward with bias + BN statistics, data
+    gradient with the fused BN-backward epilogue (mask from z) and plain, against the fp32 reference
+    and the halo kernel (same K order and epilogue arithmetic; one-ulp bf16 differences in a few
+    elements from the swapped MFMA operands)."""
+    nb, rb = _be()
+    N, H, W, ldx, xoff, ldy, yoff = shape
+    C = K = 64
+    x, xr = _act(N, H, W, C, ld=ldx, off=xoff)
+    w = (torch.randn(K, 3, 3, C, device=DEV) / (9 * C) ** 0.5).to(torch.bfloat16)
+    wT = w.permute(3, 1, 2, 0).contiguous()
+    bias = torch.randn(K, device=DEV) * 0.1
+    dy, dyr = _act(N, H, W, K)
+    z, _ = _act(N, H, W, C)
+    sc, sh = torch.rand(C, device=DEV) + 0.5, torch.randn(C, device=DEV) * 0.5
+    out = {}
+    for mode in (1, 0):   # 1: streaming kernel; 0: the halo kernel (on any grid)
+        nb.C.set_conv3_stream(mode)
+        nb.C.set_conv_halo(2)
+        y = Act(torch.zeros(N * H * W, ldy or K, dtype=torch.bfloat16, device=DEV), N, H, W, K, yoff)
+        mt = nb.conv_mtiles(N, H, W, C, K, 3, 3, 1, 1)
+        st = torch.zeros(mt, 2, K, device=DEV)
+        rows = nb.conv_fwd(x, w, K, 3, 3, 1, 1, y, bias=bias, stats=st)
+        assert rows == mt and nb.C.conv3_stream_last() == mode
+        dx = _empty(N, H, W, C)
+        part = nb.conv_dgrad(dy, wT, C, 3, 3, 1, 1, dx, fuse=BwdFuse(None, z, None, sc, sh))
+        assert nb.C.conv3_stream_last() == mode
+        dx2 = _empty(N, H, W, C)
+        nb.conv_dgrad(dy, wT, C, 3, 3, 1, 1, dx2)
+        assert nb.C.conv3_stream_last() == mode
+        torch.cuda.synchronize()
+        out[mode] = (y.buf.clone(), st.double().sum(0), dx.buf.clone(), part.double().sum(0), dx2.buf.clone())
+    nb.C.set_conv3_stream(-1)
+    nb.C.set_conv_halo(-1)
+    s_, h_ = out[1], out[0]
+    yr = _empty(N, H, W, K, torch.float32)
+    rb.conv_fwd(xr, w.float(), K, 3, 3, 1, 1, yr, bias=bias)
+    assert _rel(s_[0][:, yoff:yoff + K], yr.buf) < 1e-2
+    dxr = _empty(N, H, W, C, torch.float32)
+    rb.conv_dgrad(dyr, wT.float(), C, 3, 3, 1, 1, dxr)
+    assert _rel(s_[4], dxr.buf) < 1e-2
+    keep = (z.buf.float() * sc + sh) > 0
+    assert _rel(s_[2], torch.where(keep, dxr.buf, torch.zeros_like(dxr.buf))) < 1e-2
+    # same K order, operands swapped (D^T fragments): the fp32 sums round the other way in a few
+    # elements -- one bf16 ulp, well under 0.5 % of them
+    for a, b in ((s_[0], h_[0]), (s_[2], h_[2]), (s_[4], h_[4])):
+        assert int((a != b).sum()) <= max(8, a.numel() // 200) and _rel(a, b) < 8e-3
+    assert _rel(s_[1], h_[1]) < 2e-3 and _rel(s_[3], h_[3]) < 2e-3
 
 
 WGRAD3_SHAPES = [
@@ -765,6 +829,7 @@ def _static_kernels(on: bool):
     C.set_conv_stream(0 if on else -1)
     C.set_conv_autotune(0 if on else -1)
     C.set_conv_halo(0 if on else -1)    # 3x3 halo tiles sum chunk-major (no prologue variant)
+    C.set_conv3_stream(0 if on else -1)  # streaming 64 -> 64 3x3 kernel (no prologue variant)
     C.set_wgrad3(0 if on else -1)       # 3x3 spatial-tile weight gradient (no prologue variant)
     C.set_dgrad_stream(0 if on else -1)  # streaming 1x1 data gradient (no prologue variant)
 
