@@ -13,7 +13,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 import torch  # noqa: E402
 
-RESET = {"set_conv3_stream": -1, "set_conv_halo": -1, "set_conv3_waves": 4}
+RESET = {"set_conv3_stream": -1, "set_conv_halo": -1}
 
 
 def main():
@@ -59,6 +59,8 @@ def main():
                 if ps == "fwd":
                     st = torch.empty(be.conv_mtiles(N, H, W, C, K, 3, 3, 1, 1), 2, K, device=dev)
                     be.conv_fwd(x, w, K, 3, 3, 1, 1, y, bias=bias, stats=st)
+                elif ps == "dgradp":   # plain data gradient (no BN fusion)
+                    be.conv_dgrad(dy, wT, C, 3, 3, 1, 1, dx)
                 else:
                     be.conv_dgrad(dy, wT, C, 3, 3, 1, 1, dx, fuse=BwdFuse(None, z, None, sc, shf))
             outs = []

@@ -1643,7 +1643,6 @@ void register_ops(pybind11::module& m) {
   m.def("set_conv_pipe_dgrad", [](int mode) { g_pipe_dgrad_override = mode; });
   m.def("set_conv_pipe", [](int mode) { g_pipe_override = mode; });
   m.def("set_conv3_stream", [](int mode) { dlmpi_set_conv3_stream(mode); });
-  m.def("set_conv3_waves", [](int nw) { dlmpi_set_conv3_waves(nw); });
   m.def("conv3_stream_last", []() { return g_conv3_ran; });
   m.def("set_dgs_blocks", [](int n) { dlmpi_set_dgs_blocks(n); });
   m.def("dgs_blocks", []() { return dlmpi_dgs_blocks(); });

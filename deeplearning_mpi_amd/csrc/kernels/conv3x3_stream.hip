@@ -45,11 +45,15 @@ __device__ __forceinline__ int c3_eoff(int r, int col) {
   return r * 128 + ((((col >> 3) ^ ((r >> 1) & 7))) << 4) + ((col & 4) << 1);
 }
 
-template <int MODE, bool FLIP, int NW>
-__global__ __launch_bounds__(64 * NW) void conv3x3_stream_kernel(const Conv3StreamArgs a) {
-  constexpr int NT = 64 * NW, BM = 128, BN = 64;
-  // 4 waves: 64 x 32 per wave (one wave per SIMD); 8 waves: 32 x 32 (two per SIMD)
-  constexpr int WGM = NW / 2, WGN = 2, WM = BM / WGM, WN = BN / WGN;
+// 8 waves of 32 x 32 (two per SIMD).  Measured alternatives (profiles/r5_conv3): 4 waves of 64 x 32
+// (one per SIMD, a third fewer LDS reads per MFMA but nothing to hide their latency: 415 vs 370 us at
+// 16 x 512^2, also with a register double buffer of the next tap's fragments); the weights held in
+// registers (144 VGPRs per wave) instead of LDS: spills with the statistics epilogue, and only +6 %
+// on the plain data gradient at 512^2 (-5 % at 56^2).
+template <int MODE, bool FLIP>
+__global__ __launch_bounds__(512) void conv3x3_stream_kernel(const Conv3StreamArgs a) {
+  constexpr int NW = 8, NT = 64 * NW, BM = 128, BN = 64;
+  constexpr int WGM = 4, WGN = 2, WM = BM / WGM, WN = BN / WGN;
   constexpr int TM = WM / 16, TN = WN / 16;
   constexpr int RP = NT / 8;                    // 128-B rows staged per pass
   constexpr int HROWS = 192;                    // halo rows (host: (th + 2) (tw + 2) <= 192)
@@ -326,23 +330,15 @@ extern "C" int dlmpi_conv3_stream_plan(int N, int H, int W, int C, int K, int bl
   return 1;
 }
 
-static int g_c3_waves = 4;   // dlmpi_ext set_conv3_waves (A/B): 4 or 8 waves per block
-extern "C" void dlmpi_set_conv3_waves(int nw) { g_c3_waves = nw == 8 ? 8 : 4; }
-
-template <int NW>
-static hipError_t launch_c3(const Conv3StreamArgs* a, int mode, hipStream_t s) {
-  const dim3 g((unsigned)a->G), b(64 * NW);
-  if (mode == 0 && !a->flip && a->stats) hipLaunchKernelGGL((conv3x3_stream_kernel<0, false, NW>), g, b, 0, s, *a);
-  else if (mode == 1 && !a->flip) hipLaunchKernelGGL((conv3x3_stream_kernel<1, false, NW>), g, b, 0, s, *a);
-  else if (mode == 1 && a->flip) hipLaunchKernelGGL((conv3x3_stream_kernel<1, true, NW>), g, b, 0, s, *a);
-  else if (mode == 2 && a->flip && a->stats && a->z && a->mscale && a->mshift)
-    hipLaunchKernelGGL((conv3x3_stream_kernel<2, true, NW>), g, b, 0, s, *a);
-  else return hipErrorInvalidValue;
-  return hipGetLastError();
-}
-
 extern "C" hipError_t dlmpi_conv3x3_stream(const Conv3StreamArgs* a, int mode, hipStream_t s) {
   if (a->G <= 0) return hipSuccess;
   if (a->th * a->tw > 128 || (a->th + 2) * (a->tw + 2) > 192) return hipErrorInvalidValue;
-  return g_c3_waves == 8 ? launch_c3<8>(a, mode, s) : launch_c3<4>(a, mode, s);
+  const dim3 g((unsigned)a->G), b(512);
+  if (mode == 0 && !a->flip && a->stats) hipLaunchKernelGGL((conv3x3_stream_kernel<0, false>), g, b, 0, s, *a);
+  else if (mode == 1 && !a->flip) hipLaunchKernelGGL((conv3x3_stream_kernel<1, false>), g, b, 0, s, *a);
+  else if (mode == 1 && a->flip) hipLaunchKernelGGL((conv3x3_stream_kernel<1, true>), g, b, 0, s, *a);
+  else if (mode == 2 && a->flip && a->stats && a->z && a->mscale && a->mshift)
+    hipLaunchKernelGGL((conv3x3_stream_kernel<2, true>), g, b, 0, s, *a);
+  else return hipErrorInvalidValue;
+  return hipGetLastError();
 }

@@ -276,7 +276,6 @@ hipError_t dlmpi_wgrad3x3(const dlmpi::Wgrad3Args* a, int kt, int ct, hipStream_
 int dlmpi_conv3_stream_plan(int N, int H, int W, int C, int K, int blocks, int* th, int* tw, int* G);
 hipError_t dlmpi_conv3x3_stream(const dlmpi::Conv3StreamArgs* a, int mode, hipStream_t s);
 void dlmpi_set_conv3_stream(int mode);
-void dlmpi_set_conv3_waves(int nw);
 
 // batch norm
 hipError_t dlmpi_bn_finalize(const float* partial, int ntiles, int C, double count, const float* gamma,
