@@ -1500,8 +1500,9 @@ void grad_norm(const at::Tensor& g, double max_norm, at::Tensor norm_out, at::Te
   const int nblk = 512;
   at::Tensor partial = at::empty({nblk}, g.options().dtype(at::kFloat));
   check(dlmpi_sumsq(ptr<float>(g), g.numel(), ptr<float>(partial), nblk, cur_stream()), "sumsq");
+  if (coef_out.numel() < 2) throw std::runtime_error("grad_norm: coef_out needs 2 (or 4) floats");
   check(dlmpi_clip_coef(ptr<float>(partial), nblk, (float)max_norm, ptr<float>(norm_out), ptr<float>(coef_out),
-                        cur_stream()),
+                        (int)std::min<int64_t>(4, coef_out.numel()), cur_stream()),
         "clip_coef");
 }
 void scale_(at::Tensor x, const at::Tensor& coef) {

@@ -391,7 +391,7 @@ hipError_t dlmpi_adam(float* p, const float* g, float* m, float* v, int64_t n, f
                       float eps, float wd, int adamw, float bc1, float bc2, const float* clip_coef,
                       float* tstep, hipStream_t s);   // tstep (device step count) overrides bc1/bc2
 hipError_t dlmpi_sumsq(const float* x, int64_t n, float* partial, int nblk, hipStream_t s);
-hipError_t dlmpi_clip_coef(const float* partial, int nblk, float max_norm, float* norm_out, float* coef_out,
+hipError_t dlmpi_clip_coef(const float* partial, int nblk, float max_norm, float* norm_out, float* coef_out, int ncoef,
                            hipStream_t s);
 hipError_t dlmpi_scale_f32(float* x, int64_t n, const float* coef, hipStream_t s);
 

@@ -95,9 +95,12 @@ __global__ __launch_bounds__(256) void sumsq_kernel(const float* __restrict__ x,
   if (threadIdx.x == 0) partial[blockIdx.x] = sh[0] + sh[1] + sh[2] + sh[3];
 }
 
-// norm = sqrt(sum partial); coef_out[0] = min(1, max_norm / (norm + 1e-6)); coef_out[1] = !isfinite(norm)
+// norm = sqrt(sum partial); coef_out[0] = min(1, max_norm / (norm + 1e-6)); coef_out[1] = !isfinite(norm);
+// ncoef 4: also coef_out[2..3] = {1, !isfinite(norm)} -- the optimizer's (scale, skip) pair once the
+// gradients are scaled in place (no copy + fill per step)
 __global__ __launch_bounds__(256) void clip_coef_kernel(const float* __restrict__ partial, int nblk, float max_norm,
-                                                        float* __restrict__ norm_out, float* __restrict__ coef_out) {
+                                                        float* __restrict__ norm_out, float* __restrict__ coef_out,
+                                                        int ncoef) {
   __shared__ double sh[4];
   double s = 0.0;
   for (int i = threadIdx.x; i < nblk; i += blockDim.x) s += (double)partial[i];
@@ -112,6 +115,10 @@ __global__ __launch_bounds__(256) void clip_coef_kernel(const float* __restrict_
       const float c = max_norm / (norm + 1e-6f);
       coef_out[0] = c < 1.f ? c : 1.f;
       coef_out[1] = isfinite(norm) ? 0.f : 1.f;
+      if (ncoef >= 4) {
+        coef_out[2] = 1.f;
+        coef_out[3] = coef_out[1];
+      }
     }
   }
 }
@@ -153,8 +160,8 @@ extern "C" hipError_t dlmpi_sumsq(const float* x, int64_t n, float* partial, int
   return hipGetLastError();
 }
 extern "C" hipError_t dlmpi_clip_coef(const float* partial, int nblk, float max_norm, float* norm_out,
-                                      float* coef_out, hipStream_t s) {
-  hipLaunchKernelGGL(clip_coef_kernel, dim3(1), dim3(256), 0, s, partial, nblk, max_norm, norm_out, coef_out);
+                                      float* coef_out, int ncoef, hipStream_t s) {
+  hipLaunchKernelGGL(clip_coef_kernel, dim3(1), dim3(256), 0, s, partial, nblk, max_norm, norm_out, coef_out, ncoef);
   return hipGetLastError();
 }
 extern "C" hipError_t dlmpi_scale_f32(float* x, int64_t n, const float* coef, hipStream_t s) {

@@ -796,6 +796,9 @@ class RefBackend:
         norm_out.reshape(-1)[0] = n
         coef_out[0] = torch.clamp(max_norm / (n + 1e-6), max=1.0)
         coef_out[1] = 0.0 if torch.isfinite(n) else 1.0
+        if coef_out.numel() >= 4:
+            coef_out[2] = 1.0
+            coef_out[3] = coef_out[1]
 
     def scale_(self, x, coef):
         x.mul_(coef[0])

@@ -149,7 +149,9 @@ def clip_grad_norm_(parameters, max_norm: float, norm_type: float = 2.0, optimiz
     dev = params[0].device
     be = a.backend if a is not None else make_backend(dev)
     norm = torch.empty(1, dtype=torch.float32, device=dev)
-    coef = torch.empty(2, dtype=torch.float32, device=dev)
+    # [scale, nonfinite, 1, nonfinite]: the last pair is the optimizer's (scale, skip) once the
+    # gradients are scaled in place (written by the same kernel: no copy or fill per step)
+    coef = torch.empty(4, dtype=torch.float32, device=dev)
     if float(norm_type) != 2.0:
         grads = [a.grad] if a is not None else [p.grad.reshape(-1) for p in params]
         p = float(norm_type)
@@ -160,6 +162,8 @@ def clip_grad_norm_(parameters, max_norm: float, norm_type: float = 2.0, optimiz
         norm.copy_(n.reshape(1))
         coef[0] = torch.clamp(max_norm / (n + 1e-6), max=1.0)
         coef[1] = (~torch.isfinite(n)).float()
+        coef[2] = 1.0
+        coef[3] = coef[1]
         for g in grads:
             g.mul_(coef[0].to(g.dtype))
     elif a is not None:
@@ -171,7 +175,5 @@ def clip_grad_norm_(parameters, max_norm: float, norm_type: float = 2.0, optimiz
         for p in params:
             be.scale_(p.grad.view(-1), coef)
     if optimizer is not None and hasattr(optimizer, "clip"):
-        c = coef.clone()
-        c[:1].fill_(1.0)   # grads already scaled in place; keep only the skip flag (a kernel: capturable)
-        optimizer.clip = c
+        optimizer.clip = coef[2:4]   # grads already scaled in place: scale 1, keep the skip flag
     return norm[0]
