@@ -87,19 +87,13 @@ static void set_kstep(ConvArgs& a, int C) {
 // long reductions into wide outputs (UNet 3x3 convs with >= 256 channels: up to 1.3x, measured by
 // benchmarks/conv_bench.py) and loses on the short / memory-bound ResNet GEMMs; 64-row tiles for
 // small grids.  `red` = GEMM reduction length (R*S*C).
-static int bm256_min_tiles() {
-  static int v = 256;
-  return v;
-}
+constexpr int kBm256MinTiles = 256;
 
 // Shortest 1x1 reduction (red == cin) that takes the 256-row tile
 // (default 1024: the 14^2 1024->256 forward and 256<-1024 data gradient, 128x128 -> 256x128 tiles
 // halve the B-operand re-reads, -14 % each; ResNet-50 +0.8 %, profiles/r3_bm256red); other
 // reductions from 2304 as before
-static int bm256_min_red_1x1() {
-  static int v = 1024;
-  return v;
-}
+constexpr int kBm256MinRed1x1 = 1024;
 
 // cin: channel count of the GEMM's gathered operand
 static void pick_tiles(int64_t M, int Kout, int64_t red, int cin, int& bm, int& bn, bool pro = false,
@@ -115,7 +109,7 @@ static void pick_tiles(int64_t M, int Kout, int64_t red, int cin, int& bm, int& 
   // the small-channel stems (-13 % ResNet 7x7, -10 % UNet first conv) and the 4M-row UNet level-1
   // 3x3s (-4 %), loses 3-8 % on the 0.8M-row ResNet layer1 GEMMs -> only there.
   if (bn == 64 && (M + 255) / 256 >= 512 && (cin < 64 || (M >= (2 << 20) && red >= 576))) bm = 256;
-  else if (Kout >= 256 && (red >= 2304 || (wide1x1 && red == cin && red >= bm256_min_red_1x1())) && ((M + 255) / 256) * nt >= bm256_min_tiles()) bm = 256;
+  else if (Kout >= 256 && (red >= 2304 || (wide1x1 && red == cin && red >= kBm256MinRed1x1)) && ((M + 255) / 256) * nt >= kBm256MinTiles) bm = 256;
   else if (tiles < 512) bm = 64;
   // grids that do not fill the chip even with 64-row tiles (ResNet-18 on 32 x 32 CIFAR: 8-128 tiles):
   // 64-wide output tiles too -- twice the blocks before split-K (the autotuner's choice on every such
@@ -171,10 +165,7 @@ static int pipe_select(int f32, int pro, int cin, int64_t M, int Kout, int64_t r
 // set_conv_halo(0) (tests): these convolutions through the im2col gather path too.
 static int g_halo_override = -1;   // dlmpi_ext set_conv_halo (tests)
 static int g_splitk_override = 0;   // dlmpi_ext set_conv_splitk (tests): > 0 forces that many K slices
-static bool halo_on() {
-  static const int v = 1;
-  return (g_halo_override >= 0 ? g_halo_override : v) != 0;
-}
+static bool halo_on() { return g_halo_override != 0; }
 // Tile th x tw (th * tw <= bm, (th + 2) * (tw + 2) <= 192 / 352 rows for bm 128 / 256) covering a
 // P x Q grid with the fewest tiles (ties: the wider tile).
 static void halo_geom(int P, int Q, int bm, int& th, int& tw, int& tiles_h, int& tiles_w) {
@@ -402,8 +393,6 @@ static void fill_epilogue(ConvArgs& a, at::Tensor& y, int ldy, int yoff, const c
   a.relu = relu ? 1 : 0;
   a.stats = optr<float>(stats);
   a.nstat = 2;
-  static const int nt = 0;
-  a.nt_store = nt;
 }
 
 // Extras of a pro-3 launch (conv2d_fwd_bn_apply sets them around the shared forward path).
@@ -1149,9 +1138,8 @@ void conv2d_wgrad_pro(const at::Tensor& dy, int lddy, int dyoff, int Ko, const a
   }
   // 3x3 / stride 1 / pad 1 without operand prologues (UNet DoubleConv, ResNet conv2): the
   // spatial-tile kernel (conv_wgrad3.hip) -- X staged once per 8 x 8 pixel block for all 9 taps.
-  static const int w3 = 1;
   int kt = 0, ct = 0;
-  if ((g_wgrad3_override >= 0 ? g_wgrad3_override : w3) && !a.f32 && pro_a == 0 && pro_b == 0 && R == 3 && S == 3 &&
+  if (g_wgrad3_override != 0 && !a.f32 && pro_a == 0 && pro_b == 0 && R == 3 && S == 3 &&
       stride == 1 && pad == 1 && P == H && Q == W && dlmpi_wgrad3_plan(Ko, C, &kt, &ct)) {
     dlmpi::Wgrad3Args b{};
     b.dy = ptr<uint16_t>(dy);
@@ -1205,8 +1193,7 @@ void conv2d_wgrad_pro(const at::Tensor& dy, int lddy, int dyoff, int Ko, const a
   // 64 x 64) -- each dy row staged once per 256 columns, fewer LDS reads per MFMA.  The tile holds
   // ~200 VGPRs (2 blocks per CU), so its split count is floored to fit the grid in one round
   // (profiles/r2_wgrad_wide).  Gather-form only (1x1s measured no gain).
-  static const int wide = 1;
-  const bool w256 = !a.f32 && Ko <= 64 && pro_b == 0 && a.TC >= 256 && (wide == 2 || (wide == 1 && !a.direct));
+  const bool w256 = !a.f32 && Ko <= 64 && pro_b == 0 && a.TC >= 256 && !a.direct;
   const int bn = a.f32 ? 64 : (w256 ? 256 : 128);
   a.ntiles = ceil_div(a.TC, bn);
   const int tiles = a.mtiles * a.ntiles;

@@ -276,8 +276,8 @@ __global__ __launch_bounds__(256) void finalize_kernel(const double* __restrict_
 // SC1 (default): the slice partials are stored write-through (8-B agent-scope relaxed atomic
 // stores = sc1) and drained before the ticket, and the last arriver reads them with sc1 loads, so
 // neither side fences (Guideline 16 R1).  A release fence here would write back every dirty line
-// of the XCD's L2 -- right after a conv kernel, megabytes of its output.
-// !SC1: plain stores + agent release / acquire fences (the original form, kept for A/B).
+// of the XCD's L2 -- right after a conv kernel, megabytes of its output (the fenced form measured
+// ResNet-50 -1.5 %, profiles/r1_fin_sc1).
 typedef __attribute__((address_space(1))) unsigned long long gu64_t;
 typedef __attribute__((address_space(1))) int gi32_t;
 
@@ -326,7 +326,6 @@ __global__ __launch_bounds__(1024) void colsum_fin_direct_kernel(const float* __
   }
 }
 
-template <bool SC1>
 __global__ __launch_bounds__(256) void colsum_fin_kernel(const float* __restrict__ partial, int T, int C, int ns,
                                                          int k2, double* __restrict__ dpart, int* __restrict__ tickets,
                                                          FinArgs f) {
@@ -350,50 +349,31 @@ __global__ __launch_bounds__(256) void colsum_fin_kernel(const float* __restrict
   __syncthreads();
   if (rl == 0 && c < C) {
     for (int g = 1; g < 4; ++g) { a += r[0][g][lc]; b += r[1][g][lc]; }
-    if constexpr (SC1) {
-      __hip_atomic_store((gu64_t*)(dpart + (int64_t)s * 2 * C + c), (unsigned long long)__double_as_longlong(a),
-                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store((gu64_t*)(dpart + (int64_t)s * 2 * C + C + c), (unsigned long long)__double_as_longlong(b),
-                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    } else {
-      dpart[(int64_t)s * 2 * C + c] = a;
-      dpart[(int64_t)s * 2 * C + C + c] = b;
-    }
+    __hip_atomic_store((gu64_t*)(dpart + (int64_t)s * 2 * C + c), (unsigned long long)__double_as_longlong(a),
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store((gu64_t*)(dpart + (int64_t)s * 2 * C + C + c), (unsigned long long)__double_as_longlong(b),
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every storing wave drains
   __syncthreads();
   if (threadIdx.x == 0) {
-    if constexpr (!SC1) {
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
     last = __hip_atomic_fetch_add((gi32_t*)&tickets[blockIdx.x], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == S - 1;
   }
   __syncthreads();
   if (!last) return;
-  if (threadIdx.x == 0) {
-    if constexpr (!SC1) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
+  if (threadIdx.x == 0)
     __hip_atomic_store((gi32_t*)&tickets[blockIdx.x], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-  if constexpr (!SC1) __syncthreads();
-  else __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // compiler barrier only: loads stay below
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // compiler barrier only: loads stay below
   a = 0.0;
   b = 0.0;
   if (c < C) {
 #pragma unroll 4
     for (int q = rl; q < S; q += 4) {
-      if constexpr (SC1) {   // every load of the handed-off slices is an sc1 load (no L1 copy)
-        a += __longlong_as_double((long long)__hip_atomic_load((gu64_t*)(dpart + (int64_t)q * 2 * C + c),
-                                                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-        b += __longlong_as_double((long long)__hip_atomic_load((gu64_t*)(dpart + (int64_t)q * 2 * C + C + c),
-                                                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-      } else {
-        a += dpart[(int64_t)q * 2 * C + c];
-        b += dpart[(int64_t)q * 2 * C + C + c];
-      }
+      // every load of the handed-off slices is an sc1 load (no L1 copy)
+      a += __longlong_as_double((long long)__hip_atomic_load((gu64_t*)(dpart + (int64_t)q * 2 * C + c),
+                                                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+      b += __longlong_as_double((long long)__hip_atomic_load((gu64_t*)(dpart + (int64_t)q * 2 * C + C + c),
+                                                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
     }
   }
   __syncthreads();   // r is reused
@@ -710,16 +690,6 @@ extern "C" int* dlmpi_splitk_tickets(hipStream_t s, int n) {
   return g_sk_tk[dev][r];
 }
 
-static bool fused_finalize() {
-  static const bool v = true;
-  return v;
-}
-
-static bool fin_sc1() {   // false: the fenced hand-off (A/B)
-  static const bool v = true;
-  return v;
-}
-
 static int colsum_direct_max() { return kDirectMaxT; }   // the kernel holds <= kDirectMaxT rows
 
 static hipError_t colsum_finalize(const float* partial, int T, int C, int ns, int k2, double* ws, const FinArgs& f,
@@ -730,10 +700,9 @@ static hipError_t colsum_finalize(const float* partial, int T, int C, int ns, in
     hipLaunchKernelGGL(colsum_fin_direct_kernel, dim3((C + 15) / 16), dim3(1024), 0, s, partial, T, C, ns, k2, f);
     return hipGetLastError();
   }
-  int* tk = fused_finalize() && G <= 4096 ? fin_tickets(s) : nullptr;
+  int* tk = G <= 4096 ? fin_tickets(s) : nullptr;
   if (tk) {
-    if (fin_sc1()) hipLaunchKernelGGL(colsum_fin_kernel<true>, dim3(G, S), dim3(256), 0, s, partial, T, C, ns, k2, ws, tk, f);
-    else hipLaunchKernelGGL(colsum_fin_kernel<false>, dim3(G, S), dim3(256), 0, s, partial, T, C, ns, k2, ws, tk, f);
+    hipLaunchKernelGGL(colsum_fin_kernel, dim3(G, S), dim3(256), 0, s, partial, T, C, ns, k2, ws, tk, f);
   } else {
     hipLaunchKernelGGL(colsum2_kernel, dim3(G, S), dim3(256), 0, s, partial, T, C, ns, k2, ws);
     hipLaunchKernelGGL(finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, s, ws, S, C, f);

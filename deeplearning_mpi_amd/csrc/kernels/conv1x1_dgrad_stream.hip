@@ -360,15 +360,13 @@ extern "C" int dlmpi_dgs_blocks() {
 // communicator whose channels hold CUs).
 extern "C" int dlmpi_dgrad_stream_plan(int64_t M, int K, int Kout, int mask_mode, int z2, int has_res, int* bm, int* bn,
                                        int* G) {
-  static const int env = 1;
   const int blocks = dlmpi_dgs_blocks();
-  const int on = g_dgs_override >= 0 ? g_dgs_override : env;
+  const int on = g_dgs_override != 0;
   if (!on || M <= 0 || mask_mode < 0 || mask_mode > 2 || (z2 && mask_mode == 0)) return 0;
   // LDS per block (one block per CU): weights KS x BN x 128 B resident + A + 2 x epilogue operands
   if (K == 128 && Kout % 128 == 0) { *bm = 64; *bn = 128; }          // 98-146 KB
-  else if (K == 256 && Kout % 128 == 0) {   // 48 rows: 6 waves (3 x 2), 135-149 KB
-    static const int rows = 48;
-    *bm = (z2 || rows == 32) ? 32 : 48;
+  else if (K == 256 && Kout % 128 == 0) {   // 48 rows: 6 waves (3 x 2), 135-149 KB; 32 with z2
+    *bm = z2 ? 32 : 48;
     *bn = 128;
   }
   else if (K == 512 && Kout % 64 == 0) {
@@ -379,8 +377,7 @@ extern "C" int dlmpi_dgrad_stream_plan(int64_t M, int K, int Kout, int mask_mode
     // 32 x 64 tiles measured slower than the general kernel (layer3.0 conv1 dual 2x256 -> 512: 359 vs
     // 289 us; layer4 conv1 77 vs 69 us -- eight 64-wide columns re-read A, 4 waves per CU; ResNet-50
     // 12,802 / 12,803 vs 12,837 / 12,968 img/s, profiles/r3_dgrad_stream/v4)
-    static const bool k512 = false;
-    if (!k512 && g_dgs_override != 2 && *bm == 32) return 0;
+    if (g_dgs_override != 2 && *bm == 32) return 0;
   }
   else return 0;
   const int ntiles = Kout / *bn;

@@ -242,8 +242,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, const ConvPhase
         *reinterpret_cast<f32x4*>(yp + 4) = f32x4{v[4], v[5], v[6], v[7]};
       } else {
         uint16_t* yp = reinterpret_cast<uint16_t*>(a.y) + pix * a.ldy + a.yoff + c0;
-        if (a.nt_store) __builtin_nontemporal_store(pack8(v), reinterpret_cast<u32x4*>(yp));
-        else *reinterpret_cast<u32x4*>(yp) = pack8(v);
+        *reinterpret_cast<u32x4*>(yp) = pack8(v);
       }
     } else {   // narrow / unaligned output (e.g. the 1-channel UNet head written as fp32 [N,1,H,W])
 #pragma unroll

@@ -238,9 +238,8 @@ using namespace dlmpi;
 // 128-row Ko tiles where they fit (64-row tiles everywhere -- 156 instead of 252 VGPRs, room on every
 // SIMD for a wave of the concurrent data-gradient chain -- measured no better, profiles/r3_w3blocks)
 extern "C" int dlmpi_wgrad3_plan(int Ko, int C, int* kt, int* ct) {
-  static const int kt_max = 128;
   if (Ko % 64 || C % 64) return 0;
-  *kt = (Ko % 128 == 0 && kt_max >= 128) ? 128 : 64;
+  *kt = Ko % 128 == 0 ? 128 : 64;
   *ct = (*kt == 64 && C % 128 == 0) ? 128 : 64;
   return 1;
 }

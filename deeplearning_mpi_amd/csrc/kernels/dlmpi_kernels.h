@@ -141,7 +141,6 @@ struct ConvArgs {
   const void* z2;
   int ldz2, z2off;
   int nstat;                       // 2 (fwd: sum v, sum v^2; bwd: sum v, sum v*z) or 3 (bwd with z2)
-  int nt_store;                    // 1: non-temporal output stores (streaming outputs)
   int ntiles;
   int nphase;
   int splitk;                      // > 1: K split over blockIdx.y, last-arriver combine (set by the launcher)
