@@ -1139,8 +1139,11 @@ void conv2d_wgrad_pro(const at::Tensor& dy, int lddy, int dyoff, int Ko, const a
   // 3x3 / stride 1 / pad 1 without operand prologues (UNet DoubleConv, ResNet conv2): the
   // spatial-tile kernel (conv_wgrad3.hip) -- X staged once per 8 x 8 pixel block for all 9 taps.
   int kt = 0, ct = 0;
-  if (g_wgrad3_override != 0 && !a.f32 && pro_a == 0 && pro_b == 0 && R == 3 && S == 3 &&
-      stride == 1 && pad == 1 && P == H && Q == W && dlmpi_wgrad3_plan(Ko, C, &kt, &ct)) {
+  // Only where the 8 x 8 blocks are at least 3/4 full: 14^2 / 7^2 are (77 %), the 4^2 / 2^2 / 1^2 images
+  // of ResNet-18 on 32^2 CIFAR are not (25 % / 6 % / 2 %) and take the gather kernel.
+  const bool w3_full = 4 * H * W >= 3 * ceil_div(H, 8) * 8 * ceil_div(W, 8) * 8;
+  if (g_wgrad3_override != 0 && (w3_full || g_wgrad3_override == 1) && !a.f32 && pro_a == 0 && pro_b == 0 &&
+      R == 3 && S == 3 && stride == 1 && pad == 1 && P == H && Q == W && dlmpi_wgrad3_plan(Ko, C, &kt, &ct)) {
     dlmpi::Wgrad3Args b{};
     b.dy = ptr<uint16_t>(dy);
     b.ldy = lddy; b.dyoff = dyoff; b.Ko = Ko;
