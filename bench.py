@@ -259,7 +259,7 @@ def main():
             red_per_step = _native().wgrad_reduce_launches() - red0
     from deeplearning_mpi_amd.utils.profiler import ClockStamps
 
-    clk = ClockStamps(dev)   # in-kernel shader clock over the timed steps (two 32-wave stamp launches)
+    clk = ClockStamps(dev)   # in-kernel shader clock over the timed steps (two 1024-wave stamp launches, paired per CU)
     comm.barrier()
     sync()
     t0 = time.perf_counter()

@@ -1504,10 +1504,10 @@ void fill_(at::Tensor t, double v) {
   if (t.scalar_type() != at::kFloat || !t.is_contiguous()) throw std::runtime_error("fill_: contiguous fp32 tensor");
   check(dlmpi_fill_f32(ptr<float>(t), t.numel(), (float)v, cur_stream()), "fill");
 }
-// t: int64 [blocks][3] on the device (bench.py clock stamps)
+// t: int64 [blocks][4] on the device (bench.py clock stamps)
 void clock_stamp(at::Tensor t) {
-  if (t.scalar_type() != at::kLong || !t.is_contiguous() || t.dim() != 2 || t.size(1) != 3)
-    throw std::runtime_error("clock_stamp: contiguous int64 [blocks][3]");
+  if (t.scalar_type() != at::kLong || !t.is_contiguous() || t.dim() != 2 || t.size(1) != 4)
+    throw std::runtime_error("clock_stamp: contiguous int64 [blocks][4]");
   check(dlmpi_clock_stamp(reinterpret_cast<unsigned long long*>(t.data_ptr<int64_t>()), (int)t.size(0), cur_stream()),
         "clock_stamp");
 }

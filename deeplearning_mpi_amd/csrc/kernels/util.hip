@@ -79,13 +79,18 @@ extern "C" hipError_t dlmpi_gather(void* dst, const void* src, const int64_t* id
 // region give its mean shader clock per XCD: d(memtime) / d(realtime) x 100 MHz (MI355X_MICROARCH.md
 // DVFS item 6).  Blocks are dispatched round-robin over the 8 XCDs, so 32 blocks sample each a few
 // times.  Lanes 0-2 store one value each (vector stores of per-lane data).
+// One wave per block writes {XCC id, hardware id, s_memtime, s_memrealtime}.  The host pairs a start
+// and a stop stamp taken on the same CU (XCC id + the SE / SH / CU fields of HW_ID, bits 8-15): the
+// shader-clock counters of different CUs are not synchronised, so pairing by XCD alone mixes their
+// offsets into short windows.
 __global__ __launch_bounds__(64) void clock_stamp_kernel(unsigned long long* out) {
   const int l = threadIdx.x;
   const unsigned xcc = __builtin_amdgcn_s_getreg(20 | (3 << 11)) & 15u;   // hwreg(HW_REG_XCC_ID, 0, 4)
+  const unsigned hw = __builtin_amdgcn_s_getreg(4 | (31 << 11));         // hwreg(HW_REG_HW_ID, 0, 32)
   const unsigned long long t = __builtin_amdgcn_s_memtime();
   const unsigned long long r = __builtin_amdgcn_s_memrealtime();
-  const unsigned long long v = l == 0 ? (unsigned long long)xcc : (l == 1 ? t : r);
-  if (l < 3) out[3 * blockIdx.x + l] = v;
+  const unsigned long long v = l == 0 ? (unsigned long long)xcc : (l == 1 ? (unsigned long long)hw : (l == 2 ? t : r));
+  if (l < 4) out[4 * blockIdx.x + l] = v;
 }
 
 extern "C" hipError_t dlmpi_clock_stamp(unsigned long long* out, int blocks, hipStream_t s) {

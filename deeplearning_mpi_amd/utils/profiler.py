@@ -92,19 +92,21 @@ def throughput(images: int, seconds: float) -> float:
 
 class ClockStamps:
     """Mean shader clock of a GPU region, measured in-kernel: ``start()`` and
-    ``stop()`` each launch a stamp kernel (util.hip clock_stamp_kernel: 32 one-wave blocks writing
-    {XCC id, s_memtime, s_memrealtime}) on the current stream; after a synchronisation ``summary()``
-    pairs the two stamps per XCD: clock = d(memtime) / d(realtime) x 100 MHz.  Reports the mean over
-    the XCDs and their min / max, or None where the native library is absent."""
+    ``stop()`` each launch a stamp kernel (util.hip clock_stamp_kernel: BLOCKS one-wave blocks writing
+    {XCC id, HW_ID, s_memtime, s_memrealtime}) on the current stream; after a synchronisation
+    ``summary()`` pairs a start and a stop stamp taken on the same CU (the shader-clock counters of
+    different CUs are not synchronised): clock = d(memtime) / d(realtime) x 100 MHz per CU, the median
+    over each XCD's CUs, then the mean over the XCDs and their min / max.  None where the native
+    library is absent."""
 
-    BLOCKS = 32
+    BLOCKS = 1024   # ~4 per CU, so that most CUs get a stamp at both ends
 
     def __init__(self, device):
         from .._ext import has_native, native
 
         self.C = native() if has_native() and torch.device(device).type == "cuda" else None
         if self.C is not None:
-            self.buf = torch.zeros(2, self.BLOCKS, 3, dtype=torch.int64, device=device)
+            self.buf = torch.zeros(2, self.BLOCKS, 4, dtype=torch.int64, device=device)
 
     def start(self):
         if self.C is not None:
@@ -117,22 +119,28 @@ class ClockStamps:
     def summary(self):
         if self.C is None:
             return None
-        b = self.buf.cpu().tolist()
-        first = [{}, {}]
+        return self.digest(self.buf.cpu().tolist())
+
+    @staticmethod
+    def digest(b):
+        """b: [2][blocks][4] stamps (start, stop) -> the clock summary (pure, tested on the CPU)."""
+        ends = [{}, {}]
         for k in (0, 1):
-            for xcc, mt, rt in b[k]:
-                # per XCD: the earliest start stamp, the latest stop stamp
-                cur = first[k].get(xcc)
+            for xcc, hw, mt, rt in b[k]:
+                cu = (int(xcc), (int(hw) >> 8) & 0xFF)   # XCC + SE / SH / CU fields of HW_ID
+                cur = ends[k].get(cu)
+                # per CU: the earliest start stamp, the latest stop stamp
                 if cur is None or (rt < cur[1] if k == 0 else rt > cur[1]):
-                    first[k][xcc] = (mt, rt)
-        mhz = {}
-        for xcc, (mt0, rt0) in first[0].items():
-            if xcc in first[1]:
-                mt1, rt1 = first[1][xcc]
-                if rt1 > rt0:
-                    mhz[int(xcc)] = (mt1 - mt0) / (rt1 - rt0) * 100.0
-        if not mhz:
+                    ends[k][cu] = (mt, rt)
+        per_xcd = {}
+        for cu, (mt0, rt0) in ends[0].items():
+            if cu in ends[1]:
+                mt1, rt1 = ends[1][cu]
+                if rt1 > rt0 and mt1 > mt0:
+                    per_xcd.setdefault(cu[0], []).append((mt1 - mt0) / (rt1 - rt0) * 100.0)
+        if not per_xcd:
             return None
-        v = list(mhz.values())
+        v = [sorted(c)[len(c) // 2] for c in per_xcd.values()]
         return {"sclk_mhz": round(sum(v) / len(v), 1), "sclk_mhz_min": round(min(v), 1),
-                "sclk_mhz_max": round(max(v), 1), "xcds": len(v)}
+                "sclk_mhz_max": round(max(v), 1), "xcds": len(v),
+                "cus": sum(len(c) for c in per_xcd.values())}

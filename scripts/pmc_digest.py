@@ -47,7 +47,7 @@ def main():
         print(f"{k:32s} {c[k]:16.1f}")
     waves = c.get("SQ_WAVES")
     if "SQ_VALU_MFMA_BUSY_CYCLES" in c and "SQ_BUSY_CU_CYCLES" in c:
-        print(f"{'MFMA busy / CU busy':32s} {c['SQ_VALU_MFMA_BUSY_CYCLES'] / max(1.0, c['SQ_BUSY_CU_CYCLES']):16.3f}")
+        print(f"{'MFMA busy / CU busy / 4 SIMDs':32s} {c['SQ_VALU_MFMA_BUSY_CYCLES'] / max(1.0, c['SQ_BUSY_CU_CYCLES']) / 4:16.3f}")
     if waves:
         for k in ("SQ_INSTS_VALU", "SQ_INSTS_LDS", "SQ_INSTS_MFMA", "SQ_INSTS_SALU", "SQ_INSTS_VMEM_RD", "SQ_INSTS_VMEM_WR"):
             if k in c:
