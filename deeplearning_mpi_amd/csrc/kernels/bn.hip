@@ -283,14 +283,18 @@ typedef __attribute__((address_space(1))) int gi32_t;
 
 // Direct form for short partial columns (T <= 512 rows: the 14^2 / 7^2 ResNet layers): one
 // 1024-thread block per 16-channel group, 64 row lanes x 16 channels; every lane issues all of its
-// <= 8 row loads at once (predicated, no dependent chain), then a fixed-order LDS tree combines the
-// 64 row lanes and one lane per channel finalizes -- no slice stores, ticket or second pass.  (The
-// first form, 16 row lanes per 64 channels, walked up to 32 dependent loads per lane: 14 us per
-// call vs ~11 us for the sliced kernel.)
+// <= 8 row loads at once (predicated, no dependent chain), sums them in double, then a fixed-order
+// pairwise tree over the row lanes (rl += rl + s, s = 32 .. 1): s = 32 .. 4 cross waves through one
+// 8 KB LDS buffer, s = 2 and 1 are shuffles inside wave 0; one lane per channel finalizes -- no slice
+// stores, ticket or second pass.  (The first form, 16 row lanes per 64 channels, walked up to 32
+// dependent loads per lane: 14 us per call vs ~11 us for the sliced kernel.  The 17 KB all-LDS tree of
+// the same order often could not start beside a streaming conv on another stream holding 146 of the
+// CU's 160 KB of LDS: 19-103 us instead of ~5 in the ResNet-50 step.  256-thread forms with 4 row lanes
+// per thread ran ~9 us per call: 4x the load instructions per wave, profiles/r5_fin256.)
 constexpr int kDirectMaxT = 512;
 __global__ __launch_bounds__(1024) void colsum_fin_direct_kernel(const float* __restrict__ partial, int T, int C,
                                                                  int ns, int k2, FinArgs f) {
-  __shared__ double r[2][64][17];
+  __shared__ double r[2][32][16];
   const int lc = threadIdx.x & 15, rl = threadIdx.x >> 4;
   const int c = blockIdx.x * 16 + lc;
   constexpr int NR = kDirectMaxT / 64;
@@ -309,20 +313,28 @@ __global__ __launch_bounds__(1024) void colsum_fin_direct_kernel(const float* __
     a += (double)va[i];
     b += (double)vb[i];
   }
-  r[0][rl][lc] = a;
-  r[1][rl][lc] = b;
-  __syncthreads();
 #pragma unroll
-  for (int s = 32; s > 0; s >>= 1) {
+  for (int s = 32; s >= 4; s >>= 1) {
+    if (rl >= s && rl < 2 * s) {
+      r[0][rl - s][lc] = a;
+      r[1][rl - s][lc] = b;
+    }
+    __syncthreads();
     if (rl < s) {
-      r[0][rl][lc] += r[0][rl + s][lc];
-      r[1][rl][lc] += r[1][rl + s][lc];
+      a += r[0][rl][lc];
+      b += r[1][rl][lc];
     }
     __syncthreads();
   }
+  // s = 2, 1: row lanes 0..3 are wave 0 (row lane rl + s is lane + 16 s)
+  const double a2 = __shfl_down(a, 32, 64), b2 = __shfl_down(b, 32, 64);
+  if (rl < 2) { a += a2; b += b2; }
+  const double a1 = __shfl_down(a, 16, 64), b1 = __shfl_down(b, 16, 64);
   if (rl == 0 && c < C) {
-    if (f.mode == 0) fin_fwd(f, c, r[0][0][lc], r[1][0][lc]);
-    else fin_bwd(f, c, r[0][0][lc], r[1][0][lc], C);
+    a += a1;
+    b += b1;
+    if (f.mode == 0) fin_fwd(f, c, a, b);
+    else fin_bwd(f, c, a, b, C);
   }
 }
 
