@@ -58,6 +58,20 @@ __global__ __launch_bounds__(256) void cast_weights_kernel(const CastEntry* __re
     }
     return;
   }
+  // Identity layout (no padding, the source row-major in the destination's order: the forward copy of
+  // every conv whose channels need no padding -- the masters are stored [K][R][S][C] already): a plain
+  // vectorized cast, 8 elements per thread (two 16-B loads, one 16-B store for bf16).
+  if (e.valid[0] == D0 && e.valid[1] == D1 && e.valid[2] == D2 && e.valid[3] == D3 && e.st[3] == 1 &&
+      e.st[2] == D3 && e.st[1] == (int64_t)D2 * D3 && e.st[0] == (int64_t)D1 * D2 * D3 && (n & 7) == 0 &&
+      ((uintptr_t)e.src & 15) == 0 && ((uintptr_t)dst & (8 * sizeof(T) - 1)) == 0) {
+    const int64_t n8 = n >> 3;
+    for (int64_t q = sub * (int64_t)blockDim.x + threadIdx.x; q < n8; q += (int64_t)nsub * blockDim.x) {
+      const f32x4 a0 = reinterpret_cast<const f32x4*>(e.src)[2 * q], a1 = reinterpret_cast<const f32x4*>(e.src)[2 * q + 1];
+      const float v[8] = {a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]};
+      store8(dst + 8 * q, v);
+    }
+    return;
+  }
   // Direct path.  When the entry's destination and source extents fit 32-bit indices (every
   // conv / linear weight does) and rows are a multiple of 4 wide, each lane produces 4
   // consecutive destination elements with one 4-element store and one 32-bit index decomposition
