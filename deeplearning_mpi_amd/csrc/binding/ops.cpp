@@ -161,6 +161,18 @@ static int pipe_select(int f32, int pro, int cin, int64_t M, int Kout, int64_t r
   return (bm == 128 ? 4 : 2) + 1;
 }
 
+// ---- the producer's BN-apply fused into a 1x1 consumer (conv_igemm.hip conv1x1_apply_kernel) ----
+// pro-3 launches whose Kout is one 64 / 128 / 256-channel tile column run the register-staged kernel
+// (128-row tiles) instead of the single-stage pro-3 conv_igemm_kernel.  set_conv_apply(0): the latter.
+static int g_apply_override = -1;
+static bool apply_kernel(int f32, int pro, int C, int K, int R, int S, int stride, int pad) {
+  return g_apply_override != 0 && pro == 3 && !f32 && R == 1 && S == 1 && stride == 1 && pad == 0 &&
+         dlmpi_conv1x1_apply_ok(C, K);
+}
+// 128-row tiles (64-row tiles for Kout 256, one block per CU by LDS: 134.5 vs 102.8 us at 14^2
+// 1024->256, profiles/r5_apply)
+static int apply_bm(int) { return 128; }
+
 // ---- 2-D halo tiles for 3x3 / stride-1 / pad-1 convolutions (conv_igemm.hip HALO) ----------------
 // set_conv_halo(0) (tests): these convolutions through the im2col gather path too.
 static int g_halo_override = -1;   // dlmpi_ext set_conv_halo (tests)
@@ -552,6 +564,15 @@ int conv2d_fwd_bn_apply(const at::Tensor& x, int N, int H, int W, int C, int ldx
   }
 }
 
+// the BN finalize of a forward conv's statistics [rows][2][K]
+static void run_fin_after(const at::Tensor& stats, int rows, int K, const FinArgs* fin) {
+  at::Tensor ws = colsum_ws(stats, rows, K);
+  check(dlmpi_bn_finalize(ptr<float>(stats), rows, K, fin->count, fin->gamma, fin->beta, fin->running_mean,
+                          fin->running_var, fin->momentum, fin->eps, fin->scale, fin->shift, fin->save_mean,
+                          fin->save_invstd, ptr<double>(ws), cur_stream()),
+        "bn_finalize");
+}
+
 static int conv2d_fwd_impl(const at::Tensor& x, int N, int H, int W, int C, int ldx, int xoff, const at::Tensor& w, int K, int R,
                int S, int stride, int pad, at::Tensor y, int ldy, int yoff, const c10::optional<at::Tensor>& bias,
                const c10::optional<at::Tensor>& res, int ldres, int resoff, const c10::optional<at::Tensor>& scale,
@@ -660,9 +681,14 @@ static int conv2d_fwd_impl(const at::Tensor& x, int N, int H, int W, int C, int 
       }
     }
   }
-  a.ntiles = ceil_div(K, bn);
   if (pro == 3 && (R != 1 || S != 1 || stride != 1 || pad != 0))
     throw std::runtime_error("conv prologue 3: a 1x1 / stride-1 conv");
+  const bool fused_apply = bm_req <= 0 && bn_req <= 0 && apply_kernel(a.f32, pro, C, K, R, S, stride, pad);
+  if (fused_apply) {
+    bm = apply_bm(K);
+    bn = K;
+  }
+  a.ntiles = ceil_div(K, bn);
   a.nphase = 1;
   ConvPhase& p = a.ph[0];
   p.P = P; p.Q = Q; p.Tr = R; p.Ts = S;
@@ -670,6 +696,13 @@ static int conv2d_fwd_impl(const at::Tensor& x, int N, int H, int W, int C, int 
   p.wr0 = 0; p.wrs = 1; p.ws0 = 0; p.wss = 1;
   p.oh0 = 0; p.ow0 = 0;
   finish_phase(p, N, C, bm, a.f32);
+  if (fused_apply) {
+    if (fin != nullptr && (!a.stats || stats->size(0) < p.mtiles))
+      throw std::runtime_error("conv2d_fwd_bn: stats [mtiles][2][K] required");
+    check(dlmpi_conv1x1_apply(&a, bm, cur_stream()), "conv2d_fwd (fused apply 1x1)");
+    if (fin != nullptr) run_fin_after(*stats, p.mtiles, K, fin);
+    return p.mtiles;
+  }
   if (halo) apply_halo(a, N, bm);
   g_halo_ran = halo ? 1 : 0;
   // autotuned tiling: BN-stats launches only through conv2d_fwd_bn (its buffer is sized for the
@@ -760,6 +793,7 @@ int conv2d_fwd_mtiles_pro(int N, int H, int W, int C, int K, int R, int S, int s
   if (bm_req <= 0 && stream1x1_shape((int64_t)N * P * Q, C, K, R, S, stride, pad, pro, f32, bm, bn, G)) return G;
   int th, tw;
   if (bm_req <= 0 && stream3x3_shape(N, H, W, C, K, R, S, stride, pad, pro, f32, th, tw, G)) return G;
+  if (bm_req <= 0 && apply_kernel(f32, pro, C, K, R, S, stride, pad)) return ceil_div((int64_t)N * P * Q, apply_bm(K));
   if (bm_req <= 0) {
     int hbm, hbn;
     pick_tiles((int64_t)N * P * Q, K, (int64_t)R * S * C, C, hbm, hbn, pro != 0);
@@ -1633,6 +1667,7 @@ void register_ops(pybind11::module& m) {
   m.def("set_conv_splitk", [](int n) { g_splitk_override = n; });
   m.def("set_conv_pipe_dgrad", [](int mode) { g_pipe_dgrad_override = mode; });
   m.def("set_conv_pipe", [](int mode) { g_pipe_override = mode; });
+  m.def("set_conv_apply", [](int mode) { g_apply_override = mode; });
   m.def("set_conv3_stream", [](int mode) { dlmpi_set_conv3_stream(mode); });
   m.def("conv3_stream_last", []() { return g_conv3_ran; });
   m.def("set_dgs_blocks", [](int n) { dlmpi_set_dgs_blocks(n); });

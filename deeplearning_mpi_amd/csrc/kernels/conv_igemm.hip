@@ -864,6 +864,181 @@ __global__ __launch_bounds__(64 * WGM * WGN) __attribute__((amdgpu_waves_per_eu(
   conv_epilogue<BM, BN, NT, WGM, WGN, uint16_t, false>(a, ph, acc, smem, tid, m0, n0, mt, 0, 0, 0);
 }
 
+// ---- the producer's BN-apply fused into a 1x1 consumer, register-staged ----------------------------
+// conv1x1_apply_kernel: pro-3 launches (ConvArgs::pro 3: x = the producer BN's input z, pz its
+// residual) of a 1x1 / stride-1 conv whose Kout (64 / 128 / 256) is ONE output tile column, so every
+// input element is applied exactly once.  The single-stage pro-3 path of conv_igemm_kernel stages z
+// and the residual by LDS-DMA, rewrites them in LDS after a barrier and only then runs the MFMAs: a
+// memory-bound GEMM with no load in flight while it computes (ResNet-50 28^2 512->128: 215 us vs
+// 115 + 58 us for the apply pass and the plain conv).  Here every K-step (64 channels) goes
+//   global z / residual / weight pieces -> VGPRs (issued one K-step ahead, under the MFMAs)
+//   -> y = relu(z * scale + shift + r) in registers (bn_apply_kernel's fma order: bit-identical y)
+//   -> y and its ReLU mask bits to global, y and the weights into the LDS stage of the next K-step
+// with two LDS stages and ONE barrier per K-step (the stage written at step k was last read at
+// step k - 1, before the previous barrier).  128-row tiles, 8 waves, conv_epilogue (statistics, bias).
+template <int BM, int BN, int WGM, int WGN>
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(BN <= 128 ? 4 : 2, 8)))
+void conv1x1_apply_kernel(const ConvArgs a) {
+  constexpr int NT = 512;
+  static_assert(WGM * WGN == 8, "8 waves");
+  constexpr int WM = BM / WGM, WN = BN / WGN, TM = WM / 16, TN = WN / 16;
+  constexpr int A_BYTES = BM * 128, B_BYTES = BN * 128, SB = A_BYTES + B_BYTES;
+  constexpr int MAXC = 4 * BN;                // the apply's per-channel vectors live in LDS (C <= MAXC)
+  constexpr int PRM_BYTES = 4 * MAXC * 4;     // scale, shift, residual scale, residual shift
+  constexpr int EPI_NEED = EpiSmem<BM, BN, NT, WM>::bytes;
+  constexpr int SMEM = 2 * SB + PRM_BYTES > EPI_NEED ? 2 * SB + PRM_BYTES : EPI_NEED;
+  constexpr int RP = NT / 8;                  // 64 tile rows per pass (8 lanes per 128-B row)
+  constexpr int AL = BM / RP, BL = BN / RP;   // pieces per thread per K-step
+  static_assert(AL >= 1 && BL >= 1, "tile shape");
+  __shared__ __attribute__((aligned(16))) char smem[SMEM];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wid / WGN, wn = wid % WGN;
+  const int lrow = tid >> 3, jc = tid & 7;    // row lrow + RP i, 16-B chunk jc (channels 8 jc ..)
+  const ConvPhase& ph = a.ph[0];
+  const int M = a.Nimg * ph.P * ph.Q;
+  const uint32_t mt = xcd_remap(blockIdx.x, (uint32_t)ph.mtiles);
+  const int m0 = (int)mt * BM;
+  const int C = a.C, nk = C / 64;
+  const bool rbn = a.prscale != nullptr;
+
+  // per-channel vectors -> LDS once (read back per piece: no global loads in the K loop besides the
+  // operands, and 16 fewer VGPRs than holding them)
+  float* prm = reinterpret_cast<float*>(smem + 2 * SB);
+  for (int i = tid; i < C; i += NT) {
+    prm[i] = a.pscale[i];
+    prm[MAXC + i] = a.pshift[i];
+    if (rbn) {
+      prm[2 * MAXC + i] = a.prscale[i];
+      prm[3 * MAXC + i] = a.prshift[i];
+    }
+  }
+
+  // 32-bit element offsets of this thread's rows (< 2^31: host-checked); 1x1 / stride 1 / pad 0:
+  // the input pixel is the tile row
+  const uint16_t* xb = static_cast<const uint16_t*>(a.x);
+  const uint16_t* rb = static_cast<const uint16_t*>(a.pz);
+  uint32_t zo[AL], ro[AL], yo[AL], bo[AL];
+  uint32_t okm = 0;
+#pragma unroll
+  for (int i = 0; i < AL; ++i) {
+    const int m = m0 + lrow + RP * i;
+    if (m < M) okm |= 1u << i;
+    const uint32_t mm = m < M ? (uint32_t)m : 0u;
+    zo[i] = mm * (uint32_t)a.ldx + (uint32_t)a.xoff + 8 * jc;
+    ro[i] = mm * (uint32_t)a.ldpz + (uint32_t)a.pzoff + 8 * jc;
+    yo[i] = mm * (uint32_t)a.ldpy + (uint32_t)a.pyoff + 8 * jc;
+    bo[i] = mm * (uint32_t)(C >> 3) + jc;
+  }
+  const uint16_t* wb = static_cast<const uint16_t*>(a.w) + (int64_t)lrow * a.ldw + 8 * jc;   // Kout == BN
+  const int64_t wstep = (int64_t)RP * a.ldw;
+
+  u32x4 zv[AL], rv[AL], wv[BL];
+  auto load = [&](int k) {
+    const int c = 64 * k;
+#pragma unroll
+    for (int i = 0; i < AL; ++i) {
+      zv[i] = *reinterpret_cast<const u32x4*>(xb + zo[i] + c);
+      rv[i] = *reinterpret_cast<const u32x4*>(rb + ro[i] + c);
+    }
+#pragma unroll
+    for (int i = 0; i < BL; ++i) wv[i] = *reinterpret_cast<const u32x4*>(wb + i * wstep + c);
+  };
+  // y of the loaded pieces -> global (+ mask bits) and the LDS stage `buf`; weights -> the stage
+  auto commit = [&](int k, int buf) {
+    char* As = smem + buf * SB;
+    char* Bs = As + A_BYTES;
+    const int cc = 64 * k + 8 * jc;
+    const f32x4 s0 = *reinterpret_cast<const f32x4*>(prm + cc), s1 = *reinterpret_cast<const f32x4*>(prm + cc + 4);
+    const f32x4 h0 = *reinterpret_cast<const f32x4*>(prm + MAXC + cc);
+    const f32x4 h1 = *reinterpret_cast<const f32x4*>(prm + MAXC + cc + 4);
+#pragma unroll
+    for (int i = 0; i < AL; ++i) {
+      const int r = lrow + RP * i;
+      u32x4 pk = u32x4{0u, 0u, 0u, 0u};   // rows past M: zeros (their outputs are dropped)
+      if ((okm >> i) & 1) {
+        float v[8], q[8];
+        unpack8(zv[i], v);
+        unpack8(rv[i], q);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          v[e] = __builtin_fmaf(v[e], s0[e], h0[e]);
+          v[e + 4] = __builtin_fmaf(v[e + 4], s1[e], h1[e]);
+        }
+        if (rbn) {
+          const f32x4 a0 = *reinterpret_cast<const f32x4*>(prm + 2 * MAXC + cc);
+          const f32x4 a1 = *reinterpret_cast<const f32x4*>(prm + 2 * MAXC + cc + 4);
+          const f32x4 b0 = *reinterpret_cast<const f32x4*>(prm + 3 * MAXC + cc);
+          const f32x4 b1 = *reinterpret_cast<const f32x4*>(prm + 3 * MAXC + cc + 4);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            q[e] = __builtin_fmaf(q[e], a0[e], b0[e]);
+            q[e + 4] = __builtin_fmaf(q[e + 4], a1[e], b1[e]);
+          }
+        }
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e] + q[e], 0.f);
+        pk = pack8(v);
+        *reinterpret_cast<u32x4*>(a.py + yo[i] + 64 * k) = pk;
+        uint32_t b = 0;
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          b |= (uint32_t)((pk[t] & 0xffffu) != 0u && !(pk[t] & 0x8000u)) << (2 * t);
+          b |= (uint32_t)((pk[t] >> 16) != 0u && !(pk[t] & 0x80000000u)) << (2 * t + 1);
+        }
+        a.pmbits[bo[i] + 8 * k] = (uint8_t)b;
+      }
+      *reinterpret_cast<u32x4*>(As + r * 128 + ((jc ^ (r & 7)) << 4)) = pk;
+    }
+#pragma unroll
+    for (int i = 0; i < BL; ++i) {
+      const int r = lrow + RP * i;
+      *reinterpret_cast<u32x4*>(Bs + r * 128 + ((jc ^ (r & 7)) << 4)) = wv[i];
+    }
+  };
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int mi = 0; mi < TM; ++mi)
+#pragma unroll
+    for (int ni = 0; ni < TN; ++ni) acc[mi][ni] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int fr = lane & 15, fg = lane >> 4;
+
+  load(0);
+  __syncthreads();   // the per-channel vectors are in LDS
+  commit(0, 0);
+  __syncthreads();
+  for (int k = 0; k < nk; ++k) {
+    if (k + 1 < nk) load(k + 1);   // in flight under this step's MFMAs
+    const char* As = smem + (k & 1) * SB;
+    const char* Bs = As + A_BYTES;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      bf16x8 af[TM], bfr[TN];
+      const int ch = kk * 4 + fg;
+#pragma unroll
+      for (int mi = 0; mi < TM; ++mi) {
+        const int r = wm * WM + mi * 16 + fr;
+        af[mi] = *reinterpret_cast<const bf16x8*>(As + r * 128 + ((ch ^ (r & 7)) << 4));
+      }
+#pragma unroll
+      for (int ni = 0; ni < TN; ++ni) {
+        const int r = wn * WN + ni * 16 + fr;
+        bfr[ni] = *reinterpret_cast<const bf16x8*>(Bs + r * 128 + ((ch ^ (r & 7)) << 4));
+      }
+#pragma unroll
+      for (int mi = 0; mi < TM; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < TN; ++ni)
+          acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[mi], bfr[ni], acc[mi][ni], 0, 0, 0);
+    }
+    if (k + 1 < nk) commit(k + 1, (k + 1) & 1);   // the stage read at step k - 1 (before the last barrier)
+    __syncthreads();
+  }
+  conv_epilogue<BM, BN, NT, WGM, WGN, uint16_t, false>(a, ph, acc, smem, tid, m0, 0, (int)mt, 0, 0, 0);
+}
+
 }  // namespace dlmpi
 
 using namespace dlmpi;
@@ -919,6 +1094,28 @@ static hipError_t launch_pipe(const ConvArgs* a, int bm, int bn, int var, dim3 g
   else if (bm == 256 && bn == 128) hipLaunchKernelGGL((conv_pipe_kernel<256, 128, 4, 2, 3, 2>), grid, dim3(512), 0, s, *a);
   else if (bm == 128 && bn == 256) hipLaunchKernelGGL((conv_pipe_kernel<128, 256, 2, 4, 3, 4>), grid, dim3(512), 0, s, *a);
   else if (bm == 512 && bn == 64) hipLaunchKernelGGL((conv_pipe_kernel<512, 64, 8, 1, 2, 2>), grid, dim3(512), 0, s, *a);
+  else return hipErrorInvalidValue;
+  return hipGetLastError();
+}
+
+// The fused apply + 1x1 kernel applies (shape only; the launch checks the rest)
+extern "C" int dlmpi_conv1x1_apply_ok(int C, int K) {
+  return C % 64 == 0 && C <= 4 * K && (K == 64 || K == 128 || K == 256);   // C <= 4 K: the LDS vectors
+}
+
+extern "C" hipError_t dlmpi_conv1x1_apply(const ConvArgs* a, int bm, hipStream_t s) {
+  if (a->pro != 3 || a->f32 || a->halo || a->nphase != 1 || a->ntiles != 1 || !a->vec_store || a->res ||
+      a->scale || a->relu || a->mask || a->mscale || a->mbits || a->z || a->splitk_req > 1 ||
+      !dlmpi_conv1x1_apply_ok(a->C, a->Kout) || a->ph[0].Tr != 1 || a->ph[0].Ts != 1 || a->sa != 1 ||
+      a->ph[0].mtiles != (a->Nimg * a->ph[0].P * a->ph[0].Q + bm - 1) / bm || a->ldw != a->C ||
+      (int64_t)a->Nimg * a->H * a->W * (a->ldx > a->ldpz ? (a->ldx > a->ldpy ? a->ldx : a->ldpy)
+                                                          : (a->ldpz > a->ldpy ? a->ldpz : a->ldpy)) >= (1ll << 31))
+    return hipErrorInvalidValue;
+  const dim3 grid((unsigned)a->ph[0].mtiles);
+  if (grid.x == 0) return hipSuccess;
+  if (bm == 128 && a->Kout == 64) hipLaunchKernelGGL((conv1x1_apply_kernel<128, 64, 8, 1>), grid, dim3(512), 0, s, *a);
+  else if (bm == 128 && a->Kout == 128) hipLaunchKernelGGL((conv1x1_apply_kernel<128, 128, 4, 2>), grid, dim3(512), 0, s, *a);
+  else if (bm == 128 && a->Kout == 256) hipLaunchKernelGGL((conv1x1_apply_kernel<128, 256, 2, 4>), grid, dim3(512), 0, s, *a);
   else return hipErrorInvalidValue;
   return hipGetLastError();
 }

@@ -260,6 +260,10 @@ hipError_t dlmpi_conv_igemm(const dlmpi::ConvArgs* a, int bm, int bn, hipStream_
 // pipe = 1: the pipelined 8-wave kernel (tiles 256x256, 256x128, 128x256, 256x64, 512x64; bf16,
 // C % 64 == 0, no prologue / halo / split); pipe = 0: dlmpi_conv_igemm
 hipError_t dlmpi_conv_igemm_ex(const dlmpi::ConvArgs* a, int bm, int bn, int pipe, hipStream_t s);
+// pro-3 (fused producer BN-apply) 1x1 / stride-1 launches with one 64 / 128 / 256-channel output
+// column: the register-staged kernel (conv_igemm.hip conv1x1_apply_kernel), 128-row tiles
+int dlmpi_conv1x1_apply_ok(int C, int K);
+hipError_t dlmpi_conv1x1_apply(const dlmpi::ConvArgs* a, int bm, hipStream_t s);
 hipError_t dlmpi_conv_wgrad(const dlmpi::WgradArgs* a, int bm, int bn, hipStream_t s);   // bn: 128 | 256
 // sum of split partials -> grad (accumulated), with channel un-padding and row limit
 hipError_t dlmpi_wgrad_reduce(const float* ws, int splits, int Ko, int T, int Cpad, int Creal,

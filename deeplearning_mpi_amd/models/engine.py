@@ -139,13 +139,12 @@ DUAL_WGRAD_PRO = True
 # profiles/r2_chunk_fwd_rejected -- and was removed, as was rebuilding bn2 in the streaming conv3's
 # prologue: bit-identical but neutral, profiles/r3_stream_pro.)
 FUSE_APPLY = True
-# Only the 64-output-channel consumers (ResNet-50 layer-1 conv1, 56^2 256->64): there the fused GEMM
-# moves the apply's 1.3 GB at 4.3 TB/s (298 us vs 248 + 95 us unfused).  The layer-2 conv1 (28^2
-# 512->128) fused ran 215 us vs ~115 + 58 us unfused -- the single-stage GEMM does not stream the
-# apply's bytes as fast as the apply kernel -- so 128 lost: same box ResNet-50 13,226 / 13,225 (64) vs
-# 13,177 / 13,187 (128) vs 13,108 / 13,128 (off), ResNet-152 4,752 / 4,755 vs 4,744 / 4,733
-# (profiles/r5_policy).
-FUSE_APPLY_MAX_K = 64
+# Consumers of one 64 / 128 / 256-channel output column (ResNet-50 conv1 of layers 1-3) run the
+# register-staged kernel (conv_igemm.hip conv1x1_apply_kernel): isolated, 56^2 256->64 277 us vs 292
+# (the single-stage pro-3 kernel) / 335 (apply pass + conv), 28^2 512->128 162 vs 214 / 194, 14^2
+# 1024->256 103 vs 194 / 106 (107 vs 202 / 119 with a BN-output residual), profiles/r5_apply.  (With the
+# single-stage kernel only 64 channels paid: 128 lost in the step, profiles/r5_policy.)
+FUSE_APPLY_MAX_K = 256
 
 # The step's last weight gradient (a unit with ``wgrad_main``: the ResNet stem, whose input needs no
 # gradient) runs on the main stream -- idle by then -- instead of queueing behind the side stream's

@@ -53,9 +53,11 @@ def test_conv_fwd_bn_apply_matches_unfused(shape):
     w = (torch.randn(K, 1, 1, C, device=DEV, generator=g) / C ** 0.5).to(torch.bfloat16)
     gamma, beta = torch.rand(K, device=DEV, generator=g) + 0.5, torch.randn(K, device=DEV, generator=g)
     out = {}
-    # the unfused conv on the single-stage kernel too (the fused prologue's kernel, same split-K plan):
-    # the pipelined kernel would sum a small grid unsplit, i.e. in another order
+    # the unfused conv on the single-stage kernel, unsplit: the fused kernel (conv1x1_apply_kernel)
+    # never splits K, and the pipelined kernel would tile differently -- every output element then
+    # sums its K in the same order in both schedules
     be.C.set_conv_pipe(0)
+    be.C.set_conv_splitk(1)
     for fused in (True, False):
         y = Act.empty(N, H, W, C, torch.bfloat16, DEV)
         y.buf.fill_(7.0)
@@ -74,6 +76,7 @@ def test_conv_fwd_bn_apply_matches_unfused(shape):
         torch.cuda.synchronize()
         out[fused] = (y.buf.clone(), mb.clone(), z.buf.clone(), st.double().sum(0), v.clone(), rm.clone(), rv.clone())
     be.C.set_conv_pipe(-1)
+    be.C.set_conv_splitk(0)
     a, b = out[True], out[False]
     assert torch.equal(a[0], b[0])          # the stored apply output
     assert torch.equal(a[1], b[1])          # its ReLU mask bits
