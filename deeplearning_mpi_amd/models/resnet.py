@@ -18,7 +18,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from ..ops.act import Act, padc
-from .engine import BwdFuse, ConvUnit, EngineModule, S2DConvUnit, record_on, resolve
+from .engine import PendingApply, BwdFuse, ConvUnit, EngineModule, S2DConvUnit, record_on, resolve
 
 
 def conv3x3(i, o, stride=1):
@@ -105,7 +105,12 @@ class _BlockExec:
         stream it runs beside conv1 -> conv2 and joins before the residual add of conv3's BN."""
         ctxs = []
         lazy = train and save   # the block output's BN-apply may run inside its consumer (PendingApply)
+        first = None
         if self.ud is not None:   # the branch reads the whole block input
+            if isinstance(x, PendingApply) and self.u[0].can_fuse_apply(be, x, train, save):
+                # the previous block's BN-apply runs inside conv1 (which stores it); the branch reads
+                # the stored output after conv1 instead of both reading a separate apply pass's output
+                first = self.u[0].fwd(be, x, train, save=save, lazy=lazy)
             x = resolve(be, x)
         # the downsample BN output is read once, as the residual of the last unit's BN-apply: applied
         # there on the fly (Deferred.bn), which removes its own apply pass (read z_ds + write idn)
@@ -125,7 +130,10 @@ class _BlockExec:
         if br is not None:
             idn, cd = branch_fwd(x)
         h = x
-        for u in self.u[:-1]:
+        if first is not None:
+            h = first[0]
+            ctxs.append(first[1])
+        for u in self.u[1 if first is not None else 0:-1]:
             h, c = u.fwd(be, h, train, save=save, lazy=lazy)
             ctxs.append(c)
         join = None

@@ -117,10 +117,11 @@ def test_resnet50_step_fused_apply_vs_unfused(monkeypatch):
         calls[on] = n[0]
         del be
     torch.cuda.synchronize()
-    # layer1.1, layer1.2 (conv1 of 64 channels, identity blocks), + layer2.1..3 (128) with
-    # FUSE_APPLY_MAX_K >= 128, + layer3.1..5 (1024 -> 256: two output tile columns) with >= 256
+    # layer1.1, layer1.2 (conv1 of 64 channels, identity blocks), + layer2.0 (the downsample block:
+    # its branch then reads conv1's stored apply) and layer2.1..3 (128) with FUSE_APPLY_MAX_K >= 128,
+    # + layer3.0..5 (256) with >= 256
     K = engine.FUSE_APPLY_MAX_K
-    assert calls[True] == 2 + (3 if K >= 128 else 0) + (5 if K >= 256 else 0)
+    assert calls[True] == 2 + (4 if K >= 128 else 0) + (6 if K >= 256 else 0)
     # a fused conv1 may pick another M tile than the unfused conv (operand-prologue tile rules), i.e.
     # another fp32 order of its BN statistics.  A random-init bf16
     # ResNet-50 is chaotic under such perturbations: switching ONLY the statistics summation order
