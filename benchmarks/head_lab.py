@@ -1,0 +1,58 @@
+"""UNet head (1x1 conv, 64 -> 1, fp32 logits, bias) at bench scale: the streaming dot-product kernel
+(csrc/kernels/head.hip) vs the GEMM path (set_head1x1 0), interleaved rounds.
+
+python benchmarks/head_lab.py [--iters 20] [--rounds 3]
+"""
+import argparse
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import torch  # noqa: E402
+
+
+def timeit(fn, iters):
+    for _ in range(3):
+        fn()
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(iters):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / iters * 1e3
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--rounds", type=int, default=3)
+    a = ap.parse_args()
+    from deeplearning_mpi_amd.ops.act import Act
+    from deeplearning_mpi_amd.ops.backend import NativeBackend
+
+    be = NativeBackend("cuda")
+    for N, H, W in ((16, 512, 512), (16, 1024, 1024)):
+        M, C, Kp = N * H * W, 64, 8
+        x = Act(torch.randn(M, C, device="cuda").to(torch.bfloat16), N, H, W, C)
+        w = (torch.randn(Kp, C, device="cuda") / 8).to(torch.bfloat16)
+        b = torch.randn(Kp, device="cuda")
+        y = Act(torch.empty(M, 1, device="cuda"), N, H, W, 1)
+        res = {}
+        for _ in range(a.rounds):
+            for name, on in (("head", 1), ("gemm", 0)):
+                be.C.set_head1x1(on)
+                try:
+                    t = timeit(lambda: be.conv_fwd(x, w, Kp, 1, 1, 1, 0, y, bias=b, kvalid=1), a.iters)
+                finally:
+                    be.C.set_head1x1(1)
+                res[name] = round(min(res.get(name, 1e9), t), 1)
+        res["head_TBps"] = round(M * C * 2 / res["head"] / 1e6, 2)
+        print(json.dumps({"shape": [N, H, W, C], "us": res}), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -460,6 +460,8 @@ static bool stream1x1_shape(int64_t M, int C, int K, int R, int S, int stride, i
 // decision, as stream1x1_shape (its statistics have G rows, one per block).  Its grid shares the
 // RCCL-aware budget of the streaming data gradient (one block per CU).
 static int g_conv3_ran = 0;   // 1 if the last conv2d_fwd / conv2d_dgrad ran the streaming 3x3 kernel (tests)
+static int g_head_ran = 0;           // 1 if the last conv2d_fwd ran the 1x1 head kernel (head.hip)
+static int g_head_on = 1;            // dlmpi_ext set_head1x1 (A/B)
 static bool stream3x3_shape(int N, int H, int W, int C, int K, int R, int S, int stride, int pad, int pro, int f32,
                             int& th, int& tw, int& G) {
   if (R != 3 || S != 3 || stride != 1 || pad != 1 || pro != 0 || f32) return false;
@@ -616,6 +618,20 @@ static int conv2d_fwd_impl(const at::Tensor& x, int N, int H, int W, int C, int 
   }
   g_stream_ran = 0;
   g_conv3_ran = 0;
+  g_head_ran = 0;
+  {  // <= 4 output channels, 1x1, no epilogue beyond the bias (the UNet head): a streaming dot product
+    const int kv = a.kvalid > 0 ? a.kvalid : K;
+    if (g_head_on && bm_req <= 0 && bn_req <= 0 && pro == 0 && !a.f32 && R == 1 && S == 1 && stride == 1 &&
+        pad == 0 && !stats.has_value() && !res.has_value() && !scale.has_value() && !relu && fin == nullptr &&
+        dlmpi_head1x1_ok(C, kv) && ldx % 8 == 0 && xoff % 8 == 0 &&
+        (y.scalar_type() == at::kFloat || y.scalar_type() == at::kBFloat16)) {
+      check(dlmpi_head1x1(a.x, ldx, xoff, (int64_t)N * H * W, C, a.w, a.ldw, a.bias, a.y, ldy, yoff, kv,
+                          y.scalar_type() == at::kFloat ? 1 : 0, cur_stream()),
+            "conv2d_fwd (1x1 head)");
+      g_head_ran = 1;
+      return 0;
+    }
+  }
   {  // streaming 3x3 kernel (64 -> 64: the full-resolution UNet layers, ResNet layer-1 conv2)
     int th, tw, G;
     if (bm_req <= 0 && bn_req <= 0 && stream3x3_shape(N, H, W, C, K, R, S, stride, pad, pro, a.f32, th, tw, G)) {
@@ -1651,6 +1667,8 @@ void register_ops(pybind11::module& m) {
   m.def("set_conv_autotune", [](int mode) { g_autotune_override = mode; });
   m.def("set_wgrad3", [](int mode) { g_wgrad3_override = mode; });
   m.def("set_wgrad3_blocks", [](int n) { g_wgrad3_blocks = n; });
+  m.def("set_head1x1", [](int v) { g_head_on = v; });
+  m.def("head1x1_last", []() { return g_head_ran; });
   m.def("set_wgrad_defer", [](bool on) {
     if (!on) wgrad_flush();
     g_wgrad_defer = on;
