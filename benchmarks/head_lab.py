@@ -1,5 +1,7 @@
-"""UNet head (1x1 conv, 64 -> 1, fp32 logits, bias) at bench scale: the streaming dot-product kernel
-(csrc/kernels/head.hip) vs the GEMM path (set_head1x1 0), interleaved rounds.
+"""UNet head (1x1 conv, 64 -> 1, fp32 logits, bias) and input conv (3x3, 8-channel padded image -> 64,
+bias, BN statistics) at bench scale: the streaming dot-product kernel (csrc/kernels/head.hip) vs the
+GEMM path (set_head1x1 0), the 8-channel 3x3 kernel (csrc/kernels/conv_small.hip) vs the GEMM path
+(set_conv_c8 0), interleaved rounds.
 
 python benchmarks/head_lab.py [--iters 20] [--rounds 3]
 """
@@ -52,6 +54,22 @@ def main():
                 res[name] = round(min(res.get(name, 1e9), t), 1)
         res["head_TBps"] = round(M * C * 2 / res["head"] / 1e6, 2)
         print(json.dumps({"shape": [N, H, W, C], "us": res}), flush=True)
+        xi = Act(torch.randn(M, 8, device="cuda").to(torch.bfloat16), N, H, W, 8)
+        wi = (torch.randn(64, 3, 3, 8, device="cuda") / 8).to(torch.bfloat16)
+        bi = torch.randn(64, device="cuda")
+        z = Act(torch.empty(M, 64, device="cuda", dtype=torch.bfloat16), N, H, W, 64)
+        res = {}
+        for _ in range(a.rounds):
+            for name, on in (("c8", 1), ("gemm", 0)):
+                be.C.set_conv_c8(on)
+                try:
+                    st = torch.empty(be.C.conv2d_fwd_mtiles(N, H, W, 8, 64, 3, 3, 1, 1, 0), 2, 64, device="cuda")
+                    t = timeit(lambda: be.conv_fwd(xi, wi, 64, 3, 3, 1, 1, z, bias=bi, stats=st), a.iters)
+                finally:
+                    be.C.set_conv_c8(1)
+                res[name] = round(min(res.get(name, 1e9), t), 1)
+        res["c8_TBps_out"] = round(M * 64 * 2 / res["c8"] / 1e6, 2)
+        print(json.dumps({"input_conv": [N, H, W, 8, 64], "us": res}), flush=True)
 
 
 if __name__ == "__main__":

@@ -462,6 +462,16 @@ static bool stream1x1_shape(int64_t M, int C, int K, int R, int S, int stride, i
 static int g_conv3_ran = 0;   // 1 if the last conv2d_fwd / conv2d_dgrad ran the streaming 3x3 kernel (tests)
 static int g_head_ran = 0;           // 1 if the last conv2d_fwd ran the 1x1 head kernel (head.hip)
 static int g_head_on = 1;            // dlmpi_ext set_head1x1 (A/B)
+static int g_c8_ran = 0;             // 1 if the last conv2d_fwd ran the 8-channel 3x3 kernel (conv_small.hip)
+static int g_c8_on = 1;              // dlmpi_ext set_conv_c8 (A/B)
+
+// 3x3 / s1 / p1 from an 8-channel (padded image) input into 64 channels: conv_small.hip
+static bool c8_shape(int64_t M, int C, int K, int R, int S, int stride, int pad, int W, int pro, int f32, int& G) {
+  if (!g_c8_on || C != 8 || K != 64 || R != 3 || S != 3 || stride != 1 || pad != 1 || W % 16 || pro || f32)
+    return false;
+  G = dlmpi_conv3x3_c8_blocks(M);
+  return true;
+}
 static bool stream3x3_shape(int N, int H, int W, int C, int K, int R, int S, int stride, int pad, int pro, int f32,
                             int& th, int& tw, int& G) {
   if (R != 3 || S != 3 || stride != 1 || pad != 1 || pro != 0 || f32) return false;
@@ -619,6 +629,25 @@ static int conv2d_fwd_impl(const at::Tensor& x, int N, int H, int W, int C, int 
   g_stream_ran = 0;
   g_conv3_ran = 0;
   g_head_ran = 0;
+  g_c8_ran = 0;
+  {  // the UNet input conv: 8-channel image -> 64, 3x3
+    int G;
+    if (bm_req <= 0 && bn_req <= 0 && c8_shape((int64_t)N * H * W, C, K, R, S, stride, pad, W, pro, a.f32, G)) {
+      const bool ok = !res.has_value() && !scale.has_value() && !relu && a.kvalid == K && ldx % 8 == 0 &&
+                      xoff % 8 == 0 && ldy % 8 == 0 && yoff % 8 == 0 && (int64_t)N * H * W < (1ll << 31) &&
+                      y.scalar_type() == at::kBFloat16;
+      if (a.stats && !ok)
+        throw std::runtime_error("conv2d_fwd: statistics were sized for the 8-channel 3x3 kernel, which cannot run");
+      if (ok) {
+        if (a.stats && stats->size(0) < G) throw std::runtime_error("conv2d_fwd: stats buffer too small");
+        check(dlmpi_conv3x3_c8(a.x, ldx, xoff, N, H, W, a.w, a.bias, a.y, ldy, yoff, a.stats, G, cur_stream()),
+              "conv2d_fwd (8-channel 3x3)");
+        g_c8_ran = 1;
+        if (fin != nullptr) run_fin_after(*stats, G, K, fin);
+        return G;
+      }
+    }
+  }
   {  // <= 4 output channels, 1x1, no epilogue beyond the bias (the UNet head): a streaming dot product
     const int kv = a.kvalid > 0 ? a.kvalid : K;
     if (g_head_on && bm_req <= 0 && bn_req <= 0 && pro == 0 && !a.f32 && R == 1 && S == 1 && stride == 1 &&
@@ -806,6 +835,7 @@ int conv2d_fwd_mtiles_pro(int N, int H, int W, int C, int K, int R, int S, int s
   const int P = (H + 2 * pad - R) / stride + 1, Q = (W + 2 * pad - S) / stride + 1;
   int bm, bn;
   int G;
+  if (bm_req <= 0 && c8_shape((int64_t)N * H * W, C, K, R, S, stride, pad, W, pro, f32, G)) return G;
   if (bm_req <= 0 && stream1x1_shape((int64_t)N * P * Q, C, K, R, S, stride, pad, pro, f32, bm, bn, G)) return G;
   int th, tw;
   if (bm_req <= 0 && stream3x3_shape(N, H, W, C, K, R, S, stride, pad, pro, f32, th, tw, G)) return G;
@@ -1668,6 +1698,8 @@ void register_ops(pybind11::module& m) {
   m.def("set_wgrad3", [](int mode) { g_wgrad3_override = mode; });
   m.def("set_wgrad3_blocks", [](int n) { g_wgrad3_blocks = n; });
   m.def("set_head1x1", [](int v) { g_head_on = v; });
+  m.def("set_conv_c8", [](int v) { g_c8_on = v; });
+  m.def("conv_c8_last", []() { return g_c8_ran; });
   m.def("head1x1_last", []() { return g_head_ran; });
   m.def("set_wgrad_defer", [](bool on) {
     if (!on) wgrad_flush();

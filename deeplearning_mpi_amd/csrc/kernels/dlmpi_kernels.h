@@ -276,6 +276,9 @@ hipError_t dlmpi_wgrad_reduce_batch(dlmpi::WgradReduceBatch* b, hipStream_t s);
 int dlmpi_wgrad3_plan(int Ko, int C, int* kt, int* ct);
 hipError_t dlmpi_wgrad3x3(const dlmpi::Wgrad3Args* a, int kt, int ct, hipStream_t s);
 int dlmpi_head1x1_ok(int C, int kv);
+int dlmpi_conv3x3_c8_blocks(int64_t pixels);
+hipError_t dlmpi_conv3x3_c8(const void* x, int ldx, int xoff, int N, int H, int W, const void* w, const float* bias,
+                            void* y, int ldy, int yoff, float* stats, int G, hipStream_t s);
 hipError_t dlmpi_head1x1(const void* x, int ldx, int xoff, int64_t M, int C, const void* w, int ldw,
                          const float* bias, void* y, int ldy, int yoff, int kv, int y_f32, hipStream_t s);
 // streaming 64 -> 64 3x3 conv: plan (tile th x tw, G blocks; 0 if it does not apply) + launch

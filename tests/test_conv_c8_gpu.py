@@ -1,0 +1,77 @@
+"""3x3 convolution of an 8-channel (padded image) input into 64 channels (the UNet input conv,
+csrc/kernels/conv_small.hip): output against an fp32 reference of the same op (bf16 operands, fp32
+accumulation, bias), BN statistics against fp32 sums of the stored values, the conv + BN-finalize entry
+against the generic GEMM path (forced off), and the dispatch taking the kernel."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from deeplearning_mpi_amd.ops.act import Act
+from deeplearning_mpi_amd.ops.backend import NativeBackend
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _rel(a, b):
+    a, b = a.double(), b.double()
+    return ((a - b).abs().max() / b.abs().max().clamp_min(1e-30)).item()
+
+
+@pytest.mark.parametrize("on", [1, 0], ids=["c8", "gemm"])
+@pytest.mark.parametrize("N,H,W,cin", [(2, 32, 48, 3), (1, 17, 16, 1), (3, 64, 64, 8), (16, 40, 80, 3)])
+def test_conv3x3_c8_matches_fp32(N, H, W, cin, on):
+    be = NativeBackend(DEV)
+    be.C.set_conv_c8(on)
+    g = torch.Generator(device=DEV).manual_seed(N * 100 + H + cin)
+    xi = torch.zeros(N * H * W, 8, device=DEV)
+    xi[:, :cin] = torch.randn(N * H * W, cin, device=DEV, generator=g)
+    xb = xi.to(torch.bfloat16)
+    w = torch.zeros(64, 3, 3, 8, device=DEV)
+    w[..., :cin] = torch.randn(64, 3, 3, cin, device=DEV, generator=g) * 0.2
+    wb = w.to(torch.bfloat16)
+    bias = torch.randn(64, device=DEV, generator=g)
+    y = torch.empty(N * H * W, 64, device=DEV, dtype=torch.bfloat16)
+    rows = be.C.conv2d_fwd_mtiles(N, H, W, 8, 64, 3, 3, 1, 1, 0)
+    stats = torch.full((rows, 2, 64), float("nan"), device=DEV)
+    try:
+        used = be.conv_fwd(Act(xb, N, H, W, 8), wb, 64, 3, 3, 1, 1, Act(y, N, H, W, 64), bias=bias, stats=stats)
+        torch.cuda.synchronize()
+        assert be.C.conv_c8_last() == on and used == rows
+    finally:
+        be.C.set_conv_c8(1)
+    xt = xb.float().view(N, H, W, 8).permute(0, 3, 1, 2)
+    ref = F.conv2d(xt, wb.float().permute(0, 3, 1, 2), bias, 1, 1).permute(0, 2, 3, 1).reshape(-1, 64)
+    assert _rel(y.float(), ref) < 8e-3
+    yf = y.float()
+    st = stats[:used].double().sum(0)
+    assert _rel(st[0], yf.double().sum(0)) < 1e-5
+    assert _rel(st[1], (yf.double() ** 2).sum(0)) < 1e-5
+
+
+def test_conv3x3_c8_bn_entry_matches_gemm_path():
+    be = NativeBackend(DEV)
+    N, H, W = 4, 48, 64
+    g = torch.Generator(device=DEV).manual_seed(5)
+    xb = torch.randn(N * H * W, 8, device=DEV, generator=g).to(torch.bfloat16)
+    wb = (torch.randn(64, 3, 3, 8, device=DEV, generator=g) * 0.2).to(torch.bfloat16)
+    bias = torch.randn(64, device=DEV, generator=g)
+    gamma, beta = torch.rand(64, device=DEV, generator=g) + 0.5, torch.randn(64, device=DEV, generator=g)
+    outs = {}
+    for on in (1, 0):
+        be.C.set_conv_c8(on)
+        try:
+            rows = be.C.conv2d_fwd_mtiles(N, H, W, 8, 64, 3, 3, 1, 1, 0)
+            z = torch.empty(N * H * W, 64, device=DEV, dtype=torch.bfloat16)
+            st = torch.empty(rows, 2, 64, device=DEV)
+            vec = torch.empty(4, 64, device=DEV)
+            rm, rv = torch.zeros(64, device=DEV), torch.ones(64, device=DEV)
+            be.conv_fwd_bn(Act(xb, N, H, W, 8), wb, 64, 3, 3, 1, 1, Act(z, N, H, W, 64), bias, st, N * H * W, gamma,
+                           beta, rm, rv, 0.1, 1e-5, vec[0], vec[1], vec[2], vec[3])
+            torch.cuda.synchronize()
+            assert be.C.conv_c8_last() == on
+            outs[on] = (z.float(), vec.clone(), rm.clone(), rv.clone())
+        finally:
+            be.C.set_conv_c8(1)
+    for name, a, b in zip(("z", "vec", "running_mean", "running_var"), outs[1], outs[0]):
+        assert _rel(a, b) < 1e-2, name
