@@ -10,7 +10,7 @@
 // whole persistent loop.  The product is computed transposed, D[channel][pixel] (weights as the A
 // operand), so a lane holds 4 consecutive channels of one pixel; the wave assembles its 64 output
 // rows in LDS (XOR-swizzled 16-B chunks) and stores them as whole 128-B rows, 16 B per lane (the
-// 8-byte scattered stores straight from the accumulators ran at 2.3 TB/s).  Each wave takes 4 groups
+// 8-byte scattered stores straight from the accumulators ran at 2.3 TB/s).  Each wave takes 2 groups
 // of 16 consecutive pixels of a row per iteration.
 // BN statistics: per-lane fp32 sums of the stored (bf16) values, a fixed shuffle tree over the 16
 // pixels of a lane group, the 4 waves combined in LDS in wave order -> stats[block][2][64].
@@ -22,7 +22,7 @@ __global__ __launch_bounds__(256) void conv3x3_c8_kernel(const uint16_t* __restr
                                                          int H, int W, const uint16_t* __restrict__ w,
                                                          const float* __restrict__ bias, uint16_t* __restrict__ y,
                                                          int ldy, int yoff, float* __restrict__ stats) {
-  constexpr int GP = 4;   // 16-pixel groups per wave iteration
+  constexpr int GP = 2;   // 16-pixel groups per wave iteration
   // per wave: the 64 output pixels of an iteration, 128 B each, 16-B chunks XOR-swizzled by (pixel & 7)
   __shared__ __attribute__((aligned(16))) char tile[4][GP * 16 * 128];
   __shared__ float red[4][2][64];
