@@ -1,7 +1,8 @@
 """UNet head (1x1 conv, 64 -> 1, fp32 logits, bias) and input conv (3x3, 8-channel padded image -> 64,
 bias, BN statistics) at bench scale: the streaming dot-product kernel (csrc/kernels/head.hip) vs the
 GEMM path (set_head1x1 0), the 8-channel 3x3 kernel (csrc/kernels/conv_small.hip) vs the GEMM path
-(set_conv_c8 0), interleaved rounds.
+(set_conv_c8 0), and the 2x2/s2 up-sampling into its concat slice (streaming 1x1 kernel over 4 Cout
+columns vs the 4-phase implicit GEMM, set_convT_stream 0), interleaved rounds.
 
 python benchmarks/head_lab.py [--iters 20] [--rounds 3]
 """
@@ -70,6 +71,26 @@ def main():
                 res[name] = round(min(res.get(name, 1e9), t), 1)
         res["c8_TBps_out"] = round(M * 64 * 2 / res["c8"] / 1e6, 2)
         print(json.dumps({"input_conv": [N, H, W, 8, 64], "us": res}), flush=True)
+        if H > 512:
+            continue
+        for C, skip in ((128, 64), (256, 128)):
+            h, w_ = H * 128 // C // 2, W * 128 // C // 2   # the level below: 256^2 x 128, 128^2 x 256
+            xt = Act(torch.randn(N * h * w_, C, device="cuda").to(torch.bfloat16), N, h, w_, C)
+            wt = (torch.randn(C, 2, 2, C, device="cuda") / C ** 0.5).to(torch.bfloat16)
+            bt = torch.randn(C, device="cuda")
+            cat = Act(torch.empty(N * 4 * h * w_, C + skip, device="cuda", dtype=torch.bfloat16), N, 2 * h, 2 * w_,
+                      C + skip)
+            res = {}
+            for _ in range(a.rounds):
+                for name, on in (("stream", 1), ("igemm", 0)):
+                    be.C.set_convT_stream(on)
+                    try:
+                        t = timeit(lambda: be.convT_fwd(xt, wt, C, cat.slice(0, C), bt), a.iters)
+                    finally:
+                        be.C.set_convT_stream(1)
+                    res[name] = round(min(res.get(name, 1e9), t), 1)
+            res["stream_TBps"] = round((N * h * w_ * C * 2 + N * 4 * h * w_ * C * 2) / res["stream"] / 1e6, 2)
+            print(json.dumps({"convT": [N, h, w_, C, C], "us": res}), flush=True)
 
 
 if __name__ == "__main__":

@@ -464,6 +464,8 @@ static int g_head_ran = 0;           // 1 if the last conv2d_fwd ran the 1x1 hea
 static int g_head_on = 1;            // dlmpi_ext set_head1x1 (A/B)
 static int g_c8_ran = 0;             // 1 if the last conv2d_fwd ran the 8-channel 3x3 kernel (conv_small.hip)
 static int g_c8_on = 1;              // dlmpi_ext set_conv_c8 (A/B)
+static int g_convT_stream = 1;       // dlmpi_ext set_convT_stream (A/B)
+static int g_convT_stream_ran = 0;   // 1 if the last convT2x2_fwd ran the streaming kernel
 
 // 3x3 / s1 / p1 from an 8-channel (padded image) input into 64 channels: conv_small.hip
 static bool c8_shape(int64_t M, int C, int K, int R, int S, int stride, int pad, int W, int pro, int f32, int& G) {
@@ -1069,6 +1071,32 @@ void convT2x2_fwd(const at::Tensor& x, int N, int H, int W, int Cin, int ldx, in
   fill_epilogue(a, y, ldy, yoff, bias, c10::nullopt, 0, 0, c10::nullopt, c10::nullopt, false, c10::nullopt);
   a.vec_store = ((ldy % 8) == 0 && (yoff % 8) == 0) ? 1 : 0;
   set_kstep(a, Cin);
+  g_convT_stream_ran = 0;
+  {  // the streaming 1x1 kernel over 4 Cout columns (input read once for the four sub-pixel positions)
+    const int64_t M = (int64_t)N * H * W;
+    int sbm, sbn, G;
+    if (g_convT_stream && !a.f32 && a.vec_store && ldx % 8 == 0 && xoff % 8 == 0 && M * ldx < (1ll << 31) &&
+        4 * M * ldy * 2 < (1ll << 31) && (int64_t)y.numel() * 2 < (1ll << 31) &&
+        dlmpi_stream1x1_plan(M, Cin, 4 * Cout, 1, &sbm, &sbn, &G) && Cout % sbn == 0) {
+      Stream1x1Args sa{};
+      sa.x = ptr<uint16_t>(x);
+      sa.ldx = ldx; sa.xoff = xoff;
+      sa.w = ptr<uint16_t>(wf);
+      sa.y = reinterpret_cast<uint16_t*>(a.y);
+      sa.ldy = ldy; sa.yoff = yoff;
+      sa.y_bytes = (int)((int64_t)y.numel() * 2);
+      sa.M = (int)M; sa.C = Cin; sa.Kout = 4 * Cout;
+      sa.bias = a.bias;
+      sa.G = G; sa.ntiles = 4 * Cout / sbn; sa.mtiles = ceil_div(M, sbm);
+      sa.H = H; sa.W = W;
+      sa.fdPQ = make_fastdiv((uint32_t)(H * W));
+      sa.fdQ = make_fastdiv((uint32_t)W);
+      sa.up2 = 1; sa.Cup = Cout;
+      check(dlmpi_conv1x1_stream(&sa, sbm, sbn, cur_stream()), "convT2x2_fwd (stream)");
+      g_convT_stream_ran = 1;
+      return;
+    }
+  }
   int bm, bn;
   pick_tiles((int64_t)N * H * W, Cout, Cin, Cin, bm, bn, false, false);   // 4-phase convT: unmeasured at 256 rows
   if (a.f32) f32_tiles(bm, bn);
@@ -1699,6 +1727,8 @@ void register_ops(pybind11::module& m) {
   m.def("set_wgrad3_blocks", [](int n) { g_wgrad3_blocks = n; });
   m.def("set_head1x1", [](int v) { g_head_on = v; });
   m.def("set_conv_c8", [](int v) { g_c8_on = v; });
+  m.def("set_convT_stream", [](int v) { g_convT_stream = v; });
+  m.def("convT_stream_last", []() { return g_convT_stream_ran; });
   m.def("conv_c8_last", []() { return g_c8_ran; });
   m.def("head1x1_last", []() { return g_head_ran; });
   m.def("set_wgrad_defer", [](bool on) {

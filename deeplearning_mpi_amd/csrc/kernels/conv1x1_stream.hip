@@ -22,6 +22,10 @@
 // BatchNorm statistics of the stored (bf16) values accumulate per thread over ALL of the block's
 // tiles and are written as ONE partial row per block: the finalize reduces G rows per N-tile
 // (G = blocks per N-tile, a few hundred) instead of one row per 64/128-pixel tile.
+// UP2: ConvTranspose2d(kernel 2, stride 2) (the UNet up-sampling, reference model.py:60-63) as ONE
+// 1x1 GEMM with 4 Cup output columns ordered (i, j, co): an N-tile lies inside one (i, j) block, so its
+// rows are stored to output pixel (2h + i, 2w + j) -- the input tile is read once for all four
+// sub-pixel positions instead of once per phase.
 //
 // Reference semantics: nn.Conv2d(k=1, bias=False) + BatchNorm2d statistics (torchvision Bottleneck
 // conv3 / downsample, /root/reference/pytorch/resnet/main.py:40-41).
@@ -43,7 +47,7 @@ constexpr int vmcnt_imm(int n) { return (n & 15) | 0x70 | 0xF00 | ((n >> 4) << 1
 
 __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
-template <int BM, int BN, int KS, bool STATS, bool S2>
+template <int BM, int BN, int KS, bool STATS, bool S2, bool UP2 = false>
 __global__ __launch_bounds__(256) void conv1x1_stream_kernel(const Stream1x1Args a) {
   constexpr int NT = 256;
   constexpr int WM = BM / 2, WN = BN / 2;       // 2 x 2 waves
@@ -77,6 +81,8 @@ __global__ __launch_bounds__(256) void conv1x1_stream_kernel(const Stream1x1Args
   const uint32_t lb = xcd_remap(blockIdx.x, gridDim.x);
   const int nt = lb % a.ntiles, g = lb / a.ntiles;
   const int n0 = nt * BN;
+  // UP2: sub-pixel block (i, j) = ub of this N-tile and its first output channel
+  const int ub = UP2 ? n0 / a.Cup : 0, c0 = UP2 ? n0 - ub * a.Cup : n0;
 
   // ---- weights: staged once ----------------------------------------------------------------
 #pragma unroll
@@ -84,7 +90,8 @@ __global__ __launch_bounds__(256) void conv1x1_stream_kernel(const Stream1x1Args
 #pragma unroll
     for (int i = 0; i < BL; ++i) {
       const int n = n0 + lrow + RP * i;
-      const char* src = n < a.Kout ? reinterpret_cast<const char*>(a.w + (int64_t)n * a.C + ks * 64 + 8 * jc) : zp;
+      const int wrow = UP2 ? (c0 + lrow + RP * i) * 4 + ub : n;   // w [Cup][2][2][C]
+      const char* src = n < a.Kout ? reinterpret_cast<const char*>(a.w + (int64_t)wrow * a.C + ks * 64 + 8 * jc) : zp;
       __builtin_amdgcn_global_load_lds(src, (s1x1_lds_void*)(Ws + ks * BN * 128 + (RP * i + 8 * wid) * 128), 16, 0, 0);
     }
   auto issue_a = [&](int mt) {
@@ -116,7 +123,7 @@ __global__ __launch_bounds__(256) void conv1x1_stream_kernel(const Stream1x1Args
   f32x4 bq[TN];
 #pragma unroll
   for (int ni = 0; ni < TN; ++ni)
-    bq[ni] = a.bias ? *reinterpret_cast<const f32x4*>(a.bias + n0 + wn * WN + ni * 16 + 4 * fg) : f32x4{0.f, 0.f, 0.f, 0.f};
+    bq[ni] = a.bias ? *reinterpret_cast<const f32x4*>(a.bias + c0 + wn * WN + ni * 16 + 4 * fg) : f32x4{0.f, 0.f, 0.f, 0.f};
   float s1[8], s2[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) { s1[e] = 0.f; s2[e] = 0.f; }
@@ -195,7 +202,14 @@ __global__ __launch_bounds__(256) void conv1x1_stream_kernel(const Stream1x1Args
           s2[e] += u * u;
         }
       }
-      const uint32_t off0 = (uint32_t)(m * a.ldy + a.yoff + n0 + cg * 8) * 2u;   // 32-bit: host-checked
+      uint32_t orow = (uint32_t)m;
+      if constexpr (UP2) {   // input pixel (n, h, w) -> output pixel (n, 2h + i, 2w + j)
+        const uint32_t mm = m < a.M ? (uint32_t)m : 0u;
+        const uint32_t n = fdiv(mm, a.fdPQ), rem = mm - n * a.fdPQ.d;
+        const uint32_t h = fdiv(rem, a.fdQ), w = rem - h * a.fdQ.d;
+        orow = (n * 2u * a.H + 2u * h + (uint32_t)(ub >> 1)) * 2u * a.W + 2u * w + (uint32_t)(ub & 1);
+      }
+      const uint32_t off0 = (orow * a.ldy + a.yoff + c0 + cg * 8) * 2u;   // 32-bit: host-checked
       const uint32_t off = m < a.M ? off0 : 0x80000000u;
       __builtin_amdgcn_raw_buffer_store_b128(q, yr, off, 0, 0);
     }
@@ -259,7 +273,13 @@ extern "C" hipError_t dlmpi_conv1x1_stream(const Stream1x1Args* a, int bm, int b
     if (a->stats) hipLaunchKernelGGL((conv1x1_stream_kernel<BM_, BN_, KS_, true, S2_>), grid, block, 0, s, *a);     \
     else hipLaunchKernelGGL((conv1x1_stream_kernel<BM_, BN_, KS_, false, S2_>), grid, block, 0, s, *a);          \
   } while (0)
-  if (a->s2) {   // the stride-2 projection (layer-2 downsample, 56^2 256 -> 512)
+  if (a->up2) {   // ConvTranspose2d(2, 2): no statistics
+    if (a->stats || a->Kout != 4 * a->Cup || a->Cup % bn) return hipErrorInvalidValue;
+    if (bm == 64 && bn == 128 && a->C == 128) hipLaunchKernelGGL((conv1x1_stream_kernel<64, 128, 2, false, false, true>), grid, block, 0, s, *a);
+    else if (bm == 64 && bn == 64 && a->C == 256) hipLaunchKernelGGL((conv1x1_stream_kernel<64, 64, 4, false, false, true>), grid, block, 0, s, *a);
+    else if (bm == 128 && bn == 128 && a->C == 64) hipLaunchKernelGGL((conv1x1_stream_kernel<128, 128, 1, false, false, true>), grid, block, 0, s, *a);
+    else return hipErrorInvalidValue;
+  } else if (a->s2) {   // the stride-2 projection (layer-2 downsample, 56^2 256 -> 512)
     if (bm == 64 && bn == 64 && a->C == 256) LAUNCH_S1(64, 64, 4, true);
     else return hipErrorInvalidValue;
   } else if (bm == 128 && bn == 128 && a->C == 64) LAUNCH_S1(128, 128, 1, false);

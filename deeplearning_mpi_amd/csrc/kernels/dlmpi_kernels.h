@@ -72,6 +72,8 @@ struct Stream1x1Args {
   int G, ntiles, mtiles;
   int s2, H, W;                    // stride-2 gather (s2 = 1): input grid
   FastDiv fdPQ, fdQ;               // output grid P x Q
+  int up2;                         // 1: ConvTranspose2d(2, 2): Kout = 4 Cup rows (i, j, co), w [Cup][2][2][C],
+  int Cup;                         //    output pixel (2h + i, 2w + j); fdPQ / fdQ = the input grid H W / W
 };
 
 // Streaming 1x1 / stride-1 data gradient with the fused BN-backward epilogue (conv1x1_dgrad_stream.hip)

@@ -523,18 +523,31 @@ def test_unet_head_1ch():
     assert _rel(o, orf) < 1e-2
 
 
-@pytest.mark.parametrize("N,H,W,Ci,Co", [(2, 8, 12, 256, 256), (2, 4, 4, 1024, 512)])   # 2nd: split-K
-def test_convT(N, H, W, Ci, Co):
+@pytest.mark.parametrize("stream", [1, 0], ids=["stream", "igemm"])
+@pytest.mark.parametrize("N,H,W,Ci,Co", [(2, 8, 12, 256, 256), (2, 4, 4, 1024, 512),   # 2nd: split-K
+                                         (2, 8, 12, 128, 128), (3, 5, 7, 256, 256), (2, 6, 8, 64, 64)])
+def test_convT(N, H, W, Ci, Co, stream):
+    """ConvTranspose2d(2, 2) into a channel slice of a concat buffer: the streaming 1x1 kernel over
+    4 Cout columns (C 64 / 128 / 256 where an N-tile fits one sub-pixel block) and the 4-phase
+    implicit GEMM, against the fp32 reference; the rest of the buffer is untouched."""
     nb, rb = _be()
     x, xr = _act(N, H, W, Ci)
     wf = (torch.randn(Co, 2, 2, Ci, device=DEV) / Ci ** 0.5).to(torch.bfloat16)
     bias = torch.randn(Co, device=DEV)
     cat = _empty(N, 2 * H, 2 * W, Co + 128)
+    cat.buf.fill_(7.0)
     catr = _empty(N, 2 * H, 2 * W, Co + 128, torch.float32)
-    nb.convT_fwd(x, wf, Co, cat.slice(0, Co), bias)
+    nb.C.set_convT_stream(stream)
+    try:
+        nb.convT_fwd(x, wf, Co, cat.slice(0, Co), bias)
+        torch.cuda.synchronize()
+        assert nb.C.convT_stream_last() == int(stream and Ci in (128, 256))
+    finally:
+        nb.C.set_convT_stream(1)
     rb.convT_fwd(xr, wf.float(), Co, catr.slice(0, Co), bias)
     torch.cuda.synchronize()
     assert _rel(cat.nhwc()[..., :Co], catr.nhwc()[..., :Co]) < 1e-2
+    assert bool((cat.buf[:, Co:] == 7.0).all())
 
 
 def test_bn_family():
