@@ -1075,8 +1075,9 @@ void convT2x2_fwd(const at::Tensor& x, int N, int H, int W, int Cin, int ldx, in
   {  // the streaming 1x1 kernel over 4 Cout columns (input read once for the four sub-pixel positions)
     const int64_t M = (int64_t)N * H * W;
     int sbm, sbn, G;
+    // (output offsets are relative to each tile's first output row: any buffer size; input 32-bit)
     if (g_convT_stream && !a.f32 && a.vec_store && ldx % 8 == 0 && xoff % 8 == 0 && M * ldx < (1ll << 31) &&
-        4 * M * ldy * 2 < (1ll << 31) && (int64_t)y.numel() * 2 < (1ll << 31) &&
+        4 * (int64_t)W * ldy * 2 * 4 < (1ll << 31) && 4 * M < (1ll << 31) &&
         dlmpi_stream1x1_plan(M, Cin, 4 * Cout, 1, &sbm, &sbn, &G) && Cout % sbn == 0) {
       Stream1x1Args sa{};
       sa.x = ptr<uint16_t>(x);
@@ -1084,7 +1085,7 @@ void convT2x2_fwd(const at::Tensor& x, int N, int H, int W, int Cin, int ldx, in
       sa.w = ptr<uint16_t>(wf);
       sa.y = reinterpret_cast<uint16_t*>(a.y);
       sa.ldy = ldy; sa.yoff = yoff;
-      sa.y_bytes = (int)((int64_t)y.numel() * 2);
+      sa.y_bytes = (int)std::min<int64_t>(INT32_MAX, (int64_t)y.numel() * 2);   // (UP2: per-tile descriptors)
       sa.M = (int)M; sa.C = Cin; sa.Kout = 4 * Cout;
       sa.bias = a.bias;
       sa.G = G; sa.ntiles = 4 * Cout / sbn; sa.mtiles = ceil_div(M, sbm);

@@ -185,6 +185,18 @@ __global__ __launch_bounds__(256) void conv1x1_stream_kernel(const Stream1x1Args
         *reinterpret_cast<u32x2*>(Os + row * OP + col * 2) = u32x2{pack2bf(v[0], v[1]), pack2bf(v[2], v[3])};
       }
     lds_barrier();
+    // UP2: the tile's output rows are addressed relative to its first one (a 64-bit base in a per-tile
+    // buffer descriptor), so the concat buffer may exceed 2 GB
+    uint32_t orow0 = 0;
+    __amdgpu_buffer_rsrc_t yo = yr;
+    if constexpr (UP2) {
+      const uint32_t m0 = (uint32_t)(mt * BM);
+      const uint32_t n = fdiv(m0, a.fdPQ), rem = m0 - n * a.fdPQ.d;
+      const uint32_t h = fdiv(rem, a.fdQ), w = rem - h * a.fdQ.d;
+      orow0 = (n * 2u * a.H + 2u * h + (uint32_t)(ub >> 1)) * 2u * a.W + 2u * w + (uint32_t)(ub & 1);
+      yo = __builtin_amdgcn_make_buffer_rsrc(a.y + (int64_t)orow0 * a.ldy + a.yoff + c0, (short)0, 0x7fffffff,
+                                             0x00020000);
+    }
     // rows out: 16 bytes per thread per row, statistics of the stored values
 #pragma unroll
     for (int i = 0; i < NSTORE; ++i) {
@@ -202,16 +214,18 @@ __global__ __launch_bounds__(256) void conv1x1_stream_kernel(const Stream1x1Args
           s2[e] += u * u;
         }
       }
-      uint32_t orow = (uint32_t)m;
-      if constexpr (UP2) {   // input pixel (n, h, w) -> output pixel (n, 2h + i, 2w + j)
+      if constexpr (UP2) {   // input pixel (n, h, w) -> output pixel (n, 2h + i, 2w + j), relative to the tile's
         const uint32_t mm = m < a.M ? (uint32_t)m : 0u;
         const uint32_t n = fdiv(mm, a.fdPQ), rem = mm - n * a.fdPQ.d;
         const uint32_t h = fdiv(rem, a.fdQ), w = rem - h * a.fdQ.d;
-        orow = (n * 2u * a.H + 2u * h + (uint32_t)(ub >> 1)) * 2u * a.W + 2u * w + (uint32_t)(ub & 1);
+        const uint32_t orow = (n * 2u * a.H + 2u * h + (uint32_t)(ub >> 1)) * 2u * a.W + 2u * w + (uint32_t)(ub & 1);
+        const uint32_t off = m < a.M ? ((orow - orow0) * a.ldy + cg * 8) * 2u : 0x80000000u;
+        __builtin_amdgcn_raw_buffer_store_b128(q, yo, off, 0, 0);
+      } else {
+        const uint32_t off0 = (uint32_t)(m * a.ldy + a.yoff + n0 + cg * 8) * 2u;   // 32-bit: host-checked
+        const uint32_t off = m < a.M ? off0 : 0x80000000u;
+        __builtin_amdgcn_raw_buffer_store_b128(q, yr, off, 0, 0);
       }
-      const uint32_t off0 = (orow * a.ldy + a.yoff + c0 + cg * 8) * 2u;   // 32-bit: host-checked
-      const uint32_t off = m < a.M ? off0 : 0x80000000u;
-      __builtin_amdgcn_raw_buffer_store_b128(q, yr, off, 0, 0);
     }
   }
 
