@@ -1452,12 +1452,15 @@ void channel_sum(const at::Tensor& x, int64_t M, int C, int ldx, int xoff, at::T
 }
 
 // --------------------------------- pooling / layout ----------------------------------------
+// ys (optional): also store the applied input relu(x * scale + shift) there (2x2 / s2 windows only)
 void maxpool_fwd(const at::Tensor& x, int N, int H, int W, int C, int ldx, int xoff, int k, int stride, int pad,
                  at::Tensor y, at::Tensor idx, int OH, int OW, const c10::optional<at::Tensor>& scale,
-                 const c10::optional<at::Tensor>& shift) {
+                 const c10::optional<at::Tensor>& shift, const c10::optional<at::Tensor>& ys, int ldys, int ysoff) {
   same_type(x, y, "maxpool_fwd y");
+  same_type(x, ys, "maxpool_fwd ys");
   check(dlmpi_maxpool_fwd(x.data_ptr(), N, H, W, C, ldx, xoff, k, stride, pad, y.data_ptr(), ptr<uint8_t>(idx), OH, OW,
-                          optr<float>(scale), optr<float>(shift), act_f32(x, "maxpool_fwd"), cur_stream()),
+                          optr<float>(scale), optr<float>(shift), ys.has_value() ? ys->data_ptr() : nullptr, ldys,
+                          ysoff, act_f32(x, "maxpool_fwd"), cur_stream()),
         "maxpool_fwd");
 }
 void maxpool_bwd(const at::Tensor& dy, const at::Tensor& idx, int N, int H, int W, int C, int k, int stride, int pad,
@@ -1696,7 +1699,10 @@ void register_ops(pybind11::module& m) {
   m.def("bn_bwd_apply", &bn_bwd_apply);
   m.def("dual_dgrad_weights", &dual_dgrad_weights);
   m.def("channel_sum", &channel_sum);
-  m.def("maxpool_fwd", &maxpool_fwd);
+  m.def("maxpool_fwd", &maxpool_fwd, py::arg("x"), py::arg("N"), py::arg("H"), py::arg("W"), py::arg("C"),
+        py::arg("ldx"), py::arg("xoff"), py::arg("k"), py::arg("stride"), py::arg("pad"), py::arg("y"), py::arg("idx"),
+        py::arg("OH"), py::arg("OW"), py::arg("scale"), py::arg("shift"), py::arg("ys") = py::none(),
+        py::arg("ldys") = 0, py::arg("ysoff") = 0);
   m.def("maxpool_bwd", &maxpool_bwd);
   m.def("maxpool_bwd_bn", &maxpool_bwd_bn);
   m.def("outer_dgrad_bn", &outer_dgrad_bn);

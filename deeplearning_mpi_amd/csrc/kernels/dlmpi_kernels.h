@@ -331,8 +331,8 @@ int dlmpi_reduce_blocks(int64_t M, int C);
 // pooling / layout
 // scale/shift (optional): pool relu(x * scale + shift) (rounded to the storage type), i.e. BN-apply + ReLU fused
 hipError_t dlmpi_maxpool_fwd(const void* x, int N, int H, int W, int C, int ldx, int xoff, int k, int stride, int pad,
-                             void* y, uint8_t* idx, int OH, int OW, const float* scale, const float* shift, int f32,
-                             hipStream_t s);
+                             void* y, uint8_t* idx, int OH, int OW, const float* scale, const float* shift, void* ys,
+                             int ldys, int ysoff, int f32, hipStream_t s);
 hipError_t dlmpi_maxpool_bwd(const void* dy, const uint8_t* idx, int N, int H, int W, int C, int k, int stride,
                              int pad, int OH, int OW, const void* add, int ldadd, int addoff, void* dx, int lddx,
                              int dxoff, int f32, hipStream_t s);

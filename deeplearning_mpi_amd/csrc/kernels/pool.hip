@@ -74,13 +74,18 @@ __global__ void maxpool_fwd_kernel(const T* __restrict__ x, int N, int H, int W,
 // in-image address and are masked to -inf, which never wins), instead of one dependent round trip per
 // tap of the runtime-k loop (182 -> ~100 us for the ResNet-50 bs-256 stem pool).  Same scan order and
 // compares as maxpool_fwd_kernel: identical values and indices.
+//
+// ys (with scale / shift, K == S: every input pixel in exactly one window): the applied values
+// relu(fma(x, scale, shift)) -- bn_apply_kernel's arithmetic, bit-identical -- are also stored to ys, so
+// a BN-apply whose output is both kept and pooled (the UNet encoder skip) needs one pass, not two.
 template <int K, int S, typename T>
 __global__ __launch_bounds__(256) void maxpool_fwd_fixed_kernel(const T* __restrict__ x, int N, int H, int W, int C,
                                                                 int ldx, int xoff, int pad, T* __restrict__ y,
                                                                 uint8_t* __restrict__ idx, int OH, int OW,
                                                                 const float* __restrict__ scale,
                                                                 const float* __restrict__ shift, FastDiv fdCC,
-                                                                FastDiv fdOW, FastDiv fdOH) {
+                                                                FastDiv fdOW, FastDiv fdOH, T* __restrict__ ys,
+                                                                int ldys, int ysoff) {
   const int CC = C >> 3;
   const int64_t total = (int64_t)N * OH * OW * CC;   // < 2^31 (launcher)
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
@@ -119,7 +124,11 @@ __global__ __launch_bounds__(256) void maxpool_fwd_fixed_kernel(const T* __restr
         unpack8(raw[kh][kw], v);
         if (scale) {
 #pragma unroll
-          for (int e = 0; e < 8; ++e) v[e] = stored<T>(fmaxf(v[e] * sc[e] + sh[e], 0.f));
+          for (int e = 0; e < 8; ++e) v[e] = stored<T>(fmaxf(__builtin_fmaf(v[e], sc[e], sh[e]), 0.f));
+          if (ys) {
+            const int ih = oh * S - pad + kh, iw = ow * S - pad + kw;
+            store8(ys + (((int64_t)n_ * H + ih) * W + iw) * ldys + ysoff + cc * 8, v);
+          }
         }
 #pragma unroll
         for (int e = 0; e < 8; ++e)
@@ -372,8 +381,13 @@ using namespace dlmpi;
 // f32: 1 = fp32 activations (the fp32 precision path), 0 = bf16 (uint16_t storage)
 extern "C" hipError_t dlmpi_maxpool_fwd(const void* x, int N, int H, int W, int C, int ldx, int xoff, int k,
                                         int stride, int pad, void* y, uint8_t* idx, int OH, int OW,
-                                        const float* scale, const float* shift, int f32, hipStream_t s) {
+                                        const float* scale, const float* shift, void* ys, int ldys, int ysoff,
+                                        int f32, hipStream_t s) {
   if (C % 8) return hipErrorInvalidValue;
+  // ys: K == S, no padding, the windows tile the input exactly, an applied input (scale / shift)
+  if (ys && (!scale || !shift || k != 2 || stride != 2 || pad != 0 || H != 2 * OH || W != 2 * OW || ldys % 8 ||
+             ysoff % 8))
+    return hipErrorInvalidValue;
   const int64_t total = (int64_t)N * OH * OW * (C / 8);
   if (total >= (1ll << 31)) return hipErrorInvalidValue;
   const FastDiv a = make_fastdiv(C / 8), b = make_fastdiv(OW), c = make_fastdiv(OH);
@@ -381,11 +395,12 @@ extern "C" hipError_t dlmpi_maxpool_fwd(const void* x, int N, int H, int W, int 
   do {                                                                                                            \
     if (f32)                                                                                                      \
       hipLaunchKernelGGL((maxpool_fwd_fixed_kernel<K_, S_, float>), dim3(ew_blocks(total)), dim3(256), 0, s,      \
-                         (const float*)x, N, H, W, C, ldx, xoff, pad, (float*)y, idx, OH, OW, scale, shift, a, b, c);  \
+                         (const float*)x, N, H, W, C, ldx, xoff, pad, (float*)y, idx, OH, OW, scale, shift, a, b, c, \
+                         (float*)ys, ldys, ysoff);                                                                \
     else                                                                                                          \
       hipLaunchKernelGGL((maxpool_fwd_fixed_kernel<K_, S_, uint16_t>), dim3(ew_blocks(total)), dim3(256), 0, s,   \
                          (const uint16_t*)x, N, H, W, C, ldx, xoff, pad, (uint16_t*)y, idx, OH, OW, scale, shift, a, \
-                         b, c);                                                                                   \
+                         b, c, (uint16_t*)ys, ldys, ysoff);                                                       \
     return hipGetLastError();                                                                                     \
   } while (0)
   if (k == 3 && stride == 2 && H > 0 && W > 0) LAUNCH_MPF(3, 2);

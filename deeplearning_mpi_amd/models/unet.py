@@ -22,6 +22,11 @@ import torch.nn as nn
 from ..ops.act import Act, padc
 from .engine import ConvTUnit, ConvUnit, EngineModule
 
+# Training forward: each encoder DoubleConv's last BN-apply + ReLU runs inside the 2x2 max-pool that
+# reads it, which also stores it as the skip (pool.hip maxpool_fwd_fixed_kernel, ys): one pass over the
+# BN input instead of the apply pass plus the pool re-reading its output (profiles/r5_poolapply).
+FUSE_POOL_APPLY = True
+
 
 
 class DoubleConv(nn.Module):
@@ -153,9 +158,14 @@ class UNet(EngineModule):
             ua, ub = self.enc[k]
             t, ca = ua.fwd(be, a, train, save=save)
             skip = cat.slice(self.up_ch[k], self.skip_ch[k])
-            _, cb = ub.fwd(be, t, train, out=skip, save=save)
             down = Act.empty(N, h // 2, w // 2, self.skip_ch[k], dt, dev)
-            idx = be.maxpool_fwd(skip, 2, 2, 0, down)
+            if FUSE_POOL_APPLY and train and save:
+                # the skip's BN-apply runs inside the pool, which stores it (one pass over z, not two)
+                z, cb = ub.fwd(be, t, train, out=skip, save=save, defer_apply=True)
+                idx = be.maxpool_fwd(z, 2, 2, 0, down, bn=(cb[5], cb[6]), store=skip)
+            else:
+                _, cb = ub.fwd(be, t, train, out=skip, save=save)
+                idx = be.maxpool_fwd(skip, 2, 2, 0, down)
             ctx_enc.append((ca, cb))
             idxs.append(idx)
             skips.append(skip)

@@ -302,12 +302,15 @@ class NativeBackend:
         self.C.channel_sum(x.buf, x.rows, x.C, x.ld, x.off, out_acc)
 
     # ---------------- pooling / layout ----------------
-    def maxpool_fwd(self, x: Act, k, s, p, y: Act, bn=None):
-        """bn = (scale, shift): pool relu(x * scale + shift) -- a BN-apply + ReLU fused into the pool."""
+    def maxpool_fwd(self, x: Act, k, s, p, y: Act, bn=None, store: Act = None):
+        """bn = (scale, shift): pool relu(x * scale + shift) -- a BN-apply + ReLU fused into the pool;
+        store (2x2 / s2 only): also write that applied input there (the BN-apply's own output)."""
         idx = torch.empty(y.rows * y.C, dtype=torch.uint8, device=x.device)
         assert y.ld == y.C and y.off == 0
         sc, sh = bn if bn is not None else (None, None)
-        self.C.maxpool_fwd(x.buf, x.N, x.H, x.W, x.C, x.ld, x.off, k, s, p, y.buf, idx, y.H, y.W, sc, sh)
+        self.C.maxpool_fwd(x.buf, x.N, x.H, x.W, x.C, x.ld, x.off, k, s, p, y.buf, idx, y.H, y.W, sc, sh,
+                           store.buf if store is not None else None, store.ld if store is not None else 0,
+                           store.off if store is not None else 0)
         return idx
 
     def maxpool_bwd(self, dy: Act, idx, x: Act, k, s, p, dx: Act, add: Act = None, fuse=None):
@@ -662,10 +665,12 @@ class RefBackend:
     def channel_sum(self, x: Act, out_acc):
         out_acc.add_(x.nhwc().to(self.dt).sum((0, 1, 2)))
 
-    def maxpool_fwd(self, x: Act, k, s, p, y: Act, bn=None):
+    def maxpool_fwd(self, x: Act, k, s, p, y: Act, bn=None, store: Act = None):
         v = x.nchw().to(self.dt)
         if bn is not None:
             v = F.relu(v * bn[0].view(1, -1, 1, 1) + bn[1].view(1, -1, 1, 1)).to(x.dtype).to(self.dt)
+        if store is not None:
+            self._store(store, v)
         out, idx = F.max_pool2d(v, k, s, p, return_indices=True)
         self._store(y, out)
         return idx
