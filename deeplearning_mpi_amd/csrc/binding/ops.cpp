@@ -657,7 +657,7 @@ static int conv2d_fwd_impl(const at::Tensor& x, int N, int H, int W, int C, int 
         dlmpi_head1x1_ok(C, kv) && ldx % 8 == 0 && xoff % 8 == 0 &&
         (y.scalar_type() == at::kFloat || y.scalar_type() == at::kBFloat16)) {
       check(dlmpi_head1x1(a.x, ldx, xoff, (int64_t)N * H * W, C, a.w, a.ldw, a.bias, a.y, ldy, yoff, kv,
-                          y.scalar_type() == at::kFloat ? 1 : 0, cur_stream()),
+                          y.scalar_type() == at::kFloat ? 1 : 0, nullptr, nullptr, cur_stream()),
             "conv2d_fwd (1x1 head)");
       g_head_ran = 1;
       return 0;
@@ -767,6 +767,22 @@ static int conv2d_fwd_impl(const at::Tensor& x, int N, int H, int W, int C, int 
           "bn_finalize");
   }
   return p.mtiles;   // rows of the stats partial buffer
+}
+
+// The 1x1 head (<= 4 outputs) over a deferred BN-apply + ReLU input relu(z * scale + shift) (the UNet's
+// last decoder BN output, never stored): head.hip with the apply computed on the fly.
+void conv1x1_head_affine(const at::Tensor& z, int N, int H, int W, int C, int ldz, int zoff, const at::Tensor& w,
+                         int ldw, int kv, const at::Tensor& scale, const at::Tensor& shift, at::Tensor y, int ldy,
+                         int yoff, const c10::optional<at::Tensor>& bias) {
+  require_gpu(z, "z");
+  if (act_f32(z, "conv1x1_head_affine") || !dlmpi_head1x1_ok(C, kv) || ldz % 8 || zoff % 8 ||
+      scale.numel() < C || shift.numel() < C || (y.scalar_type() != at::kFloat && y.scalar_type() != at::kBFloat16))
+    throw std::runtime_error("conv1x1_head_affine: bf16 z, C in 16..512, <= 4 outputs, aligned rows");
+  check(dlmpi_head1x1(z.data_ptr(), ldz, zoff, (int64_t)N * H * W, C, w.data_ptr(), ldw, optr<float>(bias),
+                      y.data_ptr(), ldy, yoff, kv, y.scalar_type() == at::kFloat ? 1 : 0, ptr<float>(scale),
+                      ptr<float>(shift), cur_stream()),
+        "conv1x1_head_affine");
+  g_head_ran = 1;
 }
 
 int conv2d_fwd(const at::Tensor& x, int N, int H, int W, int C, int ldx, int xoff, const at::Tensor& w, int K, int R,
@@ -1733,6 +1749,8 @@ void register_ops(pybind11::module& m) {
   m.def("set_wgrad3", [](int mode) { g_wgrad3_override = mode; });
   m.def("set_wgrad3_blocks", [](int n) { g_wgrad3_blocks = n; });
   m.def("set_head1x1", [](int v) { g_head_on = v; });
+  m.def("head1x1_on", []() { return g_head_on; });
+  m.def("conv1x1_head_affine", &conv1x1_head_affine);
   m.def("set_conv_c8", [](int v) { g_c8_on = v; });
   m.def("set_convT_stream", [](int v) { g_convT_stream = v; });
   m.def("convT_stream_last", []() { return g_convT_stream_ran; });

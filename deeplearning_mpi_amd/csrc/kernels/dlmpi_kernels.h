@@ -282,7 +282,8 @@ int dlmpi_conv3x3_c8_blocks(int64_t pixels);
 hipError_t dlmpi_conv3x3_c8(const void* x, int ldx, int xoff, int N, int H, int W, const void* w, const float* bias,
                             void* y, int ldy, int yoff, float* stats, int G, hipStream_t s);
 hipError_t dlmpi_head1x1(const void* x, int ldx, int xoff, int64_t M, int C, const void* w, int ldw,
-                         const float* bias, void* y, int ldy, int yoff, int kv, int y_f32, hipStream_t s);
+                         const float* bias, void* y, int ldy, int yoff, int kv, int y_f32, const float* psc,
+                         const float* psh, hipStream_t s);
 // streaming 64 -> 64 3x3 conv: plan (tile th x tw, G blocks; 0 if it does not apply) + launch
 int dlmpi_conv3_stream_plan(int N, int H, int W, int C, int K, int blocks, int* th, int* tw, int* G);
 hipError_t dlmpi_conv3x3_stream(const dlmpi::Conv3StreamArgs* a, int mode, hipStream_t s);

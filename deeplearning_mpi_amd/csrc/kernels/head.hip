@@ -9,6 +9,8 @@
 // combined by a fixed xor-shuffle tree; the first lane of the row adds the bias and stores.  Four
 // row groups per wave are in flight per iteration.  The result differs from the MFMA path only in
 // the fp32 summation order.
+// psc / psh (optional): the input is a deferred BN-apply + ReLU of x -- bf16(relu(fma(x, psc, psh))),
+// bn_apply_kernel's arithmetic, so identical to reading the stored BN output -- computed on the fly.
 #include "common.h"
 
 namespace dlmpi {
@@ -17,7 +19,8 @@ template <int L, int KV, typename TO>
 __global__ __launch_bounds__(256) void head1x1_kernel(const uint16_t* __restrict__ x, int ldx, int xoff, int64_t M,
                                                       const uint16_t* __restrict__ w, int ldw,
                                                       const float* __restrict__ bias, TO* __restrict__ y, int ldy,
-                                                      int yoff) {
+                                                      int yoff, const float* __restrict__ psc,
+                                                      const float* __restrict__ psh) {
   constexpr int RPW = 64 / L;   // rows per wave instruction
   constexpr int U = 4;          // row groups in flight per wave
   const int lane = threadIdx.x & 63;
@@ -28,6 +31,10 @@ __global__ __launch_bounds__(256) void head1x1_kernel(const uint16_t* __restrict
     load8(w + (int64_t)k * ldw + sub * 8, wv[k]);
     b[k] = bias ? bias[k] : 0.f;
   }
+  float ps[8], ph[8];
+  if (psc)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) { ps[e] = psc[sub * 8 + e]; ph[e] = psh[sub * 8 + e]; }
   const int64_t wave = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   const int64_t step = (int64_t)gridDim.x * 4 * RPW * U;
   for (int64_t base = wave * RPW * U; base < M; base += step) {
@@ -39,6 +46,9 @@ __global__ __launch_bounds__(256) void head1x1_kernel(const uint16_t* __restrict
       else
 #pragma unroll
         for (int e = 0; e < 8; ++e) v[u][e] = 0.f;
+      if (psc)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[u][e] = bf2f(f2bf(fmaxf(__builtin_fmaf(v[u][e], ps[e], ph[e]), 0.f)));
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -65,7 +75,9 @@ extern "C" int dlmpi_head1x1_ok(int C, int kv) {
 }
 
 extern "C" hipError_t dlmpi_head1x1(const void* x, int ldx, int xoff, int64_t M, int C, const void* w, int ldw,
-                                    const float* bias, void* y, int ldy, int yoff, int kv, int y_f32, hipStream_t s) {
+                                    const float* bias, void* y, int ldy, int yoff, int kv, int y_f32,
+                                    const float* psc, const float* psh, hipStream_t s) {
+  if ((psc == nullptr) != (psh == nullptr)) return hipErrorInvalidValue;
   if (!dlmpi_head1x1_ok(C, kv) || M <= 0 || ldx % 8 || xoff % 8 || ldw % 8) return hipErrorInvalidValue;
   const int L = C / 8;
   const int64_t rows_per_block = 4LL * (64 / L) * 4;
@@ -76,10 +88,10 @@ extern "C" hipError_t dlmpi_head1x1(const void* x, int ldx, int xoff, int64_t M,
   do {                                                                                                         \
     if (y_f32)                                                                                                 \
       hipLaunchKernelGGL((head1x1_kernel<L_, KV_, float>), dim3(nblk), dim3(256), 0, s, xp, ldx, xoff, M, wp,   \
-                         ldw, bias, static_cast<float*>(y), ldy, yoff);                                        \
+                         ldw, bias, static_cast<float*>(y), ldy, yoff, psc, psh);                              \
     else                                                                                                       \
       hipLaunchKernelGGL((head1x1_kernel<L_, KV_, uint16_t>), dim3(nblk), dim3(256), 0, s, xp, ldx, xoff, M,    \
-                         wp, ldw, bias, static_cast<uint16_t*>(y), ldy, yoff);                                 \
+                         wp, ldw, bias, static_cast<uint16_t*>(y), ldy, yoff, psc, psh);                       \
   } while (0)
 #define HEAD_L(L_)                        \
   do {                                    \

@@ -26,6 +26,9 @@ from .engine import ConvTUnit, ConvUnit, EngineModule
 # reads it, which also stores it as the skip (pool.hip maxpool_fwd_fixed_kernel, ys): one pass over the
 # BN input instead of the apply pass plus the pool re-reading its output (profiles/r5_poolapply).
 FUSE_POOL_APPLY = True
+# Training forward: the last decoder BN-apply + ReLU is applied inside the 1x1 head kernel and the
+# head's weight gradient (operand prologue) instead of a stored pass (profiles/r5_poolapply).
+FUSE_HEAD_APPLY = True
 
 
 
@@ -185,7 +188,8 @@ class UNet(EngineModule):
             below = a
             ua, ub = self.dec[k]
             t, ca = ua.fwd(be, cat, train, save=save)
-            a, cb = ub.fwd(be, t, train, save=save)
+            # level 1's output is read only by the 1x1 head (forward and weight gradient): never stored
+            a, cb = ub.fwd(be, t, train, save=save, defer_apply="act" if (k == 0 and FUSE_HEAD_APPLY) else False)
             ctx_dec[k] = (below, ca, cb)
         K = self.out_classes
         out = torch.empty(N, H, W, K, dtype=be.dt, device=dev)

@@ -157,7 +157,15 @@ class NativeBackend:
 
     def conv_fwd(self, x, w, K, R, S, stride, pad, y: Act, bias=None, res: Act = None, scale=None,
                  shift=None, relu=False, stats=None, kvalid=0):
-        """Returns the number of BN-statistics rows written (stats given)."""
+        """Returns the number of BN-statistics rows written (stats given).  A Deferred.affine input is
+        materialized, except for the <= 4-output 1x1 head, which applies it on the fly."""
+        if (isinstance(x, Deferred) and x.kind == "affine" and R == 1 and S == 1 and stride == 1 and pad == 0
+                and 0 < kvalid <= 4 and res is None and scale is None and not relu and stats is None
+                and not self.f32 and x.C in (16, 32, 64, 128, 256, 512) and self.C.head1x1_on()):
+            z = x.src
+            self.C.conv1x1_head_affine(z.buf, z.N, z.H, z.W, z.C, z.ld, z.off, w, w.shape[-1], int(kvalid), x.k0,
+                                       x.k1, y.buf, y.ld, y.off, bias)
+            return 0
         x = self.materialize(x)
         return self.C.conv2d_fwd(x.buf, x.N, x.H, x.W, x.C, x.ld, x.off, w, K, R, S, stride, pad, y.buf, y.ld,
                                  y.off, bias, res.buf if res is not None else None,

@@ -1,7 +1,9 @@
 """The UNet encoder skip's BN-apply fused into the 2x2 max-pool (models/unet.py FUSE_POOL_APPLY,
-pool.hip maxpool_fwd_fixed_kernel with ys): kernel level -- pooled values, indices and the stored
-applied input bit-identical to bn_apply + max-pool; model level -- one UNet training step (loss, every
-gradient, running statistics) bit-identical to the unfused schedule."""
+pool.hip maxpool_fwd_fixed_kernel with ys) and the last decoder BN-apply fused into the 1x1 head and its
+weight gradient (FUSE_HEAD_APPLY): kernel level -- pooled values, indices and the stored applied input
+bit-identical to bn_apply + max-pool, the head over a Deferred.affine input bit-identical to the head
+over the stored apply; model level -- one UNet training step (loss, every gradient, running
+statistics) bit-identical to the unfused schedule."""
 import copy
 
 import pytest
@@ -10,7 +12,7 @@ import torch
 import deeplearning_mpi_amd.models.unet as unet_mod
 from deeplearning_mpi_amd.models import UNet
 from deeplearning_mpi_amd.ops import bce_with_logits
-from deeplearning_mpi_amd.ops.act import Act
+from deeplearning_mpi_amd.ops.act import Act, Deferred
 from deeplearning_mpi_amd.ops.backend import NativeBackend
 
 pytestmark = pytest.mark.gpu
@@ -39,6 +41,24 @@ def test_pool_apply_kernel_bit_identical(N, H, W, C, ld, off):
     assert torch.equal(idx0, idx1)
 
 
+def test_head_over_deferred_apply_bit_identical():
+    be = NativeBackend(DEV)
+    N, H, W, C = 2, 32, 48, 64
+    g = torch.Generator(device=DEV).manual_seed(11)
+    z = Act(torch.randn(N * H * W, C, device=DEV, generator=g).to(torch.bfloat16), N, H, W, C)
+    sc = torch.rand(C, device=DEV, generator=g) + 0.5
+    sh = torch.randn(C, device=DEV, generator=g) * 0.3
+    w = (torch.randn(8, C, device=DEV, generator=g) / 8).to(torch.bfloat16)
+    b = torch.randn(8, device=DEV, generator=g)
+    y0 = torch.empty(N * H * W, 1, device=DEV)
+    y1 = torch.empty(N * H * W, 1, device=DEV)
+    be.conv_fwd(be.materialize(Deferred.affine(z, sc, sh)), w, 8, 1, 1, 1, 0, Act(y0, N, H, W, 1), bias=b, kvalid=1)
+    be.conv_fwd(Deferred.affine(z, sc, sh), w, 8, 1, 1, 1, 0, Act(y1, N, H, W, 1), bias=b, kvalid=1)
+    torch.cuda.synchronize()
+    assert be.C.head1x1_last() == 1
+    assert torch.equal(y0, y1)
+
+
 def test_unet_step_bit_identical_to_unfused(monkeypatch):
     torch.manual_seed(0)
     base = UNet(out_classes=1).to(DEV)
@@ -47,6 +67,7 @@ def test_unet_step_bit_identical_to_unfused(monkeypatch):
     res = {}
     for fuse in (True, False):
         monkeypatch.setattr(unet_mod, "FUSE_POOL_APPLY", fuse)
+        monkeypatch.setattr(unet_mod, "FUSE_HEAD_APPLY", fuse)
         m = copy.deepcopy(base)
         loss = bce_with_logits(m(x).squeeze(1), t)
         loss.backward()
