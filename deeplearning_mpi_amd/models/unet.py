@@ -189,7 +189,9 @@ class UNet(EngineModule):
             ua, ub = self.dec[k]
             t, ca = ua.fwd(be, cat, train, save=save)
             # level 1's output is read only by the 1x1 head (forward and weight gradient): never stored
-            a, cb = ub.fwd(be, t, train, save=save, defer_apply="act" if (k == 0 and FUSE_HEAD_APPLY) else False)
+            # (the head's weight gradient rebuilds it in an operand prologue: bf16 backends only)
+            head_defer = k == 0 and FUSE_HEAD_APPLY and getattr(be, "prologue", False)
+            a, cb = ub.fwd(be, t, train, save=save, defer_apply="act" if head_defer else False)
             ctx_dec[k] = (below, ca, cb)
         K = self.out_classes
         out = torch.empty(N, H, W, K, dtype=be.dt, device=dev)
