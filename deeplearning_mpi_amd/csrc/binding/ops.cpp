@@ -1615,7 +1615,7 @@ void adam_step(at::Tensor p, const at::Tensor& g, at::Tensor m, at::Tensor v, do
 }
 // total L2 norm of a flat fp32 buffer -> norm_out[0]; coef_out = {min(1, max_norm/(norm+1e-6)), nonfinite}
 void grad_norm(const at::Tensor& g, double max_norm, at::Tensor norm_out, at::Tensor coef_out) {
-  const int nblk = 512;
+  const int nblk = 1024;
   at::Tensor partial = at::empty({nblk}, g.options().dtype(at::kFloat));
   check(dlmpi_sumsq(ptr<float>(g), g.numel(), ptr<float>(partial), nblk, cur_stream()), "sumsq");
   if (coef_out.numel() < 2) throw std::runtime_error("grad_norm: coef_out needs 2 (or 4) floats");

@@ -81,14 +81,37 @@ __global__ void adam_step_advance_kernel(float* __restrict__ tstep, const float*
   if (threadIdx.x == 0 && !(clip_coef && clip_coef[1] != 0.f)) *tstep += 1.f;
 }
 
+// 16-byte loads, four independent sums per thread, four loads in flight per iteration (the scalar
+// grid-stride loop ran at 1.1 TB/s: 110 us for the 31 M UNet gradients), scalar tail
 __global__ __launch_bounds__(256) void sumsq_kernel(const float* __restrict__ x, int64_t n,
                                                     float* __restrict__ partial) {
   __shared__ float sh[4];
-  float s = 0.f;
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-    const float v = x[i];
-    s += v * v;
+  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+  const int64_t n4 = ((uintptr_t)x & 15) == 0 ? n / 4 : 0;
+  const f32x4* x4 = reinterpret_cast<const f32x4*>(x);
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  for (; i + 3 * stride < n4; i += 4 * stride) {
+    f32x4 v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) v[u] = x4[i + u * stride];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      s0 = __builtin_fmaf(v[u][0], v[u][0], s0);
+      s1 = __builtin_fmaf(v[u][1], v[u][1], s1);
+      s2 = __builtin_fmaf(v[u][2], v[u][2], s2);
+      s3 = __builtin_fmaf(v[u][3], v[u][3], s3);
+    }
   }
+  for (; i < n4; i += stride) {
+    const f32x4 v = x4[i];
+    s0 = __builtin_fmaf(v[0], v[0], s0);
+    s1 = __builtin_fmaf(v[1], v[1], s1);
+    s2 = __builtin_fmaf(v[2], v[2], s2);
+    s3 = __builtin_fmaf(v[3], v[3], s3);
+  }
+  for (int64_t j = 4 * n4 + blockIdx.x * (int64_t)blockDim.x + threadIdx.x; j < n; j += stride) s0 += x[j] * x[j];
+  float s = (s0 + s1) + (s2 + s3);
   s = warp_sum(s);
   if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = s;
   __syncthreads();
