@@ -66,7 +66,28 @@ __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, const 
     bc1 = 1.f - powf(b1, t);
     bc2 = 1.f - powf(b2, t);
   }
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+  // 16-byte accesses when every state array is aligned (the flat arenas are), scalar tail; the
+  // per-element arithmetic is unchanged (bit-identical)
+  const bool vec = (((uintptr_t)p | (uintptr_t)g | (uintptr_t)m | (uintptr_t)v) & 15) == 0;
+  const int64_t n4 = vec ? n / 4 : 0;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n4; i += stride) {
+    f32x4 pv = reinterpret_cast<f32x4*>(p)[i], mv = reinterpret_cast<f32x4*>(m)[i];
+    f32x4 vv = reinterpret_cast<f32x4*>(v)[i];
+    const f32x4 gv = reinterpret_cast<const f32x4*>(g)[i];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      float pe = pv[e], me = mv[e], ve = vv[e];
+      adam_elem(pe, gv[e], me, ve, lr, b1, b2, eps, wd, adamw, bc1, bc2, coef);
+      pv[e] = pe;
+      mv[e] = me;
+      vv[e] = ve;
+    }
+    reinterpret_cast<f32x4*>(p)[i] = pv;
+    reinterpret_cast<f32x4*>(m)[i] = mv;
+    reinterpret_cast<f32x4*>(v)[i] = vv;
+  }
+  for (int64_t i = 4 * n4 + blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += stride) {
     float pv = p[i], mv = m[i], vv = v[i];
     adam_elem(pv, g[i], mv, vv, lr, b1, b2, eps, wd, adamw, bc1, bc2, coef);
     p[i] = pv;
@@ -173,7 +194,7 @@ extern "C" hipError_t dlmpi_sgd(float* p, const float* g, float* m, int64_t n, f
 extern "C" hipError_t dlmpi_adam(float* p, const float* g, float* m, float* v, int64_t n, float lr, float b1, float b2,
                                  float eps, float wd, int adamw, float bc1, float bc2, const float* clip_coef,
                                  float* tstep, hipStream_t s) {
-  hipLaunchKernelGGL(adam_kernel, dim3(blocks_for(n)), dim3(256), 0, s, p, g, m, v, n, lr, b1, b2, eps, wd, adamw,
+  hipLaunchKernelGGL(adam_kernel, dim3(blocks_for(n / 4 + 1)), dim3(256), 0, s, p, g, m, v, n, lr, b1, b2, eps, wd, adamw,
                      bc1, bc2, clip_coef, tstep);
   if (tstep) hipLaunchKernelGGL(adam_step_advance_kernel, dim3(1), dim3(64), 0, s, tstep, clip_coef);
   return hipGetLastError();
