@@ -162,7 +162,9 @@ class UNet(EngineModule):
             t, ca = ua.fwd(be, a, train, save=save)
             skip = cat.slice(self.up_ch[k], self.skip_ch[k])
             down = Act.empty(N, h // 2, w // 2, self.skip_ch[k], dt, dev)
-            if FUSE_POOL_APPLY and train and save:
+            # (only with the fused BN backward: its data gradient takes the ReLU mask from z, the unfused
+            # bn_bwd needs the stored y in the saved context)
+            if FUSE_POOL_APPLY and train and save and self.fuse_bn_bwd:
                 # the skip's BN-apply runs inside the pool, which stores it (one pass over z, not two)
                 z, cb = ub.fwd(be, t, train, out=skip, save=save, defer_apply=True)
                 idx = be.maxpool_fwd(z, 2, 2, 0, down, bn=(cb[5], cb[6]), store=skip)
@@ -190,7 +192,7 @@ class UNet(EngineModule):
             t, ca = ua.fwd(be, cat, train, save=save)
             # level 1's output is read only by the 1x1 head (forward and weight gradient): never stored
             # (the head's weight gradient rebuilds it in an operand prologue: bf16 backends only)
-            head_defer = k == 0 and FUSE_HEAD_APPLY and getattr(be, "prologue", False)
+            head_defer = k == 0 and FUSE_HEAD_APPLY and self.fuse_bn_bwd and getattr(be, "prologue", False)
             a, cb = ub.fwd(be, t, train, save=save, defer_apply="act" if head_defer else False)
             ctx_dec[k] = (below, ca, cb)
         K = self.out_classes

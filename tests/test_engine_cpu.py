@@ -92,13 +92,22 @@ def test_bottleneck_blocks_exact():
             assert ((p1.grad - p2.grad).abs().max() / p2.grad.abs().max()).item() < 1e-5, n
 
 
+@pytest.mark.parametrize("fused", [True, False])
 @pytest.mark.parametrize("mode", ["conv_transpose", "bilinear"])
-def test_unet_train_step_matches_torch(mode):
+def test_unet_train_step_matches_torch(mode, fused):
+    """Both backward schedules: fused BN-backward epilogues, and separate bn_bwd passes (the pool-
+    and head-apply deferrals must then keep the stored BN output for the ReLU mask)."""
     g = torch.Generator().manual_seed(1)
     x = torch.randn(4, 3, 64, 64, generator=g)
     y = (torch.rand(4, 64, 64, generator=g) > 0.5).float()
     skip = lambda n: n.endswith("bias") and "double_conv.double_conv" in n  # conv bias before train-BN: grad == 0
-    _run_pair(lambda: UNet(out_classes=1, up_sample_mode=mode), x, y, lambda o, t: bce_with_logits(o.squeeze(1), t),
+
+    def make():
+        m = UNet(out_classes=1, up_sample_mode=mode)
+        m.fuse_bn_bwd = fused
+        return m
+
+    _run_pair(make, x, y, lambda o, t: bce_with_logits(o.squeeze(1), t),
               lambda o, t: F.binary_cross_entropy_with_logits(o.squeeze(1), t), skip=skip)
 
 
