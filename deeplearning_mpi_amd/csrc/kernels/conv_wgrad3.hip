@@ -6,9 +6,9 @@
 // K-step and gathers X once per (pixel, tap): every X element is fetched 9 times per Ko tile and
 // every K-step pays a per-lane im2col decode.  Here a K-step is an 8 x 8 block of output pixels of
 // one image: its dY rows [64][KT] and the 10 x 10 X halo around it [100][CT] are staged once
-// (LDS-DMA, double-buffered: the next block's DMA is issued right after the K-step's barrier through
-// glds16_raw, so the compiler adds no drain before the transposed reads -- with the builtin it did,
-// and no DMA latency was hidden: profiles/r5_wgrad), and all 9 taps are 9 GEMMs over the SAME staged tiles --
+// (LDS-DMA through a 3-stage ring, issued through glds16_raw, so the compiler adds no drain before
+// the transposed reads -- with the builtin it did, and no DMA latency was hidden: profiles/r5_wgrad),
+// and all 9 taps are 9 GEMMs over the SAME staged tiles --
 // tap (r, s) reads the halo window shifted by (r, s).  Out-of-image halo pixels are staged as
 // zeros, which IS the zero padding for every tap, so no per-tap masking exists anywhere.  The
 // block owns dW for all 9 taps of a KT x CT (ko, c) tile: 9 x (KT x CT) fp32 accumulators over 8
@@ -28,6 +28,7 @@
 // Reference semantics: nn.Conv2d(3x3, padding=1) weight gradient of every UNet DoubleConv and the
 // ResNet bottleneck conv2 (/root/reference/pytorch/unet/model.py:9-14, resnet main.py:40-41).
 #include <cstdlib>
+#include <type_traits>
 
 #include "common.h"
 
@@ -57,19 +58,32 @@ __device__ __forceinline__ int w3_halo_swz(int line, int col) {
 // transposed reads per 9 x 64 x 16 MACs.  128 x 64 = 2 x 4 waves, 64 x 128 = 1 x 8, 64 x 64 = 1 x 4
 // (a 4-wave block, 2 per CU: the 2 x 2 grid of 32 x 16 wave tiles it replaced read 1.7x the LDS
 // bytes per MFMA).
+//
+// Pipeline (round 6, profiles/r6_wgrad3: -9 to -10 % on every UNet / ResNet 3x3 shape against the
+// round-5 double buffer, bit-identical):
+//  * a 3-stage LDS ring: the DMA of step t + 2 is issued during step t (two steps of latency cover;
+//    a 4th stage measured no better, and costs the 64 x 64 tile its second block per CU);
+//  * a wave's AL + BL DMA pieces go out one per tap slot of the first 32 pixels, between its MFMAs,
+//    instead of all at once after the barrier (where every wave of the CU issued at once);
+//  * the step loop is unrolled by the 3 stages, so each stage index is a constant: LDS holds the
+//    three A stages, then the three B stages, and every fragment read is a loop-invariant lane offset
+//    plus an immediate (no address arithmetic per read);
+//  * every step issues a DMA (past the split's last tile: that tile again, into the stage nobody
+//    reads), so the vmcnt of a step is a constant.
 template <int KT, int CT, int WR, int WC>
 __global__ __launch_bounds__(64 * WR * WC) __attribute__((amdgpu_waves_per_eu(2, 8)))
 void wgrad3x3_kernel(const Wgrad3Args a) {
+  constexpr int STAGES = 3;
   constexpr int NT = 64 * WR * WC;
   constexpr int WM = KT / WR, WN = CT / WC;   // per-wave ko x c
   constexpr int TM = WM / 16, TN = WN / 16;
   constexpr int A_ROW = KT * 2, B_ROW = CT * 2;
   constexpr int A_BYTES = 64 * A_ROW;         // 64 output pixels
   constexpr int B_BYTES = 128 * B_ROW;        // 100 halo rows, slots of rows 100..127 unused
-  constexpr int SB = A_BYTES + B_BYTES;
   constexpr int AL = A_BYTES / (16 * NT), BL = B_BYTES / (16 * NT);
-  static_assert(AL >= 1 && BL >= 1 && TM >= 1 && TN >= 1, "tile shape");
-  __shared__ __attribute__((aligned(16))) char smem[2 * SB];
+  constexpr int PER = AL + BL;                // DMA pieces per wave per step
+  static_assert(AL >= 1 && BL >= 1 && TM >= 1 && TN >= 1 && PER <= 9, "tile shape");
+  __shared__ __attribute__((aligned(16))) char smem[STAGES * (A_BYTES + B_BYTES)];
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -78,10 +92,14 @@ void wgrad3x3_kernel(const Wgrad3Args a) {
   const uint32_t bid = xcd_remap(blockIdx.x, gridDim.x);
   const int z = bid / nkc;
   const int kc = bid - z * nkc;
-  const int mt = kc / a.ntiles, nt = kc - mt * a.ntiles;
+  // consecutive blocks (one XCD's range, xcd_remap) walk the ko tiles fastest: an XCD's blocks share
+  // a few X tiles AND a few dY tiles in its L2 (ko-slowest: every X tile of the row once per XCD; L2
+  // hit rate 66 % -> 81 % at 64^2 1536 -> 512, profiles/r6_wgrad3)
+  const int mt = kc % a.mtiles, nt = kc / a.mtiles;
   const int ko0 = mt * KT, c0 = nt * CT;
   const int t_beg = z * a.tiles_per_split;
   const int t_end = min(a.ntiles_pix, t_beg + a.tiles_per_split);
+  if (t_beg >= t_end) return;   // (never: the host sizes the splits to the tiles)
   const char* zp = reinterpret_cast<const char*>(g_zero_page);
   const int H = a.H, W = a.W;
 
@@ -110,52 +128,70 @@ void wgrad3x3_kernel(const Wgrad3Args a) {
   }
   const char* dyb = static_cast<const char*>(a.dy);
   const char* xb = static_cast<const char*>(a.x);
+  char* const sA = smem;                        // A stages
+  char* const sB = smem + STAGES * A_BYTES;     // B stages
 
-  auto issue = [&](int buf, int n, int h0, int w0) {
-    char* As = smem + buf * SB;
-    char* Bs = As + A_BYTES;
-    const int64_t pix = ((int64_t)n * H + h0) * W + w0;   // wave-uniform tile origin
-    const char* da = dyb + 2 * pix * a.ldy;
-    const char* db = xb + 2 * pix * a.ldx;
-    const int hl = H - h0, wl = W - w0;
-#pragma unroll
-    for (int i = 0; i < AL; ++i) {
-      const bool ok = a_pi[i] < hl && a_pj[i] < wl;
-      const char* src = ok ? da + a_off[i] : zp;
-      glds16_raw(src, As + 16 * (NT * i + 64 * wid));
+  // the tile whose DMA goes out next (walked incrementally, wave-uniform; clamped to the last tile)
+  int n = 0, ti = 0, tj = 0, t_iss = t_beg;
+  {
+    const int per_img = a.tiles_h * a.tiles_w;
+    n = t_beg / per_img;
+    const int rem = t_beg - n * per_img;
+    ti = rem / a.tiles_w;
+    tj = rem - ti * a.tiles_w;
+  }
+  const char* da = nullptr;   // origin of the tile being issued
+  const char* db = nullptr;
+  int ih0 = 0, iw0 = 0;
+  auto set_origin = [&]() {
+    ih0 = ti * 8;
+    iw0 = tj * 8;
+    const int64_t pix = ((int64_t)n * H + ih0) * W + iw0;
+    da = dyb + 2 * pix * a.ldy;
+    db = xb + 2 * pix * a.ldx;
+    if (++t_iss < t_end && ++tj == a.tiles_w) {
+      tj = 0;
+      if (++ti == a.tiles_h) { ti = 0; ++n; }
     }
-#pragma unroll
-    for (int i = 0; i < BL; ++i) {
-      const bool ok = (unsigned)(h0 + b_li[i]) < (unsigned)H && (unsigned)(w0 + b_co[i]) < (unsigned)W;
-      const char* src = ok ? db + b_off[i] : zp;
-      glds16_raw(src, Bs + 16 * (NT * i + 64 * wid));
+  };
+  auto piece = [&](int buf, int i) {
+    if (i < AL) {
+      const bool ok = a_pi[i] < H - ih0 && a_pj[i] < W - iw0;
+      glds16_raw(ok ? da + a_off[i] : zp, sA + buf * A_BYTES + 16 * (NT * i + 64 * wid));
+    } else {
+      const int j = i - AL;
+      const bool ok = (unsigned)(ih0 + b_li[j]) < (unsigned)H && (unsigned)(iw0 + b_co[j]) < (unsigned)W;
+      glds16_raw(ok ? db + b_off[j] : zp, sB + buf * B_BYTES + 16 * (NT * j + 64 * wid));
     }
   };
 
-  // ---- fragment reads ------------------------------------------------------------------------
+  // ---- fragment reads: loop-invariant lane byte offsets (kk = 0; kk = 1 adds an immediate) ------
+  // dY fragment mi: ko columns 16 cb .. +15, pixels kk*32 + 8g + {q, q+4}; X fragment of tap t = (r, s):
+  // c columns 16 cb .. +15, the same pixels -> halo (line, col) = (4 kk + g + r, {q, q+4} + s)
   const int g = lane >> 4, fi = lane & 15, q = fi >> 2, p = fi & 3;
-  auto tr2 = [](const char* p0, const char* p1) -> bf16x8 {
-    const i16x4 v0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((w3_lds_i16x4*)(p0));
-    const i16x4 v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((w3_lds_i16x4*)(p1));
+  int a_ln[TM][2], b_ln[9][TN][2];
+#pragma unroll
+  for (int mi = 0; mi < TM; ++mi)
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int r0 = 8 * g + q + 4 * h;
+      const int ch = 2 * ((wm * WM) / 16 + mi) + (p >> 1);
+      a_ln[mi][h] = r0 * A_ROW + ((ch ^ w3_dy_swz<A_ROW>(r0)) << 4) + (p & 1) * 8;
+    }
+#pragma unroll
+  for (int t = 0; t < 9; ++t)
+#pragma unroll
+    for (int ni = 0; ni < TN; ++ni)
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int line = g + t / 3, col = q + t % 3 + 4 * h;
+        const int ch = 2 * ((wn * WN) / 16 + ni) + (p >> 1);
+        b_ln[t][ni][h] = (line * 10 + col) * B_ROW + ((ch ^ w3_halo_swz<B_ROW>(line, col)) << 4) + (p & 1) * 8;
+      }
+  auto rd = [](const char* ptr) { return __builtin_amdgcn_ds_read_tr16_b64_v4i16((w3_lds_i16x4*)(ptr)); };
+  auto frag = [](i16x4 v0, i16x4 v1) -> bf16x8 {
     typedef short i16x8 __attribute__((ext_vector_type(8)));
     return __builtin_bit_cast(bf16x8, (i16x8)__builtin_shufflevector(v0, v1, 0, 1, 2, 3, 4, 5, 6, 7));
-  };
-  // dY fragment: ko columns 16 cb .. +15, pixels kk*32 + 8g + {q, q+4}
-  auto a_frag = [&](const char* As, int kk, int cb) -> bf16x8 {
-    const int r0 = kk * 32 + 8 * g + q;
-    const int ch = 2 * cb + (p >> 1);
-    const char* p0 = As + r0 * A_ROW + ((ch ^ w3_dy_swz<A_ROW>(r0)) << 4) + (p & 1) * 8;
-    const char* p1 = As + (r0 + 4) * A_ROW + ((ch ^ w3_dy_swz<A_ROW>(r0 + 4)) << 4) + (p & 1) * 8;
-    return tr2(p0, p1);
-  };
-  // X fragment of tap (r, s): c columns 16 cb .. +15, pixels kk*32 + 8g + {q, q+4} -> halo
-  // (line, col) = (4 kk + g + r, {q, q+4} + s)
-  auto b_frag = [&](const char* Bs, int kk, int r, int s, int cb) -> bf16x8 {
-    const int line = 4 * kk + g + r, col = q + s;
-    const int ch = 2 * cb + (p >> 1);
-    const char* p0 = Bs + (line * 10 + col) * B_ROW + ((ch ^ w3_halo_swz<B_ROW>(line, col)) << 4) + (p & 1) * 8;
-    const char* p1 = Bs + (line * 10 + col + 4) * B_ROW + ((ch ^ w3_halo_swz<B_ROW>(line, col + 4)) << 4) + (p & 1) * 8;
-    return tr2(p0, p1);
   };
 
   f32x4 acc[9][TM][TN];
@@ -166,53 +202,54 @@ void wgrad3x3_kernel(const Wgrad3Args a) {
 #pragma unroll
       for (int ni = 0; ni < TN; ++ni) acc[t][mi][ni] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  // pixel-tile walk: tile t -> (n, ti, tj), advanced incrementally (wave-uniform)
-  int n = 0, ti = 0, tj = 0;
-  if (t_beg < t_end) {
-    const int per_img = a.tiles_h * a.tiles_w;
-    n = t_beg / per_img;
-    const int rem = t_beg - n * per_img;
-    ti = rem / a.tiles_w;
-    tj = rem - ti * a.tiles_w;
-    issue(0, n, ti * 8, tj * 8);
+#pragma unroll
+  for (int st = 0; st < STAGES - 1; ++st) {
+    set_origin();
+#pragma unroll
+    for (int i = 0; i < PER; ++i) piece(st, i);
   }
-  for (int t = t_beg; t < t_end; ++t) {
-    const int cur = (t - t_beg) & 1;
-    if (++tj == a.tiles_w) {
-      tj = 0;
-      if (++ti == a.tiles_h) { ti = 0; ++n; }
-    }
-    // stage cur landed (this wave's DMA: vmcnt(0); every wave's: the barrier); every wave's reads of
-    // stage cur^1 (step t - 1) have returned (lgkmcnt(0)) -> it may be refilled.  The DMA is issued
-    // through glds16_raw, so no compiler wait drains it before the fragment reads below: it has the
-    // whole K-step to land.
-    asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)" ::: "memory");
+  // one K-step on stage S (a constant)
+  auto step = [&](auto Sc) {
+    constexpr int S = decltype(Sc)::value;
+    constexpr int NB = (S + STAGES - 1) % STAGES;   // the stage refilled during this step
+    // stage S landed (this wave's DMA: only the newer stage may still be in flight; every wave's: the
+    // barrier); every wave's reads of stage NB (the previous step) have returned (lgkmcnt(0)).  The DMA
+    // goes through glds16_raw, so no compiler wait drains it before the fragment reads.
+    asm volatile("s_waitcnt vmcnt(%0)\n\ts_waitcnt lgkmcnt(0)" ::"n"((STAGES - 2) * PER) : "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
-    if (t + 1 < t_end) issue(cur ^ 1, n, ti * 8, tj * 8);
-    const char* As = smem + cur * SB;
-    const char* Bs = As + A_BYTES;
+    set_origin();
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
+      const char* As = sA + S * A_BYTES + kk * 32 * A_ROW;
+      const char* Bs = sB + S * B_BYTES + kk * 4 * 10 * B_ROW;
       bf16x8 af[TM];
 #pragma unroll
-      for (int mi = 0; mi < TM; ++mi) af[mi] = a_frag(As, kk, (wm * WM) / 16 + mi);
+      for (int mi = 0; mi < TM; ++mi) af[mi] = frag(rd(As + a_ln[mi][0]), rd(As + a_ln[mi][1]));
 #pragma unroll
-      for (int r = 0; r < 3; ++r)
+      for (int t = 0; t < 9; ++t) {
+        bf16x8 bfr[TN];
 #pragma unroll
-        for (int s = 0; s < 3; ++s) {
-          bf16x8 bfr[TN];
+        for (int ni = 0; ni < TN; ++ni) bfr[ni] = frag(rd(Bs + b_ln[t][ni][0]), rd(Bs + b_ln[t][ni][1]));
 #pragma unroll
-          for (int ni = 0; ni < TN; ++ni) bfr[ni] = b_frag(Bs, kk, r, s, (wn * WN) / 16 + ni);
+        for (int mi = 0; mi < TM; ++mi)
 #pragma unroll
-          for (int mi = 0; mi < TM; ++mi)
+          for (int ni = 0; ni < TN; ++ni)
+            acc[t][mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[mi], bfr[ni], acc[t][mi][ni], 0, 0, 0);
+        if (kk == 0) {   // DMA piece i after tap slot (9 i) / PER
 #pragma unroll
-            for (int ni = 0; ni < TN; ++ni)
-              acc[r * 3 + s][mi][ni] =
-                  __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[mi], bfr[ni], acc[r * 3 + s][mi][ni], 0, 0, 0);
+          for (int i = 0; i < PER; ++i)
+            if ((9 * i) / PER == t) piece(NB, i);
         }
+      }
     }
+  };
+  for (int t = t_beg; t < t_end; t += STAGES) {
+    step(std::integral_constant<int, 0>{});
+    if (t + 1 < t_end) step(std::integral_constant<int, 1>{});
+    if (t + 2 < t_end) step(std::integral_constant<int, 2>{});
   }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the trailing (unread) DMA lands before exit
 
   // ---- partial of this split: ws[z][ko][tap * C + c] (D: lane holds c = lane & 15, ko rows 4g + j)
   float* wsz = a.ws + (int64_t)z * a.Ko * (9 * a.C);
