@@ -74,12 +74,12 @@ def _free_port() -> int:
         return s.getsockname()[1]
 
 
-def launch_ranks(n: int, launcher: str, argv) -> int:
-    """Start ``n`` ranks of this script as child processes (no torch import, no GPU touched in this
-    process) and return the first non-zero exit code (0 if all ranks succeeded)."""
+def launch_ranks(n: int, launcher: str, argv, script: str | None = None) -> int:
+    """Start ``n`` ranks of ``script`` (default: this one) as child processes (no torch import, no GPU
+    touched in this process) and return the first non-zero exit code (0 if all ranks succeeded)."""
     env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", MASTER_ADDR="127.0.0.1")
     env["PYTHONPATH"] = ROOT + (os.pathsep + env["PYTHONPATH"] if env.get("PYTHONPATH") else "")
-    script = os.path.abspath(__file__)
+    script = script or os.path.abspath(__file__)
     if launcher == "mpirun":
         mpirun = shutil.which("mpirun") or "/opt/conda/bin/mpirun"
         cmd = [mpirun, "-n", str(n), sys.executable, script, *argv]
@@ -137,7 +137,17 @@ def main():
                     help="A/B only: kernel-choice pins NAME=V[,NAME=V] -- pipe / halo / stream / dgrad_stream / "
                          "autotune / wgrad3 / splitk (the extension's test setters; -1 = production choice), "
                          "defer=0 (weight-gradient reductions launched one by one)")
+    ap.add_argument("--rccl_channels", default=None,
+                    help="RCCL channel (CU) cap: N, 0 (RCCL's choice) or auto (calibrated at init: the smallest cap "
+                         "of 8/16/32 reaching 90 %% of the best all-reduce bus bandwidth, parallel/comm.py "
+                         "calibrate_channels); default DLMPI_RCCL_CHANNELS or 16")
+    ap.add_argument("--bucket_probe", type=int, default=1,
+                    help="1 (default): with an RCCL reducer (N > 1 or --rccl1) and no hipGraph, one untimed step "
+                         "after the timed region times every bucket all-reduce on the comm stream (dist.buckets)")
     args = ap.parse_args()
+    if args.rccl_channels is not None:
+        os.environ["DLMPI_RCCL_CHANNELS"] = str(args.rccl_channels)
+        os.environ.pop("NCCL_MAX_NCHANNELS", None)
     if args.rehearse > 0:
         args.rccl1 = 1
         os.environ["DLMPI_RCCL_CHANNELS"] = str(args.rehearse)
@@ -370,12 +380,46 @@ def main():
                                   "ooms": ms.get("num_ooms", 0),
                                   "device_total_gb": round(torch.cuda.get_device_properties(dev).total_memory / 2 ** 30, 1)}}),
               file=sys.stderr, flush=True)
+    # one untimed step with every bucket all-reduce timed on the comm stream: when each bucket left,
+    # how long it ran, its bus bandwidth, and how far the last one ended after the backward's compute
+    bucket_info = None
+    bc = getattr(ddp, "_bucket_comm", None)
+    if args.bucket_probe and not args.graph and bc is not None and hasattr(bc, "set_timing"):
+        bc.set_timing(True)
+        step()
+        sync()
+        bc.set_timing(False)
+        tm_ = bc.timings()
+        bl = tm_["buckets"]
+        if bl and "compute_end_ms" in tm_:
+            v = torch.tensor([b["dur_ms"] for b in bl] + [b["start_ms"] + b["dur_ms"] for b in bl] +
+                             [tm_["compute_end_ms"]], dtype=torch.float64, device=dev)
+            comm.allreduce(v, "max")   # every rank's slowest: the collective ends on the last rank
+            nb = len(bl)
+            durs, ends, cend = v[:nb].tolist(), v[nb:2 * nb].tolist(), float(v[-1])
+            from deeplearning_mpi_amd.parallel.comm import bus_gbps
+
+            bucket_info = {
+                "buckets": [{"mb": round(b["bytes"] / 2 ** 20, 2), "start_ms": round(b["start_ms"], 3),
+                             "dur_ms": round(d, 3),
+                             "busbw_gbps": round(bus_gbps("allreduce", b["bytes"], d / 1e3, world), 1)}
+                            for b, d in zip(bl, durs)],
+                "backward_compute_end_ms": round(cend, 3),
+                # > 0: all-reduce still running after the backward's compute (exposed); < 0: hidden
+                "comm_tail_ms": round(max(ends) - cend, 3),
+                "allreduce_ms_total": round(sum(durs), 3),
+            }
     # distributed facts of this run: the world size RCCL itself reports, its CU (channel) budget,
     # the gradient bucket layout, per-rank step times and the exposed all-reduce (max over ranks)
-    native_comm = getattr(getattr(ddp.comm, "inner", ddp.comm), "c", None)
+    inner = getattr(ddp.comm, "inner", ddp.comm)
+    native_comm = getattr(inner, "c", None)
+    budget = getattr(inner, "budget", None) or {}
+    cap = int(native_comm.max_ctas()) if native_comm is not None and hasattr(native_comm, "max_ctas") else 0
     dist_info = {
         "rccl_world_size": int(native_comm.size()) if native_comm is not None else None,
-        "rccl_channels": os.environ.get("NCCL_MAX_NCHANNELS") if native_comm is not None else None,
+        "rccl_channels": (str(cap) if cap > 0 else os.environ.get("NCCL_MAX_NCHANNELS")) if native_comm is not None else None,
+        "rccl_channel_calibration": budget.get("calibration"),
+        "bucket_probe": bucket_info,
         "dgrad_stream_blocks": int(_native().dgs_blocks()),
         "wgrad_reduce_launches_per_step": int(red_per_step) if args.warmup > 0 else None,
         "bucket_mb": [round(b, 2) for b in ddp.bucket_sizes_mb()],

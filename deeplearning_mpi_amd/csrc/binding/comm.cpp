@@ -77,7 +77,7 @@ struct RcclComm::Impl {
   c10::hip::HIPStream stream;
   hipStream_t raw = nullptr;                 // owned; `stream` wraps it
   std::vector<hipStream_t> retired;          // streams abandoned in capture mode (never reused)
-  int rank = 0, size = 1, device = 0;
+  int rank = 0, size = 1, device = 0, max_ctas = 0;
   std::vector<hipEvent_t> events;   // ring of pre-created events for stream fences
   size_t next_event = 0;
   explicit Impl(c10::hip::HIPStream s) : stream(s) {}
@@ -202,21 +202,13 @@ pybind11::bytes RcclComm::unique_id() {
   return pybind11::bytes(reinterpret_cast<const char*>(&id), sizeof(id));
 }
 
-RcclComm::RcclComm(const std::string& uid, int rank, int size, int device) {
+RcclComm::RcclComm(const std::string& uid, int rank, int size, int device, int max_ctas) {
   if (uid.size() != sizeof(ncclUniqueId)) throw std::runtime_error("RcclComm: bad unique id size");
   hip_check(hipSetDevice(device), "hipSetDevice");
   // Default priority: a high-priority stream inside a hipGraph capture was seen to segfault in
   // capture_end on this ROCm build (profiles/r1_hipri_rejected), and the comm stream joins every
   // captured DDP step.
-  constexpr bool hipri = false;
-  hipStream_t raw = nullptr;
-  if (hipri) {
-    int lo = 0, hi = 0;
-    hip_check(hipDeviceGetStreamPriorityRange(&lo, &hi), "hipDeviceGetStreamPriorityRange");
-    hip_check(hipStreamCreateWithPriority(&raw, hipStreamNonBlocking, hi), "hipStreamCreateWithPriority");
-  } else {
-    raw = new_raw_stream();
-  }
+  hipStream_t raw = new_raw_stream();
   impl_ = std::make_unique<Impl>(c10::hip::getStreamFromExternal(raw, (c10::DeviceIndex)device));
   impl_->raw = raw;
   impl_->rank = rank;
@@ -224,7 +216,16 @@ RcclComm::RcclComm(const std::string& uid, int rank, int size, int device) {
   impl_->device = device;
   ncclUniqueId id;
   std::memcpy(&id, uid.data(), sizeof(id));
-  nccl_check(ncclCommInitRank(&impl_->comm, size, id, rank), "ncclCommInitRank");
+  if (max_ctas > 0) {
+    // (the fields up to maxCTAs sit at the same offsets in every RCCL 2.2x config layout; the library
+    // reads the ones its version knows)
+    ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+    cfg.maxCTAs = max_ctas;
+    nccl_check(ncclCommInitRankConfig(&impl_->comm, size, id, rank, &cfg), "ncclCommInitRankConfig");
+  } else {
+    nccl_check(ncclCommInitRank(&impl_->comm, size, id, rank), "ncclCommInitRank");
+  }
+  impl_->max_ctas = max_ctas;
   impl_->start_watchdog();
 }
 
@@ -248,6 +249,7 @@ void RcclComm::destroy() {
 
 int RcclComm::rank() const { return impl_->rank; }
 int RcclComm::size() const { return impl_->size; }
+int RcclComm::max_ctas() const { return impl_->max_ctas; }
 int64_t RcclComm::stream_handle() const { return (int64_t)(void*)impl_->stream.stream(); }
 
 // comm stream waits for everything enqueued so far on the caller's current stream
@@ -399,6 +401,7 @@ Reducer::Reducer(std::vector<at::Tensor> buckets, std::vector<int64_t> param_buc
 }
 
 void Reducer::prepare_for_backward() {
+  comm_->begin_step();
   pending_ = expected_;
   std::fill(seen_.begin(), seen_.end(), 0);
   next_ = 0;
@@ -438,11 +441,12 @@ void Reducer::finalize() {
 void register_comm(pybind11::module& m) {
   namespace py = pybind11;
   py::class_<RcclComm, std::shared_ptr<RcclComm>>(m, "RcclComm")
-      .def(py::init<const std::string&, int, int, int>(), py::arg("uid"), py::arg("rank"), py::arg("size"),
-           py::arg("device"))
+      .def(py::init<const std::string&, int, int, int, int>(), py::arg("uid"), py::arg("rank"), py::arg("size"),
+           py::arg("device"), py::arg("max_ctas") = 0)
       .def_static("unique_id", &RcclComm::unique_id)
       .def("rank", &RcclComm::rank)
       .def("size", &RcclComm::size)
+      .def("max_ctas", &RcclComm::max_ctas)
       .def("stream_handle", &RcclComm::stream_handle)
       .def("allreduce", &RcclComm::allreduce, py::arg("t"), py::arg("op") = "sum", py::arg("async_op") = false)
       .def("broadcast", &RcclComm::broadcast, py::arg("t"), py::arg("root") = 0, py::arg("async_op") = false)
@@ -460,12 +464,15 @@ void register_comm(pybind11::module& m) {
 
   py::class_<CommBase, PyCommBase, std::shared_ptr<CommBase>>(m, "CommBase")
       .def(py::init<>())
+      .def("begin_step", &CommBase::begin_step)
       .def("begin_bucket", &CommBase::begin_bucket)
       .def("allreduce_bucket", &CommBase::allreduce_bucket)
       .def("end_backward", &CommBase::end_backward);
 
   py::class_<RcclBucketComm, CommBase, std::shared_ptr<RcclBucketComm>>(m, "RcclBucketComm")
-      .def(py::init<std::shared_ptr<RcclComm>>());
+      .def(py::init<std::shared_ptr<RcclComm>>())
+      .def("set_timing", &RcclBucketComm::set_timing)
+      .def("timings", &RcclBucketComm::timings);
 
   py::class_<RehearsalBucketComm, CommBase, std::shared_ptr<RehearsalBucketComm>>(m, "RehearsalBucketComm")
       .def(py::init<std::shared_ptr<RcclComm>, int, int, int, double, double, double>())
@@ -484,9 +491,69 @@ void register_comm(pybind11::module& m) {
 // RCCL-backed bucket comm: begin_bucket fences the comm stream behind the compute stream once
 // per newly completed group of buckets, allreduce_bucket enqueues on the comm stream,
 // end_backward makes the compute stream wait for all of them.
+RcclBucketComm::~RcclBucketComm() {
+  for (hipEvent_t e : pool_) hipEventDestroy(e);
+}
+hipEvent_t RcclBucketComm::tev() {   // a timing event from the pool (reused every timed step)
+  if (used_ == pool_.size()) {
+    hipEvent_t e;
+    hip_check(hipEventCreate(&e), "hipEventCreate");
+    pool_.push_back(e);
+  }
+  return pool_[used_++];
+}
+void RcclBucketComm::begin_step() {
+  recs_.clear();
+  used_ = 0;
+  ref_ = cend_ = nullptr;
+  if (!timing_) return;
+  ref_ = tev();
+  hip_check(hipEventRecord(ref_, c10::hip::getCurrentHIPStream().stream()), "hipEventRecord");
+}
 void RcclBucketComm::begin_bucket() { comm_->fence_in(); }
-void RcclBucketComm::allreduce_bucket(at::Tensor t, bool average) { comm_->allreduce_async(t, average ? "avg" : "sum"); }
-void RcclBucketComm::end_backward() { comm_->fence_out(); }
+void RcclBucketComm::allreduce_bucket(at::Tensor t, bool average) {
+  if (!timing_ || ref_ == nullptr) {
+    comm_->allreduce_async(t, average ? "avg" : "sum");
+    return;
+  }
+  hipStream_t cs = reinterpret_cast<hipStream_t>(comm_->stream_handle());
+  Rec r{t.numel() * t.element_size(), tev(), tev()};
+  hip_check(hipEventRecord(r.a, cs), "hipEventRecord");
+  comm_->allreduce_async(t, average ? "avg" : "sum");
+  hip_check(hipEventRecord(r.b, cs), "hipEventRecord");
+  recs_.push_back(r);
+}
+void RcclBucketComm::end_backward() {
+  if (timing_ && ref_ != nullptr) {
+    cend_ = tev();
+    hip_check(hipEventRecord(cend_, c10::hip::getCurrentHIPStream().stream()), "hipEventRecord");
+  }
+  comm_->fence_out();
+}
+pybind11::dict RcclBucketComm::timings() {
+  namespace py = pybind11;
+  py::dict d;
+  py::list bl;
+  if (ref_ != nullptr && cend_ != nullptr) {
+    hip_check(hipEventSynchronize(cend_), "hipEventSynchronize");
+    for (const Rec& r : recs_) {
+      hip_check(hipEventSynchronize(r.b), "hipEventSynchronize");
+      float a = 0.f, b = 0.f;
+      hip_check(hipEventElapsedTime(&a, ref_, r.a), "hipEventElapsedTime");
+      hip_check(hipEventElapsedTime(&b, r.a, r.b), "hipEventElapsedTime");
+      py::dict e;
+      e["bytes"] = r.bytes;
+      e["start_ms"] = a;
+      e["dur_ms"] = b;
+      bl.append(e);
+    }
+    float ce = 0.f;
+    hip_check(hipEventElapsedTime(&ce, ref_, cend_), "hipEventElapsedTime");
+    d["compute_end_ms"] = ce;
+  }
+  d["buckets"] = bl;
+  return d;
+}
 
 RehearsalBucketComm::RehearsalBucketComm(std::shared_ptr<RcclComm> c, int world, int channels, int lds_bytes,
                                          double gbps_per_channel, double gbps_max, double latency_us)

@@ -1,4 +1,5 @@
 #pragma once
+#include <hip/hip_runtime_api.h>
 #include <torch/extension.h>
 
 #include <memory>
@@ -11,10 +12,13 @@ namespace dlmpi_ext {
 class RcclComm {
  public:
   static pybind11::bytes unique_id();
-  RcclComm(const std::string& uid, int rank, int size, int device);
+  // max_ctas > 0: this communicator's channel (workgroup) cap, through ncclCommInitRankConfig
+  // (maxCTAs) -- per communicator, unlike NCCL_MAX_NCHANNELS, which RCCL reads once per process
+  RcclComm(const std::string& uid, int rank, int size, int device, int max_ctas = 0);
   ~RcclComm();
   int rank() const;
   int size() const;
+  int max_ctas() const;
   int64_t stream_handle() const;
   void fence_in();
   void fence_out();
@@ -46,6 +50,7 @@ class RcclComm {
 class CommBase {
  public:
   virtual ~CommBase() = default;
+  virtual void begin_step() {}     // a synchronised step starts (Reducer::prepare_for_backward, DDP forward)
   virtual void begin_bucket() {}
   virtual void allreduce_bucket(at::Tensor t, bool average) = 0;
   virtual void end_backward() {}
@@ -54,6 +59,7 @@ class CommBase {
 class PyCommBase : public CommBase {
  public:
   using CommBase::CommBase;
+  void begin_step() override { PYBIND11_OVERRIDE(void, CommBase, begin_step, ); }
   void begin_bucket() override { PYBIND11_OVERRIDE(void, CommBase, begin_bucket, ); }
   void allreduce_bucket(at::Tensor t, bool average) override {
     PYBIND11_OVERRIDE_PURE(void, CommBase, allreduce_bucket, t, average);
@@ -64,12 +70,31 @@ class PyCommBase : public CommBase {
 class RcclBucketComm : public CommBase {
  public:
   explicit RcclBucketComm(std::shared_ptr<RcclComm> c) : comm_(std::move(c)) {}
+  ~RcclBucketComm() override;
+  void begin_step() override;
   void begin_bucket() override;
   void allreduce_bucket(at::Tensor t, bool average) override;
   void end_backward() override;
+  // Per-bucket timing (off by default; never inside a hipGraph capture): timing events at the step's
+  // start (begin_step: the DDP forward, compute stream), around every bucket all-reduce (comm stream)
+  // and at the end of the backward's compute (compute stream, before it waits for the comm stream).
+  void set_timing(bool on) { timing_ = on; }
+  // The last timed step (synchronises its events): per bucket {bytes, start_ms, dur_ms} with start_ms
+  // relative to the step's start, and compute_end_ms.
+  pybind11::dict timings();
 
  private:
+  hipEvent_t tev();
   std::shared_ptr<RcclComm> comm_;
+  bool timing_ = false;
+  std::vector<hipEvent_t> pool_;
+  size_t used_ = 0;
+  hipEvent_t ref_ = nullptr, cend_ = nullptr;
+  struct Rec {
+    int64_t bytes;
+    hipEvent_t a, b;
+  };
+  std::vector<Rec> recs_;
 };
 
 // One-GPU rehearsal of an N-rank all-reduce's cost to the compute streams (comm.cpp): the real

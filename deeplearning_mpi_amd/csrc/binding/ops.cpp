@@ -163,15 +163,23 @@ static int pipe_select(int f32, int pro, int cin, int64_t M, int Kout, int64_t r
 
 // ---- the producer's BN-apply fused into a 1x1 consumer (conv_igemm.hip conv1x1_apply_kernel) ----
 // pro-3 launches whose Kout is one 64 / 128 / 256-channel tile column run the register-staged kernel
-// (128-row tiles) instead of the single-stage pro-3 conv_igemm_kernel.  set_conv_apply(0): the latter.
+// (128-row tiles: 64-row tiles measured slower, profiles/r5_apply) instead of the single-stage pro-3
+// conv_igemm_kernel.  set_conv_apply(0): the latter.  Every other pro-3 launch -- and one whose
+// operands the register-staged kernel cannot address (apply_launch_ok) -- runs the single-stage kernel
+// on 128 x 64 tiles (kPro3Bm x kPro3Bn; the larger pro-3 tiles spilled and are not built), so both
+// paths produce ceil(M / 128) BN-statistics rows and the caller's buffer fits either.
 static int g_apply_override = -1;
+constexpr int kPro3Bm = 128, kPro3Bn = 64;
 static bool apply_kernel(int f32, int pro, int C, int K, int R, int S, int stride, int pad) {
   return g_apply_override != 0 && pro == 3 && !f32 && R == 1 && S == 1 && stride == 1 && pad == 0 &&
          dlmpi_conv1x1_apply_ok(C, K);
 }
-// 128-row tiles (64-row tiles for Kout 256, one block per CU by LDS: 134.5 vs 102.8 us at 14^2
-// 1024->256, profiles/r5_apply)
-static int apply_bm(int) { return 128; }
+// the launch-time conditions of dlmpi_conv1x1_apply beyond the shape: 16-byte output rows and 32-bit
+// element offsets of every operand
+static bool apply_launch_ok(const ConvArgs& a) {
+  const int64_t ld = std::max<int64_t>(a.ldx, std::max<int64_t>(a.ldpz, a.ldpy));
+  return a.vec_store && (int64_t)a.Nimg * a.H * a.W * ld < (1ll << 31);
+}
 
 // ---- 2-D halo tiles for 3x3 / stride-1 / pad-1 convolutions (conv_igemm.hip HALO) ----------------
 // set_conv_halo(0) (tests): these convolutions through the im2col gather path too.
@@ -638,8 +646,6 @@ static int conv2d_fwd_impl(const at::Tensor& x, int N, int H, int W, int C, int 
       const bool ok = !res.has_value() && !scale.has_value() && !relu && a.kvalid == K && ldx % 8 == 0 &&
                       xoff % 8 == 0 && ldy % 8 == 0 && yoff % 8 == 0 && (int64_t)N * H * W < (1ll << 31) &&
                       y.scalar_type() == at::kBFloat16;
-      if (a.stats && !ok)
-        throw std::runtime_error("conv2d_fwd: statistics were sized for the 8-channel 3x3 kernel, which cannot run");
       if (ok) {
         if (a.stats && stats->size(0) < G) throw std::runtime_error("conv2d_fwd: stats buffer too small");
         check(dlmpi_conv3x3_c8(a.x, ldx, xoff, N, H, W, a.w, a.bias, a.y, ldy, yoff, a.stats, G, cur_stream()),
@@ -669,8 +675,6 @@ static int conv2d_fwd_impl(const at::Tensor& x, int N, int H, int W, int C, int 
       const bool ok = !res.has_value() && !scale.has_value() && !relu && a.kvalid == K && a.vec_store &&
                       ldx % 8 == 0 && xoff % 8 == 0 && (int64_t)H * W * ldy * 2 < (1ll << 31) &&
                       y.scalar_type() == at::kBFloat16 && w.scalar_type() == at::kBFloat16;
-      if (a.stats && !ok)
-        throw std::runtime_error("conv2d_fwd: statistics were sized for the streaming 3x3 kernel, which cannot run");
       if (ok) {
         if (a.stats && stats->size(0) < G) throw std::runtime_error("conv2d_fwd: stats buffer too small");
         dlmpi::Conv3StreamArgs c = conv3_args(x, N, H, W, ldx, xoff, w, 0, a.y, ldy, yoff, th, tw, G);
@@ -696,8 +700,6 @@ static int conv2d_fwd_impl(const at::Tensor& x, int N, int H, int W, int C, int 
       const bool ok = !res.has_value() && !scale.has_value() && !relu && a.kvalid == K && a.vec_store &&
                       ldx % 8 == 0 && xoff % 8 == 0 && (int64_t)N * H * W * ldx < (1ll << 31) &&
                       M * ldy * 2 < (1ll << 31) && y.scalar_type() == at::kBFloat16;
-      if (a.stats && !ok)
-        throw std::runtime_error("conv2d_fwd: statistics were sized for the streaming 1x1 kernel, which cannot run");
       if (ok) {
         Stream1x1Args sa{};
         sa.x = ptr<uint16_t>(x);
@@ -730,10 +732,14 @@ static int conv2d_fwd_impl(const at::Tensor& x, int N, int H, int W, int C, int 
   }
   if (pro == 3 && (R != 1 || S != 1 || stride != 1 || pad != 0))
     throw std::runtime_error("conv prologue 3: a 1x1 / stride-1 conv");
-  const bool fused_apply = bm_req <= 0 && bn_req <= 0 && apply_kernel(a.f32, pro, C, K, R, S, stride, pad);
+  const bool fused_apply = bm_req <= 0 && bn_req <= 0 && apply_kernel(a.f32, pro, C, K, R, S, stride, pad) &&
+                           apply_launch_ok(a);
   if (fused_apply) {
-    bm = apply_bm(K);
+    bm = kPro3Bm;
     bn = K;
+  } else if (pro == 3) {
+    bm = kPro3Bm;
+    bn = kPro3Bn;
   }
   a.ntiles = ceil_div(K, bn);
   a.nphase = 1;
@@ -852,27 +858,34 @@ int conv2d_fwd_mtiles_pro(int N, int H, int W, int C, int K, int R, int S, int s
                           int f32) {
   const int P = (H + 2 * pad - R) / stride + 1, Q = (W + 2 * pad - S) / stride + 1;
   int bm, bn;
-  int G;
-  if (bm_req <= 0 && c8_shape((int64_t)N * H * W, C, K, R, S, stride, pad, W, pro, f32, G)) return G;
-  if (bm_req <= 0 && stream1x1_shape((int64_t)N * P * Q, C, K, R, S, stride, pad, pro, f32, bm, bn, G)) return G;
-  int th, tw;
-  if (bm_req <= 0 && stream3x3_shape(N, H, W, C, K, R, S, stride, pad, pro, f32, th, tw, G)) return G;
-  if (bm_req <= 0 && apply_kernel(f32, pro, C, K, R, S, stride, pad)) return ceil_div((int64_t)N * P * Q, apply_bm(K));
-  if (bm_req <= 0) {
-    int hbm, hbn;
-    pick_tiles((int64_t)N * P * Q, K, (int64_t)R * S * C, C, hbm, hbn, pro != 0);
-    if (f32) f32_tiles(hbm, hbn);
-    const bool halo_ok = halo_eligible(f32, pro, C, R, S, stride, pad, P, Q);
-    if (!halo_first(halo_ok, K) && pipe_select(f32, pro, C, (int64_t)N * P * Q, K, (int64_t)R * S * C, hbm, hbn))
-      return ceil_div((int64_t)N * P * Q, hbm);
-    if (halo_ok) return halo_mtiles(N, P, Q, K, hbn);
-  }
-  // autotuned launches may pick any M tile: size for the smallest (64 rows)
-  if (bm_req <= 0 && conv_autotune_on() && !f32 && pro == 0) return ceil_div((int64_t)N * P * Q, 64);
-  pick_tiles((int64_t)N * P * Q, K, (int64_t)R * S * C, C, bm, bn, pro != 0);
-  if (f32) f32_tiles(bm, bn);
-  if (bm_req > 0) bm = bm_req;
-  return ceil_div((int64_t)N * P * Q, bm);
+  if (pro == 3) return ceil_div((int64_t)N * P * Q, kPro3Bm);   // either pro-3 path (apply_kernel)
+  // The rows of the tiled (conv_igemm / pipe / halo) launch ...
+  const int general = [&]() -> int {
+    if (bm_req <= 0) {
+      int hbm, hbn;
+      pick_tiles((int64_t)N * P * Q, K, (int64_t)R * S * C, C, hbm, hbn, pro != 0);
+      if (f32) f32_tiles(hbm, hbn);
+      const bool halo_ok = halo_eligible(f32, pro, C, R, S, stride, pad, P, Q);
+      if (!halo_first(halo_ok, K) && pipe_select(f32, pro, C, (int64_t)N * P * Q, K, (int64_t)R * S * C, hbm, hbn))
+        return ceil_div((int64_t)N * P * Q, hbm);
+      if (halo_ok) return halo_mtiles(N, P, Q, K, hbn);
+    }
+    // autotuned launches may pick any M tile: size for the smallest (64 rows)
+    if (bm_req <= 0 && conv_autotune_on() && !f32 && pro == 0) return ceil_div((int64_t)N * P * Q, 64);
+    pick_tiles((int64_t)N * P * Q, K, (int64_t)R * S * C, C, bm, bn, pro != 0);
+    if (f32) f32_tiles(bm, bn);
+    if (bm_req > 0) bm = bm_req;
+    return ceil_div((int64_t)N * P * Q, bm);
+  }();
+  // ... and, where a persistent kernel is planned (one statistics row per block), the larger of the
+  // two: its launch conditions on strides / offsets / storage are checked at launch time, and when one
+  // fails the forward takes the tiled path into the same buffer
+  int G, th, tw;
+  if (bm_req <= 0 && c8_shape((int64_t)N * H * W, C, K, R, S, stride, pad, W, pro, f32, G)) return std::max(G, general);
+  if (bm_req <= 0 && stream1x1_shape((int64_t)N * P * Q, C, K, R, S, stride, pad, pro, f32, bm, bn, G))
+    return std::max(G, general);
+  if (bm_req <= 0 && stream3x3_shape(N, H, W, C, K, R, S, stride, pad, pro, f32, th, tw, G)) return std::max(G, general);
+  return general;
 }
 int conv2d_fwd_mtiles(int N, int H, int W, int C, int K, int R, int S, int stride, int pad, int bm_req) {
   return conv2d_fwd_mtiles_pro(N, H, W, C, K, R, S, stride, pad, bm_req, 0, 0);
@@ -1315,6 +1328,8 @@ void conv2d_wgrad_pro(const at::Tensor& dy, int lddy, int dyoff, int Ko, const a
   a.TC = R * S * C;
   a.npix = N * P * Q;
   a.direct = (R == 1 && S == 1 && stride == 1 && pad == 0 && P == H && Q == W) ? 1 : 0;
+  if (!dlmpi_wgrad_pro_ok(a.direct, pro_a, pro_b))
+    throw std::runtime_error("conv2d_wgrad: operand prologues: one of them, x's only for 1x1 gradients");
   const int bm = a.f32 || Ko <= 64 ? 64 : 128;   // fp32: conv_wgrad_f32_kernel's 64 x 64 tile
   a.mtiles = ceil_div(Ko, bm);
   // Ko <= 64 gather-form (3x3 / strided / stem) weight gradients: 64 x 256 tiles (1 x 4 waves of

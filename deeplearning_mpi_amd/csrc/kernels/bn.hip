@@ -846,7 +846,6 @@ extern "C" hipError_t dlmpi_maxpool_bwd_bn(const void* dy, const uint8_t* idx, i
                                            void* dx, float* partial, int nblk, int f32, hipStream_t s) {
   if (C % 8 || C > 2048 || (int64_t)N * H * W >= (1ll << 31)) return hipErrorInvalidValue;
   const int nw = (k + stride - 1) / stride;
-  constexpr bool generic = false;   // true: the dependent window loop (measured slower, kept generic)
 #define LAUNCH_MPB1(NW, T)                                                                                          \
   hipLaunchKernelGGL((maxpool_bwd_bn_kernel<NW, T>), dim3(nblk), dim3(256), 0, s, CT(dy), idx, N, H, W, C, k, stride, \
                      pad, OH, OW, make_fastdiv(W), make_fastdiv(H), CT(z), mscale, mshift, CT(add), ldadd, addoff,   \
@@ -861,8 +860,9 @@ extern "C" hipError_t dlmpi_maxpool_bwd_bn(const void* dy, const uint8_t* idx, i
       LAUNCH_MPB1(NW, T);       \
     }                          \
   } while (0)
-  if (!generic && nw == 1) LAUNCH_MPB(1);
-  else if (!generic && nw == 2) LAUNCH_MPB(2);
+  // fixed window extents for the 2x2/s2 and 3x3/s2 pools; NW 0: the general window loop
+  if (nw == 1) LAUNCH_MPB(1);
+  else if (nw == 2) LAUNCH_MPB(2);
   else LAUNCH_MPB(0);
 #undef LAUNCH_MPB
 #undef LAUNCH_MPB1

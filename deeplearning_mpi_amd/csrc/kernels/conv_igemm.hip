@@ -1043,11 +1043,16 @@ void conv1x1_apply_kernel(const ConvArgs a) {
 
 using namespace dlmpi;
 
+// The operand prologue (pro 3) is built for the 128 x 64 tile only (the host's kPro3Bm x kPro3Bn; the
+// 256 x 128 / 128 x 128 / 256 x 64 pro-3 instances spilled 40 / 17 / 0 VGPRs and 24 / 3 / 29 SGPRs).
 template <int BM, int BN>
-static void launch_tile(const ConvArgs* a, dim3 grid, hipStream_t s) {
-  if (a->pro == 3) hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, false, 2, 3>), grid, dim3(256), 0, s, *a);
-  else if (a->C < 64) hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, true, 2>), grid, dim3(256), 0, s, *a);
+static hipError_t launch_tile(const ConvArgs* a, dim3 grid, hipStream_t s) {
+  if (a->pro == 3) {
+    if constexpr (BM == 128 && BN == 64) hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, false, 2, 3>), grid, dim3(256), 0, s, *a);
+    else return hipErrorInvalidValue;
+  } else if (a->C < 64) hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, true, 2>), grid, dim3(256), 0, s, *a);
   else hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, false, 2>), grid, dim3(256), 0, s, *a);
+  return hipSuccess;
 }
 
 // Split-K plan for small grids (ResNet-18 on 32x32 CIFAR: layer4 is 1x1 pixels, 8 tiles x 72
@@ -1162,17 +1167,18 @@ extern "C" hipError_t dlmpi_conv_igemm_ex(const ConvArgs* a_in, int bm, int bn, 
     return hipGetLastError();
   }
   if (a->pro != 0 && (a->pro != 3 || a->C < 64 || a->C % 64 != 0)) return hipErrorInvalidValue;
+  hipError_t e = hipSuccess;
   if (bm == 256 && bn == 64) {   // 64-channel layers: 4 x 1 waves of 64 x 64
-    if (a->pro == 3) hipLaunchKernelGGL((conv_igemm_kernel<256, 64, false, 4, 3>), grid, dim3(256), 0, s, *a);
-    else if (a->C < 64) hipLaunchKernelGGL((conv_igemm_kernel<256, 64, true, 4>), grid, dim3(256), 0, s, *a);
+    if (a->pro == 3) return hipErrorInvalidValue;
+    if (a->C < 64) hipLaunchKernelGGL((conv_igemm_kernel<256, 64, true, 4>), grid, dim3(256), 0, s, *a);
     else hipLaunchKernelGGL((conv_igemm_kernel<256, 64, false, 4>), grid, dim3(256), 0, s, *a);
-  } else if (bm == 256 && bn == 128) launch_tile<256, 128>(a, grid, s);
-  else if (bm == 128 && bn == 128) launch_tile<128, 128>(a, grid, s);
-  else if (bm == 128 && bn == 64) launch_tile<128, 64>(a, grid, s);
-  else if (bm == 64 && bn == 128) launch_tile<64, 128>(a, grid, s);
-  else if (bm == 64 && bn == 64) launch_tile<64, 64>(a, grid, s);
+  } else if (bm == 256 && bn == 128) e = launch_tile<256, 128>(a, grid, s);
+  else if (bm == 128 && bn == 128) e = launch_tile<128, 128>(a, grid, s);
+  else if (bm == 128 && bn == 64) e = launch_tile<128, 64>(a, grid, s);
+  else if (bm == 64 && bn == 128) e = launch_tile<64, 128>(a, grid, s);
+  else if (bm == 64 && bn == 64) e = launch_tile<64, 64>(a, grid, s);
   else return hipErrorInvalidValue;
-  return hipGetLastError();
+  return e != hipSuccess ? e : hipGetLastError();
 }
 
 extern "C" hipError_t dlmpi_conv_igemm(const ConvArgs* a, int bm, int bn, hipStream_t s) {

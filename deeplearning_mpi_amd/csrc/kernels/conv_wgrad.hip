@@ -499,8 +499,12 @@ __global__ __launch_bounds__(256) void wgrad_reduce_batch_s2(const WgradReduceBa
 
 using namespace dlmpi;
 
+// Prologue combinations built: either operand deferred for 1x1 (direct) gradients -- the dual data
+// gradient's dz (PA 2), the UNet head's deferred BN-apply input (PB 1) --, the dy prologue for
+// gathers; not both at once.  (The gather PB 1 forms spilled 5 VGPRs at 128 x 128 and had no caller:
+// the backend stores such an operand first, ops/backend.py conv_wgrad.)
 template <int BM, int BN, int WR>
-static void launch_wg(const WgradArgs* a, dim3 g, hipStream_t s) {
+static hipError_t launch_wg(const WgradArgs* a, dim3 g, hipStream_t s) {
   const bool d = a->direct != 0;
   const int m = (a->pro_a ? 2 : 0) | (a->pro_b ? 1 : 0);
 #define WG(D_, PA_, PB_) hipLaunchKernelGGL((conv_wgrad_kernel<BM, BN, D_, PA_, PB_, WR>), g, dim3(256), 0, s, *a)
@@ -508,14 +512,18 @@ static void launch_wg(const WgradArgs* a, dim3 g, hipStream_t s) {
     if (m == 0) WG(true, 0, 0);
     else if (m == 2) WG(true, 2, 0);
     else if (m == 1) WG(true, 0, 1);
-    else WG(true, 2, 1);
+    else return hipErrorInvalidValue;
   } else {
     if (m == 0) WG(false, 0, 0);
     else if (m == 2) WG(false, 2, 0);
-    else if (m == 1) WG(false, 0, 1);
-    else WG(false, 2, 1);
+    else return hipErrorInvalidValue;
   }
 #undef WG
+  return hipGetLastError();
+}
+// the prologue combination launch_wg builds for this gradient
+extern "C" int dlmpi_wgrad_pro_ok(int direct, int pro_a, int pro_b) {
+  return !(pro_a && pro_b) && (direct || !pro_b);
 }
 
 extern "C" hipError_t dlmpi_conv_wgrad(const WgradArgs* a, int bm, int bn, hipStream_t s) {
@@ -532,14 +540,12 @@ extern "C" hipError_t dlmpi_conv_wgrad(const WgradArgs* a, int bm, int bn, hipSt
   // 64 x 256, 1 x 4 waves (Ko <= 64 layers)
   if (bm == 64 && bn == 256) {
     if (a->pro_b != 0) return hipErrorInvalidValue;
-    launch_wg<64, 256, 1>(a, g, s);
-    return hipGetLastError();
+    return launch_wg<64, 256, 1>(a, g, s);
   }
   // (a 128 x 256 variant was measured 1.3-1.9x slower: 2 waves/SIMD and register spills)
   if (bn != 128 || (bm != 128 && bm != 64)) return hipErrorInvalidValue;
-  if (bm == 128) launch_wg<128, 128, 2>(a, g, s);
-  else launch_wg<64, 128, 2>(a, g, s);
-  return hipGetLastError();
+  if (bm == 128) return launch_wg<128, 128, 2>(a, g, s);
+  return launch_wg<64, 128, 2>(a, g, s);
 }
 
 extern "C" int dlmpi_wgrad_reduce_groups(int splits, int64_t total) { return reduce_groups(splits, total); }

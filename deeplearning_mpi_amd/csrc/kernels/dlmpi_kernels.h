@@ -267,6 +267,8 @@ hipError_t dlmpi_conv_igemm_ex(const dlmpi::ConvArgs* a, int bm, int bn, int pip
 int dlmpi_conv1x1_apply_ok(int C, int K);
 hipError_t dlmpi_conv1x1_apply(const dlmpi::ConvArgs* a, int bm, hipStream_t s);
 hipError_t dlmpi_conv_wgrad(const dlmpi::WgradArgs* a, int bm, int bn, hipStream_t s);   // bn: 128 | 256
+// 1 if dlmpi_conv_wgrad has the operand-prologue combination (pro_a 2 / pro_b 1) for this gradient
+int dlmpi_wgrad_pro_ok(int direct, int pro_a, int pro_b);
 // sum of split partials -> grad (accumulated), with channel un-padding and row limit
 hipError_t dlmpi_wgrad_reduce(const float* ws, int splits, int Ko, int T, int Cpad, int Creal,
                               int Ko_real, float* out, float* ws2, int ws2_floats, hipStream_t s);

@@ -14,8 +14,11 @@ __global__ __launch_bounds__(256) void sgd_kernel(float* __restrict__ p, const f
                                                   float dampening, float wd, int nesterov, int first,
                                                   const float* __restrict__ skip_flag) {
   if (skip_flag && *skip_flag != 0.f) return;
-  const int64_t n4 = n >> 2;
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x) {
+  // 16-byte accesses when every buffer allows them (the arena's do), else the element loop below
+  const bool vec = (((uintptr_t)p | (uintptr_t)g | (uintptr_t)m) & 15) == 0;
+  const int64_t n4 = vec ? n >> 2 : 0;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n4; i += stride) {
     f32x4 pv = reinterpret_cast<f32x4*>(p)[i];
     f32x4 gv = reinterpret_cast<const f32x4*>(g)[i];
     if (wd != 0.f) gv += wd * pv;
@@ -26,9 +29,8 @@ __global__ __launch_bounds__(256) void sgd_kernel(float* __restrict__ p, const f
     }
     reinterpret_cast<f32x4*>(p)[i] = pv - lr * gv;
   }
-  // tail
-  const int64_t t = (n4 << 2) + blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-  if (blockIdx.x == 0 && t < n) {
+  // tail (or everything, unaligned)
+  for (int64_t t = (n4 << 2) + blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < n; t += stride) {
     float pv = p[t], gv = g[t];
     if (wd != 0.f) gv += wd * pv;
     if (momentum != 0.f) {

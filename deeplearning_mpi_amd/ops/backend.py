@@ -250,6 +250,9 @@ class NativeBackend:
         self.C.set_wgrad_bypass(bool(on))
 
     def conv_wgrad(self, dy, x, R, S, stride, pad, grad, Creal, Ko_real):
+        direct = R == 1 and S == 1 and stride == 1 and pad == 0
+        if isinstance(dy, Deferred) and isinstance(x, Deferred) or (isinstance(x, Deferred) and not direct):
+            x = self.materialize(x)   # (prologue combinations the kernel is not built for: dlmpi_wgrad_pro_ok)
         dy, pa, ca, _, zb, zld, zoff = self._pro(dy)
         x, pb, sb, hb, _, _, _ = self._pro(x)
         assert pa in (0, 2) and pb in (0, 1)

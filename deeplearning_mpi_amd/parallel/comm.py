@@ -15,6 +15,7 @@ from __future__ import annotations
 
 import datetime
 import os
+import weakref
 
 import torch
 import torch.distributed as dist
@@ -113,8 +114,10 @@ class RcclCommunicator(Communicator):
         # the CUs this communicator's channels take are withheld from the persistent streaming
         # data-gradient grid for as long as it exists (rccl_channel_budget)
         self.budget = budget if budget is not None else rccl_channel_budget()
-        _LIVE_RCCL.append(self)
+        _LIVE_RCCL.add(self)
         _apply_dgs_budget()
+        # a communicator dropped without destroy() releases its CUs when it is collected
+        weakref.finalize(self, _apply_dgs_budget)
 
     def allreduce(self, t, op="sum"):
         self.c.allreduce(t, op, False)
@@ -160,16 +163,16 @@ class RcclCommunicator(Communicator):
     def destroy(self):
         self.c.destroy()
         self.control = None
-        if self in _LIVE_RCCL:
-            _LIVE_RCCL.remove(self)
+        _LIVE_RCCL.discard(self)
         _apply_dgs_budget()
 
 
 # RCCL communicators alive in this process (bench --rccl1 builds one beside init_distributed's).  The
 # streaming data-gradient grid leaves room for the channels of every one of them: the smallest grid of
 # the live budgets, the default (0) once none is left -- destroying one communicator must not hand the
-# other's channels' CUs back to the persistent grid.
-_LIVE_RCCL = []
+# other's channels' CUs back to the persistent grid.  Weak: one dropped without destroy()
+# leaves the set when it is collected, and its finalizer recomputes the grid.
+_LIVE_RCCL = weakref.WeakSet()
 
 
 def _apply_dgs_budget():
@@ -393,7 +396,99 @@ def _init(backend: str, timeout_s: float) -> Communicator:
     else:
         uid, store = uid_via_store(info, C.RcclComm.unique_id, timeout_s)
     nc = C.RcclComm(uid, info.rank, info.world_size, device.index)
+    if budget.get("mode") == "auto":
+        # DLMPI_RCCL_CHANNELS=auto: the uncapped communicator only carries the calibration; the job's
+        # communicator gets the chosen channel cap (calibrate_channels)
+        cal = calibrate_channels(nc, info.rank, info.world_size, device)
+        if cal["chosen"] > 0:
+            fin = C.RcclComm(subcomm_uid(nc, info.rank, device), info.rank, info.world_size, device.index,
+                             cal["chosen"])
+            nc.destroy()
+            nc = fin
+        budget = dict(budget, dgrad_stream_blocks=int(os.environ.get("DLMPI_DGS_BLOCKS") or
+                                                      max(64, 256 - (cal["chosen"] or 32))),
+                      calibration=cal)
     return RcclCommunicator(info, device, nc, control_group=store, budget=budget)
+
+
+def subcomm_uid(nc, rank, device) -> bytes:
+    """A fresh RCCL unique id, made by rank 0 and broadcast over the live native communicator ``nc``
+    (for a second communicator over the same ranks, e.g. with another channel cap)."""
+    from .._ext import native
+
+    C = native()
+    raw = C.RcclComm.unique_id() if rank == 0 else bytes(128)
+    t = torch.tensor(list(raw), dtype=torch.uint8, device=device)
+    nc.broadcast(t, 0, False)
+    return bytes(t.cpu().tolist())
+
+
+def time_allreduce(nc, nbytes, device, iters=10, warmup=3, op="allreduce"):
+    """Median time (s) of one ``op`` (allreduce / broadcast) of ``nbytes`` fp32 bytes on the native
+    communicator ``nc``, bracketed by HIP events on the caller's stream (the collective's fences in and
+    out), max over ranks."""
+    t = torch.ones(max(1, nbytes // 4), dtype=torch.float32, device=device)
+    fn = (lambda: nc.allreduce(t, "sum", False)) if op == "allreduce" else (lambda: nc.broadcast(t, 0, False))
+    for _ in range(warmup):
+        fn()
+    times = []
+    for _ in range(iters):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        fn()
+        b.record()
+        b.synchronize()
+        times.append(a.elapsed_time(b) / 1e3)
+    times.sort()
+    med = torch.tensor([times[len(times) // 2]], dtype=torch.float64, device=device)
+    nc.allreduce(med, "max", False)
+    return float(med.item())
+
+
+def bus_gbps(op, nbytes, seconds, world):
+    """Bus bandwidth (GB/s, nccl-tests convention): all-reduce moves 2 (n-1)/n of the buffer per rank,
+    broadcast the buffer once."""
+    if seconds <= 0:
+        return 0.0
+    alg = nbytes / seconds / 1e9
+    return alg * (2.0 * (world - 1) / world if op == "allreduce" else 1.0)
+
+
+# candidate channel caps of DLMPI_RCCL_CHANNELS=auto, and the all-reduce size it calibrates at (the
+# largest bucket cap, parallel/ddp.py)
+AUTO_CAPS = (8, 16, 32)
+AUTO_BYTES = 32 << 20
+AUTO_FRACTION = 0.9
+
+
+def calibrate_channels(nc, rank, world, device, caps=AUTO_CAPS, nbytes=AUTO_BYTES, iters=10) -> dict:
+    """Measure all-reduce bus bandwidth of an ``nbytes`` buffer with each channel cap in ``caps`` (one
+    temporary communicator each, ids broadcast over ``nc``) and with RCCL's own choice (``nc``), and
+    pick the SMALLEST cap reaching AUTO_FRACTION of the best: each channel is a CU taken from the
+    backward's compute while a bucket is in flight (profiles/r4_commload), so the fewest channels that
+    carry the bucket at ~full bus bandwidth.  World size 1 has no bus: 0 (RCCL's choice) is kept."""
+    from .._ext import native
+
+    C = native()
+    rows = [{"max_ctas": 0, "busbw_gbps": round(bus_gbps("allreduce", nbytes,
+                                                           time_allreduce(nc, nbytes, device, iters), world), 1)}]
+    for cap in caps:
+        sub = C.RcclComm(subcomm_uid(nc, rank, device), rank, world, device.index, int(cap))
+        rows.append({"max_ctas": int(cap),
+                     "busbw_gbps": round(bus_gbps("allreduce", nbytes, time_allreduce(sub, nbytes, device, iters),
+                                                  world), 1)})
+        sub.destroy()
+    return {"bytes": nbytes, "rows": rows, "chosen": choose_cap(rows, world)}
+
+
+def choose_cap(rows, world, fraction=AUTO_FRACTION) -> int:
+    """The smallest positive cap whose bus bandwidth is >= ``fraction`` of the best row's (0 = RCCL's
+    own choice: world size 1, nothing measured, or no capped row good enough)."""
+    best = max((r["busbw_gbps"] for r in rows), default=0.0)
+    if world < 2 or best <= 0:
+        return 0
+    ok = [r["max_ctas"] for r in rows if r["max_ctas"] > 0 and r["busbw_gbps"] >= fraction * best]
+    return min(ok) if ok else 0
 
 
 # Measured by the one-GPU comm-load rehearsal (bench.py --rehearse, profiles/r4_commload): with a
@@ -412,7 +507,9 @@ def rccl_channel_budget() -> dict:
     channel count is a CU budget: ``DLMPI_RCCL_CHANNELS`` (default 16 = 1/16 of the 256 CUs; 0 =
     leave RCCL its own choice) is exported as ``NCCL_MAX_NCHANNELS`` before the communicator is
     created (RCCL reads it at ``ncclCommInitRank``).  An explicit ``NCCL_MAX_NCHANNELS`` in the
-    environment wins.  The default (16) is the measured choice of the one-GPU comm-load rehearsal
+    environment wins.  ``auto``: no process-wide cap; the communicator's own cap (maxCTAs) is the
+    smallest of AUTO_CAPS that measures >= 90 % of the best all-reduce bus bandwidth at init
+    (calibrate_channels).  The default (16) is the measured choice of the one-GPU comm-load rehearsal
     (``bench.py --rehearse``, profiles/r4_commload; see DEFAULT_RCCL_CHANNELS).
 
     The persistent streaming data-gradient kernel (conv1x1_dgrad_stream.hip) splits its work
@@ -423,7 +520,12 @@ def rccl_channel_budget() -> dict:
     channel ceiling on this node size).  The communicator applies it natively for its lifetime
     (``RcclCommunicator``), so a later communicator with another budget takes effect.  Returns the
     effective settings (bench.py reports them)."""
-    want = int(os.environ.get("DLMPI_RCCL_CHANNELS", str(DEFAULT_RCCL_CHANNELS)) or 0)
+    raw = os.environ.get("DLMPI_RCCL_CHANNELS", str(DEFAULT_RCCL_CHANNELS)).strip().lower()
+    if raw == "auto" and "NCCL_MAX_NCHANNELS" not in os.environ:
+        # per-communicator caps (ncclCommInitRankConfig maxCTAs) chosen by calibrate_channels at init
+        return {"NCCL_MAX_NCHANNELS": None, "NCCL_MIN_NCHANNELS": os.environ.get("NCCL_MIN_NCHANNELS"),
+                "dgrad_stream_blocks": int(os.environ.get("DLMPI_DGS_BLOCKS") or 256 - 32), "mode": "auto"}
+    want = 0 if raw == "auto" else int(raw or 0)
     if want > 0 and "NCCL_MAX_NCHANNELS" not in os.environ:
         os.environ["NCCL_MAX_NCHANNELS"] = str(want)
     env = os.environ.get("NCCL_MAX_NCHANNELS")

@@ -47,6 +47,8 @@ def test_bench_self_launches_n_ranks(launcher):
     assert d["reducer"] and len(d["bucket_mb"]) >= 1 and d["comm_exposed_ms"] is not None
     assert 0 < d["per_rank_ms_per_step"]["min"] <= d["per_rank_ms_per_step"]["max"]
     assert d["per_rank_ms_per_step"]["max"] == pytest.approx(j["ms_per_step"], rel=1e-3, abs=1e-3)
+    # the RCCL-only instruments are reported (empty on gloo): per-bucket comm-stream timing, channel calibration
+    assert "bucket_probe" in d and "rccl_channel_calibration" in d
 
 
 def test_bench_single_rank_unchanged():

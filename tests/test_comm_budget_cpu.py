@@ -63,3 +63,29 @@ def test_destroying_one_communicator_keeps_the_other_ones_budget(monkeypatch):
     assert C.dgs_blocks() == 240
     a.destroy()
     assert C.dgs_blocks() == 256   # none left: the default grid
+
+
+def test_dropped_communicator_releases_its_budget(monkeypatch):
+    """a communicator dropped without destroy() must not hold its CUs for the rest of the
+    process -- the live set is weak and collection recomputes the grid."""
+    import gc
+
+    _clean(monkeypatch)
+    from deeplearning_mpi_amd._ext import native
+    from deeplearning_mpi_amd.parallel.bootstrap import LaunchInfo
+    from deeplearning_mpi_amd.parallel.comm import RcclCommunicator
+
+    class FakeNative:
+        def destroy(self):
+            pass
+
+    info = LaunchInfo("single", 0, 1, 0, 1)
+    C = native()
+    gc.collect()
+    C.set_dgs_blocks(0)
+    default = C.dgs_blocks()   # the grid with no communicator alive
+    a = RcclCommunicator(info, "cpu", FakeNative(), budget={"dgrad_stream_blocks": 232})
+    assert C.dgs_blocks() == 232
+    del a
+    gc.collect()
+    assert C.dgs_blocks() == default

@@ -37,7 +37,7 @@ def test_conv3x3_c8_matches_fp32(N, H, W, cin, on):
     try:
         used = be.conv_fwd(Act(xb, N, H, W, 8), wb, 64, 3, 3, 1, 1, Act(y, N, H, W, 64), bias=bias, stats=stats)
         torch.cuda.synchronize()
-        assert be.C.conv_c8_last() == on and used == rows
+        assert be.C.conv_c8_last() == on and used <= rows   # rows: capacity for either path
     finally:
         be.C.set_conv_c8(1)
     xt = xb.float().view(N, H, W, 8).permute(0, 3, 1, 2)

@@ -37,8 +37,11 @@ SHAPES = [
 ]
 
 
+@pytest.mark.parametrize("apply_kernel", [True, False], ids=["regstaged", "single_stage"])
 @pytest.mark.parametrize("shape", SHAPES, ids=lambda s: "x".join(str(v) for v in s))
-def test_conv_fwd_bn_apply_matches_unfused(shape):
+def test_conv_fwd_bn_apply_matches_unfused(shape, apply_kernel):
+    """apply_kernel False: set_conv_apply(0), the single-stage pro-3 kernel on its 128 x 64 tiles (the
+    fallback when the register-staged kernel cannot run) -- same statistics row count, same results."""
     from deeplearning_mpi_amd.ops.backend import NativeBackend
 
     N, H, W, C, K, bnres = shape
@@ -58,6 +61,7 @@ def test_conv_fwd_bn_apply_matches_unfused(shape):
     # sums its K in the same order in both schedules
     be.C.set_conv_pipe(0)
     be.C.set_conv_splitk(1)
+    be.C.set_conv_apply(-1 if apply_kernel else 0)
     for fused in (True, False):
         y = Act.empty(N, H, W, C, torch.bfloat16, DEV)
         y.buf.fill_(7.0)
@@ -77,6 +81,7 @@ def test_conv_fwd_bn_apply_matches_unfused(shape):
         out[fused] = (y.buf.clone(), mb.clone(), z.buf.clone(), st.double().sum(0), v.clone(), rm.clone(), rv.clone())
     be.C.set_conv_pipe(-1)
     be.C.set_conv_splitk(0)
+    be.C.set_conv_apply(-1)
     a, b = out[True], out[False]
     assert torch.equal(a[0], b[0])          # the stored apply output
     assert torch.equal(a[1], b[1])          # its ReLU mask bits

@@ -372,7 +372,7 @@ def test_conv3x3_halo_tiles(shape):
         mt = nb.conv_mtiles(N, H, W, Cin, K, 3, 3, 1, 1)
         st = torch.zeros(mt, 2, K, device=DEV)
         rows = nb.conv_fwd(x, w, K, 3, 3, 1, 1, y, stats=st)
-        assert rows == mt and nb.C.conv_halo_last() == (mode == 2)
+        assert rows <= mt and nb.C.conv_halo_last() == (mode == 2)
         dx = _empty(N, H, W, Cin)
         part = nb.conv_dgrad(dy, wT, Cin, 3, 3, 1, 1, dx, fuse=BwdFuse(None, z, None, sc, sh))
         assert nb.C.conv_halo_last() == (mode == 2)
@@ -427,7 +427,7 @@ def test_conv3x3_stream_64(shape):
         mt = nb.conv_mtiles(N, H, W, C, K, 3, 3, 1, 1)
         st = torch.zeros(mt, 2, K, device=DEV)
         rows = nb.conv_fwd(x, w, K, 3, 3, 1, 1, y, bias=bias, stats=st)
-        assert rows == mt and nb.C.conv3_stream_last() == mode
+        assert rows <= mt and nb.C.conv3_stream_last() == mode
         dx = _empty(N, H, W, C)
         part = nb.conv_dgrad(dy, wT, C, 3, 3, 1, 1, dx, fuse=BwdFuse(None, z, None, sc, sh))
         assert nb.C.conv3_stream_last() == mode
