@@ -389,7 +389,11 @@ def main():
         step()
         sync()
         bc.set_timing(False)
-        tm_ = bc.timings()
+        try:
+            tm_ = bc.timings()
+        except RuntimeError as e:   # an instrument: never fail the benchmark over it
+            print(f"[bench] bucket probe failed: {e}", file=sys.stderr, flush=True)
+            tm_ = {"buckets": []}
         bl = tm_["buckets"]
         if bl and "compute_end_ms" in tm_:
             v = torch.tensor([b["dur_ms"] for b in bl] + [b["start_ms"] + b["dur_ms"] for b in bl] +
