@@ -395,7 +395,14 @@ def main():
             print(f"[bench] bucket probe failed: {e}", file=sys.stderr, flush=True)
             tm_ = {"buckets": []}
         bl = tm_["buckets"]
-        if bl and "compute_end_ms" in tm_:
+        # every rank takes part in both collectives below or in neither (a rank-local failure must not
+        # leave the others waiting in an all-reduce)
+        ok = torch.tensor([1.0 if (bl and "compute_end_ms" in tm_) else 0.0, float(len(bl))], device=dev)
+        okmin = ok.clone()
+        comm.allreduce(okmin, "min")
+        okmax = ok.clone()
+        comm.allreduce(okmax, "max")
+        if okmin[0] > 0 and okmin[1] == okmax[1]:
             v = torch.tensor([b["dur_ms"] for b in bl] + [b["start_ms"] + b["dur_ms"] for b in bl] +
                              [tm_["compute_end_ms"]], dtype=torch.float64, device=dev)
             comm.allreduce(v, "max")   # every rank's slowest: the collective ends on the last rank
