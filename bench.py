@@ -141,6 +141,9 @@ def main():
                     help="RCCL channel (CU) cap: N, 0 (RCCL's choice) or auto (calibrated at init: the smallest cap "
                          "of 8/16/32 reaching 90 %% of the best all-reduce bus bandwidth, parallel/comm.py "
                          "calibrate_channels); default DLMPI_RCCL_CHANNELS or 16")
+    ap.add_argument("--precision", default="bf16", choices=["bf16", "fp32"],
+                    help="compute precision of the native engine: bf16 (default, the BASELINE dtype) or fp32 "
+                         "(the same kernels on fp32 storage -- how the reference trains ResNet-18 on CIFAR)")
     ap.add_argument("--bucket_probe", type=int, default=1,
                     help="1 (default): with an RCCL reducer (N > 1 or --rccl1) and no hipGraph, one untimed step "
                          "after the timed region times every bucket all-reduce on the comm stream (dist.buckets)")
@@ -210,6 +213,7 @@ def main():
         crit = BCEWithLogitsLoss()
         x, y = device_batch("segmentation", cfg["batch"], dev, shape, seed=1234 + comm.rank)
         optname = "Adam(lr=1e-4) + clip_grad_norm(1.0)"
+    model.precision = args.precision   # (read at the engine's first use, below)
     if args.rccl1:
         if world != 1:
             print("[bench] --rccl1 is a single-GPU option", file=sys.stderr, flush=True)

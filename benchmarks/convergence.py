@@ -8,9 +8,14 @@ A learnable synthetic task stands in for the datasets (no downloads here):
   * segmentation -- binary masks of random discs over noisy images; the reference UNet with Adam +
     BCEWithLogits + clip_grad_norm_(1.0) (/root/reference/pytorch/unet/train.py:160-194).
 Prints one JSON line per run with the loss every `--log_every` steps and the held-out accuracy /
-Dice at the end, for both implementations.
+Dice at the end, for every implementation of ``--impls``: native (the engine), autocast (stock
+PyTorch, torch.autocast bf16, channels_last -- the same compute precision) and fp32 (stock PyTorch
+fp32); ``--torch_seeds`` repeats the autocast run with other seeds (other initial weights and data
+stream) to show the SGD noise the native-vs-autocast gap is to be read against.
 
-python benchmarks/convergence.py [--task cls|seg] [--steps 300] [--batch 128]
+python benchmarks/convergence.py [--task cls|seg] [--arch resnet18|resnet50] [--size 32] [--steps 300]
+       [--batch 128] [--impls native,autocast,fp32] [--torch_seeds 1]
+Bench shapes (round 6): --task cls --arch resnet50 --size 224 --batch 256; --task seg --size 512 --batch 16.
 """
 import argparse
 import json
@@ -39,17 +44,21 @@ def seg_data(n, size, g, dev):
     return x, m
 
 
-def run(args, native):
-    from deeplearning_mpi_amd.models import UNet, resnet18
+def run(args, impl, seed):
+    from deeplearning_mpi_amd.models import ARCHS, UNet
     from deeplearning_mpi_amd.ops import BCEWithLogitsLoss, CrossEntropyLoss, dice_per_sample
     from deeplearning_mpi_amd.optim import SGD, Adam, clip_grad_norm_
 
+    native = impl == "native"
+    amp = impl == "autocast"
     dev = torch.device("cuda")
-    torch.manual_seed(args.seed)
+    torch.manual_seed(seed)
     if args.task == "cls":
-        model = resnet18(num_classes=10).to(dev)
+        model = ARCHS[args.arch](num_classes=10).to(dev)
     else:
         model = UNet(out_classes=1).to(dev)
+    if not native:
+        model = model.to(memory_format=torch.channels_last)
     if native:
         fwd = model
         if args.task == "cls":
@@ -66,18 +75,34 @@ def run(args, native):
         else:
             opt = torch.optim.Adam(model.parameters(), lr=args.lr)
             crit = torch.nn.BCEWithLogitsLoss()
-    g = torch.Generator(device=dev).manual_seed(1000 + args.seed)
-    templates = torch.randn(10, 3, 32, 32, generator=g, device=dev) if args.task == "cls" else None
+    g = torch.Generator(device=dev).manual_seed(1000 + seed)
+    # the task (class templates) is fixed by --seed; the seed of the run moves init and data order
+    gt = torch.Generator(device=dev).manual_seed(1000 + args.seed)
+    templates = torch.randn(10, 3, args.size, args.size, generator=gt, device=dev) if args.task == "cls" else None
+
+    def fwd_(x):
+        if native:
+            return fwd(x)
+        x = x.to(memory_format=torch.channels_last)
+        if amp:
+            with torch.autocast("cuda", dtype=torch.bfloat16):
+                return fwd(x).float()
+        return fwd(x)
     losses = []
     model.train()
     t0 = time.perf_counter()
+    base_lr = args.lr
     for step in range(args.steps):
+        if args.warmup_steps:   # linear learning-rate warm-up (both implementations alike)
+            for grp in opt.param_groups:
+                grp["lr"] = base_lr * min(1.0, (step + 1) / args.warmup_steps)
+        _STATE["where"] = f"{impl} seed {seed} step {step}"
         if args.task == "cls":
             x, y = cls_data(args.batch, g, templates, args.noise)
         else:
             x, y = seg_data(args.batch, args.size, g, dev)
         opt.zero_grad()
-        out = fwd(x)
+        out = fwd_(x)
         loss = crit(out, y) if args.task == "cls" else crit(out.squeeze(1), y)
         loss.backward()
         if args.task == "seg":
@@ -88,29 +113,52 @@ def run(args, native):
         opt.step()
         if step % args.log_every == 0 or step == args.steps - 1:
             losses.append((step, round(float(loss.detach()), 5)))
+            print(f"[convergence] {impl} seed {seed} step {step} loss {losses[-1][1]}", file=sys.stderr, flush=True)
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     model.eval()
     ge = torch.Generator(device=dev).manual_seed(777)
     with torch.no_grad():
         if args.task == "cls":
-            x, y = cls_data(1024, ge, templates, args.noise)
-            out = fwd(x)
-            metric = ("accuracy", (out.argmax(1) == y).float().mean().item())
+            hits = 0
+            for _ in range(4):   # 1,024 held-out samples in 4 batches
+                x, y = cls_data(256, ge, templates, args.noise)
+                hits += (fwd_(x).argmax(1) == y).sum().item()
+            metric = ("accuracy", hits / 1024)
         else:
             x, y = seg_data(16, args.size, ge, dev)
-            out = fwd(x)
+            out = fwd_(x)
             metric = ("dice", dice_per_sample(out.float(), y).mean().item())
-    return {"impl": "native-bf16" if native else "torch-fp32", "task": args.task, "steps": args.steps,
-            "batch": args.batch, "loss": losses, metric[0]: round(metric[1], 4), "seconds": round(dt, 1)}
+    name = {"native": "native-bf16", "autocast": "torch-autocast-bf16", "fp32": "torch-fp32"}[impl]
+    return {"impl": name, "seed": seed, "task": args.task, "arch": args.arch if args.task == "cls" else "unet",
+            "size": args.size, "steps": args.steps, "batch": args.batch, "lr": args.lr, "loss": losses,
+            metric[0]: round(metric[1], 4), "seconds": round(dt, 1)}
+
+
+_STATE = {"where": "start"}
+
+
+def _heartbeat():
+    # stock PyTorch's first convolutions search MIOpen algorithms for minutes: a line every 30 s keeps a
+    # silence watchdog from taking that for a hang
+    while True:
+        time.sleep(30)
+        print(f"[convergence] alive: {_STATE['where']}", file=sys.stderr, flush=True)
 
 
 def main():
+    import threading
+
+    threading.Thread(target=_heartbeat, daemon=True).start()
     ap = argparse.ArgumentParser()
     ap.add_argument("--task", default="cls", choices=["cls", "seg"])
+    ap.add_argument("--arch", default="resnet18", help="classification model (resnet18 / resnet50 / ...)")
+    ap.add_argument("--impls", default="native,fp32", help="native / autocast / fp32, comma-separated")
+    ap.add_argument("--torch_seeds", type=int, default=0, help="extra autocast runs with seeds seed+1 ..")
+    ap.add_argument("--warmup_steps", type=int, default=0, help="linear learning-rate warm-up steps")
     ap.add_argument("--steps", type=int, default=300)
     ap.add_argument("--batch", type=int, default=None)
-    ap.add_argument("--size", type=int, default=64)
+    ap.add_argument("--size", type=int, default=None, help="image size (default 32 cls / 64 seg)")
     ap.add_argument("--lr", type=float, default=None)
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--log_every", type=int, default=25)
@@ -120,8 +168,12 @@ def main():
         args.batch = 128 if args.task == "cls" else 8
     if args.lr is None:
         args.lr = 0.05 if args.task == "cls" else 1e-3
-    for native in (True, False):
-        print(json.dumps(run(args, native)), flush=True)
+    if args.size is None:
+        args.size = 32 if args.task == "cls" else 64
+    for impl in args.impls.split(","):
+        print(json.dumps(run(args, impl, args.seed)), flush=True)
+    for k in range(1, args.torch_seeds + 1):
+        print(json.dumps(run(args, "autocast", args.seed + k)), flush=True)
 
 
 if __name__ == "__main__":

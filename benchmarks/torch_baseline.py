@@ -26,6 +26,9 @@ def main():
     ap.add_argument("--config", default="resnet50", choices=sorted(PRESETS))
     ap.add_argument("--batch", type=int, default=None)
     ap.add_argument("--no_channels_last", action="store_true")
+    ap.add_argument("--precision", default="bf16", choices=["bf16", "fp32"],
+                    help="bf16: torch.autocast (default); fp32: plain fp32, as the reference trains "
+                         "(/root/reference/pytorch/resnet/main.py:123-132, no autocast)")
     args = ap.parse_args()
     cfg = dict(PRESETS[args.config])
     if args.batch:
@@ -82,7 +85,7 @@ def main():
 
     def step():
         opt.zero_grad()
-        with torch.autocast("cuda", dtype=torch.bfloat16):
+        with torch.autocast("cuda", dtype=torch.bfloat16, enabled=args.precision == "bf16"):
             out = net(x)
         if seg:
             loss = F.binary_cross_entropy_with_logits(out.float().squeeze(1), y)
@@ -109,10 +112,12 @@ def main():
         dist.barrier()
     dt = time.perf_counter() - t0
     if rank == 0:
-        print(json.dumps({"metric": "stock PyTorch DDP (MIOpen, autocast bf16, channels_last): " + cfg["metric"],
+        mode = "autocast bf16" if args.precision == "bf16" else "fp32"
+        print(json.dumps({"metric": f"stock PyTorch DDP (MIOpen, {mode}, channels_last): " + cfg["metric"],
                           "value": round(B * world * args.steps / dt, 2), "n_gpus": world,
                           "ms_per_step": round(dt / args.steps * 1000, 3), "config": args.config,
-                          "per_gpu_batch": B, "loss": round(float(loss.item()), 4)}), flush=True)
+                          "per_gpu_batch": B, "precision": args.precision,
+                          "loss": round(float(loss.item()), 4)}), flush=True)
     if world > 1:
         dist.destroy_process_group()
 

@@ -164,3 +164,50 @@ def test_resnet50_bench_scale_training_matches_stock_pytorch():
     # streaming 1x1 / halo / pipelined kernels each switched off at 5.754 / 5.705 / 5.686, torch 5.738;
     # all of them within 1 % of torch over the first 8 steps)
     assert ((lo - lr_).abs() / lr_).max() < 0.08
+
+
+def test_unet512_bench_scale_training_matches_stock_pytorch():
+    """10 steps of the UNet-512 benchmark configuration (bs 16, 3 x 512 x 512, Adam 1e-4 + BCE +
+    clip_grad_norm 1.0, /root/reference/pytorch/unet/train.py:160-196) on one fixed batch: the native
+    engine -- every round-5/6 UNet kernel in the loop: the 8-channel input conv, the streaming 3x3, the
+    pool-fused encoder apply, the streaming ConvTranspose2d, the head with the deferred apply, the
+    3x3 weight gradient -- against stock PyTorch (autocast bf16, channels_last) from identical weights
+    and the same batch.  Both compute in bf16 with fp32 accumulation but round differently."""
+    from deeplearning_mpi_amd.data import device_batch
+    from deeplearning_mpi_amd.models import UNet
+    from deeplearning_mpi_amd.ops import bce_with_logits
+    from deeplearning_mpi_amd.optim import Adam, clip_grad_norm_
+
+    torch.manual_seed(0)
+    ours = UNet(out_classes=1).to(DEV)
+    ref = UNet(out_classes=1).to(DEV)
+    ref.load_state_dict(ours.state_dict())
+    ref = ref.to(memory_format=torch.channels_last)
+    x, y = device_batch("segmentation", 16, torch.device(DEV), (3, 512, 512), seed=1234)
+    opt = Adam(ours.parameters(), lr=1e-4)
+    ropt = torch.optim.Adam(ref.parameters(), lr=1e-4)
+    lo, lr_ = [], []
+    for _ in range(10):
+        opt.zero_grad()
+        loss = bce_with_logits(ours(x).squeeze(1), y)
+        loss.backward()
+        clip_grad_norm_(ours.parameters(), 1.0, optimizer=opt)
+        opt.step()
+        lo.append(float(loss.detach()))
+        ropt.zero_grad()
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            out = ref.forward_torch(x.to(memory_format=torch.channels_last))
+        rl = torch.nn.functional.binary_cross_entropy_with_logits(out.float().squeeze(1), y)
+        rl.backward()
+        torch.nn.utils.clip_grad_norm_(ref.parameters(), 1.0)
+        ropt.step()
+        lr_.append(float(rl))
+        print(f"step {len(lo)}: native {lo[-1]:.5f} torch {lr_[-1]:.5f}", flush=True)   # (MIOpen's first
+        # calls search algorithms for minutes: progress keeps a watchdog from taking that for a hang)
+    lo, lr_ = torch.tensor(lo), torch.tensor(lr_)
+    print("native", [round(v, 5) for v in lo.tolist()])
+    print("torch ", [round(v, 5) for v in lr_.tolist()])
+    assert torch.isfinite(lo).all() and torch.isfinite(lr_).all()
+    assert abs(lo[0] - lr_[0]) < 2e-3 * lr_[0]          # same weights, same batch: first loss
+    assert ((lo[:8] - lr_[:8]).abs() / lr_[:8]).max() < 0.01
+    assert lo[-1] < lo[0] and lr_[-1] < lr_[0]
