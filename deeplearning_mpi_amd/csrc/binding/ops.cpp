@@ -134,7 +134,7 @@ static int g_pipe_dgrad_override = -1;   // dlmpi_ext set_conv_pipe_dgrad (A/B):
 // second (2) for the 256 / 224-row tiles; additionally staggered over the two waves of a SIMD (4) for
 // 128 x 256 (profiles/r4_lab: 3-8 % over issuing all at once, on every measured shape)
 static int pipe_select(int f32, int pro, int cin, int64_t M, int Kout, int64_t red, int& bm, int& bn) {
-  if (f32 || pro != 0 || cin % 64 != 0 || g_pipe_override == 0) return 0;
+  if (f32 || pro != 0 || cin % 64 != 0 || cin > 4032 || g_pipe_override == 0) return 0;   // (conv_igemm.hip kPipeMaxC)
   if (g_pipe_override == 1) {
     bm = Kout >= 256 ? 256 : (Kout > 64 ? 256 : 512);
     bn = Kout >= 256 ? 256 : (Kout > 64 ? 128 : 64);

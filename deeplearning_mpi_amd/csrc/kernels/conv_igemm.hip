@@ -661,6 +661,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BM * BN <= 
   conv_epilogue<BM, BN, NT, WGM, WGN, T, HALO>(a, ph, acc, smem, tid, m0, n0, mt, hn, hh0, hw0);
 }
 
+// 8 KB of zeros: the pipelined kernel's out-of-image A pieces read here at the K-step's channel offset
+// (2 C + 16 jc < 8 KB: C <= kPipeMaxC, checked at launch)
+static __device__ u32x4 g_zero_run[512] = {};
+constexpr int kPipeMaxC = 4032;
+
 // ---- the pipelined 8-wave kernel -----------------------------------------------------------------
 // BM x BN x 64 tiles, 512 threads = 8 waves in WGM x WGN, one block per CU, bf16, C % 64 == 0, one
 // phase per blockIdx.z (forward convs, dgrad sub-pixel phases), no operand prologue, no split-K.
@@ -741,8 +746,11 @@ __global__ __launch_bounds__(64 * WGM * WGN) __attribute__((amdgpu_waves_per_eu(
 
   const int C = a.C;
   const int nk = ph.ksteps;
-  uint32_t a_off[AL];
-  uint32_t a_vm = 0;
+  // A pieces: one pointer per piece per tap (set at the tap's first K-step), the channel offset of the
+  // K-step added as a scalar.  An out-of-image / past-M piece points into an 8 KB zero run instead,
+  // which every channel offset (2 C + 16 jc < 8 KB, host-checked) keeps inside: no per-K-step select.
+  const char* zr = reinterpret_cast<const char*>(g_zero_run);
+  const char* a_ptr[AL];
   int t_cur = 0, c_cur = 0, wtC2 = 0;
   auto tap_setup = [&](int t) {
     const int tr = (int)fdiv((uint32_t)t, ph.fdTs);
@@ -751,13 +759,11 @@ __global__ __launch_bounds__(64 * WGM * WGN) __attribute__((amdgpu_waves_per_eu(
     const int wt = (ph.wr0 + tr * ph.wrs) * a.S + (ph.ws0 + ts * ph.wss);
     wtC2 = wt * C * 2;
     const int doff = dh * a.W + dw;
-    a_vm = 0;
 #pragma unroll
     for (int i = 0; i < AL; ++i) {
       const int ih = (a_hw[i] >> 16) + dh, iw = (a_hw[i] & 0xffff) + dw;
       const bool ok = ((a_okm >> i) & 1) && (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W;
-      if (ok) a_vm |= 1u << i;
-      a_off[i] = (uint32_t)(a_pix[i] + doff) * (uint32_t)a.ldx;
+      a_ptr[i] = ok ? xlane + 2 * (uint64_t)((uint32_t)(a_pix[i] + doff) * (uint32_t)a.ldx) : zr + 16 * jc;
     }
   };
   auto advance = [&]() {
@@ -770,17 +776,17 @@ __global__ __launch_bounds__(64 * WGM * WGN) __attribute__((amdgpu_waves_per_eu(
   };
   auto issue_a = [&](int slot) {
     char* As = smem + slot * SB;
+    const int c2 = 2 * c_cur;
 #pragma unroll
-    for (int i = 0; i < AL; ++i) {
-      const char* s = ((a_vm >> i) & 1) ? xlane + 2 * ((uint64_t)a_off[i] + c_cur) : zp;
-      glds16(s, As + (RP * i + 8 * wid) * 128);
-    }
+    for (int i = 0; i < AL; ++i) glds16(a_ptr[i] + c2, As + (RP * i + 8 * wid) * 128);
   };
+  const bool b_all = b_okm == (1u << BL) - 1;   // every weight row of the tile exists (Kout % BN == 0)
   auto issue_b = [&](int slot) {
     char* Bs = smem + slot * SB + A_BYTES;
+    const int64_t boff = (int64_t)wtC2 + 2 * c_cur;
 #pragma unroll
     for (int i = 0; i < BL; ++i) {
-      const char* s = ((b_okm >> i) & 1) ? b_base + i * b_step + wtC2 + 2 * c_cur : zp;
+      const char* s = (b_all || ((b_okm >> i) & 1)) ? b_base + i * b_step + boff : zp;
       glds16(s, Bs + (RP * i + 8 * wid) * 128);
     }
   };
@@ -810,8 +816,10 @@ __global__ __launch_bounds__(64 * WGM * WGN) __attribute__((amdgpu_waves_per_eu(
       }
     }
   }
-  int rd = 0;   // slot of step ks
-  for (int ks = 0; ks < nk; ++ks) {
+  // one K-step on slot RD (a constant: the loop below is unrolled by STAGES, so every fragment read
+  // is a lane offset + an immediate)
+  auto step = [&](int ks, auto RDc) {
+    constexpr int rd = decltype(RDc)::value;
     if constexpr (STAGES == 3) {
       if (ks + 1 < nk) asm volatile("s_waitcnt vmcnt(%0)\n\ts_waitcnt lgkmcnt(0)" :: "n"(NLD) : "memory");
       else asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)" ::: "memory");
@@ -821,8 +829,7 @@ __global__ __launch_bounds__(64 * WGM * WGN) __attribute__((amdgpu_waves_per_eu(
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     const bool more = ks + STAGES - 1 < nk;
-    int wr = rd + STAGES - 1;
-    if (wr >= STAGES) wr -= STAGES;
+    constexpr int wr = (rd + STAGES - 1) % STAGES;
     if (more) advance();
     const char* As = smem + rd * SB;
     const bool up = wid >= NW / 2;   // wave-uniform: waves w and w + NW/2 share a SIMD
@@ -858,7 +865,12 @@ __global__ __launch_bounds__(64 * WGM * WGN) __attribute__((amdgpu_waves_per_eu(
               acc[h * MH + q][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[q], bfr[ni], acc[h * MH + q][ni], 0, 0, 0);
       }
     }
-    rd = rd + 1 == STAGES ? 0 : rd + 1;
+  };
+  for (int ks = 0; ks < nk; ks += STAGES) {
+    step(ks, std::integral_constant<int, 0>{});
+    if (ks + 1 < nk) step(ks + 1, std::integral_constant<int, 1>{});
+    if constexpr (STAGES == 3)
+      if (ks + 2 < nk) step(ks + 2, std::integral_constant<int, 2>{});
   }
   __syncthreads();   // the last fragment reads are done before the epilogue reuses the LDS
   conv_epilogue<BM, BN, NT, WGM, WGN, uint16_t, false>(a, ph, acc, smem, tid, m0, n0, mt, 0, 0, 0);
@@ -1090,7 +1102,7 @@ static hipError_t launch_f32(const ConvArgs* a, int bm, int bn, dim3 grid, hipSt
 // Pipelined 8-wave tiles (conv_pipe_kernel): (bm, bn) -> instance.  Returns hipErrorInvalidValue
 // when the launch does not fit the kernel (channels, prologue, split, fp32).
 static hipError_t launch_pipe(const ConvArgs* a, int bm, int bn, int var, dim3 grid, hipStream_t s) {
-  if (a->f32 || a->pro != 0 || a->C % 64 != 0 || a->halo || grid.y != 1) return hipErrorInvalidValue;
+  if (a->f32 || a->pro != 0 || a->C % 64 != 0 || a->C > kPipeMaxC || a->halo || grid.y != 1) return hipErrorInvalidValue;
   // the measured issue placement of each tile (profiles/r4_lab): VAR 2 for the 256 / 224 / 512-row
   // tiles, VAR 4 for 128 x 256; the other placements are gone (var must name the tile's own)
   if (var != (bm == 128 ? 4 : 2)) return hipErrorInvalidValue;

@@ -7,6 +7,11 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 
+# Stock PyTorch references (MIOpen) in the GPU tests: on a fresh box MIOpen's first call of each
+# convolution otherwise compiles / searches kernels for minutes (the UNet-512 bench-scale test: > 7
+# min); FAST picks an immediate-mode solution.  Set before any MIOpen handle exists in this process.
+os.environ.setdefault("MIOPEN_FIND_MODE", "FAST")
+
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (gfx950) GPU and the native extension")
