@@ -1620,12 +1620,12 @@ void sgd_step(at::Tensor p, const at::Tensor& g, at::Tensor m, double lr, double
                   (float)dampening, (float)wd, nesterov ? 1 : 0, first ? 1 : 0, optr<float>(skip_flag), cur_stream()),
         "sgd");
 }
-void adam_step(at::Tensor p, const at::Tensor& g, at::Tensor m, at::Tensor v, double lr, double b1, double b2,
+void adam_step(at::Tensor p, at::Tensor g, at::Tensor m, at::Tensor v, double lr, double b1, double b2,
                double eps, double wd, bool adamw, double bc1, double bc2, const c10::optional<at::Tensor>& clip,
-               const c10::optional<at::Tensor>& tstep) {
+               const c10::optional<at::Tensor>& tstep, bool clip_writeback) {
   check(dlmpi_adam(ptr<float>(p), ptr<float>(g), ptr<float>(m), ptr<float>(v), p.numel(), (float)lr, (float)b1,
                    (float)b2, (float)eps, (float)wd, adamw ? 1 : 0, (float)bc1, (float)bc2, optr<float>(clip),
-                   optr<float>(tstep), cur_stream()),   // advanced in place unless skipped
+                   optr<float>(tstep), clip_writeback ? 1 : 0, cur_stream()),   // tstep advanced in place unless skipped
         "adam");
 }
 // total L2 norm of a flat fp32 buffer -> norm_out[0]; coef_out = {min(1, max_norm/(norm+1e-6)), nonfinite}

@@ -401,9 +401,9 @@ hipError_t dlmpi_dice(const float* logits, int ldl, const float* target, int N, 
 // optimizers on flat fp32 buffers
 hipError_t dlmpi_sgd(float* p, const float* g, float* m, int64_t n, float lr, float momentum, float dampening,
                      float wd, int nesterov, int first, const float* skip_flag, hipStream_t s);
-hipError_t dlmpi_adam(float* p, const float* g, float* m, float* v, int64_t n, float lr, float b1, float b2,
+hipError_t dlmpi_adam(float* p, float* g, float* m, float* v, int64_t n, float lr, float b1, float b2,
                       float eps, float wd, int adamw, float bc1, float bc2, const float* clip_coef,
-                      float* tstep, hipStream_t s);   // tstep (device step count) overrides bc1/bc2
+                      float* tstep, int wb, hipStream_t s);   // tstep (device step count) overrides bc1/bc2
 hipError_t dlmpi_sumsq(const float* x, int64_t n, float* partial, int nblk, hipStream_t s);
 hipError_t dlmpi_clip_coef(const float* partial, int nblk, float max_norm, float* norm_out, float* coef_out, int ncoef,
                            hipStream_t s);

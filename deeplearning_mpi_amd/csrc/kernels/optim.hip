@@ -55,14 +55,19 @@ __device__ __forceinline__ void adam_elem(float& p, float g, float& m, float& v,
   p -= (lr / bc1) * m / denom;
 }
 
-__global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, const float* __restrict__ g,
+// clip_coef = {scale, nonfinite}: the update uses g * scale.  wb (clip_grad_norm_ handed the scaling
+// to the optimizer instead of a separate pass over the gradients): g * scale is also stored back into
+// g when scale != 1, so the gradients read afterwards are the clipped ones, as after torch's in-place
+// clip -- the same product the separate pass stored (bit-identical update and gradients).
+__global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, float* __restrict__ g,
                                                    float* __restrict__ m, float* __restrict__ v, int64_t n, float lr,
                                                    float b1, float b2, float eps, float wd, int adamw, float bc1,
                                                    float bc2, const float* __restrict__ clip_coef,
-                                                   const float* __restrict__ tstep) {
+                                                   const float* __restrict__ tstep, int wb) {
   // tstep = number of updates applied so far (device scalar): this update is number tstep + 1
   const float coef = clip_coef ? clip_coef[0] : 1.f;
   if (clip_coef && clip_coef[1] != 0.f) return;   // non-finite gradient norm: collective skip
+  const bool store_g = wb && coef != 1.f;
   if (tstep) {   // step count on the device: bias corrections stay correct under hipGraph replay
     const float t = *tstep + 1.f;
     bc1 = 1.f - powf(b1, t);
@@ -88,13 +93,16 @@ __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, const 
     reinterpret_cast<f32x4*>(p)[i] = pv;
     reinterpret_cast<f32x4*>(m)[i] = mv;
     reinterpret_cast<f32x4*>(v)[i] = vv;
+    if (store_g) reinterpret_cast<f32x4*>(g)[i] = gv * coef;
   }
   for (int64_t i = 4 * n4 + blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += stride) {
     float pv = p[i], mv = m[i], vv = v[i];
-    adam_elem(pv, g[i], mv, vv, lr, b1, b2, eps, wd, adamw, bc1, bc2, coef);
+    const float gi = g[i];
+    adam_elem(pv, gi, mv, vv, lr, b1, b2, eps, wd, adamw, bc1, bc2, coef);
     p[i] = pv;
     m[i] = mv;
     v[i] = vv;
+    if (store_g) g[i] = gi * coef;
   }
 }
 
@@ -193,11 +201,11 @@ extern "C" hipError_t dlmpi_sgd(float* p, const float* g, float* m, int64_t n, f
                      wd, nesterov, first, skip_flag);
   return hipGetLastError();
 }
-extern "C" hipError_t dlmpi_adam(float* p, const float* g, float* m, float* v, int64_t n, float lr, float b1, float b2,
+extern "C" hipError_t dlmpi_adam(float* p, float* g, float* m, float* v, int64_t n, float lr, float b1, float b2,
                                  float eps, float wd, int adamw, float bc1, float bc2, const float* clip_coef,
-                                 float* tstep, hipStream_t s) {
+                                 float* tstep, int wb, hipStream_t s) {
   hipLaunchKernelGGL(adam_kernel, dim3(blocks_for(n / 4 + 1)), dim3(256), 0, s, p, g, m, v, n, lr, b1, b2, eps, wd, adamw,
-                     bc1, bc2, clip_coef, tstep);
+                     bc1, bc2, clip_coef, tstep, wb);
   if (tstep) hipLaunchKernelGGL(adam_step_advance_kernel, dim3(1), dim3(64), 0, s, tstep, clip_coef);
   return hipGetLastError();
 }

@@ -674,6 +674,7 @@ class _EngineFn(torch.autograd.Function):
     def forward(ctx, mod, x, anchor):
         with trace_range(f"dlmpi.forward[{type(mod).__name__}]"):
             out, state = mod._engine_forward(x, train=True, save=True)
+            mod._arena.end_cast()   # the side-stream weight recast joined (normally long since, lazily)
         ctx.mod = mod
         ctx.state = state
         ctx.aux_on = getattr(mod._be, "aux_on", None)   # the backward uses the forward's stream plan
@@ -780,7 +781,7 @@ class EngineModule(nn.Module):
         be = self._be
         if hasattr(be, "aux_min_pixels"):   # auxiliary streams only for steps big enough to use them
             be.aux_on = x.shape[0] * x.shape[-2] * x.shape[-1] >= be.aux_min_pixels
-        self._arena.refresh()
+        self._arena.refresh(split=True)   # (the rest of a split recast goes out at the model's launch_cast)
         if self.training and torch.is_grad_enabled():
             self._arena.attach_grads()
             if self._arena.ibuf_total:   # every BatchNorm's num_batches_tracked, one launch
@@ -790,6 +791,7 @@ class EngineModule(nn.Module):
             if self.training and self._arena.ibuf_total:
                 be.add_i64_(self._arena.ibuf, 1)
             out, _ = self._engine_forward(x, train=self.training, save=False)
+            self._arena.end_cast()
         return out
 
     # implemented by the model

@@ -302,6 +302,8 @@ class ResNet(EngineModule):
             for b in layer:
                 self.blocks.append(_BlockExec(*b.units(ar)))
         self.u_fc = ConvUnit(ar, self.fc, None, relu=False)
+        # (no split weight recast, ar.mark_cast_group: on the side stream beside the stem conv or beside
+        # layer 1 it slowed those memory-heavy kernels by as much as it saved or more, profiles/r6_recast)
 
     def _engine_forward(self, x, train, save):
         be = self._be

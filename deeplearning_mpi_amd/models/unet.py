@@ -137,8 +137,11 @@ class UNet(EngineModule):
         self.cin_pad = padc(self.in_channels)
         downs = [self.down_conv1, self.down_conv2, self.down_conv3, self.down_conv4]
         ups = [self.up_conv1, self.up_conv2, self.up_conv3, self.up_conv4]   # level 1..4
-        self.enc = [d.double_conv.units(ar, cin_pad=self.cin_pad if k == 0 else None, need_dgrad=k != 0)
-                    for k, d in enumerate(downs)]
+        self.enc = []
+        for k, d in enumerate(downs):
+            self.enc.append(d.double_conv.units(ar, cin_pad=self.cin_pad if k == 0 else None, need_dgrad=k != 0))
+            if k == 0:   # the input DoubleConv's weights recast first; the rest beside its forward
+                ar.mark_cast_group()
         self.bott = self.double_conv.units(ar)
         self.skip_ch = [64, 128, 256, 512]
         self.up_ch = [128, 256, 512, 1024]   # channels arriving from below at levels 1..4
@@ -160,6 +163,8 @@ class UNet(EngineModule):
             cats.append(cat)
             ua, ub = self.enc[k]
             t, ca = ua.fwd(be, a, train, save=save)
+            if k == 0:   # the deeper layers' weight recast beside the 64-channel 3x3 conv (compute-bound)
+                self._arena.launch_cast()
             skip = cat.slice(self.up_ch[k], self.skip_ch[k])
             down = Act.empty(N, h // 2, w // 2, self.skip_ch[k], dt, dev)
             # (only with the fused BN backward: its data gradient takes the ReLU mask from z, the unfused

@@ -435,8 +435,8 @@ class NativeBackend:
     def sgd(self, p, g, m, lr, momentum, dampening, wd, nesterov, first, skip_flag=None):
         self.C.sgd_step(p, g, m, lr, momentum, dampening, wd, nesterov, first, skip_flag)
 
-    def adam(self, p, g, m, v, lr, b1, b2, eps, wd, adamw, bc1, bc2, clip=None, tstep=None):
-        self.C.adam_step(p, g, m, v, lr, b1, b2, eps, wd, adamw, bc1, bc2, clip, tstep)
+    def adam(self, p, g, m, v, lr, b1, b2, eps, wd, adamw, bc1, bc2, clip=None, tstep=None, clip_writeback=False):
+        self.C.adam_step(p, g, m, v, lr, b1, b2, eps, wd, adamw, bc1, bc2, clip, tstep, bool(clip_writeback))
 
     def grad_norm(self, g, max_norm, norm_out, coef_out):
         self.C.grad_norm(g, max_norm, norm_out, coef_out)
@@ -786,7 +786,7 @@ class RefBackend:
             d = d + momentum * m if nesterov else m
         p.add_(d, alpha=-lr)
 
-    def adam(self, p, g, m, v, lr, b1, b2, eps, wd, adamw, bc1, bc2, clip=None, tstep=None):
+    def adam(self, p, g, m, v, lr, b1, b2, eps, wd, adamw, bc1, bc2, clip=None, tstep=None, clip_writeback=False):
         coef = 1.0
         if clip is not None:
             if float(clip[1]) != 0:
@@ -796,7 +796,10 @@ class RefBackend:
             t = float(tstep.reshape(-1)[0]) + 1
             bc1, bc2 = 1 - b1 ** t, 1 - b2 ** t
             tstep.add_(1)
+        gin = g
         g = g * coef
+        if clip_writeback and float(coef) != 1.0:   # the clipped gradients stay visible (torch's in-place clip)
+            gin.copy_(g)
         if wd != 0:
             if adamw:
                 p.mul_(1 - lr * wd)

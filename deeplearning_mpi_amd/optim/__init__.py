@@ -102,6 +102,7 @@ class Adam(_FusedBase):
         super().__init__(params, dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay))
         self.decoupled = decoupled
         self.clip = None   # device [coef, nonfinite] from clip_grad_norm_ (applied & used to skip)
+        self._clip_handoff = False   # clip_grad_norm_ left the in-place scaling to this step (see there)
 
     @torch.no_grad()
     def step(self, closure=None):
@@ -123,7 +124,10 @@ class Adam(_FusedBase):
             if "step" not in st:
                 st["step"] = torch.zeros(1, dtype=torch.float32, device=p.device)
             self._be.adam(p, gr, m, v, g["lr"], b1, b2, g["eps"], g["weight_decay"], self.decoupled,
-                          1 - b1 ** t, 1 - b2 ** t, self.clip, st["step"])
+                          1 - b1 ** t, 1 - b2 ** t, self.clip, st["step"], clip_writeback=self._clip_handoff)
+        if self._clip_handoff:   # a handed-off coefficient is used once
+            self.clip = None
+            self._clip_handoff = False
         if self._arena is not None:
             self._arena.mark_updated()
         return loss
@@ -138,7 +142,10 @@ def clip_grad_norm_(parameters, max_norm: float, norm_type: float = 2.0, optimiz
     """L2 gradient clipping without a host synchronisation.  Returns the total norm as a device
     tensor.  With ``optimizer`` (our Adam) the clip coefficient is also handed to it so a
     non-finite norm skips the update (the same decision on every rank, because gradients are
-    identical after the all-reduce).
+    identical after the all-reduce).  With ``optimizer`` and arena-backed parameters (norm_type 2)
+    the in-place scaling of the gradients is left to that optimizer's next ``step()``: its kernel
+    stores g * coef back while it reads g (one pass over the gradients less, the same products:
+    bit-identical update and gradients), so until ``step()`` the gradients are still unscaled.
 
     ``norm_type`` 2 runs the fused single-pass kernel; any other p (including ``inf``) is the
     torch.nn.utils.clip_grad_norm_ contract computed with device-side torch reductions (still no
@@ -168,6 +175,11 @@ def clip_grad_norm_(parameters, max_norm: float, norm_type: float = 2.0, optimiz
             g.mul_(coef[0].to(g.dtype))
     elif a is not None:
         be.grad_norm(a.grad, float(max_norm), norm, coef)
+        if optimizer is not None and hasattr(optimizer, "_clip_handoff") and \
+                (optimizer._resolve_arena() or getattr(optimizer, "_arena", None) is a):
+            optimizer.clip = coef[0:2]   # (scale, skip): applied and stored back by the optimizer's step
+            optimizer._clip_handoff = True
+            return norm[0]
         be.scale_(a.grad, coef)
     else:
         flat = torch.cat([p.grad.reshape(-1).float() for p in params])

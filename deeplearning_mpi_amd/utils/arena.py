@@ -14,7 +14,10 @@ order.  Consequences (MI355X-first design):
 * conv weights are stored channels-last (memory order [K][R][S][C]) so the fp32 master already
   has the GEMM layout, and the kernels' weight-gradient output lands in it directly;
 * bf16 compute copies (forward layout and transposed data-gradient layout, channel padded) are
-  produced for all layers by ONE multi-tensor cast launch whenever the masters changed.
+  produced for all layers by ONE multi-tensor cast launch whenever the masters changed -- two when
+  the model marks its first layer (``mark_cast_group``): that layer's copies on the current stream,
+  the rest on the backend's side stream beside the first layer's forward (``launch_cast``, joined
+  lazily by ``get_compute``), so the recast is off the step's critical path.
 
 ``nn.Parameter`` objects are kept (their ``.data`` is re-pointed into the arena), so
 ``state_dict()`` keys/shapes/dtypes are unchanged and foreign optimizers still work.
@@ -125,6 +128,12 @@ class ParamArena:
         self.compute = None
         self._synced_version = None
         self.post_refresh = []      # callables run after every recast (derived weight layouts)
+        self._cast_split = None     # (entries, post_refresh) counts of the first layer (mark_cast_group)
+        self._cast_lists = None     # (first-layer entries, the rest), kept for the backend's cast cache
+        self._cast_deferred = None  # split recast's second part, not yet issued: (entries, post_refresh index)
+        self._cast_event = None     # side-stream recast in flight: (event, first offset it covers, REPLAYS)
+        self._cast_waited = []      # streams that have waited for it
+        self.split_casts = 0        # recasts that took the two-stream path (tests)
         self.hook = None            # reducer.mark_ready(param_index) during backward
         self.backward_end = None    # reducer.finalize() at the end of the engine backward
         self.buffer_fence = None    # joins an in-flight broadcast of fbuf (DDP K5) before its first use
@@ -220,9 +229,86 @@ class ParamArena:
         self.compute = None
         return (off, n, tuple(dims))
 
+    def mark_cast_group(self):
+        """Called by a model right after registering its first layer's compute copies (and derived
+        layouts): those are recast on the current stream, everything registered later on the side
+        stream (``refresh``).  Only the first call counts."""
+        if self._cast_split is None:
+            self._cast_split = (len(self._entries), len(self.post_refresh))
+
     def get_compute(self, handle) -> torch.Tensor:
         off, n, dims = handle
+        if self._cast_deferred is not None and off >= self._cast_deferred[0][0][1]:
+            self.launch_cast()
+        ev = self._cast_event
+        if ev is not None and off >= ev[1]:
+            self.join_cast()
         return self.compute[off:off + n]
+
+    def launch_cast(self):
+        """Issue the deferred part of a split recast (every compute copy after the first layer's) on
+        the backend's side stream, ordered after the current stream's work so far; the consumers join
+        it in ``get_compute``.  A no-op without a deferred part."""
+        d = self._cast_deferred
+        if d is None:
+            return
+        self._cast_deferred = None
+        rest, p1 = d
+        side = getattr(self.backend, "side_stream", None)
+        if side is None:   # (the auxiliary streams were turned off meanwhile)
+            self.backend.cast_weights(rest, self._compute_total, self.compute)
+            for fn in self.post_refresh[p1:]:
+                fn()
+            return
+        cur = torch.cuda.current_stream(self.device)
+        side.wait_stream(cur)   # the masters are final (optimizer step) and the old copies read
+        torch.cuda.set_stream(side)
+        try:
+            self.backend.cast_weights(rest, self._compute_total, self.compute)
+            for fn in self.post_refresh[p1:]:
+                fn()
+            ev = torch.cuda.Event()
+            ev.record(side)
+        finally:
+            torch.cuda.set_stream(cur)
+        from . import graphs
+
+        self._cast_event = (ev, rest[0][1], graphs.REPLAYS)
+        self._cast_waited = []
+        self.split_casts += 1
+
+    def join_cast(self):
+        """Order the current stream after the side-stream recast (a no-op once it has waited).
+        The engine forward joins on its own stream at its end.  A recast from before a hipGraph
+        replay or a failed capture (``graphs.REPLAYS`` moved on) is dropped, never waited for: the
+        next recast, queued behind it on the same side stream, supersedes it."""
+        ev = self._cast_event
+        if ev is None:
+            return
+        from . import graphs
+
+        if ev[2] != graphs.REPLAYS:
+            self._cast_event = None
+            self._cast_waited = []
+            return
+        cur = torch.cuda.current_stream(self.device)
+        if cur not in self._cast_waited:
+            cur.wait_event(ev[0])
+            self._cast_waited.append(cur)
+
+    def end_cast(self):
+        """Join the recast on the current stream and forget it (end of the engine forward)."""
+        self.launch_cast()
+        if self._cast_event is not None:
+            self.join_cast()
+            self._cast_event = None
+            self._cast_waited = []
+
+    def _split_lists(self, sp):
+        lists = self._cast_lists
+        if lists is None or sum(map(len, lists)) != len(self._entries):
+            lists = self._cast_lists = (self._entries[:sp[0]], self._entries[sp[0]:])
+        return lists
 
     def _version(self):
         # hipGraph replays update the masters without touching any host-side version counter
@@ -230,17 +316,44 @@ class ParamArena:
 
         return (sum(p._version for p in self.params) + self.flat._version, graphs.REPLAYS)
 
-    def refresh(self, force=False):
-        """Recast all compute copies if any master parameter changed (one kernel launch)."""
+    def refresh(self, force=False, split=False):
+        """Recast all compute copies if any master parameter changed (one kernel launch).  split (the
+        engine forward): with a marked first layer and a side stream, only that layer's copies now,
+        the rest at ``launch_cast`` on the side stream."""
         if self.compute is None:
             dt = self.backend.act_dtype if self.backend is not None else torch.bfloat16
             self.compute = torch.zeros(max(1, self._compute_total), dtype=dt, device=self.device)
             force = True
         v = self._version()
         if force or v != self._synced_version:
-            self.backend.cast_weights(self._entries, self._compute_total, self.compute)
-            for fn in self.post_refresh:   # derived layouts built from the compute copies
-                fn()
+            self.end_cast()   # (a recast still in flight: ordered before this one)
+            side = getattr(self.backend, "side_stream", None)
+            sp = self._cast_split
+            if not split or side is None or sp is None or not 0 < sp[0] < len(self._entries):
+                self.backend.cast_weights(self._entries, self._compute_total, self.compute)
+                for fn in self.post_refresh:   # derived layouts built from the compute copies
+                    fn()
+            elif torch.cuda.is_current_stream_capturing():
+                # inside a hipGraph capture: both parts on the capturing stream (a capture that failed
+                # after forking the side stream into it crashed HIP in the eager fallback; captured
+                # steps are the launch-bound ones anyway), with the descriptors the eager steps cached
+                # (building one would copy host memory, which a capture refuses)
+                lists = self._split_lists(sp)
+                self.backend.cast_weights(lists[0], self._compute_total, self.compute)
+                for fn in self.post_refresh[:sp[1]]:
+                    fn()
+                self.backend.cast_weights(lists[1], self._compute_total, self.compute)
+                for fn in self.post_refresh[sp[1]:]:
+                    fn()
+            else:
+                lists = self._split_lists(sp)
+                self.backend.cast_weights(lists[0], self._compute_total, self.compute)
+                for fn in self.post_refresh[:sp[1]]:
+                    fn()
+                # the rest goes out at launch_cast(): the model calls it where the side-stream recast
+                # overlaps compute-bound work (beside the memory-bound input preparation it cost
+                # as much as it saved, profiles/r6_recast)
+                self._cast_deferred = (lists[1], sp[1])
             self._synced_version = v
 
     def mark_updated(self):

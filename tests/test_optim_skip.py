@@ -36,3 +36,36 @@ def test_adam_skipped_step_is_a_no_op(device):
     assert with_skip[3] == without[3] == 3.0
     for a, b in zip(with_skip[:3], without[:3]):
         assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("device", ["cpu", pytest.param("cuda", marks=pytest.mark.gpu)])
+def test_clip_handoff_matches_in_place_clip(device):
+    """clip_grad_norm_(..., optimizer=adam) on an arena-backed model leaves the gradient scaling to
+    Adam's kernel (stored back while it reads g).  Parameters, moments AND the gradients after step()
+    must equal the separate in-place clip followed by an unscaled Adam step, bit for bit."""
+    import copy
+
+    from deeplearning_mpi_amd.models import resnet18
+    from deeplearning_mpi_amd.ops import cross_entropy
+
+    torch.manual_seed(0)
+    m1 = resnet18(num_classes=10).to(device)
+    m2 = copy.deepcopy(m1)
+    x = torch.randn(4, 3, 32, 32, device=device)
+    y = torch.tensor([1, 7, 3, 0], device=device)
+    out = []
+    for m, handoff in ((m1, True), (m2, False)):
+        opt = Adam(m.parameters(), lr=1e-3)
+        for _ in range(2):
+            opt.zero_grad()
+            cross_entropy(m(x), y).backward()
+            if handoff:
+                clip_grad_norm_(m.parameters(), 0.05, optimizer=opt)
+                assert opt._clip_handoff
+            else:
+                clip_grad_norm_(m.parameters(), 0.05)   # scales in place
+            opt.step()
+            assert opt.clip is None
+        out.append(([p.detach().clone() for p in m.parameters()], [p.grad.detach().clone() for p in m.parameters()]))
+    for a, b in zip(out[0][0] + out[0][1], out[1][0] + out[1][1]):
+        assert torch.equal(a, b)
