@@ -221,7 +221,8 @@ static bool halo_eligible(int f32, int pro, int C, int R, int S, int stride, int
 // Halo tiles before the pipelined kernel for >= 256 output channels (profiles/r4_halo: the 256 x 128
 // halo tile beat the best pipe tile on every UNet 3x3 of >= 32^2 grid, 2-5 %; 32^2 1024 -> 1024: 231.6
 // vs 243.2 us); the pipe kernel keeps the 14^2 / 7^2 grids, where halo tiles are not eligible.
-static bool halo_first(bool halo_ok, int Kout) { return halo_ok && Kout >= 256; }
+static int g_halo_first = 1;   // dlmpi_ext set_halo_first (A/B): 0 = the pipelined kernel first where it applies
+static bool halo_first(bool halo_ok, int Kout) { return halo_ok && Kout >= 256 && g_halo_first; }
 static int g_halo_ran = 0;   // 1 if the last conv2d_fwd / conv2d_dgrad ran halo tiles (tests)
 // Switch a fully set-up single-phase launch (bm 128 / 256) to halo tiles: its M-tiles (and stats rows)
 // become N x tiles_h x tiles_w.
@@ -1784,6 +1785,8 @@ void register_ops(pybind11::module& m) {
   m.def("wgrad_pending", []() { return (int)g_pending.size(); });
   m.def("wgrad_reduce_launches", []() { return g_reduce_launches; });
   m.def("set_conv_halo", [](int mode) { g_halo_override = mode; });
+  m.def("set_halo_first", [](int on) { g_halo_first = on; });
+  m.def("set_halo_pipe", [](int on) { dlmpi_set_halo_pipe(on); });
   m.def("set_conv_splitk", [](int n) { g_splitk_override = n; });
   m.def("set_conv_pipe_dgrad", [](int mode) { g_pipe_dgrad_override = mode; });
   m.def("set_conv_pipe", [](int mode) { g_pipe_override = mode; });

@@ -876,6 +876,184 @@ __global__ __launch_bounds__(64 * WGM * WGN) __attribute__((amdgpu_waves_per_eu(
   conv_epilogue<BM, BN, NT, WGM, WGN, uint16_t, false>(a, ph, acc, smem, tid, m0, n0, mt, 0, 0, 0);
 }
 
+// ---- 2-D halo tiles with the weight tile double-buffered ---------------------------------------------
+// conv_halo_pipe_kernel: conv_igemm_kernel's HALO mode (3x3 / stride 1 / pad 1, the (th + 2) x (tw + 2)
+// input halo of a 64-channel chunk staged once, the 9 taps 9 K-steps over it; same tile decode, same
+// fragment addressing, same epilogue) with two LDS slots for the weight tile, so the single-stage
+// kernel's exposed DMA latency per tap is gone: the DMA of tap k + 1 goes into the other slot while
+// the MFMAs of tap k run, and a K-step has ONE barrier:
+//     wait   this wave's DMA of step k landed (vmcnt(0): nothing younger is in flight) and its
+//            fragment reads of step k - 1 returned (lgkmcnt(0))
+//     barrier -> every wave's step-k DMA landed (RAW); every wave is done reading slot (k + 1) mod 2 (WAR)
+//     issue the weight DMA of step k + 1 into slot (k + 1) mod 2 (after this step's first fragment reads)
+//     MFMAs of step k
+// The halo itself stays single-buffered (45 KB at 256-pixel tiles; two of them would leave one block
+// per CU): at the last tap of a chunk the next chunk's halo and first weight tile are issued after a
+// second barrier, once every wave is done with the old halo -- one exposed load per 9 K-steps.
+// Same K order and per-element arithmetic as conv_igemm_kernel: bit-identical results.  No split-K
+// (the launcher keeps the single-stage kernel for split grids).
+template <int BM, int BN, int WGM>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void conv_halo_pipe_kernel(const ConvArgs a) {
+  constexpr int NW = 4, NT = 256, WGN = NW / WGM;
+  constexpr int WM = BM / WGM, WN = BN / WGN, TM = WM / 16, TN = WN / 16;
+  constexpr int RP = NT / 8;                  // 32 tile rows per staging pass
+  constexpr int BL = BN / RP;                 // weight pieces per thread per K-step
+  constexpr int HALO_ROWS = BM == 256 ? 352 : 192;
+  constexpr int HL = HALO_ROWS / RP;          // halo pieces per thread per chunk
+  constexpr int A_BYTES = HALO_ROWS * 128, B_BYTES = BN * 128;
+  constexpr int SB = A_BYTES + 2 * B_BYTES;   // [halo | weight slot 0 | weight slot 1]
+  constexpr int EPI_NEED = EpiSmem<BM, BN, NT, WM>::bytes;
+  constexpr int SMEM = SB > EPI_NEED ? SB : EPI_NEED;
+  static_assert(HALO_ROWS % RP == 0 && BN % RP == 0 && TM >= 1 && TN >= 1, "tile shape");
+  static_assert(2 * SMEM <= 160 * 1024, "two blocks per CU");
+  __shared__ __attribute__((aligned(16))) char smem[SMEM];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wid / WGN, wn = wid % WGN;
+  const int lrow = tid >> 3;
+  const int jc = (tid & 7) ^ ((tid >> 3) & 7);
+  const char* zp = reinterpret_cast<const char*>(g_zero_page);
+
+  const int zph = blockIdx.z;
+  const uint32_t nwg0 = (uint32_t)a.ph[zph].mtiles * (uint32_t)a.ntiles;
+  if (blockIdx.x >= nwg0) return;
+  const uint32_t bid = xcd_remap(blockIdx.x, nwg0);
+  const ConvPhase ph = a.ph[zph];
+  const int mt = bid / a.ntiles, nt = bid - mt * a.ntiles;
+  const int m0 = mt * BM, n0 = nt * BN;
+  const int hn = (int)fdiv((uint32_t)mt, a.fd_thw);
+  const int rem = mt - hn * a.tiles_h * a.tiles_w;
+  const int ti = (int)fdiv((uint32_t)rem, a.fd_tilesw);
+  const int hh0 = ti * a.th, hw0 = (rem - ti * a.tiles_w) * a.tw;
+
+  const char* b_base = reinterpret_cast<const char*>(a.w) + 2 * ((int64_t)(n0 + lrow) * a.ldw + 8 * jc);
+  const int64_t b_step = (int64_t)2 * RP * a.ldw;
+  uint32_t b_okm = 0;
+#pragma unroll
+  for (int i = 0; i < BL; ++i)
+    if (n0 + lrow + RP * i < a.Kout) b_okm |= 1u << i;
+  const bool b_all = b_okm == (1u << BL) - 1;
+
+  const int C = a.C;
+  const int NTAP = ph.Tr * ph.Ts;
+  const int nk = ph.ksteps;
+  const int hwd = a.tw + 2;                   // halo row length (pixels)
+  // halo piece i of this lane: halo row lrow + RP i -> (line, col) relative to the tile origin; the
+  // global pixel offset is kept per piece (-1: outside the image or past the halo: the zero page)
+  int64_t hl_off[HL];
+  {
+    const int nrows = (a.th + 2) * hwd;
+#pragma unroll
+    for (int i = 0; i < HL; ++i) {
+      const int hr = lrow + RP * i;
+      const int line = hr / hwd;
+      const int ih = hh0 + line - 1, iw = hw0 + (hr - line * hwd) - 1;
+      const bool ok = hr < nrows && (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W;
+      hl_off[i] = ok ? (int64_t)2 * (((int64_t)hn * a.H + ih) * a.W + iw) * a.ldx : -1;
+    }
+  }
+  const char* xlane = reinterpret_cast<const char*>(a.x) + 2 * ((int64_t)a.xoff + 8 * jc);
+
+  int t_cur = 0, c_cur = 0, wtC2 = 0, toff = 0;
+  auto tap_setup = [&](int t) {
+    const int tr = (int)fdiv((uint32_t)t, ph.fdTs);
+    const int ts = t - tr * ph.Ts;
+    const int dh = ph.dh0 + tr * ph.dhs, dw = ph.dw0 + ts * ph.dws;
+    const int wt = (ph.wr0 + tr * ph.wrs) * a.S + (ph.ws0 + ts * ph.wss);
+    wtC2 = wt * C * 2;
+    toff = (dh + 1) * hwd + (dw + 1);
+  };
+  auto issue_halo = [&]() {
+    const char* xb = xlane + 2 * c_cur;
+#pragma unroll
+    for (int i = 0; i < HL; ++i) glds16(hl_off[i] >= 0 ? xb + hl_off[i] : zp, smem + (RP * i + 8 * wid) * 128);
+  };
+  auto issue_b = [&](int slot) {
+    char* Bs = smem + A_BYTES + slot * B_BYTES;
+    const int64_t boff = (int64_t)wtC2 + 2 * c_cur;
+#pragma unroll
+    for (int i = 0; i < BL; ++i) {
+      const char* src = (b_all || ((b_okm >> i) & 1)) ? b_base + i * b_step + boff : zp;
+      glds16(src, Bs + (RP * i + 8 * wid) * 128);
+    }
+  };
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int mi = 0; mi < TM; ++mi)
+#pragma unroll
+    for (int ni = 0; ni < TN; ++ni) acc[mi][ni] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int fr = lane & 15, fg = lane >> 4;
+  // halo row of this lane's fragment pixel at tap offset 0 (pixels past th * tw read row 0, never stored)
+  int hb[TM];
+#pragma unroll
+  for (int mi = 0; mi < TM; ++mi) {
+    const int r = wm * WM + mi * 16 + fr;
+    const int pr = (int)fdiv((uint32_t)r, a.fd_tw), pc = r - pr * a.tw;
+    hb[mi] = r < a.th * a.tw ? pr * hwd + pc : 0;
+  }
+  const int b_row0 = A_BYTES + (wn * WN + fr) * 128;
+  const int sw = fr & 7;   // (r & 7) of every B fragment row of this lane
+
+  if (nk > 0) {
+    tap_setup(0);
+    issue_halo();
+    issue_b(0);
+  }
+  auto step = [&](int ks, auto SLc) {
+    constexpr int sl = decltype(SLc)::value;
+    asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    const int tcur = toff;
+    const bool more = ks + 1 < nk;
+    const bool chunk_end = more && t_cur + 1 == NTAP;
+    if (more) {   // the next K-step's tap (and chunk)
+      if (++t_cur == NTAP) {
+        t_cur = 0;
+        c_cur += 64;
+      }
+      tap_setup(t_cur);
+    }
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const int ch = kk * 4 + fg;
+      bf16x8 af[TM], bfr[TN];
+#pragma unroll
+      for (int ni = 0; ni < TN; ++ni)
+        bfr[ni] = *reinterpret_cast<const bf16x8*>(smem + b_row0 + sl * B_BYTES + ni * 16 * 128 + ((ch ^ sw) << 4));
+#pragma unroll
+      for (int mi = 0; mi < TM; ++mi) {
+        const int r = hb[mi] + tcur;
+        af[mi] = *reinterpret_cast<const bf16x8*>(smem + r * 128 + ((ch ^ (r & 7)) << 4));
+      }
+      if (kk == 0 && more && !chunk_end) {
+        issue_b(sl ^ 1);
+        asm volatile("" ::: "memory");
+      }
+#pragma unroll
+      for (int mi = 0; mi < TM; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < TN; ++ni)
+          acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[mi], bfr[ni], acc[mi][ni], 0, 0, 0);
+    }
+    if (chunk_end) {   // every wave done with the old halo: stage the next chunk's and its first weights
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      issue_halo();
+      issue_b(sl ^ 1);
+    }
+  };
+  for (int ks = 0; ks < nk; ks += 2) {
+    step(ks, std::integral_constant<int, 0>{});
+    if (ks + 1 < nk) step(ks + 1, std::integral_constant<int, 1>{});
+  }
+  __syncthreads();   // the last fragment reads are done before the epilogue reuses the LDS
+  conv_epilogue<BM, BN, NT, WGM, WGN, uint16_t, true>(a, ph, acc, smem, tid, m0, n0, mt, hn, hh0, hw0);
+}
+
 // ---- the producer's BN-apply fused into a 1x1 consumer, register-staged ----------------------------
 // conv1x1_apply_kernel: pro-3 launches (ConvArgs::pro 3: x = the producer BN's input z, pz its
 // residual) of a 1x1 / stride-1 conv whose Kout (64 / 128 / 256) is ONE output tile column, so every
@@ -1137,6 +1315,10 @@ extern "C" hipError_t dlmpi_conv1x1_apply(const ConvArgs* a, int bm, hipStream_t
   return hipGetLastError();
 }
 
+// 256 x 128 halo tiles on conv_halo_pipe_kernel (dlmpi_set_halo_pipe(0): the single-stage kernel, A/B)
+static int g_halo_pipe = 1;
+extern "C" void dlmpi_set_halo_pipe(int on) { g_halo_pipe = on; }
+
 // pipe != 0: the launch runs the pipelined kernel (tile bm x bn must be one of launch_pipe's)
 extern "C" hipError_t dlmpi_conv_igemm_ex(const ConvArgs* a_in, int bm, int bn, int pipe, hipStream_t s) {
   int maxt = 0, tiles = 0, maxk = 0;
@@ -1174,8 +1356,10 @@ extern "C" hipError_t dlmpi_conv_igemm_ex(const ConvArgs* a_in, int bm, int bn, 
     else if (bm == 128 && bn == 64) hipLaunchKernelGGL((conv_igemm_kernel<128, 64, false, 2, 0, uint16_t, true>), grid, dim3(256), 0, s, *a);
     // 256-pixel tiles: per-wave 64 x 64 (4 x 1 waves) / 128 x 64 (2 x 2): half the LDS reads per MFMA
     else if (bm == 256 && bn == 64) hipLaunchKernelGGL((conv_igemm_kernel<256, 64, false, 4, 0, uint16_t, true>), grid, dim3(256), 0, s, *a);
-    else if (bm == 256 && bn == 128) hipLaunchKernelGGL((conv_igemm_kernel<256, 128, false, 2, 0, uint16_t, true>), grid, dim3(256), 0, s, *a);
-    else return hipErrorInvalidValue;
+    else if (bm == 256 && bn == 128) {
+      if (g_halo_pipe && ab.splitk == 1) hipLaunchKernelGGL((conv_halo_pipe_kernel<256, 128, 2>), grid, dim3(256), 0, s, *a);
+      else hipLaunchKernelGGL((conv_igemm_kernel<256, 128, false, 2, 0, uint16_t, true>), grid, dim3(256), 0, s, *a);
+    } else return hipErrorInvalidValue;
     return hipGetLastError();
   }
   if (a->pro != 0 && (a->pro != 3 || a->C < 64 || a->C % 64 != 0)) return hipErrorInvalidValue;

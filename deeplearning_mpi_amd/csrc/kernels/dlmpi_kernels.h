@@ -258,6 +258,7 @@ struct Wgrad3Args {
 
 extern "C" {
 // conv / gemm
+void dlmpi_set_halo_pipe(int on);   // 256 x 128 halo tiles on the weight-double-buffered kernel (A/B)
 hipError_t dlmpi_conv_igemm(const dlmpi::ConvArgs* a, int bm, int bn, hipStream_t s);
 // pipe = 1: the pipelined 8-wave kernel (tiles 256x256, 256x128, 128x256, 256x64, 512x64; bf16,
 // C % 64 == 0, no prologue / halo / split); pipe = 0: dlmpi_conv_igemm

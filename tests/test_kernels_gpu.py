@@ -394,6 +394,51 @@ def test_conv3x3_halo_tiles(shape):
     assert _rel(h[3], g[3]) < 1e-3
 
 
+HALO_PIPE_SHAPES = [
+    # N, H, W, Cin, Cout, x channel stride / offset: shapes on 256 x 128 halo tiles (Cout >= 256)
+    (2, 16, 16, 64, 256, None, 0),        # one 64-channel chunk: 9 K-steps (odd)
+    (2, 14, 14, 256, 256, None, 0),       # ResNet layer 3, 4 chunks
+    (1, 28, 30, 128, 384, None, 0),       # ragged tiles, 3 output tile columns
+    (2, 9, 37, 64, 256, 192, 64),         # x a channel slice of a concat buffer
+    (1, 32, 32, 512, 512, None, 0),       # UNet bottleneck-like, 8 chunks; dgrad on 256 x 128 too
+    (2, 4, 4, 512, 512, None, 0),         # tiny grid: split-K keeps the single-stage kernel
+]
+
+
+@pytest.mark.parametrize("shape", HALO_PIPE_SHAPES, ids=lambda s: "x".join(str(v) for v in s[:5]))
+def test_halo_pipe_bit_identical(shape):
+    """conv_halo_pipe_kernel (the 256 x 128 halo tile with a double-buffered weight tile) against the
+    single-stage halo kernel: same K order and epilogue, so forward output + BN statistics and the data
+    gradient + fused BN-backward partials are bit-identical."""
+    nb, _ = _be()
+    N, H, W, Cin, K, ldx, xoff = shape
+    x, _ = _act(N, H, W, Cin, ld=ldx, off=xoff)
+    w = (torch.randn(K, 3, 3, Cin, device=DEV) / (9 * Cin) ** 0.5).to(torch.bfloat16)
+    wT = w.permute(3, 1, 2, 0).contiguous()
+    dy, _ = _act(N, H, W, K)
+    z, _ = _act(N, H, W, Cin)
+    sc, sh = torch.rand(Cin, device=DEV) + 0.5, torch.randn(Cin, device=DEV) * 0.5
+    out = {}
+    nb.C.set_conv_halo(2)   # halo tiles on any grid
+    try:
+        for on in (1, 0):
+            nb.C.set_halo_pipe(on)
+            y = _empty(N, H, W, K)
+            mt = nb.conv_mtiles(N, H, W, Cin, K, 3, 3, 1, 1)
+            st = torch.zeros(mt, 2, K, device=DEV)
+            nb.conv_fwd(x, w, K, 3, 3, 1, 1, y, stats=st)
+            assert nb.C.conv_halo_last()
+            dx = _empty(N, H, W, Cin)
+            part = nb.conv_dgrad(dy, wT, Cin, 3, 3, 1, 1, dx, fuse=BwdFuse(None, z, None, sc, sh))
+            torch.cuda.synchronize()
+            out[on] = (y.buf.clone(), st.clone(), dx.buf.clone(), part.clone())
+    finally:
+        nb.C.set_halo_pipe(1)
+        nb.C.set_conv_halo(-1)
+    for a, b in zip(out[1], out[0]):
+        assert torch.equal(a, b)
+
+
 CONV3_STREAM_SHAPES = [
     # N, H, W, x channel stride / offset, y channel stride / offset
     (2, 16, 16, None, 0, None, 0),      # one 8 x 16 tile per 8 rows
