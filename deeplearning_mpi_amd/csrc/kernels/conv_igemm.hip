@@ -933,7 +933,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 #pragma unroll
   for (int i = 0; i < BL; ++i)
     if (n0 + lrow + RP * i < a.Kout) b_okm |= 1u << i;
-  const bool b_all = b_okm == (1u << BL) - 1;
 
   const int C = a.C;
   const int NTAP = ph.Tr * ph.Ts;
@@ -974,7 +973,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     const int64_t boff = (int64_t)wtC2 + 2 * c_cur;
 #pragma unroll
     for (int i = 0; i < BL; ++i) {
-      const char* src = (b_all || ((b_okm >> i) & 1)) ? b_base + i * b_step + boff : zp;
+      const char* src = ((b_okm >> i) & 1) ? b_base + i * b_step + boff : zp;
       glds16(src, Bs + (RP * i + 8 * wid) * 128);
     }
   };

@@ -24,6 +24,8 @@ order.  Consequences (MI355X-first design):
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.nn as nn
 
@@ -233,7 +235,7 @@ class ParamArena:
         """Called by a model right after registering its first layer's compute copies (and derived
         layouts): those are recast on the current stream, everything registered later on the side
         stream (``refresh``).  Only the first call counts."""
-        if self._cast_split is None:
+        if self._cast_split is None and os.environ.get("DLMPI_SPLIT_CAST", "1") != "0":   # (0: one launch, A/B)
             self._cast_split = (len(self._entries), len(self.post_refresh))
 
     def get_compute(self, handle) -> torch.Tensor:
