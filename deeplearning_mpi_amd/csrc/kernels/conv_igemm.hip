@@ -927,12 +927,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   const int ti = (int)fdiv((uint32_t)rem, a.fd_tilesw);
   const int hh0 = ti * a.th, hw0 = (rem - ti * a.tiles_w) * a.tw;
 
-  const char* b_base = reinterpret_cast<const char*>(a.w) + 2 * ((int64_t)(n0 + lrow) * a.ldw + 8 * jc);
-  const int64_t b_step = (int64_t)2 * RP * a.ldw;
+  // weight pieces: a wave-uniform base (tile column, tap, chunk) + a per-lane 32-bit offset, so the
+  // DMA takes the scalar-base address form (no 64-bit vector arithmetic per piece)
+  const char* w_col = reinterpret_cast<const char*>(a.w) + (int64_t)2 * n0 * a.ldw;
+  const uint32_t b_lane = 2u * ((uint32_t)lrow * (uint32_t)a.ldw + 8u * (uint32_t)jc);
+  const uint32_t b_step = 2u * RP * (uint32_t)a.ldw;
   uint32_t b_okm = 0;
 #pragma unroll
   for (int i = 0; i < BL; ++i)
     if (n0 + lrow + RP * i < a.Kout) b_okm |= 1u << i;
+  const bool b_all = __builtin_amdgcn_readfirstlane(__builtin_amdgcn_ballot_w64(b_okm != (1u << BL) - 1) == 0);
 
   const int C = a.C;
   const int NTAP = ph.Tr * ph.Ts;
@@ -954,14 +958,29 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   }
   const char* xlane = reinterpret_cast<const char*>(a.x) + 2 * ((int64_t)a.xoff + 8 * jc);
 
-  int t_cur = 0, c_cur = 0, wtC2 = 0, toff = 0;
-  auto tap_setup = [&](int t) {
-    const int tr = (int)fdiv((uint32_t)t, ph.fdTs);
-    const int ts = t - tr * ph.Ts;
-    const int dh = ph.dh0 + tr * ph.dhs, dw = ph.dw0 + ts * ph.dws;
-    const int wt = (ph.wr0 + tr * ph.wrs) * a.S + (ph.ws0 + ts * ph.wss);
-    wtC2 = wt * C * 2;
-    toff = (dh + 1) * hwd + (dw + 1);
+  // the tap walk (tap t = (tr, ts) of a Tr x Ts window, chunk-major): halo-row offset and weight-tap
+  // byte offset advanced by per-tap deltas instead of recomputed from t
+  const int toff0 = (ph.dh0 + 1) * hwd + (ph.dw0 + 1);
+  const int wt0 = (ph.wr0 * a.S + ph.ws0) * C * 2;
+  const int dto_s = ph.dws, dwt_s = ph.wss * C * 2;                       // next ts
+  const int dto_r = ph.dhs * hwd - (ph.Ts - 1) * ph.dws;                  // next tr (ts back to 0)
+  const int dwt_r = (ph.wrs * a.S - (ph.Ts - 1) * ph.wss) * C * 2;
+  int t_cur = 0, ts_cur = 0, c_cur = 0, wtC2 = wt0, toff = toff0;
+  auto tap_next = [&]() {   // (t_cur, ts_cur, toff, wtC2) -> the next K-step's tap
+    if (++t_cur == NTAP) {
+      t_cur = 0;
+      ts_cur = 0;
+      c_cur += 64;
+      toff = toff0;
+      wtC2 = wt0;
+    } else if (++ts_cur == ph.Ts) {
+      ts_cur = 0;
+      toff += dto_r;
+      wtC2 += dwt_r;
+    } else {
+      toff += dto_s;
+      wtC2 += dwt_s;
+    }
   };
   auto issue_halo = [&]() {
     const char* xb = xlane + 2 * c_cur;
@@ -970,11 +989,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   };
   auto issue_b = [&](int slot) {
     char* Bs = smem + A_BYTES + slot * B_BYTES;
-    const int64_t boff = (int64_t)wtC2 + 2 * c_cur;
+    const char* wb = w_col + wtC2 + 2 * c_cur;
+    if (b_all) {
 #pragma unroll
-    for (int i = 0; i < BL; ++i) {
-      const char* src = ((b_okm >> i) & 1) ? b_base + i * b_step + boff : zp;
-      glds16(src, Bs + (RP * i + 8 * wid) * 128);
+      for (int i = 0; i < BL; ++i) glds16(wb + (b_lane + i * b_step), Bs + (RP * i + 8 * wid) * 128);
+    } else {
+#pragma unroll
+      for (int i = 0; i < BL; ++i)
+        glds16(((b_okm >> i) & 1) ? wb + (b_lane + i * b_step) : zp, Bs + (RP * i + 8 * wid) * 128);
     }
   };
 
@@ -996,7 +1018,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   const int sw = fr & 7;   // (r & 7) of every B fragment row of this lane
 
   if (nk > 0) {
-    tap_setup(0);
     issue_halo();
     issue_b(0);
   }
@@ -1005,16 +1026,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
-    const int tcur = toff;
+    // this tap's A fragment addresses for K-half 0; K-half 1 flips chunk bit 2 = address bit 6
+    // ((4 + fg) ^ s == (fg ^ s) ^ 4 for fg < 4)
+    int a_addr[TM];
+#pragma unroll
+    for (int mi = 0; mi < TM; ++mi) {
+      const int r = hb[mi] + toff;
+      a_addr[mi] = r * 128 + ((fg ^ (r & 7)) << 4);
+    }
     const bool more = ks + 1 < nk;
     const bool chunk_end = more && t_cur + 1 == NTAP;
-    if (more) {   // the next K-step's tap (and chunk)
-      if (++t_cur == NTAP) {
-        t_cur = 0;
-        c_cur += 64;
-      }
-      tap_setup(t_cur);
-    }
+    if (more) tap_next();   // the next K-step's tap (and chunk)
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
       const int ch = kk * 4 + fg;
@@ -1023,10 +1045,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
       for (int ni = 0; ni < TN; ++ni)
         bfr[ni] = *reinterpret_cast<const bf16x8*>(smem + b_row0 + sl * B_BYTES + ni * 16 * 128 + ((ch ^ sw) << 4));
 #pragma unroll
-      for (int mi = 0; mi < TM; ++mi) {
-        const int r = hb[mi] + tcur;
-        af[mi] = *reinterpret_cast<const bf16x8*>(smem + r * 128 + ((ch ^ (r & 7)) << 4));
-      }
+      for (int mi = 0; mi < TM; ++mi)
+        af[mi] = *reinterpret_cast<const bf16x8*>(smem + (kk ? (a_addr[mi] ^ 64) : a_addr[mi]));
       if (kk == 0 && more && !chunk_end) {
         issue_b(sl ^ 1);
         asm volatile("" ::: "memory");
