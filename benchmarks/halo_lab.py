@@ -11,10 +11,13 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 import torch  # noqa: E402
 
-SHAPES = [  # H, Cin, Cout at 512^2 input (scale 2: 1024^2)
+SHAPES = [  # H, Cin, Cout at 512^2 input (scale 2: 1024^2); 256 x 128 halo tiles
     (128, 128, 256), (128, 256, 256), (128, 768, 256),
     (64, 256, 512), (64, 512, 512), (64, 1536, 512),
     (32, 512, 1024), (32, 1024, 1024),
+]
+SHAPES_SMALL = [  # 128 x 128 (128-channel outputs) and 256 x 64 (64-channel) halo tiles
+    (256, 64, 128), (256, 128, 128), (256, 384, 128), (512, 192, 64),
 ]
 
 
@@ -24,14 +27,17 @@ def main():
     ap.add_argument("--scale", type=int, default=1)
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--modes", default="1,0", help="set_halo_pipe values to compare (first = the candidate)")
+    ap.add_argument("--small", type=int, default=0, help="1: the 128 x 128 / 256 x 64 halo shapes instead")
     a = ap.parse_args()
+    modes = [int(v) for v in a.modes.split(",")]
     from deeplearning_mpi_amd.ops.act import Act
     from deeplearning_mpi_amd.ops.backend import NativeBackend
 
     be = NativeBackend("cuda")
     dev = "cuda"
-    tot = {0: 0.0, 1: 0.0}
-    for H0, Cin, K in SHAPES:
+    tot = {m: 0.0 for m in modes}
+    for H0, Cin, K in (SHAPES_SMALL if a.small else SHAPES):
         H = H0 * a.scale
         N = a.n
         x = Act(torch.randn(N * H * H, Cin, device=dev).to(torch.bfloat16), N, H, H, Cin)
@@ -44,9 +50,9 @@ def main():
         fns = {"fwd": lambda: be.conv_fwd(x, w, K, 3, 3, 1, 1, y, stats=st),
                "dgrad": lambda: be.conv_dgrad(dy, wT, Cin, 3, 3, 1, 1, dx)}
         for ps, fn in fns.items():
-            best = {0: 1e9, 1: 1e9}
+            best = {m: 1e9 for m in modes}
             for r in range(a.rounds):
-                for on in ((1, 0) if r % 2 == 0 else (0, 1)):
+                for on in (modes if r % 2 == 0 else modes[::-1]):
                     be.C.set_halo_pipe(on)
                     fn()
                     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -58,12 +64,13 @@ def main():
                     best[on] = min(best[on], e0.elapsed_time(e1) * 1000 / a.iters)
             flop = 2.0 * N * H * H * K * 9 * Cin
             halo = be.C.conv_halo_last()
-            print(f"{N}x{H}^2 {Cin}->{K} {ps:5s} halo={halo} pipe {best[1]:8.1f} us ({flop / best[1] / 1e6:6.0f} TF/s)"
-                  f"  single {best[0]:8.1f} us ({flop / best[0] / 1e6:6.0f} TF/s)  {best[1] / best[0]:.3f}", flush=True)
-            tot[0] += best[0]
-            tot[1] += best[1]
+            cols = "  ".join(f"mode {m}: {best[m]:8.1f} us ({flop / best[m] / 1e6:5.0f} TF/s)" for m in modes)
+            print(f"{N}x{H}^2 {Cin}->{K} {ps:5s} halo={halo}  {cols}  {best[modes[0]] / best[modes[-1]]:.3f}", flush=True)
+            for m in modes:
+                tot[m] += best[m]
     be.C.set_halo_pipe(1)
-    print(f"total pipe {tot[1]:.1f} us single {tot[0]:.1f} us ratio {tot[1] / tot[0]:.3f}")
+    print("total " + "  ".join(f"mode {m}: {tot[m]:.1f} us" for m in modes) +
+          f"  ratio {tot[modes[0]] / tot[modes[-1]]:.3f}")
 
 
 if __name__ == "__main__":

@@ -420,6 +420,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BM * BN <= 
     }
   }
   int toff = 0;                                        // HALO: halo-row offset of the current tap
+  int ts_cur = 0;                                      // HALO: column of the current tap
   bool need_halo = true;
   auto tap_setup_halo = [&](int t) {
     const int tr = (int)fdiv((uint32_t)t, ph.fdTs);
@@ -428,6 +429,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BM * BN <= 
     const int wt = (ph.wr0 + tr * ph.wrs) * a.S + (ph.ws0 + ts * ph.wss);
     wtC2 = wt * C * ES;
     toff = (dh + 1) * hwd + (dw + 1);
+    ts_cur = ts;
   };
 
   auto issue = [&](int ks) {
@@ -574,13 +576,22 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BM * BN <= 
     }
   }
   auto advance = [&]() {
-    if constexpr (HALO) {   // chunk-major, tap-minor
+    if constexpr (HALO) {   // chunk-major, tap-minor; the tap offsets advance by per-tap deltas
       if (++t_cur == NTAP) {
         t_cur = 0;
         c_cur += BK;
         need_halo = true;
+        ts_cur = 0;
+        toff = (ph.dh0 + 1) * hwd + (ph.dw0 + 1);
+        wtC2 = (ph.wr0 * a.S + ph.ws0) * C * ES;
+      } else if (++ts_cur == ph.Ts) {
+        ts_cur = 0;
+        toff += ph.dhs * hwd - (ph.Ts - 1) * ph.dws;
+        wtC2 += (ph.wrs * a.S - (ph.Ts - 1) * ph.wss) * C * ES;
+      } else {
+        toff += ph.dws;
+        wtC2 += ph.wss * C * ES;
       }
-      tap_setup_halo(t_cur);
     } else if constexpr (!SMALLC) {
       c_cur += BK;
       if (c_cur >= C) {
@@ -621,6 +632,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BM * BN <= 
     }
     const char* As = smem;
     const char* Bs = As + A_BYTES;
+    // HALO: this tap's A fragment addresses for K-half 0 (K-half 1 flips address bit 6:
+    // (4 + fg) ^ s == (fg ^ s) ^ 4 for fg < 4)
+    int a_addr[HALO ? TM : 1];
+    if constexpr (HALO) {
+#pragma unroll
+      for (int mi = 0; mi < TM; ++mi) {
+        const int r = hb[mi] + toff;
+        a_addr[mi] = r * 128 + ((fg ^ (r & 7)) << 4);
+      }
+    }
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
       typedef typename std::conditional<sizeof(T) == 2, bf16x8, f32x4>::type frag_t;
@@ -628,10 +649,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BM * BN <= 
       const int ch = kk * 4 + fg;
 #pragma unroll
       for (int mi = 0; mi < TM; ++mi) {
-        int r;
-        if constexpr (HALO) r = hb[mi] + toff;
-        else r = wm * WM + mi * 16 + fr;
-        af[mi] = *reinterpret_cast<const frag_t*>(As + r * 128 + ((ch ^ (r & 7)) << 4));
+        if constexpr (HALO) {
+          af[mi] = *reinterpret_cast<const frag_t*>(As + (kk ? (a_addr[mi] ^ 64) : a_addr[mi]));
+        } else {
+          const int r = wm * WM + mi * 16 + fr;
+          af[mi] = *reinterpret_cast<const frag_t*>(As + r * 128 + ((ch ^ (r & 7)) << 4));
+        }
       }
 #pragma unroll
       for (int ni = 0; ni < TN; ++ni) {
@@ -1334,7 +1357,9 @@ extern "C" hipError_t dlmpi_conv1x1_apply(const ConvArgs* a, int bm, hipStream_t
   return hipGetLastError();
 }
 
-// 256 x 128 halo tiles on conv_halo_pipe_kernel (dlmpi_set_halo_pipe(0): the single-stage kernel, A/B)
+// 256 x 128 halo tiles on conv_halo_pipe_kernel (dlmpi_set_halo_pipe(0): the single-stage kernel, A/B).
+// The 128 x 128 / 256 x 64 halo tiles stay single-stage: on the pipelined kernel (2 blocks per CU instead
+// of 3) they measured 8 % slower (profiles/r6_halo_pipe/lab_small.log).
 static int g_halo_pipe = 1;
 extern "C" void dlmpi_set_halo_pipe(int on) { g_halo_pipe = on; }
 
