@@ -483,6 +483,16 @@ static bool c8_shape(int64_t M, int C, int K, int R, int S, int stride, int pad,
   G = dlmpi_conv3x3_c8_blocks(M);
   return true;
 }
+// the ResNet stem on its 2x2 space-to-depth image (4x4 / s1 / p0, 16 channels -> 64): conv_small.hip
+static int g_c16_on = 1;    // dlmpi_ext set_conv_c16 (A/B)
+static int g_c16_ran = 0;   // 1 if the last conv2d_fwd ran it
+static bool c16_shape(int N, int H, int W, int C, int K, int R, int S, int stride, int pad, int pro, int f32, int& G) {
+  if (!g_c16_on || C != 16 || K != 64 || R != 4 || S != 4 || stride != 1 || pad != 0 || H < 4 || (W - 3) % 16 ||
+      W < 19 || pro || f32)
+    return false;
+  G = dlmpi_conv4x4_c16_blocks((int64_t)N * (H - 3) * (W - 3));
+  return true;
+}
 static bool stream3x3_shape(int N, int H, int W, int C, int K, int R, int S, int stride, int pad, int pro, int f32,
                             int& th, int& tw, int& G) {
   if (R != 3 || S != 3 || stride != 1 || pad != 1 || pro != 0 || f32) return false;
@@ -652,6 +662,23 @@ static int conv2d_fwd_impl(const at::Tensor& x, int N, int H, int W, int C, int 
         check(dlmpi_conv3x3_c8(a.x, ldx, xoff, N, H, W, a.w, a.bias, a.y, ldy, yoff, a.stats, G, cur_stream()),
               "conv2d_fwd (8-channel 3x3)");
         g_c8_ran = 1;
+        if (fin != nullptr) run_fin_after(*stats, G, K, fin);
+        return G;
+      }
+    }
+  }
+  g_c16_ran = 0;
+  {  // the ResNet stem (space-to-depth image, 16 channels -> 64, 4x4 taps)
+    int G;
+    if (bm_req <= 0 && bn_req <= 0 && c16_shape(N, H, W, C, K, R, S, stride, pad, pro, a.f32, G)) {
+      const bool ok = !res.has_value() && !scale.has_value() && !relu && a.kvalid == K && ldx % 8 == 0 &&
+                      xoff % 8 == 0 && ldy % 8 == 0 && yoff % 8 == 0 && (int64_t)N * H * W * ldx < (1ll << 31) &&
+                      (int64_t)N * P * Q * ldy < (1ll << 31) && y.scalar_type() == at::kBFloat16 && a.ldw == 256;
+      if (ok) {
+        if (a.stats && stats->size(0) < G) throw std::runtime_error("conv2d_fwd: stats buffer too small");
+        check(dlmpi_conv4x4_c16(a.x, ldx, xoff, N, H, W, a.w, a.bias, a.y, ldy, yoff, a.stats, G, cur_stream()),
+              "conv2d_fwd (stem 4x4 x 16 channels)");
+        g_c16_ran = 1;
         if (fin != nullptr) run_fin_after(*stats, G, K, fin);
         return G;
       }
@@ -883,6 +910,7 @@ int conv2d_fwd_mtiles_pro(int N, int H, int W, int C, int K, int R, int S, int s
   // fails the forward takes the tiled path into the same buffer
   int G, th, tw;
   if (bm_req <= 0 && c8_shape((int64_t)N * H * W, C, K, R, S, stride, pad, W, pro, f32, G)) return std::max(G, general);
+  if (bm_req <= 0 && c16_shape(N, H, W, C, K, R, S, stride, pad, pro, f32, G)) return std::max(G, general);
   if (bm_req <= 0 && stream1x1_shape((int64_t)N * P * Q, C, K, R, S, stride, pad, pro, f32, bm, bn, G))
     return std::max(G, general);
   if (bm_req <= 0 && stream3x3_shape(N, H, W, C, K, R, S, stride, pad, pro, f32, th, tw, G)) return std::max(G, general);
@@ -1768,6 +1796,8 @@ void register_ops(pybind11::module& m) {
   m.def("head1x1_on", []() { return g_head_on; });
   m.def("conv1x1_head_affine", &conv1x1_head_affine);
   m.def("set_conv_c8", [](int v) { g_c8_on = v; });
+  m.def("set_conv_c16", [](int v) { g_c16_on = v; });
+  m.def("conv_c16_last", []() { return g_c16_ran; });
   m.def("set_convT_stream", [](int v) { g_convT_stream = v; });
   m.def("convT_stream_last", []() { return g_convT_stream_ran; });
   m.def("conv_c8_last", []() { return g_c8_ran; });

@@ -18,26 +18,41 @@
 
 namespace dlmpi {
 
-__global__ __launch_bounds__(256) void conv3x3_c8_kernel(const uint16_t* __restrict__ x, int ldx, int xoff, int N,
-                                                         int H, int W, const uint16_t* __restrict__ w,
-                                                         const float* __restrict__ bias, uint16_t* __restrict__ y,
-                                                         int ldy, int yoff, float* __restrict__ stats) {
-  constexpr int GP = 2;   // 16-pixel groups per wave iteration
-  // per wave: the 64 output pixels of an iteration, 128 B each, 16-B chunks XOR-swizzled by (pixel & 7)
+// The same scheme, generalized (conv_small_kernel<CIN, TR, TS, PAD, GP>): a TR x TS / stride-1 / pad-PAD
+// convolution of a CIN-channel input (CIN 8 or 16) into 64 channels.  K index = tap * CIN + channel;
+// a lane group supplies 8 channels of one tap (CIN / 8 lane groups per tap, 32 / CIN taps per K
+// step).  Instances:
+//   <8, 3, 3, 1, 2>  the UNet input conv (3 K steps, taps 9-11 zero);
+//   <16, 4, 4, 0, 1> the ResNet stem as the 4x4 stride-1 conv over its 2x2 space-to-depth image
+//                    (models/engine.py S2DConvUnit: 16 taps x 16 channels = 8 K steps, the padding is
+//                    in the image, so no bounds checks).  Through the generic GEMM (256 x 64 tiles of
+//                    16-B-piece taps) it ran at 1.5 TB/s of output: 268 us at bs 256 for a 411 MB store.
+template <int CIN, int TR, int TS, int PAD, int GP>
+__global__ __launch_bounds__(256) void conv_small_kernel(const uint16_t* __restrict__ x, int ldx, int xoff, int N,
+                                                        int H, int W, int P, int Q, const uint16_t* __restrict__ w,
+                                                        const float* __restrict__ bias, uint16_t* __restrict__ y,
+                                                        int ldy, int yoff, float* __restrict__ stats) {
+  constexpr int LPT = CIN / 8;                    // lane groups per tap
+  constexpr int TPK = 4 / LPT;                    // taps per K step
+  constexpr int NTAP = TR * TS, KTOT = NTAP * CIN;
+  constexpr int KS = (NTAP + TPK - 1) / TPK;      // K steps of 32
+  static_assert(CIN == 8 || CIN == 16, "8 or 16 input channels");
+  // per wave: the 16 GP output pixels of an iteration, 128 B each, 16-B chunks XOR-swizzled by (pixel & 7)
   __shared__ __attribute__((aligned(16))) char tile[4][GP * 16 * 128];
   __shared__ float red[4][2][64];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int g = lane >> 4, i = lane & 15;
   char* const wt = tile[wid];
-  // weights: A operand of channel tile ct, K step k: row 16 ct + i, K 8g..8g+7 = tap 4k + g, channels 0..7
-  bf16x8 wf[4][3];
+  // weights: A operand of channel tile ct, K step k: row 16 ct + i, K 32 k + 8 g .. + 7 = tap TPK k + g / LPT,
+  // channels 8 (g % LPT) ..
+  bf16x8 wf[4][KS];
 #pragma unroll
   for (int ct = 0; ct < 4; ++ct)
 #pragma unroll
-    for (int k = 0; k < 3; ++k) {
-      const int tap = 4 * k + g;
+    for (int k = 0; k < KS; ++k) {
+      const int tap = TPK * k + g / LPT;
       u32x4 v = u32x4{0u, 0u, 0u, 0u};
-      if (tap < 9) v = *reinterpret_cast<const u32x4*>(w + (16 * ct + i) * 72 + tap * 8);
+      if (tap < NTAP) v = *reinterpret_cast<const u32x4*>(w + (16 * ct + i) * KTOT + tap * CIN + 8 * (g % LPT));
       wf[ct][k] = __builtin_bit_cast(bf16x8, v);
     }
   float bv[4][4];
@@ -46,34 +61,36 @@ __global__ __launch_bounds__(256) void conv3x3_c8_kernel(const uint16_t* __restr
 #pragma unroll
     for (int r = 0; r < 4; ++r) bv[ct][r] = bias ? bias[16 * ct + 4 * g + r] : 0.f;
   float ssum[4][4] = {}, ssq[4][4] = {};
-  // tap (4k + g) of this lane: row / column offsets
-  int dr[3], ds[3];
-  bool tv[3];
+  // this lane's tap of each K step: row / column offsets and channel chunk
+  int dr[KS], ds[KS];
+  bool tv[KS];
 #pragma unroll
-  for (int k = 0; k < 3; ++k) {
-    const int tap = 4 * k + g;
-    tv[k] = tap < 9;
-    dr[k] = tap / 3 - 1;
-    ds[k] = tap % 3 - 1;
+  for (int k = 0; k < KS; ++k) {
+    const int tap = TPK * k + g / LPT;
+    tv[k] = tap < NTAP;
+    dr[k] = tap / TS - PAD;
+    ds[k] = tap % TS - PAD;
   }
-  const uint32_t uW = W, uH = H;
-  const uint32_t ngroups = (uint32_t)((int64_t)N * H * W / 16);   // host: N H W < 2^31
+  const int cofs = xoff + 8 * (g % LPT);
+  const uint32_t uQ = Q, uP = P;
+  const uint32_t ngroups = (uint32_t)((int64_t)N * P * Q / 16);   // host: N P Q < 2^31, Q % 16 == 0
   const uint32_t nwaves = gridDim.x * 4;
   for (uint32_t g0 = (blockIdx.x * 4 + wid) * GP; g0 < ngroups; g0 += nwaves * GP) {
-    bf16x8 xf[GP][3];
+    bf16x8 xf[GP][KS];
 #pragma unroll
     for (int q = 0; q < GP; ++q) {
       const uint32_t grp = g0 + q;
-      const uint32_t row = grp * 16 / uW;                 // image row n * H + h of the 16-pixel group
-      const int wc = (int)(grp * 16 - row * uW) + i;
-      const uint32_t n = row / uH;
-      const int h = (int)(row - n * uH);
+      const uint32_t row = grp * 16 / uQ;                 // output row n * P + p of the 16-pixel group
+      const int wc = (int)(grp * 16 - row * uQ) + i;
+      const uint32_t n = row / uP;
+      const int h = (int)(row - n * uP);
 #pragma unroll
-      for (int k = 0; k < 3; ++k) {
+      for (int k = 0; k < KS; ++k) {
         const int hh = h + dr[k], ww = wc + ds[k];
         u32x4 v = u32x4{0u, 0u, 0u, 0u};
-        if (grp < ngroups && tv[k] && (unsigned)hh < uH && (unsigned)ww < uW)
-          v = *reinterpret_cast<const u32x4*>(x + ((int64_t)(n * uH + hh) * W + ww) * ldx + xoff);
+        const bool in = PAD == 0 || ((unsigned)hh < (unsigned)H && (unsigned)ww < (unsigned)W);
+        if (grp < ngroups && tv[k] && in)
+          v = *reinterpret_cast<const u32x4*>(x + ((int64_t)((int)n * H + hh) * W + ww) * ldx + cofs);
         xf[q][k] = __builtin_bit_cast(bf16x8, v);
       }
     }
@@ -84,7 +101,7 @@ __global__ __launch_bounds__(256) void conv3x3_c8_kernel(const uint16_t* __restr
       for (int ct = 0; ct < 4; ++ct) {
         acc[ct] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int k = 0; k < 3; ++k) acc[ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[ct][k], xf[q][k], acc[ct], 0, 0, 0);
+        for (int k = 0; k < KS; ++k) acc[ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[ct][k], xf[q][k], acc[ct], 0, 0, 0);
       }
       const bool live = g0 + q < ngroups;
       const int px = q * 16 + i;
@@ -161,8 +178,25 @@ extern "C" hipError_t dlmpi_conv3x3_c8(const void* x, int ldx, int xoff, int N, 
                                        hipStream_t s) {
   if (W % 16 || ldx % 8 || xoff % 8 || ldy % 8 || yoff % 8 || G <= 0 || (int64_t)N * H * W >= (1ll << 31))
     return hipErrorInvalidValue;
-  hipLaunchKernelGGL(conv3x3_c8_kernel, dim3((unsigned)G), dim3(256), 0, s, static_cast<const uint16_t*>(x), ldx,
-                     xoff, N, H, W, static_cast<const uint16_t*>(w), bias, static_cast<uint16_t*>(y), ldy, yoff,
-                     stats);
+  hipLaunchKernelGGL((conv_small_kernel<8, 3, 3, 1, 2>), dim3((unsigned)G), dim3(256), 0, s,
+                     static_cast<const uint16_t*>(x), ldx, xoff, N, H, W, H, W, static_cast<const uint16_t*>(w), bias,
+                     static_cast<uint16_t*>(y), ldy, yoff, stats);
+  return hipGetLastError();
+}
+
+// The ResNet stem on its space-to-depth image: 4 x 4 taps, 16 channels, no padding (input U x V, output
+// (U - 3) x (V - 3)).  Blocks: the same rule as the 8-channel kernel (~16 pixel groups per block).
+extern "C" int dlmpi_conv4x4_c16_blocks(int64_t pixels) { return dlmpi_conv3x3_c8_blocks(pixels); }
+
+extern "C" hipError_t dlmpi_conv4x4_c16(const void* x, int ldx, int xoff, int N, int U, int V, const void* w,
+                                        const float* bias, void* y, int ldy, int yoff, float* stats, int G,
+                                        hipStream_t s) {
+  const int P = U - 3, Q = V - 3;
+  if (P <= 0 || Q % 16 || ldx % 8 || xoff % 8 || ldy % 8 || yoff % 8 || G <= 0 ||
+      (int64_t)N * U * V * ldx >= (1ll << 31) || (int64_t)N * P * Q * ldy >= (1ll << 31))
+    return hipErrorInvalidValue;
+  hipLaunchKernelGGL((conv_small_kernel<16, 4, 4, 0, 1>), dim3((unsigned)G), dim3(256), 0, s,
+                     static_cast<const uint16_t*>(x), ldx, xoff, N, U, V, P, Q, static_cast<const uint16_t*>(w), bias,
+                     static_cast<uint16_t*>(y), ldy, yoff, stats);
   return hipGetLastError();
 }

@@ -282,6 +282,9 @@ int dlmpi_wgrad3_plan(int Ko, int C, int* kt, int* ct);
 hipError_t dlmpi_wgrad3x3(const dlmpi::Wgrad3Args* a, int kt, int ct, hipStream_t s);
 int dlmpi_head1x1_ok(int C, int kv);
 int dlmpi_conv3x3_c8_blocks(int64_t pixels);
+int dlmpi_conv4x4_c16_blocks(int64_t pixels);
+hipError_t dlmpi_conv4x4_c16(const void* x, int ldx, int xoff, int N, int U, int V, const void* w, const float* bias,
+                             void* y, int ldy, int yoff, float* stats, int G, hipStream_t s);
 hipError_t dlmpi_conv3x3_c8(const void* x, int ldx, int xoff, int N, int H, int W, const void* w, const float* bias,
                             void* y, int ldy, int yoff, float* stats, int G, hipStream_t s);
 hipError_t dlmpi_head1x1(const void* x, int ldx, int xoff, int64_t M, int C, const void* w, int ldw,
