@@ -597,6 +597,63 @@ int conv2d_fwd_bn_apply(const at::Tensor& x, int N, int H, int W, int C, int ldx
   }
 }
 
+static void run_fin_after(const at::Tensor& stats, int rows, int K, const FinArgs* fin);
+static int g_c3pro_on = 1;   // dlmpi_ext set_conv3_pro (A/B): 0 = the standalone BN-apply before the conv
+// The streaming 64 -> 64 3x3 forward takes this launch with the producer's BN-apply + ReLU fused
+// (conv3x3_stream_kernel PRO): shape and operand conditions (the model asks before it defers the apply).
+static bool conv3_pro_ok(int N, int H, int W, int C, int K, int ldx, int xoff, int ldz, int zoff, int ldyapp,
+                         int yappoff) {
+  int th, tw, G;
+  return g_c3pro_on && C == 64 && K == 64 && stream3x3_shape(N, H, W, C, K, 3, 3, 1, 1, 0, 0, th, tw, G) &&
+         ldx % 8 == 0 && xoff % 8 == 0 && ldz % 8 == 0 && zoff % 8 == 0 && ldyapp % 8 == 0 && yappoff % 8 == 0 &&
+         (int64_t)H * W * std::max(ldz, ldyapp) * 2 < (1ll << 31);
+}
+// conv2d_fwd_bn of a 3x3 / s1 / p1 64 -> 64 conv whose input is the producer's pending BN-apply + ReLU
+// (no residual): x = that BN's input z, (ascale, ashift) its coefficients; the streaming kernel applies
+// them to its staged halo and stores the applied input to yapp (each pixel once).  Returns the
+// statistics rows (G), or -1 if the fused launch does not apply (the caller applies first).
+int conv3x3_fwd_bn_apply(const at::Tensor& x, int N, int H, int W, int ldx, int xoff, const at::Tensor& w,
+                         at::Tensor z, int ldz, int zoff, const c10::optional<at::Tensor>& bias, const at::Tensor& stats,
+                         const at::Tensor& ascale, const at::Tensor& ashift, at::Tensor yapp, int ldyapp, int yappoff,
+                         double count, const c10::optional<at::Tensor>& gamma, const c10::optional<at::Tensor>& beta,
+                         const c10::optional<at::Tensor>& running_mean, const c10::optional<at::Tensor>& running_var,
+                         double momentum, double eps, at::Tensor bnscale, at::Tensor bnshift,
+                         const c10::optional<at::Tensor>& save_mean, const c10::optional<at::Tensor>& save_invstd) {
+  require_gpu(x, "conv3x3_fwd_bn_apply x");
+  if (act_f32(x, "conv3x3_fwd_bn_apply") || z.scalar_type() != at::kBFloat16 || yapp.scalar_type() != at::kBFloat16 ||
+      !conv3_pro_ok(N, H, W, 64, 64, ldx, xoff, ldz, zoff, ldyapp, yappoff) || ascale.numel() < 64 ||
+      ashift.numel() < 64)
+    return -1;
+  int th, tw, G;
+  stream3x3_shape(N, H, W, 64, 64, 3, 3, 1, 1, 0, 0, th, tw, G);
+  if (stats.size(0) < G) throw std::runtime_error("conv3x3_fwd_bn_apply: stats buffer too small");
+  dlmpi::Conv3StreamArgs c = conv3_args(x, N, H, W, ldx, xoff, w, 0, z.data_ptr(), ldz, zoff, th, tw, G);
+  c.bias = optr<float>(bias);
+  c.stats = ptr<float>(stats);
+  c.psc = ptr<float>(ascale);
+  c.psh = ptr<float>(ashift);
+  c.py = ptr<uint16_t>(yapp);
+  c.ldpy = ldyapp;
+  c.pyoff = yappoff;
+  check(dlmpi_conv3x3_stream(&c, 0, cur_stream()), "conv3x3_fwd_bn_apply");
+  g_conv3_ran = 1;
+  FinArgs f{};
+  f.mode = 0;
+  f.count = count;
+  f.gamma = optr<float>(gamma);
+  f.beta = optr<float>(beta);
+  f.running_mean = optr<float>(running_mean);
+  f.running_var = optr<float>(running_var);
+  f.momentum = (float)momentum;
+  f.eps = (float)eps;
+  f.scale = ptr<float>(bnscale);
+  f.shift = ptr<float>(bnshift);
+  f.save_mean = optr<float>(save_mean);
+  f.save_invstd = optr<float>(save_invstd);
+  run_fin_after(stats, G, 64, &f);
+  return G;
+}
+
 // the BN finalize of a forward conv's statistics [rows][2][K]
 static void run_fin_after(const at::Tensor& stats, int rows, int K, const FinArgs* fin) {
   at::Tensor ws = colsum_ws(stats, rows, K);
@@ -1797,6 +1854,9 @@ void register_ops(pybind11::module& m) {
   m.def("conv1x1_head_affine", &conv1x1_head_affine);
   m.def("set_conv_c8", [](int v) { g_c8_on = v; });
   m.def("set_conv_c16", [](int v) { g_c16_on = v; });
+  m.def("set_conv3_pro", [](int v) { g_c3pro_on = v; });
+  m.def("conv3_pro_ok", &conv3_pro_ok);
+  m.def("conv3x3_fwd_bn_apply", &conv3x3_fwd_bn_apply);
   m.def("conv_c16_last", []() { return g_c16_ran; });
   m.def("set_convT_stream", [](int v) { g_convT_stream = v; });
   m.def("convT_stream_last", []() { return g_convT_stream_ran; });

@@ -50,8 +50,14 @@ __device__ __forceinline__ int c3_eoff(int r, int col) {
 // 16 x 512^2, also with a register double buffer of the next tap's fragments); the weights held in
 // registers (144 VGPRs per wave) instead of LDS: spills with the statistics epilogue, and only +6 %
 // on the plain data gradient at 512^2 (-5 % at 56^2).
-template <int MODE, bool FLIP>
+// PRO (forward only): the input is the producer BN's input z.  Once a tile's halo has landed, every
+// lane rewrites its own in-image halo pieces in LDS as bf16(relu(fma(z, psc, psh))) -- bn_apply_kernel's
+// arithmetic, bit-identical -- and stores the pieces of the tile's own pixels to py (every pixel is in
+// exactly one tile: the applied activation is written once and the standalone apply pass, a read of z
+// and a write of y, is gone); out-of-image pieces stay the zero padding.  One extra barrier per tile.
+template <int MODE, bool FLIP, bool PRO = false>
 __global__ __launch_bounds__(512) void conv3x3_stream_kernel(const Conv3StreamArgs a) {
+  static_assert(!PRO || (MODE == 0 && !FLIP), "prologue: forward only");
   constexpr int NW = 8, NT = 64 * NW, BM = 128, BN = 64;
   constexpr int WGM = 4, WGN = 2, WM = BM / WGM, WN = BN / WGN;
   constexpr int TM = WM / 16, TN = WN / 16;
@@ -172,6 +178,16 @@ __global__ __launch_bounds__(512) void conv3x3_stream_kernel(const Conv3StreamAr
   static_assert(HROWS % RP == 0 && (9 * BN) % RP == 0 && BM % RP == 0, "staging passes");
   const int img_bytes = H * W * a.ldy * 2;   // one image's output rows (host: < 2^31)
 
+  // PRO: this lane's halo pieces -- channels 8 jc .. + 7 at LDS slot (tid & 7) of row lrow + RP i
+  f32x4 psa = {}, psb = {}, pha = {}, phb = {};
+  if constexpr (PRO) {
+    psa = *reinterpret_cast<const f32x4*>(a.psc + 8 * jc);
+    psb = *reinterpret_cast<const f32x4*>(a.psc + 8 * jc + 4);
+    pha = *reinterpret_cast<const f32x4*>(a.psh + 8 * jc);
+    phb = *reinterpret_cast<const f32x4*>(a.psh + 8 * jc + 4);
+  }
+  const int py_img = PRO ? H * W * a.ldpy * 2 : 0;   // one image of the applied output (host: < 2^31)
+
   int t = blockIdx.x;   // tiles t, t + G, ...: the grid holds one block per CU
   issue_a(t, OFF_A0);
   issue_e(t, OFF_E0);
@@ -182,11 +198,42 @@ __global__ __launch_bounds__(512) void conv3x3_stream_kernel(const Conv3StreamAr
     const int offA = (it & 1) ? OFF_A1 : OFF_A0, offAn = (it & 1) ? OFF_A0 : OFF_A1;
     const int offE = Z ? ((it & 1) ? OFF_E1 : OFF_E0) : OFF_E0, offEn = Z ? ((it & 1) ? OFF_E0 : OFF_E1) : OFF_E0;
     // this tile's halo / z landed (the younger vector-memory operations of this wave are the previous
-    // tile's NSTORE row stores); every wave is done with the previous tile's buffers
-    __builtin_amdgcn_s_waitcnt(c3_vmcnt(NSTORE));
+    // tile's NSTORE row stores, and with PRO its HL applied-input stores before them); every wave is
+    // done with the previous tile's buffers
+    __builtin_amdgcn_s_waitcnt(c3_vmcnt(NSTORE + (PRO ? HL : 0)));
     c3_barrier();
     issue_a(t + a.G, offAn);   // the next tile streams in under this tile's MFMAs and epilogue
     issue_e(t + a.G, offEn);
+    if constexpr (PRO) {
+      int n, h0, w0;
+      origin(t, n, h0, w0);
+      const __amdgpu_buffer_rsrc_t pr = __builtin_amdgcn_make_buffer_rsrc(
+          reinterpret_cast<char*>(a.py) + (int64_t)n * py_img, (short)0, py_img, 0x00020000);
+#pragma unroll
+      for (int i = 0; i < HL; ++i) {
+        const int ih = h0 + hdh[i], iw = w0 + hdw[i];
+        const bool in = ((hok >> i) & 1) && (unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W;
+        u32x4* pc = reinterpret_cast<u32x4*>(smem + offA + (RP * i + lrow) * 128 + (tid & 7) * 16);
+        u32x4 q = u32x4{0u, 0u, 0u, 0u};
+        if (in) {
+          float v[8];
+          unpack8(*pc, v);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            v[e] = fmaxf(__builtin_fmaf(v[e], psa[e], pha[e]), 0.f);
+            v[e + 4] = fmaxf(__builtin_fmaf(v[e + 4], psb[e], phb[e]), 0.f);
+          }
+          q = pack8(v);
+          *pc = q;
+        }
+        // the tile's own pixels (halo line / column 1 .. th / tw): stored once; others dropped by the
+        // buffer range check (offset 2^31), so every lane issues exactly HL stores (the vmcnt above)
+        const bool own = in && hdh[i] >= 0 && hdh[i] < th && hdw[i] >= 0 && hdw[i] < tw;
+        const uint32_t off = (uint32_t)(((ih * W + iw) * a.ldpy + a.pyoff + 8 * jc) * 2);
+        __builtin_amdgcn_raw_buffer_store_b128(q, pr, own ? off : 0x80000000u, 0, 0);
+      }
+      c3_barrier();   // every wave's pieces are applied before any fragment read
+    }
 
     f32x4 acc[TM][TN];
 #pragma unroll
@@ -334,7 +381,11 @@ extern "C" hipError_t dlmpi_conv3x3_stream(const Conv3StreamArgs* a, int mode, h
   if (a->G <= 0) return hipSuccess;
   if (a->th * a->tw > 128 || (a->th + 2) * (a->tw + 2) > 192) return hipErrorInvalidValue;
   const dim3 g((unsigned)a->G), b(512);
-  if (mode == 0 && !a->flip && a->stats) hipLaunchKernelGGL((conv3x3_stream_kernel<0, false>), g, b, 0, s, *a);
+  if (mode == 0 && !a->flip && a->stats && a->psc) {
+    if (!a->psh || !a->py || a->ldpy % 8 || a->pyoff % 8 || (int64_t)a->H * a->W * a->ldpy * 2 >= (1ll << 31))
+      return hipErrorInvalidValue;
+    hipLaunchKernelGGL((conv3x3_stream_kernel<0, false, true>), g, b, 0, s, *a);
+  } else if (mode == 0 && !a->flip && a->stats) hipLaunchKernelGGL((conv3x3_stream_kernel<0, false>), g, b, 0, s, *a);
   else if (mode == 1 && !a->flip) hipLaunchKernelGGL((conv3x3_stream_kernel<1, false>), g, b, 0, s, *a);
   else if (mode == 1 && a->flip) hipLaunchKernelGGL((conv3x3_stream_kernel<1, true>), g, b, 0, s, *a);
   else if (mode == 2 && a->flip && a->stats && a->z && a->mscale && a->mshift)

@@ -221,6 +221,12 @@ struct Conv3StreamArgs {
   const float* mscale;
   const float* mshift;
   float* stats;
+  // forward with the producer's BN-apply + ReLU fused (conv3x3_stream_kernel PRO): x is the producer
+  // BN's input z; the kernel stages relu(z * psc + psh) and stores it (each pixel once) to py
+  const float* psc;
+  const float* psh;
+  uint16_t* py;
+  int ldpy, pyoff;
 };
 
 // 3x3 / stride-1 / pad-1 weight gradient by 8 x 8 output-pixel tiles (conv_wgrad3.hip): split z

@@ -145,6 +145,11 @@ FUSE_APPLY = True
 # 1024->256 103 vs 194 / 106 (107 vs 202 / 119 with a BN-output residual), profiles/r5_apply.  (With the
 # single-stage kernel only 64 channels paid: 128 lost in the step, profiles/r5_policy.)
 FUSE_APPLY_MAX_K = 256
+# A BN-apply + ReLU without residual feeding a 64 -> 64 3x3 / s1 / p1 conv (UNet level-1 DoubleConv,
+# ResNet layer-1 conv2) is computed by the streaming 3x3 kernel on its staged input tiles, which also
+# stores it once (backend conv3_fwd_bn_apply, conv3x3_stream.hip PRO): the apply pass's read of z and
+# its launch go; the stored output is what the weight gradient reads (profiles/r6_c3pro).
+FUSE_APPLY_3X3 = True
 
 # The step's last weight gradient (a unit with ``wgrad_main``: the ResNet stem, whose input needs no
 # gradient) runs on the main stream -- idle by then -- instead of queueing behind the side stream's
@@ -292,11 +297,23 @@ class ConvUnit:
 
     def can_fuse_apply(self, be, x, train: bool, save=True) -> bool:
         """True if ``fwd`` computes the pending BN-apply ``x`` inside its GEMM's operand prologue
-        (FUSE_APPLY): a 1x1 / stride-1 conv of <= FUSE_APPLY_MAX_K outputs behind a residual BN + ReLU."""
+        (FUSE_APPLY): a 1x1 / stride-1 conv of <= FUSE_APPLY_MAX_K outputs behind a residual BN + ReLU,
+        or (FUSE_APPLY_3X3) a 64 -> 64 3x3 conv behind a BN + ReLU without residual."""
+        if self._fuse3(be, x, train, save):
+            return True
         return (FUSE_APPLY and train and save and isinstance(x, PendingApply) and not x.done
                 and self.bn is not None and self.R == 1 and self.S == 1 and self.stride == 1 and self.pad == 0
                 and self.Kp <= FUSE_APPLY_MAX_K and x.relu and x.res is not None and x.mbits is not None
                 and x.C == self.Cp and hasattr(be, "conv_fwd_bn_apply") and not getattr(be, "f32", False))
+
+    def _fuse3(self, be, x, train, save) -> bool:
+        if not (FUSE_APPLY_3X3 and train and save and isinstance(x, PendingApply) and not x.done
+                and self.bn is not None and self.R == 3 and self.S == 3 and self.stride == 1 and self.pad == 1
+                and self.Cp == 64 and self.Kp == 64 and x.C == 64 and x.relu and x.res is None and x.mbits is None
+                and hasattr(be, "conv3_fwd_bn_apply") and not getattr(be, "f32", False)):
+            return False
+        ok = getattr(be, "conv3_pro_ok", None)
+        return ok is None or ok(x.z, x.y)
 
     def fwd(self, be, x, train: bool, res: Act = None, out: Act = None, save=True, defer_apply=False,
             before_res=None, lazy=False):
@@ -345,7 +362,14 @@ class ConvUnit:
             fin = (N * P * Q, bn.weight.data if bn.affine else None, bn.bias.data if bn.affine else None,
                    bn.running_mean if bn.track_running_stats else None,
                    bn.running_var if bn.track_running_stats else None, mom, bn.eps, scale, shift, mean, invstd)
-            if fuse_apply:   # the producer's BN-apply runs (and is stored) inside this GEMM
+            if fuse_apply and self.R == 3:   # the producer's BN-apply inside the streaming 3x3 kernel
+                mt = be.conv_mtiles(N, x.H, x.W, x.C, self.Kp, 3, 3, 1, 1)
+                stats = torch.empty(mt, 2, self.Kp, dtype=be.dt, device=dev)
+                self.arena.wait_buffers()
+                be.conv3_fwd_bn_apply(x, wf, self.Kp, z, self._bias_vec(), stats, *fin)
+                x.done = True
+                x = x.y
+            elif fuse_apply:   # the producer's BN-apply runs (and is stored) inside this GEMM
                 mt = be.conv_mtiles(N, x.H, x.W, x.C, self.Kp, 1, 1, 1, 0, pro=3)
                 stats = torch.empty(mt, 2, self.Kp, dtype=be.dt, device=dev)
                 self.arena.wait_buffers()

@@ -162,7 +162,8 @@ class UNet(EngineModule):
             cat = Act.empty(N, h, w, ccat, dt, dev)
             cats.append(cat)
             ua, ub = self.enc[k]
-            t, ca = ua.fwd(be, a, train, save=save)
+            # lazy: the BN-apply may run inside ub (the level-1 64 -> 64 conv: FUSE_APPLY_3X3)
+            t, ca = ua.fwd(be, a, train, save=save, lazy=train and save)
             if k == 0:   # the deeper layers' weight recast beside the 64-channel 3x3 conv (compute-bound)
                 self._arena.launch_cast()
             skip = cat.slice(self.up_ch[k], self.skip_ch[k])
@@ -194,7 +195,7 @@ class UNet(EngineModule):
                 be.upsample_fwd(a, up)
             below = a
             ua, ub = self.dec[k]
-            t, ca = ua.fwd(be, cat, train, save=save)
+            t, ca = ua.fwd(be, cat, train, save=save, lazy=train and save)
             # level 1's output is read only by the 1x1 head (forward and weight gradient): never stored
             # (the head's weight gradient rebuilds it in an operand prologue: bf16 backends only)
             head_defer = k == 0 and FUSE_HEAD_APPLY and self.fuse_bn_bwd and getattr(be, "prologue", False)

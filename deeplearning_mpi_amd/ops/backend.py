@@ -198,6 +198,25 @@ class NativeBackend:
                                    float(count), gamma, beta, rm, rv, float(momentum), float(eps), scale, shift,
                                    save_mean, save_invstd)
 
+    def conv3_pro_ok(self, z: Act, y: Act) -> bool:
+        """The fused BN-apply + streaming 3x3 launch applies to this input z / applied output y."""
+        return bool(self.C.conv3_pro_ok(z.N, z.H, z.W, z.C, 64, z.ld, z.off, y.ld, y.off, y.ld, y.off))
+
+    def conv3_fwd_bn_apply(self, xp, w, K, z: Act, bias, stats, count, gamma, beta, rm, rv, momentum, eps, scale,
+                           shift, save_mean, save_invstd):
+        """conv_fwd_bn of a 3x3 / s1 / p1 64 -> 64 conv whose input is a pending BN-apply + ReLU without
+        residual (engine.PendingApply): the streaming 3x3 kernel applies it to its staged input tiles and
+        stores it to xp.y (each pixel once) -- no separate apply pass.  Falls back to the apply pass +
+        conv_fwd_bn where the fused launch does not apply."""
+        x, y = xp.z, xp.y
+        r = self.C.conv3x3_fwd_bn_apply(x.buf, x.N, x.H, x.W, x.ld, x.off, w, z.buf, z.ld, z.off, bias, stats,
+                                        xp.scale, xp.shift, y.buf, y.ld, y.off, float(count), gamma, beta, rm, rv,
+                                        float(momentum), float(eps), scale, shift, save_mean, save_invstd)
+        if r < 0:
+            self.bn_apply(xp.z, xp.scale, xp.shift, None, True, y)
+            self.conv_fwd_bn(y, w, K, 3, 3, 1, 1, z, bias, stats, count, gamma, beta, rm, rv, momentum, eps, scale,
+                             shift, save_mean, save_invstd)
+
     def conv_fwd_bnbwd(self, x: Act, w, K, R, S, stride, pad, y: Act, fuse):
         """Forward conv producing the gradient of relu(BN(z)) (fuse = BwdFuse(None, z, None, scale,
         shift)): masked in the epilogue, BN-backward partials [tiles][2][K] returned."""
@@ -568,6 +587,11 @@ class RefBackend:
         """Reference form of the fused consumer: the pending BN-apply as its own pass, then conv_fwd_bn."""
         self.bn_apply(xp.z, xp.scale, xp.shift, xp.res, xp.relu, xp.y, mbits=xp.mbits)
         self.conv_fwd_bn(xp.y, w, K, 1, 1, 1, 0, z, bias, stats, *fin)
+
+    def conv3_fwd_bn_apply(self, xp, w, K, z: Act, bias, stats, *fin):
+        """Reference form of the fused 3x3 consumer (the engine schedule is the same on every backend)."""
+        self.bn_apply(xp.z, xp.scale, xp.shift, None, True, xp.y)
+        self.conv_fwd_bn(xp.y, w, K, 3, 3, 1, 1, z, bias, stats, *fin)
 
     def conv_fwd_bnbwd(self, x: Act, w, K, R, S, stride, pad, y: Act, fuse):
         wk = w.view(K, R, S, x.C).permute(0, 3, 1, 2).to(self.dt)
