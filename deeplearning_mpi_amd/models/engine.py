@@ -148,7 +148,9 @@ FUSE_APPLY_MAX_K = 256
 # A BN-apply + ReLU without residual feeding a 64 -> 64 3x3 / s1 / p1 conv (UNet level-1 DoubleConv,
 # ResNet layer-1 conv2) is computed by the streaming 3x3 kernel on its staged input tiles, which also
 # stores it once (backend conv3_fwd_bn_apply, conv3x3_stream.hip PRO): the apply pass's read of z and
-# its launch go; the stored output is what the weight gradient reads (profiles/r6_c3pro).
+# its launch go; the stored output is what the weight gradient reads (profiles/r6_c3pro).  Per unit
+# (ConvUnit.fuse3): the UNet level-1 DoubleConvs take it; ResNet layer 1 does not (its first block's
+# conv2 runs beside the downsample branch, where the fused kernel lost what the others gained).
 FUSE_APPLY_3X3 = True
 
 # The step's last weight gradient (a unit with ``wgrad_main``: the ResNet stem, whose input needs no
@@ -228,6 +230,7 @@ class ConvUnit:
     """conv2d / linear (+ training or folded-eval BatchNorm) (+ residual) (+ ReLU)."""
 
     wgrad_main = False   # see WGRAD_TAIL_MAIN
+    fuse3 = False        # FUSE_APPLY_3X3 for this unit (set by the model where it measured faster)
 
     def __init__(self, arena: ParamArena, conv, bn=None, relu=True, cin_pad=None, need_dgrad=True):
         self.arena, self.conv, self.bn, self.relu = arena, conv, bn, relu
@@ -307,7 +310,7 @@ class ConvUnit:
                 and x.C == self.Cp and hasattr(be, "conv_fwd_bn_apply") and not getattr(be, "f32", False))
 
     def _fuse3(self, be, x, train, save) -> bool:
-        if not (FUSE_APPLY_3X3 and train and save and isinstance(x, PendingApply) and not x.done
+        if not (FUSE_APPLY_3X3 and self.fuse3 and train and save and isinstance(x, PendingApply) and not x.done
                 and self.bn is not None and self.R == 3 and self.S == 3 and self.stride == 1 and self.pad == 1
                 and self.Cp == 64 and self.Kp == 64 and x.C == 64 and x.relu and x.res is None and x.mbits is None
                 and hasattr(be, "conv3_fwd_bn_apply") and not getattr(be, "f32", False)):

@@ -148,6 +148,9 @@ class UNet(EngineModule):
         self.dec = [u.double_conv.units(ar, cin_pad=self.up_ch[k] + self.skip_ch[k]) for k, u in enumerate(ups)]
         self.upT = [ConvTUnit(ar, u.up_sample) if self.up_sample_mode == "conv_transpose" else None for u in ups]
         self.u_last = ConvUnit(ar, self.conv_last, None, relu=False)
+        # level 1 (64 -> 64): the first conv's BN-apply inside the second conv's streaming kernel
+        self.enc[0][1].fuse3 = True
+        self.dec[0][1].fuse3 = True
 
     def _engine_forward(self, x, train, save):
         be = self._be

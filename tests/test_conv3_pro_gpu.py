@@ -16,9 +16,11 @@ pytestmark = pytest.mark.gpu
 DEV = "cuda"
 
 
-def _steps(model, make_opt, x, y, loss_fn, fused, clip=False, steps=3):
+def _steps(model, make_opt, x, y, loss_fn, fused, clip=False, steps=3, units=()):
     model.train()
     model.engine_setup(DEV)
+    for u in units(model) if units else ():
+        u.fuse3 = True
     C = model._be.C
     C.set_conv3_pro(1 if fused else 0)
     calls = {"n": 0}   # fused launches through the backend
@@ -64,6 +66,14 @@ def test_unet_fused_3x3_apply_bit_identical():
         assert torch.equal(a, b)
 
 
+def test_resnet50_default_schedule_does_not_fuse():
+    torch.manual_seed(0)
+    m = resnet50(num_classes=10).to(DEV)
+    _, _, n = _steps(m, lambda ps: SGD(ps, lr=0.05), torch.randn(2, 3, 64, 64, device=DEV),
+                     torch.randint(0, 10, (2,), device=DEV), cross_entropy, True, steps=1)
+    assert n == 0
+
+
 def test_resnet50_fused_3x3_apply_bit_identical():
     torch.manual_seed(0)
     m = resnet50(num_classes=10).to(DEV)
@@ -71,8 +81,10 @@ def test_resnet50_fused_3x3_apply_bit_identical():
     x = torch.randn(4, 3, 112, 112, device=DEV)
     y = torch.randint(0, 10, (4,), device=DEV)
     opt = lambda ps: SGD(ps, lr=0.05, momentum=0.9, weight_decay=1e-5)
-    la, pa, na = _steps(m, opt, x, y, cross_entropy, True)
-    lb, pb, nb = _steps(m2, opt, x, y, cross_entropy, False)
+    # ResNet keeps the unfused schedule by default; the kernel path is checked on layer 1's conv2
+    units = lambda mm: [b.u[1] for b in mm.blocks[:3]]
+    la, pa, na = _steps(m, opt, x, y, cross_entropy, True, units=units)
+    lb, pb, nb = _steps(m2, opt, x, y, cross_entropy, False, units=units)
     assert na >= 3 * 3   # layer 1's three conv2
     for a, b in zip(la + pa, lb + pb):
         assert torch.equal(a, b)
