@@ -18,7 +18,7 @@ import torch  # noqa: E402
 
 from conv_bench import resnet50_shapes, unet_shapes  # noqa: E402
 
-RESET = {"set_wgrad3_blocks": 0, "set_wgrad3": -1}
+RESET = {"set_wgrad3_blocks": 0, "set_wgrad3": -1, "set_wgrad_fast": 1}
 
 
 def parse_arms(spec):

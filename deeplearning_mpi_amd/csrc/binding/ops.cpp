@@ -1877,6 +1877,7 @@ void register_ops(pybind11::module& m) {
   m.def("set_conv_halo", [](int mode) { g_halo_override = mode; });
   m.def("set_halo_first", [](int on) { g_halo_first = on; });
   m.def("set_halo_pipe", [](int on) { dlmpi_set_halo_pipe(on); });
+  m.def("set_wgrad_fast", [](int on) { dlmpi_set_wgrad_fast(on); });
   m.def("set_conv_splitk", [](int n) { g_splitk_override = n; });
   m.def("set_conv_pipe_dgrad", [](int mode) { g_pipe_dgrad_override = mode; });
   m.def("set_conv_pipe", [](int mode) { g_pipe_override = mode; });

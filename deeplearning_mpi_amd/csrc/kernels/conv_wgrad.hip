@@ -147,18 +147,64 @@ void conv_wgrad_kernel(const WgradArgs a) {
     return reinterpret_cast<const char*>(ok ? a0 : z);
   };
   const uint16_t* zb = PA == 2 ? a.pz + a.pzoff : nullptr;
+
+  // Fast staging for K-steps whose 64 pixel rows all lie inside the split, when every column piece
+  // of the tile exists (wave-uniform, from a ballot): a per-K-step base in SGPRs (pix0 * ld) plus a
+  // loop-invariant 32-bit byte offset per piece, so no DMA address costs vector arithmetic or a
+  // select.  dy rows always qualify; x rows only for DIRECT (the gather decodes its pixel).  Not in
+  // the prologue forms: their extra offsets push the 128 x 128 tile past 168 VGPRs (spills).
+  constexpr bool FAST = PA == 0 && PB == 0;
+  uint32_t a_lane[AL], z_lane[PA == 2 ? AL : 1], b_lane[DIRECT ? BL : 1];
+  bool lane_ok = true;
+#pragma unroll
+  for (int i = 0; i < AL; ++i) {
+    int row, ch;
+    piece(i, A_ROW, row, ch);
+    const int col = m0 + 8 * ch;
+    lane_ok = lane_ok && col < a.Ko;
+    a_lane[i] = 2u * ((uint32_t)row * (uint32_t)a.ldy + (uint32_t)col);
+    if constexpr (PA == 2) z_lane[i] = 2u * ((uint32_t)row * (uint32_t)a.ldpz + (uint32_t)col);
+  }
+  if constexpr (DIRECT) {
+#pragma unroll
+    for (int i = 0; i < BL; ++i) {
+      int row, ch;
+      piece(i, B_ROW, row, ch);
+      lane_ok = lane_ok && b_pack[i] >= 0;
+      b_lane[i] = 2u * ((uint32_t)row * (uint32_t)a.ldx + (uint32_t)(b_pack[i] & 0xffff));
+    }
+  }
+  const bool cols_all = FAST && a.fast && __builtin_amdgcn_readfirstlane(__builtin_amdgcn_ballot_w64(!lane_ok) == 0);
+
   auto issue = [&](int buf, int pix0) {
     char* As = smem + buf * SB;
     char* Bs = As + A_BYTES;
+    if (cols_all && pix0 + BK <= pend) {
+      const char* ab = reinterpret_cast<const char*>(dyb + (int64_t)pix0 * a.ldy);
 #pragma unroll
-    for (int i = 0; i < AL; ++i) {
-      int row, ch;
-      piece(i, A_ROW, row, ch);
-      const int pix = pix0 + row, col = m0 + 8 * ch;
-      glds16(pick(pix < pend && col < a.Ko, dyb + (int64_t)pix * a.ldy + col), As + 16 * (256 * i + 64 * wid));
-      if constexpr (PA == 2)
-        glds16(pick(pix < pend && col < a.Ko, zb + (int64_t)pix * a.ldpz + col),
-               As + A_BYTES + B_BYTES + 16 * (256 * i + 64 * wid));
+      for (int i = 0; i < AL; ++i) {
+        glds16(ab + a_lane[i], As + 16 * (256 * i + 64 * wid));
+        if constexpr (PA == 2)
+          glds16(reinterpret_cast<const char*>(zb + (int64_t)pix0 * a.ldpz) + z_lane[i],
+                 As + A_BYTES + B_BYTES + 16 * (256 * i + 64 * wid));
+      }
+      if constexpr (DIRECT) {
+        const char* bb = reinterpret_cast<const char*>(xb + (int64_t)pix0 * a.ldx);
+#pragma unroll
+        for (int i = 0; i < BL; ++i) glds16(bb + b_lane[i], Bs + 16 * (256 * i + 64 * wid));
+        return;
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < AL; ++i) {
+        int row, ch;
+        piece(i, A_ROW, row, ch);
+        const int pix = pix0 + row, col = m0 + 8 * ch;
+        glds16(pick(pix < pend && col < a.Ko, dyb + (int64_t)pix * a.ldy + col), As + 16 * (256 * i + 64 * wid));
+        if constexpr (PA == 2)
+          glds16(pick(pix < pend && col < a.Ko, zb + (int64_t)pix * a.ldpz + col),
+                 As + A_BYTES + B_BYTES + 16 * (256 * i + 64 * wid));
+      }
     }
 #pragma unroll
     for (int i = 0; i < BL; ++i) {
@@ -526,7 +572,13 @@ extern "C" int dlmpi_wgrad_pro_ok(int direct, int pro_a, int pro_b) {
   return !(pro_a && pro_b) && (direct || !pro_b);
 }
 
-extern "C" hipError_t dlmpi_conv_wgrad(const WgradArgs* a, int bm, int bn, hipStream_t s) {
+static int g_wgrad_fast = 1;
+extern "C" void dlmpi_set_wgrad_fast(int on) { g_wgrad_fast = on; }
+
+extern "C" hipError_t dlmpi_conv_wgrad(const WgradArgs* a0, int bm, int bn, hipStream_t s) {
+  WgradArgs args = *a0;
+  args.fast = g_wgrad_fast;
+  const WgradArgs* a = &args;
   const unsigned nwg = (unsigned)(a->mtiles * a->ntiles * a->splits);
   if (nwg == 0) return hipSuccess;
   const dim3 g(nwg), b(256);

@@ -199,6 +199,7 @@ struct WgradArgs {
   int ldpz, pzoff;
   const float* pscale;
   const float* pshift;
+  int fast;                        // set by dlmpi_conv_wgrad: scalar-base DMA staging allowed (A/B knob)
 };
 
 // Streaming 3x3 / stride-1 / pad-1 convolution, 64 -> 64 channels (conv3x3_stream.hip): persistent
@@ -264,6 +265,7 @@ struct Wgrad3Args {
 
 extern "C" {
 // conv / gemm
+void dlmpi_set_wgrad_fast(int on);  // conv_wgrad_kernel scalar-base DMA staging (A/B)
 void dlmpi_set_halo_pipe(int on);   // 256 x 128 halo tiles on the weight-double-buffered kernel (A/B)
 hipError_t dlmpi_conv_igemm(const dlmpi::ConvArgs* a, int bm, int bn, hipStream_t s);
 // pipe = 1: the pipelined 8-wave kernel (tiles 256x256, 256x128, 128x256, 256x64, 512x64; bf16,

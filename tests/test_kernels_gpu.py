@@ -1012,3 +1012,41 @@ def test_stream1x1_matches_general_kernel(shape, ld_out):
     assert _rel(out[1][1], out[0][1]) < tol
     for a, b in zip(out[1][2:5], out[0][2:5]):
         assert _rel(a, b) < tol
+
+
+WGRAD_FAST_SHAPES = [
+    # N, H, W, Cin, Cout, R, stride, pad, x channel stride / offset
+    (4, 14, 14, 256, 1024, 1, 1, 0, None, 0),   # direct 1x1, 128 x 128 tiles
+    (2, 28, 28, 512, 128, 1, 1, 0, None, 0),
+    (3, 9, 11, 64, 64, 1, 1, 0, None, 0),       # Ko = 64: 64 x 256 tiles; 297 pixels (ragged K-step)
+    (2, 14, 14, 96, 96, 1, 1, 0, None, 0),      # ragged column tiles: the general staging
+    (2, 13, 13, 64, 256, 1, 1, 0, 192, 64),     # x a channel slice of a concat buffer
+    (2, 28, 28, 256, 512, 1, 2, 0, None, 0),    # strided 1x1 (gather): dy side only
+    (2, 15, 15, 64, 128, 3, 2, 1, None, 0),     # 3x3 stride 2 (gather)
+]
+
+
+@pytest.mark.parametrize("shape", WGRAD_FAST_SHAPES, ids=lambda s: "x".join(str(v) for v in s[:8]))
+def test_wgrad_fast_staging_bit_identical(shape):
+    """conv_wgrad_kernel's scalar-base staging (full K-steps of a tile whose column pieces all exist)
+    against the per-piece selected staging: the same bytes land in the same LDS slots, so the weight
+    gradient is bit-identical; and it matches an fp32 reference."""
+    nb, rb = _be()
+    N, H, W, Cin, K, R, s, p, ldx, xoff = shape
+    P = (H + 2 * p - R) // s + 1
+    x, xr = _act(N, H, W, Cin, ld=ldx, off=xoff)
+    dy, dyr = _act(N, P, P, K)
+    out = {}
+    try:
+        for on in (1, 0):
+            nb.C.set_wgrad_fast(on)
+            g = torch.zeros(K * R * R * Cin, device=DEV)
+            nb.conv_wgrad(dy, x, R, R, s, p, g, Cin, K)
+            torch.cuda.synchronize()
+            out[on] = g
+    finally:
+        nb.C.set_wgrad_fast(1)
+    assert torch.equal(out[1], out[0])
+    ref = torch.zeros_like(out[0])
+    rb.conv_wgrad(dyr, xr, R, R, s, p, ref, Cin, K)
+    assert _rel(out[1], ref) < 1e-2
