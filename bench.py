@@ -192,7 +192,7 @@ def main():
                    "splitk": "set_conv_splitk", "pipe_dgrad": "set_conv_pipe_dgrad", "wgrad_batch": "set_wgrad_batch",
                    "defer_direct": "set_defer_direct", "wgrad3_blocks": "set_wgrad3_blocks",
                    "conv3_stream": "set_conv3_stream", "head": "set_head1x1", "c8": "set_conv_c8", "c16": "set_conv_c16", "c3pro": "set_conv3_pro", "convT_stream": "set_convT_stream",
-                   "halo_first": "set_halo_first", "halo_pipe": "set_halo_pipe", "wgrad_fast": "set_wgrad_fast"}
+                   "halo_first": "set_halo_first", "halo_pipe": "set_halo_pipe", "wgrad_fast": "set_wgrad_fast", "wgrad_blocks": "set_wgrad_blocks"}
         for k, v in pins.items():
             if k in setters:
                 getattr(_nat(), setters[k])(int(v))

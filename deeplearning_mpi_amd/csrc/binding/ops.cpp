@@ -1332,6 +1332,7 @@ static void wgrad_reduce_or_defer(const at::Tensor& ws, int splits, int G, int64
 static int g_wgrad3_override = -1;   // dlmpi_ext set_wgrad3 (tests); -1: on
 static int g_wgrad3_blocks = 0;      // dlmpi_ext set_wgrad3_blocks (A/B): > 0 overrides the grid target
 static int g_wgrad3_ran = 0;         // 1 if the last weight gradient ran the 3x3 spatial-tile kernel
+static int g_wgrad_blocks = 0;       // dlmpi_ext set_wgrad_blocks (A/B): > 0 overrides the gather kernel's grid target
 
 void conv2d_wgrad_pro(const at::Tensor& dy, int lddy, int dyoff, int Ko, const at::Tensor& x, int N, int H, int W,
                       int C, int ldx, int xoff, int R, int S, int stride, int pad, int P, int Q, at::Tensor grad,
@@ -1430,7 +1431,7 @@ void conv2d_wgrad_pro(const at::Tensor& dy, int lddy, int dyoff, int Ko, const a
   // least 8 K-steps (512 pixels) so the fp32 slab traffic stays small next to the MFMA work.
   // target grid size (the weight gradients share the GPU with the data-gradient
   // chain on another stream, so they need not fill it alone)
-  constexpr int target_blocks = 512;
+  const int target_blocks = g_wgrad_blocks > 0 ? g_wgrad_blocks : 512;
   const int maxsplit = std::max(1, ceil_div(a.npix, 512));
   int splits = std::max(1, std::min(maxsplit, w256 ? target_blocks / tiles : ceil_div(target_blocks, tiles)));
   int pps = ceil_div(a.npix, splits);
@@ -1878,6 +1879,7 @@ void register_ops(pybind11::module& m) {
   m.def("set_halo_first", [](int on) { g_halo_first = on; });
   m.def("set_halo_pipe", [](int on) { dlmpi_set_halo_pipe(on); });
   m.def("set_wgrad_fast", [](int on) { dlmpi_set_wgrad_fast(on); });
+  m.def("set_wgrad_blocks", [](int n) { g_wgrad_blocks = n; });
   m.def("set_conv_splitk", [](int n) { g_splitk_override = n; });
   m.def("set_conv_pipe_dgrad", [](int mode) { g_pipe_dgrad_override = mode; });
   m.def("set_conv_pipe", [](int mode) { g_pipe_override = mode; });
