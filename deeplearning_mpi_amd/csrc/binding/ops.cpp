@@ -304,7 +304,7 @@ static int apply_tiles(ConvArgs& a, int bm, int bn) {
 // Plan for a fully set-up (default-tiled) launch: the cached one, or tune now.  Returns false if
 // autotuning does not apply (the caller keeps its static plan).
 static bool conv_plan(ConvArgs& a, int pass, int& bm, int& bn) {
-  if (!conv_autotune_on() || a.f32 || a.pro != 0 || a.halo) return false;
+  if (!conv_autotune_on() || a.pro != 0 || a.halo) return false;
   // trials re-run the launch: an output that is also one of its inputs (in-place residual / mask /
   // z) would be transformed once per trial -- keep the static plan there
   const void* y = a.y;
@@ -325,6 +325,7 @@ static bool conv_plan(ConvArgs& a, int pass, int& bm, int& bn) {
         if (tbm == 256 && tbn == 256 && a.C < 64) continue;
         if (tbm == 128 && tbn == 256 && a.C < 64) continue;
         if (tbm == 64 && tbn == 256) continue;
+        if (a.f32 && (tbm > 128 || tbn > 128)) continue;   // launch_f32's tiles
         cands.push_back({tbm, tbn, 0});
         if (maxk >= 16) cands.push_back({tbm, tbn, 2});
         if (maxk >= 8) cands.push_back({tbm, tbn, 1});
